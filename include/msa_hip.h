@@ -1,0 +1,155 @@
+/*
+ * msa_hip.h -- C ABI of libmsa_hip, the MI355X (gfx950) implementation of the
+ * Music-Analyst-AI hot path (/root/reference/src/parallel_spotify.c).
+ *
+ * Plain C: pointers, sizes and ints only -- no torch / HIP types cross this
+ * boundary (streams are passed as `void *`, device buffers as `void *`).
+ * Every entry point returns MSA_OK (0) or a negative MSA_ERR_* code; the
+ * message of the last failure is available from msa_last_error().
+ *
+ * Which reference function each entry point replaces (file:line in
+ * /root/reference/src/parallel_spotify.c):
+ *
+ *   msa_split_columns   read_csv_record 549-633, parse_csv_line 258-304,
+ *                       duplicate_field 215-255, split_dataset_columns
+ *                       640-721, header handling in main 788-827
+ *   msa_count           the text / artist rank loops of main 853-999,
+ *                       process_lyrics 350-394, ht_put 126-149
+ *   msa_shard_*         (multi-GPU) the even byte split of main 866-882,
+ *                       done exactly instead of at raw byte offsets
+ *   msa_export_partition / msa_merge_partition
+ *                       send_hash_table 397-410, receive_hash_table 413-432,
+ *                       ht_merge 152-158
+ *   msa_rank            ht_to_array 161-175 + qsort(entry_compare_desc)
+ *                       178-188 inside write_table_csv 325-344
+ *   msa_write_table_csv write_table_csv 325-344 / write_csv_entry 307-319
+ *   msa_run             all of the above for one GPU
+ */
+#ifndef MSA_HIP_H
+#define MSA_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MSA_ABI_VERSION 1
+
+/* A device buffer handed to msa_bind_csv must stay readable this many bytes
+ * past its logical end (vector loads run ahead; the bytes are ignored). */
+#define MSA_INPUT_PAD 4096
+
+enum {
+    MSA_OK = 0,
+    MSA_ERR_ARG = -1,        /* bad argument / call order                  */
+    MSA_ERR_HIP = -2,        /* HIP runtime failure (no GPU, OOM, fault)   */
+    MSA_ERR_NOHEADER = -3,   /* "Dataset does not contain a header row"    */
+    MSA_ERR_BADHEADER = -4,  /* "Unable to parse dataset header"           */
+    MSA_ERR_CAPACITY = -5,   /* a table or list overflowed its capacity     */
+    MSA_ERR_COLLISION = -6,  /* 64-bit key-hash collision detected          */
+    MSA_ERR_IO = -7          /* file write failed                           */
+};
+
+/* ---------------------------------------------------------------- corpus */
+
+enum { MSA_GEN_ZIPF = 0, MSA_GEN_HIGHCARD = 1, MSA_GEN_TORTURE = 2 };
+
+typedef struct {
+    uint64_t seed;
+    uint64_t n_songs;
+    uint32_t vocab;          /* distinct lyric words (ZIPF/HIGHCARD)      */
+    uint32_t n_artists;
+    uint32_t words_per_song; /* mean lyric length in words                */
+    int mode;                /* MSA_GEN_*                                 */
+    int crlf;                /* 1: records end in "\r\n"                  */
+} msa_gen_params;
+
+/* Deterministic synthetic corpus; *out is malloc'ed, release with msa_free. */
+int msa_gen_corpus(const msa_gen_params *p, char **out, size_t *len);
+void msa_free(void *p);
+
+/* --------------------------------------------------------------- context */
+
+typedef struct msa_ctx msa_ctx;
+
+int msa_create(int device, msa_ctx **out);
+void msa_destroy(msa_ctx *ctx);
+const char *msa_last_error(const msa_ctx *ctx);
+/* The HIP stream (hipStream_t) every kernel of this context runs on. */
+void *msa_stream(msa_ctx *ctx);
+int msa_sync(msa_ctx *ctx);
+
+/* Input: copy a host CSV into context-owned HBM, or bind a caller-owned
+ * device buffer (zero copy; MSA_INPUT_PAD readable bytes past n). */
+int msa_load_csv(msa_ctx *ctx, const void *host_csv, size_t n);
+int msa_bind_csv(msa_ctx *ctx, const void *dev_csv, size_t n);
+
+/* ---------------------------------------------------------------- stages */
+
+enum {
+    MSA_SPLIT_TEXT_COLUMN = 1  /* also materialise text.csv (CLI output)    */
+};
+
+/* Header parse + record/field scan of the whole CSV in HBM + artist.csv
+ * materialisation.  Word tokens of the lyric column are counted in the same
+ * pass (the scan and the tokenizer share one read of the input). */
+int msa_split_columns(msa_ctx *ctx, int flags);
+/* Artist pass over the materialised artist column; finishes the counts. */
+int msa_count(msa_ctx *ctx);
+/* Rank both tables: count descending, ties by strcmp of the key bytes. */
+int msa_rank(msa_ctx *ctx);
+/* split + count + rank, single GPU; returns when results are on device. */
+int msa_run(msa_ctx *ctx, int flags);
+
+/* --------------------------------------------------------------- results */
+
+typedef struct {
+    long long total_songs;     /* records read from the artist column      */
+    long long total_words;     /* tokens of length >= 3                    */
+    uint64_t n_words;          /* distinct words                           */
+    uint64_t n_artists;        /* distinct non-empty artist names          */
+    uint64_t n_records;        /* CSV records incl. header                 */
+    char artist_label[128];    /* header labels (parallel_spotify.c:810)   */
+    char text_label[128];
+    char artist_file[128];     /* sanitised split file base names          */
+    char text_file[128];
+} msa_summary;
+
+int msa_get_summary(msa_ctx *ctx, msa_summary *out);
+
+enum { MSA_TABLE_WORDS = 0, MSA_TABLE_ARTISTS = 1 };
+
+/* Copy ranked entries [first, first+count) of a table to the host.
+ * counts[i] = occurrences; key i is keys[offsets[i] .. offsets[i+1]).
+ * offsets needs count+1 slots; keys needs keys_cap bytes (returns
+ * MSA_ERR_CAPACITY and the needed size in *keys_needed when too small). */
+int msa_get_ranked(msa_ctx *ctx, int table, uint64_t first, uint64_t count,
+                   long long *counts, uint64_t *offsets, char *keys,
+                   uint64_t keys_cap, uint64_t *keys_needed);
+
+/* write_table_csv: "<key_header>,count" then "\"key\",count" lines
+ * (quotes doubled), limit <= 0 means all entries. */
+int msa_write_table_csv(msa_ctx *ctx, int table, const char *path,
+                        const char *key_header, int limit);
+
+/* Host copy of a materialised split column (0 = artist.csv, 1 = text.csv). */
+int msa_get_split_column(msa_ctx *ctx, int which, char **out, size_t *len);
+
+/* ------------------------------------------------- multi-GPU (one process
+ * per GPU; the caller moves bytes with RCCL).  A shard is a contiguous byte
+ * range of one logical CSV; shard 0 holds the header. */
+
+/* Transfer function of this shard's bytes over the record-reader state, as
+ * MSA_SHARD_FN_BYTES opaque bytes (all-gather them across ranks). */
+#define MSA_SHARD_FN_BYTES 64
+int msa_shard_function(msa_ctx *ctx, void *fn_out);
+/* Feed the functions of all shards before this one (in order), so the shard
+ * starts in the exact reader state of the single-file scan. */
+int msa_shard_set_prefix(msa_ctx *ctx, const void *fns, int nshards_before);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MSA_HIP_H */

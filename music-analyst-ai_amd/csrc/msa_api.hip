@@ -1,0 +1,833 @@
+// msa_api.hip -- C ABI of libmsa_hip (include/msa_hip.h): buffer management and
+// the stage order of one GPU's pipeline.  All data-path work is in kernels
+// (msa_scan.hip, msa_post.hip); the host only sizes buffers from a handful of
+// device counters and parses the single header record (the reference does the
+// same serially on rank 0 before its timed region, parallel_spotify.c:788-819).
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <errno.h>
+#include <stdarg.h>
+#include <algorithm>
+
+#include <string>
+#include <vector>
+
+#include "msa_hip.h"
+#include "msa_internal.h"
+
+// ---- launchers (msa_scan.hip / msa_post.hip)
+hipError_t msa_launch_summary(const u8 *, u64, u64, u32, ChunkSum *, hipStream_t);
+hipError_t msa_launch_fn(const ChunkSum *, u64, u32, Fn *, Fn *, const State *, State *, State *, hipStream_t, bool,
+                         bool);
+hipError_t msa_launch_scan(const ScanArgs &, int, hipStream_t);
+hipError_t msa_exclusive_scan(const u64 *, u64, u64 *, u64 *, u64 *, hipStream_t);
+hipError_t msa_launch_artist_len(const u8 *, const u64 *, const u32 *, const u32 *, u64, u64 *, hipStream_t);
+hipError_t msa_launch_artist_write(const u8 *, const u64 *, const u32 *, const u32 *, u64, const u64 *, u64, u8 *,
+                                   hipStream_t);
+hipError_t msa_launch_text_len(const u8 *, const u64 *, const u64 *, const u32 *, const u32 *, u64, u64 *, hipStream_t);
+hipError_t msa_launch_text_write(const u8 *, const u64 *, const u64 *, const u32 *, const u32 *, u64, const u64 *, u64,
+                                 u8 *, hipStream_t);
+hipError_t msa_launch_artist_key(const u8 *, const u64 *, const u64 *, u64, u8 *, u64 *, u32 *, u64 *, u64 *, u64,
+                                 u32 *, u64, Counters *, hipStream_t);
+hipError_t msa_launch_long(const u8 *, u64, const u64 *, u64, u32 *, u64 *, u64 *, u64, u32 *, u64, Counters *,
+                           hipStream_t);
+hipError_t msa_launch_word_entries(const EntryArgs &, hipStream_t);
+hipError_t msa_launch_artist_entries(const u64 *, const u32 *, u64, const u8 *, const u64 *, const u32 *, u64 *, u64 *,
+                                     u64 *, u32 *, u64 *, u64 *, hipStream_t);
+hipError_t msa_launch_radix_hist_all(const u64 *, const u64 *, const u64 *, u64, u32 *, hipStream_t);
+u64 msa_radix_blocks(u64 n);
+hipError_t msa_launch_radix_pass(const u64 *, const u64 *, const u64 *, const u32 *, u64, u32, u64 *, u64 *, u64 *,
+                                 u64 *, u64 *, u64 *, u32 *, hipStream_t);
+hipError_t msa_launch_fixup(const u64 *, const u64 *, const u64 *, const u32 *, u64, const u64 *, const u8 *,
+                            const u64 *, const u32 *, const u8 *, const u64 *, const u32 *, u32 *, hipStream_t);
+hipError_t msa_launch_blob(const u32 *, u64, const u64 *, const u64 *, const u64 *, const u64 *, const u8 *,
+                           const u64 *, const u32 *, const u8 *, const u64 *, const u32 *, u64 *, u64 *, u64 *, u64 *,
+                           u8 *, u64 *, hipStream_t, int);
+
+// ---------------------------------------------------------------------------
+namespace {
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    template <class T> T *as() const { return reinterpret_cast<T *>(p); }
+};
+
+struct Ranked {
+    DevBuf K[3][3];  // [set][k2,k1,k0]: set 0 = input, 1/2 = ping-pong
+    DevBuf V[3];
+    DevBuf ref, cnt, order, len, off, blob, counts;
+    DevBuf bhist, boff, bsum, ghist;
+    u64 n = 0, blob_len = 0;
+    std::vector<u64> h_counts, h_off;
+    std::vector<char> h_blob;
+    bool host_valid = false;
+};
+
+u64 next_pow2(u64 v) {
+    u64 p = 1;
+    while (p < v) p <<= 1;
+    return p;
+}
+
+}  // namespace
+
+struct msa_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    // input
+    DevBuf in_own;
+    const u8 *in = nullptr;
+    u64 n = 0;
+    // scan scratch
+    DevBuf sums, carry, runpre, small;  // small: Fn total + 2 States + ...
+    // CSV records
+    DevBuf rec_start, rec_term, f0rel, f3rel, nulrel;
+    u64 nrec = 0, rec_cap = 0;
+    bool have_text_arrays = false;
+    // columns
+    DevBuf acol, alen, aoff, tcol, tlen, toff, scan_bsum, scan_total;
+    u64 acol_len = 0, a_hdr_getline = 0, tcol_len = 0;
+    bool have_tcol = false;
+    // artist.csv records + keys
+    DevBuf ar_start, ar_term, arena, key_off, key_len, key_slot;
+    u64 nrec_a = 0;
+    // tables
+    DevBuf s_tab, s_list, m_tab, m_list, l_pos, l_len, l_slot, l_tab, l_list, a_tab, a_list;
+    u64 s_slots = 0, m_slots = 0, l_occ_cap = 0, lt_slots = 0, a_slots = 0;
+    u64 s_used_prev = 0, m_used_prev = 0, lt_used_prev = 0, a_used_prev = 0;
+    u64 cap_scale = 1;
+    // counters
+    DevBuf ctr;
+    Counters h_ctr{};
+    // results
+    Ranked rw, ra;
+    msa_summary sum{};
+    int stage = 0;  // 0 none, 1 split, 2 counted, 3 ranked
+};
+
+static int fail(msa_ctx *c, int code, const char *fmt, ...) {
+    char b[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(b, sizeof b, fmt, ap);
+    va_end(ap);
+    if (c) c->err = b;
+    return code;
+}
+
+#define HIPC(c, x)                                                                                      \
+    do {                                                                                                \
+        hipError_t e_ = (x);                                                                            \
+        if (e_ != hipSuccess) return fail(c, MSA_ERR_HIP, "%s failed: %s (%s:%d)", #x, hipGetErrorString(e_), \
+                                          __FILE__, __LINE__);                                          \
+    } while (0)
+
+static hipError_t ensure(DevBuf &b, size_t bytes, bool zero = false) {
+    if (bytes == 0) bytes = 16;
+    if (b.cap >= bytes) return hipSuccess;
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.cap = 0;
+    size_t want = bytes + bytes / 4;
+    hipError_t e = hipMalloc(&b.p, want);
+    if (e != hipSuccess) return e;
+    b.cap = want;
+    if (zero) e = hipMemset(b.p, 0, want);
+    return e;
+}
+
+static void release(DevBuf &b) {
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.cap = 0;
+}
+
+// ---------------------------------------------------------------- host CSV bits
+// Header record parsing (parse_csv_line + duplicate_field with preserve = 0,
+// parallel_spotify.c:258-304, 215-255) for the one header record.
+static bool h_space(unsigned c) { return c == ' ' || (c >= 9 && c <= 13); }
+
+static std::string h_dup_field(const unsigned char *f, size_t len) {
+    size_t s = 0, e = len;
+    while (s < len && h_space(f[s])) s++;
+    while (e > s && h_space(f[e - 1])) e--;
+    bool quoted = (e > s + 1 && f[s] == '"' && f[e - 1] == '"');
+    size_t a = s, z = e;
+    if (quoted) { a++; z--; }
+    std::string r;
+    for (size_t i = a; i < z; ++i) {
+        if (f[i] == '"' && i + 1 < z && f[i + 1] == '"') { r.push_back('"'); i++; }
+        else r.push_back((char)f[i]);
+    }
+    size_t x = 0, y = r.size();
+    while (x < y && h_space((unsigned char)r[x])) x++;
+    while (y > x && h_space((unsigned char)r[y - 1])) y--;
+    return r.substr(x, y - x);
+}
+
+static bool h_parse_header(const unsigned char *rec, size_t len, std::string &a, std::string &t) {
+    const void *z = memchr(rec, 0, len);
+    if (z) len = (size_t)((const unsigned char *)z - rec);
+    while (len > 0 && (rec[len - 1] == '\n' || rec[len - 1] == '\r')) len--;
+    size_t comma[3];
+    int nc = 0, q = 0;
+    for (size_t i = 0; i < len && nc < 3; ++i) {
+        if (rec[i] == '"') {
+            if (q && i + 1 < len && rec[i + 1] == '"') i++;
+            else q = !q;
+        } else if (rec[i] == ',' && !q) {
+            comma[nc++] = i;
+        }
+    }
+    if (nc < 3) return false;
+    a = h_dup_field(rec, comma[0]);
+    t = h_dup_field(rec + comma[2] + 1, len - comma[2] - 1);
+    return true;
+}
+
+// sanitize_header_name (parallel_spotify.c:510-543)
+static void h_sanitize(const std::string &in, char *out) {
+    size_t j = 0;
+    for (unsigned char c : in) {
+        if (c == '\n' || c == '\r') continue;
+        if (j + 1 >= 128) continue;
+        if (h_space(c)) out[j++] = '_';
+        else if ((c >= '0' && c <= '9') || ((c | 0x20) >= 'a' && (c | 0x20) <= 'z') || c == '-' || c == '.' ||
+                 c == '_')
+            out[j++] = (char)c;
+        else out[j++] = '_';
+    }
+    if (j == 0) { strcpy(out, "col"); return; }
+    out[j] = 0;
+}
+
+// ------------------------------------------------------------------- scanning
+// Scan a byte segment [b, e) of `buf`: K1 + K2 (+ K3 in `mode`).  Returns the
+// reader state at the end of the segment in *fin.
+static int run_scan_fn(msa_ctx *c, const u8 *buf, u64 b, u64 e, State init, State *fin) {
+    const u64 len = e > b ? e - b : 0;
+    const u32 nch = (u32)((len + MSA_CHUNK - 1) / MSA_CHUNK);
+    HIPC(c, ensure(c->sums, sizeof(ChunkSum) * (size_t)(nch + 1)));
+    HIPC(c, ensure(c->carry, sizeof(State) * (size_t)(nch + 1)));
+    HIPC(c, ensure(c->runpre, sizeof(Fn) * 256));
+    HIPC(c, ensure(c->small, 4096));
+    Fn *total = c->small.as<Fn>();
+    State *d_init = reinterpret_cast<State *>(c->small.as<char>() + 1024);
+    State *d_fin = d_init + 1;
+    HIPC(c, hipMemcpyAsync(d_init, &init, sizeof(State), hipMemcpyHostToDevice, c->stream));
+    if (nch) {
+        HIPC(c, msa_launch_summary(buf, b, e, nch, c->sums.as<ChunkSum>(), c->stream));
+        HIPC(c, msa_launch_fn(c->sums.as<ChunkSum>(), b, nch, c->runpre.as<Fn>(), total, d_init, c->carry.as<State>(),
+                              d_fin, c->stream, false, false));
+        HIPC(c, hipMemcpyAsync(fin, d_fin, sizeof(State), hipMemcpyDeviceToHost, c->stream));
+        HIPC(c, hipStreamSynchronize(c->stream));
+    } else {
+        *fin = init;
+    }
+    return MSA_OK;
+}
+
+static int ensure_tables(msa_ctx *c) {
+    // Capacities scale with the input; the tables are zeroed once and, after
+    // each run, only the claimed slots are cleared again (no per-run memset
+    // of the whole table).
+    const u64 n = c->n;
+    u64 s_slots = next_pow2(std::max<u64>(1ull << 20, std::min<u64>(n / 16, 1ull << 28)) * c->cap_scale);
+    u64 m_slots = next_pow2(std::max<u64>(1ull << 18, std::min<u64>(n / 64, 1ull << 27)) * c->cap_scale);
+    u64 l_occ = std::max<u64>(1ull << 18, n / 512) * c->cap_scale;
+    u64 lt_slots = next_pow2(l_occ * 2);
+    u64 a_slots = next_pow2(std::max<u64>(1ull << 16, (c->nrec + 1) * 2));
+    if (s_slots != c->s_slots) {
+        release(c->s_tab);
+        HIPC(c, ensure(c->s_tab, s_slots * 16, true));
+        HIPC(c, ensure(c->s_list, (s_slots / 2) * 4));
+        c->s_slots = s_slots;
+        c->s_used_prev = 0;
+    }
+    if (m_slots != c->m_slots) {
+        release(c->m_tab);
+        HIPC(c, ensure(c->m_tab, m_slots * 32, true));
+        HIPC(c, ensure(c->m_list, (m_slots / 2) * 4));
+        c->m_slots = m_slots;
+        c->m_used_prev = 0;
+    }
+    if (l_occ != c->l_occ_cap) {
+        HIPC(c, ensure(c->l_pos, l_occ * 8));
+        HIPC(c, ensure(c->l_len, l_occ * 4));
+        HIPC(c, ensure(c->l_slot, l_occ * 8));
+        c->l_occ_cap = l_occ;
+    }
+    if (lt_slots != c->lt_slots) {
+        release(c->l_tab);
+        HIPC(c, ensure(c->l_tab, lt_slots * 32, true));
+        HIPC(c, ensure(c->l_list, (lt_slots / 2) * 4));
+        c->lt_slots = lt_slots;
+        c->lt_used_prev = 0;
+    }
+    if (a_slots > c->a_slots) {
+        release(c->a_tab);
+        HIPC(c, ensure(c->a_tab, a_slots * 32, true));
+        HIPC(c, ensure(c->a_list, (a_slots / 2) * 4));
+        c->a_slots = a_slots;
+        c->a_used_prev = 0;
+    }
+    return MSA_OK;
+}
+
+// clear only the slots the previous run claimed
+__global__ void k_clear_slots(u64 *tab, const u32 *list, u64 n, u32 words_per_slot) {
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    u64 *s = tab + (u64)list[i] * words_per_slot;
+    for (u32 k = 0; k < words_per_slot; ++k) s[k] = 0;
+}
+
+static int clear_tables(msa_ctx *c) {
+    struct {
+        DevBuf *tab, *list;
+        u64 *used;
+        u32 w;
+    } t[4] = {{&c->s_tab, &c->s_list, &c->s_used_prev, 2},
+              {&c->m_tab, &c->m_list, &c->m_used_prev, 4},
+              {&c->l_tab, &c->l_list, &c->lt_used_prev, 4},
+              {&c->a_tab, &c->a_list, &c->a_used_prev, 4}};
+    for (auto &x : t) {
+        if (*x.used && x.tab->p) {
+            hipLaunchKernelGGL(k_clear_slots, dim3((u32)((*x.used + 255) / 256)), dim3(256), 0, c->stream,
+                               x.tab->as<u64>(), x.list->as<u32>(), *x.used, x.w);
+            HIPC(c, hipGetLastError());
+        }
+        *x.used = 0;
+    }
+    return MSA_OK;
+}
+
+static int sync_counters(msa_ctx *c) {
+    HIPC(c, hipMemcpyAsync(&c->h_ctr, c->ctr.p, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    return MSA_OK;
+}
+
+// ------------------------------------------------------------------ stage 1
+static int materialise_column(msa_ctx *c, bool text, const std::string &hdr_line, DevBuf &col, DevBuf &lenb,
+                              DevBuf &offb, u64 *col_len) {
+    const u64 nrec = c->nrec;
+    HIPC(c, ensure(lenb, nrec * 8));
+    HIPC(c, ensure(offb, nrec * 8));
+    HIPC(c, ensure(c->scan_bsum, ((nrec + 1023) / 1024 + 1) * 8));
+    HIPC(c, ensure(c->scan_total, 64));
+    if (text)
+        HIPC(c, msa_launch_text_len(c->in, c->rec_start.as<u64>(), c->rec_term.as<u64>(), c->f3rel.as<u32>(),
+                                    c->nulrel.as<u32>(), nrec, lenb.as<u64>(), c->stream));
+    else
+        HIPC(c, msa_launch_artist_len(c->in, c->rec_start.as<u64>(), c->f0rel.as<u32>(), c->f3rel.as<u32>(), nrec,
+                                      lenb.as<u64>(), c->stream));
+    HIPC(c, msa_exclusive_scan(lenb.as<u64>(), nrec, offb.as<u64>(), c->scan_bsum.as<u64>(), c->scan_total.as<u64>(),
+                               c->stream));
+    u64 body = 0;
+    HIPC(c, hipMemcpyAsync(&body, c->scan_total.p, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    const u64 total = hdr_line.size() + body;
+    HIPC(c, ensure(col, total + MSA_INPUT_PAD));
+    HIPC(c, hipMemcpyAsync(col.p, hdr_line.data(), hdr_line.size(), hipMemcpyHostToDevice, c->stream));
+    HIPC(c, hipMemsetAsync(col.as<char>() + total, 0, MSA_INPUT_PAD, c->stream));
+    if (text)
+        HIPC(c, msa_launch_text_write(c->in, c->rec_start.as<u64>(), c->rec_term.as<u64>(), c->f3rel.as<u32>(),
+                                      c->nulrel.as<u32>(), nrec, offb.as<u64>(), hdr_line.size(), col.as<u8>(),
+                                      c->stream));
+    else
+        HIPC(c, msa_launch_artist_write(c->in, c->rec_start.as<u64>(), c->f0rel.as<u32>(), c->f3rel.as<u32>(), nrec,
+                                        offb.as<u64>(), hdr_line.size(), col.as<u8>(), c->stream));
+    *col_len = total;
+    return MSA_OK;
+}
+
+static int do_split(msa_ctx *c, int flags) {
+    int rc;
+    if (!c->in) return fail(c, MSA_ERR_ARG, "no input bound (msa_load_csv / msa_bind_csv)");
+    if (c->n == 0) return fail(c, MSA_ERR_NOHEADER, "Dataset does not contain a header row");
+    const bool want_text = (flags & MSA_SPLIT_TEXT_COLUMN) != 0;
+    HIPC(c, ensure(c->ctr, sizeof(Counters)));
+    if ((rc = clear_tables(c))) return rc;
+    HIPC(c, hipMemsetAsync(c->ctr.p, 0, sizeof(Counters), c->stream));
+
+    State init{0, 0, 0, 0, 0, 0}, fin;
+    if ((rc = run_scan_fn(c, c->in, 0, c->n, init, &fin))) return rc;
+    const u64 nterm = fin.rec;
+    c->nrec = nterm + (fin.rs < c->n ? 1 : 0);
+    const u64 cap = nterm + 2;
+    HIPC(c, ensure(c->rec_start, cap * 8));
+    HIPC(c, ensure(c->rec_term, cap * 8));
+    HIPC(c, ensure(c->f0rel, cap * 4));
+    HIPC(c, ensure(c->f3rel, cap * 4));
+    HIPC(c, ensure(c->nulrel, cap * 4));
+    c->rec_cap = cap;
+    HIPC(c, hipMemsetAsync(c->f0rel.p, 0, cap * 4, c->stream));
+    HIPC(c, hipMemsetAsync(c->f3rel.p, 0, cap * 4, c->stream));
+    if (want_text) HIPC(c, hipMemsetAsync(c->nulrel.p, 0, cap * 4, c->stream));
+    u64 zero = 0;
+    HIPC(c, hipMemcpyAsync(c->rec_start.p, &zero, 8, hipMemcpyHostToDevice, c->stream));
+    if ((rc = ensure_tables(c))) return rc;
+
+    ScanArgs a{};
+    a.buf = c->in;
+    a.seg_begin = 0;
+    a.seg_end = c->n;
+    a.nchunks = (u32)((c->n + MSA_CHUNK - 1) / MSA_CHUNK);
+    a.carry = c->carry.as<State>();
+    a.rec_start = c->rec_start.as<u64>();
+    a.rec_term = c->rec_term.as<u64>();
+    a.f0rel = c->f0rel.as<u32>();
+    a.f3rel = c->f3rel.as<u32>();
+    a.nulrel = c->nulrel.as<u32>();
+    a.rec_cap = cap;
+    a.s_tab = c->s_tab.as<u64>();
+    a.s_mask = c->s_slots - 1;
+    a.s_list = c->s_list.as<u32>();
+    a.s_list_cap = c->s_slots / 2;
+    a.m_tab = c->m_tab.as<u64>();
+    a.m_mask = c->m_slots - 1;
+    a.m_list = c->m_list.as<u32>();
+    a.m_list_cap = c->m_slots / 2;
+    a.l_pos = c->l_pos.as<u64>();
+    a.l_cap = c->l_occ_cap;
+    a.ctr = c->ctr.as<Counters>();
+    a.want_term = want_text ? 1 : 0;
+    HIPC(c, msa_launch_scan(a, 0, c->stream));
+    // the last record may end at EOF instead of a terminator
+    if (fin.rs < c->n) {
+        u64 v = c->n;
+        HIPC(c, hipMemcpyAsync(c->rec_term.as<u64>() + (c->nrec - 1), &v, 8, hipMemcpyHostToDevice, c->stream));
+    }
+    // header record = record 0
+    u64 hend = c->n;
+    if (nterm > 0) {
+        // record 0's terminator offset: the start of record 1 minus its terminator bytes is not
+        // enough ('\r\n'), so read the terminator slot K3 wrote for record 0.
+        HIPC(c, hipMemcpyAsync(&hend, c->rec_term.p, 8, hipMemcpyDeviceToHost, c->stream));
+    }
+    HIPC(c, hipStreamSynchronize(c->stream));
+    if (hend > c->n) hend = c->n;
+    std::vector<unsigned char> hdr(hend + 1);
+    if (hend) HIPC(c, hipMemcpy(hdr.data(), c->in, hend, hipMemcpyDeviceToHost));
+    std::string al, tl;
+    if (!h_parse_header(hdr.data(), hend, al, tl)) return fail(c, MSA_ERR_BADHEADER, "Unable to parse dataset header");
+    memset(c->sum.artist_label, 0, 128);
+    memset(c->sum.text_label, 0, 128);
+    strncpy(c->sum.artist_label, al.c_str(), 127);
+    strncpy(c->sum.text_label, tl.c_str(), 127);
+    h_sanitize(al, c->sum.artist_file);
+    h_sanitize(tl, c->sum.text_file);
+
+    std::string ah = c->sum.artist_label[0] ? c->sum.artist_label : "Artists";
+    ah.push_back('\n');
+    if ((rc = materialise_column(c, false, ah, c->acol, c->alen, c->aoff, &c->acol_len))) return rc;
+    {
+        size_t p = ah.find('\n');
+        c->a_hdr_getline = p + 1;  // compute_header_length (parallel_spotify.c:444-459)
+    }
+    c->have_tcol = false;
+    if (want_text) {
+        std::string th = c->sum.text_label[0] ? c->sum.text_label : "Texts";
+        th.push_back('\n');
+        if ((rc = materialise_column(c, true, th, c->tcol, c->tlen, c->toff, &c->tcol_len))) return rc;
+        c->have_tcol = true;
+    }
+    c->stage = 1;
+    return MSA_OK;
+}
+
+// ------------------------------------------------------------------ stage 2
+static int do_count(msa_ctx *c) {
+    int rc;
+    if (c->stage < 1) return fail(c, MSA_ERR_ARG, "msa_count before msa_split_columns");
+    // artist pass over artist.csv records from its getline header end
+    const u64 b = c->a_hdr_getline, e = c->acol_len;
+    State init{0, b, 0, 0, 0, 0}, fin;
+    if ((rc = run_scan_fn(c, c->acol.as<u8>(), b, e, init, &fin))) return rc;
+    const u64 nterm = fin.rec;
+    c->nrec_a = nterm + (fin.rs < e ? 1 : 0);
+    const u64 cap = nterm + 2;
+    HIPC(c, ensure(c->ar_start, cap * 8));
+    HIPC(c, ensure(c->ar_term, cap * 8));
+    HIPC(c, ensure(c->arena, e + 64));
+    HIPC(c, ensure(c->key_off, cap * 8));
+    HIPC(c, ensure(c->key_len, cap * 4));
+    HIPC(c, ensure(c->key_slot, cap * 8));
+    HIPC(c, hipMemcpyAsync(c->ar_start.p, &b, 8, hipMemcpyHostToDevice, c->stream));
+    if (e > b) {
+        ScanArgs a{};
+        a.buf = c->acol.as<u8>();
+        a.seg_begin = b;
+        a.seg_end = e;
+        a.nchunks = (u32)((e - b + MSA_CHUNK - 1) / MSA_CHUNK);
+        a.carry = c->carry.as<State>();
+        a.rec_start = c->ar_start.as<u64>();
+        a.rec_term = c->ar_term.as<u64>();
+        a.rec_cap = cap;
+        a.ctr = c->ctr.as<Counters>();
+        a.want_term = 1;
+        HIPC(c, msa_launch_scan(a, 1, c->stream));
+    }
+    if (fin.rs < e) HIPC(c, hipMemcpyAsync(c->ar_term.as<u64>() + (c->nrec_a - 1), &e, 8, hipMemcpyHostToDevice, c->stream));
+    HIPC(c, msa_launch_artist_key(c->acol.as<u8>(), c->ar_start.as<u64>(), c->ar_term.as<u64>(), c->nrec_a,
+                                  c->arena.as<u8>(), c->key_off.as<u64>(), c->key_len.as<u32>(), c->key_slot.as<u64>(),
+                                  c->a_tab.as<u64>(), c->a_slots - 1, c->a_list.as<u32>(), c->a_slots / 2,
+                                  c->ctr.as<Counters>(), c->stream));
+    if ((rc = sync_counters(c))) return rc;
+    // words longer than 16 bytes
+    const u64 nl = std::min<u64>(c->h_ctr.l_occ, c->l_occ_cap);
+    HIPC(c, msa_launch_long(c->in, c->n, c->l_pos.as<u64>(), nl, c->l_len.as<u32>(), c->l_slot.as<u64>(),
+                            c->l_tab.as<u64>(), c->lt_slots - 1, c->l_list.as<u32>(), c->lt_slots / 2,
+                            c->ctr.as<Counters>(), c->stream));
+    if ((rc = sync_counters(c))) return rc;
+    c->s_used_prev = std::min<u64>(c->h_ctr.s_claimed, c->s_slots / 2);
+    c->m_used_prev = std::min<u64>(c->h_ctr.m_claimed, c->m_slots / 2);
+    c->lt_used_prev = std::min<u64>(c->h_ctr.l_claimed, c->lt_slots / 2);
+    c->a_used_prev = std::min<u64>(c->h_ctr.a_claimed, c->a_slots / 2);
+    if (c->h_ctr.overflow) return fail(c, MSA_ERR_CAPACITY, "table capacity overflow (flags 0x%llx)",
+                                       (unsigned long long)c->h_ctr.overflow);
+    if (c->h_ctr.collision)
+        return fail(c, MSA_ERR_COLLISION, "64-bit key hash collision detected (%llu occurrences)",
+                    (unsigned long long)c->h_ctr.collision);
+    c->sum.total_songs = (long long)c->nrec_a;
+    c->sum.total_words = (long long)c->h_ctr.total_words;
+    c->sum.n_words = c->h_ctr.s_claimed + c->h_ctr.m_claimed + c->h_ctr.l_claimed;
+    c->sum.n_artists = c->h_ctr.a_claimed;
+    c->sum.n_records = c->nrec;
+    c->stage = 2;
+    return MSA_OK;
+}
+
+// ------------------------------------------------------------------ stage 3
+static int sort_and_blob(msa_ctx *c, Ranked &R, const u8 *arena, const u64 *key_off, const u32 *key_len) {
+    const u64 n = R.n;
+    R.host_valid = false;
+    if (n == 0) {
+        R.blob_len = 0;
+        return MSA_OK;
+    }
+    const u64 nb = msa_radix_blocks(n);
+    for (int s = 1; s < 3; ++s) {
+        for (int k = 0; k < 3; ++k) HIPC(c, ensure(R.K[s][k], n * 8));
+        HIPC(c, ensure(R.V[s], n * 4));
+    }
+    HIPC(c, ensure(R.bhist, nb * 256 * 8));
+    HIPC(c, ensure(R.boff, nb * 256 * 8));
+    HIPC(c, ensure(R.bsum, ((nb * 256 + 1023) / 1024 + 1) * 8));
+    HIPC(c, ensure(R.ghist, 24 * 256 * 4));
+    HIPC(c, msa_launch_radix_hist_all(R.K[0][0].as<u64>(), R.K[0][1].as<u64>(), R.K[0][2].as<u64>(), n,
+                                      R.ghist.as<u32>(), c->stream));
+    std::vector<u32> gh(24 * 256);
+    HIPC(c, hipMemcpyAsync(gh.data(), R.ghist.p, gh.size() * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    int cur = 0;
+    // digit d: 0..7 = K0 bytes, 8..15 = K1 bytes, 16..23 = K2 bytes (LSD first)
+    for (u32 d = 0; d < 24; ++d) {
+        bool trivial = false;
+        for (int i = 0; i < 256; ++i)
+            if (gh[d * 256 + i] == n) { trivial = true; break; }
+        if (trivial) continue;
+        const int nxt = (cur == 1) ? 2 : 1;
+        HIPC(c, msa_launch_radix_pass(R.K[cur][0].as<u64>(), R.K[cur][1].as<u64>(), R.K[cur][2].as<u64>(),
+                                      R.V[cur].as<u32>(), n, d, R.bhist.as<u64>(), R.boff.as<u64>(), R.bsum.as<u64>(),
+                                      R.K[nxt][0].as<u64>(), R.K[nxt][1].as<u64>(), R.K[nxt][2].as<u64>(),
+                                      R.V[nxt].as<u32>(), c->stream));
+        cur = nxt;
+    }
+    HIPC(c, ensure(R.order, n * 4));
+    HIPC(c, msa_launch_fixup(R.K[cur][0].as<u64>(), R.K[cur][1].as<u64>(), R.K[cur][2].as<u64>(), R.V[cur].as<u32>(),
+                             n, R.ref.as<u64>(), c->in, c->l_pos.as<u64>(), c->l_len.as<u32>(), arena, key_off,
+                             key_len, R.order.as<u32>(), c->stream));
+    // key blob in rank order
+    HIPC(c, ensure(R.len, n * 8));
+    HIPC(c, ensure(R.off, (n + 1) * 8));
+    HIPC(c, ensure(R.counts, n * 8));
+    HIPC(c, ensure(c->scan_total, 64));
+    HIPC(c, ensure(c->scan_bsum, ((n + 1023) / 1024 + 1) * 8));
+    HIPC(c, msa_launch_blob(R.order.as<u32>(), n, R.ref.as<u64>(), R.K[0][1].as<u64>(), R.K[0][2].as<u64>(),
+                            R.cnt.as<u64>(), c->in, c->l_pos.as<u64>(), c->l_len.as<u32>(), arena, key_off, key_len,
+                            R.len.as<u64>(), R.off.as<u64>(), c->scan_bsum.as<u64>(), c->scan_total.as<u64>(), nullptr,
+                            nullptr, c->stream, 0));
+    HIPC(c, hipMemcpyAsync(&R.blob_len, c->scan_total.p, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    HIPC(c, ensure(R.blob, R.blob_len + 16));
+    HIPC(c, msa_launch_blob(R.order.as<u32>(), n, R.ref.as<u64>(), R.K[0][1].as<u64>(), R.K[0][2].as<u64>(),
+                            R.cnt.as<u64>(), c->in, c->l_pos.as<u64>(), c->l_len.as<u32>(), arena, key_off, key_len,
+                            R.len.as<u64>(), R.off.as<u64>(), c->scan_bsum.as<u64>(), c->scan_total.as<u64>(),
+                            R.blob.as<u8>(), R.counts.as<u64>(), c->stream, 1));
+    return MSA_OK;
+}
+
+static int do_rank(msa_ctx *c) {
+    int rc;
+    if (c->stage < 2) return fail(c, MSA_ERR_ARG, "msa_rank before msa_count");
+    // words
+    Ranked &W = c->rw;
+    W.n = c->sum.n_words;
+    if (W.n) {
+        for (int k = 0; k < 3; ++k) HIPC(c, ensure(W.K[0][k], W.n * 8));
+        HIPC(c, ensure(W.V[0], W.n * 4));
+        HIPC(c, ensure(W.ref, W.n * 8));
+        HIPC(c, ensure(W.cnt, W.n * 8));
+        EntryArgs ea{};
+        ea.s_tab = c->s_tab.as<u64>();
+        ea.s_list = c->s_list.as<u32>();
+        ea.ns = c->h_ctr.s_claimed;
+        ea.m_tab = c->m_tab.as<u64>();
+        ea.m_list = c->m_list.as<u32>();
+        ea.nm = c->h_ctr.m_claimed;
+        ea.l_tab = c->l_tab.as<u64>();
+        ea.l_list = c->l_list.as<u32>();
+        ea.nl = c->h_ctr.l_claimed;
+        ea.buf = c->in;
+        ea.l_pos = c->l_pos.as<u64>();
+        ea.l_len = c->l_len.as<u32>();
+        ea.K2 = W.K[0][0].as<u64>();
+        ea.K1 = W.K[0][1].as<u64>();
+        ea.K0 = W.K[0][2].as<u64>();
+        ea.val = W.V[0].as<u32>();
+        ea.ref = W.ref.as<u64>();
+        ea.cnt = W.cnt.as<u64>();
+        HIPC(c, msa_launch_word_entries(ea, c->stream));
+    }
+    if ((rc = sort_and_blob(c, W, nullptr, nullptr, nullptr))) return rc;
+    // artists
+    Ranked &A = c->ra;
+    A.n = c->sum.n_artists;
+    if (A.n) {
+        for (int k = 0; k < 3; ++k) HIPC(c, ensure(A.K[0][k], A.n * 8));
+        HIPC(c, ensure(A.V[0], A.n * 4));
+        HIPC(c, ensure(A.ref, A.n * 8));
+        HIPC(c, ensure(A.cnt, A.n * 8));
+        HIPC(c, msa_launch_artist_entries(c->a_tab.as<u64>(), c->a_list.as<u32>(), A.n, c->arena.as<u8>(),
+                                          c->key_off.as<u64>(), c->key_len.as<u32>(), A.K[0][0].as<u64>(),
+                                          A.K[0][1].as<u64>(), A.K[0][2].as<u64>(), A.V[0].as<u32>(), A.ref.as<u64>(),
+                                          A.cnt.as<u64>(), c->stream));
+    }
+    if ((rc = sort_and_blob(c, A, c->arena.as<u8>(), c->key_off.as<u64>(), c->key_len.as<u32>()))) return rc;
+    HIPC(c, hipStreamSynchronize(c->stream));
+    c->stage = 3;
+    return MSA_OK;
+}
+
+static int fetch_ranked(msa_ctx *c, Ranked &R) {
+    if (R.host_valid) return MSA_OK;
+    R.h_counts.resize(R.n);
+    R.h_off.resize(R.n + 1);
+    R.h_blob.resize(R.blob_len + 1);
+    if (R.n) {
+        HIPC(c, hipMemcpy(R.h_counts.data(), R.counts.p, R.n * 8, hipMemcpyDeviceToHost));
+        HIPC(c, hipMemcpy(R.h_off.data(), R.off.p, R.n * 8, hipMemcpyDeviceToHost));
+        if (R.blob_len) HIPC(c, hipMemcpy(R.h_blob.data(), R.blob.p, R.blob_len, hipMemcpyDeviceToHost));
+    }
+    R.h_off[R.n] = R.blob_len;
+    R.host_valid = true;
+    return MSA_OK;
+}
+
+// ===================================================================== C ABI
+extern "C" {
+
+int msa_create(int device, msa_ctx **out) {
+    if (!out) return MSA_ERR_ARG;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return MSA_ERR_HIP;
+    if (device < 0 || device >= ndev) return MSA_ERR_ARG;
+    if (hipSetDevice(device) != hipSuccess) return MSA_ERR_HIP;
+    msa_ctx *c = new msa_ctx();
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return MSA_ERR_HIP;
+    }
+    *out = c;
+    return MSA_OK;
+}
+
+void msa_destroy(msa_ctx *c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    DevBuf *all[] = {&c->in_own, &c->sums, &c->carry, &c->runpre, &c->small, &c->rec_start, &c->rec_term,
+                     &c->f0rel, &c->f3rel, &c->nulrel, &c->acol, &c->alen, &c->aoff, &c->tcol, &c->tlen, &c->toff,
+                     &c->scan_bsum, &c->scan_total, &c->ar_start, &c->ar_term, &c->arena, &c->key_off,
+                     &c->key_len, &c->key_slot, &c->s_tab, &c->s_list, &c->m_tab, &c->m_list, &c->l_pos, &c->l_len,
+                     &c->l_slot, &c->l_tab, &c->l_list, &c->a_tab, &c->a_list, &c->ctr};
+    for (DevBuf *b : all) release(*b);
+    for (Ranked *R : {&c->rw, &c->ra}) {
+        for (auto &s : R->K)
+            for (auto &k : s) release(k);
+        for (auto &v : R->V) release(v);
+        DevBuf *rb[] = {&R->ref, &R->cnt, &R->order, &R->len, &R->off, &R->blob, &R->counts, &R->bhist, &R->boff,
+                        &R->bsum, &R->ghist};
+        for (DevBuf *b : rb) release(*b);
+    }
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char *msa_last_error(const msa_ctx *c) { return c ? c->err.c_str() : "no context"; }
+void *msa_stream(msa_ctx *c) { return c ? (void *)c->stream : nullptr; }
+
+int msa_sync(msa_ctx *c) {
+    if (!c) return MSA_ERR_ARG;
+    HIPC(c, hipStreamSynchronize(c->stream));
+    return MSA_OK;
+}
+
+int msa_load_csv(msa_ctx *c, const void *host, size_t n) {
+    if (!c || (!host && n)) return MSA_ERR_ARG;
+    HIPC(c, hipSetDevice(c->device));
+    HIPC(c, ensure(c->in_own, n + MSA_INPUT_PAD));
+    if (n) HIPC(c, hipMemcpy(c->in_own.p, host, n, hipMemcpyHostToDevice));
+    HIPC(c, hipMemset(c->in_own.as<char>() + n, 0, MSA_INPUT_PAD));
+    c->in = c->in_own.as<u8>();
+    c->n = n;
+    c->stage = 0;
+    return MSA_OK;
+}
+
+int msa_bind_csv(msa_ctx *c, const void *dev, size_t n) {
+    if (!c || (!dev && n)) return MSA_ERR_ARG;
+    c->in = reinterpret_cast<const u8 *>(dev);
+    c->n = n;
+    c->stage = 0;
+    return MSA_OK;
+}
+
+int msa_split_columns(msa_ctx *c, int flags) {
+    if (!c) return MSA_ERR_ARG;
+    HIPC(c, hipSetDevice(c->device));
+    return do_split(c, flags);
+}
+
+int msa_count(msa_ctx *c) {
+    if (!c) return MSA_ERR_ARG;
+    HIPC(c, hipSetDevice(c->device));
+    return do_count(c);
+}
+
+int msa_rank(msa_ctx *c) {
+    if (!c) return MSA_ERR_ARG;
+    HIPC(c, hipSetDevice(c->device));
+    return do_rank(c);
+}
+
+int msa_run(msa_ctx *c, int flags) {
+    if (!c) return MSA_ERR_ARG;
+    HIPC(c, hipSetDevice(c->device));
+    int rc = MSA_OK;
+    for (int attempt = 0; attempt < 4; ++attempt) {
+        rc = do_split(c, flags);
+        if (!rc) rc = do_count(c);
+        if (rc == MSA_ERR_CAPACITY) {
+            c->cap_scale *= 4;
+            continue;
+        }
+        break;
+    }
+    if (!rc) rc = do_rank(c);
+    return rc;
+}
+
+int msa_get_summary(msa_ctx *c, msa_summary *out) {
+    if (!c || !out) return MSA_ERR_ARG;
+    if (c->stage < 1) return fail(c, MSA_ERR_ARG, "no results yet");
+    *out = c->sum;
+    return MSA_OK;
+}
+
+int msa_get_ranked(msa_ctx *c, int table, uint64_t first, uint64_t count, long long *counts, uint64_t *offsets,
+                   char *keys, uint64_t keys_cap, uint64_t *keys_needed) {
+    if (!c || (table != MSA_TABLE_WORDS && table != MSA_TABLE_ARTISTS)) return MSA_ERR_ARG;
+    if (c->stage < 3) return fail(c, MSA_ERR_ARG, "msa_get_ranked before msa_rank");
+    HIPC(c, hipSetDevice(c->device));
+    Ranked &R = table == MSA_TABLE_WORDS ? c->rw : c->ra;
+    int rc = fetch_ranked(c, R);
+    if (rc) return rc;
+    if (first > R.n) first = R.n;
+    if (count > R.n - first) count = R.n - first;
+    const u64 kb = R.h_off[first], ke = R.h_off[first + count];
+    if (keys_needed) *keys_needed = ke - kb;
+    if (keys && keys_cap < ke - kb) return fail(c, MSA_ERR_CAPACITY, "key buffer too small");
+    for (u64 i = 0; i < count; ++i) {
+        if (counts) counts[i] = (long long)R.h_counts[first + i];
+        if (offsets) offsets[i] = R.h_off[first + i] - kb;
+    }
+    if (offsets) offsets[count] = ke - kb;
+    if (keys && ke > kb) memcpy(keys, R.h_blob.data() + kb, ke - kb);
+    return MSA_OK;
+}
+
+int msa_write_table_csv(msa_ctx *c, int table, const char *path, const char *key_header, int limit) {
+    if (!c || !path || !key_header) return MSA_ERR_ARG;
+    if (table != MSA_TABLE_WORDS && table != MSA_TABLE_ARTISTS) return MSA_ERR_ARG;
+    if (c->stage < 3) return fail(c, MSA_ERR_ARG, "msa_write_table_csv before msa_rank");
+    HIPC(c, hipSetDevice(c->device));
+    Ranked &R = table == MSA_TABLE_WORDS ? c->rw : c->ra;
+    int rc = fetch_ranked(c, R);
+    if (rc) return rc;
+    FILE *fp = fopen(path, "w");
+    if (!fp) return fail(c, MSA_ERR_IO, "Failed to open output file %s: %s", path, strerror(errno));
+    std::vector<char> out;
+    out.reserve(1 << 20);
+    auto flush = [&]() {
+        if (!out.empty()) fwrite(out.data(), 1, out.size(), fp);
+        out.clear();
+    };
+    fprintf(fp, "%s,count\n", key_header);
+    u64 m = R.n;
+    if (limit > 0 && (u64)limit < m) m = (u64)limit;
+    char num[32];
+    for (u64 i = 0; i < m; ++i) {
+        out.push_back('"');
+        for (u64 k = R.h_off[i]; k < R.h_off[i + 1]; ++k) {
+            char ch = R.h_blob[k];
+            if (ch == '"') out.push_back('"');
+            out.push_back(ch);
+        }
+        int l = snprintf(num, sizeof num, "\",%lld\n", (long long)R.h_counts[i]);
+        out.insert(out.end(), num, num + l);
+        if (out.size() > (1 << 20)) flush();
+    }
+    flush();
+    if (fclose(fp) != 0) return fail(c, MSA_ERR_IO, "write failed: %s", path);
+    return MSA_OK;
+}
+
+int msa_get_split_column(msa_ctx *c, int which, char **out, size_t *len) {
+    if (!c || !out || !len || (which != 0 && which != 1)) return MSA_ERR_ARG;
+    if (c->stage < 1) return fail(c, MSA_ERR_ARG, "msa_get_split_column before msa_split_columns");
+    if (which == 1 && !c->have_tcol)
+        return fail(c, MSA_ERR_ARG, "text column not materialised (pass MSA_SPLIT_TEXT_COLUMN)");
+    HIPC(c, hipSetDevice(c->device));
+    const DevBuf &b = which ? c->tcol : c->acol;
+    const u64 n = which ? c->tcol_len : c->acol_len;
+    char *p = (char *)malloc(n + 1);
+    if (!p) return fail(c, MSA_ERR_ARG, "out of host memory");
+    HIPC(c, hipStreamSynchronize(c->stream));
+    if (n) HIPC(c, hipMemcpy(p, b.p, n, hipMemcpyDeviceToHost));
+    p[n] = 0;
+    *out = p;
+    *len = n;
+    return MSA_OK;
+}
+
+int msa_shard_function(msa_ctx *c, void *fn_out) {
+    if (!c || !fn_out) return MSA_ERR_ARG;
+    return fail(c, MSA_ERR_ARG, "multi-shard scan not available in this build");
+}
+
+int msa_shard_set_prefix(msa_ctx *c, const void *fns, int nshards_before) {
+    (void)fns;
+    (void)nshards_before;
+    if (!c) return MSA_ERR_ARG;
+    return fail(c, MSA_ERR_ARG, "multi-shard scan not available in this build");
+}
+
+}  // extern "C"

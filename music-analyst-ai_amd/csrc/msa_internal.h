@@ -1,0 +1,289 @@
+// msa_internal.h -- shared device/host definitions of libmsa_hip (gfx950).
+//
+// Byte layout in HBM: the CSV is one flat byte array; all per-record data is
+// structure-of-arrays indexed by record number; hash tables are open-address
+// arrays of 16/32-byte slots.  Scan granularity:
+//   MSA_ITER  = 1 KiB  = one wave-iteration (64 lanes x 16 B, one dwordx4 each)
+//   MSA_CHUNK = 16 KiB = the unit whose reader-state transfer function is
+//               summarised (K1) and scanned (K2) before the main pass (K3).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef uint64_t u64;
+typedef uint32_t u32;
+typedef uint16_t u16;
+typedef uint8_t u8;
+
+#define MSA_ITER 1024
+#define MSA_CHUNK 16384
+#define MSA_ITERS (MSA_CHUNK / MSA_ITER)
+
+// ---------------------------------------------------------------------------
+// Reader state.  The reference's record reader (parallel_spotify.c:549-633)
+// and field splitter (258-304) are a finite-state machine over bytes; what a
+// later byte needs from everything before it is:
+//   p     quote parity (1 = inside a quoted run)
+//   cr    previous byte was an unquoted '\r' (a following '\n' is swallowed)
+//   c     unquoted commas since the record start, saturated at 3
+//   z     a NUL was seen since the record start (C-string truncation)
+//   rec   index of the current record (terminators so far)
+//   rs    absolute offset where the current record starts
+struct State {
+    u64 rec;
+    u64 rs;
+    u32 p, cr, c, z;
+};
+
+// Transfer function of a byte range, one entry per input (p, cr) in
+// {(0,0), (1,0), (0,1)}.  If the range holds a terminator ("has"), c/z/rs are
+// the values after its last terminator; otherwise c adds (saturating) and z ORs.
+struct FnEnt {
+    u64 nterm;
+    u64 rs;       // absolute start of the record open at the range end (if has)
+    u32 p, cr, has, c, z, pad;
+};
+struct Fn {
+    FnEnt e[3];
+};
+
+// K1 output per chunk: the chunk's function for hypotheses p=0 / p=1 with
+// cr=0 (the cr=1 entry is derived from first_nl).  Packed flags word:
+//   [15:0] nterm  [17:16] c  [18] z  [19] cr_out  [20] parity  [21] first_nl
+struct ChunkSum {
+    u32 h[2];
+    u32 last_end[2];  // offset in chunk just past the last terminator
+};
+
+__host__ __device__ inline u32 st_index(u32 p, u32 cr) { return cr ? 2u : p; }
+
+__host__ __device__ inline FnEnt chunk_entry(const ChunkSum &s, u64 base, u32 idx) {
+    FnEnt e;
+    u32 hyp = (idx == 1) ? 1u : 0u;
+    u32 f = s.h[hyp];
+    u32 nterm = f & 0xFFFFu;
+    e.pad = 0;
+    e.p = hyp ^ ((f >> 20) & 1u);
+    e.cr = (f >> 19) & 1u;
+    e.c = (f >> 16) & 3u;
+    e.z = (f >> 18) & 1u;
+    e.rs = base + s.last_end[hyp];
+    if (idx == 2 && ((f >> 21) & 1u)) nterm -= 1;  // leading '\n' swallowed by the carried '\r'
+    e.nterm = nterm;
+    e.has = nterm > 0;
+    return e;
+}
+
+__host__ __device__ inline FnEnt fn_then(const FnEnt &a, const Fn &g) {
+    const FnEnt &b = g.e[st_index(a.p, a.cr)];
+    FnEnt r;
+    r.p = b.p;
+    r.cr = b.cr;
+    r.nterm = a.nterm + b.nterm;
+    r.has = a.has | b.has;
+    if (b.has) {
+        r.c = b.c; r.z = b.z; r.rs = b.rs;
+    } else {
+        u32 c = a.c + b.c;
+        r.c = c > 3 ? 3 : c;
+        r.z = a.z | b.z;
+        r.rs = a.rs;
+    }
+    r.pad = 0;
+    return r;
+}
+
+__host__ __device__ inline Fn fn_compose(const Fn &f, const Fn &g) {  // f then g
+    Fn r;
+    for (int i = 0; i < 3; ++i) r.e[i] = fn_then(f.e[i], g);
+    return r;
+}
+
+__host__ __device__ inline Fn fn_identity(u64 pos) {
+    Fn r;
+    for (u32 i = 0; i < 3; ++i) {
+        r.e[i].nterm = 0; r.e[i].rs = pos; r.e[i].has = 0; r.e[i].c = 0; r.e[i].z = 0; r.e[i].pad = 0;
+        r.e[i].p = (i == 1); r.e[i].cr = (i == 2);
+    }
+    return r;
+}
+
+__host__ __device__ inline State fn_apply(const State &s, const Fn &f) {
+    const FnEnt &b = f.e[st_index(s.p, s.cr)];
+    State r;
+    r.p = b.p;
+    r.cr = b.cr;
+    r.rec = s.rec + b.nterm;
+    if (b.has) { r.c = b.c; r.z = b.z; r.rs = b.rs; }
+    else { u32 c = s.c + b.c; r.c = c > 3 ? 3 : c; r.z = s.z | b.z; r.rs = s.rs; }
+    return r;
+}
+
+// ---------------------------------------------------------------------------
+// SWAR byte classification (4 bytes per u32, exact, no cross-byte carries).
+__device__ __forceinline__ u32 swar_eq(u32 x, u32 byte) {
+    u32 y = x ^ (byte * 0x01010101u);
+    return ~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y | 0x7F7F7F7Fu);  // 0x80 where equal
+}
+__device__ __forceinline__ u32 swar_ge7(u32 y7, u32 c) {  // y7 bytes < 0x80; 0x80 where byte >= c
+    return (y7 + (0x80u - c) * 0x01010101u) & 0x80808080u;
+}
+// 0x80-per-byte mask -> 4-bit mask (byte j -> bit j)
+__device__ __forceinline__ u32 swar_pack4(u32 m) { return (((m >> 7) * 0x00204081u) >> 21) & 0xFu; }
+
+// Token byte of process_lyrics (parallel_spotify.c:359): isalnum (C locale) or '\''.
+__device__ __forceinline__ u32 swar_tok(u32 x) {
+    u32 hi = x & 0x80808080u;
+    u32 y = x & 0x7F7F7F7Fu;
+    u32 l = y | 0x20202020u;
+    u32 alpha = swar_ge7(l, 'a') & ~swar_ge7(l, 'z' + 1);
+    u32 digit = swar_ge7(y, '0') & ~swar_ge7(y, '9' + 1);
+    return ((alpha | digit) & ~hi) | swar_eq(x, '\'');
+}
+
+struct Classes {
+    u32 Q, C, NL, CR, Z, T;  // 16-bit masks, bit j = byte j of the lane's 16 bytes
+};
+
+__device__ __forceinline__ Classes classify16(uint4 v, u32 vmask) {
+    Classes k;
+    u32 w[4] = {v.x, v.y, v.z, v.w};
+    u32 Q = 0, C = 0, NL = 0, CR = 0, Z = 0, T = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        Q |= swar_pack4(swar_eq(w[i], '"')) << (4 * i);
+        C |= swar_pack4(swar_eq(w[i], ',')) << (4 * i);
+        NL |= swar_pack4(swar_eq(w[i], '\n')) << (4 * i);
+        CR |= swar_pack4(swar_eq(w[i], '\r')) << (4 * i);
+        Z |= swar_pack4(swar_eq(w[i], 0)) << (4 * i);
+        T |= swar_pack4(swar_tok(w[i])) << (4 * i);
+    }
+    k.Q = Q & vmask; k.C = C & vmask; k.NL = NL & vmask; k.CR = CR & vmask; k.Z = Z & vmask; k.T = T & vmask;
+    return k;
+}
+
+__device__ __forceinline__ u32 tok16(uint4 v, u32 vmask) {
+    return (swar_pack4(swar_tok(v.x)) | (swar_pack4(swar_tok(v.y)) << 4) |
+            (swar_pack4(swar_tok(v.z)) << 8) | (swar_pack4(swar_tok(v.w)) << 12)) & vmask;
+}
+
+// exclusive prefix-xor over 16 bits: bit j = xor of bits < j
+__device__ __forceinline__ u32 pxor_excl16(u32 q) {
+    u32 x = q << 1;
+    x ^= x << 1;
+    x ^= x << 2;
+    x ^= x << 4;
+    x ^= x << 8;
+    return x & 0xFFFFu;
+}
+
+// ---------------------------------------------------------------------------
+// Wave (64-lane) helpers.
+__device__ __forceinline__ u32 lane_id() { return __lane_id(); }
+__device__ __forceinline__ u32 mbcnt(u64 m) {  // popcount of m's bits below this lane
+    return __builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, 0u));
+}
+// Exclusive wave prefix sum of small values (< 2^BITS) via ballot bit-planes.
+template <int BITS>
+__device__ __forceinline__ u32 wave_prefix(u32 x, u32 &total) {
+    u32 pre = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < BITS; ++k) {
+        u64 b = __ballot((x >> k) & 1u);
+        pre += mbcnt(b) << k;
+        tot += (u32)__popcll(b) << k;
+    }
+    total = tot;
+    return pre;
+}
+__device__ __forceinline__ u32 readlane(u32 x, int l) { return __builtin_amdgcn_readlane(x, l); }
+__device__ __forceinline__ u64 readlane64(u64 x, int l) {
+    return ((u64)readlane((u32)(x >> 32), l) << 32) | readlane((u32)x, l);
+}
+__device__ __forceinline__ u64 wave_sum64(u64 v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// ---------------------------------------------------------------------------
+// Hashing.
+__host__ __device__ __forceinline__ u64 fmix64(u64 k) {
+    k ^= k >> 33;
+    k *= 0xff51afd7ed558ccdULL;
+    k ^= k >> 33;
+    k *= 0xc4ceb9fe1a85ec53ULL;
+    k ^= k >> 33;
+    return k;
+}
+__device__ __forceinline__ u32 lds_hash(u64 k) { return (u32)((k * 0x9E3779B97F4A7C15ULL) >> 40); }
+
+// Lower-case ASCII letters in 8 packed bytes (all bytes < 0x80 here).
+__device__ __forceinline__ u64 lower8(u64 x) {
+    u64 y = x & 0x7F7F7F7F7F7F7F7FULL;
+    u64 ge_a = (y + 0x3F3F3F3F3F3F3F3FULL) & 0x8080808080808080ULL;  // >= 'A' (0x41)
+    u64 ge_z = (y + 0x2525252525252525ULL) & 0x8080808080808080ULL;  // >= 'Z'+1 (0x5B)
+    return x | ((ge_a & ~ge_z) >> 2);
+}
+
+// ---------------------------------------------------------------------------
+// Device-resident run counters (one struct, zeroed per run).
+struct Counters {
+    u64 total_words;
+    u64 s_claimed, m_claimed, l_occ, l_claimed, a_claimed;
+    u64 overflow;    // bitmask of capacity overflows
+    u64 collision;   // hash-collision detections
+    u64 songs;
+    u64 pad[7];
+};
+
+enum { OVF_S = 1, OVF_M = 2, OVF_L = 4, OVF_LT = 8, OVF_A = 16, OVF_REC = 32 };
+
+// Arguments of the main scan (K3) and of the ranking-entry builder.
+struct ScanArgs {
+    const u8 *buf;
+    u64 seg_begin, seg_end;
+    u32 nchunks;
+    const State *carry;
+    u64 *rec_start;
+    u64 *rec_term;
+    u32 *f0rel;
+    u32 *f3rel;
+    u32 *nulrel;
+    u64 rec_cap;
+    u64 *s_tab;
+    u64 s_mask;
+    u32 *s_list;
+    u64 s_list_cap;
+    u64 *m_tab;
+    u64 m_mask;
+    u32 *m_list;
+    u64 m_list_cap;
+    u64 *l_pos;
+    u64 l_cap;
+    Counters *ctr;
+    int want_term;
+};
+struct EntryArgs {
+    const u64 *s_tab;
+    const u32 *s_list;
+    u64 ns;
+    const u64 *m_tab;
+    const u32 *m_list;
+    u64 nm;
+    const u64 *l_tab;
+    const u32 *l_list;
+    u64 nl;
+    const u8 *buf;
+    const u64 *l_pos;
+    const u32 *l_len;
+    u64 *K2, *K1, *K0;
+    u32 *val;
+    u64 *ref;
+    u64 *cnt;
+};
+
+#define MSA_HIP_CHECK(x)                                                     \
+    do {                                                                     \
+        hipError_t e_ = (x);                                                 \
+        if (e_ != hipSuccess) return msa_fail_hip(e_, #x, __FILE__, __LINE__); \
+    } while (0)

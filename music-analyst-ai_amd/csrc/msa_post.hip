@@ -1,0 +1,642 @@
+// msa_post.hip -- everything after the main scan:
+//   * artist column: duplicate_field (parallel_spotify.c:215-255) of field 0,
+//     split_dataset_columns' artist.csv (640-721), and the artist pass's
+//     duplicate_field(line, 0) + ht_put (948-998) as exact 64-bit-hash counts
+//   * words longer than 16 bytes (H-table + byte-exact verification)
+//   * ranking: stable LSD radix sort on (count desc, first 16 key bytes) with
+//     an exact strcmp fix-up of the rare equal-prefix runs -- the order of
+//     entry_compare_desc (178-188) without a comparison sort
+//   * generic exclusive scan (u64)
+#include "msa_internal.h"
+#include "msa_tables.h"
+
+namespace {
+__device__ __forceinline__ bool c_space(u32 c) { return c == ' ' || (c >= 9 && c <= 13); }
+__device__ __forceinline__ bool c_tok(u32 c) {
+    return ((c | 0x20u) >= 'a' && (c | 0x20u) <= 'z') || (c >= '0' && c <= '9') || c == '\'';
+}
+__device__ __forceinline__ u64 bswap64(u64 x) { return __builtin_bswap64(x); }
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// generic exclusive scan over u64 (3 phases)
+#define SCAN_T 256
+#define SCAN_PER 4
+#define SCAN_TILE (SCAN_T * SCAN_PER)
+
+__global__ __launch_bounds__(SCAN_T) void k_scan_reduce(const u64 *__restrict__ in, u64 n, u64 *__restrict__ bsum) {
+    __shared__ u64 red[SCAN_T / 64];
+    const u64 base = (u64)blockIdx.x * SCAN_TILE;
+    u64 s = 0;
+    for (int i = 0; i < SCAN_PER; ++i) {
+        const u64 idx = base + (u64)i * SCAN_T + threadIdx.x;
+        if (idx < n) s += in[idx];
+    }
+    s = wave_sum64(s);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        u64 t = 0;
+        for (int w = 0; w < SCAN_T / 64; ++w) t += red[w];
+        bsum[blockIdx.x] = t;
+    }
+}
+
+__global__ __launch_bounds__(SCAN_T) void k_scan_top(u64 *__restrict__ bsum, u64 nb, u64 *__restrict__ total) {
+    __shared__ u64 part[SCAN_T];
+    const u64 per = (nb + SCAN_T - 1) / SCAN_T;
+    const u64 a = min(nb, (u64)threadIdx.x * per), b = min(nb, a + per);
+    u64 s = 0;
+    for (u64 i = a; i < b; ++i) s += bsum[i];
+    part[threadIdx.x] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        u64 acc = 0;
+        for (int i = 0; i < SCAN_T; ++i) { u64 v = part[i]; part[i] = acc; acc += v; }
+        if (total) *total = acc;
+    }
+    __syncthreads();
+    u64 acc = part[threadIdx.x];
+    for (u64 i = a; i < b; ++i) { u64 v = bsum[i]; bsum[i] = acc; acc += v; }
+}
+
+__global__ __launch_bounds__(SCAN_T) void k_scan_down(const u64 *__restrict__ in, u64 n, const u64 *__restrict__ bsum,
+                                                     u64 *__restrict__ out) {
+    __shared__ u64 wsum[SCAN_T / 64];
+    const u64 base = (u64)blockIdx.x * SCAN_TILE;
+    const u32 lane = lane_id(), w = threadIdx.x >> 6;
+    // thread t owns elements base + t*SCAN_PER .. +SCAN_PER (blocked)
+    u64 v[SCAN_PER], s = 0;
+    for (int i = 0; i < SCAN_PER; ++i) {
+        const u64 idx = base + (u64)threadIdx.x * SCAN_PER + i;
+        v[i] = idx < n ? in[idx] : 0;
+        s += v[i];
+    }
+    // inclusive wave scan of s
+    u64 x = s;
+    for (int o = 1; o < 64; o <<= 1) {
+        u64 y = __shfl_up(x, o);
+        if (lane >= (u32)o) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    u64 pre = bsum[blockIdx.x];
+    for (u32 i = 0; i < w; ++i) pre += wsum[i];
+    pre += x - s;
+    for (int i = 0; i < SCAN_PER; ++i) {
+        const u64 idx = base + (u64)threadIdx.x * SCAN_PER + i;
+        if (idx < n) out[idx] = pre;
+        pre += v[i];
+    }
+}
+
+hipError_t msa_exclusive_scan(const u64 *in, u64 n, u64 *out, u64 *bsum_scratch, u64 *total, hipStream_t s) {
+    if (n == 0) {
+        if (total) return hipMemsetAsync(total, 0, sizeof(u64), s);
+        return hipSuccess;
+    }
+    const u64 nb = (n + SCAN_TILE - 1) / SCAN_TILE;
+    hipLaunchKernelGGL(k_scan_reduce, dim3((u32)nb), dim3(SCAN_T), 0, s, in, n, bsum_scratch);
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(SCAN_T), 0, s, bsum_scratch, nb, total);
+    hipLaunchKernelGGL(k_scan_down, dim3((u32)nb), dim3(SCAN_T), 0, s, in, n, bsum_scratch, out);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// duplicate_field (parallel_spotify.c:215-255).  Writes to `out` when given;
+// returns the result as (offset into out, length) -- the final trim is done
+// by offset so no byte moves twice.
+struct Span {
+    u64 off, len;
+};
+
+__device__ Span dup_field(const u8 *f, u64 len, int preserve, u8 *out) {
+    u64 s = 0, e = len;
+    while (s < len && c_space(f[s])) ++s;
+    while (e > s && c_space(f[e - 1])) --e;
+    const bool quoted = (e > s + 1 && f[s] == '"' && f[e - 1] == '"');
+    u64 j = 0;
+    if (preserve && quoted) {
+        if (out)
+            for (u64 i = s; i < e; ++i) out[i - s] = f[i];
+        Span r = {0, e - s};
+        return r;  // already trimmed at both ends
+    }
+    u64 a = s, z = e;
+    if (quoted) { ++a; --z; }
+    u64 first_ns = ~0ull, last_ns = 0;
+    for (u64 i = a; i < z; ++i) {
+        u8 c = f[i];
+        if (c == '"' && i + 1 < z && f[i + 1] == '"') ++i;
+        if (out) out[j] = c;
+        if (!c_space(c)) {
+            if (first_ns == ~0ull) first_ns = j;
+            last_ns = j;
+        }
+        ++j;
+    }
+    Span r;
+    if (first_ns == ~0ull) { r.off = 0; r.len = 0; }
+    else { r.off = first_ns; r.len = last_ns + 1 - first_ns; }
+    return r;
+}
+
+// Length of artist.csv line r: |dup_field(field 0, preserve)| + 1, 0 if the
+// record is skipped (record 0 = header, or fewer than 3 commas before a NUL).
+__global__ void k_artist_len(const u8 *__restrict__ buf, const u64 *__restrict__ rec_start,
+                             const u32 *__restrict__ f0rel, const u32 *__restrict__ f3rel, u64 nrec,
+                             u64 *__restrict__ line_len) {
+    const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nrec) return;
+    u64 L = 0;
+    if (r >= 1 && f3rel[r]) {
+        const Span sp = dup_field(buf + rec_start[r], f0rel[r] - 1u, 1, nullptr);
+        L = sp.len + 1;
+    }
+    line_len[r] = L;
+}
+
+__global__ void k_artist_write(const u8 *__restrict__ buf, const u64 *__restrict__ rec_start,
+                               const u32 *__restrict__ f0rel, const u32 *__restrict__ f3rel, u64 nrec,
+                               const u64 *__restrict__ line_off, u64 hdr_len, u8 *__restrict__ col) {
+    const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nrec || r == 0 || !f3rel[r]) return;
+    u8 *dst = col + hdr_len + line_off[r];
+    const Span sp = dup_field(buf + rec_start[r], f0rel[r] - 1u, 1, dst);
+    dst[sp.len] = '\n';
+}
+
+// text.csv line of record r: dup_field(field 3 up to NUL / record end, preserve)
+__device__ __forceinline__ u64 text_field_len(const u64 *rec_start, const u64 *rec_term, const u32 *f3rel,
+                                              const u32 *nulrel, u64 r, u64 *start) {
+    const u64 rs = rec_start[r];
+    u64 end = rec_term[r];
+    if (nulrel[r]) end = min(end, rs + nulrel[r] - 1);
+    const u64 s = rs + f3rel[r] - 1;
+    *start = s;
+    return end > s ? end - s : 0;
+}
+
+__global__ void k_text_len(const u8 *__restrict__ buf, const u64 *__restrict__ rec_start,
+                           const u64 *__restrict__ rec_term, const u32 *__restrict__ f3rel,
+                           const u32 *__restrict__ nulrel, u64 nrec, u64 *__restrict__ line_len) {
+    const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nrec) return;
+    u64 L = 0;
+    if (r >= 1 && f3rel[r]) {
+        u64 s;
+        const u64 n = text_field_len(rec_start, rec_term, f3rel, nulrel, r, &s);
+        L = dup_field(buf + s, n, 1, nullptr).len + 1;
+    }
+    line_len[r] = L;
+}
+
+__global__ void k_text_write(const u8 *__restrict__ buf, const u64 *__restrict__ rec_start,
+                             const u64 *__restrict__ rec_term, const u32 *__restrict__ f3rel,
+                             const u32 *__restrict__ nulrel, u64 nrec, const u64 *__restrict__ line_off,
+                             u64 hdr_len, u8 *__restrict__ col) {
+    const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nrec || r == 0 || !f3rel[r]) return;
+    u64 s;
+    const u64 n = text_field_len(rec_start, rec_term, f3rel, nulrel, r, &s);
+    u8 *dst = col + hdr_len + line_off[r];
+    const Span sp = dup_field(buf + s, n, 1, dst);
+    dst[sp.len] = '\n';
+}
+
+// Artist pass over artist.csv records: strip EOL, duplicate_field(line, 0),
+// count non-empty names (parallel_spotify.c:986-994).  Key bytes go to the
+// arena at the record's own offset.
+__global__ void k_artist_key(const u8 *__restrict__ col, const u64 *__restrict__ ar_start,
+                             const u64 *__restrict__ ar_term, u64 nrec, u8 *__restrict__ arena,
+                             u64 *__restrict__ key_off, u32 *__restrict__ key_len, u64 *__restrict__ key_slot,
+                             u64 *atab, u64 amask, u32 *alist, u64 alist_cap, Counters *ctr) {
+    const u64 j = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= nrec) return;
+    const u64 s = ar_start[j];
+    u64 n = ar_term[j] - s;
+    const u8 *p = col + s;
+    while (n > 0 && (p[n - 1] == '\n' || p[n - 1] == '\r')) --n;
+    const Span sp = dup_field(p, n, 0, arena + s);
+    key_off[j] = s + sp.off;
+    key_len[j] = (u32)sp.len;
+    if (sp.len == 0) {
+        key_slot[j] = ~0ull;
+        return;
+    }
+    const u64 h = bytes_hash(arena + s + sp.off, sp.len, 0);
+    key_slot[j] = h_insert(atab, amask, h, 1, j, alist, alist_cap, &ctr->a_claimed, ctr, OVF_A);
+}
+
+__global__ void k_artist_verify(const u8 *__restrict__ arena, const u64 *__restrict__ key_off,
+                                const u32 *__restrict__ key_len, const u64 *__restrict__ key_slot, u64 nrec,
+                                const u64 *__restrict__ atab, Counters *ctr) {
+    const u64 j = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= nrec || key_len[j] == 0 || key_slot[j] == ~0ull) return;
+    const u64 rep = atab[4 * key_slot[j] + 2];
+    if (rep == j) return;
+    const u32 n = key_len[j];
+    bool same = key_len[rep] == n;
+    const u8 *a = arena + key_off[j], *b = arena + key_off[rep];
+    for (u32 i = 0; same && i < n; ++i) same = a[i] == b[i];
+    if (!same) atomicAdd((unsigned long long *)&ctr->collision, 1ull);
+}
+
+// ---------------------------------------------------------------------------
+// words > 16 bytes
+__global__ void k_long_insert(const u8 *__restrict__ buf, u64 seg_end, const u64 *__restrict__ l_pos, u64 n,
+                              u32 *__restrict__ l_len, u64 *__restrict__ l_slot, u64 *ltab, u64 lmask, u32 *llist,
+                              u64 llist_cap, Counters *ctr) {
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const u64 p = l_pos[i];
+    u64 len = 0;
+    while (p + len < seg_end && c_tok(buf[p + len])) ++len;
+    l_len[i] = (u32)len;
+    const u64 h = bytes_hash(buf + p, len, 1);
+    l_slot[i] = h_insert(ltab, lmask, h, 1, i, llist, llist_cap, &ctr->l_claimed, ctr, OVF_LT);
+}
+
+__device__ __forceinline__ u32 lower1(u32 c) { return (c >= 'A' && c <= 'Z') ? c + 32 : c; }
+
+__global__ void k_long_verify(const u8 *__restrict__ buf, const u64 *__restrict__ l_pos,
+                              const u32 *__restrict__ l_len, const u64 *__restrict__ l_slot, u64 n,
+                              const u64 *__restrict__ ltab, Counters *ctr) {
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || l_slot[i] == ~0ull) return;
+    const u64 rep = ltab[4 * l_slot[i] + 2];
+    if (rep == i) return;
+    const u32 len = l_len[i];
+    bool same = l_len[rep] == len;
+    const u8 *a = buf + l_pos[i], *b = buf + l_pos[rep];
+    for (u32 k = 0; same && k < len; ++k) same = lower1(a[k]) == lower1(b[k]);
+    if (!same) atomicAdd((unsigned long long *)&ctr->collision, 1ull);
+}
+
+// ---------------------------------------------------------------------------
+// Ranking entries.  Sort key = (K2 = ~count, K1 = key bytes 0..7 big-endian,
+// K0 = key bytes 8..15 big-endian); ascending == entry_compare_desc for all
+// keys that differ within their first 16 bytes (zero padding sorts first,
+// exactly like strcmp's terminator).  ref = (kind << 60) | index.
+enum { KIND_S = 0, KIND_M = 1, KIND_L = 2, KIND_A = 3 };
+
+__device__ __forceinline__ void be16(const u8 *p, u64 n, int lower, u64 *hi, u64 *lo) {
+    u64 h = 0, l = 0;
+    for (u64 i = 0; i < 16; ++i) {
+        u32 c = i < n ? p[i] : 0;
+        if (lower) c = lower1(c);
+        if (i < 8) h = (h << 8) | c;
+        else l = (l << 8) | c;
+    }
+    *hi = h;
+    *lo = l;
+}
+
+__global__ void k_word_entries(EntryArgs a) {
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    const u64 n = a.ns + a.nm + a.nl;
+    if (i >= n) return;
+    u64 c, hi, lo, ref;
+    if (i < a.ns) {
+        const u64 slot = a.s_list[i];
+        const u64 key = a.s_tab[2 * slot];
+        c = a.s_tab[2 * slot + 1];
+        hi = __builtin_bswap64(key);
+        lo = 0;
+        ref = ((u64)KIND_S << 60) | slot;
+    } else if (i < a.ns + a.nm) {
+        const u64 slot = a.m_list[i - a.ns];
+        hi = __builtin_bswap64(a.m_tab[4 * slot]);
+        lo = __builtin_bswap64(a.m_tab[4 * slot + 1]);
+        c = a.m_tab[4 * slot + 2];
+        ref = ((u64)KIND_M << 60) | slot;
+    } else {
+        const u64 slot = a.l_list[i - a.ns - a.nm];
+        c = a.l_tab[4 * slot + 1];
+        const u64 rep = a.l_tab[4 * slot + 2];
+        be16(a.buf + a.l_pos[rep], a.l_len[rep], 1, &hi, &lo);
+        ref = ((u64)KIND_L << 60) | rep;
+    }
+    a.K2[i] = ~c;
+    a.K1[i] = hi;
+    a.K0[i] = lo;
+    a.val[i] = (u32)i;
+    a.ref[i] = ref;
+    a.cnt[i] = c;
+}
+
+__global__ void k_artist_entries(const u64 *__restrict__ atab, const u32 *__restrict__ alist, u64 n,
+                                 const u8 *__restrict__ arena, const u64 *__restrict__ key_off,
+                                 const u32 *__restrict__ key_len, u64 *K2, u64 *K1, u64 *K0, u32 *val, u64 *ref,
+                                 u64 *cnt) {
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const u64 slot = alist[i];
+    const u64 c = atab[4 * slot + 1];
+    const u64 rep = atab[4 * slot + 2];
+    u64 hi, lo;
+    be16(arena + key_off[rep], key_len[rep], 0, &hi, &lo);
+    K2[i] = ~c;
+    K1[i] = hi;
+    K0[i] = lo;
+    val[i] = (u32)i;
+    ref[i] = ((u64)KIND_A << 60) | rep;
+    cnt[i] = c;
+}
+
+// ---------------------------------------------------------------------------
+// Stable LSD radix sort, 8-bit digits, on (K2, K1, K0) with u32 values.
+#define RS_T 256
+#define RS_ITEMS 8
+#define RS_TILE (RS_T * RS_ITEMS)
+
+__device__ __forceinline__ u32 digit_of(const u64 *K2, const u64 *K1, const u64 *K0, u64 i, u32 d) {
+    const u64 *k = d < 8 ? K0 : (d < 16 ? K1 : K2);
+    return (u32)(k[i] >> (8 * (d & 7))) & 0xFFu;
+}
+
+__global__ __launch_bounds__(RS_T) void k_radix_hist_all(const u64 *__restrict__ K2, const u64 *__restrict__ K1,
+                                                         const u64 *__restrict__ K0, u64 n, u32 *__restrict__ ghist) {
+    __shared__ u32 h[24 * 256];
+    for (u32 i = threadIdx.x; i < 24 * 256; i += RS_T) h[i] = 0;
+    __syncthreads();
+    for (u64 i = (u64)blockIdx.x * RS_T + threadIdx.x; i < n; i += (u64)gridDim.x * RS_T) {
+        const u64 k[3] = {K0[i], K1[i], K2[i]};
+        for (u32 d = 0; d < 24; ++d) atomicAdd(&h[d * 256 + ((k[d >> 3] >> (8 * (d & 7))) & 0xFF)], 1u);
+    }
+    __syncthreads();
+    for (u32 i = threadIdx.x; i < 24 * 256; i += RS_T)
+        if (h[i]) atomicAdd(&ghist[i], h[i]);
+}
+
+__global__ __launch_bounds__(RS_T) void k_radix_count(const u64 *__restrict__ K2, const u64 *__restrict__ K1,
+                                                      const u64 *__restrict__ K0, u64 n, u32 d, u64 nb,
+                                                      u64 *__restrict__ bhist) {
+    __shared__ u32 h[256];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const u64 base = (u64)blockIdx.x * RS_TILE;
+    for (int r = 0; r < RS_ITEMS; ++r) {
+        const u64 i = base + (u64)r * RS_T + threadIdx.x;
+        if (i < n) atomicAdd(&h[digit_of(K2, K1, K0, i, d)], 1u);
+    }
+    __syncthreads();
+    bhist[(u64)threadIdx.x * nb + blockIdx.x] = h[threadIdx.x];
+}
+
+__global__ __launch_bounds__(RS_T) void k_radix_scatter(const u64 *__restrict__ K2, const u64 *__restrict__ K1,
+                                                        const u64 *__restrict__ K0, const u32 *__restrict__ V, u64 n,
+                                                        u32 d, u64 nb, const u64 *__restrict__ boff,
+                                                        u64 *__restrict__ O2, u64 *__restrict__ O1,
+                                                        u64 *__restrict__ O0, u32 *__restrict__ OV) {
+    __shared__ u64 run[256];
+    __shared__ u32 wc[RS_T / 64][256];
+    const u32 lane = lane_id(), w = threadIdx.x >> 6;
+    run[threadIdx.x] = boff[(u64)threadIdx.x * nb + blockIdx.x];
+    const u64 base = (u64)blockIdx.x * RS_TILE;
+    for (int r = 0; r < RS_ITEMS; ++r) {
+        for (u32 ww = 0; ww < RS_T / 64; ++ww) wc[ww][threadIdx.x] = 0;
+        __syncthreads();
+        const u64 i = base + (u64)r * RS_T + threadIdx.x;
+        const bool ok = i < n;
+        u32 dg = ok ? digit_of(K2, K1, K0, i, d) : 0;
+        u32 rank = 0;
+        if (ok) {
+            u64 m = __ballot(1);
+            for (int b = 0; b < 8; ++b) {
+                const u64 bb = __ballot((dg >> b) & 1u);
+                m &= ((dg >> b) & 1u) ? bb : ~bb;
+            }
+            rank = mbcnt(m);
+            if (rank == 0) wc[w][dg] = (u32)__popcll(m);
+        }
+        __syncthreads();
+        if (ok) {
+            u64 pos = run[dg] + rank;
+            for (u32 ww = 0; ww < w; ++ww) pos += wc[ww][dg];
+            O2[pos] = K2[i];
+            O1[pos] = K1[i];
+            O0[pos] = K0[i];
+            OV[pos] = V[i];
+        }
+        __syncthreads();
+        u32 tot = 0;
+        for (u32 ww = 0; ww < RS_T / 64; ++ww) tot += wc[ww][threadIdx.x];
+        run[threadIdx.x] += tot;
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Exact tie fix-up: runs of equal (K2, K1, K0) (keys sharing 16 leading bytes
+// and a count) are re-ordered by full strcmp.  Run sizes are tiny.
+__device__ __forceinline__ void key_bytes(u64 ref, u64 k1, u64 k0, const u8 *buf, const u64 *l_pos,
+                                          const u32 *l_len, const u8 *arena, const u64 *key_off,
+                                          const u32 *key_len, const u8 **p, u64 *n, int *lower) {
+    const u32 kind = (u32)(ref >> 60);
+    const u64 idx = ref & ((1ull << 60) - 1);
+    *lower = 0;
+    if (kind == KIND_L) { *p = buf + l_pos[idx]; *n = l_len[idx]; *lower = 1; }
+    else if (kind == KIND_A) { *p = arena + key_off[idx]; *n = key_len[idx]; }
+    else { *p = nullptr; *n = 0; }
+}
+
+__device__ int full_cmp(u64 refa, u64 refb, u64 k1, u64 k0, const u8 *buf, const u64 *l_pos, const u32 *l_len,
+                        const u8 *arena, const u64 *key_off, const u32 *key_len) {
+    const u8 *pa, *pb;
+    u64 na, nb;
+    int la, lb;
+    key_bytes(refa, k1, k0, buf, l_pos, l_len, arena, key_off, key_len, &pa, &na, &la);
+    key_bytes(refb, k1, k0, buf, l_pos, l_len, arena, key_off, key_len, &pb, &nb, &lb);
+    // S/M keys are fully described by (k1, k0): 16 bytes, zero padded
+    u8 tmp[16];
+    for (int i = 0; i < 8; ++i) { tmp[i] = (u8)(k1 >> (56 - 8 * i)); tmp[8 + i] = (u8)(k0 >> (56 - 8 * i)); }
+    if (!pa) { pa = tmp; na = 0; while (na < 16 && tmp[na]) ++na; la = 0; }
+    if (!pb) { pb = tmp; nb = 0; while (nb < 16 && tmp[nb]) ++nb; lb = 0; }
+    const u64 m = na < nb ? na : nb;
+    for (u64 i = 0; i < m; ++i) {
+        u32 x = pa[i], y = pb[i];
+        if (la) x = lower1(x);
+        if (lb) y = lower1(y);
+        if (x != y) return x < y ? -1 : 1;
+    }
+    return na < nb ? -1 : (na > nb ? 1 : 0);
+}
+
+__global__ void k_tie_fixup(const u64 *__restrict__ K2, const u64 *__restrict__ K1, const u64 *__restrict__ K0,
+                            const u32 *__restrict__ V, u64 n, const u64 *__restrict__ ref, const u8 *buf,
+                            const u64 *l_pos, const u32 *l_len, const u8 *arena, const u64 *key_off,
+                            const u32 *key_len, u32 *__restrict__ out) {
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const u64 a2 = K2[i], a1 = K1[i], a0 = K0[i];
+    const bool eq_prev = i > 0 && K2[i - 1] == a2 && K1[i - 1] == a1 && K0[i - 1] == a0;
+    const bool eq_next = i + 1 < n && K2[i + 1] == a2 && K1[i + 1] == a1 && K0[i + 1] == a0;
+    if (!eq_prev && !eq_next) { out[i] = V[i]; return; }
+    u64 s = i, e = i + 1;
+    while (s > 0 && K2[s - 1] == a2 && K1[s - 1] == a1 && K0[s - 1] == a0) --s;
+    while (e < n && K2[e] == a2 && K1[e] == a1 && K0[e] == a0) ++e;
+    const u64 me = ref[V[i]];
+    u64 rank = 0;
+    for (u64 j = s; j < e; ++j) {
+        if (j == i) continue;
+        const int c = full_cmp(ref[V[j]], me, a1, a0, buf, l_pos, l_len, arena, key_off, key_len);
+        if (c < 0 || (c == 0 && j < i)) ++rank;
+    }
+    out[s + rank] = V[i];
+}
+
+// ---------------------------------------------------------------------------
+// Ranked key blob: lengths, then bytes (in rank order).
+__device__ __forceinline__ u64 entry_key_len(u64 ref, u64 k1, u64 k0, const u32 *l_len, const u32 *key_len) {
+    const u32 kind = (u32)(ref >> 60);
+    const u64 idx = ref & ((1ull << 60) - 1);
+    if (kind == KIND_L) return l_len[idx];
+    if (kind == KIND_A) return key_len[idx];
+    u64 n = 0;
+    for (int i = 0; i < 16; ++i) {
+        const u8 b = (u8)((i < 8 ? k1 : k0) >> (56 - 8 * (i & 7)));
+        if (!b) break;
+        ++n;
+    }
+    return n;
+}
+
+__global__ void k_blob_len(const u32 *__restrict__ order, u64 n, const u64 *__restrict__ ref,
+                           const u64 *__restrict__ K1u, const u64 *__restrict__ K0u, const u32 *l_len,
+                           const u32 *key_len, u64 *__restrict__ len) {
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const u32 e = order[i];
+    len[i] = entry_key_len(ref[e], K1u[e], K0u[e], l_len, key_len);
+}
+
+__global__ void k_blob_write(const u32 *__restrict__ order, u64 n, const u64 *__restrict__ ref,
+                             const u64 *__restrict__ K1u, const u64 *__restrict__ K0u, const u64 *__restrict__ cnt,
+                             const u8 *buf, const u64 *l_pos, const u32 *l_len, const u8 *arena,
+                             const u64 *key_off, const u32 *key_len, const u64 *__restrict__ off,
+                             u8 *__restrict__ blob, u64 *__restrict__ counts_out) {
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const u32 e = order[i];
+    const u64 r = ref[e];
+    const u32 kind = (u32)(r >> 60);
+    const u64 idx = r & ((1ull << 60) - 1);
+    u8 *dst = blob + off[i];
+    counts_out[i] = cnt[e];
+    if (kind == KIND_L) {
+        const u8 *p = buf + l_pos[idx];
+        for (u32 k = 0; k < l_len[idx]; ++k) dst[k] = (u8)lower1(p[k]);
+    } else if (kind == KIND_A) {
+        const u8 *p = arena + key_off[idx];
+        for (u32 k = 0; k < key_len[idx]; ++k) dst[k] = p[k];
+    } else {
+        for (int k = 0; k < 16; ++k) {
+            const u8 b = (u8)((k < 8 ? K1u[e] : K0u[e]) >> (56 - 8 * (k & 7)));
+            if (!b) break;
+            dst[k] = b;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// host launchers
+static inline dim3 grid1(u64 n, u32 t = 256) { return dim3((u32)((n + t - 1) / t)); }
+
+hipError_t msa_launch_artist_len(const u8 *buf, const u64 *rs, const u32 *f0, const u32 *f3, u64 nrec, u64 *len,
+                                 hipStream_t s) {
+    if (nrec) hipLaunchKernelGGL(k_artist_len, grid1(nrec), dim3(256), 0, s, buf, rs, f0, f3, nrec, len);
+    return hipGetLastError();
+}
+hipError_t msa_launch_artist_write(const u8 *buf, const u64 *rs, const u32 *f0, const u32 *f3, u64 nrec,
+                                   const u64 *off, u64 hdr, u8 *col, hipStream_t s) {
+    if (nrec) hipLaunchKernelGGL(k_artist_write, grid1(nrec), dim3(256), 0, s, buf, rs, f0, f3, nrec, off, hdr, col);
+    return hipGetLastError();
+}
+hipError_t msa_launch_text_len(const u8 *buf, const u64 *rs, const u64 *rt, const u32 *f3, const u32 *nul, u64 nrec,
+                               u64 *len, hipStream_t s) {
+    if (nrec) hipLaunchKernelGGL(k_text_len, grid1(nrec), dim3(256), 0, s, buf, rs, rt, f3, nul, nrec, len);
+    return hipGetLastError();
+}
+hipError_t msa_launch_text_write(const u8 *buf, const u64 *rs, const u64 *rt, const u32 *f3, const u32 *nul,
+                                 u64 nrec, const u64 *off, u64 hdr, u8 *col, hipStream_t s) {
+    if (nrec)
+        hipLaunchKernelGGL(k_text_write, grid1(nrec), dim3(256), 0, s, buf, rs, rt, f3, nul, nrec, off, hdr, col);
+    return hipGetLastError();
+}
+hipError_t msa_launch_artist_key(const u8 *col, const u64 *ar_start, const u64 *ar_term, u64 nrec, u8 *arena,
+                                 u64 *key_off, u32 *key_len, u64 *key_slot, u64 *atab, u64 amask, u32 *alist,
+                                 u64 alist_cap, Counters *ctr, hipStream_t s) {
+    if (nrec) {
+        hipLaunchKernelGGL(k_artist_key, grid1(nrec), dim3(256), 0, s, col, ar_start, ar_term, nrec, arena, key_off,
+                           key_len, key_slot, atab, amask, alist, alist_cap, ctr);
+        hipLaunchKernelGGL(k_artist_verify, grid1(nrec), dim3(256), 0, s, (const u8 *)arena, key_off, key_len,
+                           key_slot, nrec, (const u64 *)atab, ctr);
+    }
+    return hipGetLastError();
+}
+hipError_t msa_launch_long(const u8 *buf, u64 seg_end, const u64 *l_pos, u64 n, u32 *l_len, u64 *l_slot, u64 *ltab,
+                           u64 lmask, u32 *llist, u64 llist_cap, Counters *ctr, hipStream_t s) {
+    if (n) {
+        hipLaunchKernelGGL(k_long_insert, grid1(n), dim3(256), 0, s, buf, seg_end, l_pos, n, l_len, l_slot, ltab, lmask,
+                           llist, llist_cap, ctr);
+        hipLaunchKernelGGL(k_long_verify, grid1(n), dim3(256), 0, s, buf, l_pos, (const u32 *)l_len,
+                           (const u64 *)l_slot, n, (const u64 *)ltab, ctr);
+    }
+    return hipGetLastError();
+}
+hipError_t msa_launch_word_entries(const EntryArgs &a, hipStream_t s) {
+    const u64 n = a.ns + a.nm + a.nl;
+    if (n) hipLaunchKernelGGL(k_word_entries, grid1(n), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+hipError_t msa_launch_artist_entries(const u64 *atab, const u32 *alist, u64 n, const u8 *arena, const u64 *key_off,
+                                     const u32 *key_len, u64 *K2, u64 *K1, u64 *K0, u32 *val, u64 *ref, u64 *cnt,
+                                     hipStream_t s) {
+    if (n)
+        hipLaunchKernelGGL(k_artist_entries, grid1(n), dim3(256), 0, s, atab, alist, n, arena, key_off, key_len, K2,
+                           K1, K0, val, ref, cnt);
+    return hipGetLastError();
+}
+hipError_t msa_launch_radix_hist_all(const u64 *K2, const u64 *K1, const u64 *K0, u64 n, u32 *ghist, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(ghist, 0, 24 * 256 * sizeof(u32), s);
+    if (e != hipSuccess) return e;
+    if (n) {
+        u64 blocks = (n + RS_T - 1) / RS_T;
+        if (blocks > 1024) blocks = 1024;
+        hipLaunchKernelGGL(k_radix_hist_all, dim3((u32)blocks), dim3(RS_T), 0, s, K2, K1, K0, n, ghist);
+    }
+    return hipGetLastError();
+}
+u64 msa_radix_blocks(u64 n) { return (n + RS_TILE - 1) / RS_TILE; }
+hipError_t msa_launch_radix_pass(const u64 *K2, const u64 *K1, const u64 *K0, const u32 *V, u64 n, u32 d, u64 *bhist,
+                                 u64 *boff, u64 *bsum, u64 *O2, u64 *O1, u64 *O0, u32 *OV, hipStream_t s) {
+    const u64 nb = msa_radix_blocks(n);
+    hipLaunchKernelGGL(k_radix_count, dim3((u32)nb), dim3(RS_T), 0, s, K2, K1, K0, n, d, nb, bhist);
+    hipError_t e = msa_exclusive_scan(bhist, nb * 256, boff, bsum, nullptr, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_radix_scatter, dim3((u32)nb), dim3(RS_T), 0, s, K2, K1, K0, V, n, d, nb,
+                       (const u64 *)boff, O2, O1, O0, OV);
+    return hipGetLastError();
+}
+hipError_t msa_launch_fixup(const u64 *K2, const u64 *K1, const u64 *K0, const u32 *V, u64 n, const u64 *ref,
+                            const u8 *buf, const u64 *l_pos, const u32 *l_len, const u8 *arena, const u64 *key_off,
+                            const u32 *key_len, u32 *out, hipStream_t s) {
+    if (n)
+        hipLaunchKernelGGL(k_tie_fixup, grid1(n), dim3(256), 0, s, K2, K1, K0, V, n, ref, buf, l_pos, l_len, arena,
+                           key_off, key_len, out);
+    return hipGetLastError();
+}
+hipError_t msa_launch_blob(const u32 *order, u64 n, const u64 *ref, const u64 *K1u, const u64 *K0u, const u64 *cnt,
+                           const u8 *buf, const u64 *l_pos, const u32 *l_len, const u8 *arena, const u64 *key_off,
+                           const u32 *key_len, u64 *len, u64 *off, u64 *bsum, u64 *total, u8 *blob, u64 *counts_out,
+                           hipStream_t s, int phase) {
+    if (!n) return hipSuccess;
+    if (phase == 0) {
+        hipLaunchKernelGGL(k_blob_len, grid1(n), dim3(256), 0, s, order, n, ref, K1u, K0u, l_len, key_len, len);
+        return msa_exclusive_scan(len, n, off, bsum, total, s);
+    }
+    hipLaunchKernelGGL(k_blob_write, grid1(n), dim3(256), 0, s, order, n, ref, K1u, K0u, cnt, buf, l_pos, l_len, arena,
+                       key_off, key_len, (const u64 *)off, blob, counts_out);
+    return hipGetLastError();
+}

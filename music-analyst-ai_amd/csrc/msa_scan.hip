@@ -1,0 +1,450 @@
+// msa_scan.hip -- record/field scan and lyric tokenizer over a CSV in HBM.
+//
+// Replaces the byte-serial reader of the reference (read_csv_record,
+// parallel_spotify.c:549-633; parse_csv_line 258-304; process_lyrics 350-394)
+// with a three-kernel data-parallel scan:
+//
+//   K1 k_chunk_summary  one wave per 16 KiB chunk: the chunk's transfer
+//                       function over the reader state, for BOTH possible
+//                       incoming quote parities (wave-ballot prefix-xor)
+//   K2 k_fn_compose /   compose the chunk functions (tiny), then apply the
+//      k_fn_apply       initial state -> exact reader state at every chunk
+//   K3 k_scan_main      one wave per chunk again, now knowing its state:
+//                       record terminators, the first three unquoted commas
+//                       of every record, NUL truncation, and -- for the
+//                       lyric field -- token starts, lengths, lower-cased
+//                       keys, counted in an LDS-private table (Zipf head)
+//                       with device-scope atomics only on overflow.
+//
+// Every wave moves 1 KiB per iteration as one coalesced dwordx4 per lane; all
+// cross-lane work is ballot/mbcnt based (64-wide wavefronts).
+#include "msa_internal.h"
+#include "msa_tables.h"
+
+namespace {
+
+__device__ __forceinline__ uint4 ld16(const u8 *p) { return *reinterpret_cast<const uint4 *>(p); }
+
+__device__ __forceinline__ u32 valid_mask(u64 lpos, u64 end) {
+    if (lpos >= end) return 0;
+    u64 r = end - lpos;
+    return r >= 16 ? 0xFFFFu : ((1u << r) - 1u);
+}
+
+__device__ __forceinline__ u32 range_mask(u32 from, u32 to) {  // bits [from, to)
+    return ((0xFFFFu << from) & (0xFFFFu >> (16 - to))) & 0xFFFFu;
+}
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// K1: per-chunk transfer function, both parity hypotheses.
+__global__ __launch_bounds__(256) void k_chunk_summary(const u8 *__restrict__ buf, u64 seg_begin,
+                                                       u64 seg_end, u32 nchunks,
+                                                       ChunkSum *__restrict__ out) {
+    const u32 lane = lane_id();
+    const u32 gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const u32 nw = (gridDim.x * blockDim.x) >> 6;
+    const u64 lt = (1ull << lane) - 1ull;
+    for (u32 c = gw; c < nchunks; c += nw) {
+        const u64 cbase = seg_begin + (u64)c * MSA_CHUNK;
+        const u64 cend = min(cbase + (u64)MSA_CHUNK, seg_end);
+        u32 par = 0, first_nl = 0;
+        u32 cr[2] = {0, 0}, nterm[2] = {0, 0}, cc[2] = {0, 0}, zz[2] = {0, 0}, lend[2] = {0, 0};
+        for (u64 ibase = cbase; ibase < cend; ibase += MSA_ITER) {
+            const u64 lpos = ibase + lane * 16;
+            const uint4 v = ld16(buf + lpos);
+            const u32 vmask = valid_mask(lpos, cend);
+            const Classes k = classify16(v, vmask);
+            if (ibase == cbase) first_nl = readlane(k.NL, 0) & 1u;
+            const u64 B = __ballot(__popc(k.Q) & 1u);
+            const u32 pin0 = par ^ (mbcnt(B) & 1u);
+            const u32 inq0 = pxor_excl16(k.Q) ^ (pin0 ? 0xFFFFu : 0u);
+            par ^= (u32)__popcll(B) & 1u;
+            // raw '\n' at the following byte (for the '\r\n' swallow)
+            const u64 nb_pos = ibase + MSA_ITER;
+            const u32 nb_nl = (nb_pos < seg_end && buf[nb_pos] == '\n') ? 1u : 0u;
+            const u32 dn = __shfl_down(k.NL, 1);
+            const u32 nlnext = (k.NL >> 1) | (((lane == 63) ? nb_nl : (dn & 1u)) << 15);
+            const u32 lastb = (u32)(min(ibase + (u64)MSA_ITER, cend) - 1 - ibase);
+            const int Lz = (int)(lastb >> 4);
+            const u32 bz = lastb & 15u;
+            const u32 anyZ = k.Z != 0;
+            const u64 Bz = __ballot(anyZ);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const u32 inq = h ? (~inq0 & 0xFFFFu) : inq0;
+                const u32 CRu = k.CR & ~inq, NLu = k.NL & ~inq, Cu = k.C & ~inq;
+                const u32 up = __shfl_up(CRu, 1);
+                const u32 pc0 = lane ? ((up >> 15) & 1u) : cr[h];
+                const u32 TERM = (CRu | (NLu & ~((CRu << 1) | pc0))) & 0xFFFFu;
+                const u32 SW = CRu & nlnext;
+                const u32 nt = __popc(TERM);
+                const u32 lastT = nt ? 31u - __clz(TERM) : 0u;
+                const u32 above = nt ? ((0xFFFFu << (lastT + 1)) & 0xFFFFu) : 0xFFFFu;
+                const u32 cC = __popc(Cu);
+                const u32 tailC = __popc(Cu & above);
+                const u32 tailZ = (k.Z & above) != 0;
+                u32 totC, totT;
+                const u32 PC = wave_prefix<5>(cC, totC);
+                wave_prefix<5>(nt, totT);
+                const u64 Bh = __ballot(nt != 0);
+                if (Bh) {
+                    const int jl = 63 - __clzll(Bh);
+                    const u32 after = totC - (readlane(PC, jl) + readlane(cC, jl));
+                    const u32 c_new = readlane(tailC, jl) + after;
+                    cc[h] = c_new > 3 ? 3 : c_new;
+                    const u64 above_lanes = (jl == 63) ? 0ull : (~0ull << (jl + 1));
+                    zz[h] = readlane(tailZ, jl) | ((Bz & above_lanes) != 0);
+                    const u32 lt_j = readlane(lastT, jl);
+                    const u32 sw_j = (readlane(SW, jl) >> lt_j) & 1u;
+                    lend[h] = (u32)(ibase - cbase) + (u32)jl * 16u + lt_j + 1u + sw_j;
+                } else {
+                    const u32 c_new = cc[h] + totC;
+                    cc[h] = c_new > 3 ? 3 : c_new;
+                    zz[h] |= (Bz != 0);
+                }
+                nterm[h] += totT;
+                cr[h] = (readlane(CRu, Lz) >> bz) & 1u;
+            }
+        }
+        if (lane == 0) {
+            ChunkSum s;
+            for (int h = 0; h < 2; ++h) {
+                s.h[h] = nterm[h] | (cc[h] << 16) | (zz[h] << 18) | (cr[h] << 19) | (par << 20) | (first_nl << 21);
+                s.last_end[h] = lend[h];
+            }
+            out[c] = s;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// K2a: compose chunk functions.  One block of 256 threads; thread t owns a
+// contiguous run of chunks.  Writes the run prefix functions and the total.
+#define FN_THREADS 256
+__global__ __launch_bounds__(FN_THREADS) void k_fn_compose(const ChunkSum *__restrict__ sums, u64 seg_begin,
+                                                           u32 nchunks, Fn *__restrict__ run_prefix,
+                                                           Fn *__restrict__ total) {
+    __shared__ Fn runs[FN_THREADS];
+    const u32 t = threadIdx.x;
+    const u32 per = (nchunks + FN_THREADS - 1) / FN_THREADS;
+    const u32 a = min(nchunks, t * per), b = min(nchunks, a + per);
+    Fn f = fn_identity(seg_begin + (u64)a * MSA_CHUNK);
+    for (u32 c = a; c < b; ++c) {
+        const ChunkSum s = sums[c];
+        const u64 base = seg_begin + (u64)c * MSA_CHUNK;
+        Fn g;
+        for (u32 i = 0; i < 3; ++i) g.e[i] = chunk_entry(s, base, i);
+        f = fn_compose(f, g);
+    }
+    runs[t] = f;
+    __syncthreads();
+    if (t == 0) {
+        Fn acc = fn_identity(seg_begin);
+        for (u32 i = 0; i < FN_THREADS; ++i) {
+            run_prefix[i] = acc;
+            acc = fn_compose(acc, runs[i]);
+        }
+        *total = acc;
+    }
+}
+
+// K2b: apply the initial state; write every chunk's incoming state.
+__global__ __launch_bounds__(FN_THREADS) void k_fn_apply(const ChunkSum *__restrict__ sums, u64 seg_begin,
+                                                         u32 nchunks, const Fn *__restrict__ run_prefix,
+                                                         const State *__restrict__ init,
+                                                         State *__restrict__ carry, State *__restrict__ final_state) {
+    const u32 t = threadIdx.x;
+    const u32 per = (nchunks + FN_THREADS - 1) / FN_THREADS;
+    const u32 a = min(nchunks, t * per), b = min(nchunks, a + per);
+    State s = fn_apply(*init, run_prefix[t]);
+    for (u32 c = a; c < b; ++c) {
+        carry[c] = s;
+        const ChunkSum cs = sums[c];
+        const u64 base = seg_begin + (u64)c * MSA_CHUNK;
+        Fn g;
+        for (u32 i = 0; i < 3; ++i) g.e[i] = chunk_entry(cs, base, i);
+        s = fn_apply(s, g);
+    }
+    if (t == FN_THREADS - 1) *final_state = s;
+}
+
+// ---------------------------------------------------------------------------
+// K3: the main pass.
+#define K3_THREADS 512
+#define K3_WAVES (K3_THREADS / 64)
+#define LSLOTS 4096
+#define LPROBE 8
+#define WAVE_LDS (2048 + 256 + 1024)
+#define K3_LDS (LSLOTS * 12 + K3_WAVES * WAVE_LDS)
+
+template <int MODE>  // 0 = CSV (fields + tokens), 1 = LINES (records only)
+__global__ __launch_bounds__(K3_THREADS) void k_scan_main(ScanArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    u64 *lkey = reinterpret_cast<u64 *>(smem);
+    u32 *lcnt = reinterpret_cast<u32 *>(smem + LSLOTS * 8);
+    const u32 lane = lane_id();
+    const u32 wib = threadIdx.x >> 6;
+    unsigned char *wl = smem + LSLOTS * 12 + wib * WAVE_LDS;
+    u64 *ring = reinterpret_cast<u64 *>(wl);             // 2 KiB: two 1 KiB iteration slots
+    u64 *bm = reinterpret_cast<u64 *>(wl + 2048);        // token-class bitmap of the ring
+    u16 *starts = reinterpret_cast<u16 *>(wl + 2048 + 256);
+    const u64 lt = (1ull << lane) - 1ull;
+
+    if (MODE == 0) {
+        for (u32 i = threadIdx.x; i < LSLOTS; i += K3_THREADS) { lkey[i] = 0; lcnt[i] = 0; }
+        __syncthreads();
+    }
+    const u32 gw = blockIdx.x * K3_WAVES + wib;
+    const u32 nw = gridDim.x * K3_WAVES;
+    u64 words = 0;
+
+    for (u32 c = gw; c < a.nchunks; c += nw) {
+        State st = a.carry[c];
+        const u64 cbase = a.seg_begin + (u64)c * MSA_CHUNK;
+        const u64 cend = min(cbase + (u64)MSA_CHUNK, a.seg_end);
+        u32 prevT = 0;
+        if (MODE == 0 && cbase > 0) {
+            const u32 b = a.buf[cbase - 1];
+            prevT = (u32)(((b | 0x20u) >= 'a' && (b | 0x20u) <= 'z') || (b >= '0' && b <= '9') || b == '\'');
+        }
+        uint4 cur = ld16(a.buf + cbase + lane * 16);
+        uint4 nxt = ld16(a.buf + cbase + MSA_ITER + lane * 16);
+        if (MODE == 0) {
+            reinterpret_cast<uint4 *>(ring)[lane] = cur;
+            reinterpret_cast<u16 *>(bm)[lane] = (u16)tok16(cur, valid_mask(cbase + lane * 16, a.seg_end));
+        }
+        u32 it = 0;
+        for (u64 ibase = cbase; ibase < cend; ibase += MSA_ITER, ++it) {
+            const u64 lpos = ibase + lane * 16;
+            const u64 npos = ibase + MSA_ITER;
+            uint4 nn = ld16(a.buf + npos + MSA_ITER + lane * 16);  // prefetch it+2
+            if (MODE == 0) {
+                // stage the following 1 KiB (token continuation only) in the other ring slot
+                const u32 slot = (it + 1) & 1u;
+                reinterpret_cast<uint4 *>(ring)[slot * 64 + lane] = nxt;
+                reinterpret_cast<u16 *>(bm)[slot * 64 + lane] = (u16)tok16(nxt, valid_mask(npos + lane * 16, a.seg_end));
+            }
+            const u32 vmask = valid_mask(lpos, cend);
+            const Classes k = classify16(cur, vmask);
+            const u64 B = __ballot(__popc(k.Q) & 1u);
+            const u32 pin = st.p ^ (mbcnt(B) & 1u);
+            const u32 inq = pxor_excl16(k.Q) ^ (pin ? 0xFFFFu : 0u);
+            const u32 CRu = k.CR & ~inq, NLu = k.NL & ~inq;
+            const u32 Cu = (MODE == 0) ? (k.C & ~inq) : 0u;
+            const u32 Zm = (MODE == 0) ? k.Z : 0u;
+            const u32 upCR = __shfl_up(CRu, 1);
+            const u32 pc0 = lane ? ((upCR >> 15) & 1u) : st.cr;
+            const u32 TERM = (CRu | (NLu & ~((CRu << 1) | pc0))) & 0xFFFFu;
+            const u32 nb_nl = (npos < a.seg_end) ? ((readlane(nxt.x, 0) & 0xFFu) == '\n') : 0u;
+            const u32 dn = __shfl_down(k.NL, 1);
+            const u32 nlnext = (k.NL >> 1) | (((lane == 63) ? nb_nl : (dn & 1u)) << 15);
+            const u32 SW = CRu & nlnext;
+            // segmented (per-record) state at this lane's first byte
+            const u32 nt = __popc(TERM);
+            const u32 lastT = nt ? 31u - __clz(TERM) : 0u;
+            const u32 above = nt ? ((0xFFFFu << (lastT + 1)) & 0xFFFFu) : 0xFFFFu;
+            const u32 cC = __popc(Cu);
+            const u32 tailC = __popc(Cu & above);
+            const u32 tailZ = (Zm & above) != 0;
+            const u64 endpos = lpos + lastT + 1 + ((SW >> lastT) & 1u);
+            u32 totC, totT;
+            const u32 PC = wave_prefix<5>(cC, totC);
+            const u32 PT = wave_prefix<5>(nt, totT);
+            const u64 Bh = __ballot(nt != 0);
+            const u64 Bz = __ballot(Zm != 0);
+            const u64 J = Bh & lt;
+            const int j = J ? (63 - __clzll(J)) : (int)lane;
+            const u32 pk = tailC | (tailZ << 5) | ((PC + cC) << 6);
+            const u32 gpk = __shfl(pk, j);
+            const u64 gend = __shfl(endpos, j);
+            u32 cin, zin;
+            u64 rs;
+            if (J) {
+                cin = (gpk & 31u) + (PC - (gpk >> 6));
+                const u64 between = lt & ~((2ull << j) - 1ull);
+                zin = ((gpk >> 5) & 1u) | ((Bz & between) != 0);
+                rs = gend;
+            } else {
+                cin = st.c + PC;
+                zin = st.z | ((Bz & lt) != 0);
+                rs = st.rs;
+            }
+            u32 cs = cin > 3 ? 3 : cin, zs = zin;
+            u64 rr = st.rec + PT;
+            // walk this lane's events (terminators, unquoted commas, NULs)
+            u32 E = TERM | Cu | Zm;
+            u32 live = 0, from = 0;
+            while (E) {
+                const u32 b = __ffs(E) - 1;
+                E &= E - 1;
+                if (MODE == 0 && rr >= 1 && cs >= 3 && !zs) live |= range_mask(from, b);
+                const u64 bpos = lpos + b;
+                if ((TERM >> b) & 1u) {
+                    if ((a.want_term || rr == 0) && rr < a.rec_cap) a.rec_term[rr] = bpos;
+                    const u64 ns = bpos + 1 + ((SW >> b) & 1u);
+                    ++rr;
+                    if (rr < a.rec_cap) a.rec_start[rr] = ns;
+                    cs = 0;
+                    zs = 0;
+                    rs = ns;
+                } else if ((Zm >> b) & 1u) {
+                    if (!zs) {
+                        zs = 1;
+                        if (a.want_term && rr < a.rec_cap) a.nulrel[rr] = (u32)(bpos - rs) + 1u;
+                    }
+                } else if (cs < 3) {
+                    ++cs;
+                    if (rr < a.rec_cap) {
+                        if (cs == 1) a.f0rel[rr] = (u32)(bpos - rs) + 1u;
+                        if (cs == 3 && !zs) a.f3rel[rr] = (u32)(bpos + 1 - rs) + 1u;
+                    }
+                }
+                from = b + 1;
+            }
+            if (MODE == 0 && rr >= 1 && cs >= 3 && !zs) live |= range_mask(from, 16);
+
+            // carry to the next iteration (lane 63 has seen every byte)
+            const u32 lastb = (u32)(min(ibase + (u64)MSA_ITER, cend) - 1 - ibase);
+            const int Lz = (int)(lastb >> 4);
+            const u32 bz = lastb & 15u;
+            st.p ^= (u32)__popcll(B) & 1u;
+            st.cr = (readlane(CRu, Lz) >> bz) & 1u;
+            st.c = readlane(cs, 63);
+            st.z = readlane(zs, 63);
+            st.rec = readlane64(rr, 63);
+            st.rs = readlane64(rs, 63);
+
+            if (MODE == 0) {
+                // ---- tokens of the lyric field
+                const u32 upT = __shfl_up(k.T, 1);
+                const u32 pt0 = lane ? ((upT >> 15) & 1u) : prevT;
+                const u32 S = (k.T & live) & ~((k.T << 1) | pt0) & 0xFFFFu;
+                prevT = (readlane(k.T, Lz) >> bz) & 1u;
+                u32 ntok;
+                u32 idx = wave_prefix<4>(__popc(S), ntok);
+                for (u32 s = S; s; s &= s - 1) starts[idx++] = (u16)(lane * 16 + (__ffs(s) - 1));
+                wave_sync();
+                const u32 slot_off = (it & 1u) << 10;
+                for (u32 t = lane; t < ntok; t += 64) {
+                    const u32 o = slot_off + starts[t];
+                    const u32 wi = o >> 6, bi = o & 63u;
+                    const u64 w = bm[wi] >> bi;
+                    u32 len = (u32)__ffsll((long long)~w) - 1u;
+                    if (len >= 64u - bi) {
+                        const u64 w2 = ~bm[(wi + 1) & 31u];
+                        len = (64u - bi) + (w2 ? (u32)__ffsll((long long)w2) - 1u : 64u);
+                    }
+                    if (len < 3) continue;
+                    ++words;
+                    if (len > 16) {
+                        const u64 i = atomicAdd((unsigned long long *)&a.ctr->l_occ, 1ull);
+                        if (i < a.l_cap) a.l_pos[i] = ibase + (o & 1023u);
+                        else atomicOr((unsigned long long *)&a.ctr->overflow, (unsigned long long)OVF_L);
+                        continue;
+                    }
+                    const u32 q = o >> 3, sh = (o & 7u) * 8u;
+                    const u64 w0 = ring[q], w1 = ring[(q + 1) & 255u];
+                    u64 k0 = sh ? ((w0 >> sh) | (w1 << (64 - sh))) : w0;
+                    if (len <= 8) {
+                        if (len < 8) k0 &= (1ull << (8 * len)) - 1ull;
+                        const u64 key = lower8(k0);
+                        u32 h = lds_hash(key) & (LSLOTS - 1);
+                        bool done = false;
+                        for (u32 p = 0; p < LPROBE; ++p) {
+                            u64 kc = lkey[h];
+                            if (kc == 0) {
+                                kc = atomicCAS((unsigned long long *)&lkey[h], 0ull, (unsigned long long)key);
+                                if (kc == 0) kc = key;
+                            }
+                            if (kc == key) {
+                                atomicAdd(&lcnt[h], 1u);
+                                done = true;
+                                break;
+                            }
+                            h = (h + 1) & (LSLOTS - 1);
+                        }
+                        if (!done) s_insert(a.s_tab, a.s_mask, key, 1, a.s_list, a.s_list_cap, a.ctr);
+                    } else {
+                        const u64 w2 = ring[(q + 2) & 255u];
+                        u64 k1 = sh ? ((w1 >> sh) | (w2 << (64 - sh))) : w1;
+                        if (len < 16) k1 &= (1ull << (8 * (len - 8))) - 1ull;
+                        m_insert(a.m_tab, a.m_mask, lower8(k0), lower8(k1), 1, a.m_list, a.m_list_cap, a.ctr);
+                    }
+                }
+                wave_sync();
+            }
+            cur = nxt;
+            nxt = nn;
+        }
+    }
+    if (MODE == 0) {
+        words = wave_sum64(words);
+        if (lane == 0 && words) atomicAdd((unsigned long long *)&a.ctr->total_words, (unsigned long long)words);
+        __syncthreads();
+        for (u32 i = threadIdx.x; i < LSLOTS; i += K3_THREADS) {
+            const u32 n = lcnt[i];
+            if (n) s_insert(a.s_tab, a.s_mask, lkey[i], n, a.s_list, a.s_list_cap, a.ctr);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// host launchers
+static int g_cus = 0;
+static int num_cus() {
+    if (!g_cus) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        hipDeviceProp_t p;
+        if (hipGetDeviceProperties(&p, dev) == hipSuccess) g_cus = p.multiProcessorCount;
+        if (g_cus <= 0) g_cus = 256;
+    }
+    return g_cus;
+}
+
+hipError_t msa_launch_summary(const u8 *buf, u64 seg_begin, u64 seg_end, u32 nchunks, ChunkSum *out,
+                              hipStream_t s) {
+    if (!nchunks) return hipSuccess;
+    u32 blocks = (nchunks + 3) / 4;
+    u32 cap = (u32)num_cus() * 8;
+    if (blocks > cap) blocks = cap;
+    hipLaunchKernelGGL(k_chunk_summary, dim3(blocks), dim3(256), 0, s, buf, seg_begin, seg_end, nchunks, out);
+    return hipGetLastError();
+}
+
+hipError_t msa_launch_fn(const ChunkSum *sums, u64 seg_begin, u32 nchunks, Fn *run_prefix, Fn *total,
+                         const State *init, State *carry, State *final_state, hipStream_t s, bool apply_only,
+                         bool compose_only) {
+    if (!apply_only)
+        hipLaunchKernelGGL(k_fn_compose, dim3(1), dim3(FN_THREADS), 0, s, sums, seg_begin, nchunks, run_prefix, total);
+    if (!compose_only)
+        hipLaunchKernelGGL(k_fn_apply, dim3(1), dim3(FN_THREADS), 0, s, sums, seg_begin, nchunks, run_prefix, init,
+                           carry, final_state);
+    return hipGetLastError();
+}
+
+hipError_t msa_launch_scan(const ScanArgs &a, int mode, hipStream_t s) {
+    if (!a.nchunks) return hipSuccess;
+    u32 blocks = (a.nchunks + K3_WAVES - 1) / K3_WAVES;
+    u32 cap = (u32)num_cus() * 2;
+    if (blocks > cap) blocks = cap;
+    if (mode == 0) {
+        static bool attr = false;
+        if (!attr) {
+            hipFuncSetAttribute((const void *)k_scan_main<0>, hipFuncAttributeMaxDynamicSharedMemorySize, K3_LDS);
+            attr = true;
+        }
+        hipLaunchKernelGGL(k_scan_main<0>, dim3(blocks), dim3(K3_THREADS), K3_LDS, s, a);
+    } else {
+        hipLaunchKernelGGL(k_scan_main<1>, dim3(blocks), dim3(K3_THREADS), 0, s, a);
+    }
+    return hipGetLastError();
+}

@@ -1,0 +1,140 @@
+// msa_tables.h -- open-addressing count tables in HBM (device code).
+//
+// Replaces the reference's HashTable/ht_put (parallel_spotify.c:47-149), which
+// keys by strdup'ed strings.  Keys here are exact and fixed-width:
+//   S-table  words of 1..8 bytes  : key = the 8 lower-cased bytes (LE, 0-pad)
+//                                   slot = {key u64, count u64}   16 B
+//   M-table  words of 9..16 bytes : key = two such words
+//                                   slot = {k0, k1, count, 0}     32 B
+//   H-table  anything longer (rare words, artist names): key = 64-bit hash,
+//            slot = {hash, count, rep}; rep = index of the first occurrence,
+//            every occurrence is later byte-compared against rep, so a hash
+//            collision is detected, never silently merged.
+// All shared words are touched with device-scope atomics only (no plain loads
+// of another CU's writes: per-XCD L2s are not coherent).
+#pragma once
+#include "msa_internal.h"
+
+#define MSA_MAX_PROBE 4096u
+
+__device__ __forceinline__ u64 ld_relaxed(const u64 *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// S-table insert; claimed slots are appended to `list` (dense, for ranking).
+__device__ __forceinline__ void s_insert(u64 *tab, u64 mask, u64 key, u64 cnt, u32 *list,
+                                         u64 list_cap, Counters *ctr) {
+    u64 h = fmix64(key) & mask;
+    for (u32 probe = 0; probe < MSA_MAX_PROBE; ++probe) {
+        u64 *slot = tab + 2 * h;
+        u64 cur = ld_relaxed(slot);
+        if (cur == 0) {
+            u64 old = atomicCAS((unsigned long long *)slot, 0ull, (unsigned long long)key);
+            if (old == 0) {
+                atomicAdd((unsigned long long *)(slot + 1), (unsigned long long)cnt);
+                u64 i = atomicAdd((unsigned long long *)&ctr->s_claimed, 1ull);
+                if (i < list_cap) list[i] = (u32)h;
+                else atomicOr((unsigned long long *)&ctr->overflow, (unsigned long long)OVF_S);
+                return;
+            }
+            cur = old;
+        }
+        if (cur == key) {
+            atomicAdd((unsigned long long *)(slot + 1), (unsigned long long)cnt);
+            return;
+        }
+        h = (h + 1) & mask;
+    }
+    atomicOr((unsigned long long *)&ctr->overflow, (unsigned long long)OVF_S);
+}
+
+// M-table insert (two-word key).  The slot is claimed by CAS on k0 and the
+// winner then publishes k1; a prober that finds k0 equal but k1 still 0 simply
+// retries that slot on its next loop trip (no spin inside a divergent branch,
+// so a same-wave winner always gets to publish).
+__device__ __forceinline__ void m_insert(u64 *tab, u64 mask, u64 k0, u64 k1, u64 cnt, u32 *list,
+                                         u64 list_cap, Counters *ctr) {
+    u64 h = fmix64(k0 ^ fmix64(k1)) & mask;
+    u32 probe = 0, spins = 0;
+    while (probe < MSA_MAX_PROBE) {
+        u64 *slot = tab + 4 * h;
+        u64 c0 = ld_relaxed(slot);
+        if (c0 == 0) {
+            u64 old = atomicCAS((unsigned long long *)slot, 0ull, (unsigned long long)k0);
+            if (old == 0) {
+                __hip_atomic_store(slot + 1, k1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                atomicAdd((unsigned long long *)(slot + 2), (unsigned long long)cnt);
+                u64 i = atomicAdd((unsigned long long *)&ctr->m_claimed, 1ull);
+                if (i < list_cap) list[i] = (u32)h;
+                else atomicOr((unsigned long long *)&ctr->overflow, (unsigned long long)OVF_M);
+                return;
+            }
+            c0 = old;
+        }
+        if (c0 == k0) {
+            u64 c1 = ld_relaxed(slot + 1);
+            if (c1 == 0) {  // claimed, k1 not yet visible: retry this slot
+                if (++spins > (1u << 24)) break;
+                __builtin_amdgcn_s_sleep(1);
+                continue;
+            }
+            if (c1 == k1) {
+                atomicAdd((unsigned long long *)(slot + 2), (unsigned long long)cnt);
+                return;
+            }
+        }
+        h = (h + 1) & mask;
+        ++probe;
+    }
+    atomicOr((unsigned long long *)&ctr->overflow, (unsigned long long)OVF_M);
+}
+
+// H-table insert by 64-bit hash; returns the slot index (or ~0 on overflow).
+// The CAS winner records `rep`; readers only look at rep in a later kernel.
+__device__ __forceinline__ u64 h_insert(u64 *tab, u64 mask, u64 hash, u64 cnt, u64 rep, u32 *list,
+                                        u64 list_cap, u64 *claimed, Counters *ctr, u64 ovf_bit) {
+    if (hash == 0) hash = 0x8000000000000000ULL;
+    u64 h = hash & mask;
+    for (u32 probe = 0; probe < MSA_MAX_PROBE; ++probe) {
+        u64 *slot = tab + 4 * h;
+        u64 cur = ld_relaxed(slot);
+        if (cur == 0) {
+            u64 old = atomicCAS((unsigned long long *)slot, 0ull, (unsigned long long)hash);
+            if (old == 0) {
+                __hip_atomic_store(slot + 2, rep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                atomicAdd((unsigned long long *)(slot + 1), (unsigned long long)cnt);
+                u64 i = atomicAdd((unsigned long long *)claimed, 1ull);
+                if (i < list_cap) list[i] = (u32)h;
+                else atomicOr((unsigned long long *)&ctr->overflow, (unsigned long long)ovf_bit);
+                return h;
+            }
+            cur = old;
+        }
+        if (cur == hash) {
+            atomicAdd((unsigned long long *)(slot + 1), (unsigned long long)cnt);
+            return h;
+        }
+        h = (h + 1) & mask;
+    }
+    atomicOr((unsigned long long *)&ctr->overflow, (unsigned long long)ovf_bit);
+    return ~0ull;
+}
+
+// 64-bit hash of a byte string (lower-cased when `lower`), for the H-table.
+__device__ __forceinline__ u64 bytes_hash(const u8 *p, u64 n, int lower) {
+    u64 h = 0x243F6A8885A308D3ULL ^ (n * 0x9E3779B97F4A7C15ULL);
+    u64 acc = 0;
+    u32 k = 0;
+    for (u64 i = 0; i < n; ++i) {
+        u32 c = p[i];
+        if (lower && c >= 'A' && c <= 'Z') c += 32;
+        acc |= (u64)c << (8 * k);
+        if (++k == 8) {
+            h = fmix64(h ^ acc) * 0x9E3779B97F4A7C15ULL;
+            acc = 0;
+            k = 0;
+        }
+    }
+    h = fmix64(h ^ acc ^ ((u64)k << 59));
+    return h;
+}

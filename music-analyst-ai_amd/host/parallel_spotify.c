@@ -1,0 +1,201 @@
+/*
+ * parallel_spotify -- drop-in for the reference CLI
+ * (/root/reference/src/parallel_spotify.c, main at 724-1113) running the hot
+ * path on one MI355X through libmsa_hip.
+ *
+ *   parallel_spotify <dataset.csv> [--word-limit N] [--artist-limit N]
+ *                    [--output-dir DIR] [--device D]
+ *
+ * Writes, like the reference: DIR/split_columns/<artist>.csv and <text>.csv,
+ * DIR/word_counts.csv, DIR/top_artists.csv, DIR/performance_metrics.json and
+ * the same stdout summary.  The ranked CSVs are byte-identical to
+ * `mpirun -np 1 bin/parallel_spotify`; performance_metrics.json has the same
+ * shape with "processes": 1 (one GPU) and this run's times.
+ */
+#define _GNU_SOURCE
+#include <errno.h>
+#include <limits.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/stat.h>
+#include <time.h>
+
+#include "msa_hip.h"
+
+static double now_s(void) {
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return t.tv_sec + 1e-9 * t.tv_nsec;
+}
+
+/* ensure_directory_recursive (parallel_spotify.c:476-504) */
+static int mkdirs(const char *path) {
+    char b[PATH_MAX];
+    size_t n = strlen(path);
+    if (!n) return 0;
+    if (n >= sizeof b) { errno = ENAMETOOLONG; return -1; }
+    memcpy(b, path, n + 1);
+    for (size_t i = 1; i < n; ++i)
+        if (b[i] == '/' || b[i] == '\\') {
+            char s = b[i];
+            b[i] = 0;
+            if (b[0] && strcmp(b, ".") && mkdir(b, 0777) != 0 && errno != EEXIST) { b[i] = s; return -1; }
+            b[i] = s;
+        }
+    if (mkdir(b, 0777) != 0 && errno != EEXIST) return -1;
+    return 0;
+}
+
+static char *read_file(const char *path, size_t *len) {
+    FILE *fp = fopen(path, "rb");
+    if (!fp) return NULL;
+    size_t cap = 1 << 20, n = 0;
+    char *p = (char *)malloc(cap);
+    for (;;) {
+        if (n == cap) { cap *= 2; p = (char *)realloc(p, cap); }
+        if (!p) { fclose(fp); return NULL; }
+        size_t got = fread(p + n, 1, cap - n, fp);
+        if (!got) break;
+        n += got;
+    }
+    fclose(fp);
+    *len = n;
+    return p;
+}
+
+static int write_all(const char *path, const char *p, size_t n) {
+    FILE *fp = fopen(path, "wb");
+    if (!fp) return -1;
+    if (n && fwrite(p, 1, n, fp) != n) { fclose(fp); return -1; }
+    return fclose(fp);
+}
+
+static void die(msa_ctx *ctx, int rc, const char *what) {
+    fprintf(stderr, "%s: %s\n", what, ctx ? msa_last_error(ctx) : "");
+    if (ctx) msa_destroy(ctx);
+    exit(rc == MSA_ERR_NOHEADER || rc == MSA_ERR_BADHEADER ? EXIT_FAILURE : 2);
+}
+
+static void print_top(msa_ctx *ctx, int table, const char *fmt_suffix, const char *title) {
+    msa_summary s;
+    msa_get_summary(ctx, &s);
+    uint64_t n = table == MSA_TABLE_WORDS ? s.n_words : s.n_artists;
+    uint64_t k = n < 10 ? n : 10;
+    long long counts[10];
+    uint64_t offs[11], need = 0;
+    char *keys = NULL;
+    msa_get_ranked(ctx, table, 0, k, NULL, NULL, NULL, 0, &need);
+    keys = (char *)malloc(need + 1);
+    msa_get_ranked(ctx, table, 0, k, counts, offs, keys, need + 1, &need);
+    printf("Top %zu %s:\n", (size_t)k, title);
+    for (uint64_t i = 0; i < k; ++i) {
+        printf("  %.*s: %lld%s\n", (int)(offs[i + 1] - offs[i]), keys + offs[i], counts[i], fmt_suffix);
+    }
+    free(keys);
+}
+
+int main(int argc, char **argv) {
+    if (argc < 2) {
+        fprintf(stderr, "Usage: %s <dataset.csv> [--word-limit N] [--artist-limit N] [--output-dir DIR] [--device D]\n",
+                argv[0]);
+        return EXIT_FAILURE;
+    }
+    const char *dataset = argv[1];
+    int word_limit = 0, artist_limit = 0, device = 0;
+    char outdir[PATH_MAX];
+    snprintf(outdir, sizeof outdir, "output");
+    for (int i = 2; i < argc; ++i) {
+        if (!strcmp(argv[i], "--word-limit") && i + 1 < argc) word_limit = atoi(argv[++i]);
+        else if (!strcmp(argv[i], "--artist-limit") && i + 1 < argc) artist_limit = atoi(argv[++i]);
+        else if (!strcmp(argv[i], "--output-dir") && i + 1 < argc) {
+            strncpy(outdir, argv[++i], sizeof outdir - 1);
+            outdir[sizeof outdir - 1] = 0;
+        } else if (!strcmp(argv[i], "--device") && i + 1 < argc) device = atoi(argv[++i]);
+        else fprintf(stderr, "Ignoring unknown argument: %s\n", argv[i]);
+    }
+    char split_dir[PATH_MAX], path[PATH_MAX];
+    int l = snprintf(split_dir, sizeof split_dir, "%s/split_columns", outdir);
+    if (l < 0 || (size_t)l >= sizeof split_dir) { fprintf(stderr, "Split directory path is too long\n"); return EXIT_FAILURE; }
+    if (mkdirs(outdir) != 0) {
+        fprintf(stderr, "Failed to prepare output directory %s: %s\n", outdir, strerror(errno));
+        return EXIT_FAILURE;
+    }
+    if (mkdirs(split_dir) != 0) {
+        fprintf(stderr, "Failed to prepare split directory %s: %s\n", split_dir, strerror(errno));
+        return EXIT_FAILURE;
+    }
+    size_t n = 0;
+    char *csv = read_file(dataset, &n);
+    if (!csv) { fprintf(stderr, "Failed to open dataset %s\n", dataset); return EXIT_FAILURE; }
+
+    msa_ctx *ctx = NULL;
+    int rc = msa_create(device, &ctx);
+    if (rc) { fprintf(stderr, "libmsa_hip: cannot open GPU %d (code %d)\n", device, rc); return 2; }
+    if ((rc = msa_load_csv(ctx, csv, n))) die(ctx, rc, "load");
+    free(csv);
+
+    double t_split0 = now_s();
+    rc = msa_split_columns(ctx, MSA_SPLIT_TEXT_COLUMN);
+    if (rc == MSA_ERR_NOHEADER) die(ctx, rc, "Dataset does not contain a header row");
+    if (rc == MSA_ERR_BADHEADER) die(ctx, rc, "Unable to parse dataset header");
+    if (rc) die(ctx, rc, "Failed to split dataset columns");
+    (void)t_split0;
+    msa_summary s;
+    msa_get_summary(ctx, &s);
+    for (int which = 0; which < 2; ++which) {
+        char *col = NULL;
+        size_t cl = 0;
+        if ((rc = msa_get_split_column(ctx, which, &col, &cl))) die(ctx, rc, "split column");
+        snprintf(path, sizeof path, "%s/%s.csv", split_dir, which ? s.text_file : s.artist_file);
+        if (write_all(path, col, cl) != 0) fprintf(stderr, "Failed to create split files in %s\n", split_dir);
+        msa_free(col);
+    }
+
+    /* timed region of the reference: after the split, through the outputs */
+    double t0 = now_s();
+    if ((rc = msa_count(ctx))) die(ctx, rc, "count");
+    if ((rc = msa_sync(ctx))) die(ctx, rc, "sync");
+    double compute = now_s() - t0;
+    if ((rc = msa_rank(ctx))) die(ctx, rc, "rank");
+    msa_get_summary(ctx, &s);
+
+    snprintf(path, sizeof path, "%s/word_counts.csv", outdir);
+    if ((rc = msa_write_table_csv(ctx, MSA_TABLE_WORDS, path, "word", word_limit)))
+        fprintf(stderr, "%s\n", msa_last_error(ctx));
+    snprintf(path, sizeof path, "%s/top_artists.csv", outdir);
+    if ((rc = msa_write_table_csv(ctx, MSA_TABLE_ARTISTS, path, "artist", artist_limit)))
+        fprintf(stderr, "%s\n", msa_last_error(ctx));
+
+    printf("=== Parallel Spotify Analysis ===\n");
+    printf("Total songs processed: %lld\n", s.total_songs);
+    printf("Total words counted: %lld\n", s.total_words);
+    print_top(ctx, MSA_TABLE_WORDS, "", "words");
+    print_top(ctx, MSA_TABLE_ARTISTS, " songs", "artists");
+    double total = now_s() - t0;
+
+    snprintf(path, sizeof path, "%s/performance_metrics.json", outdir);
+    FILE *mf = fopen(path, "w");
+    if (mf) {
+        fprintf(mf, "{\n");
+        fprintf(mf, "  \"processes\": %d,\n", 1);
+        fprintf(mf, "  \"total_songs\": %lld,\n", s.total_songs);
+        fprintf(mf, "  \"total_words\": %lld,\n", s.total_words);
+        fprintf(mf, "  \"compute_time\": {\n");
+        fprintf(mf, "    \"avg_seconds\": %.6f,\n", compute);
+        fprintf(mf, "    \"min_seconds\": %.6f,\n", compute);
+        fprintf(mf, "    \"max_seconds\": %.6f\n", compute);
+        fprintf(mf, "  },\n");
+        fprintf(mf, "  \"total_time\": {\n");
+        fprintf(mf, "    \"avg_seconds\": %.6f,\n", total);
+        fprintf(mf, "    \"min_seconds\": %.6f,\n", total);
+        fprintf(mf, "    \"max_seconds\": %.6f\n", total);
+        fprintf(mf, "  }\n");
+        fprintf(mf, "}\n");
+        fclose(mf);
+    } else {
+        fprintf(stderr, "Failed to write performance metrics file\n");
+    }
+    msa_destroy(ctx);
+    return EXIT_SUCCESS;
+}
