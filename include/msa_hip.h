@@ -137,6 +137,22 @@ int msa_write_table_csv(msa_ctx *ctx, int table, const char *path,
 /* Host copy of a materialised split column (0 = artist.csv, 1 = text.csv). */
 int msa_get_split_column(msa_ctx *ctx, int which, char **out, size_t *len);
 
+/* ------------------------------------------------------------- profiling
+ * HIP-event timing of each pipeline stage on the context's stream (no
+ * reference counterpart; the reference's MPI_Wtime bracketing lives in the
+ * CLI).  Stage times accumulate over runs until read with reset != 0.     */
+#define MSA_PROF_MAX 16
+typedef struct {
+    int n;                          /* stages with data                      */
+    char name[MSA_PROF_MAX][32];
+    double ms[MSA_PROF_MAX];        /* summed event time                     */
+    uint64_t launches[MSA_PROF_MAX];/* how many times the stage ran          */
+    uint64_t bytes[MSA_PROF_MAX];   /* summed algorithmic bytes  */
+} msa_profile;
+
+int msa_set_profiling(msa_ctx *ctx, int on);
+int msa_get_profile(msa_ctx *ctx, msa_profile *out, int reset);
+
 /* ------------------------------------------------- multi-GPU (one process
  * per GPU; the caller moves bytes with RCCL).  A shard is a contiguous byte
  * range of one logical CSV; shard 0 holds the header. */

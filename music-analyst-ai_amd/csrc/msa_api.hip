@@ -30,8 +30,8 @@ hipError_t msa_launch_text_write(const u8 *, const u64 *, const u64 *, const u32
                                  u8 *, hipStream_t);
 hipError_t msa_launch_artist_key(const u8 *, const u64 *, const u64 *, u64, u8 *, u64 *, u32 *, u64 *, u64 *, u64,
                                  u32 *, u64, Counters *, hipStream_t);
-hipError_t msa_launch_long(const u8 *, u64, const u64 *, u64, u32 *, u64 *, u64 *, u64, u32 *, u64, Counters *,
-                           hipStream_t);
+hipError_t msa_launch_long(const u8 *, u64, const u8 *, u64, const u64 *, u64, u32 *, u64 *, u64 *, u64, u32 *, u64,
+                           Counters *, hipStream_t);
 hipError_t msa_launch_word_entries(const EntryArgs &, hipStream_t);
 hipError_t msa_launch_artist_entries(const u64 *, const u32 *, u64, const u8 *, const u64 *, const u32 *, u64 *, u64 *,
                                      u64 *, u32 *, u64 *, u64 *, hipStream_t);
@@ -40,9 +40,9 @@ u64 msa_radix_blocks(u64 n);
 hipError_t msa_launch_radix_pass(const u64 *, const u64 *, const u64 *, const u32 *, u64, u32, u64 *, u64 *, u64 *,
                                  u64 *, u64 *, u64 *, u32 *, hipStream_t);
 hipError_t msa_launch_fixup(const u64 *, const u64 *, const u64 *, const u32 *, u64, const u64 *, const u8 *,
-                            const u64 *, const u32 *, const u8 *, const u64 *, const u32 *, u32 *, hipStream_t);
+                            const u8 *, const u64 *, const u32 *, const u8 *, const u64 *, const u32 *, u32 *, hipStream_t);
 hipError_t msa_launch_blob(const u32 *, u64, const u64 *, const u64 *, const u64 *, const u64 *, const u8 *,
-                           const u64 *, const u32 *, const u8 *, const u64 *, const u32 *, u64 *, u64 *, u64 *, u64 *,
+                           const u8 *, const u64 *, const u32 *, const u8 *, const u64 *, const u32 *, u64 *, u64 *, u64 *, u64 *,
                            u8 *, u64 *, hipStream_t, int);
 
 // ---------------------------------------------------------------------------
@@ -71,6 +71,31 @@ u64 next_pow2(u64 v) {
     return p;
 }
 
+// Pipeline stages timed with HIP events when profiling is on.
+enum {
+    ST_CSV_SUMMARY = 0,  // K1 + K2 over the CSV (chunk functions + prefix)
+    ST_CSV_SCAN,         // K3: records, fields, lyric tokens -> word tables
+    ST_ARTIST_COLUMN,    // artist.csv materialisation
+    ST_TEXT_COLUMN,      // text.csv materialisation
+    ST_ARTIST_SUMMARY,   // K1 + K2 over artist.csv
+    ST_ARTIST_SCAN,      // K3 (records only) over artist.csv
+    ST_ARTIST_KEYS,      // duplicate_field + artist table
+    ST_LONG_WORDS,       // > 16-byte words: hash table + verification
+    ST_RANK_WORDS,       // entries + radix sort + key blob, words
+    ST_RANK_ARTISTS,     // the same, artists
+    ST_COUNT_
+};
+const char *const kStageName[ST_COUNT_] = {"csv_summary", "csv_scan",    "artist_column", "text_column",
+                                           "artist_summary", "artist_scan", "artist_keys",  "long_words",
+                                           "rank_words",  "rank_artists"};
+
+struct ProfStage {
+    hipEvent_t a = nullptr, b = nullptr;
+    bool pending = false;
+    double ms = 0;
+    u64 launches = 0, bytes = 0, pend_bytes = 0;
+};
+
 }  // namespace
 
 struct msa_ctx {
@@ -87,6 +112,9 @@ struct msa_ctx {
     DevBuf rec_start, rec_term, f0rel, f3rel, nulrel;
     u64 nrec = 0, rec_cap = 0;
     bool have_text_arrays = false;
+    // side buffer: text.csv header-label remainder read back as lyrics
+    DevBuf extra;
+    u64 extra_len = 0;
     // columns
     DevBuf acol, alen, aoff, tcol, tlen, toff, scan_bsum, scan_total;
     u64 acol_len = 0, a_hdr_getline = 0, tcol_len = 0;
@@ -106,7 +134,40 @@ struct msa_ctx {
     Ranked rw, ra;
     msa_summary sum{};
     int stage = 0;  // 0 none, 1 split, 2 counted, 3 ranked
+    // profiling
+    bool prof = false;
+    ProfStage ps[ST_COUNT_];
 };
+
+// Fold a finished stage's event pair into its accumulator (waits for it).
+static void prof_harvest(msa_ctx *c, int id) {
+    ProfStage &s = c->ps[id];
+    if (!s.pending) return;
+    float ms = 0;
+    if (hipEventSynchronize(s.b) == hipSuccess && hipEventElapsedTime(&ms, s.a, s.b) == hipSuccess) {
+        s.ms += ms;
+        s.launches += 1;
+        s.bytes += s.pend_bytes;
+    }
+    s.pending = false;
+}
+static void prof_begin(msa_ctx *c, int id) {
+    if (!c->prof) return;
+    ProfStage &s = c->ps[id];
+    prof_harvest(c, id);
+    if (!s.a) {
+        (void)hipEventCreate(&s.a);
+        (void)hipEventCreate(&s.b);
+    }
+    (void)hipEventRecord(s.a, c->stream);
+}
+static void prof_end(msa_ctx *c, int id, u64 bytes) {
+    if (!c->prof) return;
+    ProfStage &s = c->ps[id];
+    (void)hipEventRecord(s.b, c->stream);
+    s.pend_bytes = bytes;
+    s.pending = true;
+}
 
 static int fail(msa_ctx *c, int code, const char *fmt, ...) {
     char b[512];
@@ -207,7 +268,7 @@ static void h_sanitize(const std::string &in, char *out) {
 // ------------------------------------------------------------------- scanning
 // Scan a byte segment [b, e) of `buf`: K1 + K2 (+ K3 in `mode`).  Returns the
 // reader state at the end of the segment in *fin.
-static int run_scan_fn(msa_ctx *c, const u8 *buf, u64 b, u64 e, State init, State *fin) {
+static int run_scan_fn(msa_ctx *c, const u8 *buf, u64 b, u64 e, State init, State *fin, int stage_id) {
     const u64 len = e > b ? e - b : 0;
     const u32 nch = (u32)((len + MSA_CHUNK - 1) / MSA_CHUNK);
     HIPC(c, ensure(c->sums, sizeof(ChunkSum) * (size_t)(nch + 1)));
@@ -219,9 +280,11 @@ static int run_scan_fn(msa_ctx *c, const u8 *buf, u64 b, u64 e, State init, Stat
     State *d_fin = d_init + 1;
     HIPC(c, hipMemcpyAsync(d_init, &init, sizeof(State), hipMemcpyHostToDevice, c->stream));
     if (nch) {
+        prof_begin(c, stage_id);
         HIPC(c, msa_launch_summary(buf, b, e, nch, c->sums.as<ChunkSum>(), c->stream));
         HIPC(c, msa_launch_fn(c->sums.as<ChunkSum>(), b, nch, c->runpre.as<Fn>(), total, d_init, c->carry.as<State>(),
                               d_fin, c->stream, false, false));
+        prof_end(c, stage_id, len);
         HIPC(c, hipMemcpyAsync(fin, d_fin, sizeof(State), hipMemcpyDeviceToHost, c->stream));
         HIPC(c, hipStreamSynchronize(c->stream));
     } else {
@@ -355,7 +418,7 @@ static int do_split(msa_ctx *c, int flags) {
     HIPC(c, hipMemsetAsync(c->ctr.p, 0, sizeof(Counters), c->stream));
 
     State init{0, 0, 0, 0, 0, 0}, fin;
-    if ((rc = run_scan_fn(c, c->in, 0, c->n, init, &fin))) return rc;
+    if ((rc = run_scan_fn(c, c->in, 0, c->n, init, &fin, ST_CSV_SUMMARY))) return rc;
     const u64 nterm = fin.rec;
     c->nrec = nterm + (fin.rs < c->n ? 1 : 0);
     const u64 cap = nterm + 2;
@@ -396,7 +459,10 @@ static int do_split(msa_ctx *c, int flags) {
     a.l_cap = c->l_occ_cap;
     a.ctr = c->ctr.as<Counters>();
     a.want_term = want_text ? 1 : 0;
+    prof_begin(c, ST_CSV_SCAN);
     HIPC(c, msa_launch_scan(a, 0, c->stream));
+    // algorithmic bytes: every CSV byte once + the per-record SoA it writes
+    prof_end(c, ST_CSV_SCAN, c->n + c->nrec * (want_text ? 28ull : 16ull));
     // the last record may end at EOF instead of a terminator
     if (fin.rs < c->n) {
         u64 v = c->n;
@@ -422,9 +488,37 @@ static int do_split(msa_ctx *c, int flags) {
     h_sanitize(al, c->sum.artist_file);
     h_sanitize(tl, c->sum.text_file);
 
+    // text.csv's header line is "<label>\n"; compute_header_length (parallel_spotify.c:444-459)
+    // stops at the label's first '\n', so the rest of a multi-line label is read back as
+    // lyrics by the text pass (918-941).  Tokenise that remainder too (FLAT scan).
+    c->extra_len = 0;
+    {
+        std::string th = c->sum.text_label[0] ? c->sum.text_label : "Texts";
+        const size_t nl = th.find('\n');
+        if (nl != std::string::npos) {
+            std::string rem = th.substr(nl + 1);
+            rem.push_back('\n');
+            c->extra_len = rem.size();
+            HIPC(c, ensure(c->extra, c->extra_len + MSA_INPUT_PAD + MSA_CHUNK));
+            HIPC(c, hipMemsetAsync(c->extra.p, 0, c->extra_len + MSA_INPUT_PAD + MSA_CHUNK, c->stream));
+            HIPC(c, hipMemcpyAsync(c->extra.p, rem.data(), rem.size(), hipMemcpyHostToDevice, c->stream));
+            State *d_zero = reinterpret_cast<State *>(c->small.as<char>() + 2048);
+            HIPC(c, hipMemsetAsync(d_zero, 0, sizeof(State), c->stream));
+            ScanArgs f = a;  // same tables and counters
+            f.buf = c->extra.as<u8>();
+            f.seg_begin = 0;
+            f.seg_end = c->extra_len;
+            f.nchunks = 1;
+            f.carry = d_zero;
+            f.lpos_tag = MSA_POS_EXTRA;
+            HIPC(c, msa_launch_scan(f, 2, c->stream));
+        }
+    }
     std::string ah = c->sum.artist_label[0] ? c->sum.artist_label : "Artists";
     ah.push_back('\n');
+    prof_begin(c, ST_ARTIST_COLUMN);
     if ((rc = materialise_column(c, false, ah, c->acol, c->alen, c->aoff, &c->acol_len))) return rc;
+    prof_end(c, ST_ARTIST_COLUMN, c->acol_len * 2 + c->nrec * 32);
     {
         size_t p = ah.find('\n');
         c->a_hdr_getline = p + 1;  // compute_header_length (parallel_spotify.c:444-459)
@@ -433,7 +527,9 @@ static int do_split(msa_ctx *c, int flags) {
     if (want_text) {
         std::string th = c->sum.text_label[0] ? c->sum.text_label : "Texts";
         th.push_back('\n');
+        prof_begin(c, ST_TEXT_COLUMN);
         if ((rc = materialise_column(c, true, th, c->tcol, c->tlen, c->toff, &c->tcol_len))) return rc;
+        prof_end(c, ST_TEXT_COLUMN, c->tcol_len * 2 + c->nrec * 40);
         c->have_tcol = true;
     }
     c->stage = 1;
@@ -447,7 +543,7 @@ static int do_count(msa_ctx *c) {
     // artist pass over artist.csv records from its getline header end
     const u64 b = c->a_hdr_getline, e = c->acol_len;
     State init{0, b, 0, 0, 0, 0}, fin;
-    if ((rc = run_scan_fn(c, c->acol.as<u8>(), b, e, init, &fin))) return rc;
+    if ((rc = run_scan_fn(c, c->acol.as<u8>(), b, e, init, &fin, ST_ARTIST_SUMMARY))) return rc;
     const u64 nterm = fin.rec;
     c->nrec_a = nterm + (fin.rs < e ? 1 : 0);
     const u64 cap = nterm + 2;
@@ -470,19 +566,25 @@ static int do_count(msa_ctx *c) {
         a.rec_cap = cap;
         a.ctr = c->ctr.as<Counters>();
         a.want_term = 1;
+        prof_begin(c, ST_ARTIST_SCAN);
         HIPC(c, msa_launch_scan(a, 1, c->stream));
+        prof_end(c, ST_ARTIST_SCAN, (e - b) + c->nrec_a * 16);
     }
     if (fin.rs < e) HIPC(c, hipMemcpyAsync(c->ar_term.as<u64>() + (c->nrec_a - 1), &e, 8, hipMemcpyHostToDevice, c->stream));
+    prof_begin(c, ST_ARTIST_KEYS);
     HIPC(c, msa_launch_artist_key(c->acol.as<u8>(), c->ar_start.as<u64>(), c->ar_term.as<u64>(), c->nrec_a,
                                   c->arena.as<u8>(), c->key_off.as<u64>(), c->key_len.as<u32>(), c->key_slot.as<u64>(),
                                   c->a_tab.as<u64>(), c->a_slots - 1, c->a_list.as<u32>(), c->a_slots / 2,
                                   c->ctr.as<Counters>(), c->stream));
+    prof_end(c, ST_ARTIST_KEYS, (e - b) * 2 + c->nrec_a * 48);
     if ((rc = sync_counters(c))) return rc;
     // words longer than 16 bytes
     const u64 nl = std::min<u64>(c->h_ctr.l_occ, c->l_occ_cap);
-    HIPC(c, msa_launch_long(c->in, c->n, c->l_pos.as<u64>(), nl, c->l_len.as<u32>(), c->l_slot.as<u64>(),
+    prof_begin(c, ST_LONG_WORDS);
+    HIPC(c, msa_launch_long(c->in, c->n, c->extra.as<u8>(), c->extra_len, c->l_pos.as<u64>(), nl, c->l_len.as<u32>(), c->l_slot.as<u64>(),
                             c->l_tab.as<u64>(), c->lt_slots - 1, c->l_list.as<u32>(), c->lt_slots / 2,
                             c->ctr.as<Counters>(), c->stream));
+    prof_end(c, ST_LONG_WORDS, nl * 64);
     if ((rc = sync_counters(c))) return rc;
     c->s_used_prev = std::min<u64>(c->h_ctr.s_claimed, c->s_slots / 2);
     c->m_used_prev = std::min<u64>(c->h_ctr.m_claimed, c->m_slots / 2);
@@ -540,7 +642,7 @@ static int sort_and_blob(msa_ctx *c, Ranked &R, const u8 *arena, const u64 *key_
     }
     HIPC(c, ensure(R.order, n * 4));
     HIPC(c, msa_launch_fixup(R.K[cur][0].as<u64>(), R.K[cur][1].as<u64>(), R.K[cur][2].as<u64>(), R.V[cur].as<u32>(),
-                             n, R.ref.as<u64>(), c->in, c->l_pos.as<u64>(), c->l_len.as<u32>(), arena, key_off,
+                             n, R.ref.as<u64>(), c->in, c->extra.as<u8>(), c->l_pos.as<u64>(), c->l_len.as<u32>(), arena, key_off,
                              key_len, R.order.as<u32>(), c->stream));
     // key blob in rank order
     HIPC(c, ensure(R.len, n * 8));
@@ -549,14 +651,14 @@ static int sort_and_blob(msa_ctx *c, Ranked &R, const u8 *arena, const u64 *key_
     HIPC(c, ensure(c->scan_total, 64));
     HIPC(c, ensure(c->scan_bsum, ((n + 1023) / 1024 + 1) * 8));
     HIPC(c, msa_launch_blob(R.order.as<u32>(), n, R.ref.as<u64>(), R.K[0][1].as<u64>(), R.K[0][2].as<u64>(),
-                            R.cnt.as<u64>(), c->in, c->l_pos.as<u64>(), c->l_len.as<u32>(), arena, key_off, key_len,
+                            R.cnt.as<u64>(), c->in, c->extra.as<u8>(), c->l_pos.as<u64>(), c->l_len.as<u32>(), arena, key_off, key_len,
                             R.len.as<u64>(), R.off.as<u64>(), c->scan_bsum.as<u64>(), c->scan_total.as<u64>(), nullptr,
                             nullptr, c->stream, 0));
     HIPC(c, hipMemcpyAsync(&R.blob_len, c->scan_total.p, 8, hipMemcpyDeviceToHost, c->stream));
     HIPC(c, hipStreamSynchronize(c->stream));
     HIPC(c, ensure(R.blob, R.blob_len + 16));
     HIPC(c, msa_launch_blob(R.order.as<u32>(), n, R.ref.as<u64>(), R.K[0][1].as<u64>(), R.K[0][2].as<u64>(),
-                            R.cnt.as<u64>(), c->in, c->l_pos.as<u64>(), c->l_len.as<u32>(), arena, key_off, key_len,
+                            R.cnt.as<u64>(), c->in, c->extra.as<u8>(), c->l_pos.as<u64>(), c->l_len.as<u32>(), arena, key_off, key_len,
                             R.len.as<u64>(), R.off.as<u64>(), c->scan_bsum.as<u64>(), c->scan_total.as<u64>(),
                             R.blob.as<u8>(), R.counts.as<u64>(), c->stream, 1));
     return MSA_OK;
@@ -568,6 +670,7 @@ static int do_rank(msa_ctx *c) {
     // words
     Ranked &W = c->rw;
     W.n = c->sum.n_words;
+    prof_begin(c, ST_RANK_WORDS);
     if (W.n) {
         for (int k = 0; k < 3; ++k) HIPC(c, ensure(W.K[0][k], W.n * 8));
         HIPC(c, ensure(W.V[0], W.n * 4));
@@ -584,6 +687,7 @@ static int do_rank(msa_ctx *c) {
         ea.l_list = c->l_list.as<u32>();
         ea.nl = c->h_ctr.l_claimed;
         ea.buf = c->in;
+        ea.extra = c->extra.as<u8>();
         ea.l_pos = c->l_pos.as<u64>();
         ea.l_len = c->l_len.as<u32>();
         ea.K2 = W.K[0][0].as<u64>();
@@ -595,9 +699,11 @@ static int do_rank(msa_ctx *c) {
         HIPC(c, msa_launch_word_entries(ea, c->stream));
     }
     if ((rc = sort_and_blob(c, W, nullptr, nullptr, nullptr))) return rc;
+    prof_end(c, ST_RANK_WORDS, W.n * 64 + W.blob_len);
     // artists
     Ranked &A = c->ra;
     A.n = c->sum.n_artists;
+    prof_begin(c, ST_RANK_ARTISTS);
     if (A.n) {
         for (int k = 0; k < 3; ++k) HIPC(c, ensure(A.K[0][k], A.n * 8));
         HIPC(c, ensure(A.V[0], A.n * 4));
@@ -609,6 +715,7 @@ static int do_rank(msa_ctx *c) {
                                           A.cnt.as<u64>(), c->stream));
     }
     if ((rc = sort_and_blob(c, A, c->arena.as<u8>(), c->key_off.as<u64>(), c->key_len.as<u32>()))) return rc;
+    prof_end(c, ST_RANK_ARTISTS, A.n * 64 + A.blob_len);
     HIPC(c, hipStreamSynchronize(c->stream));
     c->stage = 3;
     return MSA_OK;
@@ -653,7 +760,7 @@ void msa_destroy(msa_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
-    DevBuf *all[] = {&c->in_own, &c->sums, &c->carry, &c->runpre, &c->small, &c->rec_start, &c->rec_term,
+    DevBuf *all[] = {&c->in_own, &c->sums, &c->carry, &c->runpre, &c->small, &c->rec_start, &c->rec_term, &c->extra,
                      &c->f0rel, &c->f3rel, &c->nulrel, &c->acol, &c->alen, &c->aoff, &c->tcol, &c->tlen, &c->toff,
                      &c->scan_bsum, &c->scan_total, &c->ar_start, &c->ar_term, &c->arena, &c->key_off,
                      &c->key_len, &c->key_slot, &c->s_tab, &c->s_list, &c->m_tab, &c->m_list, &c->l_pos, &c->l_len,
@@ -666,6 +773,10 @@ void msa_destroy(msa_ctx *c) {
         DevBuf *rb[] = {&R->ref, &R->cnt, &R->order, &R->len, &R->off, &R->blob, &R->counts, &R->bhist, &R->boff,
                         &R->bsum, &R->ghist};
         for (DevBuf *b : rb) release(*b);
+    }
+    for (ProfStage &s : c->ps) {
+        if (s.a) (void)hipEventDestroy(s.a);
+        if (s.b) (void)hipEventDestroy(s.b);
     }
     (void)hipStreamDestroy(c->stream);
     delete c;
@@ -815,6 +926,30 @@ int msa_get_split_column(msa_ctx *c, int which, char **out, size_t *len) {
     p[n] = 0;
     *out = p;
     *len = n;
+    return MSA_OK;
+}
+
+int msa_set_profiling(msa_ctx *c, int on) {
+    if (!c) return MSA_ERR_ARG;
+    c->prof = on != 0;
+    return MSA_OK;
+}
+
+int msa_get_profile(msa_ctx *c, msa_profile *out, int reset) {
+    if (!c || !out) return MSA_ERR_ARG;
+    HIPC(c, hipSetDevice(c->device));
+    memset(out, 0, sizeof *out);
+    for (int i = 0; i < ST_COUNT_ && i < MSA_PROF_MAX; ++i) {
+        prof_harvest(c, i);
+        ProfStage &s = c->ps[i];
+        if (!s.launches) continue;
+        const int k = out->n++;
+        snprintf(out->name[k], sizeof out->name[k], "%s", kStageName[i]);
+        out->ms[k] = s.ms;
+        out->launches[k] = s.launches;
+        out->bytes[k] = s.bytes;
+        if (reset) { s.ms = 0; s.launches = 0; s.bytes = 0; }
+    }
     return MSA_OK;
 }
 

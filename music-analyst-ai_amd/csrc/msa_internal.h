@@ -260,9 +260,17 @@ struct ScanArgs {
     u64 m_list_cap;
     u64 *l_pos;
     u64 l_cap;
+    u64 lpos_tag;    // OR'ed into recorded long-token positions (MSA_POS_EXTRA: the side buffer)
     Counters *ctr;
     int want_term;
 };
+
+// A long-token position with this bit set indexes the context's side buffer
+// (text.csv header-label remainder, see do_split) instead of the CSV.
+#define MSA_POS_EXTRA (1ull << 63)
+__host__ __device__ inline const u8 *tok_at(const u8 *buf, const u8 *extra, u64 pos) {
+    return (pos & MSA_POS_EXTRA) ? extra + (pos & ~MSA_POS_EXTRA) : buf + pos;
+}
 struct EntryArgs {
     const u64 *s_tab;
     const u32 *s_list;
@@ -274,6 +282,7 @@ struct EntryArgs {
     const u32 *l_list;
     u64 nl;
     const u8 *buf;
+    const u8 *extra;
     const u64 *l_pos;
     const u32 *l_len;
     u64 *K2, *K1, *K0;

@@ -244,22 +244,25 @@ __global__ void k_artist_verify(const u8 *__restrict__ arena, const u64 *__restr
 
 // ---------------------------------------------------------------------------
 // words > 16 bytes
-__global__ void k_long_insert(const u8 *__restrict__ buf, u64 seg_end, const u64 *__restrict__ l_pos, u64 n,
+__global__ void k_long_insert(const u8 *__restrict__ buf, u64 seg_end, const u8 *__restrict__ extra, u64 extra_len,
+                              const u64 *__restrict__ l_pos, u64 n,
                               u32 *__restrict__ l_len, u64 *__restrict__ l_slot, u64 *ltab, u64 lmask, u32 *llist,
                               u64 llist_cap, Counters *ctr) {
     const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const u64 p = l_pos[i];
+    const u8 *src = tok_at(buf, extra, p);
+    const u64 lim = (p & MSA_POS_EXTRA) ? extra_len - (p & ~MSA_POS_EXTRA) : seg_end - p;
     u64 len = 0;
-    while (p + len < seg_end && c_tok(buf[p + len])) ++len;
+    while (len < lim && c_tok(src[len])) ++len;
     l_len[i] = (u32)len;
-    const u64 h = bytes_hash(buf + p, len, 1);
+    const u64 h = bytes_hash(src, len, 1);
     l_slot[i] = h_insert(ltab, lmask, h, 1, i, llist, llist_cap, &ctr->l_claimed, ctr, OVF_LT);
 }
 
 __device__ __forceinline__ u32 lower1(u32 c) { return (c >= 'A' && c <= 'Z') ? c + 32 : c; }
 
-__global__ void k_long_verify(const u8 *__restrict__ buf, const u64 *__restrict__ l_pos,
+__global__ void k_long_verify(const u8 *__restrict__ buf, const u8 *__restrict__ extra, const u64 *__restrict__ l_pos,
                               const u32 *__restrict__ l_len, const u64 *__restrict__ l_slot, u64 n,
                               const u64 *__restrict__ ltab, Counters *ctr) {
     const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
@@ -268,7 +271,7 @@ __global__ void k_long_verify(const u8 *__restrict__ buf, const u64 *__restrict_
     if (rep == i) return;
     const u32 len = l_len[i];
     bool same = l_len[rep] == len;
-    const u8 *a = buf + l_pos[i], *b = buf + l_pos[rep];
+    const u8 *a = tok_at(buf, extra, l_pos[i]), *b = tok_at(buf, extra, l_pos[rep]);
     for (u32 k = 0; same && k < len; ++k) same = lower1(a[k]) == lower1(b[k]);
     if (!same) atomicAdd((unsigned long long *)&ctr->collision, 1ull);
 }
@@ -314,7 +317,7 @@ __global__ void k_word_entries(EntryArgs a) {
         const u64 slot = a.l_list[i - a.ns - a.nm];
         c = a.l_tab[4 * slot + 1];
         const u64 rep = a.l_tab[4 * slot + 2];
-        be16(a.buf + a.l_pos[rep], a.l_len[rep], 1, &hi, &lo);
+        be16(tok_at(a.buf, a.extra, a.l_pos[rep]), a.l_len[rep], 1, &hi, &lo);
         ref = ((u64)KIND_L << 60) | rep;
     }
     a.K2[i] = ~c;
@@ -430,24 +433,25 @@ __global__ __launch_bounds__(RS_T) void k_radix_scatter(const u64 *__restrict__ 
 // ---------------------------------------------------------------------------
 // Exact tie fix-up: runs of equal (K2, K1, K0) (keys sharing 16 leading bytes
 // and a count) are re-ordered by full strcmp.  Run sizes are tiny.
-__device__ __forceinline__ void key_bytes(u64 ref, u64 k1, u64 k0, const u8 *buf, const u64 *l_pos,
+__device__ __forceinline__ void key_bytes(u64 ref, u64 k1, u64 k0, const u8 *buf, const u8 *extra, const u64 *l_pos,
                                           const u32 *l_len, const u8 *arena, const u64 *key_off,
                                           const u32 *key_len, const u8 **p, u64 *n, int *lower) {
     const u32 kind = (u32)(ref >> 60);
     const u64 idx = ref & ((1ull << 60) - 1);
     *lower = 0;
-    if (kind == KIND_L) { *p = buf + l_pos[idx]; *n = l_len[idx]; *lower = 1; }
+    if (kind == KIND_L) { *p = tok_at(buf, extra, l_pos[idx]); *n = l_len[idx]; *lower = 1; }
     else if (kind == KIND_A) { *p = arena + key_off[idx]; *n = key_len[idx]; }
     else { *p = nullptr; *n = 0; }
 }
 
-__device__ int full_cmp(u64 refa, u64 refb, u64 k1, u64 k0, const u8 *buf, const u64 *l_pos, const u32 *l_len,
+__device__ int full_cmp(u64 refa, u64 refb, u64 k1, u64 k0, const u8 *buf, const u8 *extra, const u64 *l_pos,
+                        const u32 *l_len,
                         const u8 *arena, const u64 *key_off, const u32 *key_len) {
     const u8 *pa, *pb;
     u64 na, nb;
     int la, lb;
-    key_bytes(refa, k1, k0, buf, l_pos, l_len, arena, key_off, key_len, &pa, &na, &la);
-    key_bytes(refb, k1, k0, buf, l_pos, l_len, arena, key_off, key_len, &pb, &nb, &lb);
+    key_bytes(refa, k1, k0, buf, extra, l_pos, l_len, arena, key_off, key_len, &pa, &na, &la);
+    key_bytes(refb, k1, k0, buf, extra, l_pos, l_len, arena, key_off, key_len, &pb, &nb, &lb);
     // S/M keys are fully described by (k1, k0): 16 bytes, zero padded
     u8 tmp[16];
     for (int i = 0; i < 8; ++i) { tmp[i] = (u8)(k1 >> (56 - 8 * i)); tmp[8 + i] = (u8)(k0 >> (56 - 8 * i)); }
@@ -465,7 +469,7 @@ __device__ int full_cmp(u64 refa, u64 refb, u64 k1, u64 k0, const u8 *buf, const
 
 __global__ void k_tie_fixup(const u64 *__restrict__ K2, const u64 *__restrict__ K1, const u64 *__restrict__ K0,
                             const u32 *__restrict__ V, u64 n, const u64 *__restrict__ ref, const u8 *buf,
-                            const u64 *l_pos, const u32 *l_len, const u8 *arena, const u64 *key_off,
+                            const u8 *extra, const u64 *l_pos, const u32 *l_len, const u8 *arena, const u64 *key_off,
                             const u32 *key_len, u32 *__restrict__ out) {
     const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -480,7 +484,7 @@ __global__ void k_tie_fixup(const u64 *__restrict__ K2, const u64 *__restrict__ 
     u64 rank = 0;
     for (u64 j = s; j < e; ++j) {
         if (j == i) continue;
-        const int c = full_cmp(ref[V[j]], me, a1, a0, buf, l_pos, l_len, arena, key_off, key_len);
+        const int c = full_cmp(ref[V[j]], me, a1, a0, buf, extra, l_pos, l_len, arena, key_off, key_len);
         if (c < 0 || (c == 0 && j < i)) ++rank;
     }
     out[s + rank] = V[i];
@@ -513,7 +517,7 @@ __global__ void k_blob_len(const u32 *__restrict__ order, u64 n, const u64 *__re
 
 __global__ void k_blob_write(const u32 *__restrict__ order, u64 n, const u64 *__restrict__ ref,
                              const u64 *__restrict__ K1u, const u64 *__restrict__ K0u, const u64 *__restrict__ cnt,
-                             const u8 *buf, const u64 *l_pos, const u32 *l_len, const u8 *arena,
+                             const u8 *buf, const u8 *extra, const u64 *l_pos, const u32 *l_len, const u8 *arena,
                              const u64 *key_off, const u32 *key_len, const u64 *__restrict__ off,
                              u8 *__restrict__ blob, u64 *__restrict__ counts_out) {
     const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
@@ -525,7 +529,7 @@ __global__ void k_blob_write(const u32 *__restrict__ order, u64 n, const u64 *__
     u8 *dst = blob + off[i];
     counts_out[i] = cnt[e];
     if (kind == KIND_L) {
-        const u8 *p = buf + l_pos[idx];
+        const u8 *p = tok_at(buf, extra, l_pos[idx]);
         for (u32 k = 0; k < l_len[idx]; ++k) dst[k] = (u8)lower1(p[k]);
     } else if (kind == KIND_A) {
         const u8 *p = arena + key_off[idx];
@@ -575,12 +579,13 @@ hipError_t msa_launch_artist_key(const u8 *col, const u64 *ar_start, const u64 *
     }
     return hipGetLastError();
 }
-hipError_t msa_launch_long(const u8 *buf, u64 seg_end, const u64 *l_pos, u64 n, u32 *l_len, u64 *l_slot, u64 *ltab,
-                           u64 lmask, u32 *llist, u64 llist_cap, Counters *ctr, hipStream_t s) {
+hipError_t msa_launch_long(const u8 *buf, u64 seg_end, const u8 *extra, u64 extra_len, const u64 *l_pos, u64 n,
+                           u32 *l_len, u64 *l_slot, u64 *ltab, u64 lmask, u32 *llist, u64 llist_cap, Counters *ctr,
+                           hipStream_t s) {
     if (n) {
-        hipLaunchKernelGGL(k_long_insert, grid1(n), dim3(256), 0, s, buf, seg_end, l_pos, n, l_len, l_slot, ltab, lmask,
-                           llist, llist_cap, ctr);
-        hipLaunchKernelGGL(k_long_verify, grid1(n), dim3(256), 0, s, buf, l_pos, (const u32 *)l_len,
+        hipLaunchKernelGGL(k_long_insert, grid1(n), dim3(256), 0, s, buf, seg_end, extra, extra_len, l_pos, n, l_len,
+                           l_slot, ltab, lmask, llist, llist_cap, ctr);
+        hipLaunchKernelGGL(k_long_verify, grid1(n), dim3(256), 0, s, buf, extra, l_pos, (const u32 *)l_len,
                            (const u64 *)l_slot, n, (const u64 *)ltab, ctr);
     }
     return hipGetLastError();
@@ -620,15 +625,15 @@ hipError_t msa_launch_radix_pass(const u64 *K2, const u64 *K1, const u64 *K0, co
     return hipGetLastError();
 }
 hipError_t msa_launch_fixup(const u64 *K2, const u64 *K1, const u64 *K0, const u32 *V, u64 n, const u64 *ref,
-                            const u8 *buf, const u64 *l_pos, const u32 *l_len, const u8 *arena, const u64 *key_off,
+                            const u8 *buf, const u8 *extra, const u64 *l_pos, const u32 *l_len, const u8 *arena, const u64 *key_off,
                             const u32 *key_len, u32 *out, hipStream_t s) {
     if (n)
-        hipLaunchKernelGGL(k_tie_fixup, grid1(n), dim3(256), 0, s, K2, K1, K0, V, n, ref, buf, l_pos, l_len, arena,
+        hipLaunchKernelGGL(k_tie_fixup, grid1(n), dim3(256), 0, s, K2, K1, K0, V, n, ref, buf, extra, l_pos, l_len, arena,
                            key_off, key_len, out);
     return hipGetLastError();
 }
 hipError_t msa_launch_blob(const u32 *order, u64 n, const u64 *ref, const u64 *K1u, const u64 *K0u, const u64 *cnt,
-                           const u8 *buf, const u64 *l_pos, const u32 *l_len, const u8 *arena, const u64 *key_off,
+                           const u8 *buf, const u8 *extra, const u64 *l_pos, const u32 *l_len, const u8 *arena, const u64 *key_off,
                            const u32 *key_len, u64 *len, u64 *off, u64 *bsum, u64 *total, u8 *blob, u64 *counts_out,
                            hipStream_t s, int phase) {
     if (!n) return hipSuccess;
@@ -636,7 +641,7 @@ hipError_t msa_launch_blob(const u32 *order, u64 n, const u64 *ref, const u64 *K
         hipLaunchKernelGGL(k_blob_len, grid1(n), dim3(256), 0, s, order, n, ref, K1u, K0u, l_len, key_len, len);
         return msa_exclusive_scan(len, n, off, bsum, total, s);
     }
-    hipLaunchKernelGGL(k_blob_write, grid1(n), dim3(256), 0, s, order, n, ref, K1u, K0u, cnt, buf, l_pos, l_len, arena,
+    hipLaunchKernelGGL(k_blob_write, grid1(n), dim3(256), 0, s, order, n, ref, K1u, K0u, cnt, buf, extra, l_pos, l_len, arena,
                        key_off, key_len, (const u64 *)off, blob, counts_out);
     return hipGetLastError();
 }

@@ -51,7 +51,6 @@ __global__ __launch_bounds__(256) void k_chunk_summary(const u8 *__restrict__ bu
     const u32 lane = lane_id();
     const u32 gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const u32 nw = (gridDim.x * blockDim.x) >> 6;
-    const u64 lt = (1ull << lane) - 1ull;
     for (u32 c = gw; c < nchunks; c += nw) {
         const u64 cbase = seg_begin + (u64)c * MSA_CHUNK;
         const u64 cend = min(cbase + (u64)MSA_CHUNK, seg_end);
@@ -185,8 +184,11 @@ __global__ __launch_bounds__(FN_THREADS) void k_fn_apply(const ChunkSum *__restr
 #define WAVE_LDS (2048 + 256 + 1024)
 #define K3_LDS (LSLOTS * 12 + K3_WAVES * WAVE_LDS)
 
-template <int MODE>  // 0 = CSV (fields + tokens), 1 = LINES (records only)
+// MODE 0 = CSV (records, fields, lyric tokens), 1 = LINES (records only),
+//      2 = FLAT (every byte is lyric text: tokens only, no record structure)
+template <int MODE>
 __global__ __launch_bounds__(K3_THREADS) void k_scan_main(ScanArgs a) {
+    constexpr bool TOK = MODE != 1;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     u64 *lkey = reinterpret_cast<u64 *>(smem);
     u32 *lcnt = reinterpret_cast<u32 *>(smem + LSLOTS * 8);
@@ -198,7 +200,7 @@ __global__ __launch_bounds__(K3_THREADS) void k_scan_main(ScanArgs a) {
     u16 *starts = reinterpret_cast<u16 *>(wl + 2048 + 256);
     const u64 lt = (1ull << lane) - 1ull;
 
-    if (MODE == 0) {
+    if (TOK) {
         for (u32 i = threadIdx.x; i < LSLOTS; i += K3_THREADS) { lkey[i] = 0; lcnt[i] = 0; }
         __syncthreads();
     }
@@ -211,13 +213,13 @@ __global__ __launch_bounds__(K3_THREADS) void k_scan_main(ScanArgs a) {
         const u64 cbase = a.seg_begin + (u64)c * MSA_CHUNK;
         const u64 cend = min(cbase + (u64)MSA_CHUNK, a.seg_end);
         u32 prevT = 0;
-        if (MODE == 0 && cbase > 0) {
+        if (TOK && cbase > 0) {
             const u32 b = a.buf[cbase - 1];
             prevT = (u32)(((b | 0x20u) >= 'a' && (b | 0x20u) <= 'z') || (b >= '0' && b <= '9') || b == '\'');
         }
         uint4 cur = ld16(a.buf + cbase + lane * 16);
         uint4 nxt = ld16(a.buf + cbase + MSA_ITER + lane * 16);
-        if (MODE == 0) {
+        if (TOK) {
             reinterpret_cast<uint4 *>(ring)[lane] = cur;
             reinterpret_cast<u16 *>(bm)[lane] = (u16)tok16(cur, valid_mask(cbase + lane * 16, a.seg_end));
         }
@@ -226,7 +228,7 @@ __global__ __launch_bounds__(K3_THREADS) void k_scan_main(ScanArgs a) {
             const u64 lpos = ibase + lane * 16;
             const u64 npos = ibase + MSA_ITER;
             uint4 nn = ld16(a.buf + npos + MSA_ITER + lane * 16);  // prefetch it+2
-            if (MODE == 0) {
+            if (TOK) {
                 // stage the following 1 KiB (token continuation only) in the other ring slot
                 const u32 slot = (it + 1) & 1u;
                 reinterpret_cast<uint4 *>(ring)[slot * 64 + lane] = nxt;
@@ -234,6 +236,11 @@ __global__ __launch_bounds__(K3_THREADS) void k_scan_main(ScanArgs a) {
             }
             const u32 vmask = valid_mask(lpos, cend);
             const Classes k = classify16(cur, vmask);
+            const u32 lastb = (u32)(min(ibase + (u64)MSA_ITER, cend) - 1 - ibase);
+            const int Lz = (int)(lastb >> 4);
+            const u32 bz = lastb & 15u;
+            u32 live = (MODE == 2) ? 0xFFFFu : 0u;  // lyric bytes of this lane
+            if (MODE != 2) {
             const u64 B = __ballot(__popc(k.Q) & 1u);
             const u32 pin = st.p ^ (mbcnt(B) & 1u);
             const u32 inq = pxor_excl16(k.Q) ^ (pin ? 0xFFFFu : 0u);
@@ -281,7 +288,7 @@ __global__ __launch_bounds__(K3_THREADS) void k_scan_main(ScanArgs a) {
             u64 rr = st.rec + PT;
             // walk this lane's events (terminators, unquoted commas, NULs)
             u32 E = TERM | Cu | Zm;
-            u32 live = 0, from = 0;
+            u32 from = 0;
             while (E) {
                 const u32 b = __ffs(E) - 1;
                 E &= E - 1;
@@ -312,17 +319,15 @@ __global__ __launch_bounds__(K3_THREADS) void k_scan_main(ScanArgs a) {
             if (MODE == 0 && rr >= 1 && cs >= 3 && !zs) live |= range_mask(from, 16);
 
             // carry to the next iteration (lane 63 has seen every byte)
-            const u32 lastb = (u32)(min(ibase + (u64)MSA_ITER, cend) - 1 - ibase);
-            const int Lz = (int)(lastb >> 4);
-            const u32 bz = lastb & 15u;
             st.p ^= (u32)__popcll(B) & 1u;
             st.cr = (readlane(CRu, Lz) >> bz) & 1u;
             st.c = readlane(cs, 63);
             st.z = readlane(zs, 63);
             st.rec = readlane64(rr, 63);
             st.rs = readlane64(rs, 63);
+            }
 
-            if (MODE == 0) {
+            if (TOK) {
                 // ---- tokens of the lyric field
                 const u32 upT = __shfl_up(k.T, 1);
                 const u32 pt0 = lane ? ((upT >> 15) & 1u) : prevT;
@@ -346,7 +351,7 @@ __global__ __launch_bounds__(K3_THREADS) void k_scan_main(ScanArgs a) {
                     ++words;
                     if (len > 16) {
                         const u64 i = atomicAdd((unsigned long long *)&a.ctr->l_occ, 1ull);
-                        if (i < a.l_cap) a.l_pos[i] = ibase + (o & 1023u);
+                        if (i < a.l_cap) a.l_pos[i] = (ibase + (o & 1023u)) | a.lpos_tag;
                         else atomicOr((unsigned long long *)&a.ctr->overflow, (unsigned long long)OVF_L);
                         continue;
                     }
@@ -385,7 +390,7 @@ __global__ __launch_bounds__(K3_THREADS) void k_scan_main(ScanArgs a) {
             nxt = nn;
         }
     }
-    if (MODE == 0) {
+    if (TOK) {
         words = wave_sum64(words);
         if (lane == 0 && words) atomicAdd((unsigned long long *)&a.ctr->total_words, (unsigned long long)words);
         __syncthreads();
@@ -436,15 +441,14 @@ hipError_t msa_launch_scan(const ScanArgs &a, int mode, hipStream_t s) {
     u32 blocks = (a.nchunks + K3_WAVES - 1) / K3_WAVES;
     u32 cap = (u32)num_cus() * 2;
     if (blocks > cap) blocks = cap;
-    if (mode == 0) {
-        static bool attr = false;
-        if (!attr) {
-            hipFuncSetAttribute((const void *)k_scan_main<0>, hipFuncAttributeMaxDynamicSharedMemorySize, K3_LDS);
-            attr = true;
-        }
-        hipLaunchKernelGGL(k_scan_main<0>, dim3(blocks), dim3(K3_THREADS), K3_LDS, s, a);
-    } else {
-        hipLaunchKernelGGL(k_scan_main<1>, dim3(blocks), dim3(K3_THREADS), 0, s, a);
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void *)k_scan_main<0>, hipFuncAttributeMaxDynamicSharedMemorySize, K3_LDS);
+        (void)hipFuncSetAttribute((const void *)k_scan_main<2>, hipFuncAttributeMaxDynamicSharedMemorySize, K3_LDS);
+        attr = true;
     }
+    if (mode == 0) hipLaunchKernelGGL(k_scan_main<0>, dim3(blocks), dim3(K3_THREADS), K3_LDS, s, a);
+    else if (mode == 2) hipLaunchKernelGGL(k_scan_main<2>, dim3(blocks), dim3(K3_THREADS), K3_LDS, s, a);
+    else hipLaunchKernelGGL(k_scan_main<1>, dim3(blocks), dim3(K3_THREADS), 0, s, a);
     return hipGetLastError();
 }

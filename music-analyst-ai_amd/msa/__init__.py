@@ -1,0 +1,265 @@
+"""ctypes binding of libmsa_hip (include/msa_hip.h) for tests, bench.py and smoke().
+
+The product is C: libmsa_hip.so (gfx950 HIP kernels behind a C ABI) and the
+drop-in CLI bin/parallel_spotify (music-analyst-ai_amd/host/parallel_spotify.c,
+mirroring /root/reference/src/parallel_spotify.c:724-1113).  This module only
+drives that library from Python.  There is no fallback: if libmsa_hip.so is
+missing, or no GPU is visible, every call raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Tuple
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "libmsa_hip.so")
+CLI_PATH = os.path.join(PKG_DIR, "bin", "parallel_spotify")
+GEN_PATH = os.path.join(PKG_DIR, "bin", "msa_gen")
+
+MSA_OK = 0
+MSA_ERR = {
+    -1: "MSA_ERR_ARG",
+    -2: "MSA_ERR_HIP",
+    -3: "MSA_ERR_NOHEADER",
+    -4: "MSA_ERR_BADHEADER",
+    -5: "MSA_ERR_CAPACITY",
+    -6: "MSA_ERR_COLLISION",
+    -7: "MSA_ERR_IO",
+}
+MSA_SPLIT_TEXT_COLUMN = 1
+MSA_TABLE_WORDS = 0
+MSA_TABLE_ARTISTS = 1
+GEN_MODES = {"zipf": 0, "highcard": 1, "torture": 2}
+PROF_MAX = 16
+
+# Every symbol include/msa_hip.h declares (tests check the .so exports them).
+EXPORTS = [
+    "msa_gen_corpus", "msa_free", "msa_create", "msa_destroy", "msa_last_error",
+    "msa_stream", "msa_sync", "msa_load_csv", "msa_bind_csv", "msa_split_columns",
+    "msa_count", "msa_rank", "msa_run", "msa_get_summary", "msa_get_ranked",
+    "msa_write_table_csv", "msa_get_split_column", "msa_shard_function",
+    "msa_shard_set_prefix", "msa_set_profiling", "msa_get_profile",
+]
+
+
+class MsaError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{MSA_ERR.get(code, code)}: {msg}")
+        self.code = code
+
+
+class _GenParams(C.Structure):
+    _fields_ = [
+        ("seed", C.c_uint64),
+        ("n_songs", C.c_uint64),
+        ("vocab", C.c_uint32),
+        ("n_artists", C.c_uint32),
+        ("words_per_song", C.c_uint32),
+        ("mode", C.c_int),
+        ("crlf", C.c_int),
+    ]
+
+
+class _Summary(C.Structure):
+    _fields_ = [
+        ("total_songs", C.c_longlong),
+        ("total_words", C.c_longlong),
+        ("n_words", C.c_uint64),
+        ("n_artists", C.c_uint64),
+        ("n_records", C.c_uint64),
+        ("artist_label", C.c_char * 128),
+        ("text_label", C.c_char * 128),
+        ("artist_file", C.c_char * 128),
+        ("text_file", C.c_char * 128),
+    ]
+
+
+class _Profile(C.Structure):
+    _fields_ = [
+        ("n", C.c_int),
+        ("name", (C.c_char * 32) * PROF_MAX),
+        ("ms", C.c_double * PROF_MAX),
+        ("launches", C.c_uint64 * PROF_MAX),
+        ("bytes", C.c_uint64 * PROF_MAX),
+    ]
+
+
+_lib = None
+
+
+def load(path: str = LIB_PATH):
+    """Load libmsa_hip.so (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise FileNotFoundError(f"{path} not built: run `make -C music-analyst-ai_amd` (or __graft_entry__.build())")
+    lib = C.CDLL(path)
+    vp, sz, u64, i = C.c_void_p, C.c_size_t, C.c_uint64, C.c_int
+    lib.msa_gen_corpus.argtypes = [C.POINTER(_GenParams), C.POINTER(C.c_void_p), C.POINTER(sz)]
+    lib.msa_free.argtypes = [vp]
+    lib.msa_free.restype = None
+    lib.msa_create.argtypes = [i, C.POINTER(vp)]
+    lib.msa_destroy.argtypes = [vp]
+    lib.msa_destroy.restype = None
+    lib.msa_last_error.argtypes = [vp]
+    lib.msa_last_error.restype = C.c_char_p
+    lib.msa_stream.argtypes = [vp]
+    lib.msa_stream.restype = vp
+    lib.msa_sync.argtypes = [vp]
+    lib.msa_load_csv.argtypes = [vp, vp, sz]
+    lib.msa_bind_csv.argtypes = [vp, vp, sz]
+    lib.msa_split_columns.argtypes = [vp, i]
+    lib.msa_count.argtypes = [vp]
+    lib.msa_rank.argtypes = [vp]
+    lib.msa_run.argtypes = [vp, i]
+    lib.msa_get_summary.argtypes = [vp, C.POINTER(_Summary)]
+    lib.msa_get_ranked.argtypes = [vp, i, u64, u64, C.POINTER(C.c_longlong), C.POINTER(u64), C.c_char_p, u64,
+                                   C.POINTER(u64)]
+    lib.msa_write_table_csv.argtypes = [vp, i, C.c_char_p, C.c_char_p, i]
+    lib.msa_get_split_column.argtypes = [vp, i, C.POINTER(C.c_void_p), C.POINTER(sz)]
+    lib.msa_shard_function.argtypes = [vp, vp]
+    lib.msa_shard_set_prefix.argtypes = [vp, vp, i]
+    lib.msa_set_profiling.argtypes = [vp, i]
+    lib.msa_get_profile.argtypes = [vp, C.POINTER(_Profile), i]
+    _lib = lib
+    return lib
+
+
+def gen_corpus(n_songs: int, mode: str = "zipf", seed: int = 1, vocab: int = 50000, n_artists: int = 5000,
+               words_per_song: int = 30, crlf: bool = False) -> bytes:
+    """Deterministic synthetic corpus (csrc/msa_gen.c) -- host code, no GPU."""
+    lib = load()
+    p = _GenParams(seed, n_songs, vocab, n_artists, words_per_song, GEN_MODES[mode], int(crlf))
+    out = C.c_void_p()
+    n = C.c_size_t()
+    rc = lib.msa_gen_corpus(C.byref(p), C.byref(out), C.byref(n))
+    if rc:
+        raise MsaError(rc, "corpus generation failed")
+    try:
+        return C.string_at(out, n.value)
+    finally:
+        lib.msa_free(out)
+
+
+@dataclass
+class Summary:
+    total_songs: int
+    total_words: int
+    n_words: int
+    n_artists: int
+    n_records: int
+    artist_label: bytes
+    text_label: bytes
+    artist_file: str
+    text_file: str
+
+
+class Context:
+    """One msa_ctx: one GPU, one HIP stream (msa_create / msa_destroy)."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load()
+        h = C.c_void_p()
+        rc = self.lib.msa_create(device, C.byref(h))
+        if rc:
+            raise MsaError(rc, f"msa_create(device={device}) failed (no GPU visible?)")
+        self.h = h
+
+    def close(self):
+        if self.h:
+            self.lib.msa_destroy(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _check(self, rc: int):
+        if rc:
+            raise MsaError(rc, (self.lib.msa_last_error(self.h) or b"").decode(errors="replace"))
+
+    @property
+    def stream(self) -> int:
+        return self.lib.msa_stream(self.h) or 0
+
+    def load_csv(self, data: bytes):
+        self._check(self.lib.msa_load_csv(self.h, data, len(data)))
+
+    def bind_csv(self, dev_ptr: int, n: int):
+        self._check(self.lib.msa_bind_csv(self.h, C.c_void_p(dev_ptr), n))
+
+    def split_columns(self, text_column: bool = True):
+        self._check(self.lib.msa_split_columns(self.h, MSA_SPLIT_TEXT_COLUMN if text_column else 0))
+
+    def count(self):
+        self._check(self.lib.msa_count(self.h))
+
+    def rank(self):
+        self._check(self.lib.msa_rank(self.h))
+
+    def run(self, text_column: bool = True):
+        self._check(self.lib.msa_run(self.h, MSA_SPLIT_TEXT_COLUMN if text_column else 0))
+
+    def sync(self):
+        self._check(self.lib.msa_sync(self.h))
+
+    def set_profiling(self, on: bool = True):
+        self._check(self.lib.msa_set_profiling(self.h, int(on)))
+
+    def profile(self, reset: bool = False) -> Dict[str, dict]:
+        """HIP-event time per pipeline stage, accumulated since the last reset."""
+        p = _Profile()
+        self._check(self.lib.msa_get_profile(self.h, C.byref(p), int(reset)))
+        out = {}
+        for k in range(p.n):
+            out[p.name[k].value.decode()] = {"ms": p.ms[k], "launches": p.launches[k], "bytes": p.bytes[k]}
+        return out
+
+    def summary(self) -> Summary:
+        s = _Summary()
+        self._check(self.lib.msa_get_summary(self.h, C.byref(s)))
+        return Summary(s.total_songs, s.total_words, s.n_words, s.n_artists, s.n_records, s.artist_label,
+                       s.text_label, s.artist_file.decode(), s.text_file.decode())
+
+    def ranked(self, table: int, first: int = 0, count: Optional[int] = None) -> List[Tuple[bytes, int]]:
+        s = self.summary()
+        n = s.n_words if table == MSA_TABLE_WORDS else s.n_artists
+        if count is None:
+            count = max(0, n - first)
+        count = min(count, max(0, n - first))
+        need = C.c_uint64()
+        self._check(self.lib.msa_get_ranked(self.h, table, first, count, None, None, None, 0, C.byref(need)))
+        counts = (C.c_longlong * max(count, 1))()
+        offs = (C.c_uint64 * (count + 1))()
+        keys = C.create_string_buffer(need.value + 1)
+        self._check(self.lib.msa_get_ranked(self.h, table, first, count, counts, offs, keys, need.value + 1,
+                                            C.byref(need)))
+        raw = keys.raw
+        return [(raw[offs[i]:offs[i + 1]], counts[i]) for i in range(count)]
+
+    def write_table_csv(self, table: int, path: str, key_header: str, limit: int = 0):
+        self._check(self.lib.msa_write_table_csv(self.h, table, path.encode(), key_header.encode(), limit))
+
+    def split_column(self, which: int) -> bytes:
+        out = C.c_void_p()
+        n = C.c_size_t()
+        self._check(self.lib.msa_get_split_column(self.h, which, C.byref(out), C.byref(n)))
+        try:
+            return C.string_at(out, n.value)
+        finally:
+            self.lib.msa_free(out)
+
+
+def table_csv_bytes(entries: List[Tuple[bytes, int]], key_header: str, limit: int = 0) -> bytes:
+    """write_table_csv's byte format (parallel_spotify.c:307-344) for a ranked list."""
+    if limit > 0:
+        entries = entries[:limit]
+    out = [key_header.encode() + b",count\n"]
+    for k, c in entries:
+        out.append(b'"' + k.replace(b'"', b'""') + b'",' + str(c).encode() + b"\n")
+    return b"".join(out)

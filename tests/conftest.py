@@ -1,0 +1,71 @@
+"""Shared test helpers.
+
+CPU tests (`-m "not gpu"`) check the oracle against the golden vectors made by
+the REAL reference (tests/golden/), the host logic and the C ABI surface.
+GPU tests (`-m gpu`) run libmsa_hip on an MI355X and compare it byte-for-byte
+with the oracle / golden vectors.  The oracle (oracle/msa_oracle) is only ever
+used here as the checker.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "music-analyst-ai_amd")
+GOLDEN = os.path.join(REPO, "tests", "golden")
+ORACLE = os.path.join(REPO, "oracle", "msa_oracle")
+REF_BIN = os.path.join(REPO, "oracle", "_ref", "parallel_spotify")
+MPIRUN = "/opt/conda/bin/mpirun"
+
+if PKG not in sys.path:
+    sys.path.insert(0, PKG)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs libmsa_hip kernels)")
+
+
+def _read(path):
+    with open(path, "rb") as f:
+        return f.read()
+
+
+def read_outputs(outdir):
+    """The files a parallel_spotify run leaves in its --output-dir."""
+    out = {
+        "word_counts.csv": _read(os.path.join(outdir, "word_counts.csv")),
+        "top_artists.csv": _read(os.path.join(outdir, "top_artists.csv")),
+        "split": {},
+    }
+    sd = os.path.join(outdir, "split_columns")
+    if os.path.isdir(sd):
+        for n in sorted(os.listdir(sd)):
+            out["split"][n] = _read(os.path.join(sd, n))
+    with open(os.path.join(outdir, "performance_metrics.json")) as f:
+        m = json.load(f)
+    out["metrics"] = {k: m[k] for k in ("processes", "total_songs", "total_words")}
+    return out
+
+
+def run_oracle(csv_path, outdir, ranks=1, word_limit=0, artist_limit=0):
+    """The CPU oracle (C restatement of parallel_spotify.c, virtual np)."""
+    if not os.path.exists(ORACLE):
+        pytest.skip("oracle not built (make -C oracle)")
+    cmd = [ORACLE, csv_path, "--output-dir", outdir, "--ranks", str(ranks)]
+    if word_limit:
+        cmd += ["--word-limit", str(word_limit)]
+    if artist_limit:
+        cmd += ["--artist-limit", str(artist_limit)]
+    p = subprocess.run(cmd, capture_output=True, timeout=300)
+    return p
+
+
+@pytest.fixture(scope="session")
+def msa_mod():
+    import msa
+
+    msa.load()
+    return msa

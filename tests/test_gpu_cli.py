@@ -1,0 +1,53 @@
+"""GPU: the drop-in CLI (music-analyst-ai_amd/bin/parallel_spotify, the C host
+over libmsa_hip) against the reference's own outputs -- same files, same bytes,
+same stdout (parallel_spotify.c:1027-1053)."""
+import json
+import os
+import subprocess
+
+import pytest
+
+from conftest import GOLDEN, PKG, read_outputs
+from test_oracle import CASES, golden
+
+pytestmark = pytest.mark.gpu
+CLI = os.path.join(PKG, "bin", "parallel_spotify")
+
+
+@pytest.mark.parametrize("case", [c for c in CASES if c.startswith(("zipf", "torture", "multiline", "nul", "long"))])
+def test_cli_matches_reference(case, tmp_path):
+    res, files = golden(case, 1)
+    out = tmp_path / "out"
+    p = subprocess.run([CLI, os.path.join(GOLDEN, case, "input.csv"), "--output-dir", str(out)],
+                       capture_output=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    got = read_outputs(str(out))
+    assert got["metrics"] == {k: res[k] for k in ("processes", "total_songs", "total_words")}
+    assert got["word_counts.csv"] == files["word_counts.csv"]
+    assert got["top_artists.csv"] == files["top_artists.csv"]
+    assert got["split"] == files["split"]
+    assert p.stdout.decode("latin-1") == res["stdout"]
+    m = json.load(open(out / "performance_metrics.json"))
+    assert set(m) == {"processes", "total_songs", "total_words", "compute_time", "total_time"}
+
+
+def test_cli_limits(tmp_path):
+    case = "zipf_small"
+    res, files = golden(case, 1)
+    out = tmp_path / "out"
+    p = subprocess.run([CLI, os.path.join(GOLDEN, case, "input.csv"), "--output-dir", str(out),
+                        "--word-limit", "7", "--artist-limit", "3"], capture_output=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    w = open(out / "word_counts.csv", "rb").read()
+    a = open(out / "top_artists.csv", "rb").read()
+    assert w == b"\n".join(files["word_counts.csv"].split(b"\n")[:8]) + b"\n"
+    assert a == b"\n".join(files["top_artists.csv"].split(b"\n")[:4]) + b"\n"
+
+
+@pytest.mark.parametrize("case,msg", [("empty_file", b"Dataset does not contain a header row"),
+                                      ("bad_header", b"Unable to parse dataset header")])
+def test_cli_errors(case, msg, tmp_path):
+    p = subprocess.run([CLI, os.path.join(GOLDEN, case, "input.csv"), "--output-dir", str(tmp_path / "o")],
+                       capture_output=True, timeout=120)
+    assert p.returncode != 0
+    assert msg in p.stderr

@@ -1,0 +1,132 @@
+"""GPU parity: libmsa_hip (gfx950 kernels, called through the C ABI) against the
+CPU oracle on the same inputs -- byte-identical word_counts.csv, top_artists.csv,
+split column files and totals (reference semantics of `mpirun -np 1`,
+/root/reference/src/parallel_spotify.c)."""
+import os
+
+import pytest
+
+from conftest import read_outputs, run_oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx(msa_mod):
+    c = msa_mod.Context(0)
+    yield c
+    c.close()
+
+
+def gpu_outputs(msa, ctx, data):
+    ctx.load_csv(data)
+    ctx.run(text_column=True)
+    s = ctx.summary()
+    out = {
+        "word_counts.csv": msa.table_csv_bytes(ctx.ranked(msa.MSA_TABLE_WORDS), "word"),
+        "top_artists.csv": msa.table_csv_bytes(ctx.ranked(msa.MSA_TABLE_ARTISTS), "artist"),
+        "split": {s.artist_file + ".csv": ctx.split_column(0), s.text_file + ".csv": ctx.split_column(1)},
+        "metrics": {"processes": 1, "total_songs": s.total_songs, "total_words": s.total_words},
+    }
+    return out
+
+
+def check_against_oracle(msa, ctx, data, tmp_path, name):
+    p = tmp_path / f"{name}.csv"
+    p.write_bytes(data)
+    od = tmp_path / f"orc_{name}"
+    r = run_oracle(str(p), str(od), ranks=1)
+    assert r.returncode == 0, r.stderr
+    exp = read_outputs(str(od))
+    got = gpu_outputs(msa, ctx, data)
+    assert got["metrics"] == exp["metrics"]
+    assert sorted(got["split"]) == sorted(exp["split"])
+    for k in exp["split"]:
+        assert got["split"][k] == exp["split"][k], f"split column {k} differs"
+    for k in ("word_counts.csv", "top_artists.csv"):
+        if got[k] != exp[k]:
+            gl, el = got[k].split(b"\n"), exp[k].split(b"\n")
+            first = next((i for i, (a, b) in enumerate(zip(gl, el)) if a != b), min(len(gl), len(el)))
+            pytest.fail(f"{k} differs at line {first}: gpu={gl[first:first + 3]} oracle={el[first:first + 3]} "
+                        f"(lines {len(gl)} vs {len(el)})")
+
+
+@pytest.mark.parametrize("seed", list(range(1, 13)))
+def test_torture(msa_mod, ctx, tmp_path, seed):
+    data = msa_mod.gen_corpus(1500, mode="torture", seed=seed)
+    check_against_oracle(msa_mod, ctx, data, tmp_path, f"torture{seed}")
+
+
+@pytest.mark.parametrize("mode,songs,crlf", [("zipf", 3000, False), ("zipf", 2000, True), ("highcard", 3000, False)])
+def test_small_corpora(msa_mod, ctx, tmp_path, mode, songs, crlf):
+    data = msa_mod.gen_corpus(songs, mode=mode, seed=7, vocab=20000, n_artists=500, crlf=crlf)
+    check_against_oracle(msa_mod, ctx, data, tmp_path, f"{mode}{songs}{int(crlf)}")
+
+
+@pytest.mark.parametrize("mode", ["zipf", "highcard"])
+def test_medium_corpora(msa_mod, ctx, tmp_path, mode):
+    """~40-60 MB: many chunks, many waves, real hash-table pressure."""
+    data = msa_mod.gen_corpus(200_000, mode=mode, seed=21)
+    check_against_oracle(msa_mod, ctx, data, tmp_path, f"{mode}_medium")
+
+
+EDGE = {
+    "header_only": b"artist,song,link,text\n",
+    "header_no_newline": b"artist,song,link,text",
+    "no_trailing_newline": b"artist,song,link,text\nA,s,l,\"hello world again\"",
+    "cr_only": b"artist,song,link,text\rA,s,l,one two three\rB,s,l,\"four five\rsix\"\r",
+    "short_records": b"a,b,c,d\nonly,two\n\n,,,\nX,y,z,alpha beta\n",
+    "nul_bytes": b"a,b,c,d\nA\x00B,s,l,zero one\nC,s,l,two\x00three four\nD,s\x00,l,five six\n",
+    "long_words": b"a,b,c,d\nA,s,l,\"" + b"x" * 17 + b" " + b"Y" * 300 + b" supercalifragilistic supercalifragilistic\"\n",
+    "shared_prefix_ties": b"a,b,c,d\n" + b"".join(
+        b"A,s,l,abcdefghijklmnop%s\n" % s for s in [b"zz", b"z", b"zzz", b"a", b"b", b"abc", b"z\x27"]),
+    "multiline_text_header": b"a,b,c,\"multi\nline, header\"\nA,s,l,words here\n",
+    "multiline_artist_header": b"\"art\nist, name\",b,c,d\nA,s,l,words here\nB,s,l,more\n",
+    "quotes_everywhere": b"a,b,c,d\n\"A \"\"x\"\"\",s,l,\"say \"\"hi\"\" now\"\nB\"q,s,l,open quote\n\"z\n",
+    "apostrophes": b"a,b,c,d\nA,s,l,''' '' 'tis rock'n'roll don't O'NEIL\n",
+    "whitespace_fields": b"a,b,c,d\n  A  ,s,l,   \t  \n\t,s,l, x y z \n",
+    "utf8": "a,b,c,d\nBeyoncé,s,l,café naïve über straße\n".encode(),
+}
+
+
+@pytest.mark.parametrize("name", sorted(EDGE))
+def test_edge_cases(msa_mod, ctx, tmp_path, name):
+    check_against_oracle(msa_mod, ctx, EDGE[name], tmp_path, name)
+
+
+def test_empty_file_fails_loudly(msa_mod, ctx):
+    ctx.load_csv(b"")
+    with pytest.raises(msa_mod.MsaError) as e:
+        ctx.run()
+    assert e.value.code == -3  # MSA_ERR_NOHEADER
+
+
+def test_bad_header_fails_loudly(msa_mod, ctx):
+    ctx.load_csv(b"a,b\nA,s,l,x\n")
+    with pytest.raises(msa_mod.MsaError) as e:
+        ctx.run()
+    assert e.value.code == -4  # MSA_ERR_BADHEADER
+
+
+# ---------------------------------------------------------------- golden vectors
+from test_oracle import CASES as GOLDEN_CASES, golden  # noqa: E402
+
+
+@pytest.mark.parametrize("case", GOLDEN_CASES)
+def test_golden_reference_np1(msa_mod, ctx, case):
+    """Byte-identical to the REAL reference (`mpirun -np 1`) on its own outputs."""
+    from conftest import GOLDEN
+
+    res, files = golden(case, 1)
+    data = open(os.path.join(GOLDEN, case, "input.csv"), "rb").read()
+    if res["returncode"] != 0:
+        ctx.load_csv(data)
+        with pytest.raises(msa_mod.MsaError) as e:
+            ctx.run()
+        assert e.value.code in (-3, -4)
+        return
+    got = gpu_outputs(msa_mod, ctx, data)
+    assert got["metrics"] == {k: res[k] for k in ("processes", "total_songs", "total_words")}
+    assert got["word_counts.csv"] == files["word_counts.csv"]
+    assert got["top_artists.csv"] == files["top_artists.csv"]
+    assert got["split"] == files["split"]
