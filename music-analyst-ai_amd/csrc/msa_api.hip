@@ -22,12 +22,10 @@ hipError_t msa_launch_fn(const ChunkSum *, u64, u32, Fn *, Fn *, const State *, 
                          bool);
 hipError_t msa_launch_scan(const ScanArgs &, int, hipStream_t);
 hipError_t msa_exclusive_scan(const u64 *, u64, u64 *, u64 *, u64 *, hipStream_t);
-hipError_t msa_launch_artist_len(const u8 *, const u64 *, const u32 *, const u32 *, u64, u64 *, hipStream_t);
-hipError_t msa_launch_artist_write(const u8 *, const u64 *, const u32 *, const u32 *, u64, const u64 *, u64, u8 *,
-                                   hipStream_t);
-hipError_t msa_launch_text_len(const u8 *, const u64 *, const u64 *, const u32 *, const u32 *, u64, u64 *, hipStream_t);
-hipError_t msa_launch_text_write(const u8 *, const u64 *, const u64 *, const u32 *, const u32 *, u64, const u64 *, u64,
-                                 u8 *, hipStream_t);
+hipError_t msa_launch_col_span(int, const u8 *, const u64 *, const u64 *, const u32 *, const u32 *, const u32 *, u64,
+                               u64 *, u64 *, u32 *, hipStream_t);
+hipError_t msa_launch_col_write(const u8 *, const u64 *, const u64 *, const u64 *, const u32 *, u64, u64, u8 *, int,
+                                hipStream_t);
 hipError_t msa_launch_artist_key(const u8 *, const u64 *, const u64 *, u64, u8 *, u64 *, u32 *, u64 *, u64 *, u64,
                                  u32 *, u64, Counters *, hipStream_t);
 hipError_t msa_launch_long(const u8 *, u64, const u8 *, u64, const u64 *, u64, u32 *, u64 *, u64 *, u64, u32 *, u64,
@@ -116,7 +114,9 @@ struct msa_ctx {
     DevBuf extra;
     u64 extra_len = 0;
     // columns
-    DevBuf acol, alen, aoff, tcol, tlen, toff, scan_bsum, scan_total;
+    DevBuf acol, alen, aoff, asrc, apairs, tcol, tlen, toff, tsrc, tpairs, scan_bsum, scan_total;
+    int cus = 256;
+    int ablate = 0;  // MSA_ABLATE: diagnostic kernel ablations (results invalid)
     u64 acol_len = 0, a_hdr_getline = 0, tcol_len = 0;
     bool have_tcol = false;
     // artist.csv records + keys
@@ -126,7 +126,12 @@ struct msa_ctx {
     DevBuf s_tab, s_list, m_tab, m_list, l_pos, l_len, l_slot, l_tab, l_list, a_tab, a_list;
     u64 s_slots = 0, m_slots = 0, l_occ_cap = 0, lt_slots = 0, a_slots = 0;
     u64 s_used_prev = 0, m_used_prev = 0, lt_used_prev = 0, a_used_prev = 0;
-    u64 cap_scale = 1;
+    // Table capacities (log2 slots / occurrence capacity).  They start small --
+    // a table that fits the Infinity Cache is much faster than one sized for
+    // the worst case -- and grow only when a run reports an overflow of that
+    // table (msa_run retries); the grown size is kept for later runs.
+    u32 s_log2 = 0, m_log2 = 0, lt_log2 = 0, a_log2 = 0;
+    u64 l_occ_want = 0;
     // counters
     DevBuf ctr;
     Counters h_ctr{};
@@ -293,16 +298,27 @@ static int run_scan_fn(msa_ctx *c, const u8 *buf, u64 b, u64 e, State init, Stat
     return MSA_OK;
 }
 
+static u32 log2_ceil(u64 v) {
+    u32 k = 0;
+    while ((1ull << k) < v) ++k;
+    return k;
+}
+
 static int ensure_tables(msa_ctx *c) {
-    // Capacities scale with the input; the tables are zeroed once and, after
-    // each run, only the claimed slots are cleared again (no per-run memset
-    // of the whole table).
+    // Tables are zeroed once at allocation; after each run only the claimed
+    // slots are cleared again (no per-run memset of a whole table).
     const u64 n = c->n;
-    u64 s_slots = next_pow2(std::max<u64>(1ull << 20, std::min<u64>(n / 16, 1ull << 28)) * c->cap_scale);
-    u64 m_slots = next_pow2(std::max<u64>(1ull << 18, std::min<u64>(n / 64, 1ull << 27)) * c->cap_scale);
-    u64 l_occ = std::max<u64>(1ull << 18, n / 512) * c->cap_scale;
-    u64 lt_slots = next_pow2(l_occ * 2);
-    u64 a_slots = next_pow2(std::max<u64>(1ull << 16, (c->nrec + 1) * 2));
+    // distinct keys can never exceed tokens (<= n/4) / records: cap the growth there
+    const u32 cap_s = std::max<u32>(16, log2_ceil(n / 2 + 1));
+    if (!c->s_log2) c->s_log2 = std::min<u32>(20, cap_s);
+    if (!c->m_log2) c->m_log2 = std::min<u32>(18, cap_s);
+    if (!c->lt_log2) c->lt_log2 = std::min<u32>(16, cap_s);
+    if (!c->l_occ_want) c->l_occ_want = std::max<u64>(1ull << 16, n / 1024);
+    const u32 a_need = log2_ceil(std::max<u64>(1ull << 12, 2 * (c->nrec + 1)));
+    if (!c->a_log2) c->a_log2 = std::min<u32>(16, a_need);
+    const u64 s_slots = 1ull << c->s_log2, m_slots = 1ull << c->m_log2, lt_slots = 1ull << c->lt_log2;
+    const u64 a_slots = 1ull << c->a_log2;
+    const u64 l_occ = c->l_occ_want;
     if (s_slots != c->s_slots) {
         release(c->s_tab);
         HIPC(c, ensure(c->s_tab, s_slots * 16, true));
@@ -330,7 +346,7 @@ static int ensure_tables(msa_ctx *c) {
         c->lt_slots = lt_slots;
         c->lt_used_prev = 0;
     }
-    if (a_slots > c->a_slots) {
+    if (a_slots != c->a_slots) {
         release(c->a_tab);
         HIPC(c, ensure(c->a_tab, a_slots * 32, true));
         HIPC(c, ensure(c->a_list, (a_slots / 2) * 4));
@@ -338,6 +354,23 @@ static int ensure_tables(msa_ctx *c) {
         c->a_used_prev = 0;
     }
     return MSA_OK;
+}
+
+// After an overflow: grow exactly the tables that overflowed, to at least
+// twice what the failed run claimed (claim counters keep counting past the
+// list capacity), and at least 8x.
+static void grow_tables(msa_ctx *c) {
+    const u64 f = c->h_ctr.overflow;
+    auto grow = [](u32 &lg, u64 claimed) {
+        const u32 want = log2_ceil(std::max<u64>(claimed * 4, 1));
+        lg = std::max<u32>(lg + 3, want);
+        if (lg > 31) lg = 31;  // slot lists hold u32 indices
+    };
+    if (f & OVF_S) grow(c->s_log2, c->h_ctr.s_claimed);
+    if (f & OVF_M) grow(c->m_log2, c->h_ctr.m_claimed);
+    if (f & OVF_LT) grow(c->lt_log2, c->h_ctr.l_claimed);
+    if (f & OVF_A) grow(c->a_log2, c->h_ctr.a_claimed);
+    if (f & OVF_L) c->l_occ_want = std::max<u64>(c->l_occ_want * 8, c->h_ctr.l_occ * 2);
 }
 
 // clear only the slots the previous run claimed
@@ -376,18 +409,17 @@ static int sync_counters(msa_ctx *c) {
 
 // ------------------------------------------------------------------ stage 1
 static int materialise_column(msa_ctx *c, bool text, const std::string &hdr_line, DevBuf &col, DevBuf &lenb,
-                              DevBuf &offb, u64 *col_len) {
+                              DevBuf &offb, DevBuf &srcb, DevBuf &pairsb, u64 *col_len) {
     const u64 nrec = c->nrec;
     HIPC(c, ensure(lenb, nrec * 8));
     HIPC(c, ensure(offb, nrec * 8));
     HIPC(c, ensure(c->scan_bsum, ((nrec + 1023) / 1024 + 1) * 8));
     HIPC(c, ensure(c->scan_total, 64));
-    if (text)
-        HIPC(c, msa_launch_text_len(c->in, c->rec_start.as<u64>(), c->rec_term.as<u64>(), c->f3rel.as<u32>(),
-                                    c->nulrel.as<u32>(), nrec, lenb.as<u64>(), c->stream));
-    else
-        HIPC(c, msa_launch_artist_len(c->in, c->rec_start.as<u64>(), c->f0rel.as<u32>(), c->f3rel.as<u32>(), nrec,
-                                      lenb.as<u64>(), c->stream));
+    HIPC(c, ensure(srcb, nrec * 8));
+    HIPC(c, ensure(pairsb, nrec * 4));
+    HIPC(c, msa_launch_col_span(text ? 1 : 0, c->in, c->rec_start.as<u64>(), c->rec_term.as<u64>(), c->f0rel.as<u32>(),
+                                c->f3rel.as<u32>(), c->nulrel.as<u32>(), nrec, lenb.as<u64>(), srcb.as<u64>(),
+                                pairsb.as<u32>(), c->stream));
     HIPC(c, msa_exclusive_scan(lenb.as<u64>(), nrec, offb.as<u64>(), c->scan_bsum.as<u64>(), c->scan_total.as<u64>(),
                                c->stream));
     u64 body = 0;
@@ -397,13 +429,8 @@ static int materialise_column(msa_ctx *c, bool text, const std::string &hdr_line
     HIPC(c, ensure(col, total + MSA_INPUT_PAD));
     HIPC(c, hipMemcpyAsync(col.p, hdr_line.data(), hdr_line.size(), hipMemcpyHostToDevice, c->stream));
     HIPC(c, hipMemsetAsync(col.as<char>() + total, 0, MSA_INPUT_PAD, c->stream));
-    if (text)
-        HIPC(c, msa_launch_text_write(c->in, c->rec_start.as<u64>(), c->rec_term.as<u64>(), c->f3rel.as<u32>(),
-                                      c->nulrel.as<u32>(), nrec, offb.as<u64>(), hdr_line.size(), col.as<u8>(),
-                                      c->stream));
-    else
-        HIPC(c, msa_launch_artist_write(c->in, c->rec_start.as<u64>(), c->f0rel.as<u32>(), c->f3rel.as<u32>(), nrec,
-                                        offb.as<u64>(), hdr_line.size(), col.as<u8>(), c->stream));
+    HIPC(c, msa_launch_col_write(c->in, lenb.as<u64>(), offb.as<u64>(), srcb.as<u64>(), pairsb.as<u32>(), nrec,
+                                 hdr_line.size(), col.as<u8>(), c->cus, c->stream));
     *col_len = total;
     return MSA_OK;
 }
@@ -459,6 +486,7 @@ static int do_split(msa_ctx *c, int flags) {
     a.l_cap = c->l_occ_cap;
     a.ctr = c->ctr.as<Counters>();
     a.want_term = want_text ? 1 : 0;
+    a.ablate = c->ablate;
     prof_begin(c, ST_CSV_SCAN);
     HIPC(c, msa_launch_scan(a, 0, c->stream));
     // algorithmic bytes: every CSV byte once + the per-record SoA it writes
@@ -517,7 +545,7 @@ static int do_split(msa_ctx *c, int flags) {
     std::string ah = c->sum.artist_label[0] ? c->sum.artist_label : "Artists";
     ah.push_back('\n');
     prof_begin(c, ST_ARTIST_COLUMN);
-    if ((rc = materialise_column(c, false, ah, c->acol, c->alen, c->aoff, &c->acol_len))) return rc;
+    if ((rc = materialise_column(c, false, ah, c->acol, c->alen, c->aoff, c->asrc, c->apairs, &c->acol_len))) return rc;
     prof_end(c, ST_ARTIST_COLUMN, c->acol_len * 2 + c->nrec * 32);
     {
         size_t p = ah.find('\n');
@@ -528,7 +556,7 @@ static int do_split(msa_ctx *c, int flags) {
         std::string th = c->sum.text_label[0] ? c->sum.text_label : "Texts";
         th.push_back('\n');
         prof_begin(c, ST_TEXT_COLUMN);
-        if ((rc = materialise_column(c, true, th, c->tcol, c->tlen, c->toff, &c->tcol_len))) return rc;
+        if ((rc = materialise_column(c, true, th, c->tcol, c->tlen, c->toff, c->tsrc, c->tpairs, &c->tcol_len))) return rc;
         prof_end(c, ST_TEXT_COLUMN, c->tcol_len * 2 + c->nrec * 40);
         c->have_tcol = true;
     }
@@ -748,6 +776,12 @@ int msa_create(int device, msa_ctx **out) {
     if (hipSetDevice(device) != hipSuccess) return MSA_ERR_HIP;
     msa_ctx *c = new msa_ctx();
     c->device = device;
+    if (const char *ab = getenv("MSA_ABLATE")) c->ablate = atoi(ab);
+    {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+            c->cus = prop.multiProcessorCount;
+    }
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return MSA_ERR_HIP;
@@ -761,7 +795,7 @@ void msa_destroy(msa_ctx *c) {
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     DevBuf *all[] = {&c->in_own, &c->sums, &c->carry, &c->runpre, &c->small, &c->rec_start, &c->rec_term, &c->extra,
-                     &c->f0rel, &c->f3rel, &c->nulrel, &c->acol, &c->alen, &c->aoff, &c->tcol, &c->tlen, &c->toff,
+                     &c->f0rel, &c->f3rel, &c->nulrel, &c->acol, &c->alen, &c->aoff, &c->asrc, &c->apairs, &c->tcol, &c->tlen, &c->toff, &c->tsrc, &c->tpairs,
                      &c->scan_bsum, &c->scan_total, &c->ar_start, &c->ar_term, &c->arena, &c->key_off,
                      &c->key_len, &c->key_slot, &c->s_tab, &c->s_list, &c->m_tab, &c->m_list, &c->l_pos, &c->l_len,
                      &c->l_slot, &c->l_tab, &c->l_list, &c->a_tab, &c->a_list, &c->ctr};
@@ -833,11 +867,11 @@ int msa_run(msa_ctx *c, int flags) {
     if (!c) return MSA_ERR_ARG;
     HIPC(c, hipSetDevice(c->device));
     int rc = MSA_OK;
-    for (int attempt = 0; attempt < 4; ++attempt) {
+    for (int attempt = 0; attempt < 8; ++attempt) {
         rc = do_split(c, flags);
         if (!rc) rc = do_count(c);
-        if (rc == MSA_ERR_CAPACITY) {
-            c->cap_scale *= 4;
+        if (rc == MSA_ERR_CAPACITY && c->h_ctr.overflow) {
+            grow_tables(c);
             continue;
         }
         break;

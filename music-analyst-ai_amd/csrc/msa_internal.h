@@ -263,6 +263,7 @@ struct ScanArgs {
     u64 lpos_tag;    // OR'ed into recorded long-token positions (MSA_POS_EXTRA: the side buffer)
     Counters *ctr;
     int want_term;
+    int ablate;      // diagnostic builds only (MSA_ABLATE env): see msa_scan.hip
 };
 
 // A long-token position with this bit set indexes the context's side buffer

@@ -141,91 +141,141 @@ __device__ Span dup_field(const u8 *f, u64 len, int preserve, u8 *out) {
     return r;
 }
 
-// Length of artist.csv line r: |dup_field(field 0, preserve)| + 1, 0 if the
-// record is skipped (record 0 = header, or fewer than 3 commas before a NUL).
-__global__ void k_artist_len(const u8 *__restrict__ buf, const u64 *__restrict__ rec_start,
-                             const u32 *__restrict__ f0rel, const u32 *__restrict__ f3rel, u64 nrec,
-                             u64 *__restrict__ line_len) {
+// Column lines (split_dataset_columns, parallel_spotify.c:699-714): line r is
+// duplicate_field(field, preserve=1) + '\n'.  After the outer trim a quoted
+// field -- every lyric of the real corpus -- is copied raw; an unquoted one
+// has its "" pairs collapsed, and needs no second trim (its first and last
+// bytes are non-space and a collapsed pair yields '"').  k_col_span records
+// (source, pairs) per record; k_col_write copies one record per wave with
+// coalesced byte lanes (the collapsing copy, rare, runs on one lane).
+template <int TEXT>
+__global__ __launch_bounds__(256) void k_col_span(const u8 *__restrict__ buf, const u64 *__restrict__ rec_start,
+                                                  const u64 *__restrict__ rec_term, const u32 *__restrict__ f0rel,
+                                                  const u32 *__restrict__ f3rel, const u32 *__restrict__ nulrel,
+                                                  u64 nrec, u64 *__restrict__ line_len, u64 *__restrict__ span_src,
+                                                  u32 *__restrict__ span_pairs) {
     const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= nrec) return;
-    u64 L = 0;
-    if (r >= 1 && f3rel[r]) {
-        const Span sp = dup_field(buf + rec_start[r], f0rel[r] - 1u, 1, nullptr);
-        L = sp.len + 1;
+    if (r == 0 || !f3rel[r]) {  // header, or a record parse_csv_line rejects
+        line_len[r] = 0;
+        return;
     }
-    line_len[r] = L;
-}
-
-__global__ void k_artist_write(const u8 *__restrict__ buf, const u64 *__restrict__ rec_start,
-                               const u32 *__restrict__ f0rel, const u32 *__restrict__ f3rel, u64 nrec,
-                               const u64 *__restrict__ line_off, u64 hdr_len, u8 *__restrict__ col) {
-    const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= nrec || r == 0 || !f3rel[r]) return;
-    u8 *dst = col + hdr_len + line_off[r];
-    const Span sp = dup_field(buf + rec_start[r], f0rel[r] - 1u, 1, dst);
-    dst[sp.len] = '\n';
-}
-
-// text.csv line of record r: dup_field(field 3 up to NUL / record end, preserve)
-__device__ __forceinline__ u64 text_field_len(const u64 *rec_start, const u64 *rec_term, const u32 *f3rel,
-                                              const u32 *nulrel, u64 r, u64 *start) {
     const u64 rs = rec_start[r];
-    u64 end = rec_term[r];
-    if (nulrel[r]) end = min(end, rs + nulrel[r] - 1);
-    const u64 s = rs + f3rel[r] - 1;
-    *start = s;
-    return end > s ? end - s : 0;
-}
-
-__global__ void k_text_len(const u8 *__restrict__ buf, const u64 *__restrict__ rec_start,
-                           const u64 *__restrict__ rec_term, const u32 *__restrict__ f3rel,
-                           const u32 *__restrict__ nulrel, u64 nrec, u64 *__restrict__ line_len) {
-    const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= nrec) return;
-    u64 L = 0;
-    if (r >= 1 && f3rel[r]) {
-        u64 s;
-        const u64 n = text_field_len(rec_start, rec_term, f3rel, nulrel, r, &s);
-        L = dup_field(buf + s, n, 1, nullptr).len + 1;
+    u64 s, e;
+    if (TEXT) {  // field 3: after the third comma up to the terminator / first NUL
+        s = rs + f3rel[r] - 1;
+        e = rec_term[r];
+        if (nulrel[r]) e = min(e, rs + nulrel[r] - 1);
+        if (e < s) e = s;
+    } else {  // field 0: up to the first comma
+        s = rs;
+        e = rs + f0rel[r] - 1;
     }
-    line_len[r] = L;
+    while (s < e && c_space(buf[s])) ++s;
+    while (e > s && c_space(buf[e - 1])) --e;
+    u32 pairs = 0;
+    if (!(e > s + 1 && buf[s] == '"' && buf[e - 1] == '"')) {
+        for (u64 i = s; i + 1 < e; ++i)
+            if (buf[i] == '"' && buf[i + 1] == '"') { ++pairs; ++i; }
+    }
+    line_len[r] = (e - s) - pairs + 1;
+    span_src[r] = s;
+    span_pairs[r] = pairs;
 }
 
-__global__ void k_text_write(const u8 *__restrict__ buf, const u64 *__restrict__ rec_start,
-                             const u64 *__restrict__ rec_term, const u32 *__restrict__ f3rel,
-                             const u32 *__restrict__ nulrel, u64 nrec, const u64 *__restrict__ line_off,
-                             u64 hdr_len, u8 *__restrict__ col) {
-    const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= nrec || r == 0 || !f3rel[r]) return;
-    u64 s;
-    const u64 n = text_field_len(rec_start, rec_term, f3rel, nulrel, r, &s);
-    u8 *dst = col + hdr_len + line_off[r];
-    const Span sp = dup_field(buf + s, n, 1, dst);
-    dst[sp.len] = '\n';
+__global__ __launch_bounds__(256) void k_col_write(const u8 *__restrict__ buf, const u64 *__restrict__ line_len,
+                                                   const u64 *__restrict__ line_off, const u64 *__restrict__ span_src,
+                                                   const u32 *__restrict__ span_pairs, u64 nrec, u64 hdr,
+                                                   u8 *__restrict__ col) {
+    const u32 lane = lane_id();
+    const u64 nw = ((u64)gridDim.x * blockDim.x) >> 6;
+    for (u64 r = ((u64)blockIdx.x * blockDim.x + threadIdx.x) >> 6; r < nrec; r += nw) {
+        const u64 L = line_len[r];
+        if (!L) continue;
+        const u64 len = L - 1;
+        const u8 *src = buf + span_src[r];
+        u8 *dst = col + hdr + line_off[r];
+        const u32 pairs = span_pairs[r];
+        if (!pairs) {
+            for (u64 i = lane; i < len; i += 64) dst[i] = src[i];
+        } else if (lane == 0) {
+            const u64 n = len + pairs;
+            u64 j = 0;
+            for (u64 i = 0; i < n; ++i) {
+                const u8 ch = src[i];
+                if (ch == '"' && i + 1 < n && src[i + 1] == '"') ++i;
+                dst[j++] = ch;
+            }
+        }
+        if (lane == 0) dst[len] = '\n';
+    }
 }
 
 // Artist pass over artist.csv records: strip EOL, duplicate_field(line, 0),
 // count non-empty names (parallel_spotify.c:986-994).  Key bytes go to the
-// arena at the record's own offset.
-__global__ void k_artist_key(const u8 *__restrict__ col, const u64 *__restrict__ ar_start,
-                             const u64 *__restrict__ ar_term, u64 nrec, u8 *__restrict__ arena,
-                             u64 *__restrict__ key_off, u32 *__restrict__ key_len, u64 *__restrict__ key_slot,
-                             u64 *atab, u64 amask, u32 *alist, u64 alist_cap, Counters *ctr) {
-    const u64 j = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= nrec) return;
-    const u64 s = ar_start[j];
-    u64 n = ar_term[j] - s;
-    const u8 *p = col + s;
-    while (n > 0 && (p[n - 1] == '\n' || p[n - 1] == '\r')) --n;
-    const Span sp = dup_field(p, n, 0, arena + s);
-    key_off[j] = s + sp.off;
-    key_len[j] = (u32)sp.len;
-    if (sp.len == 0) {
-        key_slot[j] = ~0ull;
-        return;
+// arena at the record's own offset.  Counting is privatised per workgroup in
+// an LDS table keyed by the 64-bit key hash (the artist distribution is
+// skewed: without it the head artists serialise on one HBM counter); the
+// block then adds each distinct key once to the HBM table.
+#define AK_T 256
+#define AK_SLOTS 4096
+#define AK_LOCAL (1ull << 63)
+__global__ __launch_bounds__(AK_T) void k_artist_key(const u8 *__restrict__ col, const u64 *__restrict__ ar_start,
+                                                     const u64 *__restrict__ ar_term, u64 nrec, u8 *__restrict__ arena,
+                                                     u64 *__restrict__ key_off, u32 *__restrict__ key_len,
+                                                     u64 *__restrict__ key_slot, u64 *atab, u64 amask, u32 *alist,
+                                                     u64 alist_cap, Counters *ctr) {
+    __shared__ u64 lh[AK_SLOTS];
+    __shared__ u64 lrep[AK_SLOTS];  // first local record; after the flush: global slot
+    __shared__ u32 lc[AK_SLOTS];
+    for (u32 i = threadIdx.x; i < AK_SLOTS; i += AK_T) { lh[i] = 0; lc[i] = 0; }
+    __syncthreads();
+    const u64 stride = (u64)gridDim.x * AK_T;
+    for (u64 j = (u64)blockIdx.x * AK_T + threadIdx.x; j < nrec; j += stride) {
+        const u64 s = ar_start[j];
+        u64 n = ar_term[j] - s;
+        const u8 *p = col + s;
+        while (n > 0 && (p[n - 1] == '\n' || p[n - 1] == '\r')) --n;
+        const Span sp = dup_field(p, n, 0, arena + s);
+        key_off[j] = s + sp.off;
+        key_len[j] = (u32)sp.len;
+        if (sp.len == 0) {
+            key_slot[j] = ~0ull;
+            continue;
+        }
+        u64 h = bytes_hash(arena + s + sp.off, sp.len, 0);
+        if (h == 0) h = 0x8000000000000000ULL;
+        u32 q = (u32)(h >> 20) & (AK_SLOTS - 1);
+        bool done = false;
+        for (u32 probe = 0; probe < 32; ++probe) {
+            u64 cur = lh[q];
+            if (cur == 0) {
+                cur = atomicCAS((unsigned long long *)&lh[q], 0ull, (unsigned long long)h);
+                if (cur == 0) {
+                    lrep[q] = j;
+                    cur = h;
+                }
+            }
+            if (cur == h) {
+                atomicAdd(&lc[q], 1u);
+                key_slot[j] = AK_LOCAL | q;
+                done = true;
+                break;
+            }
+            q = (q + 1) & (AK_SLOTS - 1);
+        }
+        if (!done) key_slot[j] = h_insert(atab, amask, h, 1, j, alist, alist_cap, &ctr->a_claimed, ctr, OVF_A);
     }
-    const u64 h = bytes_hash(arena + s + sp.off, sp.len, 0);
-    key_slot[j] = h_insert(atab, amask, h, 1, j, alist, alist_cap, &ctr->a_claimed, ctr, OVF_A);
+    __syncthreads();
+    for (u32 i = threadIdx.x; i < AK_SLOTS; i += AK_T) {
+        const u32 cnt = lc[i];
+        if (cnt) lrep[i] = h_insert(atab, amask, lh[i], cnt, lrep[i], alist, alist_cap, &ctr->a_claimed, ctr, OVF_A);
+    }
+    __syncthreads();
+    for (u64 j = (u64)blockIdx.x * AK_T + threadIdx.x; j < nrec; j += stride) {
+        const u64 k = key_slot[j];
+        if (k != ~0ull && (k & AK_LOCAL)) key_slot[j] = lrep[k & (AK_SLOTS - 1)];
+    }
 }
 
 __global__ void k_artist_verify(const u8 *__restrict__ arena, const u64 *__restrict__ key_off,
@@ -547,33 +597,32 @@ __global__ void k_blob_write(const u32 *__restrict__ order, u64 n, const u64 *__
 // host launchers
 static inline dim3 grid1(u64 n, u32 t = 256) { return dim3((u32)((n + t - 1) / t)); }
 
-hipError_t msa_launch_artist_len(const u8 *buf, const u64 *rs, const u32 *f0, const u32 *f3, u64 nrec, u64 *len,
-                                 hipStream_t s) {
-    if (nrec) hipLaunchKernelGGL(k_artist_len, grid1(nrec), dim3(256), 0, s, buf, rs, f0, f3, nrec, len);
+hipError_t msa_launch_col_span(int text, const u8 *buf, const u64 *rs, const u64 *rt, const u32 *f0, const u32 *f3,
+                               const u32 *nul, u64 nrec, u64 *len, u64 *src, u32 *pairs, hipStream_t s) {
+    if (!nrec) return hipSuccess;
+    if (text)
+        hipLaunchKernelGGL(k_col_span<1>, grid1(nrec), dim3(256), 0, s, buf, rs, rt, f0, f3, nul, nrec, len, src, pairs);
+    else
+        hipLaunchKernelGGL(k_col_span<0>, grid1(nrec), dim3(256), 0, s, buf, rs, rt, f0, f3, nul, nrec, len, src, pairs);
     return hipGetLastError();
 }
-hipError_t msa_launch_artist_write(const u8 *buf, const u64 *rs, const u32 *f0, const u32 *f3, u64 nrec,
-                                   const u64 *off, u64 hdr, u8 *col, hipStream_t s) {
-    if (nrec) hipLaunchKernelGGL(k_artist_write, grid1(nrec), dim3(256), 0, s, buf, rs, f0, f3, nrec, off, hdr, col);
-    return hipGetLastError();
-}
-hipError_t msa_launch_text_len(const u8 *buf, const u64 *rs, const u64 *rt, const u32 *f3, const u32 *nul, u64 nrec,
-                               u64 *len, hipStream_t s) {
-    if (nrec) hipLaunchKernelGGL(k_text_len, grid1(nrec), dim3(256), 0, s, buf, rs, rt, f3, nul, nrec, len);
-    return hipGetLastError();
-}
-hipError_t msa_launch_text_write(const u8 *buf, const u64 *rs, const u64 *rt, const u32 *f3, const u32 *nul,
-                                 u64 nrec, const u64 *off, u64 hdr, u8 *col, hipStream_t s) {
-    if (nrec)
-        hipLaunchKernelGGL(k_text_write, grid1(nrec), dim3(256), 0, s, buf, rs, rt, f3, nul, nrec, off, hdr, col);
+hipError_t msa_launch_col_write(const u8 *buf, const u64 *len, const u64 *off, const u64 *src, const u32 *pairs,
+                                u64 nrec, u64 hdr, u8 *col, int cus, hipStream_t s) {
+    if (!nrec) return hipSuccess;
+    u64 blocks = (nrec + 3) / 4;
+    const u64 cap = (u64)cus * 16;
+    if (blocks > cap) blocks = cap;
+    hipLaunchKernelGGL(k_col_write, dim3((u32)blocks), dim3(256), 0, s, buf, len, off, src, pairs, nrec, hdr, col);
     return hipGetLastError();
 }
 hipError_t msa_launch_artist_key(const u8 *col, const u64 *ar_start, const u64 *ar_term, u64 nrec, u8 *arena,
                                  u64 *key_off, u32 *key_len, u64 *key_slot, u64 *atab, u64 amask, u32 *alist,
                                  u64 alist_cap, Counters *ctr, hipStream_t s) {
     if (nrec) {
-        hipLaunchKernelGGL(k_artist_key, grid1(nrec), dim3(256), 0, s, col, ar_start, ar_term, nrec, arena, key_off,
-                           key_len, key_slot, atab, amask, alist, alist_cap, ctr);
+        u64 blocks = (nrec + AK_T - 1) / AK_T;
+        if (blocks > 1024) blocks = 1024;
+        hipLaunchKernelGGL(k_artist_key, dim3((u32)blocks), dim3(AK_T), 0, s, col, ar_start, ar_term, nrec, arena,
+                           key_off, key_len, key_slot, atab, amask, alist, alist_cap, ctr);
         hipLaunchKernelGGL(k_artist_verify, grid1(nrec), dim3(256), 0, s, (const u8 *)arena, key_off, key_len,
                            key_slot, nrec, (const u64 *)atab, ctr);
     }

@@ -179,10 +179,12 @@ __global__ __launch_bounds__(FN_THREADS) void k_fn_apply(const ChunkSum *__restr
 // K3: the main pass.
 #define K3_THREADS 512
 #define K3_WAVES (K3_THREADS / 64)
-#define LSLOTS 4096
+#define LSLOTS 2048
+#define MSLOTS 1024
 #define LPROBE 8
 #define WAVE_LDS (2048 + 256 + 1024)
-#define K3_LDS (LSLOTS * 12 + K3_WAVES * WAVE_LDS)
+#define TAB_LDS (LSLOTS * 12 + MSLOTS * 20)
+#define K3_LDS (TAB_LDS + K3_WAVES * WAVE_LDS)
 
 // MODE 0 = CSV (records, fields, lyric tokens), 1 = LINES (records only),
 //      2 = FLAT (every byte is lyric text: tokens only, no record structure)
@@ -192,9 +194,15 @@ __global__ __launch_bounds__(K3_THREADS) void k_scan_main(ScanArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     u64 *lkey = reinterpret_cast<u64 *>(smem);
     u32 *lcnt = reinterpret_cast<u32 *>(smem + LSLOTS * 8);
+    // M words (9..16 bytes): key (k0, k1), claimed by CAS on k0; k1 is published
+    // after the claim, and a prober that finds k0 but not yet k1 moves on (a
+    // key may then own two slots -- both flush into the same HBM entry).
+    u64 *mk0 = reinterpret_cast<u64 *>(smem + LSLOTS * 12);
+    u64 *mk1 = mk0 + MSLOTS;
+    u32 *mcnt = reinterpret_cast<u32 *>(mk1 + MSLOTS);
     const u32 lane = lane_id();
     const u32 wib = threadIdx.x >> 6;
-    unsigned char *wl = smem + LSLOTS * 12 + wib * WAVE_LDS;
+    unsigned char *wl = smem + TAB_LDS + wib * WAVE_LDS;
     u64 *ring = reinterpret_cast<u64 *>(wl);             // 2 KiB: two 1 KiB iteration slots
     u64 *bm = reinterpret_cast<u64 *>(wl + 2048);        // token-class bitmap of the ring
     u16 *starts = reinterpret_cast<u16 *>(wl + 2048 + 256);
@@ -202,6 +210,7 @@ __global__ __launch_bounds__(K3_THREADS) void k_scan_main(ScanArgs a) {
 
     if (TOK) {
         for (u32 i = threadIdx.x; i < LSLOTS; i += K3_THREADS) { lkey[i] = 0; lcnt[i] = 0; }
+        for (u32 i = threadIdx.x; i < MSLOTS; i += K3_THREADS) { mk0[i] = 0; mk1[i] = 0; mcnt[i] = 0; }
         __syncthreads();
     }
     const u32 gw = blockIdx.x * K3_WAVES + wib;
@@ -289,6 +298,7 @@ __global__ __launch_bounds__(K3_THREADS) void k_scan_main(ScanArgs a) {
             // walk this lane's events (terminators, unquoted commas, NULs)
             u32 E = TERM | Cu | Zm;
             u32 from = 0;
+            if (a.ablate & 8) E = TERM;  // ablation: skip field events
             while (E) {
                 const u32 b = __ffs(E) - 1;
                 E &= E - 1;
@@ -327,7 +337,7 @@ __global__ __launch_bounds__(K3_THREADS) void k_scan_main(ScanArgs a) {
             st.rs = readlane64(rs, 63);
             }
 
-            if (TOK) {
+            if (TOK && !(a.ablate & 1)) {
                 // ---- tokens of the lyric field
                 const u32 upT = __shfl_up(k.T, 1);
                 const u32 pt0 = lane ? ((upT >> 15) & 1u) : prevT;
@@ -349,6 +359,7 @@ __global__ __launch_bounds__(K3_THREADS) void k_scan_main(ScanArgs a) {
                     }
                     if (len < 3) continue;
                     ++words;
+                    if (a.ablate & 2) continue;  // ablation: count only
                     if (len > 16) {
                         const u64 i = atomicAdd((unsigned long long *)&a.ctr->l_occ, 1ull);
                         if (i < a.l_cap) a.l_pos[i] = (ibase + (o & 1023u)) | a.lpos_tag;
@@ -359,6 +370,7 @@ __global__ __launch_bounds__(K3_THREADS) void k_scan_main(ScanArgs a) {
                     const u64 w0 = ring[q], w1 = ring[(q + 1) & 255u];
                     u64 k0 = sh ? ((w0 >> sh) | (w1 << (64 - sh))) : w0;
                     if (len <= 8) {
+                        if (a.ablate & 32) continue;  // ablation: skip S words
                         if (len < 8) k0 &= (1ull << (8 * len)) - 1ull;
                         const u64 key = lower8(k0);
                         u32 h = lds_hash(key) & (LSLOTS - 1);
@@ -376,12 +388,33 @@ __global__ __launch_bounds__(K3_THREADS) void k_scan_main(ScanArgs a) {
                             }
                             h = (h + 1) & (LSLOTS - 1);
                         }
-                        if (!done) s_insert(a.s_tab, a.s_mask, key, 1, a.s_list, a.s_list_cap, a.ctr);
+                        if (!done && !(a.ablate & 4)) s_insert(a.s_tab, a.s_mask, key, 1, a.s_list, a.s_list_cap, a.ctr);
                     } else {
                         const u64 w2 = ring[(q + 2) & 255u];
                         u64 k1 = sh ? ((w1 >> sh) | (w2 << (64 - sh))) : w1;
                         if (len < 16) k1 &= (1ull << (8 * (len - 8))) - 1ull;
-                        m_insert(a.m_tab, a.m_mask, lower8(k0), lower8(k1), 1, a.m_list, a.m_list_cap, a.ctr);
+                        if (a.ablate & 16) continue;  // ablation: skip M words
+                        const u64 x0 = lower8(k0), x1 = lower8(k1);
+                        u32 h = lds_hash(x0 ^ (x1 * 0xC2B2AE3D27D4EB4FULL)) & (MSLOTS - 1);
+                        bool done = false;
+                        for (u32 p = 0; p < LPROBE; ++p) {
+                            u64 c0 = mk0[h];
+                            bool mine = false;
+                            if (c0 == 0) {
+                                c0 = atomicCAS((unsigned long long *)&mk0[h], 0ull, (unsigned long long)x0);
+                                if (c0 == 0) {
+                                    mk1[h] = x1;
+                                    mine = true;
+                                }
+                            }
+                            if (mine || (c0 == x0 && mk1[h] == x1)) {
+                                atomicAdd(&mcnt[h], 1u);
+                                done = true;
+                                break;
+                            }
+                            h = (h + 1) & (MSLOTS - 1);
+                        }
+                        if (!done) m_insert(a.m_tab, a.m_mask, x0, x1, 1, a.m_list, a.m_list_cap, a.ctr);
                     }
                 }
                 wave_sync();
@@ -397,6 +430,10 @@ __global__ __launch_bounds__(K3_THREADS) void k_scan_main(ScanArgs a) {
         for (u32 i = threadIdx.x; i < LSLOTS; i += K3_THREADS) {
             const u32 n = lcnt[i];
             if (n) s_insert(a.s_tab, a.s_mask, lkey[i], n, a.s_list, a.s_list_cap, a.ctr);
+        }
+        for (u32 i = threadIdx.x; i < MSLOTS; i += K3_THREADS) {
+            const u32 n = mcnt[i];
+            if (n) m_insert(a.m_tab, a.m_mask, mk0[i], mk1[i], n, a.m_list, a.m_list_cap, a.ctr);
         }
     }
 }
