@@ -18,8 +18,8 @@
 
 // ---- launchers (msa_scan.hip / msa_post.hip)
 hipError_t msa_launch_summary(const u8 *, u64, u64, u32, ChunkSum *, hipStream_t);
-hipError_t msa_launch_fn(const ChunkSum *, u64, u32, Fn *, Fn *, const State *, State *, State *, hipStream_t, bool,
-                         bool);
+u32 msa_fn_blocks(u32 nchunks);
+hipError_t msa_launch_fn(const ChunkSum *, u64, u32, Fn *, State *, Fn *, const State *, State *, State *, hipStream_t);
 hipError_t msa_launch_scan(const ScanArgs &, int, hipStream_t);
 hipError_t msa_exclusive_scan(const u64 *, u64, u64 *, u64 *, u64 *, hipStream_t);
 hipError_t msa_launch_col_span(int, const u8 *, const u64 *, const u64 *, const u32 *, const u32 *, const u32 *, u64,
@@ -105,7 +105,7 @@ struct msa_ctx {
     const u8 *in = nullptr;
     u64 n = 0;
     // scan scratch
-    DevBuf sums, carry, runpre, small;  // small: Fn total + 2 States + ...
+    DevBuf sums, carry, btot, bstate, small;  // small: Fn total + 2 States + ...
     // CSV records
     DevBuf rec_start, rec_term, f0rel, f3rel, nulrel;
     u64 nrec = 0, rec_cap = 0;
@@ -278,7 +278,8 @@ static int run_scan_fn(msa_ctx *c, const u8 *buf, u64 b, u64 e, State init, Stat
     const u32 nch = (u32)((len + MSA_CHUNK - 1) / MSA_CHUNK);
     HIPC(c, ensure(c->sums, sizeof(ChunkSum) * (size_t)(nch + 1)));
     HIPC(c, ensure(c->carry, sizeof(State) * (size_t)(nch + 1)));
-    HIPC(c, ensure(c->runpre, sizeof(Fn) * 256));
+    HIPC(c, ensure(c->btot, sizeof(Fn) * (size_t)(msa_fn_blocks(nch) + 1)));
+    HIPC(c, ensure(c->bstate, sizeof(State) * (size_t)(msa_fn_blocks(nch) + 1)));
     HIPC(c, ensure(c->small, 4096));
     Fn *total = c->small.as<Fn>();
     State *d_init = reinterpret_cast<State *>(c->small.as<char>() + 1024);
@@ -287,8 +288,8 @@ static int run_scan_fn(msa_ctx *c, const u8 *buf, u64 b, u64 e, State init, Stat
     if (nch) {
         prof_begin(c, stage_id);
         HIPC(c, msa_launch_summary(buf, b, e, nch, c->sums.as<ChunkSum>(), c->stream));
-        HIPC(c, msa_launch_fn(c->sums.as<ChunkSum>(), b, nch, c->runpre.as<Fn>(), total, d_init, c->carry.as<State>(),
-                              d_fin, c->stream, false, false));
+        HIPC(c, msa_launch_fn(c->sums.as<ChunkSum>(), b, nch, c->btot.as<Fn>(), c->bstate.as<State>(), total, d_init,
+                              c->carry.as<State>(), d_fin, c->stream));
         prof_end(c, stage_id, len);
         HIPC(c, hipMemcpyAsync(fin, d_fin, sizeof(State), hipMemcpyDeviceToHost, c->stream));
         HIPC(c, hipStreamSynchronize(c->stream));
@@ -794,7 +795,7 @@ void msa_destroy(msa_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
-    DevBuf *all[] = {&c->in_own, &c->sums, &c->carry, &c->runpre, &c->small, &c->rec_start, &c->rec_term, &c->extra,
+    DevBuf *all[] = {&c->in_own, &c->sums, &c->carry, &c->btot, &c->bstate, &c->small, &c->rec_start, &c->rec_term, &c->extra,
                      &c->f0rel, &c->f3rel, &c->nulrel, &c->acol, &c->alen, &c->aoff, &c->asrc, &c->apairs, &c->tcol, &c->tlen, &c->toff, &c->tsrc, &c->tpairs,
                      &c->scan_bsum, &c->scan_total, &c->ar_start, &c->ar_term, &c->arena, &c->key_off,
                      &c->key_len, &c->key_slot, &c->s_tab, &c->s_list, &c->m_tab, &c->m_list, &c->l_pos, &c->l_len,

@@ -74,8 +74,20 @@ __host__ __device__ inline FnEnt chunk_entry(const ChunkSum &s, u64 base, u32 id
     return e;
 }
 
+// g's entry for input state (p, cr), by value selects (a dynamic index into
+// the entry array would put Fn in scratch memory).
+__host__ __device__ inline FnEnt fn_pick(const Fn &g, u32 p, u32 cr) {
+    const bool two = cr != 0, one = p != 0;
+    FnEnt r;
+#define MSA_PICK(f) r.f = two ? g.e[2].f : (one ? g.e[1].f : g.e[0].f)
+    MSA_PICK(nterm); MSA_PICK(rs); MSA_PICK(p); MSA_PICK(cr); MSA_PICK(has); MSA_PICK(c); MSA_PICK(z);
+#undef MSA_PICK
+    r.pad = 0;
+    return r;
+}
+
 __host__ __device__ inline FnEnt fn_then(const FnEnt &a, const Fn &g) {
-    const FnEnt &b = g.e[st_index(a.p, a.cr)];
+    const FnEnt b = fn_pick(g, a.p, a.cr);
     FnEnt r;
     r.p = b.p;
     r.cr = b.cr;
@@ -95,7 +107,9 @@ __host__ __device__ inline FnEnt fn_then(const FnEnt &a, const Fn &g) {
 
 __host__ __device__ inline Fn fn_compose(const Fn &f, const Fn &g) {  // f then g
     Fn r;
-    for (int i = 0; i < 3; ++i) r.e[i] = fn_then(f.e[i], g);
+    r.e[0] = fn_then(f.e[0], g);
+    r.e[1] = fn_then(f.e[1], g);
+    r.e[2] = fn_then(f.e[2], g);
     return r;
 }
 
@@ -109,7 +123,7 @@ __host__ __device__ inline Fn fn_identity(u64 pos) {
 }
 
 __host__ __device__ inline State fn_apply(const State &s, const Fn &f) {
-    const FnEnt &b = f.e[st_index(s.p, s.cr)];
+    const FnEnt b = fn_pick(f, s.p, s.cr);
     State r;
     r.p = b.p;
     r.cr = b.cr;

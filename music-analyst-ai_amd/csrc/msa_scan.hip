@@ -7,8 +7,9 @@
 //   K1 k_chunk_summary  one wave per 16 KiB chunk: the chunk's transfer
 //                       function over the reader state, for BOTH possible
 //                       incoming quote parities (wave-ballot prefix-xor)
-//   K2 k_fn_compose /   compose the chunk functions (tiny), then apply the
-//      k_fn_apply       initial state -> exact reader state at every chunk
+//   K2 k_fn_reduce /    scan the chunk functions (associative composition)
+//      k_fn_top /       and apply the initial state -> exact reader state at
+//      k_fn_down        every chunk
 //   K3 k_scan_main      one wave per chunk again, now knowing its state:
 //                       record terminators, the first three unquoted commas
 //                       of every record, NUL truncation, and -- for the
@@ -125,54 +126,89 @@ __global__ __launch_bounds__(256) void k_chunk_summary(const u8 *__restrict__ bu
 }
 
 // ---------------------------------------------------------------------------
-// K2a: compose chunk functions.  One block of 256 threads; thread t owns a
-// contiguous run of chunks.  Writes the run prefix functions and the total.
-#define FN_THREADS 256
-__global__ __launch_bounds__(FN_THREADS) void k_fn_compose(const ChunkSum *__restrict__ sums, u64 seg_begin,
-                                                           u32 nchunks, Fn *__restrict__ run_prefix,
-                                                           Fn *__restrict__ total) {
-    __shared__ Fn runs[FN_THREADS];
+// K2: exact reader state at every chunk start = the initial state pushed
+// through the composition of all earlier chunk functions (an exclusive scan
+// over the associative "f then g" monoid), in three launches:
+//   k_fn_reduce  one block per 256 chunks: tree-compose -> block total
+//   k_fn_top     one block: runs of block totals -> each block's start state
+//   k_fn_down    one block per 256 chunks: Hillis-Steele scan in LDS, apply
+#define FN_T 256
+
+__device__ __forceinline__ Fn chunk_fn(const ChunkSum *__restrict__ sums, u64 seg_begin, u32 nchunks, u32 c) {
+    const u64 base = seg_begin + (u64)c * MSA_CHUNK;
+    if (c >= nchunks) return fn_identity(base);
+    const ChunkSum cs = sums[c];
+    Fn g;
+    g.e[0] = chunk_entry(cs, base, 0);
+    g.e[1] = chunk_entry(cs, base, 1);
+    g.e[2] = chunk_entry(cs, base, 2);
+    return g;
+}
+
+__global__ __launch_bounds__(FN_T) void k_fn_reduce(const ChunkSum *__restrict__ sums, u64 seg_begin, u32 nchunks,
+                                                    Fn *__restrict__ btot) {
+    __shared__ Fn sh[FN_T];
     const u32 t = threadIdx.x;
-    const u32 per = (nchunks + FN_THREADS - 1) / FN_THREADS;
-    const u32 a = min(nchunks, t * per), b = min(nchunks, a + per);
-    Fn f = fn_identity(seg_begin + (u64)a * MSA_CHUNK);
-    for (u32 c = a; c < b; ++c) {
-        const ChunkSum s = sums[c];
-        const u64 base = seg_begin + (u64)c * MSA_CHUNK;
-        Fn g;
-        for (u32 i = 0; i < 3; ++i) g.e[i] = chunk_entry(s, base, i);
-        f = fn_compose(f, g);
+    sh[t] = chunk_fn(sums, seg_begin, nchunks, blockIdx.x * FN_T + t);
+    __syncthreads();
+    for (u32 w = 1; w < FN_T; w <<= 1) {
+        if ((t & (2 * w - 1)) == 0) sh[t] = fn_compose(sh[t], sh[t + w]);
+        __syncthreads();
     }
+    if (t == 0) btot[blockIdx.x] = sh[0];
+}
+
+__global__ __launch_bounds__(FN_T) void k_fn_top(const Fn *__restrict__ btot, u32 nb, u64 seg_begin,
+                                                 const State *__restrict__ init, State *__restrict__ bstate,
+                                                 Fn *__restrict__ total) {
+    __shared__ Fn runs[FN_T];
+    __shared__ State rst[FN_T];
+    const u32 t = threadIdx.x;
+    const u32 per = (nb + FN_T - 1) / FN_T;
+    const u32 a = min(nb, t * per), b = min(nb, a + per);
+    Fn f = fn_identity(seg_begin);
+    for (u32 i = a; i < b; ++i) f = fn_compose(f, btot[i]);
     runs[t] = f;
     __syncthreads();
     if (t == 0) {
+        State s = *init;
         Fn acc = fn_identity(seg_begin);
-        for (u32 i = 0; i < FN_THREADS; ++i) {
-            run_prefix[i] = acc;
+        for (u32 i = 0; i < FN_T; ++i) {
+            rst[i] = s;
+            s = fn_apply(s, runs[i]);
             acc = fn_compose(acc, runs[i]);
         }
-        *total = acc;
+        if (total) *total = acc;
+    }
+    __syncthreads();
+    State s = rst[t];
+    for (u32 i = a; i < b; ++i) {
+        bstate[i] = s;
+        s = fn_apply(s, btot[i]);
     }
 }
 
-// K2b: apply the initial state; write every chunk's incoming state.
-__global__ __launch_bounds__(FN_THREADS) void k_fn_apply(const ChunkSum *__restrict__ sums, u64 seg_begin,
-                                                         u32 nchunks, const Fn *__restrict__ run_prefix,
-                                                         const State *__restrict__ init,
-                                                         State *__restrict__ carry, State *__restrict__ final_state) {
+__global__ __launch_bounds__(FN_T) void k_fn_down(const ChunkSum *__restrict__ sums, u64 seg_begin, u32 nchunks,
+                                                  const State *__restrict__ bstate, State *__restrict__ carry,
+                                                  State *__restrict__ final_state) {
+    __shared__ Fn sh[2][FN_T];
     const u32 t = threadIdx.x;
-    const u32 per = (nchunks + FN_THREADS - 1) / FN_THREADS;
-    const u32 a = min(nchunks, t * per), b = min(nchunks, a + per);
-    State s = fn_apply(*init, run_prefix[t]);
-    for (u32 c = a; c < b; ++c) {
-        carry[c] = s;
-        const ChunkSum cs = sums[c];
-        const u64 base = seg_begin + (u64)c * MSA_CHUNK;
-        Fn g;
-        for (u32 i = 0; i < 3; ++i) g.e[i] = chunk_entry(cs, base, i);
-        s = fn_apply(s, g);
+    const u32 c = blockIdx.x * FN_T + t;
+    sh[0][t] = chunk_fn(sums, seg_begin, nchunks, c);
+    __syncthreads();
+    u32 cur = 0;
+    for (u32 off = 1; off < FN_T; off <<= 1) {  // inclusive scan, ping-pong buffers
+        const u32 src = (t >= off) ? t - off : t;
+        Fn g = fn_compose(sh[cur][src], sh[cur][t]);
+        if (t < off) g = sh[cur][t];
+        sh[cur ^ 1][t] = g;
+        cur ^= 1;
+        __syncthreads();
     }
-    if (t == FN_THREADS - 1) *final_state = s;
+    State s = bstate[blockIdx.x];
+    if (t > 0) s = fn_apply(s, sh[cur][t - 1]);
+    if (c < nchunks) carry[c] = s;
+    if (c + 1 == nchunks) *final_state = fn_apply(bstate[blockIdx.x], sh[cur][t]);
 }
 
 // ---------------------------------------------------------------------------
@@ -462,14 +498,16 @@ hipError_t msa_launch_summary(const u8 *buf, u64 seg_begin, u64 seg_end, u32 nch
     return hipGetLastError();
 }
 
-hipError_t msa_launch_fn(const ChunkSum *sums, u64 seg_begin, u32 nchunks, Fn *run_prefix, Fn *total,
-                         const State *init, State *carry, State *final_state, hipStream_t s, bool apply_only,
-                         bool compose_only) {
-    if (!apply_only)
-        hipLaunchKernelGGL(k_fn_compose, dim3(1), dim3(FN_THREADS), 0, s, sums, seg_begin, nchunks, run_prefix, total);
-    if (!compose_only)
-        hipLaunchKernelGGL(k_fn_apply, dim3(1), dim3(FN_THREADS), 0, s, sums, seg_begin, nchunks, run_prefix, init,
-                           carry, final_state);
+u32 msa_fn_blocks(u32 nchunks) { return (nchunks + FN_T - 1) / FN_T; }
+
+hipError_t msa_launch_fn(const ChunkSum *sums, u64 seg_begin, u32 nchunks, Fn *btot, State *bstate, Fn *total,
+                         const State *init, State *carry, State *final_state, hipStream_t s) {
+    if (!nchunks) return hipSuccess;
+    const u32 nb = msa_fn_blocks(nchunks);
+    hipLaunchKernelGGL(k_fn_reduce, dim3(nb), dim3(FN_T), 0, s, sums, seg_begin, nchunks, btot);
+    hipLaunchKernelGGL(k_fn_top, dim3(1), dim3(FN_T), 0, s, (const Fn *)btot, nb, seg_begin, init, bstate, total);
+    hipLaunchKernelGGL(k_fn_down, dim3(nb), dim3(FN_T), 0, s, sums, seg_begin, nchunks, (const State *)bstate, carry,
+                       final_state);
     return hipGetLastError();
 }
 
