@@ -24,7 +24,7 @@ hipError_t msa_launch_scan(const ScanArgs &, int, hipStream_t);
 hipError_t msa_exclusive_scan(const u64 *, u64, u64 *, u64 *, u64 *, hipStream_t);
 hipError_t msa_launch_col_span(int, const u8 *, const u64 *, const u64 *, const u32 *, const u32 *, const u32 *, u64,
                                u64 *, u64 *, u32 *, hipStream_t);
-hipError_t msa_launch_col_write(const u8 *, const u64 *, const u64 *, const u64 *, const u32 *, u64, u64, u8 *, int,
+hipError_t msa_launch_col_write(const u8 *, const u64 *, const u64 *, const u64 *, const u32 *, u64, u64, u64, u8 *,
                                 hipStream_t);
 hipError_t msa_launch_artist_key(const u8 *, const u64 *, const u64 *, u64, u8 *, u64 *, u32 *, u64 *, u64 *, u64,
                                  u32 *, u64, Counters *, hipStream_t);
@@ -431,7 +431,7 @@ static int materialise_column(msa_ctx *c, bool text, const std::string &hdr_line
     HIPC(c, hipMemcpyAsync(col.p, hdr_line.data(), hdr_line.size(), hipMemcpyHostToDevice, c->stream));
     HIPC(c, hipMemsetAsync(col.as<char>() + total, 0, MSA_INPUT_PAD, c->stream));
     HIPC(c, msa_launch_col_write(c->in, lenb.as<u64>(), offb.as<u64>(), srcb.as<u64>(), pairsb.as<u32>(), nrec,
-                                 hdr_line.size(), col.as<u8>(), c->cus, c->stream));
+                                 hdr_line.size(), body, col.as<u8>(), c->stream));
     *col_len = total;
     return MSA_OK;
 }

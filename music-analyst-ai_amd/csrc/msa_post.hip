@@ -183,32 +183,88 @@ __global__ __launch_bounds__(256) void k_col_span(const u8 *__restrict__ buf, co
     span_pairs[r] = pairs;
 }
 
-__global__ __launch_bounds__(256) void k_col_write(const u8 *__restrict__ buf, const u64 *__restrict__ line_len,
-                                                   const u64 *__restrict__ line_off, const u64 *__restrict__ span_src,
-                                                   const u32 *__restrict__ span_pairs, u64 nrec, u64 hdr,
-                                                   u8 *__restrict__ col) {
-    const u32 lane = lane_id();
-    const u64 nw = ((u64)gridDim.x * blockDim.x) >> 6;
-    for (u64 r = ((u64)blockIdx.x * blockDim.x + threadIdx.x) >> 6; r < nrec; r += nw) {
-        const u64 L = line_len[r];
-        if (!L) continue;
-        const u64 len = L - 1;
-        const u8 *src = buf + span_src[r];
-        u8 *dst = col + hdr + line_off[r];
-        const u32 pairs = span_pairs[r];
-        if (!pairs) {
-            for (u64 i = lane; i < len; i += 64) dst[i] = src[i];
-        } else if (lane == 0) {
-            const u64 n = len + pairs;
-            u64 j = 0;
-            for (u64 i = 0; i < n; ++i) {
-                const u8 ch = src[i];
-                if (ch == '"' && i + 1 < n && src[i + 1] == '"') ++i;
-                dst[j++] = ch;
-            }
-        }
-        if (lane == 0) dst[len] = '\n';
+// Segmented gather.  A workgroup owns 256 consecutive lines (their metadata
+// is one coalesced load into LDS) and therefore the contiguous output range
+// [off[r0], off[r0+256]).  Its threads walk the 16-byte slots (aligned in
+// memory) of that range: a slot inside the raw part of one line is gathered
+// with five dword loads + alignbyte and stored whole; a slot that crosses a
+// line end, or the range's ragged first/last slot, is written byte by byte
+// (only the bytes this workgroup owns).  Lines whose "" pairs collapse are
+// left to k_col_collapse (one lane each; rare).  Every byte is written once.
+#define CG_T 256
+#define CG_SLOT 16
+__global__ __launch_bounds__(CG_T) void k_col_gather(const u8 *__restrict__ buf, const u64 *__restrict__ line_len,
+                                                     const u64 *__restrict__ line_off,
+                                                     const u64 *__restrict__ span_src,
+                                                     const u32 *__restrict__ span_pairs, u64 nrec, u64 hdr, u64 body,
+                                                     u8 *__restrict__ col) {
+    __shared__ u64 w_off[CG_T + 1], w_src[CG_T];
+    __shared__ u32 w_flag[CG_T];  // bit0: line has pairs to collapse
+    const u64 r0 = (u64)blockIdx.x * CG_T;
+    const u32 wn = (u32)min((u64)CG_T, nrec - r0);
+    const u32 t = threadIdx.x;
+    if (t < wn) {
+        w_off[t] = line_off[r0 + t];
+        w_src[t] = span_src[r0 + t];
+        w_flag[t] = span_pairs[r0 + t] ? 1u : 0u;
     }
+    if (t == 0) w_off[wn] = (r0 + wn < nrec) ? line_off[r0 + wn] : body;
+    __syncthreads();
+    const u64 O0 = hdr + w_off[0], O1 = hdr + w_off[wn];  // absolute column bytes owned
+    if (O1 <= O0) return;
+    const u64 S0 = O0 & ~(u64)(CG_SLOT - 1);
+    const u64 nslots = (O1 - S0 + CG_SLOT - 1) / CG_SLOT;
+    for (u64 si = t; si < nslots; si += CG_T) {
+        const u64 A = S0 + si * CG_SLOT;
+        const u64 lo = max(A, O0), hi = min(A + CG_SLOT, O1);
+        // line holding absolute byte lo: last j with hdr + w_off[j] <= lo
+        u32 j = 0, jhi = wn;
+        while (jhi - j > 1) {
+            const u32 mid = (j + jhi) >> 1;
+            if (hdr + w_off[mid] <= lo) j = mid;
+            else jhi = mid;
+        }
+        const u64 lstart = hdr + w_off[j], lend = hdr + w_off[j + 1];  // line j incl. '\n' at lend-1
+        if (lo == A && hi == A + CG_SLOT && A + CG_SLOT < lend && !w_flag[j]) {
+            const u64 s = w_src[j] + (A - lstart);
+            const u32 *w = reinterpret_cast<const u32 *>(buf + (s & ~3ull));
+            const u32 sh = (u32)(s & 3) * 8;
+            u32 v[5];
+#pragma unroll
+            for (int i = 0; i < 5; ++i) v[i] = w[i];
+            uint4 outv;
+            outv.x = (u32)((((u64)v[1] << 32) | v[0]) >> sh);
+            outv.y = (u32)((((u64)v[2] << 32) | v[1]) >> sh);
+            outv.z = (u32)((((u64)v[3] << 32) | v[2]) >> sh);
+            outv.w = (u32)((((u64)v[4] << 32) | v[3]) >> sh);
+            *reinterpret_cast<uint4 *>(col + A) = outv;
+            continue;
+        }
+        for (u64 p = lo; p < hi; ++p) {
+            while (p >= hdr + w_off[j + 1]) ++j;
+            if (w_flag[j]) continue;  // k_col_collapse writes this line
+            const u64 ls = hdr + w_off[j], le = hdr + w_off[j + 1];
+            col[p] = (p + 1 == le) ? (u8)'\n' : buf[w_src[j] + (p - ls)];
+        }
+    }
+}
+
+// Lines with "" pairs to collapse (duplicate_field, parallel_spotify.c:243-250).
+__global__ void k_col_collapse(const u8 *__restrict__ buf, const u64 *__restrict__ line_len,
+                               const u64 *__restrict__ line_off, const u64 *__restrict__ span_src,
+                               const u32 *__restrict__ span_pairs, u64 nrec, u64 hdr, u8 *__restrict__ col) {
+    const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nrec || !span_pairs[r] || !line_len[r]) return;
+    const u64 len = line_len[r] - 1, n = len + span_pairs[r];
+    const u8 *src = buf + span_src[r];
+    u8 *dst = col + hdr + line_off[r];
+    u64 j = 0;
+    for (u64 i = 0; i < n; ++i) {
+        const u8 ch = src[i];
+        if (ch == '"' && i + 1 < n && src[i + 1] == '"') ++i;
+        dst[j++] = ch;
+    }
+    dst[len] = '\n';
 }
 
 // Artist pass over artist.csv records: strip EOL, duplicate_field(line, 0),
@@ -607,12 +663,12 @@ hipError_t msa_launch_col_span(int text, const u8 *buf, const u64 *rs, const u64
     return hipGetLastError();
 }
 hipError_t msa_launch_col_write(const u8 *buf, const u64 *len, const u64 *off, const u64 *src, const u32 *pairs,
-                                u64 nrec, u64 hdr, u8 *col, int cus, hipStream_t s) {
-    if (!nrec) return hipSuccess;
-    u64 blocks = (nrec + 3) / 4;
-    const u64 cap = (u64)cus * 16;
-    if (blocks > cap) blocks = cap;
-    hipLaunchKernelGGL(k_col_write, dim3((u32)blocks), dim3(256), 0, s, buf, len, off, src, pairs, nrec, hdr, col);
+                                u64 nrec, u64 hdr, u64 body, u8 *col, hipStream_t s) {
+    if (!nrec || !body) return hipSuccess;
+    const u64 groups = (nrec + CG_T - 1) / CG_T;
+    hipLaunchKernelGGL(k_col_gather, dim3((u32)groups), dim3(CG_T), 0, s, buf, len, off, src, pairs, nrec, hdr, body,
+                       col);
+    hipLaunchKernelGGL(k_col_collapse, grid1(nrec), dim3(256), 0, s, buf, len, off, src, pairs, nrec, hdr, col);
     return hipGetLastError();
 }
 hipError_t msa_launch_artist_key(const u8 *col, const u64 *ar_start, const u64 *ar_term, u64 nrec, u8 *arena,

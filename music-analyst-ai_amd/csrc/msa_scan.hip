@@ -222,6 +222,65 @@ __global__ __launch_bounds__(FN_T) void k_fn_down(const ChunkSum *__restrict__ s
 #define TAB_LDS (LSLOTS * 12 + MSLOTS * 20)
 #define K3_LDS (TAB_LDS + K3_WAVES * WAVE_LDS)
 
+// LDS count tables are bucketised: 4 keys per 32-byte bucket, read with two
+// 16-byte LDS loads, so a lookup costs one round trip whether it hits or
+// misses (a linear probe chain made the whole wave wait for its slowest lane).
+// A key lives in its bucket or the next; a miss in both goes to HBM.
+#define LB 4
+__device__ __forceinline__ u32 lds_find_s(u64 *lkey, u64 key) {
+    const u32 nb = LSLOTS / LB;
+    u32 b = lds_hash(key) & (nb - 1);
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+        const u32 base = b * LB;
+        const ulonglong2 q0 = *reinterpret_cast<const ulonglong2 *>(&lkey[base]);
+        const ulonglong2 q1 = *reinterpret_cast<const ulonglong2 *>(&lkey[base + 2]);
+        const u64 kk[4] = {q0.x, q0.y, q1.x, q1.y};
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if (kk[i] == key) return base + i;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            if (kk[i] == 0) {
+                const u64 old = atomicCAS((unsigned long long *)&lkey[base + i], 0ull, (unsigned long long)key);
+                if (old == 0 || old == key) return base + i;
+            }
+        }
+        b = (b + 1) & (nb - 1);
+    }
+    return ~0u;
+}
+
+// 9..16-byte keys (k0, k1): claimed by CAS on k0, k1 published after the
+// claim; a prober that finds k0 but not (yet) k1 moves on -- a key may then
+// own two slots, and both flush into the same HBM entry.
+__device__ __forceinline__ u32 lds_find_m(u64 *mk0, u64 *mk1, u64 x0, u64 x1) {
+    const u32 nb = MSLOTS / LB;
+    u32 b = lds_hash(x0 ^ (x1 * 0xC2B2AE3D27D4EB4FULL)) & (nb - 1);
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+        const u32 base = b * LB;
+        const ulonglong2 q0 = *reinterpret_cast<const ulonglong2 *>(&mk0[base]);
+        const ulonglong2 q1 = *reinterpret_cast<const ulonglong2 *>(&mk0[base + 2]);
+        const u64 kk[4] = {q0.x, q0.y, q1.x, q1.y};
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if (kk[i] == x0 && mk1[base + i] == x1) return base + i;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            if (kk[i] == 0) {
+                const u64 old = atomicCAS((unsigned long long *)&mk0[base + i], 0ull, (unsigned long long)x0);
+                if (old == 0) {
+                    mk1[base + i] = x1;
+                    return base + i;
+                }
+            }
+        }
+        b = (b + 1) & (nb - 1);
+    }
+    return ~0u;
+}
+
 // MODE 0 = CSV (records, fields, lyric tokens), 1 = LINES (records only),
 //      2 = FLAT (every byte is lyric text: tokens only, no record structure)
 template <int MODE>
@@ -240,7 +299,6 @@ __global__ __launch_bounds__(K3_THREADS) void k_scan_main(ScanArgs a) {
     const u32 wib = threadIdx.x >> 6;
     unsigned char *wl = smem + TAB_LDS + wib * WAVE_LDS;
     u64 *ring = reinterpret_cast<u64 *>(wl);             // 2 KiB: two 1 KiB iteration slots
-    u64 *bm = reinterpret_cast<u64 *>(wl + 2048);        // token-class bitmap of the ring
     u16 *starts = reinterpret_cast<u16 *>(wl + 2048 + 256);
     const u64 lt = (1ull << lane) - 1ull;
 
@@ -266,18 +324,18 @@ __global__ __launch_bounds__(K3_THREADS) void k_scan_main(ScanArgs a) {
         uint4 nxt = ld16(a.buf + cbase + MSA_ITER + lane * 16);
         if (TOK) {
             reinterpret_cast<uint4 *>(ring)[lane] = cur;
-            reinterpret_cast<u16 *>(bm)[lane] = (u16)tok16(cur, valid_mask(cbase + lane * 16, a.seg_end));
         }
         u32 it = 0;
         for (u64 ibase = cbase; ibase < cend; ibase += MSA_ITER, ++it) {
             const u64 lpos = ibase + lane * 16;
             const u64 npos = ibase + MSA_ITER;
+            u32 tnext = 0;  // token mask of the following 1 KiB (token continuation)
             uint4 nn = ld16(a.buf + npos + MSA_ITER + lane * 16);  // prefetch it+2
             if (TOK) {
                 // stage the following 1 KiB (token continuation only) in the other ring slot
                 const u32 slot = (it + 1) & 1u;
                 reinterpret_cast<uint4 *>(ring)[slot * 64 + lane] = nxt;
-                reinterpret_cast<u16 *>(bm)[slot * 64 + lane] = (u16)tok16(nxt, valid_mask(npos + lane * 16, a.seg_end));
+                tnext = tok16(nxt, valid_mask(npos + lane * 16, a.seg_end));
             }
             const u32 vmask = valid_mask(lpos, cend);
             const Classes k = classify16(cur, vmask);
@@ -374,28 +432,35 @@ __global__ __launch_bounds__(K3_THREADS) void k_scan_main(ScanArgs a) {
             }
 
             if (TOK && !(a.ablate & 1)) {
-                // ---- tokens of the lyric field
+                // ---- tokens of the lyric field (process_lyrics, parallel_spotify.c:350-394)
+                // token starts S; each start's length comes from this lane's token mask
+                // and the next two lanes' (a token of <= 17 bytes spans <= 3 lanes)
                 const u32 upT = __shfl_up(k.T, 1);
                 const u32 pt0 = lane ? ((upT >> 15) & 1u) : prevT;
                 const u32 S = (k.T & live) & ~((k.T << 1) | pt0) & 0xFFFFu;
                 prevT = (readlane(k.T, Lz) >> bz) & 1u;
+                const u32 n0 = readlane(tnext, 0), n1 = readlane(tnext, 1);
+                const u32 d1 = __shfl_down(k.T, 1), d2 = __shfl_down(k.T, 2);
+                const u32 T1 = lane == 63 ? n0 : d1;
+                const u32 T2 = lane == 63 ? n1 : (lane == 62 ? n0 : d2);
+                const u64 win = (u64)k.T | ((u64)T1 << 16) | ((u64)T2 << 32);
                 u32 ntok;
                 u32 idx = wave_prefix<4>(__popc(S), ntok);
-                for (u32 s = S; s; s &= s - 1) starts[idx++] = (u16)(lane * 16 + (__ffs(s) - 1));
+                for (u32 sm = S; sm; sm &= sm - 1) {
+                    const u32 b = __ffs(sm) - 1;
+                    u32 len = (u32)__ffsll((long long)~(win >> b)) - 1u;  // win has >= 33 bits past b
+                    len = len > 63u ? 63u : len;
+                    starts[idx++] = (u16)((lane * 16 + b) | (len << 10));
+                }
                 wave_sync();
                 const u32 slot_off = (it & 1u) << 10;
                 for (u32 t = lane; t < ntok; t += 64) {
-                    const u32 o = slot_off + starts[t];
-                    const u32 wi = o >> 6, bi = o & 63u;
-                    const u64 w = bm[wi] >> bi;
-                    u32 len = (u32)__ffsll((long long)~w) - 1u;
-                    if (len >= 64u - bi) {
-                        const u64 w2 = ~bm[(wi + 1) & 31u];
-                        len = (64u - bi) + (w2 ? (u32)__ffsll((long long)w2) - 1u : 64u);
-                    }
+                    const u32 ent = starts[t];
+                    const u32 len = ent >> 10;
                     if (len < 3) continue;
                     ++words;
                     if (a.ablate & 2) continue;  // ablation: count only
+                    const u32 o = slot_off + (ent & 1023u);
                     if (len > 16) {
                         const u64 i = atomicAdd((unsigned long long *)&a.ctr->l_occ, 1ull);
                         if (i < a.l_cap) a.l_pos[i] = (ibase + (o & 1023u)) | a.lpos_tag;
@@ -409,48 +474,18 @@ __global__ __launch_bounds__(K3_THREADS) void k_scan_main(ScanArgs a) {
                         if (a.ablate & 32) continue;  // ablation: skip S words
                         if (len < 8) k0 &= (1ull << (8 * len)) - 1ull;
                         const u64 key = lower8(k0);
-                        u32 h = lds_hash(key) & (LSLOTS - 1);
-                        bool done = false;
-                        for (u32 p = 0; p < LPROBE; ++p) {
-                            u64 kc = lkey[h];
-                            if (kc == 0) {
-                                kc = atomicCAS((unsigned long long *)&lkey[h], 0ull, (unsigned long long)key);
-                                if (kc == 0) kc = key;
-                            }
-                            if (kc == key) {
-                                atomicAdd(&lcnt[h], 1u);
-                                done = true;
-                                break;
-                            }
-                            h = (h + 1) & (LSLOTS - 1);
-                        }
-                        if (!done && !(a.ablate & 4)) s_insert(a.s_tab, a.s_mask, key, 1, a.s_list, a.s_list_cap, a.ctr);
+                        const u32 slot = lds_find_s(lkey, key);
+                        if (slot != ~0u) atomicAdd(&lcnt[slot], 1u);
+                        else if (!(a.ablate & 4)) s_insert(a.s_tab, a.s_mask, key, 1, a.s_list, a.s_list_cap, a.ctr);
                     } else {
                         const u64 w2 = ring[(q + 2) & 255u];
                         u64 k1 = sh ? ((w1 >> sh) | (w2 << (64 - sh))) : w1;
                         if (len < 16) k1 &= (1ull << (8 * (len - 8))) - 1ull;
                         if (a.ablate & 16) continue;  // ablation: skip M words
                         const u64 x0 = lower8(k0), x1 = lower8(k1);
-                        u32 h = lds_hash(x0 ^ (x1 * 0xC2B2AE3D27D4EB4FULL)) & (MSLOTS - 1);
-                        bool done = false;
-                        for (u32 p = 0; p < LPROBE; ++p) {
-                            u64 c0 = mk0[h];
-                            bool mine = false;
-                            if (c0 == 0) {
-                                c0 = atomicCAS((unsigned long long *)&mk0[h], 0ull, (unsigned long long)x0);
-                                if (c0 == 0) {
-                                    mk1[h] = x1;
-                                    mine = true;
-                                }
-                            }
-                            if (mine || (c0 == x0 && mk1[h] == x1)) {
-                                atomicAdd(&mcnt[h], 1u);
-                                done = true;
-                                break;
-                            }
-                            h = (h + 1) & (MSLOTS - 1);
-                        }
-                        if (!done) m_insert(a.m_tab, a.m_mask, x0, x1, 1, a.m_list, a.m_list_cap, a.ctr);
+                        const u32 slot = lds_find_m(mk0, mk1, x0, x1);
+                        if (slot != ~0u) atomicAdd(&mcnt[slot], 1u);
+                        else m_insert(a.m_tab, a.m_mask, x0, x1, 1, a.m_list, a.m_list_cap, a.ctr);
                     }
                 }
                 wave_sync();
