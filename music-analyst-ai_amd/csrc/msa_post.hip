@@ -183,6 +183,27 @@ __global__ __launch_bounds__(256) void k_col_span(const u8 *__restrict__ buf, co
     span_pairs[r] = pairs;
 }
 
+__device__ __forceinline__ u32 sel4(const uint4 &v, u32 i) {
+    return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w));
+}
+// Bytes [off, off + 16) of the 32-byte window (a, b).
+__device__ __forceinline__ uint4 funnel16(const uint4 &a, const uint4 &b, u32 off) {
+    if (off == 0) return a;
+    const u32 dw = off >> 2, sh = (off & 3) * 8;
+    u32 d[5];
+#pragma unroll
+    for (u32 i = 0; i < 5; ++i) {
+        const u32 k = dw + i;  // 0..7
+        d[i] = k < 4 ? sel4(a, k) : sel4(b, k - 4);
+    }
+    uint4 r;
+    r.x = (u32)((((u64)d[1] << 32) | d[0]) >> sh);
+    r.y = (u32)((((u64)d[2] << 32) | d[1]) >> sh);
+    r.z = (u32)((((u64)d[3] << 32) | d[2]) >> sh);
+    r.w = (u32)((((u64)d[4] << 32) | d[3]) >> sh);
+    return r;
+}
+
 // Segmented gather.  A workgroup owns 256 consecutive lines (their metadata
 // is one coalesced load into LDS) and therefore the contiguous output range
 // [off[r0], off[r0+256]).  Its threads walk the 16-byte slots (aligned in
@@ -191,8 +212,13 @@ __global__ __launch_bounds__(256) void k_col_span(const u8 *__restrict__ buf, co
 // line end, or the range's ragged first/last slot, is written byte by byte
 // (only the bytes this workgroup owns).  Lines whose "" pairs collapse are
 // left to k_col_collapse (one lane each; rare).  Every byte is written once.
+#ifndef CG_T
 #define CG_T 256
+#endif
 #define CG_SLOT 16
+#ifndef CG_MAXS
+#define CG_MAXS 4096
+#endif  // slot->line map capacity (LDS); larger ranges binary-search
 __global__ __launch_bounds__(CG_T) void k_col_gather(const u8 *__restrict__ buf, const u64 *__restrict__ line_len,
                                                      const u64 *__restrict__ line_off,
                                                      const u64 *__restrict__ span_src,
@@ -200,6 +226,8 @@ __global__ __launch_bounds__(CG_T) void k_col_gather(const u8 *__restrict__ buf,
                                                      u8 *__restrict__ col) {
     __shared__ u64 w_off[CG_T + 1], w_src[CG_T];
     __shared__ u32 w_flag[CG_T];  // bit0: line has pairs to collapse
+    __shared__ u32 smap[CG_MAXS];  // slot -> line holding the slot's first byte
+    __shared__ u32 tmax[CG_T];
     const u64 r0 = (u64)blockIdx.x * CG_T;
     const u32 wn = (u32)min((u64)CG_T, nrec - r0);
     const u32 t = threadIdx.x;
@@ -214,37 +242,101 @@ __global__ __launch_bounds__(CG_T) void k_col_gather(const u8 *__restrict__ buf,
     if (O1 <= O0) return;
     const u64 S0 = O0 & ~(u64)(CG_SLOT - 1);
     const u64 nslots = (O1 - S0 + CG_SLOT - 1) / CG_SLOT;
-    for (u64 si = t; si < nslots; si += CG_T) {
-        const u64 A = S0 + si * CG_SLOT;
-        const u64 lo = max(A, O0), hi = min(A + CG_SLOT, O1);
-        // line holding absolute byte lo: last j with hdr + w_off[j] <= lo
-        u32 j = 0, jhi = wn;
-        while (jhi - j > 1) {
-            const u32 mid = (j + jhi) >> 1;
-            if (hdr + w_off[mid] <= lo) j = mid;
-            else jhi = mid;
+    const bool mapped = nslots <= CG_MAXS;
+    if (mapped) {
+        // scatter each line to the first slot starting inside it, then prefix-max
+        for (u32 i = t; i < nslots; i += CG_T) smap[i] = 0;
+        __syncthreads();
+        if (t < wn) {
+            const u64 fs = (hdr + w_off[t] - S0 + CG_SLOT - 1) / CG_SLOT;
+            if (fs < nslots) atomicMax(&smap[fs], (u32)t);
         }
-        const u64 lstart = hdr + w_off[j], lend = hdr + w_off[j + 1];  // line j incl. '\n' at lend-1
-        if (lo == A && hi == A + CG_SLOT && A + CG_SLOT < lend && !w_flag[j]) {
-            const u64 s = w_src[j] + (A - lstart);
-            const u32 *w = reinterpret_cast<const u32 *>(buf + (s & ~3ull));
-            const u32 sh = (u32)(s & 3) * 8;
-            u32 v[5];
+        __syncthreads();
+        const u32 per = (u32)((nslots + CG_T - 1) / CG_T);
+        const u32 a = min((u32)nslots, t * per), b = min((u32)nslots, a + per);
+        u32 m = 0;
+        for (u32 i = a; i < b; ++i) m = max(m, smap[i]);
+        tmax[t] = m;
+        __syncthreads();
+        if (t < 64) {  // exclusive prefix-max of the 256 per-thread maxima, one wave
+            const u32 v0 = tmax[4 * t], v1 = max(v0, tmax[4 * t + 1]), v2 = max(v1, tmax[4 * t + 2]),
+                      v3 = max(v2, tmax[4 * t + 3]);
+            u32 inc = v3;
+            for (u32 o = 1; o < 64; o <<= 1) {
+                const u32 y = __shfl_up(inc, o);
+                if (t >= o) inc = max(inc, y);
+            }
+            u32 ex = __shfl_up(inc, 1);
+            if (t == 0) ex = 0;
+            tmax[4 * t] = ex;
+            tmax[4 * t + 1] = max(ex, v0);
+            tmax[4 * t + 2] = max(ex, v1);
+            tmax[4 * t + 3] = max(ex, v2);
+        }
+        __syncthreads();
+        u32 run = tmax[t];
+        for (u32 i = a; i < b; ++i) { run = max(run, smap[i]); smap[i] = run; }
+        __syncthreads();
+    }
+    // slots in batches of CG_B per thread: every fast-path load of the batch is
+    // issued before the first store (memory-level parallelism)
+#ifndef CG_B
+#define CG_B 4
+#endif
+    for (u64 s0 = t; s0 < nslots; s0 += (u64)CG_B * CG_T) {
+        uint4 va[CG_B], vb[CG_B];
+        u32 jj[CG_B], offb[CG_B];
+        bool fast[CG_B];
 #pragma unroll
-            for (int i = 0; i < 5; ++i) v[i] = w[i];
-            uint4 outv;
-            outv.x = (u32)((((u64)v[1] << 32) | v[0]) >> sh);
-            outv.y = (u32)((((u64)v[2] << 32) | v[1]) >> sh);
-            outv.z = (u32)((((u64)v[3] << 32) | v[2]) >> sh);
-            outv.w = (u32)((((u64)v[4] << 32) | v[3]) >> sh);
-            *reinterpret_cast<uint4 *>(col + A) = outv;
-            continue;
+        for (int k = 0; k < CG_B; ++k) {
+            const u64 si = s0 + (u64)k * CG_T;
+            fast[k] = false;
+            jj[k] = 0;
+            offb[k] = 0;
+            if (si >= nslots) continue;
+            const u64 A = S0 + si * CG_SLOT;
+            const u64 lo = max(A, O0), hi = min(A + CG_SLOT, O1);
+            u32 j;
+            if (mapped) {
+                j = smap[si];
+            } else {  // last j with hdr + w_off[j] <= lo
+                u32 jl = 0, jh = wn;
+                while (jh - jl > 1) {
+                    const u32 mid = (jl + jh) >> 1;
+                    if (hdr + w_off[mid] <= lo) jl = mid;
+                    else jh = mid;
+                }
+                j = jl;
+            }
+            while (j + 1 < wn && hdr + w_off[j + 1] <= lo) ++j;  // skip empty lines
+            jj[k] = j;
+            const u64 lstart = hdr + w_off[j], lend = hdr + w_off[j + 1];  // '\n' at lend-1
+            if (lo == A && hi == A + CG_SLOT && A + CG_SLOT < lend && !w_flag[j]) {
+                const u64 src = w_src[j] + (A - lstart);
+                const uint4 *p = reinterpret_cast<const uint4 *>(buf + (src & ~15ull));
+                va[k] = p[0];
+                vb[k] = p[1];
+                offb[k] = (u32)(src & 15);
+                fast[k] = true;
+            }
         }
-        for (u64 p = lo; p < hi; ++p) {
-            while (p >= hdr + w_off[j + 1]) ++j;
-            if (w_flag[j]) continue;  // k_col_collapse writes this line
-            const u64 ls = hdr + w_off[j], le = hdr + w_off[j + 1];
-            col[p] = (p + 1 == le) ? (u8)'\n' : buf[w_src[j] + (p - ls)];
+#pragma unroll
+        for (int k = 0; k < CG_B; ++k) {
+            const u64 si = s0 + (u64)k * CG_T;
+            if (si >= nslots) continue;
+            const u64 A = S0 + si * CG_SLOT;
+            if (fast[k]) {
+                *reinterpret_cast<uint4 *>(col + A) = funnel16(va[k], vb[k], offb[k]);
+                continue;
+            }
+            const u64 lo = max(A, O0), hi = min(A + CG_SLOT, O1);
+            u32 j = jj[k];
+            for (u64 p = lo; p < hi; ++p) {
+                while (p >= hdr + w_off[j + 1]) ++j;
+                if (w_flag[j]) continue;  // k_col_collapse writes this line
+                const u64 ls = hdr + w_off[j], le = hdr + w_off[j + 1];
+                col[p] = (p + 1 == le) ? (u8)'\n' : buf[w_src[j] + (p - ls)];
+            }
         }
     }
 }

@@ -213,13 +213,22 @@ __global__ __launch_bounds__(FN_T) void k_fn_down(const ChunkSum *__restrict__ s
 
 // ---------------------------------------------------------------------------
 // K3: the main pass.
+#ifndef K3_THREADS
 #define K3_THREADS 512
+#endif
 #define K3_WAVES (K3_THREADS / 64)
+#ifndef LSLOTS
 #define LSLOTS 2048
+#endif
+#ifndef MSLOTS
 #define MSLOTS 1024
+#endif
+#ifndef K3_BLOCKS_PER_CU
+#define K3_BLOCKS_PER_CU 2
+#endif
 #define LPROBE 8
 #define WAVE_LDS (2048 + 256 + 1024)
-#define TAB_LDS (LSLOTS * 12 + MSLOTS * 20)
+#define TAB_LDS (LSLOTS * 12 + MSLOTS * 20 + (K3_DOORKEEPER ? DK_WORDS * 4 : 0))
 #define K3_LDS (TAB_LDS + K3_WAVES * WAVE_LDS)
 
 // LDS count tables are bucketised: 4 keys per 32-byte bucket, read with two
@@ -227,7 +236,19 @@ __global__ __launch_bounds__(FN_T) void k_fn_down(const ChunkSum *__restrict__ s
 // misses (a linear probe chain made the whole wave wait for its slowest lane).
 // A key lives in its bucket or the next; a miss in both goes to HBM.
 #define LB 4
-__device__ __forceinline__ u32 lds_find_s(u64 *lkey, u64 key) {
+#ifndef K3_DOORKEEPER
+#define K3_DOORKEEPER 0
+#endif
+#define DK_WORDS 2048  // doorkeeper bitset: 64 Ki bits of LDS
+// Admission filter: a key claims an LDS slot only on its second sighting in
+// this workgroup, so words seen once (the Zipf tail) do not fill the table.
+__device__ __forceinline__ bool dk_admit(u32 *dk, u64 h) {
+    if (!K3_DOORKEEPER) return true;
+    const u32 bit = (u32)(h >> 17) & (DK_WORDS * 32 - 1);
+    const u32 m = 1u << (bit & 31);
+    return (atomicOr(&dk[bit >> 5], m) & m) != 0;
+}
+__device__ __forceinline__ u32 lds_find_s(u64 *lkey, u32 *dk, u64 key) {
     const u32 nb = LSLOTS / LB;
     u32 b = lds_hash(key) & (nb - 1);
 #pragma unroll
@@ -239,6 +260,8 @@ __device__ __forceinline__ u32 lds_find_s(u64 *lkey, u64 key) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
             if (kk[i] == key) return base + i;
+        if (p == 0 && (kk[0] == 0 || kk[1] == 0 || kk[2] == 0 || kk[3] == 0) && !dk_admit(dk, key * 0x9E3779B97F4A7C15ULL))
+            return ~0u;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             if (kk[i] == 0) {
@@ -254,7 +277,7 @@ __device__ __forceinline__ u32 lds_find_s(u64 *lkey, u64 key) {
 // 9..16-byte keys (k0, k1): claimed by CAS on k0, k1 published after the
 // claim; a prober that finds k0 but not (yet) k1 moves on -- a key may then
 // own two slots, and both flush into the same HBM entry.
-__device__ __forceinline__ u32 lds_find_m(u64 *mk0, u64 *mk1, u64 x0, u64 x1) {
+__device__ __forceinline__ u32 lds_find_m(u64 *mk0, u64 *mk1, u32 *dk, u64 x0, u64 x1) {
     const u32 nb = MSLOTS / LB;
     u32 b = lds_hash(x0 ^ (x1 * 0xC2B2AE3D27D4EB4FULL)) & (nb - 1);
 #pragma unroll
@@ -266,6 +289,9 @@ __device__ __forceinline__ u32 lds_find_m(u64 *mk0, u64 *mk1, u64 x0, u64 x1) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
             if (kk[i] == x0 && mk1[base + i] == x1) return base + i;
+        if (p == 0 && (kk[0] == 0 || kk[1] == 0 || kk[2] == 0 || kk[3] == 0) &&
+            !dk_admit(dk, (x0 ^ (x1 * 0xC2B2AE3D27D4EB4FULL)) * 0x9E3779B97F4A7C15ULL))
+            return ~0u;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             if (kk[i] == 0) {
@@ -295,6 +321,7 @@ __global__ __launch_bounds__(K3_THREADS) void k_scan_main(ScanArgs a) {
     u64 *mk0 = reinterpret_cast<u64 *>(smem + LSLOTS * 12);
     u64 *mk1 = mk0 + MSLOTS;
     u32 *mcnt = reinterpret_cast<u32 *>(mk1 + MSLOTS);
+    u32 *dk = mcnt + MSLOTS;  // doorkeeper bitset (K3_DOORKEEPER)
     const u32 lane = lane_id();
     const u32 wib = threadIdx.x >> 6;
     unsigned char *wl = smem + TAB_LDS + wib * WAVE_LDS;
@@ -305,6 +332,8 @@ __global__ __launch_bounds__(K3_THREADS) void k_scan_main(ScanArgs a) {
     if (TOK) {
         for (u32 i = threadIdx.x; i < LSLOTS; i += K3_THREADS) { lkey[i] = 0; lcnt[i] = 0; }
         for (u32 i = threadIdx.x; i < MSLOTS; i += K3_THREADS) { mk0[i] = 0; mk1[i] = 0; mcnt[i] = 0; }
+        if (K3_DOORKEEPER)
+            for (u32 i = threadIdx.x; i < DK_WORDS; i += K3_THREADS) dk[i] = 0;
         __syncthreads();
     }
     const u32 gw = blockIdx.x * K3_WAVES + wib;
@@ -474,7 +503,7 @@ __global__ __launch_bounds__(K3_THREADS) void k_scan_main(ScanArgs a) {
                         if (a.ablate & 32) continue;  // ablation: skip S words
                         if (len < 8) k0 &= (1ull << (8 * len)) - 1ull;
                         const u64 key = lower8(k0);
-                        const u32 slot = lds_find_s(lkey, key);
+                        const u32 slot = lds_find_s(lkey, dk, key);
                         if (slot != ~0u) atomicAdd(&lcnt[slot], 1u);
                         else if (!(a.ablate & 4)) s_insert(a.s_tab, a.s_mask, key, 1, a.s_list, a.s_list_cap, a.ctr);
                     } else {
@@ -483,7 +512,7 @@ __global__ __launch_bounds__(K3_THREADS) void k_scan_main(ScanArgs a) {
                         if (len < 16) k1 &= (1ull << (8 * (len - 8))) - 1ull;
                         if (a.ablate & 16) continue;  // ablation: skip M words
                         const u64 x0 = lower8(k0), x1 = lower8(k1);
-                        const u32 slot = lds_find_m(mk0, mk1, x0, x1);
+                        const u32 slot = lds_find_m(mk0, mk1, dk, x0, x1);
                         if (slot != ~0u) atomicAdd(&mcnt[slot], 1u);
                         else m_insert(a.m_tab, a.m_mask, x0, x1, 1, a.m_list, a.m_list_cap, a.ctr);
                     }
@@ -549,7 +578,7 @@ hipError_t msa_launch_fn(const ChunkSum *sums, u64 seg_begin, u32 nchunks, Fn *b
 hipError_t msa_launch_scan(const ScanArgs &a, int mode, hipStream_t s) {
     if (!a.nchunks) return hipSuccess;
     u32 blocks = (a.nchunks + K3_WAVES - 1) / K3_WAVES;
-    u32 cap = (u32)num_cus() * 2;
+    u32 cap = (u32)num_cus() * K3_BLOCKS_PER_CU;
     if (blocks > cap) blocks = cap;
     static bool attr = false;
     if (!attr) {

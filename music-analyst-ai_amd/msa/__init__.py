@@ -14,7 +14,7 @@ from dataclasses import dataclass
 from typing import Dict, List, Optional, Tuple
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "libmsa_hip.so")
+LIB_PATH = os.environ.get("MSA_LIB") or os.path.join(PKG_DIR, "libmsa_hip.so")
 CLI_PATH = os.path.join(PKG_DIR, "bin", "parallel_spotify")
 GEN_PATH = os.path.join(PKG_DIR, "bin", "msa_gen")
 
