@@ -15,11 +15,12 @@
  *                       640-721, header handling in main 788-827
  *   msa_count           the text / artist rank loops of main 853-999,
  *                       process_lyrics 350-394, ht_put 126-149
- *   msa_shard_*         (multi-GPU) the even byte split of main 866-882,
- *                       done exactly instead of at raw byte offsets
- *   msa_export_partition / msa_merge_partition
+ *   msa_set_shard / msa_shard_function / msa_shard_head / msa_segment_*
+ *                       (multi-GPU) the even byte split + re-sync of main
+ *                       866-916, done exactly instead of at raw byte offsets
+ *   msa_export_partitions / msa_export_copy / msa_import_partitions
  *                       send_hash_table 397-410, receive_hash_table 413-432,
- *                       ht_merge 152-158
+ *                       ht_merge 152-158, the merge loop of main 1011-1025
  *   msa_rank            ht_to_array 161-175 + qsort(entry_compare_desc)
  *                       178-188 inside write_table_csv 325-344
  *   msa_write_table_csv write_table_csv 325-344 / write_csv_entry 307-319
@@ -154,16 +155,59 @@ int msa_set_profiling(msa_ctx *ctx, int on);
 int msa_get_profile(msa_ctx *ctx, msa_profile *out, int reset);
 
 /* ------------------------------------------------- multi-GPU (one process
- * per GPU; the caller moves bytes with RCCL).  A shard is a contiguous byte
- * range of one logical CSV; shard 0 holds the header. */
+ * per GPU; the caller moves bytes between GPUs, e.g. with RCCL all-to-all).
+ * A shard is a contiguous byte range of ONE logical CSV; shard 0 holds the
+ * header row.  Replaces the reference's even byte split of the column files
+ * plus per-rank re-synchronisation (parallel_spotify.c:866-916), which loses
+ * or double-counts records at the cut points; here every record is processed
+ * exactly once by the GPU whose shard holds its first byte.
+ *
+ *   1. msa_set_shard(ctx, rank == 0); msa_load_csv(ctx, shard)
+ *   2. fn = msa_shard_function(ctx, MSA_PIECE_CSV)      -> all-gather the fns
+ *   3. msa_shard_head(ctx, MSA_PIECE_CSV, fns[0..rank), sizes, &head)
+ *      -> all-gather heads; a head (bytes of an earlier shard's last record)
+ *         goes to the nearest earlier rank whose head < its size
+ *   4. msa_segment_set(ctx, MSA_PIECE_CSV, head, tail)  (tail = later heads)
+ *   5. msa_split_columns; then steps 2-4 again on MSA_PIECE_ARTISTS (the
+ *      artist.csv reader may also carry state across pieces); msa_count
+ *   6. msa_export_partitions / msa_export_copy -> all-to-all ->
+ *      msa_import_partitions (words, artists); msa_rank ranks each GPU's
+ *      key partition; the caller gathers the ranked partitions.            */
 
-/* Transfer function of this shard's bytes over the record-reader state, as
- * MSA_SHARD_FN_BYTES opaque bytes (all-gather them across ranks). */
-#define MSA_SHARD_FN_BYTES 64
-int msa_shard_function(msa_ctx *ctx, void *fn_out);
-/* Feed the functions of all shards before this one (in order), so the shard
- * starts in the exact reader state of the single-file scan. */
-int msa_shard_set_prefix(msa_ctx *ctx, const void *fns, int nshards_before);
+enum { MSA_PIECE_CSV = 0, MSA_PIECE_ARTISTS = 1 };
+
+typedef struct {
+    uint64_t nterm, rs;
+    uint32_t p, cr, has, c, z, pad;
+} msa_fn_entry;
+/* Transfer function of a piece over the reader state (quote parity, pending
+ * '\r', field commas, NUL, record count, open-record start). */
+typedef struct {
+    msa_fn_entry e[3];
+} msa_shard_fn;
+
+/* first != 0: this context holds shard 0 (with the header row). */
+int msa_set_shard(msa_ctx *ctx, int first);
+/* Bytes of the raw piece (the loaded shard / this shard's artist.csv body). */
+int msa_piece_size(msa_ctx *ctx, int piece, uint64_t *len);
+int msa_shard_function(msa_ctx *ctx, int piece, msa_shard_fn *out);
+/* State after the pieces before this one (fns/sizes of ranks 0..nbefore-1)
+ * -> number of leading bytes of this piece that belong to a record begun in
+ * an earlier piece. */
+int msa_shard_head(msa_ctx *ctx, int piece, const msa_shard_fn *before, int nbefore, const uint64_t *sizes,
+                   uint64_t *head);
+/* Copy bytes [off, off+len) of the raw piece to dst (host or device). */
+int msa_segment_copy(msa_ctx *ctx, int piece, uint64_t off, uint64_t len, void *dst);
+/* Process [skip, size) of the piece followed by tail (host or device bytes). */
+int msa_segment_set(msa_ctx *ctx, int piece, uint64_t skip, const void *tail, uint64_t tail_len);
+
+/* Serialise the counted table as nparts key-hash partitions (wire format in
+ * csrc/msa_merge.hip); part_bytes[p] = bytes of partition p's block.      */
+int msa_export_partitions(msa_ctx *ctx, int table, int nparts, uint64_t *part_bytes);
+int msa_export_copy(msa_ctx *ctx, void *dst);
+/* Replace the table by the union of the received blocks (counts summed);
+ * blk_off[0..nblk] are the blocks' byte offsets in src (last = total).     */
+int msa_import_partitions(msa_ctx *ctx, int table, const void *src, const uint64_t *blk_off, int nblk);
 
 #ifdef __cplusplus
 }

@@ -23,7 +23,16 @@ hipError_t msa_launch_fn(const ChunkSum *, u64, u32, Fn *, State *, Fn *, const 
 hipError_t msa_launch_scan(const ScanArgs &, int, hipStream_t);
 hipError_t msa_exclusive_scan(const u64 *, u64, u64 *, u64 *, u64 *, hipStream_t);
 hipError_t msa_launch_col_span(int, const u8 *, const u64 *, const u64 *, const u32 *, const u32 *, const u32 *, u64,
-                               u64 *, u64 *, u32 *, hipStream_t);
+                               u64, u64 *, u64 *, u32 *, hipStream_t);
+hipError_t msa_launch_first_end(const u8 *, u64, u32, u32, u64 *, hipStream_t);
+hipError_t msa_launch_artist_verify(const u8 *, const u64 *, const u32 *, const u64 *, u64, const u64 *, Counters *,
+                                    hipStream_t);
+hipError_t msa_launch_long_verify(const u8 *, const u8 *, const u64 *, const u32 *, const u64 *, u64, const u64 *,
+                                  Counters *, hipStream_t);
+hipError_t msa_launch_exp_count(const ExpSrc &, u64, u32, u64 *, u64 *, hipStream_t);
+hipError_t msa_launch_exp_write(const ExpSrc &, u64, u32, const u64 *, const u64 *, const u64 *, u64 *, u64 *, u8 *,
+                                hipStream_t);
+hipError_t msa_launch_imp(const u8 *, const u64 *, u32, u64 *, u64, const ImpDst &, hipStream_t);
 hipError_t msa_launch_col_write(const u8 *, const u64 *, const u64 *, const u64 *, const u32 *, u64, u64, u64, u8 *,
                                 hipStream_t);
 hipError_t msa_launch_artist_key(const u8 *, const u64 *, const u64 *, u64, u8 *, u64 *, u32 *, u64 *, u64 *, u64,
@@ -102,8 +111,16 @@ struct msa_ctx {
     std::string err;
     // input
     DevBuf in_own;
-    const u8 *in = nullptr;
+    const u8 *in = nullptr;  // the segment processed (a view of the input)
     u64 n = 0;
+    const u8 *in_base = nullptr;  // the loaded / bound input itself
+    u64 n_base = 0;
+    bool cont = false;  // continuation shard: no header row (multi-GPU)
+    u64 a_beg = 0, a_end = 0;  // artist.csv segment the artist pass reads
+    // multi-GPU merge
+    DevBuf exp_buf, exp_meta, imp_w, imp_a, imp_meta;
+    u64 exp_bytes = 0;
+    bool merged_w = false, merged_a = false;
     // scan scratch
     DevBuf sums, carry, btot, bstate, small;  // small: Fn total + 2 States + ...
     // CSV records
@@ -419,7 +436,7 @@ static int materialise_column(msa_ctx *c, bool text, const std::string &hdr_line
     HIPC(c, ensure(srcb, nrec * 8));
     HIPC(c, ensure(pairsb, nrec * 4));
     HIPC(c, msa_launch_col_span(text ? 1 : 0, c->in, c->rec_start.as<u64>(), c->rec_term.as<u64>(), c->f0rel.as<u32>(),
-                                c->f3rel.as<u32>(), c->nulrel.as<u32>(), nrec, lenb.as<u64>(), srcb.as<u64>(),
+                                c->f3rel.as<u32>(), c->nulrel.as<u32>(), nrec, c->cont ? 0 : 1, lenb.as<u64>(), srcb.as<u64>(),
                                 pairsb.as<u32>(), c->stream));
     HIPC(c, msa_exclusive_scan(lenb.as<u64>(), nrec, offb.as<u64>(), c->scan_bsum.as<u64>(), c->scan_total.as<u64>(),
                                c->stream));
@@ -436,11 +453,36 @@ static int materialise_column(msa_ctx *c, bool text, const std::string &hdr_line
     return MSA_OK;
 }
 
+// Column materialisation after the scan.  ah / th are the header lines of
+// artist.csv / text.csv (empty for a continuation shard).
+static int split_columns_rest(msa_ctx *c, bool want_text, const std::string &ah, const std::string &th) {
+    int rc;
+    prof_begin(c, ST_ARTIST_COLUMN);
+    if ((rc = materialise_column(c, false, ah, c->acol, c->alen, c->aoff, c->asrc, c->apairs, &c->acol_len))) return rc;
+    prof_end(c, ST_ARTIST_COLUMN, c->acol_len * 2 + c->nrec * 32);
+    // compute_header_length (parallel_spotify.c:444-459): getline's end
+    c->a_hdr_getline = ah.empty() ? 0 : ah.find('\n') + 1;
+    c->a_beg = c->a_hdr_getline;
+    c->a_end = c->acol_len;
+    c->have_tcol = false;
+    if (want_text) {
+        prof_begin(c, ST_TEXT_COLUMN);
+        if ((rc = materialise_column(c, true, th, c->tcol, c->tlen, c->toff, c->tsrc, c->tpairs, &c->tcol_len)))
+            return rc;
+        prof_end(c, ST_TEXT_COLUMN, c->tcol_len * 2 + c->nrec * 40);
+        c->have_tcol = true;
+    }
+    c->stage = 1;
+    return MSA_OK;
+}
+
 static int do_split(msa_ctx *c, int flags) {
     int rc;
     if (!c->in) return fail(c, MSA_ERR_ARG, "no input bound (msa_load_csv / msa_bind_csv)");
-    if (c->n == 0) return fail(c, MSA_ERR_NOHEADER, "Dataset does not contain a header row");
+    if (c->n == 0 && !c->cont) return fail(c, MSA_ERR_NOHEADER, "Dataset does not contain a header row");
     const bool want_text = (flags & MSA_SPLIT_TEXT_COLUMN) != 0;
+    c->merged_w = c->merged_a = false;
+    c->extra_len = 0;
     HIPC(c, ensure(c->ctr, sizeof(Counters)));
     if ((rc = clear_tables(c))) return rc;
     HIPC(c, hipMemsetAsync(c->ctr.p, 0, sizeof(Counters), c->stream));
@@ -488,6 +530,7 @@ static int do_split(msa_ctx *c, int flags) {
     a.ctr = c->ctr.as<Counters>();
     a.want_term = want_text ? 1 : 0;
     a.ablate = c->ablate;
+    a.first_rec = c->cont ? 0 : 1;
     prof_begin(c, ST_CSV_SCAN);
     HIPC(c, msa_launch_scan(a, 0, c->stream));
     // algorithmic bytes: every CSV byte once + the per-record SoA it writes
@@ -497,6 +540,7 @@ static int do_split(msa_ctx *c, int flags) {
         u64 v = c->n;
         HIPC(c, hipMemcpyAsync(c->rec_term.as<u64>() + (c->nrec - 1), &v, 8, hipMemcpyHostToDevice, c->stream));
     }
+    if (c->cont) return split_columns_rest(c, want_text, std::string(), std::string());
     // header record = record 0
     u64 hend = c->n;
     if (nterm > 0) {
@@ -544,33 +588,20 @@ static int do_split(msa_ctx *c, int flags) {
         }
     }
     std::string ah = c->sum.artist_label[0] ? c->sum.artist_label : "Artists";
+    std::string th = c->sum.text_label[0] ? c->sum.text_label : "Texts";
     ah.push_back('\n');
-    prof_begin(c, ST_ARTIST_COLUMN);
-    if ((rc = materialise_column(c, false, ah, c->acol, c->alen, c->aoff, c->asrc, c->apairs, &c->acol_len))) return rc;
-    prof_end(c, ST_ARTIST_COLUMN, c->acol_len * 2 + c->nrec * 32);
-    {
-        size_t p = ah.find('\n');
-        c->a_hdr_getline = p + 1;  // compute_header_length (parallel_spotify.c:444-459)
-    }
-    c->have_tcol = false;
-    if (want_text) {
-        std::string th = c->sum.text_label[0] ? c->sum.text_label : "Texts";
-        th.push_back('\n');
-        prof_begin(c, ST_TEXT_COLUMN);
-        if ((rc = materialise_column(c, true, th, c->tcol, c->tlen, c->toff, c->tsrc, c->tpairs, &c->tcol_len))) return rc;
-        prof_end(c, ST_TEXT_COLUMN, c->tcol_len * 2 + c->nrec * 40);
-        c->have_tcol = true;
-    }
-    c->stage = 1;
-    return MSA_OK;
+    th.push_back('\n');
+    return split_columns_rest(c, want_text, ah, th);
 }
+
 
 // ------------------------------------------------------------------ stage 2
 static int do_count(msa_ctx *c) {
     int rc;
     if (c->stage < 1) return fail(c, MSA_ERR_ARG, "msa_count before msa_split_columns");
-    // artist pass over artist.csv records from its getline header end
-    const u64 b = c->a_hdr_getline, e = c->acol_len;
+    // artist pass over artist.csv records from its getline header end (or the
+    // segment msa_segment_set chose for a shard)
+    const u64 b = c->a_beg, e = c->a_end;
     State init{0, b, 0, 0, 0, 0}, fin;
     if ((rc = run_scan_fn(c, c->acol.as<u8>(), b, e, init, &fin, ST_ARTIST_SUMMARY))) return rc;
     const u64 nterm = fin.rec;
@@ -634,7 +665,8 @@ static int do_count(msa_ctx *c) {
 }
 
 // ------------------------------------------------------------------ stage 3
-static int sort_and_blob(msa_ctx *c, Ranked &R, const u8 *arena, const u64 *key_off, const u32 *key_len) {
+static int sort_and_blob(msa_ctx *c, Ranked &R, const u8 *wbuf, const u8 *wextra, const u8 *arena, const u64 *key_off,
+                         const u32 *key_len) {
     const u64 n = R.n;
     R.host_valid = false;
     if (n == 0) {
@@ -671,7 +703,7 @@ static int sort_and_blob(msa_ctx *c, Ranked &R, const u8 *arena, const u64 *key_
     }
     HIPC(c, ensure(R.order, n * 4));
     HIPC(c, msa_launch_fixup(R.K[cur][0].as<u64>(), R.K[cur][1].as<u64>(), R.K[cur][2].as<u64>(), R.V[cur].as<u32>(),
-                             n, R.ref.as<u64>(), c->in, c->extra.as<u8>(), c->l_pos.as<u64>(), c->l_len.as<u32>(), arena, key_off,
+                             n, R.ref.as<u64>(), wbuf, wextra, c->l_pos.as<u64>(), c->l_len.as<u32>(), arena, key_off,
                              key_len, R.order.as<u32>(), c->stream));
     // key blob in rank order
     HIPC(c, ensure(R.len, n * 8));
@@ -680,14 +712,14 @@ static int sort_and_blob(msa_ctx *c, Ranked &R, const u8 *arena, const u64 *key_
     HIPC(c, ensure(c->scan_total, 64));
     HIPC(c, ensure(c->scan_bsum, ((n + 1023) / 1024 + 1) * 8));
     HIPC(c, msa_launch_blob(R.order.as<u32>(), n, R.ref.as<u64>(), R.K[0][1].as<u64>(), R.K[0][2].as<u64>(),
-                            R.cnt.as<u64>(), c->in, c->extra.as<u8>(), c->l_pos.as<u64>(), c->l_len.as<u32>(), arena, key_off, key_len,
+                            R.cnt.as<u64>(), wbuf, wextra, c->l_pos.as<u64>(), c->l_len.as<u32>(), arena, key_off, key_len,
                             R.len.as<u64>(), R.off.as<u64>(), c->scan_bsum.as<u64>(), c->scan_total.as<u64>(), nullptr,
                             nullptr, c->stream, 0));
     HIPC(c, hipMemcpyAsync(&R.blob_len, c->scan_total.p, 8, hipMemcpyDeviceToHost, c->stream));
     HIPC(c, hipStreamSynchronize(c->stream));
     HIPC(c, ensure(R.blob, R.blob_len + 16));
     HIPC(c, msa_launch_blob(R.order.as<u32>(), n, R.ref.as<u64>(), R.K[0][1].as<u64>(), R.K[0][2].as<u64>(),
-                            R.cnt.as<u64>(), c->in, c->extra.as<u8>(), c->l_pos.as<u64>(), c->l_len.as<u32>(), arena, key_off, key_len,
+                            R.cnt.as<u64>(), wbuf, wextra, c->l_pos.as<u64>(), c->l_len.as<u32>(), arena, key_off, key_len,
                             R.len.as<u64>(), R.off.as<u64>(), c->scan_bsum.as<u64>(), c->scan_total.as<u64>(),
                             R.blob.as<u8>(), R.counts.as<u64>(), c->stream, 1));
     return MSA_OK;
@@ -715,8 +747,8 @@ static int do_rank(msa_ctx *c) {
         ea.l_tab = c->l_tab.as<u64>();
         ea.l_list = c->l_list.as<u32>();
         ea.nl = c->h_ctr.l_claimed;
-        ea.buf = c->in;
-        ea.extra = c->extra.as<u8>();
+        ea.buf = c->merged_w ? c->imp_w.as<u8>() : c->in;
+        ea.extra = c->merged_w ? c->imp_w.as<u8>() : c->extra.as<u8>();
         ea.l_pos = c->l_pos.as<u64>();
         ea.l_len = c->l_len.as<u32>();
         ea.K2 = W.K[0][0].as<u64>();
@@ -727,7 +759,9 @@ static int do_rank(msa_ctx *c) {
         ea.cnt = W.cnt.as<u64>();
         HIPC(c, msa_launch_word_entries(ea, c->stream));
     }
-    if ((rc = sort_and_blob(c, W, nullptr, nullptr, nullptr))) return rc;
+    const u8 *wbuf = c->merged_w ? c->imp_w.as<u8>() : c->in;
+    const u8 *wextra = c->merged_w ? c->imp_w.as<u8>() : c->extra.as<u8>();
+    if ((rc = sort_and_blob(c, W, wbuf, wextra, nullptr, nullptr, nullptr))) return rc;
     prof_end(c, ST_RANK_WORDS, W.n * 64 + W.blob_len);
     // artists
     Ranked &A = c->ra;
@@ -738,12 +772,14 @@ static int do_rank(msa_ctx *c) {
         HIPC(c, ensure(A.V[0], A.n * 4));
         HIPC(c, ensure(A.ref, A.n * 8));
         HIPC(c, ensure(A.cnt, A.n * 8));
-        HIPC(c, msa_launch_artist_entries(c->a_tab.as<u64>(), c->a_list.as<u32>(), A.n, c->arena.as<u8>(),
+        HIPC(c, msa_launch_artist_entries(c->a_tab.as<u64>(), c->a_list.as<u32>(), A.n,
+                                          c->merged_a ? c->imp_a.as<u8>() : c->arena.as<u8>(),
                                           c->key_off.as<u64>(), c->key_len.as<u32>(), A.K[0][0].as<u64>(),
                                           A.K[0][1].as<u64>(), A.K[0][2].as<u64>(), A.V[0].as<u32>(), A.ref.as<u64>(),
                                           A.cnt.as<u64>(), c->stream));
     }
-    if ((rc = sort_and_blob(c, A, c->arena.as<u8>(), c->key_off.as<u64>(), c->key_len.as<u32>()))) return rc;
+    const u8 *aarena = c->merged_a ? c->imp_a.as<u8>() : c->arena.as<u8>();
+    if ((rc = sort_and_blob(c, A, wbuf, wextra, aarena, c->key_off.as<u64>(), c->key_len.as<u32>()))) return rc;
     prof_end(c, ST_RANK_ARTISTS, A.n * 64 + A.blob_len);
     HIPC(c, hipStreamSynchronize(c->stream));
     c->stage = 3;
@@ -795,7 +831,7 @@ void msa_destroy(msa_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
-    DevBuf *all[] = {&c->in_own, &c->sums, &c->carry, &c->btot, &c->bstate, &c->small, &c->rec_start, &c->rec_term, &c->extra,
+    DevBuf *all[] = {&c->in_own, &c->sums, &c->carry, &c->btot, &c->bstate, &c->small, &c->rec_start, &c->rec_term, &c->extra, &c->exp_buf, &c->exp_meta, &c->imp_w, &c->imp_a, &c->imp_meta,
                      &c->f0rel, &c->f3rel, &c->nulrel, &c->acol, &c->alen, &c->aoff, &c->asrc, &c->apairs, &c->tcol, &c->tlen, &c->toff, &c->tsrc, &c->tpairs,
                      &c->scan_bsum, &c->scan_total, &c->ar_start, &c->ar_term, &c->arena, &c->key_off,
                      &c->key_len, &c->key_slot, &c->s_tab, &c->s_list, &c->m_tab, &c->m_list, &c->l_pos, &c->l_len,
@@ -834,6 +870,8 @@ int msa_load_csv(msa_ctx *c, const void *host, size_t n) {
     HIPC(c, hipMemset(c->in_own.as<char>() + n, 0, MSA_INPUT_PAD));
     c->in = c->in_own.as<u8>();
     c->n = n;
+    c->in_base = c->in;
+    c->n_base = n;
     c->stage = 0;
     return MSA_OK;
 }
@@ -842,6 +880,8 @@ int msa_bind_csv(msa_ctx *c, const void *dev, size_t n) {
     if (!c || (!dev && n)) return MSA_ERR_ARG;
     c->in = reinterpret_cast<const u8 *>(dev);
     c->n = n;
+    c->in_base = c->in;
+    c->n_base = n;
     c->stage = 0;
     return MSA_OK;
 }
@@ -988,16 +1028,328 @@ int msa_get_profile(msa_ctx *c, msa_profile *out, int reset) {
     return MSA_OK;
 }
 
-int msa_shard_function(msa_ctx *c, void *fn_out) {
-    if (!c || !fn_out) return MSA_ERR_ARG;
-    return fail(c, MSA_ERR_ARG, "multi-shard scan not available in this build");
+static_assert(sizeof(msa_fn_entry) == sizeof(FnEnt), "msa_fn_entry mirrors FnEnt");
+static_assert(sizeof(msa_shard_fn) == sizeof(Fn), "msa_shard_fn mirrors Fn");
+
+int msa_set_shard(msa_ctx *c, int first) {
+    if (!c) return MSA_ERR_ARG;
+    c->cont = first == 0;
+    return MSA_OK;
 }
 
-int msa_shard_set_prefix(msa_ctx *c, const void *fns, int nshards_before) {
-    (void)fns;
-    (void)nshards_before;
-    if (!c) return MSA_ERR_ARG;
-    return fail(c, MSA_ERR_ARG, "multi-shard scan not available in this build");
+// The raw piece: the loaded CSV shard, or this shard's artist.csv body.
+static int piece_of(msa_ctx *c, int piece, const u8 **base, u64 *len) {
+    if (piece == MSA_PIECE_CSV) {
+        if (!c->in_base) return fail(c, MSA_ERR_ARG, "no input bound");
+        *base = c->in_base;
+        *len = c->n_base;
+        return MSA_OK;
+    }
+    if (piece == MSA_PIECE_ARTISTS) {
+        if (c->stage < 1) return fail(c, MSA_ERR_ARG, "artist piece before msa_split_columns");
+        *base = c->acol.as<u8>() + c->a_hdr_getline;
+        *len = c->acol_len - c->a_hdr_getline;
+        return MSA_OK;
+    }
+    return fail(c, MSA_ERR_ARG, "bad piece %d", piece);
+}
+
+int msa_piece_size(msa_ctx *c, int piece, uint64_t *len) {
+    if (!c || !len) return MSA_ERR_ARG;
+    const u8 *base;
+    u64 n;
+    int rc;
+    if ((rc = piece_of(c, piece, &base, &n))) return rc;
+    *len = n;
+    return MSA_OK;
+}
+
+int msa_shard_function(msa_ctx *c, int piece, msa_shard_fn *out) {
+    if (!c || !out) return MSA_ERR_ARG;
+    HIPC(c, hipSetDevice(c->device));
+    const u8 *base;
+    u64 len;
+    int rc;
+    if ((rc = piece_of(c, piece, &base, &len))) return rc;
+    Fn f = fn_identity(0);
+    if (len) {
+        State init{0, 0, 0, 0, 0, 0}, fin;
+        if ((rc = run_scan_fn(c, base, 0, len, init, &fin, piece ? ST_ARTIST_SUMMARY : ST_CSV_SUMMARY))) return rc;
+        HIPC(c, hipMemcpy(&f, c->small.p, sizeof(Fn), hipMemcpyDeviceToHost));  // k_fn_top's total
+    }
+    memcpy(out, &f, sizeof f);
+    return MSA_OK;
+}
+
+int msa_shard_head(msa_ctx *c, int piece, const msa_shard_fn *before, int nbefore, const uint64_t *sizes,
+                   uint64_t *head) {
+    if (!c || !head || nbefore < 0 || (nbefore && (!before || !sizes))) return MSA_ERR_ARG;
+    HIPC(c, hipSetDevice(c->device));
+    const u8 *base;
+    u64 len;
+    int rc;
+    if ((rc = piece_of(c, piece, &base, &len))) return rc;
+    // reader state at this piece's first byte: the earlier pieces' functions,
+    // their record starts moved to global offsets, applied in order
+    State s{0, 0, 0, 0, 0, 0};
+    u64 g = 0;
+    for (int q = 0; q < nbefore; ++q) {
+        Fn f;
+        memcpy(&f, &before[q], sizeof f);
+        for (int i = 0; i < 3; ++i) f.e[i].rs += g;
+        s = fn_apply(s, f);
+        g += sizes[q];
+    }
+    *head = 0;
+    if (!len || nbefore == 0) return MSA_OK;
+    u8 b0 = 0;
+    HIPC(c, hipMemcpy(&b0, base, 1, hipMemcpyDeviceToHost));
+    if (s.cr && b0 == '\n') {  // the '\r' that ended the previous piece swallows this '\n'
+        *head = 1;
+        return MSA_OK;
+    }
+    if (s.rs == g) return MSA_OK;  // a record starts exactly here
+    u64 *d_out = reinterpret_cast<u64 *>(c->small.as<char>() + 3072);
+    HIPC(c, ensure(c->small, 4096));
+    d_out = reinterpret_cast<u64 *>(c->small.as<char>() + 3072);
+    HIPC(c, msa_launch_first_end(base, len, s.p, s.cr, d_out, c->stream));
+    u64 v = len;
+    HIPC(c, hipMemcpyAsync(&v, d_out, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    *head = v;
+    return MSA_OK;
+}
+
+int msa_segment_copy(msa_ctx *c, int piece, uint64_t off, uint64_t len, void *dst) {
+    if (!c || (len && !dst)) return MSA_ERR_ARG;
+    HIPC(c, hipSetDevice(c->device));
+    const u8 *base;
+    u64 plen;
+    int rc;
+    if ((rc = piece_of(c, piece, &base, &plen))) return rc;
+    if (off > plen || len > plen - off) return fail(c, MSA_ERR_ARG, "segment out of range");
+    if (len) HIPC(c, hipMemcpyAsync(dst, base + off, len, hipMemcpyDefault, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    return MSA_OK;
+}
+
+// Grow a device buffer keeping its first `keep` bytes.
+static hipError_t grow_keep(DevBuf &b, size_t bytes, size_t keep, hipStream_t s) {
+    if (b.cap >= bytes) return hipSuccess;
+    void *np = nullptr;
+    const size_t want = bytes + bytes / 4;
+    hipError_t e = hipMalloc(&np, want);
+    if (e != hipSuccess) return e;
+    if (keep) e = hipMemcpyAsync(np, b.p, keep, hipMemcpyDeviceToDevice, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) { (void)hipFree(np); return e; }
+    if (b.p) (void)hipFree(b.p);
+    b.p = np;
+    b.cap = want;
+    return hipSuccess;
+}
+
+int msa_segment_set(msa_ctx *c, int piece, uint64_t skip, const void *tail, uint64_t tail_len) {
+    if (!c || (tail_len && !tail)) return MSA_ERR_ARG;
+    HIPC(c, hipSetDevice(c->device));
+    const u8 *base;
+    u64 len;
+    int rc;
+    if ((rc = piece_of(c, piece, &base, &len))) return rc;
+    if (skip > len) return fail(c, MSA_ERR_ARG, "skip beyond the piece");
+    if (piece == MSA_PIECE_CSV) {
+        if (tail_len && c->in_base != c->in_own.as<u8>())
+            return fail(c, MSA_ERR_ARG, "appending to a bound (caller-owned) buffer; use msa_load_csv");
+        if (tail_len) {
+            HIPC(c, grow_keep(c->in_own, c->n_base + tail_len + MSA_INPUT_PAD, c->n_base, c->stream));
+            c->in_base = c->in_own.as<u8>();
+            HIPC(c, hipMemcpyAsync(c->in_own.as<u8>() + c->n_base, tail, tail_len, hipMemcpyDefault, c->stream));
+        }
+        if (c->in_base == c->in_own.as<u8>())
+            HIPC(c, hipMemsetAsync(c->in_own.as<u8>() + c->n_base + tail_len, 0, MSA_INPUT_PAD, c->stream));
+        c->in = c->in_base + skip;
+        c->n = c->n_base - skip + tail_len;
+        c->stage = 0;
+    } else {
+        const u64 b0 = c->a_hdr_getline;
+        if (tail_len) {
+            HIPC(c, grow_keep(c->acol, c->acol_len + tail_len + MSA_INPUT_PAD, c->acol_len, c->stream));
+            HIPC(c, hipMemcpyAsync(c->acol.as<u8>() + c->acol_len, tail, tail_len, hipMemcpyDefault, c->stream));
+        }
+        HIPC(c, hipMemsetAsync(c->acol.as<u8>() + c->acol_len + tail_len, 0, MSA_INPUT_PAD, c->stream));
+        c->a_beg = b0 + skip;
+        c->a_end = c->acol_len + tail_len;
+    }
+    HIPC(c, hipStreamSynchronize(c->stream));
+    return MSA_OK;
+}
+
+// ----------------------------------------------------------------- merge
+static void fill_exp_src(msa_ctx *c, int table, ExpSrc &x, u64 *n) {
+    memset(&x, 0, sizeof x);
+    if (table == MSA_TABLE_ARTISTS) {
+        x.artists = 1;
+        x.a_tab = c->a_tab.as<u64>();
+        x.a_list = c->a_list.as<u32>();
+        x.na = c->h_ctr.a_claimed;
+        x.arena = c->merged_a ? c->imp_a.as<u8>() : c->arena.as<u8>();
+        x.key_off = c->key_off.as<u64>();
+        x.key_len = c->key_len.as<u32>();
+        *n = x.na;
+        return;
+    }
+    x.s_tab = c->s_tab.as<u64>();
+    x.s_list = c->s_list.as<u32>();
+    x.ns = c->h_ctr.s_claimed;
+    x.m_tab = c->m_tab.as<u64>();
+    x.m_list = c->m_list.as<u32>();
+    x.nm = c->h_ctr.m_claimed;
+    x.l_tab = c->l_tab.as<u64>();
+    x.l_list = c->l_list.as<u32>();
+    x.nl = c->h_ctr.l_claimed;
+    x.buf = c->merged_w ? c->imp_w.as<u8>() : c->in;
+    x.extra = c->merged_w ? c->imp_w.as<u8>() : c->extra.as<u8>();
+    x.l_pos = c->l_pos.as<u64>();
+    x.l_len = c->l_len.as<u32>();
+    *n = x.ns + x.nm + x.nl;
+}
+
+int msa_export_partitions(msa_ctx *c, int table, int nparts, uint64_t *part_bytes) {
+    if (!c || nparts < 1 || nparts > 4096 || !part_bytes) return MSA_ERR_ARG;
+    if (table != MSA_TABLE_WORDS && table != MSA_TABLE_ARTISTS) return MSA_ERR_ARG;
+    if (c->stage < 2) return fail(c, MSA_ERR_ARG, "msa_export_partitions before msa_count");
+    HIPC(c, hipSetDevice(c->device));
+    ExpSrc x;
+    u64 n;
+    fill_exp_src(c, table, x, &n);
+    const size_t P = (size_t)nparts;
+    HIPC(c, ensure(c->exp_meta, 5 * P * 8));
+    u64 *pcnt = c->exp_meta.as<u64>(), *pblob = pcnt + P, *pbase = pblob + P, *rcur = pbase + P, *bcur = rcur + P;
+    HIPC(c, hipMemsetAsync(c->exp_meta.p, 0, 5 * P * 8, c->stream));
+    HIPC(c, msa_launch_exp_count(x, n, (u32)P, pcnt, pblob, c->stream));
+    std::vector<u64> h(2 * P), base(P);
+    HIPC(c, hipMemcpyAsync(h.data(), pcnt, 2 * P * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    u64 total = 0;
+    for (size_t p = 0; p < P; ++p) {
+        base[p] = total;
+        part_bytes[p] = 32 + 32 * h[p] + h[P + p];
+        total += part_bytes[p];
+    }
+    HIPC(c, ensure(c->exp_buf, total + 16));
+    HIPC(c, hipMemcpyAsync(pbase, base.data(), P * 8, hipMemcpyHostToDevice, c->stream));
+    HIPC(c, msa_launch_exp_write(x, n, (u32)P, pbase, pcnt, pblob, rcur, bcur, c->exp_buf.as<u8>(), c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    c->exp_bytes = total;
+    return MSA_OK;
+}
+
+int msa_export_copy(msa_ctx *c, void *dst) {
+    if (!c || (c->exp_bytes && !dst)) return MSA_ERR_ARG;
+    HIPC(c, hipSetDevice(c->device));
+    if (c->exp_bytes) HIPC(c, hipMemcpyAsync(dst, c->exp_buf.p, c->exp_bytes, hipMemcpyDefault, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    return MSA_OK;
+}
+
+static int clear_one(msa_ctx *c, DevBuf &tab, DevBuf &list, u64 &used, u32 w) {
+    if (used && tab.p) {
+        hipLaunchKernelGGL(k_clear_slots, dim3((u32)((used + 255) / 256)), dim3(256), 0, c->stream, tab.as<u64>(),
+                           list.as<u32>(), used, w);
+        HIPC(c, hipGetLastError());
+    }
+    used = 0;
+    return MSA_OK;
+}
+
+int msa_import_partitions(msa_ctx *c, int table, const void *src, const uint64_t *blk_off, int nblk) {
+    if (!c || !blk_off || nblk < 1) return MSA_ERR_ARG;
+    if (table != MSA_TABLE_WORDS && table != MSA_TABLE_ARTISTS) return MSA_ERR_ARG;
+    if (c->stage < 2) return fail(c, MSA_ERR_ARG, "msa_import_partitions before msa_count");
+    HIPC(c, hipSetDevice(c->device));
+    const bool art = table == MSA_TABLE_ARTISTS;
+    const u64 total = blk_off[nblk];
+    DevBuf &imp = art ? c->imp_a : c->imp_w;
+    HIPC(c, ensure(imp, total + 64));
+    if (total) HIPC(c, hipMemcpyAsync(imp.p, src, total, hipMemcpyDefault, c->stream));
+    HIPC(c, ensure(c->imp_meta, (2 * (size_t)nblk + 2) * 8));
+    u64 *d_off = c->imp_meta.as<u64>(), *d_base = d_off + nblk + 1;
+    HIPC(c, hipMemcpyAsync(d_off, blk_off, ((size_t)nblk + 1) * 8, hipMemcpyHostToDevice, c->stream));
+    const u64 rec_bound = total / 32 + 1;  // records are >= 32 bytes
+    int rc;
+    for (int attempt = 0; attempt < 8; ++attempt) {
+        // fresh tables for this key partition; only this table's counters reset
+        if (art) {
+            if ((rc = clear_one(c, c->a_tab, c->a_list, c->a_used_prev, 4))) return rc;
+        } else {
+            if ((rc = clear_one(c, c->s_tab, c->s_list, c->s_used_prev, 2))) return rc;
+            if ((rc = clear_one(c, c->m_tab, c->m_list, c->m_used_prev, 4))) return rc;
+            if ((rc = clear_one(c, c->l_tab, c->l_list, c->lt_used_prev, 4))) return rc;
+        }
+        if ((rc = ensure_tables(c))) return rc;
+        Counters *dc = c->ctr.as<Counters>();
+        if (art) {
+            HIPC(c, hipMemsetAsync(&dc->a_claimed, 0, 8, c->stream));
+            HIPC(c, ensure(c->key_off, rec_bound * 8));
+            HIPC(c, ensure(c->key_len, rec_bound * 4));
+            HIPC(c, ensure(c->key_slot, rec_bound * 8));
+        } else {
+            HIPC(c, hipMemsetAsync(&dc->s_claimed, 0, 8, c->stream));
+            HIPC(c, hipMemsetAsync(&dc->m_claimed, 0, 8, c->stream));
+            HIPC(c, hipMemsetAsync(&dc->l_occ, 0, 8, c->stream));
+            HIPC(c, hipMemsetAsync(&dc->l_claimed, 0, 8, c->stream));
+        }
+        HIPC(c, hipMemsetAsync(&dc->overflow, 0, 8, c->stream));
+        HIPC(c, hipMemsetAsync(&dc->collision, 0, 8, c->stream));
+        ImpDst d;
+        memset(&d, 0, sizeof d);
+        d.s_tab = c->s_tab.as<u64>(); d.s_mask = c->s_slots - 1; d.s_list = c->s_list.as<u32>(); d.s_list_cap = c->s_slots / 2;
+        d.m_tab = c->m_tab.as<u64>(); d.m_mask = c->m_slots - 1; d.m_list = c->m_list.as<u32>(); d.m_list_cap = c->m_slots / 2;
+        d.l_tab = c->l_tab.as<u64>(); d.l_mask = c->lt_slots - 1; d.l_list = c->l_list.as<u32>(); d.l_list_cap = c->lt_slots / 2;
+        d.l_pos = c->l_pos.as<u64>(); d.l_len = c->l_len.as<u32>(); d.l_slot = c->l_slot.as<u64>(); d.l_cap = c->l_occ_cap;
+        d.a_tab = c->a_tab.as<u64>(); d.a_mask = c->a_slots - 1; d.a_list = c->a_list.as<u32>(); d.a_list_cap = c->a_slots / 2;
+        d.key_off = c->key_off.as<u64>(); d.key_len = c->key_len.as<u32>(); d.key_slot = c->key_slot.as<u64>();
+        d.ctr = dc;
+        d.artists = art ? 1 : 0;
+        HIPC(c, msa_launch_imp(imp.as<u8>(), d_off, (u32)nblk, d_base, rec_bound, d, c->stream));
+        if ((rc = sync_counters(c))) return rc;
+        if (art) c->a_used_prev = std::min<u64>(c->h_ctr.a_claimed, c->a_slots / 2);
+        else {
+            c->s_used_prev = std::min<u64>(c->h_ctr.s_claimed, c->s_slots / 2);
+            c->m_used_prev = std::min<u64>(c->h_ctr.m_claimed, c->m_slots / 2);
+            c->lt_used_prev = std::min<u64>(c->h_ctr.l_claimed, c->lt_slots / 2);
+        }
+        if (c->h_ctr.overflow) {
+            grow_tables(c);
+            continue;
+        }
+        break;
+    }
+    if (c->h_ctr.overflow) return fail(c, MSA_ERR_CAPACITY, "merged table capacity overflow");
+    // byte-exact collision checks of the hash-keyed entries
+    u64 nrec_in = 0;
+    HIPC(c, hipMemcpy(&nrec_in, d_base + nblk, 8, hipMemcpyDeviceToHost));
+    if (art) {
+        HIPC(c, msa_launch_artist_verify(imp.as<u8>(), c->key_off.as<u64>(), c->key_len.as<u32>(),
+                                         c->key_slot.as<u64>(), nrec_in, c->a_tab.as<u64>(), c->ctr.as<Counters>(),
+                                         c->stream));
+    } else {
+        const u64 nl = std::min<u64>(c->h_ctr.l_occ, c->l_occ_cap);
+        HIPC(c, msa_launch_long_verify(imp.as<u8>(), imp.as<u8>(), c->l_pos.as<u64>(), c->l_len.as<u32>(),
+                                       c->l_slot.as<u64>(), nl, c->l_tab.as<u64>(), c->ctr.as<Counters>(), c->stream));
+    }
+    if ((rc = sync_counters(c))) return rc;
+    if (c->h_ctr.collision)
+        return fail(c, MSA_ERR_COLLISION, "64-bit key hash collision detected while merging");
+    if (art) {
+        c->merged_a = true;
+        c->sum.n_artists = c->h_ctr.a_claimed;
+    } else {
+        c->merged_w = true;
+        c->sum.n_words = c->h_ctr.s_claimed + c->h_ctr.m_claimed + c->h_ctr.l_claimed;
+    }
+    c->stage = 2;
+    return MSA_OK;
 }
 
 }  // extern "C"

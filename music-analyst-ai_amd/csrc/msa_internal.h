@@ -277,7 +277,8 @@ struct ScanArgs {
     u64 lpos_tag;    // OR'ed into recorded long-token positions (MSA_POS_EXTRA: the side buffer)
     Counters *ctr;
     int want_term;
-    int ablate;      // diagnostic builds only (MSA_ABLATE env): see msa_scan.hip
+    int ablate;
+    u32 first_rec;   // records before this index are not data (the header: 1; a continuation shard: 0)      // diagnostic builds only (MSA_ABLATE env): see msa_scan.hip
 };
 
 // A long-token position with this bit set indexes the context's side buffer
@@ -304,6 +305,57 @@ struct EntryArgs {
     u32 *val;
     u64 *ref;
     u64 *cnt;
+};
+
+// Export source: the counted table (words or artists) of one GPU.
+struct ExpSrc {
+    const u64 *s_tab;
+    const u32 *s_list;
+    u64 ns;
+    const u64 *m_tab;
+    const u32 *m_list;
+    u64 nm;
+    const u64 *l_tab;
+    const u32 *l_list;
+    u64 nl;
+    const u8 *buf, *extra;
+    const u64 *l_pos;
+    const u32 *l_len;
+    const u64 *a_tab;
+    const u32 *a_list;
+    u64 na;
+    const u8 *arena;
+    const u64 *key_off;
+    const u32 *key_len;
+    int artists;
+};
+// Import destination: the (cleared) tables that receive a key partition.
+struct ImpDst {
+    u64 *s_tab;
+    u64 s_mask;
+    u32 *s_list;
+    u64 s_list_cap;
+    u64 *m_tab;
+    u64 m_mask;
+    u32 *m_list;
+    u64 m_list_cap;
+    u64 *l_tab;
+    u64 l_mask;
+    u32 *l_list;
+    u64 l_list_cap;
+    u64 *l_pos;
+    u32 *l_len;
+    u64 *l_slot;
+    u64 l_cap;
+    u64 *a_tab;
+    u64 a_mask;
+    u32 *a_list;
+    u64 a_list_cap;
+    u64 *key_off;
+    u32 *key_len;
+    u64 *key_slot;
+    Counters *ctr;
+    int artists;
 };
 
 #define MSA_HIP_CHECK(x)                                                     \

@@ -1,0 +1,205 @@
+// msa_merge.hip -- multi-GPU count merge: export a counted table as key-hash
+// partitions, import the partitions other GPUs sent (after an RCCL all-to-all).
+//
+// Replaces the reference's point-to-point merge (send_hash_table /
+// receive_hash_table / ht_merge, parallel_spotify.c:152-158, 397-432, driven
+// at 1011-1025), where every rank streams every key to rank 0 as three MPI
+// messages and rank 0 re-inserts them serially.  Here each GPU owns the keys
+// whose 64-bit hash falls in its partition, so the merge is one all-to-all
+// and every GPU merges and ranks its own key range in parallel.
+//
+// Wire format, one block per destination partition:
+//   header  32 B : u64 n_entries, u64 blob_bytes, u64 0, u64 0
+//   records 32 B : u64 count, u32 len, u32 blob_off, u8 key[16] (first 16 bytes, 0-padded)
+//   blob         : keys longer than 16 bytes, each padded to 16 B
+// Keys are the final key bytes (words already lower-cased, artists as
+// duplicate_field returned them).
+#include "msa_internal.h"
+#include "msa_tables.h"
+
+namespace {
+__device__ __forceinline__ u32 lower1m(u32 c) { return (c >= 'A' && c <= 'Z') ? c + 32 : c; }
+__device__ __forceinline__ u64 part_of(u64 h, u32 nparts) { return fmix64(h ^ 0xA5A5A5A55A5A5A5AULL) % nparts; }
+}  // namespace
+
+__device__ void exp_entry(const ExpSrc &x, u64 e, u64 *count, u32 *len, u64 *k0, u64 *k1, const u8 **lp,
+                          int *lower) {
+    *lp = nullptr;
+    *lower = 0;
+    *k0 = 0;
+    *k1 = 0;
+    if (x.artists) {
+        const u64 slot = x.a_list[e];
+        *count = x.a_tab[4 * slot + 1];
+        const u64 rep = x.a_tab[4 * slot + 2];
+        *len = x.key_len[rep];
+        *lp = x.arena + x.key_off[rep];
+        return;
+    }
+    if (e < x.ns) {
+        const u64 slot = x.s_list[e];
+        *k0 = x.s_tab[2 * slot];
+        *count = x.s_tab[2 * slot + 1];
+        u32 n = 0;
+        while (n < 8 && ((*k0 >> (8 * n)) & 0xFF)) ++n;
+        *len = n;
+    } else if (e < x.ns + x.nm) {
+        const u64 slot = x.m_list[e - x.ns];
+        *k0 = x.m_tab[4 * slot];
+        *k1 = x.m_tab[4 * slot + 1];
+        *count = x.m_tab[4 * slot + 2];
+        u32 n = 8;
+        while (n < 16 && ((*k1 >> (8 * (n - 8))) & 0xFF)) ++n;
+        *len = n;
+    } else {
+        const u64 slot = x.l_list[e - x.ns - x.nm];
+        *count = x.l_tab[4 * slot + 1];
+        const u64 rep = x.l_tab[4 * slot + 2];
+        *len = x.l_len[rep];
+        *lp = tok_at(x.buf, x.extra, x.l_pos[rep]);
+        *lower = 1;
+    }
+}
+
+__device__ __forceinline__ void key16_from(const u8 *lp, u32 len, int lower, u64 *k0, u64 *k1) {
+    u64 a = 0, b = 0;
+    for (u32 i = 0; i < 16 && i < len; ++i) {
+        u64 ch = lower ? lower1m(lp[i]) : lp[i];
+        if (i < 8) a |= ch << (8 * i);
+        else b |= ch << (8 * (i - 8));
+    }
+    *k0 = a;
+    *k1 = b;
+}
+
+__device__ u64 exp_hash(u64 k0, u64 k1, u32 len, const u8 *lp, int lower) {
+    if (len <= 16) return fmix64(k0 ^ fmix64(k1 ^ len));
+    return bytes_hash(lp, len, lower);
+}
+
+// pass A: per-partition entry counts and blob bytes
+__global__ void k_exp_count(ExpSrc x, u64 n, u32 nparts, u64 *pcnt, u64 *pblob) {
+    const u64 e = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n) return;
+    u64 count, k0, k1;
+    u32 len;
+    const u8 *lp;
+    int lower;
+    exp_entry(x, e, &count, &len, &k0, &k1, &lp, &lower);
+    if (lp) key16_from(lp, len, lower, &k0, &k1);
+    const u32 p = (u32)part_of(exp_hash(k0, k1, len, lp, lower), nparts);
+    atomicAdd((unsigned long long *)&pcnt[p], 1ull);
+    if (len > 16) atomicAdd((unsigned long long *)&pblob[p], (unsigned long long)((len + 15) & ~15u));
+}
+
+// pass B: write the records.  pbase[p] = byte offset of partition p's block;
+// cursors (zeroed) hand out record slots and blob space within a block.
+__global__ void k_exp_write(ExpSrc x, u64 n, u32 nparts, const u64 *pbase, const u64 *pcnt, u64 *rcur, u64 *bcur,
+                            u8 *out) {
+    const u64 e = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n) return;
+    u64 count, k0, k1;
+    u32 len;
+    const u8 *lp;
+    int lower;
+    exp_entry(x, e, &count, &len, &k0, &k1, &lp, &lower);
+    if (lp) key16_from(lp, len, lower, &k0, &k1);
+    const u32 p = (u32)part_of(exp_hash(k0, k1, len, lp, lower), nparts);
+    const u64 i = atomicAdd((unsigned long long *)&rcur[p], 1ull);
+    u8 *blk = out + pbase[p];
+    u64 boff = 0;
+    if (len > 16) {
+        boff = atomicAdd((unsigned long long *)&bcur[p], (unsigned long long)((len + 15) & ~15u));
+        u8 *dst = blk + 32 + 32 * pcnt[p] + boff;
+        for (u32 k = 0; k < len; ++k) dst[k] = (u8)(lower ? lower1m(lp[k]) : lp[k]);
+    }
+    u64 *rec = reinterpret_cast<u64 *>(blk + 32 + 32 * i);
+    rec[0] = count;
+    rec[1] = (u64)len | (boff << 32);
+    rec[2] = k0;
+    rec[3] = k1;
+}
+
+__global__ void k_exp_headers(u32 nparts, const u64 *pbase, const u64 *pcnt, const u64 *pblob, u8 *out) {
+    const u32 p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= nparts) return;
+    u64 *h = reinterpret_cast<u64 *>(out + pbase[p]);
+    h[0] = pcnt[p];
+    h[1] = pblob[p];
+    h[2] = 0;
+    h[3] = 0;
+}
+
+// ---------------------------------------------------------------------------
+// Import.  blk_off[0..nblk] = byte offsets of the received blocks (last = end);
+// rec_base[b] = index of block b's first record among all received records.
+__global__ void k_imp_index(const u8 *in, const u64 *blk_off, u32 nblk, u64 *rec_base) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    u64 acc = 0;
+    for (u32 b = 0; b < nblk; ++b) {
+        rec_base[b] = acc;
+        if (blk_off[b + 1] > blk_off[b]) acc += reinterpret_cast<const u64 *>(in + blk_off[b])[0];
+    }
+    rec_base[nblk] = acc;
+}
+
+__global__ void k_imp_insert(const u8 *in, const u64 *blk_off, const u64 *rec_base, u32 nblk, ImpDst d) {
+    const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= rec_base[nblk]) return;
+    u32 b = 0;
+    while (b + 1 < nblk && rec_base[b + 1] <= r) ++b;
+    const u8 *blk = in + blk_off[b];
+    const u64 nrec_b = reinterpret_cast<const u64 *>(blk)[0];
+    const u64 li = r - rec_base[b];
+    const u64 *rec = reinterpret_cast<const u64 *>(blk + 32 + 32 * li);
+    const u64 count = rec[0];
+    const u32 len = (u32)(rec[1] & 0xFFFFFFFFu);
+    const u64 boff = rec[1] >> 32;
+    const u64 k0 = rec[2], k1 = rec[3];
+    // key bytes: inline (record) or blob; positions are offsets into `in`
+    const u64 kpos = (len > 16) ? (blk_off[b] + 32 + 32 * nrec_b + boff) : (blk_off[b] + 32 + 32 * li + 16);
+    if (d.artists) {
+        d.key_off[r] = kpos;
+        d.key_len[r] = len;
+        u64 h = bytes_hash(in + kpos, len, 0);
+        d.key_slot[r] = h_insert(d.a_tab, d.a_mask, h, count, r, d.a_list, d.a_list_cap, &d.ctr->a_claimed, d.ctr,
+                                 OVF_A);
+        return;
+    }
+    if (len <= 8) {
+        s_insert(d.s_tab, d.s_mask, k0, count, d.s_list, d.s_list_cap, d.ctr);
+    } else if (len <= 16) {
+        m_insert(d.m_tab, d.m_mask, k0, k1, count, d.m_list, d.m_list_cap, d.ctr);
+    } else {
+        const u64 i = atomicAdd((unsigned long long *)&d.ctr->l_occ, 1ull);
+        if (i >= d.l_cap) {
+            atomicOr((unsigned long long *)&d.ctr->overflow, (unsigned long long)OVF_L);
+            return;
+        }
+        d.l_pos[i] = kpos | MSA_POS_EXTRA;
+        d.l_len[i] = len;
+        const u64 h = bytes_hash(in + kpos, len, 1);
+        d.l_slot[i] = h_insert(d.l_tab, d.l_mask, h, count, i, d.l_list, d.l_list_cap, &d.ctr->l_claimed, d.ctr,
+                               OVF_LT);
+    }
+}
+
+// ---------------------------------------------------------------------------
+static inline dim3 g1(u64 n, u32 t = 256) { return dim3((u32)((n + t - 1) / t)); }
+
+hipError_t msa_launch_exp_count(const ExpSrc &x, u64 n, u32 nparts, u64 *pcnt, u64 *pblob, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_exp_count, g1(n), dim3(256), 0, s, x, n, nparts, pcnt, pblob);
+    return hipGetLastError();
+}
+hipError_t msa_launch_exp_write(const ExpSrc &x, u64 n, u32 nparts, const u64 *pbase, const u64 *pcnt,
+                                const u64 *pblob, u64 *rcur, u64 *bcur, u8 *out, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_exp_write, g1(n), dim3(256), 0, s, x, n, nparts, pbase, pcnt, rcur, bcur, out);
+    hipLaunchKernelGGL(k_exp_headers, dim3(1), dim3(64), 0, s, nparts, pbase, pcnt, pblob, out);
+    return hipGetLastError();
+}
+hipError_t msa_launch_imp(const u8 *in, const u64 *blk_off, u32 nblk, u64 *rec_base, u64 nrec_total, const ImpDst &d,
+                          hipStream_t s) {
+    hipLaunchKernelGGL(k_imp_index, dim3(1), dim3(64), 0, s, in, blk_off, nblk, rec_base);
+    if (nrec_total) hipLaunchKernelGGL(k_imp_insert, g1(nrec_total), dim3(256), 0, s, in, blk_off, rec_base, nblk, d);
+    return hipGetLastError();
+}

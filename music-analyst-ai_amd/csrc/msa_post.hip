@@ -152,11 +152,11 @@ template <int TEXT>
 __global__ __launch_bounds__(256) void k_col_span(const u8 *__restrict__ buf, const u64 *__restrict__ rec_start,
                                                   const u64 *__restrict__ rec_term, const u32 *__restrict__ f0rel,
                                                   const u32 *__restrict__ f3rel, const u32 *__restrict__ nulrel,
-                                                  u64 nrec, u64 *__restrict__ line_len, u64 *__restrict__ span_src,
-                                                  u32 *__restrict__ span_pairs) {
+                                                  u64 nrec, u64 first_rec, u64 *__restrict__ line_len,
+                                                  u64 *__restrict__ span_src, u32 *__restrict__ span_pairs) {
     const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= nrec) return;
-    if (r == 0 || !f3rel[r]) {  // header, or a record parse_csv_line rejects
+    if (r < first_rec || !f3rel[r]) {  // header, or a record parse_csv_line rejects
         line_len[r] = 0;
         return;
     }
@@ -746,12 +746,15 @@ __global__ void k_blob_write(const u32 *__restrict__ order, u64 n, const u64 *__
 static inline dim3 grid1(u64 n, u32 t = 256) { return dim3((u32)((n + t - 1) / t)); }
 
 hipError_t msa_launch_col_span(int text, const u8 *buf, const u64 *rs, const u64 *rt, const u32 *f0, const u32 *f3,
-                               const u32 *nul, u64 nrec, u64 *len, u64 *src, u32 *pairs, hipStream_t s) {
+                               const u32 *nul, u64 nrec, u64 first_rec, u64 *len, u64 *src, u32 *pairs,
+                               hipStream_t s) {
     if (!nrec) return hipSuccess;
     if (text)
-        hipLaunchKernelGGL(k_col_span<1>, grid1(nrec), dim3(256), 0, s, buf, rs, rt, f0, f3, nul, nrec, len, src, pairs);
+        hipLaunchKernelGGL(k_col_span<1>, grid1(nrec), dim3(256), 0, s, buf, rs, rt, f0, f3, nul, nrec, first_rec, len,
+                           src, pairs);
     else
-        hipLaunchKernelGGL(k_col_span<0>, grid1(nrec), dim3(256), 0, s, buf, rs, rt, f0, f3, nul, nrec, len, src, pairs);
+        hipLaunchKernelGGL(k_col_span<0>, grid1(nrec), dim3(256), 0, s, buf, rs, rt, f0, f3, nul, nrec, first_rec, len,
+                           src, pairs);
     return hipGetLastError();
 }
 hipError_t msa_launch_col_write(const u8 *buf, const u64 *len, const u64 *off, const u64 *src, const u32 *pairs,
@@ -785,6 +788,16 @@ hipError_t msa_launch_long(const u8 *buf, u64 seg_end, const u8 *extra, u64 extr
         hipLaunchKernelGGL(k_long_verify, grid1(n), dim3(256), 0, s, buf, extra, l_pos, (const u32 *)l_len,
                            (const u64 *)l_slot, n, (const u64 *)ltab, ctr);
     }
+    return hipGetLastError();
+}
+hipError_t msa_launch_artist_verify(const u8 *arena, const u64 *key_off, const u32 *key_len, const u64 *key_slot,
+                                    u64 n, const u64 *atab, Counters *ctr, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_artist_verify, grid1(n), dim3(256), 0, s, arena, key_off, key_len, key_slot, n, atab, ctr);
+    return hipGetLastError();
+}
+hipError_t msa_launch_long_verify(const u8 *buf, const u8 *extra, const u64 *l_pos, const u32 *l_len,
+                                  const u64 *l_slot, u64 n, const u64 *ltab, Counters *ctr, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_long_verify, grid1(n), dim3(256), 0, s, buf, extra, l_pos, l_len, l_slot, n, ltab, ctr);
     return hipGetLastError();
 }
 hipError_t msa_launch_word_entries(const EntryArgs &a, hipStream_t s) {

@@ -425,7 +425,7 @@ __global__ __launch_bounds__(K3_THREADS) void k_scan_main(ScanArgs a) {
             while (E) {
                 const u32 b = __ffs(E) - 1;
                 E &= E - 1;
-                if (MODE == 0 && rr >= 1 && cs >= 3 && !zs) live |= range_mask(from, b);
+                if (MODE == 0 && rr >= a.first_rec && cs >= 3 && !zs) live |= range_mask(from, b);
                 const u64 bpos = lpos + b;
                 if ((TERM >> b) & 1u) {
                     if ((a.want_term || rr == 0) && rr < a.rec_cap) a.rec_term[rr] = bpos;
@@ -449,7 +449,7 @@ __global__ __launch_bounds__(K3_THREADS) void k_scan_main(ScanArgs a) {
                 }
                 from = b + 1;
             }
-            if (MODE == 0 && rr >= 1 && cs >= 3 && !zs) live |= range_mask(from, 16);
+            if (MODE == 0 && rr >= a.first_rec && cs >= 3 && !zs) live |= range_mask(from, 16);
 
             // carry to the next iteration (lane 63 has seen every byte)
             st.p ^= (u32)__popcll(B) & 1u;
@@ -536,6 +536,51 @@ __global__ __launch_bounds__(K3_THREADS) void k_scan_main(ScanArgs a) {
             if (n) m_insert(a.m_tab, a.m_mask, mk0[i], mk1[i], n, a.m_list, a.m_list_cap, a.ctr);
         }
     }
+}
+
+// ---------------------------------------------------------------------------
+// First record end in a shard (multi-GPU boundary resolution): one wave walks
+// the shard from its first byte with the reader state (p, cr) it inherits from
+// the shards before it, and stops at the first unquoted terminator (a '\r'
+// swallows one '\n', as in read_csv_record, parallel_spotify.c:609-627).
+// Writes the offset just past that record, or n if the shard has none.
+__global__ __launch_bounds__(64) void k_first_end(const u8 *__restrict__ buf, u64 n, u32 p0, u32 cr0,
+                                                  u64 *__restrict__ out) {
+    const u32 lane = lane_id();
+    u32 p = p0, cr = cr0;
+    for (u64 ibase = 0; ibase < n; ibase += MSA_ITER) {
+        const u64 lpos = ibase + lane * 16;
+        const uint4 v = ld16(buf + lpos);
+        const Classes k = classify16(v, valid_mask(lpos, n));
+        const u64 B = __ballot(__popc(k.Q) & 1u);
+        const u32 pin = p ^ (mbcnt(B) & 1u);
+        const u32 inq = pxor_excl16(k.Q) ^ (pin ? 0xFFFFu : 0u);
+        const u32 CRu = k.CR & ~inq, NLu = k.NL & ~inq;
+        const u32 upCR = __shfl_up(CRu, 1);
+        const u32 pc0 = lane ? ((upCR >> 15) & 1u) : cr;
+        const u32 TERM = (CRu | (NLu & ~((CRu << 1) | pc0))) & 0xFFFFu;
+        const u64 Bt = __ballot(TERM != 0);
+        if (Bt) {
+            const int jl = __ffsll((long long)Bt) - 1;
+            const u32 tm = readlane(TERM, jl);
+            const u64 pos = ibase + (u64)jl * 16 + (u64)(__ffs(tm) - 1);
+            if (lane == 0) {
+                u64 end = pos + 1;
+                if (buf[pos] == '\r' && end < n && buf[end] == '\n') ++end;
+                *out = end;
+            }
+            return;
+        }
+        p ^= (u32)__popcll(B) & 1u;
+        const u32 lastb = (u32)(min(ibase + (u64)MSA_ITER, n) - 1 - ibase);
+        cr = (readlane(CRu, (int)(lastb >> 4)) >> (lastb & 15u)) & 1u;
+    }
+    if (lane == 0) *out = n;
+}
+
+hipError_t msa_launch_first_end(const u8 *buf, u64 n, u32 p, u32 cr, u64 *out, hipStream_t s) {
+    hipLaunchKernelGGL(k_first_end, dim3(1), dim3(64), 0, s, buf, n, p, cr, out);
+    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------

@@ -39,9 +39,13 @@ EXPORTS = [
     "msa_gen_corpus", "msa_free", "msa_create", "msa_destroy", "msa_last_error",
     "msa_stream", "msa_sync", "msa_load_csv", "msa_bind_csv", "msa_split_columns",
     "msa_count", "msa_rank", "msa_run", "msa_get_summary", "msa_get_ranked",
-    "msa_write_table_csv", "msa_get_split_column", "msa_shard_function",
-    "msa_shard_set_prefix", "msa_set_profiling", "msa_get_profile",
+    "msa_write_table_csv", "msa_get_split_column", "msa_set_profiling", "msa_get_profile",
+    "msa_set_shard", "msa_piece_size", "msa_shard_function", "msa_shard_head", "msa_segment_copy",
+    "msa_segment_set", "msa_export_partitions", "msa_export_copy", "msa_import_partitions",
 ]
+PIECE_CSV = 0
+PIECE_ARTISTS = 1
+SHARD_FN_BYTES = 120  # sizeof(msa_shard_fn)
 
 
 class MsaError(RuntimeError):
@@ -120,8 +124,15 @@ def load(path: str = LIB_PATH):
                                    C.POINTER(u64)]
     lib.msa_write_table_csv.argtypes = [vp, i, C.c_char_p, C.c_char_p, i]
     lib.msa_get_split_column.argtypes = [vp, i, C.POINTER(C.c_void_p), C.POINTER(sz)]
-    lib.msa_shard_function.argtypes = [vp, vp]
-    lib.msa_shard_set_prefix.argtypes = [vp, vp, i]
+    lib.msa_set_shard.argtypes = [vp, i]
+    lib.msa_piece_size.argtypes = [vp, i, C.POINTER(u64)]
+    lib.msa_shard_function.argtypes = [vp, i, vp]
+    lib.msa_shard_head.argtypes = [vp, i, vp, i, C.POINTER(u64), C.POINTER(u64)]
+    lib.msa_segment_copy.argtypes = [vp, i, u64, u64, vp]
+    lib.msa_segment_set.argtypes = [vp, i, u64, vp, u64]
+    lib.msa_export_partitions.argtypes = [vp, i, i, C.POINTER(u64)]
+    lib.msa_export_copy.argtypes = [vp, vp]
+    lib.msa_import_partitions.argtypes = [vp, i, vp, C.POINTER(u64), i]
     lib.msa_set_profiling.argtypes = [vp, i]
     lib.msa_get_profile.argtypes = [vp, C.POINTER(_Profile), i]
     _lib = lib
@@ -219,6 +230,46 @@ class Context:
         for k in range(p.n):
             out[p.name[k].value.decode()] = {"ms": p.ms[k], "launches": p.launches[k], "bytes": p.bytes[k]}
         return out
+
+    # ---- multi-GPU shard API (msa/dist.py drives it)
+    def set_shard(self, first: bool):
+        self._check(self.lib.msa_set_shard(self.h, int(first)))
+
+    def piece_size(self, piece: int) -> int:
+        v = C.c_uint64()
+        self._check(self.lib.msa_piece_size(self.h, piece, C.byref(v)))
+        return v.value
+
+    def shard_function(self, piece: int) -> bytes:
+        buf = C.create_string_buffer(SHARD_FN_BYTES)
+        self._check(self.lib.msa_shard_function(self.h, piece, buf))
+        return buf.raw
+
+    def shard_head(self, piece: int, fns_before: List[bytes], sizes_before: List[int]) -> int:
+        k = len(fns_before)
+        blob = C.create_string_buffer(b"".join(fns_before), max(1, SHARD_FN_BYTES * k))
+        sizes = (C.c_uint64 * max(1, k))(*sizes_before)
+        v = C.c_uint64()
+        self._check(self.lib.msa_shard_head(self.h, piece, blob, k, sizes, C.byref(v)))
+        return v.value
+
+    def segment_copy(self, piece: int, off: int, length: int, dst_ptr: int):
+        self._check(self.lib.msa_segment_copy(self.h, piece, off, length, C.c_void_p(dst_ptr)))
+
+    def segment_set(self, piece: int, skip: int, tail_ptr: int = 0, tail_len: int = 0):
+        self._check(self.lib.msa_segment_set(self.h, piece, skip, C.c_void_p(tail_ptr or None), tail_len))
+
+    def export_partitions(self, table: int, nparts: int) -> List[int]:
+        out = (C.c_uint64 * nparts)()
+        self._check(self.lib.msa_export_partitions(self.h, table, nparts, out))
+        return list(out)
+
+    def export_copy(self, dst_ptr: int):
+        self._check(self.lib.msa_export_copy(self.h, C.c_void_p(dst_ptr)))
+
+    def import_partitions(self, table: int, src_ptr: int, blk_off: List[int]):
+        arr = (C.c_uint64 * len(blk_off))(*blk_off)
+        self._check(self.lib.msa_import_partitions(self.h, table, C.c_void_p(src_ptr or None), arr, len(blk_off) - 1))
 
     def summary(self) -> Summary:
         s = _Summary()

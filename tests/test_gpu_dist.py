@@ -1,0 +1,144 @@
+"""GPU: the multi-GPU path (msa/dist.py over libmsa_hip) with N processes on the
+box's one GPU (gloo carries the exchanges through host memory; RCCL/xGMI on a
+real multi-GPU node).  The logical CSV is cut at arbitrary byte offsets --
+inside quoted multi-line lyrics, between '\\r' and '\\n', on record boundaries
+-- and the merged, ranked result must be byte-identical to the single-process
+reference semantics (the oracle at np=1)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+from conftest import PKG, REPO, read_outputs, run_oracle
+
+pytestmark = pytest.mark.gpu
+
+WORKER = r'''
+import json, os, sys
+sys.path.insert(0, os.environ["MSA_PKG"])
+import torch, torch.distributed as dist
+import msa
+from msa import dist as mdist
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+dist.init_process_group("gloo", rank=rank, world_size=world)
+data = open(os.environ["MSA_CSV"], "rb").read()
+cuts = json.loads(os.environ["MSA_CUTS"])
+lo, hi = cuts[rank], cuts[rank + 1]
+ctx = msa.Context(0)
+ctx.load_csv(data[lo:hi])
+comm = mdist.Comm()
+songs, words = mdist.run_sharded(ctx, comm, text_column=False)
+w = mdist.gather_ranked(ctx, comm, msa.MSA_TABLE_WORDS)
+a = mdist.gather_ranked(ctx, comm, msa.MSA_TABLE_ARTISTS)
+if rank == 0:
+    out = os.environ["MSA_OUT"]
+    open(out + ".words", "wb").write(msa.table_csv_bytes(w, "word"))
+    open(out + ".artists", "wb").write(msa.table_csv_bytes(a, "artist"))
+    json.dump({"total_songs": songs, "total_words": words}, open(out + ".json", "w"))
+ctx.close()
+dist.destroy_process_group()
+'''
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def run_world(tmp_path, data, cuts):
+    csv = tmp_path / "in.csv"
+    csv.write_bytes(data)
+    script = tmp_path / "worker.py"
+    script.write_text(WORKER)
+    out = str(tmp_path / "res")
+    world = len(cuts) - 1
+    port = free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   MSA_PKG=PKG, MSA_CSV=str(csv), MSA_CUTS=json.dumps(cuts), MSA_OUT=out)
+        procs.append(subprocess.Popen([sys.executable, str(script)], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT))
+    logs = []
+    for p in procs:
+        try:
+            o, _ = p.communicate(timeout=100)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            pytest.fail("distributed workers timed out")
+        logs.append(o.decode(errors="replace"))
+    for p, log in zip(procs, logs):
+        assert p.returncode == 0, log[-3000:]
+    return (open(out + ".words", "rb").read(), open(out + ".artists", "rb").read(),
+            json.load(open(out + ".json")))
+
+
+def expected(tmp_path, data):
+    p = tmp_path / "o.csv"
+    p.write_bytes(data)
+    r = run_oracle(str(p), str(tmp_path / "o"), ranks=1)
+    assert r.returncode == 0
+    return read_outputs(str(tmp_path / "o"))
+
+
+def cuts_for(data, world, mode):
+    n = len(data)
+    if mode == "even":
+        return [n * r // world for r in range(world)] + [n]
+    if mode == "in_quotes":  # cut just after the opening quote of some lyric
+        cs = [0]
+        pos = 0
+        for r in range(1, world):
+            pos = data.index(b',"', n * r // world) + 2
+            cs.append(pos)
+        return cs + [n]
+    if mode == "crlf":  # cut between '\r' and '\n'
+        cs = [0]
+        for r in range(1, world):
+            cs.append(data.index(b"\r\n", n * r // world) + 1)
+        return cs + [n]
+    if mode == "record":  # exactly on record starts
+        cs = [0]
+        for r in range(1, world):
+            cs.append(data.index(b'"\n', n * r // world) + 2)
+        return cs + [n]
+    raise ValueError(mode)
+
+
+@pytest.mark.parametrize("world,mode,gen", [
+    (2, "even", ("zipf", False)),
+    (3, "in_quotes", ("zipf", False)),
+    (2, "record", ("zipf", False)),
+    (2, "crlf", ("zipf", True)),
+    (4, "even", ("highcard", False)),
+    (3, "even", ("torture", False)),
+])
+def test_sharded_equals_single_process(msa_mod, tmp_path, world, mode, gen):
+    kind, crlf = gen
+    data = msa_mod.gen_corpus(4000 if kind != "torture" else 3000, mode=kind, seed=17, crlf=crlf, vocab=8000)
+    cuts = cuts_for(data, world, mode)
+    words, artists, tot = run_world(tmp_path, data, cuts)
+    exp = expected(tmp_path, data)
+    assert tot == {k: exp["metrics"][k] for k in ("total_songs", "total_words")}
+    assert words == exp["word_counts.csv"]
+    assert artists == exp["top_artists.csv"]
+
+
+def test_sharded_tiny_shards(msa_mod, tmp_path):
+    """More ranks than records in some shards: whole shards that are one
+    record's middle, empty shards."""
+    data = msa_mod.gen_corpus(40, mode="zipf", seed=3)
+    n = len(data)
+    cuts = [0, 10, 11, n // 2, n // 2 + 5, n]
+    words, artists, tot = run_world(tmp_path, data, cuts)
+    exp = expected(tmp_path, data)
+    assert words == exp["word_counts.csv"]
+    assert artists == exp["top_artists.csv"]
+    assert tot["total_words"] == exp["metrics"]["total_words"]
