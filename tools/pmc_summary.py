@@ -63,8 +63,8 @@ def main():
         "correction": "hbm = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE halves 16B/lane streams)",
         "sq_per_launch": sq,
     }
-    os.makedirs("profiles", exist_ok=True)
-    with open(os.path.join("profiles", "pmc_scan_main.json"), "w") as f:
+    # written next to the passes (gpurun_out/ travels back); copy to profiles/
+    with open(os.path.join(out, "pmc_scan_main.json"), "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps(res, indent=1))
 
