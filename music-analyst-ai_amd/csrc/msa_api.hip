@@ -36,7 +36,7 @@ hipError_t msa_launch_imp(const u8 *, const u64 *, u32, u64 *, u64, const ImpDst
 hipError_t msa_launch_col_write(const u8 *, const u64 *, const u64 *, const u64 *, const u32 *, u64, u64, u64, u8 *,
                                 hipStream_t);
 hipError_t msa_launch_artist_key(const u8 *, const u64 *, const u64 *, u64, u8 *, u64 *, u32 *, u64 *, u64 *, u64,
-                                 u32 *, u64, Counters *, hipStream_t);
+                                 u32 *, u64, Counters *, u64, hipStream_t);
 hipError_t msa_launch_long(const u8 *, u64, const u8 *, u64, const u64 *, u64, u32 *, u64 *, u64 *, u64, u32 *, u64,
                            Counters *, hipStream_t);
 hipError_t msa_launch_word_entries(const EntryArgs &, hipStream_t);
@@ -609,7 +609,10 @@ static int do_count(msa_ctx *c) {
     const u64 cap = nterm + 2;
     HIPC(c, ensure(c->ar_start, cap * 8));
     HIPC(c, ensure(c->ar_term, cap * 8));
-    HIPC(c, ensure(c->arena, e + 64));
+    // arena: keys rewritten by duplicate_field at their artist.csv offsets, then
+    // one aligned 32-byte slot per record for keys built in registers
+    const u64 short_base = (e + 64 + 255) & ~255ull;
+    HIPC(c, ensure(c->arena, short_base + 32 * cap));
     HIPC(c, ensure(c->key_off, cap * 8));
     HIPC(c, ensure(c->key_len, cap * 4));
     HIPC(c, ensure(c->key_slot, cap * 8));
@@ -635,7 +638,7 @@ static int do_count(msa_ctx *c) {
     HIPC(c, msa_launch_artist_key(c->acol.as<u8>(), c->ar_start.as<u64>(), c->ar_term.as<u64>(), c->nrec_a,
                                   c->arena.as<u8>(), c->key_off.as<u64>(), c->key_len.as<u32>(), c->key_slot.as<u64>(),
                                   c->a_tab.as<u64>(), c->a_slots - 1, c->a_list.as<u32>(), c->a_slots / 2,
-                                  c->ctr.as<Counters>(), c->stream));
+                                  c->ctr.as<Counters>(), short_base, c->stream));
     prof_end(c, ST_ARTIST_KEYS, (e - b) * 2 + c->nrec_a * 48);
     if ((rc = sync_counters(c))) return rc;
     // words longer than 16 bytes

@@ -141,6 +141,107 @@ __device__ Span dup_field(const u8 *f, u64 len, int preserve, u8 *out) {
     return r;
 }
 
+// Bytes [off, off + 16) of the 32-byte window (a, b).
+__device__ __forceinline__ u32 sel4(const uint4 &v, u32 i) {
+    return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w));
+}
+__device__ __forceinline__ uint4 funnel16(const uint4 &a, const uint4 &b, u32 off) {
+    if (off == 0) return a;
+    const u32 dw = off >> 2, sh = (off & 3) * 8;
+    u32 d[5];
+#pragma unroll
+    for (u32 i = 0; i < 5; ++i) {
+        const u32 k = dw + i;  // 0..7
+        d[i] = k < 4 ? sel4(a, k) : sel4(b, k - 4);
+    }
+    uint4 r;
+    r.x = (u32)((((u64)d[1] << 32) | d[0]) >> sh);
+    r.y = (u32)((((u64)d[2] << 32) | d[1]) >> sh);
+    r.z = (u32)((((u64)d[3] << 32) | d[2]) >> sh);
+    r.w = (u32)((((u64)d[4] << 32) | d[3]) >> sh);
+    return r;
+}
+
+// ---------------------------------------------------------------------------
+// Short fields in registers: a 64-byte window of four aligned dwordx4 loads
+// and SWAR byte-class masks (bit i = window byte i).
+struct Win64 {
+    uint4 q[4];
+};
+__device__ __forceinline__ Win64 load_win64(const u8 *__restrict__ buf, u64 s) {
+    const uint4 *p = reinterpret_cast<const uint4 *>(buf + (s & ~15ull));
+    Win64 w;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w.q[i] = p[i];
+    return w;
+}
+__device__ __forceinline__ u32 swar_space(u32 x) {  // isspace, C locale: ' ' and 9..13
+    const u32 hi = x & 0x80808080u, y = x & 0x7F7F7F7Fu;
+    const u32 ctl = swar_ge7(y, 9) & ~swar_ge7(y, 14);
+    return (ctl & ~hi) | swar_eq(x, ' ');
+}
+template <int CLS>  // 0 = space, 1 = '"', 2 = '\n' or '\r'
+__device__ __forceinline__ u64 win_mask(const Win64 &w) {
+    u64 m = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const u32 d[4] = {w.q[i].x, w.q[i].y, w.q[i].z, w.q[i].w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            u32 v;
+            if (CLS == 0) v = swar_space(d[k]);
+            else if (CLS == 1) v = swar_eq(d[k], '"');
+            else v = swar_eq(d[k], '\n') | swar_eq(d[k], '\r');
+            m |= (u64)swar_pack4(v) << (16 * i + 4 * k);
+        }
+    }
+    return m;
+}
+__device__ __forceinline__ uint4 sel_q(const Win64 &w, u32 i) {
+    return i == 0 ? w.q[0] : (i == 1 ? w.q[1] : (i == 2 ? w.q[2] : w.q[3]));
+}
+// 32 window bytes starting at byte `at` (at + len <= 64), bytes >= len zeroed.
+__device__ __forceinline__ void win_take32(const Win64 &w, u32 at, u32 len, uint4 *o0, uint4 *o1) {
+    const u32 qi = at >> 4, off = at & 15;
+    const uint4 a = sel_q(w, qi), b = sel_q(w, min(qi + 1, 3u)), c = sel_q(w, min(qi + 2, 3u));
+    const uint4 x0 = funnel16(a, b, off), x1 = funnel16(b, c, off);
+    u32 d[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+    for (u32 k = 0; k < 8; ++k) {
+        const u32 lo = 4 * k;
+        const u32 keep = len <= lo ? 0u : (len >= lo + 4 ? 4u : len - lo);
+        d[k] &= keep == 4 ? 0xFFFFFFFFu : ((1u << (8 * keep)) - 1u);
+    }
+    *o0 = make_uint4(d[0], d[1], d[2], d[3]);
+    *o1 = make_uint4(d[4], d[5], d[6], d[7]);
+}
+// bytes_hash (msa_tables.h) of <= 32 bytes given as little-endian words
+__device__ __forceinline__ u64 bytes_hash_words(const uint4 &o0, const uint4 &o1, u32 n) {
+    const u64 w[4] = {((u64)o0.y << 32) | o0.x, ((u64)o0.w << 32) | o0.z, ((u64)o1.y << 32) | o1.x,
+                      ((u64)o1.w << 32) | o1.z};
+    u64 h = 0x243F6A8885A308D3ULL ^ ((u64)n * 0x9E3779B97F4A7C15ULL);
+    const u32 full = n >> 3, rem = n & 7;
+#pragma unroll
+    for (u32 i = 0; i < 4; ++i)
+        if (i < full) h = fmix64(h ^ w[i]) * 0x9E3779B97F4A7C15ULL;
+    const u64 acc = rem ? (full == 0 ? w[0] : (full == 1 ? w[1] : (full == 2 ? w[2] : w[3]))) : 0ull;
+    return fmix64(h ^ acc ^ ((u64)rem << 59));
+}
+__device__ __forceinline__ u64 bits_from(u32 lo) { return lo >= 64 ? 0ull : (~0ull << lo); }
+__device__ __forceinline__ u64 bits_below(u32 hi) { return hi >= 64 ? ~0ull : ((1ull << hi) - 1ull); }
+// greedy "" pairs (duplicate_field's collapse) in a quote mask: sum of floor(run/2)
+__device__ __forceinline__ u32 quote_pairs(u64 q) {
+    u32 pairs = 0;
+    while (q) {
+        const u32 st = (u32)__ffsll((long long)q) - 1;
+        const u64 rest = ~(q >> st);
+        const u32 rl = rest ? (u32)__ffsll((long long)rest) - 1 : 64 - st;
+        pairs += rl >> 1;
+        q &= ~(bits_below(rl) << st);
+    }
+    return pairs;
+}
+
 // Column lines (split_dataset_columns, parallel_spotify.c:699-714): line r is
 // duplicate_field(field, preserve=1) + '\n'.  After the outer trim a quoted
 // field -- every lyric of the real corpus -- is copied raw; an unquoted one
@@ -171,37 +272,33 @@ __global__ __launch_bounds__(256) void k_col_span(const u8 *__restrict__ buf, co
         s = rs;
         e = rs + f0rel[r] - 1;
     }
-    while (s < e && c_space(buf[s])) ++s;
-    while (e > s && c_space(buf[e - 1])) --e;
     u32 pairs = 0;
-    if (!(e > s + 1 && buf[s] == '"' && buf[e - 1] == '"')) {
-        for (u64 i = s; i + 1 < e; ++i)
-            if (buf[i] == '"' && buf[i + 1] == '"') { ++pairs; ++i; }
+    if (!TEXT && e - s <= 48) {  // short field (artist): trim and pairs in registers
+        const Win64 w = load_win64(buf, s);
+        const u32 o = (u32)(s & 15);
+        const u64 fm = bits_from(o) & bits_below(o + (u32)(e - s));
+        const u64 nsp = fm & ~win_mask<0>(w);
+        if (!nsp) {
+            e = s;
+        } else {
+            const u32 a = (u32)__ffsll((long long)nsp) - 1, b = 63u - (u32)__clzll((long long)nsp);
+            const u64 Q = win_mask<1>(w) & bits_from(a) & bits_below(b + 1);
+            if (!(b > a && ((Q >> a) & 1) && ((Q >> b) & 1))) pairs = quote_pairs(Q);
+            const u64 base = s - o;
+            s = base + a;
+            e = base + b + 1;
+        }
+    } else {
+        while (s < e && c_space(buf[s])) ++s;
+        while (e > s && c_space(buf[e - 1])) --e;
+        if (!(e > s + 1 && buf[s] == '"' && buf[e - 1] == '"')) {
+            for (u64 i = s; i + 1 < e; ++i)
+                if (buf[i] == '"' && buf[i + 1] == '"') { ++pairs; ++i; }
+        }
     }
     line_len[r] = (e - s) - pairs + 1;
     span_src[r] = s;
     span_pairs[r] = pairs;
-}
-
-__device__ __forceinline__ u32 sel4(const uint4 &v, u32 i) {
-    return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w));
-}
-// Bytes [off, off + 16) of the 32-byte window (a, b).
-__device__ __forceinline__ uint4 funnel16(const uint4 &a, const uint4 &b, u32 off) {
-    if (off == 0) return a;
-    const u32 dw = off >> 2, sh = (off & 3) * 8;
-    u32 d[5];
-#pragma unroll
-    for (u32 i = 0; i < 5; ++i) {
-        const u32 k = dw + i;  // 0..7
-        d[i] = k < 4 ? sel4(a, k) : sel4(b, k - 4);
-    }
-    uint4 r;
-    r.x = (u32)((((u64)d[1] << 32) | d[0]) >> sh);
-    r.y = (u32)((((u64)d[2] << 32) | d[1]) >> sh);
-    r.z = (u32)((((u64)d[3] << 32) | d[2]) >> sh);
-    r.w = (u32)((((u64)d[4] << 32) | d[3]) >> sh);
-    return r;
 }
 
 // Segmented gather.  A workgroup owns 256 consecutive lines (their metadata
@@ -366,13 +463,13 @@ __global__ void k_col_collapse(const u8 *__restrict__ buf, const u64 *__restrict
 // skewed: without it the head artists serialise on one HBM counter); the
 // block then adds each distinct key once to the HBM table.
 #define AK_T 256
-#define AK_SLOTS 4096
+#define AK_SLOTS 2048  // 40 KB of LDS: four 256-thread workgroups per CU
 #define AK_LOCAL (1ull << 63)
 __global__ __launch_bounds__(AK_T) void k_artist_key(const u8 *__restrict__ col, const u64 *__restrict__ ar_start,
                                                      const u64 *__restrict__ ar_term, u64 nrec, u8 *__restrict__ arena,
                                                      u64 *__restrict__ key_off, u32 *__restrict__ key_len,
                                                      u64 *__restrict__ key_slot, u64 *atab, u64 amask, u32 *alist,
-                                                     u64 alist_cap, Counters *ctr) {
+                                                     u64 alist_cap, Counters *ctr, u64 short_base) {
     __shared__ u64 lh[AK_SLOTS];
     __shared__ u64 lrep[AK_SLOTS];  // first local record; after the flush: global slot
     __shared__ u32 lc[AK_SLOTS];
@@ -381,17 +478,50 @@ __global__ __launch_bounds__(AK_T) void k_artist_key(const u8 *__restrict__ col,
     const u64 stride = (u64)gridDim.x * AK_T;
     for (u64 j = (u64)blockIdx.x * AK_T + threadIdx.x; j < nrec; j += stride) {
         const u64 s = ar_start[j];
-        u64 n = ar_term[j] - s;
-        const u8 *p = col + s;
-        while (n > 0 && (p[n - 1] == '\n' || p[n - 1] == '\r')) --n;
-        const Span sp = dup_field(p, n, 0, arena + s);
-        key_off[j] = s + sp.off;
-        key_len[j] = (u32)sp.len;
-        if (sp.len == 0) {
+        const u64 L = ar_term[j] - s;
+        u64 h = 0;
+        u32 klen = 0;
+        bool fast = false;
+        if (L <= 48) {
+            // registers: strip EOL, trim; a line without '"' is its own key
+            const Win64 w = load_win64(col, s);
+            const u32 o = (u32)(s & 15);
+            const u64 fm = bits_from(o) & bits_below(o + (u32)L);
+            const u64 ne = fm & ~win_mask<2>(w);
+            const u32 endp = ne ? 64u - (u32)__clzll((long long)ne) : o;  // past the last non-EOL byte
+            const u64 f2 = fm & bits_below(endp);
+            const u64 nsp = f2 & ~win_mask<0>(w);
+            if (!nsp) {
+                fast = true;  // empty name: a song, not an artist
+            } else if (!(f2 & win_mask<1>(w))) {
+                const u32 a = (u32)__ffsll((long long)nsp) - 1, b = 63u - (u32)__clzll((long long)nsp);
+                if (b - a + 1 <= 32) {
+                    klen = b - a + 1;
+                    uint4 k0, k1;
+                    win_take32(w, a, klen, &k0, &k1);
+                    h = bytes_hash_words(k0, k1, klen);
+                    uint4 *dst = reinterpret_cast<uint4 *>(arena + short_base + 32 * j);
+                    dst[0] = k0;
+                    dst[1] = k1;
+                    key_off[j] = short_base + 32 * j;
+                    fast = true;
+                }
+            }
+        }
+        if (!fast) {
+            u64 n = L;
+            const u8 *p = col + s;
+            while (n > 0 && (p[n - 1] == '\n' || p[n - 1] == '\r')) --n;
+            const Span sp = dup_field(p, n, 0, arena + s);
+            key_off[j] = s + sp.off;
+            klen = (u32)sp.len;
+            if (klen) h = bytes_hash(arena + s + sp.off, sp.len, 0);
+        }
+        key_len[j] = klen;
+        if (klen == 0) {
             key_slot[j] = ~0ull;
             continue;
         }
-        u64 h = bytes_hash(arena + s + sp.off, sp.len, 0);
         if (h == 0) h = 0x8000000000000000ULL;
         u32 q = (u32)(h >> 20) & (AK_SLOTS - 1);
         bool done = false;
@@ -435,8 +565,25 @@ __global__ void k_artist_verify(const u8 *__restrict__ arena, const u64 *__restr
     if (rep == j) return;
     const u32 n = key_len[j];
     bool same = key_len[rep] == n;
-    const u8 *a = arena + key_off[j], *b = arena + key_off[rep];
-    for (u32 i = 0; same && i < n; ++i) same = a[i] == b[i];
+    const u64 oa = key_off[j], ob = key_off[rep];
+    if (same && n <= 32 && ((oa | ob) & 15) == 0) {  // keys in 16-byte aligned storage: vector compare
+        const uint4 *pa = reinterpret_cast<const uint4 *>(arena + oa), *pb = reinterpret_cast<const uint4 *>(arena + ob);
+        const uint4 a0 = pa[0], b0 = pb[0];
+        const uint4 a1 = n > 16 ? pa[1] : make_uint4(0, 0, 0, 0), b1 = n > 16 ? pb[1] : make_uint4(0, 0, 0, 0);
+        const u32 x[8] = {a0.x ^ b0.x, a0.y ^ b0.y, a0.z ^ b0.z, a0.w ^ b0.w,
+                          a1.x ^ b1.x, a1.y ^ b1.y, a1.z ^ b1.z, a1.w ^ b1.w};
+        u32 acc = 0;
+#pragma unroll
+        for (u32 k = 0; k < 8; ++k) {
+            const u32 lo = 4 * k;
+            const u32 keep = n <= lo ? 0u : (n >= lo + 4 ? 4u : n - lo);
+            acc |= x[k] & (keep == 4 ? 0xFFFFFFFFu : ((1u << (8 * keep)) - 1u));
+        }
+        same = acc == 0;
+    } else {
+        const u8 *a = arena + oa, *b = arena + ob;
+        for (u32 i = 0; same && i < n; ++i) same = a[i] == b[i];
+    }
     if (!same) atomicAdd((unsigned long long *)&ctr->collision, 1ull);
 }
 
@@ -768,12 +915,12 @@ hipError_t msa_launch_col_write(const u8 *buf, const u64 *len, const u64 *off, c
 }
 hipError_t msa_launch_artist_key(const u8 *col, const u64 *ar_start, const u64 *ar_term, u64 nrec, u8 *arena,
                                  u64 *key_off, u32 *key_len, u64 *key_slot, u64 *atab, u64 amask, u32 *alist,
-                                 u64 alist_cap, Counters *ctr, hipStream_t s) {
+                                 u64 alist_cap, Counters *ctr, u64 short_base, hipStream_t s) {
     if (nrec) {
         u64 blocks = (nrec + AK_T - 1) / AK_T;
         if (blocks > 1024) blocks = 1024;
         hipLaunchKernelGGL(k_artist_key, dim3((u32)blocks), dim3(AK_T), 0, s, col, ar_start, ar_term, nrec, arena,
-                           key_off, key_len, key_slot, atab, amask, alist, alist_cap, ctr);
+                           key_off, key_len, key_slot, atab, amask, alist, alist_cap, ctr, short_base);
         hipLaunchKernelGGL(k_artist_verify, grid1(nrec), dim3(256), 0, s, (const u8 *)arena, key_off, key_len,
                            key_slot, nrec, (const u64 *)atab, ctr);
     }
