@@ -22,8 +22,9 @@ u32 msa_fn_blocks(u32 nchunks);
 hipError_t msa_launch_fn(const ChunkSum *, u64, u32, Fn *, State *, Fn *, const State *, State *, State *, hipStream_t);
 hipError_t msa_launch_scan(const ScanArgs &, int, hipStream_t);
 hipError_t msa_exclusive_scan(const u64 *, u64, u64 *, u64 *, u64 *, hipStream_t);
-hipError_t msa_launch_col_span(int, const u8 *, const u64 *, const u64 *, const u32 *, const u32 *, const u32 *, u64,
-                               u64, u64 *, u64 *, u32 *, hipStream_t);
+hipError_t msa_launch_rec_fields(const u8 *, const u64 *, u64, u32 *, u32 *, hipStream_t);
+hipError_t msa_launch_col_span(int, const u8 *, const u64 *, const u32 *, const u32 *, const u32 *, u64, u64, u64 *,
+                               u64 *, u32 *, hipStream_t);
 hipError_t msa_launch_first_end(const u8 *, u64, u32, u32, u64 *, hipStream_t);
 hipError_t msa_launch_artist_verify(const u8 *, const u64 *, const u32 *, const u64 *, u64, const u64 *, Counters *,
                                     hipStream_t);
@@ -35,7 +36,7 @@ hipError_t msa_launch_exp_write(const ExpSrc &, u64, u32, const u64 *, const u64
 hipError_t msa_launch_imp(const u8 *, const u64 *, u32, u64 *, u64, const ImpDst &, hipStream_t);
 hipError_t msa_launch_col_write(const u8 *, const u64 *, const u64 *, const u64 *, const u32 *, u64, u64, u64, u8 *,
                                 hipStream_t);
-hipError_t msa_launch_artist_key(const u8 *, const u64 *, const u64 *, u64, u8 *, u64 *, u32 *, u64 *, u64 *, u64,
+hipError_t msa_launch_artist_key(const u8 *, const u64 *, u64, u8 *, u64 *, u32 *, u64 *, u64 *, u64,
                                  u32 *, u64, Counters *, u64, hipStream_t);
 hipError_t msa_launch_long(const u8 *, u64, const u8 *, u64, const u64 *, u64, u32 *, u64 *, u64 *, u64, u32 *, u64,
                            Counters *, hipStream_t);
@@ -124,7 +125,7 @@ struct msa_ctx {
     // scan scratch
     DevBuf sums, carry, btot, bstate, small;  // small: Fn total + 2 States + ...
     // CSV records
-    DevBuf rec_start, rec_term, f0rel, f3rel, nulrel;
+    DevBuf rec_start, f0rel, f3rel, nulrel;  // rec_start[nrec] = end of the last record
     u64 nrec = 0, rec_cap = 0;
     bool have_text_arrays = false;
     // side buffer: text.csv header-label remainder read back as lyrics
@@ -137,7 +138,7 @@ struct msa_ctx {
     u64 acol_len = 0, a_hdr_getline = 0, tcol_len = 0;
     bool have_tcol = false;
     // artist.csv records + keys
-    DevBuf ar_start, ar_term, arena, key_off, key_len, key_slot;
+    DevBuf ar_start, arena, key_off, key_len, key_slot;
     u64 nrec_a = 0;
     // tables
     DevBuf s_tab, s_list, m_tab, m_list, l_pos, l_len, l_slot, l_tab, l_list, a_tab, a_list;
@@ -435,8 +436,8 @@ static int materialise_column(msa_ctx *c, bool text, const std::string &hdr_line
     HIPC(c, ensure(c->scan_total, 64));
     HIPC(c, ensure(srcb, nrec * 8));
     HIPC(c, ensure(pairsb, nrec * 4));
-    HIPC(c, msa_launch_col_span(text ? 1 : 0, c->in, c->rec_start.as<u64>(), c->rec_term.as<u64>(), c->f0rel.as<u32>(),
-                                c->f3rel.as<u32>(), c->nulrel.as<u32>(), nrec, c->cont ? 0 : 1, lenb.as<u64>(), srcb.as<u64>(),
+    HIPC(c, msa_launch_col_span(text ? 1 : 0, c->in, c->rec_start.as<u64>(), c->f0rel.as<u32>(), c->f3rel.as<u32>(),
+                                c->nulrel.as<u32>(), nrec, c->cont ? 0 : 1, lenb.as<u64>(), srcb.as<u64>(),
                                 pairsb.as<u32>(), c->stream));
     HIPC(c, msa_exclusive_scan(lenb.as<u64>(), nrec, offb.as<u64>(), c->scan_bsum.as<u64>(), c->scan_total.as<u64>(),
                                c->stream));
@@ -458,6 +459,8 @@ static int materialise_column(msa_ctx *c, bool text, const std::string &hdr_line
 static int split_columns_rest(msa_ctx *c, bool want_text, const std::string &ah, const std::string &th) {
     int rc;
     prof_begin(c, ST_ARTIST_COLUMN);
+    HIPC(c, msa_launch_rec_fields(c->in, c->rec_start.as<u64>(), c->nrec, c->f0rel.as<u32>(), c->f3rel.as<u32>(),
+                                  c->stream));
     if ((rc = materialise_column(c, false, ah, c->acol, c->alen, c->aoff, c->asrc, c->apairs, &c->acol_len))) return rc;
     prof_end(c, ST_ARTIST_COLUMN, c->acol_len * 2 + c->nrec * 32);
     // compute_header_length (parallel_spotify.c:444-459): getline's end
@@ -493,13 +496,10 @@ static int do_split(msa_ctx *c, int flags) {
     c->nrec = nterm + (fin.rs < c->n ? 1 : 0);
     const u64 cap = nterm + 2;
     HIPC(c, ensure(c->rec_start, cap * 8));
-    HIPC(c, ensure(c->rec_term, cap * 8));
     HIPC(c, ensure(c->f0rel, cap * 4));
     HIPC(c, ensure(c->f3rel, cap * 4));
     HIPC(c, ensure(c->nulrel, cap * 4));
     c->rec_cap = cap;
-    HIPC(c, hipMemsetAsync(c->f0rel.p, 0, cap * 4, c->stream));
-    HIPC(c, hipMemsetAsync(c->f3rel.p, 0, cap * 4, c->stream));
     if (want_text) HIPC(c, hipMemsetAsync(c->nulrel.p, 0, cap * 4, c->stream));
     u64 zero = 0;
     HIPC(c, hipMemcpyAsync(c->rec_start.p, &zero, 8, hipMemcpyHostToDevice, c->stream));
@@ -512,9 +512,6 @@ static int do_split(msa_ctx *c, int flags) {
     a.nchunks = (u32)((c->n + MSA_CHUNK - 1) / MSA_CHUNK);
     a.carry = c->carry.as<State>();
     a.rec_start = c->rec_start.as<u64>();
-    a.rec_term = c->rec_term.as<u64>();
-    a.f0rel = c->f0rel.as<u32>();
-    a.f3rel = c->f3rel.as<u32>();
     a.nulrel = c->nulrel.as<u32>();
     a.rec_cap = cap;
     a.s_tab = c->s_tab.as<u64>();
@@ -528,25 +525,25 @@ static int do_split(msa_ctx *c, int flags) {
     a.l_pos = c->l_pos.as<u64>();
     a.l_cap = c->l_occ_cap;
     a.ctr = c->ctr.as<Counters>();
-    a.want_term = want_text ? 1 : 0;
+    a.want_nul = want_text ? 1 : 0;
     a.ablate = c->ablate;
     a.first_rec = c->cont ? 0 : 1;
     prof_begin(c, ST_CSV_SCAN);
     HIPC(c, msa_launch_scan(a, 0, c->stream));
     // algorithmic bytes: every CSV byte once + the per-record SoA it writes
-    prof_end(c, ST_CSV_SCAN, c->n + c->nrec * (want_text ? 28ull : 16ull));
-    // the last record may end at EOF instead of a terminator
+    prof_end(c, ST_CSV_SCAN, c->n + c->nrec * (want_text ? 12ull : 8ull));
+    // rec_start[nrec] = end of the last record (EOF when it has no terminator)
     if (fin.rs < c->n) {
         u64 v = c->n;
-        HIPC(c, hipMemcpyAsync(c->rec_term.as<u64>() + (c->nrec - 1), &v, 8, hipMemcpyHostToDevice, c->stream));
+        HIPC(c, hipMemcpyAsync(c->rec_start.as<u64>() + c->nrec, &v, 8, hipMemcpyHostToDevice, c->stream));
     }
     if (c->cont) return split_columns_rest(c, want_text, std::string(), std::string());
     // header record = record 0
     u64 hend = c->n;
     if (nterm > 0) {
-        // record 0's terminator offset: the start of record 1 minus its terminator bytes is not
-        // enough ('\r\n'), so read the terminator slot K3 wrote for record 0.
-        HIPC(c, hipMemcpyAsync(&hend, c->rec_term.p, 8, hipMemcpyDeviceToHost, c->stream));
+        // record 0 = [0, start of record 1), terminator included: parse_csv_line strips
+        // trailing '\n' / '\r' itself (parallel_spotify.c:267-270, h_parse_header)
+        HIPC(c, hipMemcpyAsync(&hend, c->rec_start.as<u64>() + 1, 8, hipMemcpyDeviceToHost, c->stream));
     }
     HIPC(c, hipStreamSynchronize(c->stream));
     if (hend > c->n) hend = c->n;
@@ -608,7 +605,6 @@ static int do_count(msa_ctx *c) {
     c->nrec_a = nterm + (fin.rs < e ? 1 : 0);
     const u64 cap = nterm + 2;
     HIPC(c, ensure(c->ar_start, cap * 8));
-    HIPC(c, ensure(c->ar_term, cap * 8));
     // arena: keys rewritten by duplicate_field at their artist.csv offsets, then
     // one aligned 32-byte slot per record for keys built in registers
     const u64 short_base = (e + 64 + 255) & ~255ull;
@@ -625,17 +621,15 @@ static int do_count(msa_ctx *c) {
         a.nchunks = (u32)((e - b + MSA_CHUNK - 1) / MSA_CHUNK);
         a.carry = c->carry.as<State>();
         a.rec_start = c->ar_start.as<u64>();
-        a.rec_term = c->ar_term.as<u64>();
         a.rec_cap = cap;
         a.ctr = c->ctr.as<Counters>();
-        a.want_term = 1;
         prof_begin(c, ST_ARTIST_SCAN);
         HIPC(c, msa_launch_scan(a, 1, c->stream));
         prof_end(c, ST_ARTIST_SCAN, (e - b) + c->nrec_a * 16);
     }
-    if (fin.rs < e) HIPC(c, hipMemcpyAsync(c->ar_term.as<u64>() + (c->nrec_a - 1), &e, 8, hipMemcpyHostToDevice, c->stream));
+    if (fin.rs < e) HIPC(c, hipMemcpyAsync(c->ar_start.as<u64>() + c->nrec_a, &e, 8, hipMemcpyHostToDevice, c->stream));
     prof_begin(c, ST_ARTIST_KEYS);
-    HIPC(c, msa_launch_artist_key(c->acol.as<u8>(), c->ar_start.as<u64>(), c->ar_term.as<u64>(), c->nrec_a,
+    HIPC(c, msa_launch_artist_key(c->acol.as<u8>(), c->ar_start.as<u64>(), c->nrec_a,
                                   c->arena.as<u8>(), c->key_off.as<u64>(), c->key_len.as<u32>(), c->key_slot.as<u64>(),
                                   c->a_tab.as<u64>(), c->a_slots - 1, c->a_list.as<u32>(), c->a_slots / 2,
                                   c->ctr.as<Counters>(), short_base, c->stream));
@@ -834,9 +828,9 @@ void msa_destroy(msa_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
-    DevBuf *all[] = {&c->in_own, &c->sums, &c->carry, &c->btot, &c->bstate, &c->small, &c->rec_start, &c->rec_term, &c->extra, &c->exp_buf, &c->exp_meta, &c->imp_w, &c->imp_a, &c->imp_meta,
+    DevBuf *all[] = {&c->in_own, &c->sums, &c->carry, &c->btot, &c->bstate, &c->small, &c->rec_start, &c->extra, &c->exp_buf, &c->exp_meta, &c->imp_w, &c->imp_a, &c->imp_meta,
                      &c->f0rel, &c->f3rel, &c->nulrel, &c->acol, &c->alen, &c->aoff, &c->asrc, &c->apairs, &c->tcol, &c->tlen, &c->toff, &c->tsrc, &c->tpairs,
-                     &c->scan_bsum, &c->scan_total, &c->ar_start, &c->ar_term, &c->arena, &c->key_off,
+                     &c->scan_bsum, &c->scan_total, &c->ar_start, &c->arena, &c->key_off,
                      &c->key_len, &c->key_slot, &c->s_tab, &c->s_list, &c->m_tab, &c->m_list, &c->l_pos, &c->l_len,
                      &c->l_slot, &c->l_tab, &c->l_list, &c->a_tab, &c->a_list, &c->ctr};
     for (DevBuf *b : all) release(*b);

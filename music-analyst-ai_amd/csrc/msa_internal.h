@@ -259,9 +259,6 @@ struct ScanArgs {
     u32 nchunks;
     const State *carry;
     u64 *rec_start;
-    u64 *rec_term;
-    u32 *f0rel;
-    u32 *f3rel;
     u32 *nulrel;
     u64 rec_cap;
     u64 *s_tab;
@@ -276,7 +273,7 @@ struct ScanArgs {
     u64 l_cap;
     u64 lpos_tag;    // OR'ed into recorded long-token positions (MSA_POS_EXTRA: the side buffer)
     Counters *ctr;
-    int want_term;
+    int want_nul;    // record the first NUL of each record (text column)
     int ablate;
     u32 first_rec;   // records before this index are not data (the header: 1; a continuation shard: 0)      // diagnostic builds only (MSA_ABLATE env): see msa_scan.hip
 };

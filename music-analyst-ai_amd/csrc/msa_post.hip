@@ -180,7 +180,7 @@ __device__ __forceinline__ u32 swar_space(u32 x) {  // isspace, C locale: ' ' an
     const u32 ctl = swar_ge7(y, 9) & ~swar_ge7(y, 14);
     return (ctl & ~hi) | swar_eq(x, ' ');
 }
-template <int CLS>  // 0 = space, 1 = '"', 2 = '\n' or '\r'
+template <int CLS>  // 0 = space, 1 = '"', 2 = '\n' or '\r', 3 = ',', 4 = NUL
 __device__ __forceinline__ u64 win_mask(const Win64 &w) {
     u64 m = 0;
 #pragma unroll
@@ -191,7 +191,9 @@ __device__ __forceinline__ u64 win_mask(const Win64 &w) {
             u32 v;
             if (CLS == 0) v = swar_space(d[k]);
             else if (CLS == 1) v = swar_eq(d[k], '"');
-            else v = swar_eq(d[k], '\n') | swar_eq(d[k], '\r');
+            else if (CLS == 2) v = swar_eq(d[k], '\n') | swar_eq(d[k], '\r');
+            else if (CLS == 3) v = swar_eq(d[k], ',');
+            else v = swar_eq(d[k], 0);
             m |= (u64)swar_pack4(v) << (16 * i + 4 * k);
         }
     }
@@ -242,6 +244,47 @@ __device__ __forceinline__ u32 quote_pairs(u64 q) {
     return pairs;
 }
 
+// First three unquoted commas of every record (parse_csv_line,
+// parallel_spotify.c:258-304).  Record-local: a record always starts outside
+// quotes.  64-byte windows (four dwordx4 loads) with the quote parity carried
+// from window to window; a NUL ends the C string the reference splits, so
+// commas after it do not count.  f0rel = 1 + offset of the first comma,
+// f3rel = 1 + offset just past the third (0: fewer than three -- skipped).
+__global__ __launch_bounds__(256) void k_rec_fields(const u8 *__restrict__ buf, const u64 *__restrict__ rec_start,
+                                                    u64 nrec, u32 *__restrict__ f0rel, u32 *__restrict__ f3rel) {
+    const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nrec) return;
+    const u64 s = rec_start[r], e = rec_start[r + 1];
+    u32 par = 0, nc = 0, f0 = 0, f3 = 0;
+    for (u64 base = s & ~15ull; base < e; base += 64) {
+        const Win64 w = load_win64(buf, base);
+        u64 valid = bits_below((u32)min(e - base, (u64)64));
+        if (base < s) valid &= bits_from((u32)(s - base));
+        const u64 Q = win_mask<1>(w) & valid, Z = win_mask<4>(w) & valid;
+        u64 x = Q << 1;  // exclusive prefix-xor: bit i = parity of the quotes before byte i
+        x ^= x << 1;
+        x ^= x << 2;
+        x ^= x << 4;
+        x ^= x << 8;
+        x ^= x << 16;
+        x ^= x << 32;
+        const u64 inq = x ^ (par ? ~0ull : 0ull);
+        par ^= (u32)__popcll(Q) & 1u;
+        u64 cu = win_mask<3>(w) & valid & ~inq;
+        if (Z) cu &= bits_below((u32)__ffsll((long long)Z) - 1);
+        while (cu && nc < 3) {
+            const u32 b = (u32)__ffsll((long long)cu) - 1;
+            cu &= cu - 1;
+            ++nc;
+            if (nc == 1) f0 = (u32)(base + b - s) + 1u;
+            if (nc == 3) f3 = (u32)(base + b + 1 - s) + 1u;
+        }
+        if (nc >= 3 || Z) break;
+    }
+    f0rel[r] = f0;
+    f3rel[r] = nc >= 3 ? f3 : 0u;
+}
+
 // Column lines (split_dataset_columns, parallel_spotify.c:699-714): line r is
 // duplicate_field(field, preserve=1) + '\n'.  After the outer trim a quoted
 // field -- every lyric of the real corpus -- is copied raw; an unquoted one
@@ -251,8 +294,8 @@ __device__ __forceinline__ u32 quote_pairs(u64 q) {
 // coalesced byte lanes (the collapsing copy, rare, runs on one lane).
 template <int TEXT>
 __global__ __launch_bounds__(256) void k_col_span(const u8 *__restrict__ buf, const u64 *__restrict__ rec_start,
-                                                  const u64 *__restrict__ rec_term, const u32 *__restrict__ f0rel,
-                                                  const u32 *__restrict__ f3rel, const u32 *__restrict__ nulrel,
+                                                  const u32 *__restrict__ f0rel, const u32 *__restrict__ f3rel,
+                                                  const u32 *__restrict__ nulrel,
                                                   u64 nrec, u64 first_rec, u64 *__restrict__ line_len,
                                                   u64 *__restrict__ span_src, u32 *__restrict__ span_pairs) {
     const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
@@ -265,7 +308,7 @@ __global__ __launch_bounds__(256) void k_col_span(const u8 *__restrict__ buf, co
     u64 s, e;
     if (TEXT) {  // field 3: after the third comma up to the terminator / first NUL
         s = rs + f3rel[r] - 1;
-        e = rec_term[r];
+        e = rec_start[r + 1];  // incl. the terminator: trimmed as whitespace below
         if (nulrel[r]) e = min(e, rs + nulrel[r] - 1);
         if (e < s) e = s;
     } else {  // field 0: up to the first comma
@@ -466,7 +509,7 @@ __global__ void k_col_collapse(const u8 *__restrict__ buf, const u64 *__restrict
 #define AK_SLOTS 2048  // 40 KB of LDS: four 256-thread workgroups per CU
 #define AK_LOCAL (1ull << 63)
 __global__ __launch_bounds__(AK_T) void k_artist_key(const u8 *__restrict__ col, const u64 *__restrict__ ar_start,
-                                                     const u64 *__restrict__ ar_term, u64 nrec, u8 *__restrict__ arena,
+                                                     u64 nrec, u8 *__restrict__ arena,
                                                      u64 *__restrict__ key_off, u32 *__restrict__ key_len,
                                                      u64 *__restrict__ key_slot, u64 *atab, u64 amask, u32 *alist,
                                                      u64 alist_cap, Counters *ctr, u64 short_base) {
@@ -478,7 +521,7 @@ __global__ __launch_bounds__(AK_T) void k_artist_key(const u8 *__restrict__ col,
     const u64 stride = (u64)gridDim.x * AK_T;
     for (u64 j = (u64)blockIdx.x * AK_T + threadIdx.x; j < nrec; j += stride) {
         const u64 s = ar_start[j];
-        const u64 L = ar_term[j] - s;
+        const u64 L = ar_start[j + 1] - s;  // the record incl. its terminator
         u64 h = 0;
         u32 klen = 0;
         bool fast = false;
@@ -892,15 +935,18 @@ __global__ void k_blob_write(const u32 *__restrict__ order, u64 n, const u64 *__
 // host launchers
 static inline dim3 grid1(u64 n, u32 t = 256) { return dim3((u32)((n + t - 1) / t)); }
 
-hipError_t msa_launch_col_span(int text, const u8 *buf, const u64 *rs, const u64 *rt, const u32 *f0, const u32 *f3,
-                               const u32 *nul, u64 nrec, u64 first_rec, u64 *len, u64 *src, u32 *pairs,
-                               hipStream_t s) {
+hipError_t msa_launch_rec_fields(const u8 *buf, const u64 *rs, u64 nrec, u32 *f0, u32 *f3, hipStream_t s) {
+    if (nrec) hipLaunchKernelGGL(k_rec_fields, grid1(nrec), dim3(256), 0, s, buf, rs, nrec, f0, f3);
+    return hipGetLastError();
+}
+hipError_t msa_launch_col_span(int text, const u8 *buf, const u64 *rs, const u32 *f0, const u32 *f3, const u32 *nul,
+                               u64 nrec, u64 first_rec, u64 *len, u64 *src, u32 *pairs, hipStream_t s) {
     if (!nrec) return hipSuccess;
     if (text)
-        hipLaunchKernelGGL(k_col_span<1>, grid1(nrec), dim3(256), 0, s, buf, rs, rt, f0, f3, nul, nrec, first_rec, len,
+        hipLaunchKernelGGL(k_col_span<1>, grid1(nrec), dim3(256), 0, s, buf, rs, f0, f3, nul, nrec, first_rec, len,
                            src, pairs);
     else
-        hipLaunchKernelGGL(k_col_span<0>, grid1(nrec), dim3(256), 0, s, buf, rs, rt, f0, f3, nul, nrec, first_rec, len,
+        hipLaunchKernelGGL(k_col_span<0>, grid1(nrec), dim3(256), 0, s, buf, rs, f0, f3, nul, nrec, first_rec, len,
                            src, pairs);
     return hipGetLastError();
 }
@@ -913,13 +959,13 @@ hipError_t msa_launch_col_write(const u8 *buf, const u64 *len, const u64 *off, c
     hipLaunchKernelGGL(k_col_collapse, grid1(nrec), dim3(256), 0, s, buf, len, off, src, pairs, nrec, hdr, col);
     return hipGetLastError();
 }
-hipError_t msa_launch_artist_key(const u8 *col, const u64 *ar_start, const u64 *ar_term, u64 nrec, u8 *arena,
+hipError_t msa_launch_artist_key(const u8 *col, const u64 *ar_start, u64 nrec, u8 *arena,
                                  u64 *key_off, u32 *key_len, u64 *key_slot, u64 *atab, u64 amask, u32 *alist,
                                  u64 alist_cap, Counters *ctr, u64 short_base, hipStream_t s) {
     if (nrec) {
         u64 blocks = (nrec + AK_T - 1) / AK_T;
         if (blocks > 1024) blocks = 1024;
-        hipLaunchKernelGGL(k_artist_key, dim3((u32)blocks), dim3(AK_T), 0, s, col, ar_start, ar_term, nrec, arena,
+        hipLaunchKernelGGL(k_artist_key, dim3((u32)blocks), dim3(AK_T), 0, s, col, ar_start, nrec, arena,
                            key_off, key_len, key_slot, atab, amask, alist, alist_cap, ctr, short_base);
         hipLaunchKernelGGL(k_artist_verify, grid1(nrec), dim3(256), 0, s, (const u8 *)arena, key_off, key_len,
                            key_slot, nrec, (const u64 *)atab, ctr);

@@ -428,7 +428,6 @@ __global__ __launch_bounds__(K3_THREADS) void k_scan_main(ScanArgs a) {
                 if (MODE == 0 && rr >= a.first_rec && cs >= 3 && !zs) live |= range_mask(from, b);
                 const u64 bpos = lpos + b;
                 if ((TERM >> b) & 1u) {
-                    if ((a.want_term || rr == 0) && rr < a.rec_cap) a.rec_term[rr] = bpos;
                     const u64 ns = bpos + 1 + ((SW >> b) & 1u);
                     ++rr;
                     if (rr < a.rec_cap) a.rec_start[rr] = ns;
@@ -438,14 +437,10 @@ __global__ __launch_bounds__(K3_THREADS) void k_scan_main(ScanArgs a) {
                 } else if ((Zm >> b) & 1u) {
                     if (!zs) {
                         zs = 1;
-                        if (a.want_term && rr < a.rec_cap) a.nulrel[rr] = (u32)(bpos - rs) + 1u;
+                        if (a.want_nul && rr < a.rec_cap) a.nulrel[rr] = (u32)(bpos - rs) + 1u;
                     }
                 } else if (cs < 3) {
-                    ++cs;
-                    if (rr < a.rec_cap) {
-                        if (cs == 1) a.f0rel[rr] = (u32)(bpos - rs) + 1u;
-                        if (cs == 3 && !zs) a.f3rel[rr] = (u32)(bpos + 1 - rs) + 1u;
-                    }
+                    ++cs;  // the field offsets themselves are found later (k_rec_fields)
                 }
                 from = b + 1;
             }
