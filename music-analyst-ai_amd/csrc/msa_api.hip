@@ -41,6 +41,7 @@ hipError_t msa_launch_artist_key(const u8 *, const u64 *, u64, u8 *, u64 *, u32 
 hipError_t msa_launch_long(const u8 *, u64, const u8 *, u64, const u64 *, u64, u32 *, u64 *, u64 *, u64, u32 *, u64,
                            Counters *, hipStream_t);
 hipError_t msa_launch_word_entries(const EntryArgs &, hipStream_t);
+hipError_t msa_launch_list_build(const u64 *, u64, u32, u32 *, u64, u64 *, Counters *, u64, hipStream_t);
 hipError_t msa_launch_artist_entries(const u64 *, const u32 *, u64, const u8 *, const u64 *, const u32 *, u64 *, u64 *,
                                      u64 *, u32 *, u64 *, u64 *, hipStream_t);
 hipError_t msa_launch_radix_hist_all(const u64 *, const u64 *, const u64 *, u64, u32 *, hipStream_t);
@@ -454,6 +455,17 @@ static int materialise_column(msa_ctx *c, bool text, const std::string &hdr_line
     return MSA_OK;
 }
 
+// The main scan inserts into the HBM word tables without appending to their
+// slot lists; the lists and claimed counts are built here, once per table.
+static int build_word_lists(msa_ctx *c) {
+    Counters *dc = c->ctr.as<Counters>();
+    HIPC(c, msa_launch_list_build(c->s_tab.as<u64>(), c->s_slots, 2, c->s_list.as<u32>(), c->s_slots / 2,
+                                  &dc->s_claimed, dc, (u64)OVF_S, c->stream));
+    HIPC(c, msa_launch_list_build(c->m_tab.as<u64>(), c->m_slots, 4, c->m_list.as<u32>(), c->m_slots / 2,
+                                  &dc->m_claimed, dc, (u64)OVF_M, c->stream));
+    return MSA_OK;
+}
+
 // Column materialisation after the scan.  ah / th are the header lines of
 // artist.csv / text.csv (empty for a continuation shard).
 static int split_columns_rest(msa_ctx *c, bool want_text, const std::string &ah, const std::string &th) {
@@ -537,7 +549,10 @@ static int do_split(msa_ctx *c, int flags) {
         u64 v = c->n;
         HIPC(c, hipMemcpyAsync(c->rec_start.as<u64>() + c->nrec, &v, 8, hipMemcpyHostToDevice, c->stream));
     }
-    if (c->cont) return split_columns_rest(c, want_text, std::string(), std::string());
+    if (c->cont) {
+        if ((rc = build_word_lists(c))) return rc;
+        return split_columns_rest(c, want_text, std::string(), std::string());
+    }
     // header record = record 0
     u64 hend = c->n;
     if (nterm > 0) {
@@ -588,6 +603,7 @@ static int do_split(msa_ctx *c, int flags) {
     std::string th = c->sum.text_label[0] ? c->sum.text_label : "Texts";
     ah.push_back('\n');
     th.push_back('\n');
+    if ((rc = build_word_lists(c))) return rc;
     return split_columns_rest(c, want_text, ah, th);
 }
 

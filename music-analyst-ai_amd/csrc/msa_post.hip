@@ -683,6 +683,42 @@ __device__ __forceinline__ void be16(const u8 *p, u64 n, int lower, u64 *hi, u64
     *lo = l;
 }
 
+// Dense list of the claimed slots of an S or M word table.  The main scan
+// inserts without appending to the list (every new key would serialise on one
+// claim counter); this pass reads the keys once (16 slots per thread,
+// coalesced) and adds to the claim counter once per workgroup.
+__global__ __launch_bounds__(256) void k_list_build(const u64 *__restrict__ tab, u64 nslots, u32 stride,
+                                                    u32 *__restrict__ list, u64 cap, u64 *claimed, Counters *ctr,
+                                                    u64 ovf_bit) {
+    __shared__ u32 wsum[4];
+    __shared__ u64 gbase;
+    const u32 t = threadIdx.x, lane = t & 63u, w = t >> 6;
+    const u64 s0 = (u64)blockIdx.x * 4096;
+    u32 used = 0;
+#pragma unroll
+    for (u32 k = 0; k < 16; ++k) {
+        const u64 sl = s0 + k * 256 + t;
+        if (sl < nslots && tab[sl * stride] != 0) used |= 1u << k;
+    }
+    u32 wt;
+    const u32 pre = wave_prefix<5>((u32)__popc(used), wt);
+    if (lane == 0) wsum[w] = wt;
+    __syncthreads();
+    if (t == 0) {
+        const u32 all = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        gbase = all ? atomicAdd((unsigned long long *)claimed, (unsigned long long)all) : 0ull;
+    }
+    __syncthreads();
+    u64 i = gbase + pre;
+    for (u32 v = 0; v < w; ++v) i += wsum[v];
+    for (u32 k = 0; k < 16; ++k) {
+        if (!((used >> k) & 1u)) continue;
+        if (i < cap) list[i] = (u32)(s0 + k * 256 + t);
+        else atomicOr((unsigned long long *)&ctr->overflow, (unsigned long long)ovf_bit);
+        ++i;
+    }
+}
+
 __global__ void k_word_entries(EntryArgs a) {
     const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     const u64 n = a.ns + a.nm + a.nl;
@@ -991,6 +1027,13 @@ hipError_t msa_launch_artist_verify(const u8 *arena, const u64 *key_off, const u
 hipError_t msa_launch_long_verify(const u8 *buf, const u8 *extra, const u64 *l_pos, const u32 *l_len,
                                   const u64 *l_slot, u64 n, const u64 *ltab, Counters *ctr, hipStream_t s) {
     if (n) hipLaunchKernelGGL(k_long_verify, grid1(n), dim3(256), 0, s, buf, extra, l_pos, l_len, l_slot, n, ltab, ctr);
+    return hipGetLastError();
+}
+hipError_t msa_launch_list_build(const u64 *tab, u64 nslots, u32 stride, u32 *list, u64 cap, u64 *claimed,
+                                 Counters *ctr, u64 ovf_bit, hipStream_t s) {
+    if (nslots)
+        hipLaunchKernelGGL(k_list_build, dim3((u32)((nslots + 4095) / 4096)), dim3(256), 0, s, tab, nslots, stride, list,
+                           cap, claimed, ctr, ovf_bit);
     return hipGetLastError();
 }
 hipError_t msa_launch_word_entries(const EntryArgs &a, hipStream_t s) {

@@ -45,7 +45,12 @@ __device__ __forceinline__ void wave_sync() {
 }  // namespace
 
 // ---------------------------------------------------------------------------
-// K1: per-chunk transfer function, both parity hypotheses.
+// K1: per-chunk transfer function, both parity hypotheses.  A hypothesis
+// needs only wave totals and the values at the last lane holding a
+// terminator: the terminator count from ballot bit-planes, the commas after
+// the last terminator as saturating ballot counts (min(popc, 3) per lane; the
+// state saturates at 3), the rest by readlane at that lane (scalar work).
+// Input is loaded two 1 KiB iterations ahead (the buffers are padded).
 __global__ __launch_bounds__(256) void k_chunk_summary(const u8 *__restrict__ buf, u64 seg_begin,
                                                        u64 seg_end, u32 nchunks,
                                                        ChunkSum *__restrict__ out) {
@@ -57,11 +62,13 @@ __global__ __launch_bounds__(256) void k_chunk_summary(const u8 *__restrict__ bu
         const u64 cend = min(cbase + (u64)MSA_CHUNK, seg_end);
         u32 par = 0, first_nl = 0;
         u32 cr[2] = {0, 0}, nterm[2] = {0, 0}, cc[2] = {0, 0}, zz[2] = {0, 0}, lend[2] = {0, 0};
+        uint4 cur = ld16(buf + cbase + lane * 16);
+        uint4 nxt = ld16(buf + cbase + MSA_ITER + lane * 16);
         for (u64 ibase = cbase; ibase < cend; ibase += MSA_ITER) {
             const u64 lpos = ibase + lane * 16;
-            const uint4 v = ld16(buf + lpos);
+            const uint4 nn = ld16(buf + lpos + 2 * MSA_ITER);
             const u32 vmask = valid_mask(lpos, cend);
-            const Classes k = classify16(v, vmask);
+            const Classes k = classify16(cur, vmask);
             if (ibase == cbase) first_nl = readlane(k.NL, 0) & 1u;
             const u64 B = __ballot(__popc(k.Q) & 1u);
             const u32 pin0 = par ^ (mbcnt(B) & 1u);
@@ -69,14 +76,13 @@ __global__ __launch_bounds__(256) void k_chunk_summary(const u8 *__restrict__ bu
             par ^= (u32)__popcll(B) & 1u;
             // raw '\n' at the following byte (for the '\r\n' swallow)
             const u64 nb_pos = ibase + MSA_ITER;
-            const u32 nb_nl = (nb_pos < seg_end && buf[nb_pos] == '\n') ? 1u : 0u;
+            const u32 nb_nl = (nb_pos < seg_end && (readlane(nxt.x, 0) & 0xFFu) == '\n') ? 1u : 0u;
             const u32 dn = __shfl_down(k.NL, 1);
             const u32 nlnext = (k.NL >> 1) | (((lane == 63) ? nb_nl : (dn & 1u)) << 15);
             const u32 lastb = (u32)(min(ibase + (u64)MSA_ITER, cend) - 1 - ibase);
             const int Lz = (int)(lastb >> 4);
             const u32 bz = lastb & 15u;
-            const u32 anyZ = k.Z != 0;
-            const u64 Bz = __ballot(anyZ);
+            const u64 Bz = __ballot(k.Z != 0);
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const u32 inq = h ? (~inq0 & 0xFFFFu) : inq0;
@@ -84,35 +90,34 @@ __global__ __launch_bounds__(256) void k_chunk_summary(const u8 *__restrict__ bu
                 const u32 up = __shfl_up(CRu, 1);
                 const u32 pc0 = lane ? ((up >> 15) & 1u) : cr[h];
                 const u32 TERM = (CRu | (NLu & ~((CRu << 1) | pc0))) & 0xFFFFu;
-                const u32 SW = CRu & nlnext;
                 const u32 nt = __popc(TERM);
-                const u32 lastT = nt ? 31u - __clz(TERM) : 0u;
-                const u32 above = nt ? ((0xFFFFu << (lastT + 1)) & 0xFFFFu) : 0xFFFFu;
-                const u32 cC = __popc(Cu);
-                const u32 tailC = __popc(Cu & above);
-                const u32 tailZ = (k.Z & above) != 0;
-                u32 totC, totT;
-                const u32 PC = wave_prefix<5>(cC, totC);
-                wave_prefix<5>(nt, totT);
+                u32 totT = 0;
+#pragma unroll
+                for (int b = 0; b < 5; ++b) totT += (u32)__popcll(__ballot((nt >> b) & 1u)) << b;
+                const u32 cq = min((u32)__popc(Cu), 3u);
+                const u64 C1 = __ballot(cq >= 1u), C2 = __ballot(cq >= 2u), C3 = __ballot(cq >= 3u);
                 const u64 Bh = __ballot(nt != 0);
                 if (Bh) {
                     const int jl = 63 - __clzll(Bh);
-                    const u32 after = totC - (readlane(PC, jl) + readlane(cC, jl));
-                    const u32 c_new = readlane(tailC, jl) + after;
-                    cc[h] = c_new > 3 ? 3 : c_new;
-                    const u64 above_lanes = (jl == 63) ? 0ull : (~0ull << (jl + 1));
-                    zz[h] = readlane(tailZ, jl) | ((Bz & above_lanes) != 0);
-                    const u32 lt_j = readlane(lastT, jl);
-                    const u32 sw_j = (readlane(SW, jl) >> lt_j) & 1u;
+                    const u64 A = (jl == 63) ? 0ull : (~0ull << (jl + 1));  // lanes after jl
+                    const u32 tj = readlane(TERM, jl);
+                    const u32 lt_j = 31u - __clz(tj);
+                    const u32 above = (0xFFFFu << (lt_j + 1)) & 0xFFFFu;
+                    const u32 c_new = (u32)__popc(readlane(Cu, jl) & above) + (u32)__popcll(C1 & A) +
+                                      (u32)__popcll(C2 & A) + (u32)__popcll(C3 & A);
+                    cc[h] = min(c_new, 3u);
+                    zz[h] = ((readlane(k.Z, jl) & above) != 0) | ((Bz & A) != 0);
+                    const u32 sw_j = ((readlane(CRu, jl) & readlane(nlnext, jl)) >> lt_j) & 1u;
                     lend[h] = (u32)(ibase - cbase) + (u32)jl * 16u + lt_j + 1u + sw_j;
                 } else {
-                    const u32 c_new = cc[h] + totC;
-                    cc[h] = c_new > 3 ? 3 : c_new;
+                    cc[h] = min(cc[h] + (u32)__popcll(C1) + (u32)__popcll(C2) + (u32)__popcll(C3), 3u);
                     zz[h] |= (Bz != 0);
                 }
                 nterm[h] += totT;
                 cr[h] = (readlane(CRu, Lz) >> bz) & 1u;
             }
+            cur = nxt;
+            nxt = nn;
         }
         if (lane == 0) {
             ChunkSum s;
@@ -161,27 +166,25 @@ __global__ __launch_bounds__(FN_T) void k_fn_reduce(const ChunkSum *__restrict__
 __global__ __launch_bounds__(FN_T) void k_fn_top(const Fn *__restrict__ btot, u32 nb, u64 seg_begin,
                                                  const State *__restrict__ init, State *__restrict__ bstate,
                                                  Fn *__restrict__ total) {
-    __shared__ Fn runs[FN_T];
-    __shared__ State rst[FN_T];
+    __shared__ Fn sh[2][FN_T];
     const u32 t = threadIdx.x;
     const u32 per = (nb + FN_T - 1) / FN_T;
     const u32 a = min(nb, t * per), b = min(nb, a + per);
     Fn f = fn_identity(seg_begin);
     for (u32 i = a; i < b; ++i) f = fn_compose(f, btot[i]);
-    runs[t] = f;
+    sh[0][t] = f;
     __syncthreads();
-    if (t == 0) {
-        State s = *init;
-        Fn acc = fn_identity(seg_begin);
-        for (u32 i = 0; i < FN_T; ++i) {
-            rst[i] = s;
-            s = fn_apply(s, runs[i]);
-            acc = fn_compose(acc, runs[i]);
-        }
-        if (total) *total = acc;
+    u32 cur = 0;
+    for (u32 off = 1; off < FN_T; off <<= 1) {  // inclusive scan of the runs, ping-pong buffers
+        Fn g = sh[cur][t];
+        if (t >= off) g = fn_compose(sh[cur][t - off], g);
+        sh[cur ^ 1][t] = g;
+        cur ^= 1;
+        __syncthreads();
     }
-    __syncthreads();
-    State s = rst[t];
+    State s = *init;
+    if (t > 0) s = fn_apply(s, sh[cur][t - 1]);
+    if (t == FN_T - 1 && total) *total = sh[cur][t];
     for (u32 i = a; i < b; ++i) {
         bstate[i] = s;
         s = fn_apply(s, btot[i]);
@@ -212,22 +215,32 @@ __global__ __launch_bounds__(FN_T) void k_fn_down(const ChunkSum *__restrict__ s
 }
 
 // ---------------------------------------------------------------------------
-// K3: the main pass.
+// K3: the main pass.  Default: one 1024-thread workgroup per CU (16 waves)
+// sharing one LDS count table -- the larger the table, the fewer Zipf-tail
+// words miss it.
 #ifndef K3_THREADS
-#define K3_THREADS 512
+#define K3_THREADS 1024
 #endif
 #define K3_WAVES (K3_THREADS / 64)
 #ifndef LSLOTS
-#define LSLOTS 2048
+#define LSLOTS 4096
 #endif
 #ifndef MSLOTS
 #define MSLOTS 1024
 #endif
 #ifndef K3_BLOCKS_PER_CU
-#define K3_BLOCKS_PER_CU 2
+#define K3_BLOCKS_PER_CU 1
 #endif
-#define LPROBE 8
-#define WAVE_LDS (2048 + 256 + 1024)
+// Per-wave LDS: a 2 KiB ring (this and the next 1 KiB of input), 1 KiB of
+// token entries in three lists -- S words (3..8 bytes) at [0, 256), M words
+// (9..16) at [256, 384), long words at [384, 512) -- and the deferred-miss
+// buffer: keys that miss the LDS tables are inserted into HBM in batches of
+// > K3_MISS_CAP - 64, so a wave waits on HBM once per batch, not once per
+// token pass.
+#define K3_MISS_CAP 128
+#define ST_M 256
+#define ST_L 384
+#define WAVE_LDS (2048 + 1024 + K3_MISS_CAP * 16)
 #define TAB_LDS (LSLOTS * 12 + MSLOTS * 20 + (K3_DOORKEEPER ? DK_WORDS * 4 : 0))
 #define K3_LDS (TAB_LDS + K3_WAVES * WAVE_LDS)
 
@@ -240,6 +253,8 @@ __global__ __launch_bounds__(FN_T) void k_fn_down(const ChunkSum *__restrict__ s
 #define K3_DOORKEEPER 0
 #endif
 #define DK_WORDS 2048  // doorkeeper bitset: 64 Ki bits of LDS
+static_assert(K3_LDS * K3_BLOCKS_PER_CU <= 160 * 1024, "K3 LDS exceeds the CU's 160 KiB");
+static_assert(TAB_LDS % 16 == 0 && WAVE_LDS % 16 == 0, "K3 LDS carve-outs must stay 16-byte aligned");
 // Admission filter: a key claims an LDS slot only on its second sighting in
 // this workgroup, so words seen once (the Zipf tail) do not fill the table.
 __device__ __forceinline__ bool dk_admit(u32 *dk, u64 h) {
@@ -307,6 +322,23 @@ __device__ __forceinline__ u32 lds_find_m(u64 *mk0, u64 *mk1, u32 *dk, u64 x0, u
     return ~0u;
 }
 
+// Deferred HBM inserts of LDS-table misses (k1 == 0: an S word).
+__device__ __forceinline__ void flush_misses(const ScanArgs &a, const ulonglong2 *miss, u32 n) {
+    wave_sync();
+    for (u32 t = lane_id(); t < n; t += 64) {
+        const ulonglong2 x = miss[t];
+        if (x.y == 0) s_insert<false>(a.s_tab, a.s_mask, x.x, 1, a.s_list, a.s_list_cap, a.ctr);
+        else m_insert<false>(a.m_tab, a.m_mask, x.x, x.y, 1, a.m_list, a.m_list_cap, a.ctr);
+    }
+    wave_sync();
+}
+// Called by every lane of the wave; appends the keys of the lanes with `m`.
+__device__ __forceinline__ void push_miss(ulonglong2 *miss, u32 &nmiss, bool m, u64 x0, u64 x1) {
+    const u64 B = __ballot(m);
+    if (m) miss[nmiss + mbcnt(B)] = make_ulonglong2(x0, x1);
+    nmiss += (u32)__popcll(B);
+}
+
 // MODE 0 = CSV (records, fields, lyric tokens), 1 = LINES (records only),
 //      2 = FLAT (every byte is lyric text: tokens only, no record structure)
 template <int MODE>
@@ -326,7 +358,9 @@ __global__ __launch_bounds__(K3_THREADS) void k_scan_main(ScanArgs a) {
     const u32 wib = threadIdx.x >> 6;
     unsigned char *wl = smem + TAB_LDS + wib * WAVE_LDS;
     u64 *ring = reinterpret_cast<u64 *>(wl);             // 2 KiB: two 1 KiB iteration slots
-    u16 *starts = reinterpret_cast<u16 *>(wl + 2048 + 256);
+    u16 *starts = reinterpret_cast<u16 *>(wl + 2048);    // token entries: pos | len << 10
+    ulonglong2 *miss = reinterpret_cast<ulonglong2 *>(wl + 3072);
+    u32 nmiss = 0;  // wave-uniform
     const u64 lt = (1ull << lane) - 1ull;
 
     if (TOK) {
@@ -457,59 +491,98 @@ __global__ __launch_bounds__(K3_THREADS) void k_scan_main(ScanArgs a) {
 
             if (TOK && !(a.ablate & 1)) {
                 // ---- tokens of the lyric field (process_lyrics, parallel_spotify.c:350-394)
-                // token starts S; each start's length comes from this lane's token mask
-                // and the next two lanes' (a token of <= 17 bytes spans <= 3 lanes)
+                // token starts S and each start's length class from run masks of this
+                // lane's and the next lane's token bits: r_k bit b = bytes b..b+k-1 are
+                // token bytes (b + 16 <= 31 for every start of this lane).  Tokens of
+                // fewer than 3 bytes are not counted and never leave the producer.
                 const u32 upT = __shfl_up(k.T, 1);
                 const u32 pt0 = lane ? ((upT >> 15) & 1u) : prevT;
                 const u32 S = (k.T & live) & ~((k.T << 1) | pt0) & 0xFFFFu;
                 prevT = (readlane(k.T, Lz) >> bz) & 1u;
-                const u32 n0 = readlane(tnext, 0), n1 = readlane(tnext, 1);
-                const u32 d1 = __shfl_down(k.T, 1), d2 = __shfl_down(k.T, 2);
-                const u32 T1 = lane == 63 ? n0 : d1;
-                const u32 T2 = lane == 63 ? n1 : (lane == 62 ? n0 : d2);
-                const u64 win = (u64)k.T | ((u64)T1 << 16) | ((u64)T2 << 32);
-                u32 ntok;
-                u32 idx = wave_prefix<4>(__popc(S), ntok);
-                for (u32 sm = S; sm; sm &= sm - 1) {
+                const u32 n0 = readlane(tnext, 0);
+                const u32 d1 = __shfl_down(k.T, 1);
+                const u32 w = k.T | ((lane == 63 ? n0 : d1) << 16);
+                const u32 r2 = w & (w >> 1), r3 = r2 & (w >> 2), r4 = r2 & (r2 >> 2);
+                const u32 r8 = r4 & (r4 >> 4), r9 = r8 & (w >> 8), r16 = r8 & (r8 >> 8), r17 = r16 & (w >> 16);
+                const u32 sS = S & r3 & ~r9, sM = S & r9 & ~r17, sL = S & r17;
+                const u32 cS = __popc(sS), cM = __popc(sM), cL = __popc(sL);  // <= 4, 2, 1 per lane
+                words += cS + cM + cL;
+                u32 tS, tM, tL;
+                u32 iS = wave_prefix<3>(cS, tS);
+                u32 iM = ST_M + wave_prefix<2>(cM, tM);
+                u32 iL = ST_L + wave_prefix<1>(cL, tL);
+                for (u32 sm = sS | sM | sL; sm; sm &= sm - 1) {
                     const u32 b = __ffs(sm) - 1;
-                    u32 len = (u32)__ffsll((long long)~(win >> b)) - 1u;  // win has >= 33 bits past b
-                    len = len > 63u ? 63u : len;
-                    starts[idx++] = (u16)((lane * 16 + b) | (len << 10));
+                    const u32 len = min((u32)__ffs(~(w >> b)) - 1u, 31u);  // exact up to 16
+                    const u16 e = (u16)((lane * 16 + b) | (len << 10));
+                    if ((sL >> b) & 1u) starts[iL++] = e;
+                    else if ((sM >> b) & 1u) starts[iM++] = e;
+                    else starts[iS++] = e;
                 }
                 wave_sync();
                 const u32 slot_off = (it & 1u) << 10;
-                for (u32 t = lane; t < ntok; t += 64) {
-                    const u32 ent = starts[t];
-                    const u32 len = ent >> 10;
-                    if (len < 3) continue;
-                    ++words;
-                    if (a.ablate & 2) continue;  // ablation: count only
-                    const u32 o = slot_off + (ent & 1023u);
-                    if (len > 16) {
-                        const u64 i = atomicAdd((unsigned long long *)&a.ctr->l_occ, 1ull);
-                        if (i < a.l_cap) a.l_pos[i] = (ibase + (o & 1023u)) | a.lpos_tag;
-                        else atomicOr((unsigned long long *)&a.ctr->overflow, (unsigned long long)OVF_L);
-                        continue;
-                    }
-                    const u32 q = o >> 3, sh = (o & 7u) * 8u;
-                    const u64 w0 = ring[q], w1 = ring[(q + 1) & 255u];
-                    u64 k0 = sh ? ((w0 >> sh) | (w1 << (64 - sh))) : w0;
-                    if (len <= 8) {
-                        if (a.ablate & 32) continue;  // ablation: skip S words
+                // S words: dense passes over the wave's list (every lane stays in the
+                // loop: nmiss is wave-uniform)
+                for (u32 t0 = 0; t0 < tS && !(a.ablate & 2); t0 += 64) {
+                    const u32 t = t0 + lane;
+                    bool m = false;
+                    u64 key = 0;
+                    if (t < tS && !(a.ablate & 32)) {
+                        const u32 ent = starts[t];
+                        const u32 len = ent >> 10;
+                        const u32 o = slot_off + (ent & 1023u);
+                        const u32 q = o >> 3, sh = (o & 7u) * 8u;
+                        const u64 w0 = ring[q], w1 = ring[(q + 1) & 255u];
+                        u64 k0 = sh ? ((w0 >> sh) | (w1 << (64 - sh))) : w0;
                         if (len < 8) k0 &= (1ull << (8 * len)) - 1ull;
-                        const u64 key = lower8(k0);
+                        key = lower8(k0);
                         const u32 slot = lds_find_s(lkey, dk, key);
                         if (slot != ~0u) atomicAdd(&lcnt[slot], 1u);
-                        else if (!(a.ablate & 4)) s_insert(a.s_tab, a.s_mask, key, 1, a.s_list, a.s_list_cap, a.ctr);
-                    } else {
-                        const u64 w2 = ring[(q + 2) & 255u];
+                        else m = !(a.ablate & 4);
+                    }
+                    push_miss(miss, nmiss, m, key, 0ull);
+                    if (nmiss > K3_MISS_CAP - 64) {
+                        flush_misses(a, miss, nmiss);
+                        nmiss = 0;
+                    }
+                }
+                // M words (9..16 bytes)
+                for (u32 t0 = 0; t0 < tM && !(a.ablate & 2); t0 += 64) {
+                    const u32 t = t0 + lane;
+                    bool m = false;
+                    u64 x0 = 0, x1 = 0;
+                    if (t < tM && !(a.ablate & 16)) {
+                        const u32 ent = starts[ST_M + t];
+                        const u32 len = ent >> 10;
+                        const u32 o = slot_off + (ent & 1023u);
+                        const u32 q = o >> 3, sh = (o & 7u) * 8u;
+                        const u64 w0 = ring[q], w1 = ring[(q + 1) & 255u], w2 = ring[(q + 2) & 255u];
+                        const u64 k0 = sh ? ((w0 >> sh) | (w1 << (64 - sh))) : w0;
                         u64 k1 = sh ? ((w1 >> sh) | (w2 << (64 - sh))) : w1;
                         if (len < 16) k1 &= (1ull << (8 * (len - 8))) - 1ull;
-                        if (a.ablate & 16) continue;  // ablation: skip M words
-                        const u64 x0 = lower8(k0), x1 = lower8(k1);
+                        x0 = lower8(k0);
+                        x1 = lower8(k1);
                         const u32 slot = lds_find_m(mk0, mk1, dk, x0, x1);
                         if (slot != ~0u) atomicAdd(&mcnt[slot], 1u);
-                        else m_insert(a.m_tab, a.m_mask, x0, x1, 1, a.m_list, a.m_list_cap, a.ctr);
+                        else m = true;
+                    }
+                    push_miss(miss, nmiss, m, x0, x1);
+                    if (nmiss > K3_MISS_CAP - 64) {
+                        flush_misses(a, miss, nmiss);
+                        nmiss = 0;
+                    }
+                }
+                // long words (> 16 bytes; <= 57 per KiB): positions for k_long_insert,
+                // one occurrence-counter bump per wave
+                if (tL && !(a.ablate & 2)) {
+                    u64 base = 0;
+                    if (lane == 0) base = atomicAdd((unsigned long long *)&a.ctr->l_occ, (unsigned long long)tL);
+                    base = readlane64(base, 0);
+                    if (lane < tL) {
+                        const u64 i = base + lane;
+                        const u32 ent = starts[ST_L + lane];
+                        if (i < a.l_cap) a.l_pos[i] = (ibase + (ent & 1023u)) | a.lpos_tag;
+                        else atomicOr((unsigned long long *)&a.ctr->overflow, (unsigned long long)OVF_L);
                     }
                 }
                 wave_sync();
@@ -519,16 +592,17 @@ __global__ __launch_bounds__(K3_THREADS) void k_scan_main(ScanArgs a) {
         }
     }
     if (TOK) {
+        if (nmiss) flush_misses(a, miss, nmiss);
         words = wave_sum64(words);
         if (lane == 0 && words) atomicAdd((unsigned long long *)&a.ctr->total_words, (unsigned long long)words);
         __syncthreads();
         for (u32 i = threadIdx.x; i < LSLOTS; i += K3_THREADS) {
             const u32 n = lcnt[i];
-            if (n) s_insert(a.s_tab, a.s_mask, lkey[i], n, a.s_list, a.s_list_cap, a.ctr);
+            if (n) s_insert<false>(a.s_tab, a.s_mask, lkey[i], n, a.s_list, a.s_list_cap, a.ctr);
         }
         for (u32 i = threadIdx.x; i < MSLOTS; i += K3_THREADS) {
             const u32 n = mcnt[i];
-            if (n) m_insert(a.m_tab, a.m_mask, mk0[i], mk1[i], n, a.m_list, a.m_list_cap, a.ctr);
+            if (n) m_insert<false>(a.m_tab, a.m_mask, mk0[i], mk1[i], n, a.m_list, a.m_list_cap, a.ctr);
         }
     }
 }

@@ -21,7 +21,10 @@ __device__ __forceinline__ u64 ld_relaxed(const u64 *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// S-table insert; claimed slots are appended to `list` (dense, for ranking).
+// S-table insert; claimed slots are appended to `list` (dense, for ranking)
+// unless LIST is false (the main scan: its lists are built afterwards by
+// k_list_build, so new keys do not serialise on one claim counter).
+template <bool LIST = true>
 __device__ __forceinline__ void s_insert(u64 *tab, u64 mask, u64 key, u64 cnt, u32 *list,
                                          u64 list_cap, Counters *ctr) {
     u64 h = fmix64(key) & mask;
@@ -32,9 +35,11 @@ __device__ __forceinline__ void s_insert(u64 *tab, u64 mask, u64 key, u64 cnt, u
             u64 old = atomicCAS((unsigned long long *)slot, 0ull, (unsigned long long)key);
             if (old == 0) {
                 atomicAdd((unsigned long long *)(slot + 1), (unsigned long long)cnt);
-                u64 i = atomicAdd((unsigned long long *)&ctr->s_claimed, 1ull);
-                if (i < list_cap) list[i] = (u32)h;
-                else atomicOr((unsigned long long *)&ctr->overflow, (unsigned long long)OVF_S);
+                if (LIST) {
+                    u64 i = atomicAdd((unsigned long long *)&ctr->s_claimed, 1ull);
+                    if (i < list_cap) list[i] = (u32)h;
+                    else atomicOr((unsigned long long *)&ctr->overflow, (unsigned long long)OVF_S);
+                }
                 return;
             }
             cur = old;
@@ -51,7 +56,8 @@ __device__ __forceinline__ void s_insert(u64 *tab, u64 mask, u64 key, u64 cnt, u
 // M-table insert (two-word key).  The slot is claimed by CAS on k0 and the
 // winner then publishes k1; a prober that finds k0 equal but k1 still 0 simply
 // retries that slot on its next loop trip (no spin inside a divergent branch,
-// so a same-wave winner always gets to publish).
+// so a same-wave winner always gets to publish).  LIST as for s_insert.
+template <bool LIST = true>
 __device__ __forceinline__ void m_insert(u64 *tab, u64 mask, u64 k0, u64 k1, u64 cnt, u32 *list,
                                          u64 list_cap, Counters *ctr) {
     u64 h = fmix64(k0 ^ fmix64(k1)) & mask;
@@ -64,9 +70,11 @@ __device__ __forceinline__ void m_insert(u64 *tab, u64 mask, u64 k0, u64 k1, u64
             if (old == 0) {
                 __hip_atomic_store(slot + 1, k1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 atomicAdd((unsigned long long *)(slot + 2), (unsigned long long)cnt);
-                u64 i = atomicAdd((unsigned long long *)&ctr->m_claimed, 1ull);
-                if (i < list_cap) list[i] = (u32)h;
-                else atomicOr((unsigned long long *)&ctr->overflow, (unsigned long long)OVF_M);
+                if (LIST) {
+                    u64 i = atomicAdd((unsigned long long *)&ctr->m_claimed, 1ull);
+                    if (i < list_cap) list[i] = (u32)h;
+                    else atomicOr((unsigned long long *)&ctr->overflow, (unsigned long long)OVF_M);
+                }
                 return;
             }
             c0 = old;
