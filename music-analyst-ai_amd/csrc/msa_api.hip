@@ -34,7 +34,7 @@ hipError_t msa_launch_exp_count(const ExpSrc &, u64, u32, u64 *, u64 *, hipStrea
 hipError_t msa_launch_exp_write(const ExpSrc &, u64, u32, const u64 *, const u64 *, const u64 *, u64 *, u64 *, u8 *,
                                 hipStream_t);
 hipError_t msa_launch_imp(const u8 *, const u64 *, u32, u64 *, u64, const ImpDst &, hipStream_t);
-hipError_t msa_launch_col_write(const u8 *, const u64 *, const u64 *, const u64 *, const u32 *, u64, u64, u64, u8 *,
+hipError_t msa_launch_col_write(int, const u8 *, const u64 *, const u64 *, const u64 *, const u32 *, u64, u64, u64, u8 *,
                                 hipStream_t);
 hipError_t msa_launch_artist_key(const u8 *, const u64 *, u64, u8 *, u64 *, u32 *, u64 *, u64 *, u64,
                                  u32 *, u64, Counters *, u64, hipStream_t);
@@ -44,10 +44,7 @@ hipError_t msa_launch_word_entries(const EntryArgs &, hipStream_t);
 hipError_t msa_launch_list_build(const u64 *, u64, u32, u32 *, u64, u64 *, Counters *, u64, hipStream_t);
 hipError_t msa_launch_artist_entries(const u64 *, const u32 *, u64, const u8 *, const u64 *, const u32 *, u64 *, u64 *,
                                      u64 *, u32 *, u64 *, u64 *, hipStream_t);
-hipError_t msa_launch_radix_hist_all(const u64 *, const u64 *, const u64 *, u64, u32 *, hipStream_t);
-u64 msa_radix_blocks(u64 n);
-hipError_t msa_launch_radix_pass(const u64 *, const u64 *, const u64 *, const u32 *, u64, u32, u64 *, u64 *, u64 *,
-                                 u64 *, u64 *, u64 *, u32 *, hipStream_t);
+hipError_t msa_launch_sort(u64 *const[3], u64 *const[3], u64 *const[3], u32 *const[3], u64, int *, hipStream_t);
 hipError_t msa_launch_fixup(const u64 *, const u64 *, const u64 *, const u32 *, u64, const u64 *, const u8 *,
                             const u8 *, const u64 *, const u32 *, const u8 *, const u64 *, const u32 *, u32 *, hipStream_t);
 hipError_t msa_launch_blob(const u32 *, u64, const u64 *, const u64 *, const u64 *, const u64 *, const u8 *,
@@ -67,7 +64,6 @@ struct Ranked {
     DevBuf K[3][3];  // [set][k2,k1,k0]: set 0 = input, 1/2 = ping-pong
     DevBuf V[3];
     DevBuf ref, cnt, order, len, off, blob, counts;
-    DevBuf bhist, boff, bsum, ghist;
     u64 n = 0, blob_len = 0;
     std::vector<u64> h_counts, h_off;
     std::vector<char> h_blob;
@@ -90,7 +86,7 @@ enum {
     ST_ARTIST_SCAN,      // K3 (records only) over artist.csv
     ST_ARTIST_KEYS,      // duplicate_field + artist table
     ST_LONG_WORDS,       // > 16-byte words: hash table + verification
-    ST_RANK_WORDS,       // entries + radix sort + key blob, words
+    ST_RANK_WORDS,       // entries + sort + key blob, words
     ST_RANK_ARTISTS,     // the same, artists
     ST_COUNT_
 };
@@ -449,7 +445,7 @@ static int materialise_column(msa_ctx *c, bool text, const std::string &hdr_line
     HIPC(c, ensure(col, total + MSA_INPUT_PAD));
     HIPC(c, hipMemcpyAsync(col.p, hdr_line.data(), hdr_line.size(), hipMemcpyHostToDevice, c->stream));
     HIPC(c, hipMemsetAsync(col.as<char>() + total, 0, MSA_INPUT_PAD, c->stream));
-    HIPC(c, msa_launch_col_write(c->in, lenb.as<u64>(), offb.as<u64>(), srcb.as<u64>(), pairsb.as<u32>(), nrec,
+    HIPC(c, msa_launch_col_write(text ? 1 : 0, c->in, lenb.as<u64>(), offb.as<u64>(), srcb.as<u64>(), pairsb.as<u32>(), nrec,
                                  hdr_line.size(), body, col.as<u8>(), c->stream));
     *col_len = total;
     return MSA_OK;
@@ -686,34 +682,20 @@ static int sort_and_blob(msa_ctx *c, Ranked &R, const u8 *wbuf, const u8 *wextra
         R.blob_len = 0;
         return MSA_OK;
     }
-    const u64 nb = msa_radix_blocks(n);
     for (int s = 1; s < 3; ++s) {
         for (int k = 0; k < 3; ++k) HIPC(c, ensure(R.K[s][k], n * 8));
         HIPC(c, ensure(R.V[s], n * 4));
     }
-    HIPC(c, ensure(R.bhist, nb * 256 * 8));
-    HIPC(c, ensure(R.boff, nb * 256 * 8));
-    HIPC(c, ensure(R.bsum, ((nb * 256 + 1023) / 1024 + 1) * 8));
-    HIPC(c, ensure(R.ghist, 24 * 256 * 4));
-    HIPC(c, msa_launch_radix_hist_all(R.K[0][0].as<u64>(), R.K[0][1].as<u64>(), R.K[0][2].as<u64>(), n,
-                                      R.ghist.as<u32>(), c->stream));
-    std::vector<u32> gh(24 * 256);
-    HIPC(c, hipMemcpyAsync(gh.data(), R.ghist.p, gh.size() * 4, hipMemcpyDeviceToHost, c->stream));
-    HIPC(c, hipStreamSynchronize(c->stream));
-    int cur = 0;
-    // digit d: 0..7 = K0 bytes, 8..15 = K1 bytes, 16..23 = K2 bytes (LSD first)
-    for (u32 d = 0; d < 24; ++d) {
-        bool trivial = false;
-        for (int i = 0; i < 256; ++i)
-            if (gh[d * 256 + i] == n) { trivial = true; break; }
-        if (trivial) continue;
-        const int nxt = (cur == 1) ? 2 : 1;
-        HIPC(c, msa_launch_radix_pass(R.K[cur][0].as<u64>(), R.K[cur][1].as<u64>(), R.K[cur][2].as<u64>(),
-                                      R.V[cur].as<u32>(), n, d, R.bhist.as<u64>(), R.boff.as<u64>(), R.bsum.as<u64>(),
-                                      R.K[nxt][0].as<u64>(), R.K[nxt][1].as<u64>(), R.K[nxt][2].as<u64>(),
-                                      R.V[nxt].as<u32>(), c->stream));
-        cur = nxt;
+    u64 *k2[3], *k1[3], *k0[3];
+    u32 *vv[3];
+    for (int s = 0; s < 3; ++s) {
+        k2[s] = R.K[s][0].as<u64>();
+        k1[s] = R.K[s][1].as<u64>();
+        k0[s] = R.K[s][2].as<u64>();
+        vv[s] = R.V[s].as<u32>();
     }
+    int cur = 1;
+    HIPC(c, msa_launch_sort(k2, k1, k0, vv, n, &cur, c->stream));
     HIPC(c, ensure(R.order, n * 4));
     HIPC(c, msa_launch_fixup(R.K[cur][0].as<u64>(), R.K[cur][1].as<u64>(), R.K[cur][2].as<u64>(), R.V[cur].as<u32>(),
                              n, R.ref.as<u64>(), wbuf, wextra, c->l_pos.as<u64>(), c->l_len.as<u32>(), arena, key_off,
@@ -854,8 +836,7 @@ void msa_destroy(msa_ctx *c) {
         for (auto &s : R->K)
             for (auto &k : s) release(k);
         for (auto &v : R->V) release(v);
-        DevBuf *rb[] = {&R->ref, &R->cnt, &R->order, &R->len, &R->off, &R->blob, &R->counts, &R->bhist, &R->boff,
-                        &R->bsum, &R->ghist};
+        DevBuf *rb[] = {&R->ref, &R->cnt, &R->order, &R->len, &R->off, &R->blob, &R->counts};
         for (DevBuf *b : rb) release(*b);
     }
     for (ProfStage &s : c->ps) {

@@ -3,9 +3,9 @@
 //     split_dataset_columns' artist.csv (640-721), and the artist pass's
 //     duplicate_field(line, 0) + ht_put (948-998) as exact 64-bit-hash counts
 //   * words longer than 16 bytes (H-table + byte-exact verification)
-//   * ranking: stable LSD radix sort on (count desc, first 16 key bytes) with
-//     an exact strcmp fix-up of the rare equal-prefix runs -- the order of
-//     entry_compare_desc (178-188) without a comparison sort
+//   * ranking: sort on (count desc, first 16 key bytes) -- bitonic tiles in
+//     LDS, then merge passes by rank -- with an exact strcmp fix-up of the
+//     rare equal-prefix runs: the order of entry_compare_desc (178-188)
 //   * generic exclusive scan (u64)
 #include "msa_internal.h"
 #include "msa_tables.h"
@@ -481,6 +481,81 @@ __global__ __launch_bounds__(CG_T) void k_col_gather(const u8 *__restrict__ buf,
     }
 }
 
+// Short lines (the artist column, ~15 bytes a line): one thread per line
+// writes its bytes into LDS at the line's output offset (source from a 64-byte
+// register window; longer lines and lines with "" pairs by a byte loop), then
+// the workgroup stores its contiguous output range with aligned 16-byte
+// stores (ragged first/last chunk byte by byte).  A workgroup whose range does
+// not fit the stage writes its lines straight to the column.
+#define CL_T 256
+#define CL_LDS 16384
+template <typename P>
+__device__ __forceinline__ void put_line(P dst, const u8 *__restrict__ buf, u64 s, u64 len, u32 pairs) {
+    if (!pairs && (s & 15) + len <= 64) {
+        const Win64 w = load_win64(buf, s);
+        const u32 o = (u32)(s & 15);
+        uint4 x0, x1, y0, y1;
+        win_take32(w, o, (u32)min(len, (u64)32), &x0, &x1);
+        win_take32(w, o + 32, len > 32 ? (u32)len - 32 : 0u, &y0, &y1);
+        const u32 d[16] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w,
+                           y0.x, y0.y, y0.z, y0.w, y1.x, y1.y, y1.z, y1.w};
+#pragma unroll
+        for (u32 k = 0; k < 16; ++k) {
+            if (4 * k >= len) break;
+#pragma unroll
+            for (u32 b = 0; b < 4; ++b)
+                if (4 * k + b < len) dst[4 * k + b] = (u8)(d[k] >> (8 * b));
+        }
+    } else {
+        const u64 n = len + pairs;
+        u64 j = 0;
+        for (u64 i = 0; i < n; ++i) {
+            const u8 ch = buf[s + i];
+            if (pairs && ch == '"' && i + 1 < n && buf[s + i + 1] == '"') ++i;
+            dst[j++] = ch;
+        }
+    }
+    dst[len] = '\n';
+}
+
+__global__ __launch_bounds__(CL_T) void k_col_lines(const u8 *__restrict__ buf, const u64 *__restrict__ line_len,
+                                                    const u64 *__restrict__ line_off, const u64 *__restrict__ span_src,
+                                                    const u32 *__restrict__ span_pairs, u64 nrec, u64 hdr, u64 body,
+                                                    u8 *__restrict__ col) {
+    __shared__ __attribute__((aligned(16))) u8 st[CL_LDS];
+    const u64 r0 = (u64)blockIdx.x * CL_T;
+    const u32 t = threadIdx.x;
+    const u64 r = r0 + t;
+    const u64 wn = min((u64)CL_T, nrec - r0);
+    const u64 B0 = line_off[r0];
+    const u64 B1 = (r0 + wn < nrec) ? line_off[r0 + wn] : body;
+    const u64 A0 = hdr + B0, A1 = hdr + B1;  // this workgroup's output bytes
+    const u64 lead = A0 & 15;                // st[i] <-> col[(A0 & ~15) + i]
+    const bool staged = (A1 - A0) + lead <= CL_LDS;
+    if (r < nrec) {
+        const u64 L = line_len[r];
+        if (L) {
+            if (staged) put_line(st + lead + (line_off[r] - B0), buf, span_src[r], L - 1, span_pairs[r]);
+            else put_line(col + hdr + line_off[r], buf, span_src[r], L - 1, span_pairs[r]);
+        }
+    }
+    if (!staged) return;
+    __syncthreads();
+    const u64 C0 = A0 & ~15ull;
+    const u64 nch = (A1 - C0 + 15) / 16;
+    for (u64 k = t; k < nch; k += CL_T) {
+        const u64 a = C0 + 16 * k;
+        if (a >= A0 && a + 16 <= A1) {
+            *reinterpret_cast<uint4 *>(col + a) = *reinterpret_cast<const uint4 *>(st + 16 * k);
+        } else {
+            for (u32 b = 0; b < 16; ++b) {
+                const u64 x = a + b;
+                if (x >= A0 && x < A1) col[x] = st[16 * k + b];
+            }
+        }
+    }
+}
+
 // Lines with "" pairs to collapse (duplicate_field, parallel_spotify.c:243-250).
 __global__ void k_col_collapse(const u8 *__restrict__ buf, const u64 *__restrict__ line_len,
                                const u64 *__restrict__ line_off, const u64 *__restrict__ span_src,
@@ -772,86 +847,85 @@ __global__ void k_artist_entries(const u64 *__restrict__ atab, const u32 *__rest
 }
 
 // ---------------------------------------------------------------------------
-// Stable LSD radix sort, 8-bit digits, on (K2, K1, K0) with u32 values.
-#define RS_T 256
-#define RS_ITEMS 8
-#define RS_TILE (RS_T * RS_ITEMS)
-
-__device__ __forceinline__ u32 digit_of(const u64 *K2, const u64 *K1, const u64 *K0, u64 i, u32 d) {
-    const u64 *k = d < 8 ? K0 : (d < 16 ? K1 : K2);
-    return (u32)(k[i] >> (8 * (d & 7))) & 0xFFu;
+// Sort of (K2, K1, K0) ascending with u32 values.  Tables hold 10^3..10^6
+// distinct keys, so the sort is launch- and latency-bound: 1024-element tiles
+// are bitonic-sorted in LDS (one launch), then log2(n / 1024) merge passes,
+// each element finding its output position by one binary search in the
+// partner run (A-elements count partner keys <, B-elements <=, so equal keys
+// keep A before B and every position is written once).  Equal keys (long
+// words sharing 16 bytes and a count) are ordered by k_tie_fixup.
+#define TS_T 512
+#define TS_N 1024
+__device__ __forceinline__ bool key_lt(u64 a2, u64 a1, u64 a0, u64 b2, u64 b1, u64 b0) {
+    return a2 != b2 ? a2 < b2 : (a1 != b1 ? a1 < b1 : a0 < b0);
 }
 
-__global__ __launch_bounds__(RS_T) void k_radix_hist_all(const u64 *__restrict__ K2, const u64 *__restrict__ K1,
-                                                         const u64 *__restrict__ K0, u64 n, u32 *__restrict__ ghist) {
-    __shared__ u32 h[24 * 256];
-    for (u32 i = threadIdx.x; i < 24 * 256; i += RS_T) h[i] = 0;
-    __syncthreads();
-    for (u64 i = (u64)blockIdx.x * RS_T + threadIdx.x; i < n; i += (u64)gridDim.x * RS_T) {
-        const u64 k[3] = {K0[i], K1[i], K2[i]};
-        for (u32 d = 0; d < 24; ++d) atomicAdd(&h[d * 256 + ((k[d >> 3] >> (8 * (d & 7))) & 0xFF)], 1u);
+__global__ __launch_bounds__(TS_T) void k_tile_sort(const u64 *__restrict__ K2, const u64 *__restrict__ K1,
+                                                    const u64 *__restrict__ K0, const u32 *__restrict__ V, u64 n,
+                                                    u64 *__restrict__ O2, u64 *__restrict__ O1,
+                                                    u64 *__restrict__ O0, u32 *__restrict__ OV) {
+    __shared__ u64 s2[TS_N], s1[TS_N], s0[TS_N];
+    __shared__ u32 sv[TS_N];
+    const u64 base = (u64)blockIdx.x * TS_N;
+    const u32 t = threadIdx.x;
+    for (u32 i = t; i < TS_N; i += TS_T) {
+        const u64 g = base + i;
+        const bool ok = g < n;  // padding sorts last
+        s2[i] = ok ? K2[g] : ~0ull;
+        s1[i] = ok ? K1[g] : ~0ull;
+        s0[i] = ok ? K0[g] : ~0ull;
+        sv[i] = ok ? V[g] : ~0u;
     }
     __syncthreads();
-    for (u32 i = threadIdx.x; i < 24 * 256; i += RS_T)
-        if (h[i]) atomicAdd(&ghist[i], h[i]);
-}
-
-__global__ __launch_bounds__(RS_T) void k_radix_count(const u64 *__restrict__ K2, const u64 *__restrict__ K1,
-                                                      const u64 *__restrict__ K0, u64 n, u32 d, u64 nb,
-                                                      u64 *__restrict__ bhist) {
-    __shared__ u32 h[256];
-    h[threadIdx.x] = 0;
-    __syncthreads();
-    const u64 base = (u64)blockIdx.x * RS_TILE;
-    for (int r = 0; r < RS_ITEMS; ++r) {
-        const u64 i = base + (u64)r * RS_T + threadIdx.x;
-        if (i < n) atomicAdd(&h[digit_of(K2, K1, K0, i, d)], 1u);
-    }
-    __syncthreads();
-    bhist[(u64)threadIdx.x * nb + blockIdx.x] = h[threadIdx.x];
-}
-
-__global__ __launch_bounds__(RS_T) void k_radix_scatter(const u64 *__restrict__ K2, const u64 *__restrict__ K1,
-                                                        const u64 *__restrict__ K0, const u32 *__restrict__ V, u64 n,
-                                                        u32 d, u64 nb, const u64 *__restrict__ boff,
-                                                        u64 *__restrict__ O2, u64 *__restrict__ O1,
-                                                        u64 *__restrict__ O0, u32 *__restrict__ OV) {
-    __shared__ u64 run[256];
-    __shared__ u32 wc[RS_T / 64][256];
-    const u32 lane = lane_id(), w = threadIdx.x >> 6;
-    run[threadIdx.x] = boff[(u64)threadIdx.x * nb + blockIdx.x];
-    const u64 base = (u64)blockIdx.x * RS_TILE;
-    for (int r = 0; r < RS_ITEMS; ++r) {
-        for (u32 ww = 0; ww < RS_T / 64; ++ww) wc[ww][threadIdx.x] = 0;
-        __syncthreads();
-        const u64 i = base + (u64)r * RS_T + threadIdx.x;
-        const bool ok = i < n;
-        u32 dg = ok ? digit_of(K2, K1, K0, i, d) : 0;
-        u32 rank = 0;
-        if (ok) {
-            u64 m = __ballot(1);
-            for (int b = 0; b < 8; ++b) {
-                const u64 bb = __ballot((dg >> b) & 1u);
-                m &= ((dg >> b) & 1u) ? bb : ~bb;
+    for (u32 k = 2; k <= TS_N; k <<= 1) {
+        for (u32 j = k >> 1; j > 0; j >>= 1) {
+            const u32 i = ((t & ~(j - 1)) << 1) | (t & (j - 1)), l = i | j;
+            const u64 a2 = s2[i], a1 = s1[i], a0 = s0[i], b2 = s2[l], b1 = s1[l], b0 = s0[l];
+            const bool asc = (i & k) == 0;
+            if (key_lt(b2, b1, b0, a2, a1, a0) == asc) {
+                s2[i] = b2; s1[i] = b1; s0[i] = b0;
+                s2[l] = a2; s1[l] = a1; s0[l] = a0;
+                const u32 x = sv[i];
+                sv[i] = sv[l];
+                sv[l] = x;
             }
-            rank = mbcnt(m);
-            if (rank == 0) wc[w][dg] = (u32)__popcll(m);
+            __syncthreads();
         }
-        __syncthreads();
-        if (ok) {
-            u64 pos = run[dg] + rank;
-            for (u32 ww = 0; ww < w; ++ww) pos += wc[ww][dg];
-            O2[pos] = K2[i];
-            O1[pos] = K1[i];
-            O0[pos] = K0[i];
-            OV[pos] = V[i];
-        }
-        __syncthreads();
-        u32 tot = 0;
-        for (u32 ww = 0; ww < RS_T / 64; ++ww) tot += wc[ww][threadIdx.x];
-        run[threadIdx.x] += tot;
-        __syncthreads();
     }
+    for (u32 i = t; i < TS_N; i += TS_T) {
+        const u64 g = base + i;
+        if (g < n) {
+            O2[g] = s2[i];
+            O1[g] = s1[i];
+            O0[g] = s0[i];
+            OV[g] = sv[i];
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_merge_pass(const u64 *__restrict__ K2, const u64 *__restrict__ K1,
+                                                    const u64 *__restrict__ K0, const u32 *__restrict__ V, u64 n,
+                                                    u64 width, u64 *__restrict__ O2, u64 *__restrict__ O1,
+                                                    u64 *__restrict__ O0, u32 *__restrict__ OV) {
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const u64 run = i / width, base = (run & ~1ull) * width;
+    const bool left = (run & 1ull) == 0;
+    const u64 a2 = K2[i], a1 = K1[i], a0 = K0[i];
+    const u64 lo = left ? min(base + width, n) : base, hi = left ? min(base + 2 * width, n) : base + width;
+    u64 L = lo, H = hi;
+    while (L < H) {
+        const u64 m = (L + H) >> 1;
+        const u64 b2 = K2[m], b1 = K1[m], b0 = K0[m];
+        const bool before = left ? key_lt(b2, b1, b0, a2, a1, a0) : !key_lt(a2, a1, a0, b2, b1, b0);
+        if (before) L = m + 1;
+        else H = m;
+    }
+    const u64 out = base + (i - (left ? base : base + width)) + (L - lo);
+    O2[out] = a2;
+    O1[out] = a1;
+    O0[out] = a0;
+    OV[out] = V[i];
 }
 
 // ---------------------------------------------------------------------------
@@ -986,9 +1060,14 @@ hipError_t msa_launch_col_span(int text, const u8 *buf, const u64 *rs, const u32
                            src, pairs);
     return hipGetLastError();
 }
-hipError_t msa_launch_col_write(const u8 *buf, const u64 *len, const u64 *off, const u64 *src, const u32 *pairs,
-                                u64 nrec, u64 hdr, u64 body, u8 *col, hipStream_t s) {
+hipError_t msa_launch_col_write(int text, const u8 *buf, const u64 *len, const u64 *off, const u64 *src,
+                                const u32 *pairs, u64 nrec, u64 hdr, u64 body, u8 *col, hipStream_t s) {
     if (!nrec || !body) return hipSuccess;
+    if (!text) {
+        hipLaunchKernelGGL(k_col_lines, dim3((u32)((nrec + CL_T - 1) / CL_T)), dim3(CL_T), 0, s, buf, len, off, src,
+                           pairs, nrec, hdr, body, col);
+        return hipGetLastError();
+    }
     const u64 groups = (nrec + CG_T - 1) / CG_T;
     hipLaunchKernelGGL(k_col_gather, dim3((u32)groups), dim3(CG_T), 0, s, buf, len, off, src, pairs, nrec, hdr, body,
                        col);
@@ -1049,25 +1128,22 @@ hipError_t msa_launch_artist_entries(const u64 *atab, const u32 *alist, u64 n, c
                            K1, K0, val, ref, cnt);
     return hipGetLastError();
 }
-hipError_t msa_launch_radix_hist_all(const u64 *K2, const u64 *K1, const u64 *K0, u64 n, u32 *ghist, hipStream_t s) {
-    hipError_t e = hipMemsetAsync(ghist, 0, 24 * 256 * sizeof(u32), s);
-    if (e != hipSuccess) return e;
-    if (n) {
-        u64 blocks = (n + RS_T - 1) / RS_T;
-        if (blocks > 1024) blocks = 1024;
-        hipLaunchKernelGGL(k_radix_hist_all, dim3((u32)blocks), dim3(RS_T), 0, s, K2, K1, K0, n, ghist);
+// Sorts set `in` into one of the two ping-pong sets; returns the set holding
+// the result in *which (1 or 2).
+hipError_t msa_launch_sort(u64 *const K2[3], u64 *const K1[3], u64 *const K0[3], u32 *const V[3], u64 n, int *which,
+                           hipStream_t s) {
+    *which = 1;
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_tile_sort, dim3((u32)((n + TS_N - 1) / TS_N)), dim3(TS_T), 0, s, K2[0], K1[0], K0[0], V[0],
+                       n, K2[1], K1[1], K0[1], V[1]);
+    int cur = 1;
+    for (u64 w = TS_N; w < n; w <<= 1) {
+        const int nx = cur == 1 ? 2 : 1;
+        hipLaunchKernelGGL(k_merge_pass, grid1(n), dim3(256), 0, s, K2[cur], K1[cur], K0[cur], V[cur], n, w, K2[nx],
+                           K1[nx], K0[nx], V[nx]);
+        cur = nx;
     }
-    return hipGetLastError();
-}
-u64 msa_radix_blocks(u64 n) { return (n + RS_TILE - 1) / RS_TILE; }
-hipError_t msa_launch_radix_pass(const u64 *K2, const u64 *K1, const u64 *K0, const u32 *V, u64 n, u32 d, u64 *bhist,
-                                 u64 *boff, u64 *bsum, u64 *O2, u64 *O1, u64 *O0, u32 *OV, hipStream_t s) {
-    const u64 nb = msa_radix_blocks(n);
-    hipLaunchKernelGGL(k_radix_count, dim3((u32)nb), dim3(RS_T), 0, s, K2, K1, K0, n, d, nb, bhist);
-    hipError_t e = msa_exclusive_scan(bhist, nb * 256, boff, bsum, nullptr, s);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_radix_scatter, dim3((u32)nb), dim3(RS_T), 0, s, K2, K1, K0, V, n, d, nb,
-                       (const u64 *)boff, O2, O1, O0, OV);
+    *which = cur;
     return hipGetLastError();
 }
 hipError_t msa_launch_fixup(const u64 *K2, const u64 *K1, const u64 *K0, const u32 *V, u64 n, const u64 *ref,
