@@ -22,9 +22,8 @@ u32 msa_fn_blocks(u32 nchunks);
 hipError_t msa_launch_fn(const ChunkSum *, u64, u32, Fn *, State *, Fn *, const State *, State *, State *, hipStream_t);
 hipError_t msa_launch_scan(const ScanArgs &, int, hipStream_t);
 hipError_t msa_exclusive_scan(const u64 *, u64, u64 *, u64 *, u64 *, hipStream_t);
-hipError_t msa_launch_rec_fields(const u8 *, const u64 *, u64, u32 *, u32 *, hipStream_t);
-hipError_t msa_launch_col_span(int, const u8 *, const u64 *, const u32 *, const u32 *, const u32 *, u64, u64, u64 *,
-                               u64 *, u32 *, hipStream_t);
+hipError_t msa_launch_rec_spans(const u8 *, const u64 *, const u32 *, u64, u64, int, u64 *, u64 *, u32 *, u64 *, u64 *,
+                                u32 *, hipStream_t);
 hipError_t msa_launch_first_end(const u8 *, u64, u32, u32, u64 *, hipStream_t);
 hipError_t msa_launch_artist_verify(const u8 *, const u64 *, const u32 *, const u64 *, u64, const u64 *, Counters *,
                                     hipStream_t);
@@ -122,7 +121,7 @@ struct msa_ctx {
     // scan scratch
     DevBuf sums, carry, btot, bstate, small;  // small: Fn total + 2 States + ...
     // CSV records
-    DevBuf rec_start, f0rel, f3rel, nulrel;  // rec_start[nrec] = end of the last record
+    DevBuf rec_start, nulrel;  // rec_start[nrec] = end of the last record
     u64 nrec = 0, rec_cap = 0;
     bool have_text_arrays = false;
     // side buffer: text.csv header-label remainder read back as lyrics
@@ -427,15 +426,9 @@ static int sync_counters(msa_ctx *c) {
 static int materialise_column(msa_ctx *c, bool text, const std::string &hdr_line, DevBuf &col, DevBuf &lenb,
                               DevBuf &offb, DevBuf &srcb, DevBuf &pairsb, u64 *col_len) {
     const u64 nrec = c->nrec;
-    HIPC(c, ensure(lenb, nrec * 8));
     HIPC(c, ensure(offb, nrec * 8));
     HIPC(c, ensure(c->scan_bsum, ((nrec + 1023) / 1024 + 1) * 8));
     HIPC(c, ensure(c->scan_total, 64));
-    HIPC(c, ensure(srcb, nrec * 8));
-    HIPC(c, ensure(pairsb, nrec * 4));
-    HIPC(c, msa_launch_col_span(text ? 1 : 0, c->in, c->rec_start.as<u64>(), c->f0rel.as<u32>(), c->f3rel.as<u32>(),
-                                c->nulrel.as<u32>(), nrec, c->cont ? 0 : 1, lenb.as<u64>(), srcb.as<u64>(),
-                                pairsb.as<u32>(), c->stream));
     HIPC(c, msa_exclusive_scan(lenb.as<u64>(), nrec, offb.as<u64>(), c->scan_bsum.as<u64>(), c->scan_total.as<u64>(),
                                c->stream));
     u64 body = 0;
@@ -467,8 +460,19 @@ static int build_word_lists(msa_ctx *c) {
 static int split_columns_rest(msa_ctx *c, bool want_text, const std::string &ah, const std::string &th) {
     int rc;
     prof_begin(c, ST_ARTIST_COLUMN);
-    HIPC(c, msa_launch_rec_fields(c->in, c->rec_start.as<u64>(), c->nrec, c->f0rel.as<u32>(), c->f3rel.as<u32>(),
-                                  c->stream));
+    // line spans of both columns in one pass over the records
+    const u64 nrec = c->nrec;
+    HIPC(c, ensure(c->alen, nrec * 8));
+    HIPC(c, ensure(c->asrc, nrec * 8));
+    HIPC(c, ensure(c->apairs, nrec * 4));
+    if (want_text) {
+        HIPC(c, ensure(c->tlen, nrec * 8));
+        HIPC(c, ensure(c->tsrc, nrec * 8));
+        HIPC(c, ensure(c->tpairs, nrec * 4));
+    }
+    HIPC(c, msa_launch_rec_spans(c->in, c->rec_start.as<u64>(), c->nulrel.as<u32>(), nrec, c->cont ? 0 : 1,
+                                 want_text ? 1 : 0, c->alen.as<u64>(), c->asrc.as<u64>(), c->apairs.as<u32>(),
+                                 c->tlen.as<u64>(), c->tsrc.as<u64>(), c->tpairs.as<u32>(), c->stream));
     if ((rc = materialise_column(c, false, ah, c->acol, c->alen, c->aoff, c->asrc, c->apairs, &c->acol_len))) return rc;
     prof_end(c, ST_ARTIST_COLUMN, c->acol_len * 2 + c->nrec * 32);
     // compute_header_length (parallel_spotify.c:444-459): getline's end
@@ -504,8 +508,6 @@ static int do_split(msa_ctx *c, int flags) {
     c->nrec = nterm + (fin.rs < c->n ? 1 : 0);
     const u64 cap = nterm + 2;
     HIPC(c, ensure(c->rec_start, cap * 8));
-    HIPC(c, ensure(c->f0rel, cap * 4));
-    HIPC(c, ensure(c->f3rel, cap * 4));
     HIPC(c, ensure(c->nulrel, cap * 4));
     c->rec_cap = cap;
     if (want_text) HIPC(c, hipMemsetAsync(c->nulrel.p, 0, cap * 4, c->stream));
@@ -827,7 +829,7 @@ void msa_destroy(msa_ctx *c) {
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     DevBuf *all[] = {&c->in_own, &c->sums, &c->carry, &c->btot, &c->bstate, &c->small, &c->rec_start, &c->extra, &c->exp_buf, &c->exp_meta, &c->imp_w, &c->imp_a, &c->imp_meta,
-                     &c->f0rel, &c->f3rel, &c->nulrel, &c->acol, &c->alen, &c->aoff, &c->asrc, &c->apairs, &c->tcol, &c->tlen, &c->toff, &c->tsrc, &c->tpairs,
+                     &c->nulrel, &c->acol, &c->alen, &c->aoff, &c->asrc, &c->apairs, &c->tcol, &c->tlen, &c->toff, &c->tsrc, &c->tpairs,
                      &c->scan_bsum, &c->scan_total, &c->ar_start, &c->arena, &c->key_off,
                      &c->key_len, &c->key_slot, &c->s_tab, &c->s_list, &c->m_tab, &c->m_list, &c->l_pos, &c->l_len,
                      &c->l_slot, &c->l_tab, &c->l_list, &c->a_tab, &c->a_list, &c->ctr};

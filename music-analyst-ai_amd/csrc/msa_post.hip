@@ -244,20 +244,32 @@ __device__ __forceinline__ u32 quote_pairs(u64 q) {
     return pairs;
 }
 
-// First three unquoted commas of every record (parse_csv_line,
-// parallel_spotify.c:258-304).  Record-local: a record always starts outside
-// quotes.  64-byte windows (four dwordx4 loads) with the quote parity carried
-// from window to window; a NUL ends the C string the reference splits, so
-// commas after it do not count.  f0rel = 1 + offset of the first comma,
-// f3rel = 1 + offset just past the third (0: fewer than three -- skipped).
-__global__ __launch_bounds__(256) void k_rec_fields(const u8 *__restrict__ buf, const u64 *__restrict__ rec_start,
-                                                    u64 nrec, u32 *__restrict__ f0rel, u32 *__restrict__ f3rel) {
+// Per record (thread): the first three unquoted commas (parse_csv_line,
+// parallel_spotify.c:258-304), then the spans of both column lines
+// (split_dataset_columns 699-714): line = duplicate_field(field, preserve=1)
+// + '\n'.  After the outer trim a quoted field -- every lyric of the real
+// corpus -- is copied raw; an unquoted one has its "" pairs collapsed and
+// needs no second trim (its first and last bytes are non-space and a
+// collapsed pair yields '"').  Outputs per record: line length (0 = no line:
+// the header, or a record parse_csv_line rejects), source offset, pairs.
+//
+// Commas: record-local (a record starts outside quotes), 64-byte windows
+// (four dwordx4 loads) with the quote parity carried; a NUL ends the C string
+// the reference splits, so commas after it do not count.  The artist field
+// (<= 48 bytes) is trimmed and its pairs counted in the first window.
+__global__ __launch_bounds__(256) void k_rec_spans(const u8 *__restrict__ buf, const u64 *__restrict__ rec_start,
+                                                   const u32 *__restrict__ nulrel, u64 nrec, u64 first_rec,
+                                                   int want_text, u64 *__restrict__ alen, u64 *__restrict__ asrc,
+                                                   u32 *__restrict__ apairs, u64 *__restrict__ tlen,
+                                                   u64 *__restrict__ tsrc, u32 *__restrict__ tpairs) {
     const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= nrec) return;
     const u64 s = rec_start[r], e = rec_start[r + 1];
+    const u64 b0 = s & ~15ull;
+    const Win64 w0 = load_win64(buf, s);
     u32 par = 0, nc = 0, f0 = 0, f3 = 0;
-    for (u64 base = s & ~15ull; base < e; base += 64) {
-        const Win64 w = load_win64(buf, base);
+    for (u64 base = b0; base < e; base += 64) {
+        const Win64 w = base == b0 ? w0 : load_win64(buf, base);
         u64 valid = bits_below((u32)min(e - base, (u64)64));
         if (base < s) valid &= bits_from((u32)(s - base));
         const u64 Q = win_mask<1>(w) & valid, Z = win_mask<4>(w) & valid;
@@ -276,72 +288,58 @@ __global__ __launch_bounds__(256) void k_rec_fields(const u8 *__restrict__ buf, 
             const u32 b = (u32)__ffsll((long long)cu) - 1;
             cu &= cu - 1;
             ++nc;
-            if (nc == 1) f0 = (u32)(base + b - s) + 1u;
-            if (nc == 3) f3 = (u32)(base + b + 1 - s) + 1u;
+            if (nc == 1) f0 = (u32)(base + b - s);
+            if (nc == 3) f3 = (u32)(base + b + 1 - s);
         }
         if (nc >= 3 || Z) break;
     }
-    f0rel[r] = f0;
-    f3rel[r] = nc >= 3 ? f3 : 0u;
-}
-
-// Column lines (split_dataset_columns, parallel_spotify.c:699-714): line r is
-// duplicate_field(field, preserve=1) + '\n'.  After the outer trim a quoted
-// field -- every lyric of the real corpus -- is copied raw; an unquoted one
-// has its "" pairs collapsed, and needs no second trim (its first and last
-// bytes are non-space and a collapsed pair yields '"').  k_col_span records
-// (source, pairs) per record; k_col_write copies one record per wave with
-// coalesced byte lanes (the collapsing copy, rare, runs on one lane).
-template <int TEXT>
-__global__ __launch_bounds__(256) void k_col_span(const u8 *__restrict__ buf, const u64 *__restrict__ rec_start,
-                                                  const u32 *__restrict__ f0rel, const u32 *__restrict__ f3rel,
-                                                  const u32 *__restrict__ nulrel,
-                                                  u64 nrec, u64 first_rec, u64 *__restrict__ line_len,
-                                                  u64 *__restrict__ span_src, u32 *__restrict__ span_pairs) {
-    const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= nrec) return;
-    if (r < first_rec || !f3rel[r]) {  // header, or a record parse_csv_line rejects
-        line_len[r] = 0;
+    if (r < first_rec || nc < 3) {
+        alen[r] = 0;
+        if (want_text) tlen[r] = 0;
         return;
     }
-    const u64 rs = rec_start[r];
-    u64 s, e;
-    if (TEXT) {  // field 3: after the third comma up to the terminator / first NUL
-        s = rs + f3rel[r] - 1;
-        e = rec_start[r + 1];  // incl. the terminator: trimmed as whitespace below
-        if (nulrel[r]) e = min(e, rs + nulrel[r] - 1);
-        if (e < s) e = s;
-    } else {  // field 0: up to the first comma
-        s = rs;
-        e = rs + f0rel[r] - 1;
-    }
-    u32 pairs = 0;
-    if (!TEXT && e - s <= 48) {  // short field (artist): trim and pairs in registers
-        const Win64 w = load_win64(buf, s);
-        const u32 o = (u32)(s & 15);
-        const u64 fm = bits_from(o) & bits_below(o + (u32)(e - s));
-        const u64 nsp = fm & ~win_mask<0>(w);
-        if (!nsp) {
-            e = s;
+    {  // artist: field 0 = [s, s + f0)
+        u64 as = s, ae = s + f0;
+        u32 pairs = 0;
+        if (f0 <= 48) {
+            const u32 o = (u32)(s & 15);
+            const u64 fm = bits_from(o) & bits_below(o + f0);
+            const u64 nsp = fm & ~win_mask<0>(w0);
+            if (!nsp) {
+                ae = as;
+            } else {
+                const u32 a = (u32)__ffsll((long long)nsp) - 1, b = 63u - (u32)__clzll((long long)nsp);
+                const u64 Q = win_mask<1>(w0) & bits_from(a) & bits_below(b + 1);
+                if (!(b > a && ((Q >> a) & 1) && ((Q >> b) & 1))) pairs = quote_pairs(Q);
+                as = b0 + a;
+                ae = b0 + b + 1;
+            }
         } else {
-            const u32 a = (u32)__ffsll((long long)nsp) - 1, b = 63u - (u32)__clzll((long long)nsp);
-            const u64 Q = win_mask<1>(w) & bits_from(a) & bits_below(b + 1);
-            if (!(b > a && ((Q >> a) & 1) && ((Q >> b) & 1))) pairs = quote_pairs(Q);
-            const u64 base = s - o;
-            s = base + a;
-            e = base + b + 1;
+            while (as < ae && c_space(buf[as])) ++as;
+            while (ae > as && c_space(buf[ae - 1])) --ae;
+            if (!(ae > as + 1 && buf[as] == '"' && buf[ae - 1] == '"'))
+                for (u64 i = as; i + 1 < ae; ++i)
+                    if (buf[i] == '"' && buf[i + 1] == '"') { ++pairs; ++i; }
         }
-    } else {
-        while (s < e && c_space(buf[s])) ++s;
-        while (e > s && c_space(buf[e - 1])) --e;
-        if (!(e > s + 1 && buf[s] == '"' && buf[e - 1] == '"')) {
-            for (u64 i = s; i + 1 < e; ++i)
-                if (buf[i] == '"' && buf[i + 1] == '"') { ++pairs; ++i; }
-        }
+        alen[r] = (ae - as) - pairs + 1;
+        asrc[r] = as;
+        apairs[r] = pairs;
     }
-    line_len[r] = (e - s) - pairs + 1;
-    span_src[r] = s;
-    span_pairs[r] = pairs;
+    if (want_text) {  // field 3: after the third comma up to the first NUL; the
+                      // terminator is part of the record and trimmed as whitespace
+        u64 ts = s + f3, te = e;
+        if (nulrel[r]) te = min(te, s + nulrel[r] - 1);
+        if (te < ts) te = ts;
+        while (ts < te && c_space(buf[ts])) ++ts;
+        while (te > ts && c_space(buf[te - 1])) --te;
+        u32 pairs = 0;
+        if (!(te > ts + 1 && buf[ts] == '"' && buf[te - 1] == '"'))
+            for (u64 i = ts; i + 1 < te; ++i)
+                if (buf[i] == '"' && buf[i + 1] == '"') { ++pairs; ++i; }
+        tlen[r] = (te - ts) - pairs + 1;
+        tsrc[r] = ts;
+        tpairs[r] = pairs;
+    }
 }
 
 // Segmented gather.  A workgroup owns 256 consecutive lines (their metadata
@@ -1045,19 +1043,11 @@ __global__ void k_blob_write(const u32 *__restrict__ order, u64 n, const u64 *__
 // host launchers
 static inline dim3 grid1(u64 n, u32 t = 256) { return dim3((u32)((n + t - 1) / t)); }
 
-hipError_t msa_launch_rec_fields(const u8 *buf, const u64 *rs, u64 nrec, u32 *f0, u32 *f3, hipStream_t s) {
-    if (nrec) hipLaunchKernelGGL(k_rec_fields, grid1(nrec), dim3(256), 0, s, buf, rs, nrec, f0, f3);
-    return hipGetLastError();
-}
-hipError_t msa_launch_col_span(int text, const u8 *buf, const u64 *rs, const u32 *f0, const u32 *f3, const u32 *nul,
-                               u64 nrec, u64 first_rec, u64 *len, u64 *src, u32 *pairs, hipStream_t s) {
-    if (!nrec) return hipSuccess;
-    if (text)
-        hipLaunchKernelGGL(k_col_span<1>, grid1(nrec), dim3(256), 0, s, buf, rs, f0, f3, nul, nrec, first_rec, len,
-                           src, pairs);
-    else
-        hipLaunchKernelGGL(k_col_span<0>, grid1(nrec), dim3(256), 0, s, buf, rs, f0, f3, nul, nrec, first_rec, len,
-                           src, pairs);
+hipError_t msa_launch_rec_spans(const u8 *buf, const u64 *rs, const u32 *nul, u64 nrec, u64 first_rec, int text,
+                                u64 *alen, u64 *asrc, u32 *apairs, u64 *tlen, u64 *tsrc, u32 *tpairs, hipStream_t s) {
+    if (nrec)
+        hipLaunchKernelGGL(k_rec_spans, grid1(nrec), dim3(256), 0, s, buf, rs, nul, nrec, first_rec, text, alen, asrc,
+                           apairs, tlen, tsrc, tpairs);
     return hipGetLastError();
 }
 hipError_t msa_launch_col_write(int text, const u8 *buf, const u64 *len, const u64 *off, const u64 *src,
