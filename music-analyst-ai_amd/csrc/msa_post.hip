@@ -231,6 +231,32 @@ __device__ __forceinline__ u64 bytes_hash_words(const uint4 &o0, const uint4 &o1
 }
 __device__ __forceinline__ u64 bits_from(u32 lo) { return lo >= 64 ? 0ull : (~0ull << lo); }
 __device__ __forceinline__ u64 bits_below(u32 hi) { return hi >= 64 ? ~0ull : ((1ull << hi) - 1ull); }
+// 16 bytes at any byte address: dword-aligned loads (4 + 1) and v_alignbyte.
+__device__ __forceinline__ uint4 align16(const uint4 &v, u32 d4, u32 sh) {
+    return make_uint4(__builtin_amdgcn_alignbyte(v.y, v.x, sh), __builtin_amdgcn_alignbyte(v.z, v.y, sh),
+                      __builtin_amdgcn_alignbyte(v.w, v.z, sh), __builtin_amdgcn_alignbyte(d4, v.w, sh));
+}
+__device__ __forceinline__ uint4 load16u(const u8 *__restrict__ buf, u64 s) {
+    const u32 *p = reinterpret_cast<const u32 *>(buf + (s & ~3ull));
+    return align16(make_uint4(p[0], p[1], p[2], p[3]), p[4], (u32)(s & 3));
+}
+// out with its bytes [a, b) (0 <= a <= b <= 16) taken from v
+__device__ __forceinline__ uint4 bytes_blend(const uint4 &out, const uint4 &v, u32 a, u32 b) {
+    const u64 lo = bits_from(8 * a) & bits_below(8 * b);
+    const u64 hi = bits_from(a >= 8 ? 8 * a - 64 : 0) & (b > 8 ? bits_below(8 * b - 64) : 0ull);
+    const u32 m[4] = {(u32)lo, (u32)(lo >> 32), (u32)hi, (u32)(hi >> 32)};
+    return make_uint4(((out.x & ~m[0]) | (v.x & m[0])), (out.y & ~m[1]) | (v.y & m[1]),
+                      (out.z & ~m[2]) | (v.z & m[2]), (out.w & ~m[3]) | (v.w & m[3]));
+}
+__device__ __forceinline__ uint4 byte_put(uint4 o, u32 i, u32 ch) {
+    const u32 s = 8 * (i & 3), m = 0xFFu << s, v = ch << s;
+    if (i < 4) o.x = (o.x & ~m) | v;
+    else if (i < 8) o.y = (o.y & ~m) | v;
+    else if (i < 12) o.z = (o.z & ~m) | v;
+    else o.w = (o.w & ~m) | v;
+    return o;
+}
+
 // greedy "" pairs (duplicate_field's collapse) in a quote mask: sum of floor(run/2)
 __device__ __forceinline__ u32 quote_pairs(u64 q) {
     u32 pairs = 0;
@@ -345,11 +371,12 @@ __global__ __launch_bounds__(256) void k_rec_spans(const u8 *__restrict__ buf, c
 // Segmented gather.  A workgroup owns 256 consecutive lines (their metadata
 // is one coalesced load into LDS) and therefore the contiguous output range
 // [off[r0], off[r0+256]).  Its threads walk the 16-byte slots (aligned in
-// memory) of that range: a slot inside the raw part of one line is gathered
-// with five dword loads + alignbyte and stored whole; a slot that crosses a
-// line end, or the range's ragged first/last slot, is written byte by byte
-// (only the bytes this workgroup owns).  Lines whose "" pairs collapse are
-// left to k_col_collapse (one lane each; rare).  Every byte is written once.
+// memory) of that range: a slot inside one line is five dword loads +
+// v_alignbyte and one 16-byte store; a slot that meets a line end is composed
+// in registers from the lines it meets (byte blends + the '\n').  Only the
+// range's ragged first/last slot is stored byte by byte (only the bytes this
+// workgroup owns).  Lines whose "" pairs collapse get raw bytes here and are
+// rewritten by k_col_collapse, launched after this kernel on the same stream.
 #ifndef CG_T
 #define CG_T 256
 #endif
@@ -363,7 +390,6 @@ __global__ __launch_bounds__(CG_T) void k_col_gather(const u8 *__restrict__ buf,
                                                      const u32 *__restrict__ span_pairs, u64 nrec, u64 hdr, u64 body,
                                                      u8 *__restrict__ col) {
     __shared__ u64 w_off[CG_T + 1], w_src[CG_T];
-    __shared__ u32 w_flag[CG_T];  // bit0: line has pairs to collapse
     __shared__ u32 smap[CG_MAXS];  // slot -> line holding the slot's first byte
     __shared__ u32 tmax[CG_T];
     const u64 r0 = (u64)blockIdx.x * CG_T;
@@ -372,7 +398,6 @@ __global__ __launch_bounds__(CG_T) void k_col_gather(const u8 *__restrict__ buf,
     if (t < wn) {
         w_off[t] = line_off[r0 + t];
         w_src[t] = span_src[r0 + t];
-        w_flag[t] = span_pairs[r0 + t] ? 1u : 0u;
     }
     if (t == 0) w_off[wn] = (r0 + wn < nrec) ? line_off[r0 + wn] : body;
     __syncthreads();
@@ -416,21 +441,22 @@ __global__ __launch_bounds__(CG_T) void k_col_gather(const u8 *__restrict__ buf,
         for (u32 i = a; i < b; ++i) { run = max(run, smap[i]); smap[i] = run; }
         __syncthreads();
     }
-    // slots in batches of CG_B per thread: every fast-path load of the batch is
-    // issued before the first store (memory-level parallelism)
+    // slots in batches of CG_B per thread: every single-line slot's loads of
+    // the batch are issued before the first store (memory-level parallelism)
 #ifndef CG_B
 #define CG_B 4
 #endif
     for (u64 s0 = t; s0 < nslots; s0 += (u64)CG_B * CG_T) {
-        uint4 va[CG_B], vb[CG_B];
-        u32 jj[CG_B], offb[CG_B];
+        uint4 va[CG_B];
+        u32 jj[CG_B], d4[CG_B], sh[CG_B];
         bool fast[CG_B];
 #pragma unroll
         for (int k = 0; k < CG_B; ++k) {
             const u64 si = s0 + (u64)k * CG_T;
             fast[k] = false;
             jj[k] = 0;
-            offb[k] = 0;
+            sh[k] = 0;
+            d4[k] = 0;
             if (si >= nslots) continue;
             const u64 A = S0 + si * CG_SLOT;
             const u64 lo = max(A, O0), hi = min(A + CG_SLOT, O1);
@@ -449,12 +475,12 @@ __global__ __launch_bounds__(CG_T) void k_col_gather(const u8 *__restrict__ buf,
             while (j + 1 < wn && hdr + w_off[j + 1] <= lo) ++j;  // skip empty lines
             jj[k] = j;
             const u64 lstart = hdr + w_off[j], lend = hdr + w_off[j + 1];  // '\n' at lend-1
-            if (lo == A && hi == A + CG_SLOT && A + CG_SLOT < lend && !w_flag[j]) {
+            if (lo == A && hi == A + CG_SLOT && A + CG_SLOT < lend) {
                 const u64 src = w_src[j] + (A - lstart);
-                const uint4 *p = reinterpret_cast<const uint4 *>(buf + (src & ~15ull));
-                va[k] = p[0];
-                vb[k] = p[1];
-                offb[k] = (u32)(src & 15);
+                const u32 *p = reinterpret_cast<const u32 *>(buf + (src & ~3ull));
+                va[k] = make_uint4(p[0], p[1], p[2], p[3]);
+                d4[k] = p[4];
+                sh[k] = (u32)(src & 3);
                 fast[k] = true;
             }
         }
@@ -464,16 +490,39 @@ __global__ __launch_bounds__(CG_T) void k_col_gather(const u8 *__restrict__ buf,
             if (si >= nslots) continue;
             const u64 A = S0 + si * CG_SLOT;
             if (fast[k]) {
-                *reinterpret_cast<uint4 *>(col + A) = funnel16(va[k], vb[k], offb[k]);
+                *reinterpret_cast<uint4 *>(col + A) = align16(va[k], d4[k], sh[k]);
                 continue;
             }
+            // the slot holds a line end: compose it from the (usually two) lines
+            // it meets, in registers
             const u64 lo = max(A, O0), hi = min(A + CG_SLOT, O1);
-            u32 j = jj[k];
-            for (u64 p = lo; p < hi; ++p) {
-                while (p >= hdr + w_off[j + 1]) ++j;
-                if (w_flag[j]) continue;  // k_col_collapse writes this line
+            uint4 out = make_uint4(0, 0, 0, 0);
+            bool ok = true;
+            for (u32 j = jj[k]; j < wn; ++j) {
                 const u64 ls = hdr + w_off[j], le = hdr + w_off[j + 1];
-                col[p] = (p + 1 == le) ? (u8)'\n' : buf[w_src[j] + (p - ls)];
+                if (ls >= hi) break;
+                if (le > ls) {
+                    const u64 a = max(A, ls), b = min(A + CG_SLOT, le - 1);
+                    if (b > a) {
+                        if (w_src[j] + A < ls) { ok = false; break; }  // window would start before the buffer
+                        out = bytes_blend(out, load16u(buf, w_src[j] + A - ls), (u32)(a - A), (u32)(b - A));
+                    }
+                    if (le - 1 >= A && le - 1 < A + CG_SLOT) out = byte_put(out, (u32)(le - 1 - A), '\n');
+                }
+                if (le >= hi) break;
+            }
+            if (ok && lo == A && hi == A + CG_SLOT) {
+                *reinterpret_cast<uint4 *>(col + A) = out;
+            } else if (ok) {  // the workgroup's ragged first / last slot: owned bytes only
+                const u32 d[4] = {out.x, out.y, out.z, out.w};
+                for (u64 p = lo; p < hi; ++p) col[p] = (u8)(d[(p - A) >> 2] >> (8 * ((p - A) & 3)));
+            } else {
+                u32 j = jj[k];
+                for (u64 p = lo; p < hi; ++p) {
+                    while (p >= hdr + w_off[j + 1]) ++j;
+                    const u64 ls = hdr + w_off[j], le = hdr + w_off[j + 1];
+                    col[p] = (p + 1 == le) ? (u8)'\n' : buf[w_src[j] + (p - ls)];
+                }
             }
         }
     }
