@@ -50,7 +50,9 @@ enum {
     MSA_ERR_BADHEADER = -4,  /* "Unable to parse dataset header"           */
     MSA_ERR_CAPACITY = -5,   /* a table or list overflowed its capacity     */
     MSA_ERR_COLLISION = -6,  /* 64-bit key-hash collision detected          */
-    MSA_ERR_IO = -7          /* file write failed                           */
+    MSA_ERR_IO = -7,         /* file write failed                           */
+    MSA_ERR_INPUT = -8       /* input the reference refuses (wcs: invalid   */
+                             /* UTF-8, NUL, field limit, short row)         */
 };
 
 /* ---------------------------------------------------------------- corpus */
@@ -208,6 +210,40 @@ int msa_export_copy(msa_ctx *ctx, void *dst);
 /* Replace the table by the union of the received blocks (counts summed);
  * blk_off[0..nblk] are the blocks' byte offsets in src (last = total).     */
 int msa_import_partitions(msa_ctx *ctx, int table, const void *src, const uint64_t *blk_off, int nblk);
+
+/* ------------------------------------------- per-song word counter (row f)
+ * The GPU path of /root/reference/scripts/word_count_per_song.py:
+ *   msa_wcs_run          csv.DictReader over the "utf-8-sig" file (108-117,
+ *                        delimiter ','), tokenize 28-38, process_row 91-99,
+ *                        the Counter loops of main 124-139, most_common 145
+ *   msa_wcs_get_csv /    the csv.writer outputs word_counts_global.csv and
+ *   msa_wcs_write_outputs word_counts_by_song.csv (128-146)
+ * Inputs the script fails on (invalid UTF-8, NUL, a field over 131072
+ * characters, a row without artist/song/text) return MSA_ERR_INPUT; a header
+ * without the three columns returns MSA_ERR_BADHEADER.                      */
+typedef struct msa_wcs msa_wcs;
+typedef struct {
+    uint64_t total_rows;   /* data rows read ("Processadas N linhas")         */
+    uint64_t song_rows;    /* rows with at least one token                    */
+    uint64_t total_tokens; /* tokens counted                                  */
+    uint64_t n_words;      /* distinct words = word_counts_global.csv lines   */
+    uint64_t n_pairs;      /* word_counts_by_song.csv lines                   */
+} msa_wcs_summary;
+enum { MSA_WCS_GLOBAL = 0, MSA_WCS_BY_SONG = 1 };
+
+int msa_wcs_create(int device, msa_wcs **out);
+void msa_wcs_destroy(msa_wcs *w);
+const char *msa_wcs_last_error(const msa_wcs *w);
+void *msa_wcs_stream(msa_wcs *w);
+int msa_wcs_load_csv(msa_wcs *w, const void *host_csv, size_t n);
+/* log2 of the word-table slots of the next run (0 = sized from the input;
+ * the table grows by itself when it fills). */
+int msa_wcs_set_table_bits(msa_wcs *w, int bits);
+int msa_wcs_run(msa_wcs *w);
+int msa_wcs_get_summary(msa_wcs *w, msa_wcs_summary *out);
+/* One output file's bytes (malloc'ed, release with msa_free). */
+int msa_wcs_get_csv(msa_wcs *w, int which, char **out, size_t *len);
+int msa_wcs_write_outputs(msa_wcs *w, const char *outdir);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,1087 @@
+// msa_wcs.hip -- per-song word counter on gfx950 (DESIGN.md row f): the GPU
+// path of /root/reference/scripts/word_count_per_song.py.
+//
+// What the script does (file:line in word_count_per_song.py):
+//   * reads the CSV with csv.DictReader over open(newline="", "utf-8-sig")
+//     (108-117): Python's _csv state machine, lines split at \n, \r\n, \r
+//   * tokenize (28-38): runs of [0-9A-Za-zÀ-ÖØ-öø-ÿ'], lower-cased, >= 3
+//     characters, not only apostrophes
+//   * process_row (91-99): Counter per song (first-occurrence order), rows
+//     without tokens dropped; artist/song .strip()
+//   * main (124-146): global Counter (first-occurrence order) and
+//     most_common() = stable sort by count descending
+//
+// GPU pipeline (one context, everything resident in HBM):
+//   k_wcs_validate   UTF-8 + NUL check of every byte (the decoder / _csv errors)
+//   k_wcs_map        per 256-byte segment: the reader's transfer function over
+//                    its 6 states (3 bits each) + row ends per entering state
+//   k_wcs_state_*    block scan of the maps (composition) -> entering state of
+//                    every segment -> row-end counts
+//   k_wcs_emit       row ends at their scanned offsets
+//   k_wcs_rows       one thread per row: fields, field limit, tokenizer on the
+//                    unescaped text field, 64-bit word hash into the global
+//                    table (count, first occurrence, h2 checksum), per-row
+//                    table of (word, order, count) in a private scratch region
+//   k_wcs_list / sort / k_wcs_words  global ranking (count desc, first
+//                    occurrence asc -- exactly most_common's stable order),
+//                    word bytes in rank order, collision check
+//   k_wcs_pairs      by-song lines (rank of word, count) in file order
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <string>
+
+#include "msa_hip.h"
+#include "msa_internal.h"
+
+hipError_t msa_exclusive_scan(const u64 *in, u64 n, u64 *out, u64 *bsum_scratch, u64 *total, hipStream_t s);
+hipError_t msa_launch_sort(u64 *const K2[3], u64 *const K1[3], u64 *const K0[3], u32 *const V[3], u64 n, int *which,
+                           hipStream_t s);
+
+namespace {
+
+// Reader states of CPython's _csv.c (3.10) for the dialect the script uses.
+enum : u32 { SR = 0, SF = 1, IF = 2, IQ = 3, QQ = 4, EC = 5 };
+#define PK(a, b, c, d, e, f) ((a) | ((b) << 3) | ((c) << 6) | ((d) << 9) | ((e) << 12) | ((f) << 15))
+// next state for input state SR SF IF IQ QQ EC
+constexpr u32 T_Q = PK(IQ, IQ, IF, QQ, IQ, EC);    // '"'
+constexpr u32 T_D = PK(SF, SF, SF, IQ, SF, EC);    // ','
+constexpr u32 T_NL = PK(EC, EC, EC, IQ, EC, EC);   // '\r' or '\n'
+constexpr u32 T_O = PK(IF, IF, IF, IQ, IF, EC);    // anything else
+constexpr u32 T_EOL = PK(SR, SR, SR, IQ, SR, SR);  // end of a line
+constexpr u32 MAP_ID = PK(0, 1, 2, 3, 4, 5);
+#undef PK
+
+constexpr u32 SEG = 256;        // bytes per lane in the map / emit passes
+constexpr u32 BLK = 256;        // threads per block in the state scan
+constexpr u32 PER = 4;          // segments per thread in the state scan
+constexpr u32 BSEG = BLK * PER; // segments per block
+constexpr u32 FIELD_LIMIT = 131072;
+
+enum : u32 { E_UTF8 = 1, E_NUL = 2, E_LIMIT = 3, E_SHORT = 4 };
+enum : u32 { OVF_G = 1 };
+
+struct WCtr {
+    u64 err;        // min over (row << 8 | code), ~0 = none
+    u64 total_rows; // non-blank data rows
+    u64 song_rows;  // rows with >= 1 token
+    u64 tokens;
+    u64 distinct;   // claimed global slots
+    u64 overflow;
+    u64 collision;
+    u64 listed;
+};
+
+__host__ __device__ __forceinline__ u32 tpk(u32 b) {
+    return b == '"' ? T_Q : (b == ',' ? T_D : ((b == '\r' || b == '\n') ? T_NL : T_O));
+}
+__host__ __device__ __forceinline__ u32 step(u32 t, u32 s) { return (t >> (3 * s)) & 7u; }
+__device__ __forceinline__ u32 map_apply(u32 t, u32 m) {  // m then t
+    u32 r = 0;
+#pragma unroll
+    for (u32 k = 0; k < 6; ++k) r |= step(t, (m >> (3 * k)) & 7u) << (3 * k);
+    return r;
+}
+__device__ __forceinline__ u32 compose(u32 f, u32 g) { return map_apply(g, f); }  // f then g
+
+__device__ __forceinline__ u32 byte_of(const uint4 &v, u32 j) {
+    const u32 w = j < 8 ? (j < 4 ? v.x : v.y) : (j < 12 ? v.z : v.w);
+    return (w >> (8 * (j & 3))) & 0xFFu;
+}
+
+// ---------------------------------------------------------------------------
+// UTF-8 (strict, as Python's decoder) and NUL check.
+__device__ __forceinline__ u32 lead_len(u32 b) {
+    return b < 0x80 ? 1 : (b < 0xC2 ? 0 : (b < 0xE0 ? 2 : (b < 0xF0 ? 3 : (b < 0xF5 ? 4 : 0))));
+}
+
+__global__ __launch_bounds__(256) void k_wcs_validate(const u8 *__restrict__ buf, u64 n, WCtr *ctr) {
+    const u64 base = ((u64)blockIdx.x * blockDim.x + threadIdx.x) * 16;
+    if (base >= n) return;
+    const uint4 v = *(const uint4 *)(buf + base);
+    u32 bad = 0;
+    for (u32 j = 0; j < 16; ++j) {
+        const u64 i = base + j;
+        if (i >= n) break;
+        const u32 b = byte_of(v, j);
+        if (b == 0) { bad = bad ? bad : E_NUL; continue; }
+        if (b < 0x80) continue;
+        if (b < 0xC0) {  // continuation: must be covered by a lead at most 3 back
+            u32 k = 1;
+            bool ok = false;
+            for (; k <= 3 && i >= k; ++k) {
+                const u32 c = buf[i - k];
+                if ((c & 0xC0) != 0x80) { ok = lead_len(c) > k; break; }
+            }
+            if (!ok) bad = E_UTF8;
+            continue;
+        }
+        const u32 L = lead_len(b);
+        if (L == 0 || i + L > n) { bad = E_UTF8; continue; }
+        const u32 c1 = buf[i + 1];
+        u32 lo = 0x80, hi = 0xBF;
+        if (b == 0xE0) lo = 0xA0;
+        else if (b == 0xED) hi = 0x9F;
+        else if (b == 0xF0) lo = 0x90;
+        else if (b == 0xF4) hi = 0x8F;
+        if (c1 < lo || c1 > hi) { bad = E_UTF8; continue; }
+        for (u32 k = 2; k < L; ++k)
+            if ((buf[i + k] & 0xC0) != 0x80) bad = E_UTF8;
+    }
+    if (bad) atomicMin((unsigned long long *)&ctr->err, (unsigned long long)bad);  // row 0: before any row
+}
+
+// ---------------------------------------------------------------------------
+// Row splitting.  An end of line follows byte i when it is '\n', a '\r' not
+// followed by '\n', or the last byte (the final line has no terminator).  A
+// row ends at an end of line that takes the reader to SR.
+__device__ __forceinline__ bool eol_after(u32 b, u32 next, u64 i, u64 n) {
+    return b == '\n' || (b == '\r' && (i + 1 >= n || next != '\n')) || i + 1 == n;
+}
+
+// Per segment: map over the 6 entering states; row ends per entering state
+// (9 bits each: at most 256 per segment).
+__global__ __launch_bounds__(256) void k_wcs_map(const u8 *__restrict__ buf, u64 ds, u64 n, u64 nseg,
+                                                 u32 *__restrict__ map, u64 *__restrict__ cnt6) {
+    const u64 seg = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (seg >= nseg) return;
+    const u64 base = seg * SEG;
+    u32 m = MAP_ID;
+    u64 c6 = 0;
+    for (u32 q = 0; q < SEG / 16; ++q) {
+        const u64 b0 = base + q * 16;
+        if (b0 >= n) break;
+        const uint4 v = *(const uint4 *)(buf + b0);
+        for (u32 j = 0; j < 16; ++j) {
+            const u64 i = b0 + j;
+            if (i < ds) continue;
+            if (i >= n) break;
+            const u32 b = byte_of(v, j);
+            m = map_apply(tpk(b), m);
+            const u32 nx = j < 15 ? byte_of(v, j + 1) : buf[i + 1];
+            if (eol_after(b, nx, i, n)) {
+#pragma unroll
+                for (u32 k = 0; k < 6; ++k) {
+                    const u32 s = (m >> (3 * k)) & 7u;
+                    if (s != SR && s != IQ) c6 += 1ull << (9 * k);
+                }
+                m = map_apply(T_EOL, m);
+            }
+        }
+    }
+    map[seg] = m;
+    cnt6[seg] = c6;
+}
+
+// Inclusive scan of the 256 thread composites of a block (Hillis-Steele in LDS).
+__device__ u32 block_map_scan(u32 x, u32 *sh) {
+    const u32 t = threadIdx.x;
+    sh[t] = x;
+    __syncthreads();
+    for (u32 o = 1; o < BLK; o <<= 1) {
+        const u32 y = t >= o ? sh[t - o] : MAP_ID;
+        __syncthreads();
+        x = compose(y, x);
+        sh[t] = x;
+        __syncthreads();
+    }
+    return x;
+}
+
+__global__ __launch_bounds__(BLK) void k_wcs_state_block(const u32 *__restrict__ map, u64 nseg,
+                                                         u32 *__restrict__ bmap) {
+    __shared__ u32 sh[BLK];
+    const u64 s0 = (u64)blockIdx.x * BSEG + (u64)threadIdx.x * PER;
+    u32 x = MAP_ID;
+    for (u32 k = 0; k < PER; ++k)
+        if (s0 + k < nseg) x = compose(x, map[s0 + k]);
+    x = block_map_scan(x, sh);
+    if (threadIdx.x == BLK - 1) bmap[blockIdx.x] = x;
+}
+
+// One thread: entering state of every block (nb is small: nseg / 1024).
+__global__ void k_wcs_state_top(u32 *__restrict__ bmap, u64 nb, u32 *__restrict__ final_state) {
+    u32 s = SR;
+    for (u64 b = 0; b < nb; ++b) {
+        const u32 m = bmap[b];
+        bmap[b] = s;
+        s = step(m, s);
+    }
+    *final_state = s;
+}
+
+__global__ __launch_bounds__(BLK) void k_wcs_state_down(const u32 *__restrict__ map, const u64 *__restrict__ cnt6,
+                                                        u64 nseg, const u32 *__restrict__ bstate,
+                                                        u32 *__restrict__ sstate, u64 *__restrict__ cnt) {
+    __shared__ u32 sh[BLK];
+    const u64 s0 = (u64)blockIdx.x * BSEG + (u64)threadIdx.x * PER;
+    u32 x = MAP_ID;
+    for (u32 k = 0; k < PER; ++k)
+        if (s0 + k < nseg) x = compose(x, map[s0 + k]);
+    const u32 inc = block_map_scan(x, sh);
+    const u32 excl = threadIdx.x ? sh[threadIdx.x - 1] : MAP_ID;
+    (void)inc;
+    u32 s = step(excl, bstate[blockIdx.x]);
+    for (u32 k = 0; k < PER; ++k) {
+        const u64 g = s0 + k;
+        if (g >= nseg) break;
+        sstate[g] = s;
+        cnt[g] = (cnt6[g] >> (9 * s)) & 511u;
+        s = step(map[g], s);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_wcs_emit(const u8 *__restrict__ buf, u64 ds, u64 n, u64 nseg,
+                                                  const u32 *__restrict__ sstate, const u64 *__restrict__ roff,
+                                                  u64 *__restrict__ rend) {
+    const u64 seg = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (seg >= nseg) return;
+    const u64 base = seg * SEG;
+    u32 s = sstate[seg];
+    u64 o = roff[seg];
+    for (u32 q = 0; q < SEG / 16; ++q) {
+        const u64 b0 = base + q * 16;
+        if (b0 >= n) break;
+        const uint4 v = *(const uint4 *)(buf + b0);
+        for (u32 j = 0; j < 16; ++j) {
+            const u64 i = b0 + j;
+            if (i < ds) continue;
+            if (i >= n) break;
+            const u32 b = byte_of(v, j);
+            s = step(tpk(b), s);
+            const u32 nx = j < 15 ? byte_of(v, j + 1) : buf[i + 1];
+            if (eol_after(b, nx, i, n)) {
+                if (s != SR && s != IQ) rend[o++] = i + 1;
+                s = step(T_EOL, s);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Per-row pass.
+struct ByteReader {
+    const u32 *w;
+    u64 wi;
+    u32 cur;
+    __device__ ByteReader(const u8 *buf) : w((const u32 *)buf), wi(~0ull), cur(0) {}
+    __device__ __forceinline__ u32 get(u64 i) {
+        const u64 k = i >> 2;
+        if (k != wi) { wi = k; cur = w[k]; }
+        return (cur >> (8 * (i & 3))) & 0xFFu;
+    }
+};
+
+__host__ __device__ __forceinline__ bool tok_ascii(u32 c) {
+    return (c >= '0' && c <= '9') || ((c | 0x20u) >= 'a' && (c | 0x20u) <= 'z') || c == '\'';
+}
+// second byte d of a 0xC3 pair: U+00C0..U+00FF minus U+00D7 / U+00F7
+__host__ __device__ __forceinline__ bool tok_c3(u32 d) { return d >= 0x80 && d <= 0xBF && d != 0x97 && d != 0xB7; }
+__host__ __device__ __forceinline__ u32 low_ascii(u32 c) { return (c >= 'A' && c <= 'Z') ? c + 32 : c; }
+__host__ __device__ __forceinline__ u32 low_c3(u32 d) { return d <= 0x9E ? d + 32 : d; }
+
+constexpr u64 H1_P = 0x100000001b3ull, H1_0 = 0xcbf29ce484222325ull;
+constexpr u64 H2_P = 0x9E3779B97F4A7C15ull, H2_0 = 0x2545F4914F6CDD1Dull;
+__host__ __device__ __forceinline__ u64 h1_step(u64 h, u32 b) { return (h ^ b) * H1_P; }
+__host__ __device__ __forceinline__ u64 h2_step(u64 h, u32 b) { return (h + b + 0x100u) * H2_P ^ (h >> 29); }
+__host__ __device__ __forceinline__ u64 h1_fin(u64 h, u64 len) {
+    const u64 k = fmix64(h ^ (len * 0xD6E8FEB86659FD93ull));
+    return k ? k : 1;
+}
+__host__ __device__ __forceinline__ u64 h2_fin(u64 h, u64 len) { return fmix64(h + len); }
+
+struct RowArgs {
+    const u8 *buf;
+    u64 n;
+    const u64 *rend;
+    u64 ds;
+    u64 nrows;
+    u32 ia, isg, it, need;
+    u64 *gtab;      // 4 u64 per slot: key, h2 sum, ~first (pos << 20 | raw len), count
+    u64 gmask;
+    u64 glimit;
+    u64 *scratch;   // per-row tables, row r at scratch + row start
+    u64 *nd;        // distinct words per row
+    u64 *spans;     // 4 per row: artist start/end, song start/end (raw)
+    WCtr *ctr;
+};
+
+__device__ __forceinline__ u64 g_insert(const RowArgs &a, u64 key) {
+    u64 slot = key & a.gmask;
+    for (u64 p = 0; p <= a.gmask; ++p) {
+        u64 *k = a.gtab + slot * 4;
+        const u64 cur = __atomic_load_n(k, __ATOMIC_RELAXED);
+        if (cur == key) return slot;
+        if (cur == 0) {
+            const u64 old = atomicCAS((unsigned long long *)k, 0ull, (unsigned long long)key);
+            if (old == 0) {
+                const u64 d = atomicAdd((unsigned long long *)&a.ctr->distinct, 1ull);
+                if (d >= a.glimit) atomicOr((unsigned long long *)&a.ctr->overflow, (unsigned long long)OVF_G);
+                return slot;
+            }
+            if (old == key) return slot;
+        }
+        slot = (slot + 1) & a.gmask;
+    }
+    atomicOr((unsigned long long *)&a.ctr->overflow, (unsigned long long)OVF_G);
+    return ~0ull;
+}
+
+__device__ __forceinline__ void wcs_err(WCtr *ctr, u64 row, u32 code) {
+    atomicMin((unsigned long long *)&ctr->err, (unsigned long long)((row << 8) | code));
+}
+
+__global__ __launch_bounds__(256) void k_wcs_rows(RowArgs a) {
+    // row k of the file spans [rend[k], rend[k+1]); kernel index r = k + 1,
+    // r = 1 is the header row
+    const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x + 2;
+    if (r >= a.nrows) return;
+    const u64 rs = a.rend[r - 1], re = a.rend[r];
+    ByteReader rd(a.buf);
+    u32 s = SR, f = 0, chars = 0;
+    bool any = false;  // a field was saved (blank rows have none)
+    u64 fstart = rs;
+    u64 sp[4] = {0, 0, 0, 0};
+    // tokenizer over the added characters of field `it`
+    bool in_tok = false, alnum = false, skip = false;
+    u32 cps = 0;
+    u64 h1 = H1_0, h2 = H2_0, tlen = 0, tstart = 0;
+    u64 *rt = a.scratch + rs;
+    const u32 rcap = (u32)((re - rs) / 2 + 2);
+    u32 nd = 0, ntok = 0;
+    bool limit = false;
+
+    auto tok_end = [&](u64 end) {
+        if (in_tok && cps >= 3 && alnum) {
+            const u64 key = h1_fin(h1, tlen);
+            const u64 slot = g_insert(a, key);
+            if (slot != ~0ull) {
+                u64 *g = a.gtab + slot * 4;
+                atomicAdd((unsigned long long *)(g + 1), (unsigned long long)h2_fin(h2, tlen));
+                atomicMax((unsigned long long *)(g + 2), (unsigned long long)~((tstart << 20) | (end - tstart)));
+                atomicAdd((unsigned long long *)(g + 3), 1ull);
+                if (ntok == 0)
+                    for (u32 k = 0; k < rcap; ++k) rt[k] = 0;
+                ++ntok;
+                const u64 id = slot + 1;
+                u32 h = (u32)(((id * 0x9E3779B97F4A7C15ull) >> 32) % rcap);
+                for (;;) {
+                    const u64 v = rt[h];
+                    if (v == 0) { rt[h] = (id << 32) | ((u64)nd << 16) | 1u; ++nd; break; }
+                    if ((v >> 32) == id) { rt[h] = v + 1; break; }
+                    h = h + 1 == rcap ? 0 : h + 1;
+                }
+            }
+        }
+        in_tok = false;
+    };
+    auto save = [&](u64 end) {
+        if (f == a.it) tok_end(end);
+        if (f == a.ia) { sp[0] = fstart; sp[1] = end; }
+        if (f == a.isg) { sp[2] = fstart; sp[3] = end; }
+        ++f;
+        chars = 0;
+        any = true;
+    };
+    auto add = [&](u64 i, u32 b) {
+        if ((b & 0xC0) != 0x80 && ++chars > FIELD_LIMIT) limit = true;
+        if (f != a.it) return;
+        if (skip) { skip = false; return; }
+        u32 lo0 = 0, lo1 = 0, nb = 0;
+        if (b < 0x80 && tok_ascii(b)) { lo0 = low_ascii(b); nb = 1; }
+        else if (b == 0xC3) {
+            const u32 d = rd.get(i + 1);
+            if (tok_c3(d)) { lo0 = 0xC3; lo1 = low_c3(d); nb = 2; skip = true; }
+        }
+        if (!nb) { tok_end(i); return; }
+        if (!in_tok) { in_tok = true; alnum = false; cps = 0; h1 = H1_0; h2 = H2_0; tlen = 0; tstart = i; }
+        h1 = h1_step(h1, lo0); h2 = h2_step(h2, lo0); ++tlen;
+        if (nb == 2) { h1 = h1_step(h1, lo1); h2 = h2_step(h2, lo1); ++tlen; }
+        alnum |= b != '\'';
+        ++cps;
+    };
+
+    for (u64 i = rs; i < re; ++i) {
+        const u32 b = rd.get(i);
+        const bool eol = eol_after(b, i + 1 < a.n ? rd.get(i + 1) : 0u, i, a.n);
+        switch (s) {
+            case SR:
+                if (b == '\r' || b == '\n') { s = EC; break; }
+                s = SF;
+                fstart = i;
+                [[fallthrough]];
+            case SF:
+                if (b == '\r' || b == '\n') { save(i); s = EC; }
+                else if (b == '"') s = IQ;
+                else if (b == ',') { save(i); fstart = i + 1; }
+                else { add(i, b); s = IF; }
+                break;
+            case IF:
+                if (b == '\r' || b == '\n') { save(i); s = EC; }
+                else if (b == ',') { save(i); fstart = i + 1; s = SF; }
+                else add(i, b);
+                break;
+            case IQ:
+                if (b == '"') s = QQ;
+                else add(i, b);
+                break;
+            case QQ:
+                if (b == '"') { add(i, b); s = IQ; }
+                else if (b == ',') { save(i); fstart = i + 1; s = SF; }
+                else if (b == '\r' || b == '\n') { save(i); s = EC; }
+                else { add(i, b); s = IF; }
+                break;
+            default:
+                break;  // EC
+        }
+        if (eol) {
+            if (s == SF || s == IF || s == QQ) save(i + 1);
+            if (s != IQ) s = SR;
+        }
+    }
+    if (s == IQ) save(re);  // input ended inside a quoted field
+    if (limit) wcs_err(a.ctr, r, E_LIMIT);
+    if (!any) { a.nd[r] = 0; return; }  // blank line: DictReader skips it
+    atomicAdd((unsigned long long *)&a.ctr->total_rows, 1ull);
+    if (f <= a.need) wcs_err(a.ctr, r, E_SHORT);
+    a.nd[r] = nd;
+    if (nd) {
+        atomicAdd((unsigned long long *)&a.ctr->song_rows, 1ull);
+        atomicAdd((unsigned long long *)&a.ctr->tokens, (unsigned long long)ntok);
+    }
+    u64 *o = a.spans + r * 4;
+    o[0] = sp[0]; o[1] = sp[1]; o[2] = sp[2]; o[3] = sp[3];
+}
+
+// ---------------------------------------------------------------------------
+// Global ranking: most_common() = stable sort by count desc over the
+// first-occurrence order, i.e. the key (count desc, first position asc).
+__global__ __launch_bounds__(256) void k_wcs_list(const u64 *__restrict__ gtab, u64 nslots, WCtr *ctr,
+                                                  u64 *__restrict__ K2, u64 *__restrict__ K1, u64 *__restrict__ K0,
+                                                  u32 *__restrict__ V) {
+    const u64 slot = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (slot >= nslots) return;
+    const u64 *g = gtab + slot * 4;
+    if (g[0] == 0) return;
+    const u64 idx = atomicAdd((unsigned long long *)&ctr->listed, 1ull);
+    K2[idx] = 0xFFFFFFFFull - g[3];
+    K1[idx] = (~g[2]) >> 20;
+    K0[idx] = 0;
+    V[idx] = (u32)slot;
+}
+
+// Word bytes of rank i: the first occurrence's raw span without its (at most
+// one, structural) '"', lower-cased; re-hashed to check the slot's key and h2 sum.
+__global__ __launch_bounds__(256) void k_wcs_wordlen(const u8 *__restrict__ buf, const u64 *__restrict__ gtab,
+                                                     const u32 *__restrict__ order, u64 nw, u32 *__restrict__ rank_of,
+                                                     u64 *__restrict__ len, u32 *__restrict__ counts, WCtr *ctr) {
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nw) return;
+    const u32 slot = order[i];
+    const u64 *g = gtab + (u64)slot * 4;
+    const u64 fe = ~g[2];
+    const u64 pos = fe >> 20, raw = fe & ((1u << 20) - 1);
+    u64 h1 = H1_0, h2 = H2_0, l = 0;
+    for (u64 k = 0; k < raw; ++k) {
+        const u32 b = buf[pos + k];
+        if (b == '"') continue;
+        u32 c;
+        if (b == 0xC3) c = 0xC3;
+        else if (k > 0 && buf[pos + k - 1] == 0xC3) c = low_c3(b);
+        else c = low_ascii(b);
+        h1 = h1_step(h1, c);
+        h2 = h2_step(h2, c);
+        ++l;
+    }
+    const u64 cnt = g[3];
+    if (h1_fin(h1, l) != g[0] || h2_fin(h2, l) * cnt != g[1])
+        atomicAdd((unsigned long long *)&ctr->collision, 1ull);
+    rank_of[slot] = (u32)i;
+    len[i] = l;
+    counts[i] = (u32)cnt;
+}
+
+__global__ __launch_bounds__(256) void k_wcs_wordblob(const u8 *__restrict__ buf, const u64 *__restrict__ gtab,
+                                                      const u32 *__restrict__ order, u64 nw,
+                                                      const u64 *__restrict__ off, u8 *__restrict__ blob,
+                                                      WCtr *ctr) {
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nw) return;
+    const u64 fe = ~gtab[(u64)order[i] * 4 + 2];
+    const u64 pos = fe >> 20, raw = fe & ((1u << 20) - 1);
+    const u64 o0 = off[i];
+    u64 j = o0;
+    u32 prev = 0;
+    for (u64 k = 0; k < raw; ++k) {
+        const u32 b = buf[pos + k];
+        const u32 c = b == 0xC3 ? b : (prev == 0xC3 ? low_c3(b) : low_ascii(b));
+        prev = b;
+        if (b != '"') blob[j++] = (u8)c;
+    }
+    if (j != off[i + 1]) atomicAdd((unsigned long long *)&ctr->collision, 1ull);
+}
+
+// by-song lines of row r at poff[r] + order: (rank << 32) | count
+__global__ __launch_bounds__(256) void k_wcs_pairs(const u64 *__restrict__ rend, u64 nrows,
+                                                   const u64 *__restrict__ nd, const u64 *__restrict__ poff,
+                                                   const u64 *__restrict__ scratch, const u32 *__restrict__ rank_of,
+                                                   u64 *__restrict__ pairs) {
+    const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x + 2;
+    if (r >= nrows || nd[r] == 0) return;
+    const u64 rs = rend[r - 1], re = rend[r];
+    const u32 rcap = (u32)((re - rs) / 2 + 2);
+    const u64 *rt = scratch + rs;
+    u64 *o = pairs + poff[r];
+    for (u32 k = 0; k < rcap; ++k) {
+        const u64 v = rt[k];
+        if (!v) continue;
+        const u64 id = v >> 32;
+        o[(v >> 16) & 0xFFFFu] = ((u64)rank_of[id - 1] << 32) | (v & 0xFFFFu);
+    }
+}
+
+inline dim3 grid1(u64 n, u32 t = 256) { return dim3((u32)((n + t - 1) / t)); }
+
+}  // namespace
+
+// ===========================================================================
+// Host side.
+struct msa_wcs {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    char err[512] = {0};
+    // input
+    u8 *d_buf = nullptr;
+    u64 n = 0, cap = 0;
+    // rows
+    u64 nrows = 0;  // incl. header
+    u64 *d_rend = nullptr;
+    u64 rend_cap = 0;
+    // results (device)
+    u64 nw = 0, np = 0, blob_len = 0;
+    u32 *d_counts = nullptr;
+    u64 *d_woff = nullptr;
+    u8 *d_blob = nullptr;
+    u64 *d_pairs = nullptr;
+    u64 *d_nd = nullptr;
+    u64 *d_spans = nullptr;
+    msa_wcs_summary sum{};
+    u64 gbits = 0;  // global table size of the next run (log2), 0 = auto
+    bool have = false;
+    // scratch owned by the run
+    void *scr[24] = {nullptr};
+};
+
+static int wfail(msa_wcs *w, int code, const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(w->err, sizeof w->err, fmt, ap);
+    va_end(ap);
+    return code;
+}
+#define WCHECK(x)                                                                                           \
+    do {                                                                                                    \
+        hipError_t e_ = (x);                                                                                \
+        if (e_ != hipSuccess) return wfail(w, MSA_ERR_HIP, "%s: %s (%s:%d)", #x, hipGetErrorString(e_), __FILE__, \
+                                           __LINE__);                                                       \
+    } while (0)
+
+static void wfree(void *&p) {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+}
+template <typename T>
+static hipError_t walloc(T *&p, u64 bytes) {
+    void *q = nullptr;
+    hipError_t e = hipMalloc(&q, bytes ? bytes : 16);
+    p = (T *)q;
+    return e;
+}
+
+static void wcs_release_results(msa_wcs *w) {
+    void **ps[] = {(void **)&w->d_counts, (void **)&w->d_woff, (void **)&w->d_blob, (void **)&w->d_pairs,
+                   (void **)&w->d_nd, (void **)&w->d_spans};
+    for (void **p : ps) wfree(*p);
+    for (auto &p : w->scr) wfree(p);
+    w->have = false;
+}
+
+extern "C" int msa_wcs_create(int device, msa_wcs **out) {
+    if (!out) return MSA_ERR_ARG;
+    *out = nullptr;
+    int nd = 0;
+    if (hipGetDeviceCount(&nd) != hipSuccess || nd <= device || device < 0) return MSA_ERR_HIP;
+    if (hipSetDevice(device) != hipSuccess) return MSA_ERR_HIP;
+    msa_wcs *w = new msa_wcs();
+    w->device = device;
+    if (hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete w;
+        return MSA_ERR_HIP;
+    }
+    *out = w;
+    return MSA_OK;
+}
+
+extern "C" void msa_wcs_destroy(msa_wcs *w) {
+    if (!w) return;
+    (void)hipSetDevice(w->device);
+    (void)hipStreamSynchronize(w->stream);
+    wcs_release_results(w);
+    wfree((void *&)w->d_buf);
+    wfree((void *&)w->d_rend);
+    (void)hipStreamDestroy(w->stream);
+    delete w;
+}
+
+extern "C" const char *msa_wcs_last_error(const msa_wcs *w) { return w ? w->err : "null context"; }
+extern "C" void *msa_wcs_stream(msa_wcs *w) { return w ? (void *)w->stream : nullptr; }
+
+extern "C" int msa_wcs_load_csv(msa_wcs *w, const void *host_csv, size_t n) {
+    if (!w || (!host_csv && n)) return MSA_ERR_ARG;
+    WCHECK(hipSetDevice(w->device));
+    if (n + MSA_INPUT_PAD > w->cap) {
+        wfree((void *&)w->d_buf);
+        w->cap = n + MSA_INPUT_PAD;
+        WCHECK(walloc(w->d_buf, w->cap));
+    }
+    WCHECK(hipMemsetAsync(w->d_buf + n, 0, MSA_INPUT_PAD, w->stream));
+    if (n) WCHECK(hipMemcpyAsync(w->d_buf, host_csv, n, hipMemcpyHostToDevice, w->stream));
+    WCHECK(hipStreamSynchronize(w->stream));
+    w->n = n;
+    w->have = false;
+    return MSA_OK;
+}
+
+extern "C" int msa_wcs_set_table_bits(msa_wcs *w, int bits) {
+    if (!w || bits < 0 || bits > 31) return MSA_ERR_ARG;
+    w->gbits = (u64)bits;
+    return MSA_OK;
+}
+
+// Header row -> column indices ("dict(zip(fieldnames, row))": the last
+// duplicate name wins).  Host restatement of the same reader for one row.
+static int parse_header(msa_wcs *w, const u8 *h, u64 len, u32 *ia, u32 *isg, u32 *it) {
+    long long col[3] = {-1, -1, -1};
+    static const char *names[3] = {"artist", "song", "text"};
+    char *fld = (char *)malloc(len + 1);
+    u64 fl = 0;
+    u32 f = 0, s = SR;
+    bool any = false;
+    auto save = [&]() {
+        for (int k = 0; k < 3; ++k)
+            if (fl == strlen(names[k]) && memcmp(fld, names[k], fl) == 0) col[k] = f;
+        ++f;
+        fl = 0;
+        any = true;
+    };
+    for (u64 i = 0; i < len; ++i) {
+        const u32 b = h[i];
+        const bool eol = b == '\n' || (b == '\r' && (i + 1 >= len || h[i + 1] != '\n')) || i + 1 == len;
+        switch (s) {
+            case SR:
+                if (b == '\r' || b == '\n') { s = EC; break; }
+                s = SF;
+                [[fallthrough]];
+            case SF:
+                if (b == '\r' || b == '\n') { save(); s = EC; }
+                else if (b == '"') s = IQ;
+                else if (b == ',') save();
+                else { fld[fl++] = (char)b; s = IF; }
+                break;
+            case IF:
+                if (b == '\r' || b == '\n') { save(); s = EC; }
+                else if (b == ',') { save(); s = SF; }
+                else fld[fl++] = (char)b;
+                break;
+            case IQ:
+                if (b == '"') s = QQ;
+                else fld[fl++] = (char)b;
+                break;
+            case QQ:
+                if (b == '"') { fld[fl++] = '"'; s = IQ; }
+                else if (b == ',') { save(); s = SF; }
+                else if (b == '\r' || b == '\n') { save(); s = EC; }
+                else { fld[fl++] = (char)b; s = IF; }
+                break;
+            default:
+                break;
+        }
+        if (eol) {
+            if (s == SF || s == IF || s == QQ) save();
+            if (s != IQ) s = SR;
+        }
+    }
+    if (s == IQ) save();
+    free(fld);
+    (void)any;
+    if (col[0] < 0 || col[1] < 0 || col[2] < 0)
+        return wfail(w, MSA_ERR_BADHEADER, "CSV sem colunas esperadas. Campos necessários: artist, song, text.");
+    *ia = (u32)col[0];
+    *isg = (u32)col[1];
+    *it = (u32)col[2];
+    return MSA_OK;
+}
+
+static int wcs_input_error(msa_wcs *w, u64 e) {
+    const u32 code = (u32)(e & 0xFF);
+    const u64 row = e >> 8;
+    switch (code) {
+        case E_UTF8: return wfail(w, MSA_ERR_INPUT, "invalid UTF-8 in the input");
+        case E_NUL: return wfail(w, MSA_ERR_INPUT, "line contains NUL");
+        case E_LIMIT: return wfail(w, MSA_ERR_INPUT, "field larger than field limit (131072) (row %llu)",
+                                   (unsigned long long)row);
+        default: return wfail(w, MSA_ERR_INPUT, "row %llu has no artist/song/text value", (unsigned long long)row);
+    }
+}
+
+extern "C" int msa_wcs_run(msa_wcs *w) {
+    if (!w || !w->d_buf) return MSA_ERR_ARG;
+    WCHECK(hipSetDevice(w->device));
+    wcs_release_results(w);
+    hipStream_t st = w->stream;
+    const u8 *buf = w->d_buf;
+    const u64 n = w->n;
+    WCtr *ctr;
+    WCHECK(walloc(ctr, sizeof(WCtr)));
+    w->scr[0] = ctr;
+    WCtr h0{};
+    h0.err = ~0ull;
+    WCHECK(hipMemcpyAsync(ctr, &h0, sizeof h0, hipMemcpyHostToDevice, st));
+    if (n) hipLaunchKernelGGL(k_wcs_validate, grid1((n + 15) / 16), dim3(256), 0, st, buf, n, ctr);
+    // BOM ("utf-8-sig")
+    u8 bom[3] = {0, 0, 0};
+    if (n >= 3) WCHECK(hipMemcpyAsync(bom, buf, 3, hipMemcpyDeviceToHost, st));
+    WCHECK(hipStreamSynchronize(st));
+    const u64 ds = (n >= 3 && bom[0] == 0xEF && bom[1] == 0xBB && bom[2] == 0xBF) ? 3 : 0;
+
+    // ---- rows
+    const u64 nseg = (n + SEG - 1) / SEG;
+    u64 nrows = 0;
+    u32 fin = SR;
+    if (nseg) {
+        const u64 nb = (nseg + BSEG - 1) / BSEG;
+        u32 *map, *bmap, *sstate, *dfin;
+        u64 *cnt6, *cnt, *roff, *bsum, *total;
+        WCHECK(walloc(map, nseg * 4)); w->scr[1] = map;
+        WCHECK(walloc(cnt6, nseg * 8)); w->scr[2] = cnt6;
+        WCHECK(walloc(cnt, nseg * 8)); w->scr[3] = cnt;
+        WCHECK(walloc(roff, nseg * 8)); w->scr[4] = roff;
+        WCHECK(walloc(bmap, nb * 4 + 16)); w->scr[5] = bmap;
+        WCHECK(walloc(sstate, nseg * 4)); w->scr[6] = sstate;
+        WCHECK(walloc(bsum, (nseg / 1024 + 2) * 8)); w->scr[7] = bsum;
+        WCHECK(walloc(total, 16)); w->scr[8] = total;
+        dfin = bmap + nb;
+        hipLaunchKernelGGL(k_wcs_map, grid1(nseg), dim3(256), 0, st, buf, ds, n, nseg, map, cnt6);
+        hipLaunchKernelGGL(k_wcs_state_block, dim3((u32)nb), dim3(BLK), 0, st, (const u32 *)map, nseg, bmap);
+        hipLaunchKernelGGL(k_wcs_state_top, dim3(1), dim3(1), 0, st, bmap, nb, dfin);
+        hipLaunchKernelGGL(k_wcs_state_down, dim3((u32)nb), dim3(BLK), 0, st, (const u32 *)map, (const u64 *)cnt6,
+                           nseg, (const u32 *)bmap, sstate, cnt);
+        WCHECK(msa_exclusive_scan(cnt, nseg, roff, bsum, total, st));
+        u64 nend = 0;
+        WCHECK(hipMemcpyAsync(&nend, total, 8, hipMemcpyDeviceToHost, st));
+        WCHECK(hipMemcpyAsync(&fin, dfin, 4, hipMemcpyDeviceToHost, st));
+        WCHECK(hipStreamSynchronize(st));
+        nrows = nend + (fin == IQ ? 1 : 0);
+        if (nrows + 1 > w->rend_cap) {
+            wfree((void *&)w->d_rend);
+            w->rend_cap = nrows + 1;
+            WCHECK(walloc(w->d_rend, w->rend_cap * 8));
+        }
+        // rend[-1] = ds: rows are [rend[r-1], rend[r]) with d_rend shifted by one
+        WCHECK(hipMemcpyAsync(w->d_rend, &ds, 8, hipMemcpyHostToDevice, st));
+        hipLaunchKernelGGL(k_wcs_emit, grid1(nseg), dim3(256), 0, st, buf, ds, n, nseg, (const u32 *)sstate,
+                           (const u64 *)roff, w->d_rend + 1);
+        if (fin == IQ) WCHECK(hipMemcpyAsync(w->d_rend + nrows, &n, 8, hipMemcpyHostToDevice, st));
+    }
+    WCtr hc{};
+    WCHECK(hipMemcpyAsync(&hc, ctr, sizeof hc, hipMemcpyDeviceToHost, st));
+    WCHECK(hipStreamSynchronize(st));
+    if (hc.err != ~0ull) return wcs_input_error(w, hc.err);
+    if (nrows == 0) return wfail(w, MSA_ERR_BADHEADER, "CSV sem colunas esperadas. Campos necessários: artist, song, text.");
+
+    // ---- header (host)
+    u64 he = 0;
+    WCHECK(hipMemcpyAsync(&he, w->d_rend + 1, 8, hipMemcpyDeviceToHost, st));
+    WCHECK(hipStreamSynchronize(st));
+    u8 *hb = (u8 *)malloc(he - ds + 1);
+    if (he > ds) WCHECK(hipMemcpy(hb, buf + ds, he - ds, hipMemcpyDeviceToHost));
+    u32 ia = 0, isg = 0, it = 0;
+    int rc = parse_header(w, hb, he - ds, &ia, &isg, &it);
+    free(hb);
+    if (rc) return rc;
+    const u32 need = ia > isg ? (ia > it ? ia : it) : (isg > it ? isg : it);
+
+    // ---- per-row pass: d_rend[0] = ds, d_rend[k + 1] = end of file row k;
+    // per-row arrays are indexed by k + 1 (the header is index 1)
+    const u64 R = nrows + 1;
+    WCHECK(walloc(w->d_nd, R * 8));
+    WCHECK(walloc(w->d_spans, R * 32));
+    WCHECK(hipMemsetAsync(w->d_nd, 0, R * 8, st));
+    u64 *scratch;
+    WCHECK(walloc(scratch, (n + 64) * 8)); w->scr[9] = scratch;
+    u64 bits = w->gbits;
+    if (!bits) {
+        bits = 16;
+        while (bits < 28 && (1ull << bits) < n / 256) ++bits;
+    }
+    u64 *gtab = nullptr;
+    for (;;) {
+        const u64 slots = 1ull << bits;
+        wfree(w->scr[10]);
+        WCHECK(walloc(gtab, slots * 32)); w->scr[10] = gtab;
+        WCHECK(hipMemsetAsync(gtab, 0, slots * 32, st));
+        WCHECK(hipMemcpyAsync(ctr, &h0, sizeof h0, hipMemcpyHostToDevice, st));
+        RowArgs a;
+        a.buf = buf; a.n = n; a.rend = w->d_rend; a.ds = ds; a.nrows = R;
+        a.ia = ia; a.isg = isg; a.it = it; a.need = need;
+        a.gtab = gtab; a.gmask = slots - 1; a.glimit = slots / 4 * 3;
+        a.scratch = scratch; a.nd = w->d_nd; a.spans = w->d_spans; a.ctr = ctr;
+        if (R > 2) hipLaunchKernelGGL(k_wcs_rows, grid1(R - 2), dim3(256), 0, st, a);
+        WCHECK(hipGetLastError());
+        WCHECK(hipMemcpyAsync(&hc, ctr, sizeof hc, hipMemcpyDeviceToHost, st));
+        WCHECK(hipStreamSynchronize(st));
+        if (hc.err != ~0ull) return wcs_input_error(w, hc.err);
+        if (!(hc.overflow & OVF_G)) break;
+        if (bits >= 31) return wfail(w, MSA_ERR_CAPACITY, "word table overflow at 2^31 slots");
+        bits += 2;
+    }
+    const u64 slots = 1ull << bits;
+    const u64 nw = hc.distinct;
+
+    // ---- ranking
+    u64 *K2[3], *K1[3], *K0[3];
+    u32 *V[3];
+    u64 *kmem;
+    u32 *vmem;
+    WCHECK(walloc(kmem, (nw + 1) * 8 * 9)); w->scr[11] = kmem;
+    WCHECK(walloc(vmem, (nw + 1) * 4 * 3)); w->scr[12] = vmem;
+    for (int k = 0; k < 3; ++k) {
+        K2[k] = kmem + (u64)(3 * k + 0) * (nw + 1);
+        K1[k] = kmem + (u64)(3 * k + 1) * (nw + 1);
+        K0[k] = kmem + (u64)(3 * k + 2) * (nw + 1);
+        V[k] = vmem + (u64)k * (nw + 1);
+    }
+    hipLaunchKernelGGL(k_wcs_list, grid1(slots), dim3(256), 0, st, (const u64 *)gtab, slots, ctr, K2[0], K1[0], K0[0],
+                       V[0]);
+    int which = 1;
+    WCHECK(msa_launch_sort(K2, K1, K0, V, nw, &which, st));
+    const u32 *order = V[which];
+    u32 *rank_of;
+    WCHECK(walloc(rank_of, slots * 4)); w->scr[13] = rank_of;
+    u64 *wlen, *bsum2, *total2;
+    WCHECK(walloc(wlen, (nw + 1) * 8)); w->scr[14] = wlen;
+    WCHECK(walloc(w->d_counts, (nw + 1) * 4));
+    WCHECK(walloc(w->d_woff, (nw + 1) * 8));
+    WCHECK(walloc(bsum2, ((R > nw ? R : nw) / 1024 + 2) * 8)); w->scr[15] = bsum2;
+    WCHECK(walloc(total2, 16)); w->scr[16] = total2;
+    if (nw) {
+        hipLaunchKernelGGL(k_wcs_wordlen, grid1(nw), dim3(256), 0, st, buf, (const u64 *)gtab, order, nw, rank_of, wlen,
+                           w->d_counts, ctr);
+        WCHECK(msa_exclusive_scan(wlen, nw, w->d_woff, bsum2, total2, st));
+        WCHECK(hipMemcpyAsync(w->d_woff + nw, total2, 8, hipMemcpyDeviceToDevice, st));
+    } else {
+        WCHECK(hipMemsetAsync(w->d_woff, 0, 8, st));
+    }
+    u64 blob_len = 0;
+    WCHECK(hipMemcpyAsync(&blob_len, w->d_woff + nw, 8, hipMemcpyDeviceToHost, st));
+    WCHECK(hipStreamSynchronize(st));
+    WCHECK(walloc(w->d_blob, blob_len + 16));
+    if (nw)
+        hipLaunchKernelGGL(k_wcs_wordblob, grid1(nw), dim3(256), 0, st, buf, (const u64 *)gtab, order, nw,
+                           (const u64 *)w->d_woff, w->d_blob, ctr);
+
+    // ---- by-song lines
+    u64 *poff;
+    WCHECK(walloc(poff, R * 8)); w->scr[17] = poff;
+    WCHECK(msa_exclusive_scan(w->d_nd, R, poff, bsum2, total2, st));
+    u64 np = 0;
+    WCHECK(hipMemcpyAsync(&np, total2, 8, hipMemcpyDeviceToHost, st));
+    WCHECK(hipStreamSynchronize(st));
+    WCHECK(walloc(w->d_pairs, np * 8 + 16));
+    if (R > 2)
+        hipLaunchKernelGGL(k_wcs_pairs, grid1(R - 2), dim3(256), 0, st, (const u64 *)w->d_rend, R,
+                           (const u64 *)w->d_nd, (const u64 *)poff, (const u64 *)scratch, (const u32 *)rank_of,
+                           w->d_pairs);
+    WCHECK(hipGetLastError());
+    WCHECK(hipMemcpyAsync(&hc, ctr, sizeof hc, hipMemcpyDeviceToHost, st));
+    WCHECK(hipStreamSynchronize(st));
+    if (hc.collision) return wfail(w, MSA_ERR_COLLISION, "64-bit word-hash collision detected (%llu words)",
+                                   (unsigned long long)hc.collision);
+    w->nrows = R;
+    w->nw = nw;
+    w->np = np;
+    w->blob_len = blob_len;
+    w->sum.total_rows = hc.total_rows;
+    w->sum.song_rows = hc.song_rows;
+    w->sum.total_tokens = hc.tokens;
+    w->sum.n_words = nw;
+    w->sum.n_pairs = np;
+    w->have = true;
+    return MSA_OK;
+}
+
+extern "C" int msa_wcs_get_summary(msa_wcs *w, msa_wcs_summary *out) {
+    if (!w || !out || !w->have) return MSA_ERR_ARG;
+    *out = w->sum;
+    return MSA_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Output formatting (csv.writer, QUOTE_MINIMAL, "\r\n").
+namespace {
+struct Out {
+    char *p = nullptr;
+    size_t n = 0, cap = 0;
+    bool put(const void *s, size_t k) {
+        if (n + k > cap) {
+            size_t c = cap ? cap : 1 << 16;
+            while (c < n + k) c *= 2;
+            char *q = (char *)realloc(p, c);
+            if (!q) return false;
+            p = q;
+            cap = c;
+        }
+        memcpy(p + n, s, k);
+        n += k;
+        return true;
+    }
+    bool num(u64 v) {
+        char t[24];
+        int k = snprintf(t, sizeof t, "%llu", (unsigned long long)v);
+        return put(t, (size_t)k);
+    }
+};
+
+// Field content of a raw span: the reader's added characters.
+void field_content(const u8 *b, u64 s, u64 e, std::string &o) {
+    o.clear();
+    u32 st = SF;
+    for (u64 i = s; i < e; ++i) {
+        const u8 c = b[i];
+        switch (st) {
+            case SF:
+                if (c == '"') st = IQ;
+                else { o.push_back((char)c); st = IF; }
+                break;
+            case IF: o.push_back((char)c); break;
+            case IQ:
+                if (c == '"') st = QQ;
+                else o.push_back((char)c);
+                break;
+            default:  // QQ
+                o.push_back((char)c);
+                st = c == '"' ? IQ : IF;
+                break;
+        }
+    }
+}
+bool py_space(u32 cp) {
+    return (cp >= 0x9 && cp <= 0xD) || (cp >= 0x1C && cp <= 0x20) || cp == 0x85 || cp == 0xA0 || cp == 0x1680 ||
+           (cp >= 0x2000 && cp <= 0x200A) || cp == 0x2028 || cp == 0x2029 || cp == 0x202F || cp == 0x205F ||
+           cp == 0x3000;
+}
+u32 cp_at(const std::string &s, size_t i, size_t *len) {
+    const u8 c = (u8)s[i];
+    if (c < 0x80) { *len = 1; return c; }
+    if (c < 0xE0) { *len = 2; return ((c & 0x1Fu) << 6) | ((u8)s[i + 1] & 0x3Fu); }
+    if (c < 0xF0) { *len = 3; return ((c & 0x0Fu) << 12) | (((u8)s[i + 1] & 0x3Fu) << 6) | ((u8)s[i + 2] & 0x3Fu); }
+    *len = 4;
+    return ((c & 0x07u) << 18) | (((u8)s[i + 1] & 0x3Fu) << 12) | (((u8)s[i + 2] & 0x3Fu) << 6) | ((u8)s[i + 3] & 0x3Fu);
+}
+// str.strip() over UTF-8
+void py_strip(std::string &s) {
+    size_t a = 0, z = s.size(), l;
+    while (a < z && py_space(cp_at(s, a, &l))) a += l;
+    while (z > a) {
+        size_t k = z - 1;
+        while (k > a && ((u8)s[k] & 0xC0) == 0x80) --k;
+        if (!py_space(cp_at(s, k, &l))) break;
+        z = k;
+    }
+    s = s.substr(a, z - a);
+}
+bool csv_field(Out &o, const std::string &s) {
+    if (s.find_first_of(",\"\r\n") == std::string::npos) return o.put(s.data(), s.size());
+    if (!o.put("\"", 1)) return false;
+    for (char c : s) {
+        if (c == '"' && !o.put("\"", 1)) return false;
+        if (!o.put(&c, 1)) return false;
+    }
+    return o.put("\"", 1);
+}
+}  // namespace
+
+extern "C" int msa_wcs_get_csv(msa_wcs *w, int which, char **out, size_t *len) {
+    if (!w || !out || !len || !w->have || (which != MSA_WCS_GLOBAL && which != MSA_WCS_BY_SONG)) return MSA_ERR_ARG;
+    WCHECK(hipSetDevice(w->device));
+    const u64 nw = w->nw;
+    u32 *counts = (u32 *)malloc((nw + 1) * 4);
+    u64 *woff = (u64 *)malloc((nw + 1) * 8);
+    u8 *blob = (u8 *)malloc(w->blob_len + 1);
+    WCHECK(hipMemcpy(counts, w->d_counts, nw * 4, hipMemcpyDeviceToHost));
+    WCHECK(hipMemcpy(woff, w->d_woff, (nw + 1) * 8, hipMemcpyDeviceToHost));
+    WCHECK(hipMemcpy(blob, w->d_blob, w->blob_len, hipMemcpyDeviceToHost));
+    Out o;
+    bool ok = true;
+    if (which == MSA_WCS_GLOBAL) {
+        ok = o.put("word,count\r\n", 12);
+        for (u64 i = 0; ok && i < nw; ++i) {
+            ok = o.put(blob + woff[i], woff[i + 1] - woff[i]) && o.put(",", 1) && o.num(counts[i]) && o.put("\r\n", 2);
+        }
+    } else {
+        const u64 R = w->nrows;
+        u64 *nd = (u64 *)malloc(R * 8), *sp = (u64 *)malloc(R * 32), *pairs = (u64 *)malloc(w->np * 8 + 8);
+        u8 *csv = (u8 *)malloc(w->n + 1);
+        WCHECK(hipMemcpy(nd, w->d_nd, R * 8, hipMemcpyDeviceToHost));
+        WCHECK(hipMemcpy(sp, w->d_spans, R * 32, hipMemcpyDeviceToHost));
+        WCHECK(hipMemcpy(pairs, w->d_pairs, w->np * 8, hipMemcpyDeviceToHost));
+        WCHECK(hipMemcpy(csv, w->d_buf, w->n, hipMemcpyDeviceToHost));
+        ok = o.put("artist,song,word,count\r\n", 24);
+        std::string fa, fs;
+        Out pre;
+        u64 p = 0;
+        for (u64 r = 2; ok && r < R; ++r) {
+            if (!nd[r]) continue;
+            field_content(csv, sp[r * 4 + 0], sp[r * 4 + 1], fa);
+            field_content(csv, sp[r * 4 + 2], sp[r * 4 + 3], fs);
+            py_strip(fa);
+            py_strip(fs);
+            pre.n = 0;
+            ok = csv_field(pre, fa) && pre.put(",", 1) && csv_field(pre, fs) && pre.put(",", 1);
+            for (u64 k = 0; ok && k < nd[r]; ++k, ++p) {
+                const u64 v = pairs[p];
+                const u64 rank = v >> 32;
+                ok = o.put(pre.p, pre.n) && o.put(blob + woff[rank], woff[rank + 1] - woff[rank]) && o.put(",", 1) &&
+                     o.num(v & 0xFFFFFFFFu) && o.put("\r\n", 2);
+            }
+        }
+        free(pre.p);
+        free(nd); free(sp); free(pairs); free(csv);
+    }
+    free(counts); free(woff); free(blob);
+    if (!ok) { free(o.p); return wfail(w, MSA_ERR_HIP, "out of host memory"); }
+    *out = o.p ? o.p : (char *)malloc(1);
+    *len = o.n;
+    return MSA_OK;
+}
+
+extern "C" int msa_wcs_write_outputs(msa_wcs *w, const char *outdir) {
+    if (!w || !outdir || !w->have) return MSA_ERR_ARG;
+    static const char *names[2] = {"word_counts_global.csv", "word_counts_by_song.csv"};
+    for (int k = 0; k < 2; ++k) {
+        char *d = nullptr;
+        size_t len = 0;
+        int rc = msa_wcs_get_csv(w, k, &d, &len);
+        if (rc) return rc;
+        char path[4096];
+        snprintf(path, sizeof path, "%s/%s", outdir, names[k]);
+        FILE *f = fopen(path, "wb");
+        if (!f) { free(d); return wfail(w, MSA_ERR_IO, "cannot open %s", path); }
+        const bool ok = fwrite(d, 1, len, f) == len;
+        free(d);
+        if (fclose(f) != 0 || !ok) return wfail(w, MSA_ERR_IO, "write failed: %s", path);
+    }
+    return MSA_OK;
+}

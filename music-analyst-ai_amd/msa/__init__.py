@@ -27,6 +27,7 @@ MSA_ERR = {
     -5: "MSA_ERR_CAPACITY",
     -6: "MSA_ERR_COLLISION",
     -7: "MSA_ERR_IO",
+    -8: "MSA_ERR_INPUT",
 }
 MSA_SPLIT_TEXT_COLUMN = 1
 MSA_TABLE_WORDS = 0
@@ -42,7 +43,11 @@ EXPORTS = [
     "msa_write_table_csv", "msa_get_split_column", "msa_set_profiling", "msa_get_profile",
     "msa_set_shard", "msa_piece_size", "msa_shard_function", "msa_shard_head", "msa_segment_copy",
     "msa_segment_set", "msa_export_partitions", "msa_export_copy", "msa_import_partitions",
+    "msa_wcs_create", "msa_wcs_destroy", "msa_wcs_last_error", "msa_wcs_stream", "msa_wcs_load_csv",
+    "msa_wcs_set_table_bits", "msa_wcs_run", "msa_wcs_get_summary", "msa_wcs_get_csv", "msa_wcs_write_outputs",
 ]
+MSA_WCS_GLOBAL = 0
+MSA_WCS_BY_SONG = 1
 PIECE_CSV = 0
 PIECE_ARTISTS = 1
 SHARD_FN_BYTES = 120  # sizeof(msa_shard_fn)
@@ -90,6 +95,10 @@ class _Profile(C.Structure):
     ]
 
 
+class _WcsSummary(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in ("total_rows", "song_rows", "total_tokens", "n_words", "n_pairs")]
+
+
 _lib = None
 
 
@@ -135,6 +144,19 @@ def load(path: str = LIB_PATH):
     lib.msa_import_partitions.argtypes = [vp, i, vp, C.POINTER(u64), i]
     lib.msa_set_profiling.argtypes = [vp, i]
     lib.msa_get_profile.argtypes = [vp, C.POINTER(_Profile), i]
+    lib.msa_wcs_create.argtypes = [i, C.POINTER(vp)]
+    lib.msa_wcs_destroy.argtypes = [vp]
+    lib.msa_wcs_destroy.restype = None
+    lib.msa_wcs_last_error.argtypes = [vp]
+    lib.msa_wcs_last_error.restype = C.c_char_p
+    lib.msa_wcs_stream.argtypes = [vp]
+    lib.msa_wcs_stream.restype = vp
+    lib.msa_wcs_load_csv.argtypes = [vp, vp, sz]
+    lib.msa_wcs_set_table_bits.argtypes = [vp, i]
+    lib.msa_wcs_run.argtypes = [vp]
+    lib.msa_wcs_get_summary.argtypes = [vp, C.POINTER(_WcsSummary)]
+    lib.msa_wcs_get_csv.argtypes = [vp, i, C.POINTER(C.c_void_p), C.POINTER(sz)]
+    lib.msa_wcs_write_outputs.argtypes = [vp, C.c_char_p]
     _lib = lib
     return lib
 
@@ -314,3 +336,68 @@ def table_csv_bytes(entries: List[Tuple[bytes, int]], key_header: str, limit: in
     for k, c in entries:
         out.append(b'"' + k.replace(b'"', b'""') + b'",' + str(c).encode() + b"\n")
     return b"".join(out)
+
+
+class WordCountPerSong:
+    """Per-song word counter on the GPU (msa_wcs_*): the drop-in for
+    /root/reference/scripts/word_count_per_song.py's counting.  ``run(data)``
+    returns (rows processed, word_counts_by_song.csv bytes,
+    word_counts_global.csv bytes) -- the values the script prints/writes."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load()
+        h = C.c_void_p()
+        rc = self.lib.msa_wcs_create(device, C.byref(h))
+        if rc:
+            raise MsaError(rc, f"msa_wcs_create(device={device}) failed (no GPU visible?)")
+        self.h = h
+
+    def close(self):
+        if self.h:
+            self.lib.msa_wcs_destroy(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _check(self, rc: int):
+        if rc:
+            raise MsaError(rc, (self.lib.msa_wcs_last_error(self.h) or b"").decode(errors="replace"))
+
+    @property
+    def stream(self) -> int:
+        return self.lib.msa_wcs_stream(self.h) or 0
+
+    def load_csv(self, data: bytes):
+        self._check(self.lib.msa_wcs_load_csv(self.h, data, len(data)))
+
+    def set_table_bits(self, bits: int):
+        self._check(self.lib.msa_wcs_set_table_bits(self.h, bits))
+
+    def count(self):
+        self._check(self.lib.msa_wcs_run(self.h))
+
+    def summary(self) -> dict:
+        s = _WcsSummary()
+        self._check(self.lib.msa_wcs_get_summary(self.h, C.byref(s)))
+        return {n: getattr(s, n) for n, _ in _WcsSummary._fields_}
+
+    def csv(self, which: int) -> bytes:
+        out = C.c_void_p()
+        n = C.c_size_t()
+        self._check(self.lib.msa_wcs_get_csv(self.h, which, C.byref(out), C.byref(n)))
+        try:
+            return C.string_at(out, n.value)
+        finally:
+            self.lib.msa_free(out)
+
+    def write_outputs(self, outdir: str):
+        self._check(self.lib.msa_wcs_write_outputs(self.h, outdir.encode()))
+
+    def run(self, data: bytes) -> Tuple[int, bytes, bytes]:
+        self.load_csv(data)
+        self.count()
+        return self.summary()["total_rows"], self.csv(MSA_WCS_BY_SONG), self.csv(MSA_WCS_GLOBAL)

@@ -1,0 +1,127 @@
+"""GPU parity of the per-song word counter (msa_wcs_*, csrc/msa_wcs.hip).
+
+* golden: byte-identical word_counts_by_song.csv / word_counts_global.csv and
+  row count against outputs of the REAL reference script
+  (tests/golden/wcs/, made by tests/golden/make_wcs_golden.py); inputs the
+  script fails on must be refused.
+* oracle: oracle/wcs_oracle.py (checker only) on fresh seeded torture corpora
+  and Zipfian corpora, incl. a forced tiny word table (growth path).
+* full-size properties on a 200k-song corpus: the by-song counts of every
+  word sum to its global count, global counts sum to the token total,
+  ranking order (count desc) holds.
+"""
+import os
+import random
+import sys
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "..", "oracle"))
+sys.path.insert(0, os.path.join(HERE, "golden"))
+import wcs_oracle  # noqa: E402
+from test_wcs_oracle import CASES, load_case  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def wcs(msa_mod):
+    w = msa_mod.WordCountPerSong(0)
+    yield w
+    w.close()
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_wcs_golden(msa_mod, wcs, name):
+    data, exp = load_case(name)
+    if exp is None:
+        with pytest.raises(msa_mod.MsaError):
+            wcs.run(data)
+        return
+    assert wcs.run(data) == exp
+
+
+def _torture(seed, n):
+    from make_wcs_golden import torture
+
+    return torture(seed, n).encode("utf-8")
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3, 4, 5, 6, 7, 8])
+def test_wcs_torture_vs_oracle(wcs, seed):
+    data = _torture(1000 + seed, 400)
+    assert wcs.run(data) == wcs_oracle.word_count_per_song(data)
+
+
+@pytest.mark.parametrize("seed,crlf", [(11, False), (12, True)])
+def test_wcs_zipf_vs_oracle(msa_mod, wcs, seed, crlf):
+    data = msa_mod.gen_corpus(1500, mode="zipf", seed=seed, crlf=crlf, vocab=3000)
+    assert wcs.run(data) == wcs_oracle.word_count_per_song(data)
+
+
+def test_wcs_table_growth(msa_mod):
+    """A 2^4-slot word table overflows; the run grows it and repeats."""
+    data = msa_mod.gen_corpus(800, mode="highcard", seed=21, vocab=20000)
+    exp = wcs_oracle.word_count_per_song(data)
+    with msa_mod.WordCountPerSong(0) as w:
+        w.set_table_bits(4)
+        assert w.run(data) == exp
+
+
+def test_wcs_edge_inputs(msa_mod, wcs):
+    hdr = b"artist,song,link,text\n"
+    cases = [
+        hdr + b'A,S,/l,"' + b"x" * 5000 + b'"\n',                     # one long token
+        hdr + b'A,S,/l,"ab""cd""ef ghi"\n',                             # escaped quotes split tokens
+        hdr + b'A,S,/l,"abc"def ghi\n',                                  # token across a closing quote
+        hdr + b"A,S,/l,\xc3\x80\xc3\x81\xc3\x82 \xc3\x97\xc3\x97\xc3\x97\n",  # latin-1 letters, x sign
+        b"\xef\xbb\xbf" + hdr + b"A,S,/l,words here\r\n\r\nB,T,/l,more words\r",  # BOM, CR, blank line
+        hdr + b'A,S,/l,"unterminated words\nsecond line',               # EOF inside quotes
+        hdr + (b"A,S,/l,alpha beta gamma\n" * 3000),                    # many rows, one word set
+    ]
+    for d in cases:
+        assert wcs.run(d) == wcs_oracle.word_count_per_song(d), d[:80]
+    for bad in (hdr + b"A,S,/l,ab\xffcd\n", hdr + b"A,S,/l,ab\x00cd\n", hdr + b"A,S\n",
+                hdr + b'A,S,/l,"' + b"y" * 131073 + b'"\n', b"", b"x,y\n1,2\n"):
+        with pytest.raises(msa_mod.MsaError):
+            wcs.run(bad)
+
+
+def test_wcs_full_size_properties(msa_mod, wcs):
+    data = msa_mod.gen_corpus(200000, mode="zipf", seed=31, vocab=50000)
+    rows, by_song, glob = wcs.run(data)
+    s = wcs.summary()
+    assert rows == 200000 == s["total_rows"]
+    g = {}
+    prev = None
+    for line in glob.split(b"\r\n")[1:-1]:
+        w, c = line.rsplit(b",", 1)
+        c = int(c)
+        assert prev is None or c <= prev
+        prev = c
+        g[w] = c
+    assert len(g) == s["n_words"]
+    assert sum(g.values()) == s["total_tokens"]
+    acc = {}
+    nlines = 0
+    for line in by_song.split(b"\r\n")[1:-1]:
+        w, c = line.rsplit(b",", 2)[1:]
+        acc[w] = acc.get(w, 0) + int(c)
+        nlines += 1
+    assert nlines == s["n_pairs"]
+    assert acc == g
+    # a random sample of songs against the oracle, row by row
+    lines = data.split(b"\n")
+    rnd = random.Random(5)
+    hdr = lines[0] + b"\n"
+    for _ in range(3):
+        k = rnd.randrange(1, len(lines) - 400)
+        sample = hdr + b"\n".join(lines[k:k + 300]) + b"\n"  # may start/end inside a quoted lyric
+        try:
+            exp = wcs_oracle.word_count_per_song(sample)
+        except wcs_oracle.WcsError:  # a cut lyric leaves a short row: both refuse
+            with pytest.raises(msa_mod.MsaError):
+                wcs.run(sample)
+            continue
+        assert wcs.run(sample) == exp
