@@ -290,7 +290,10 @@ __host__ __device__ __forceinline__ u64 h1_fin(u64 h, u64 len) {
     const u64 k = fmix64(h ^ (len * 0xD6E8FEB86659FD93ull));
     return k ? k : 1;
 }
-__host__ __device__ __forceinline__ u64 h2_fin(u64 h, u64 len) { return fmix64(h + len); }
+__host__ __device__ __forceinline__ u64 h2_fin(u64 h, u64 len) {
+    const u64 k = fmix64(h + len);
+    return k ? k : 1;
+}
 
 struct RowArgs {
     const u8 *buf;
@@ -299,7 +302,7 @@ struct RowArgs {
     u64 ds;
     u64 nrows;
     u32 ia, isg, it, need;
-    u64 *gtab;      // 4 u64 per slot: key, h2 sum, ~first (pos << 20 | raw len), count
+    u64 *gtab;      // 4 u64 per slot: key, h2 of the word, ~first (pos << 20 | raw len), count
     u64 gmask;
     u64 glimit;
     u64 *scratch;   // per-row tables, row r at scratch + row start
@@ -333,11 +336,44 @@ __device__ __forceinline__ void wcs_err(WCtr *ctr, u64 row, u32 code) {
     atomicMin((unsigned long long *)&ctr->err, (unsigned long long)((row << 8) | code));
 }
 
-__global__ __launch_bounds__(256) void k_wcs_rows(RowArgs a) {
-    // row k of the file spans [rend[k], rend[k+1]); kernel index r = k + 1,
-    // r = 1 is the header row
-    const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x + 2;
-    if (r >= a.nrows) return;
+// Workgroup-private aggregation of the global word updates (the Zipf head
+// would otherwise serialise every token on a few device-scope atomics): per
+// word seen by the workgroup, LDS holds the count, the max of ~first and the
+// first token's h2 (a second, independent 64-bit hash: every token's h2 must
+// equal it, which catches 64-bit h1 collisions).  Flushed once per workgroup.
+constexpr u32 LW = 2048, LW_PROBE = 8;
+struct WgAgg {
+    u32 *id;
+    u32 *cnt;
+    u64 *h2;
+    u64 *first;
+    u64 *rows;  // [0] rows, [1] song rows, [2] tokens, [3] collisions
+};
+
+__device__ __forceinline__ void word_update(const RowArgs &a, WgAgg &g, u64 slot, u64 h2v, u64 nfirst) {
+    const u32 id = (u32)slot + 1;
+    u32 h = (id * 0x9E3779B1u) >> 21;
+    for (u32 p = 0; p < LW_PROBE; ++p, h = (h + 1) & (LW - 1)) {
+        u32 cur = g.id[h];
+        if (cur == 0) {
+            const u32 old = atomicCAS(&g.id[h], 0u, id);
+            cur = old == 0 ? id : old;
+        }
+        if (cur != id) continue;
+        atomicAdd(&g.cnt[h], 1u);
+        atomicMax((unsigned long long *)&g.first[h], (unsigned long long)nfirst);
+        const u64 o = atomicCAS((unsigned long long *)&g.h2[h], 0ull, (unsigned long long)h2v);
+        if (o != 0 && o != h2v) atomicAdd((unsigned long long *)&g.rows[3], 1ull);
+        return;
+    }
+    u64 *gt = a.gtab + slot * 4;  // LDS table full here: straight to HBM
+    atomicAdd((unsigned long long *)(gt + 3), 1ull);
+    atomicMax((unsigned long long *)(gt + 2), (unsigned long long)nfirst);
+    const u64 o = atomicCAS((unsigned long long *)(gt + 1), 0ull, (unsigned long long)h2v);
+    if (o != 0 && o != h2v) atomicAdd((unsigned long long *)&a.ctr->collision, 1ull);
+}
+
+__device__ __forceinline__ void wcs_row(const RowArgs &a, WgAgg &agg, u64 r) {
     const u64 rs = a.rend[r - 1], re = a.rend[r];
     ByteReader rd(a.buf);
     u32 s = SR, f = 0, chars = 0;
@@ -358,10 +394,7 @@ __global__ __launch_bounds__(256) void k_wcs_rows(RowArgs a) {
             const u64 key = h1_fin(h1, tlen);
             const u64 slot = g_insert(a, key);
             if (slot != ~0ull) {
-                u64 *g = a.gtab + slot * 4;
-                atomicAdd((unsigned long long *)(g + 1), (unsigned long long)h2_fin(h2, tlen));
-                atomicMax((unsigned long long *)(g + 2), (unsigned long long)~((tstart << 20) | (end - tstart)));
-                atomicAdd((unsigned long long *)(g + 3), 1ull);
+                word_update(a, agg, slot, h2_fin(h2, tlen), ~((tstart << 20) | (end - tstart)));
                 if (ntok == 0)
                     for (u32 k = 0; k < rcap; ++k) rt[k] = 0;
                 ++ntok;
@@ -444,15 +477,45 @@ __global__ __launch_bounds__(256) void k_wcs_rows(RowArgs a) {
     if (s == IQ) save(re);  // input ended inside a quoted field
     if (limit) wcs_err(a.ctr, r, E_LIMIT);
     if (!any) { a.nd[r] = 0; return; }  // blank line: DictReader skips it
-    atomicAdd((unsigned long long *)&a.ctr->total_rows, 1ull);
+    atomicAdd((unsigned long long *)&agg.rows[0], 1ull);
     if (f <= a.need) wcs_err(a.ctr, r, E_SHORT);
     a.nd[r] = nd;
     if (nd) {
-        atomicAdd((unsigned long long *)&a.ctr->song_rows, 1ull);
-        atomicAdd((unsigned long long *)&a.ctr->tokens, (unsigned long long)ntok);
+        atomicAdd((unsigned long long *)&agg.rows[1], 1ull);
+        atomicAdd((unsigned long long *)&agg.rows[2], (unsigned long long)ntok);
     }
     u64 *o = a.spans + r * 4;
     o[0] = sp[0]; o[1] = sp[1]; o[2] = sp[2]; o[3] = sp[3];
+}
+
+__global__ __launch_bounds__(256) void k_wcs_rows(RowArgs a) {
+    __shared__ u32 l_id[LW], l_cnt[LW];
+    __shared__ u64 l_h2[LW], l_first[LW], l_rows[4];
+    for (u32 k = threadIdx.x; k < LW; k += blockDim.x) { l_id[k] = 0; l_cnt[k] = 0; l_h2[k] = 0; l_first[k] = 0; }
+    if (threadIdx.x < 4) l_rows[threadIdx.x] = 0;
+    __syncthreads();
+    WgAgg agg{l_id, l_cnt, l_h2, l_first, l_rows};
+    // row k of the file spans [rend[k], rend[k+1]); kernel index r = k + 1,
+    // r = 1 is the header row
+    const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x + 2;
+    if (r < a.nrows) wcs_row(a, agg, r);
+    __syncthreads();
+    for (u32 k = threadIdx.x; k < LW; k += blockDim.x) {
+        const u32 id = l_id[k];
+        if (!id) continue;
+        u64 *gt = a.gtab + (u64)(id - 1) * 4;
+        atomicAdd((unsigned long long *)(gt + 3), (unsigned long long)l_cnt[k]);
+        atomicMax((unsigned long long *)(gt + 2), (unsigned long long)l_first[k]);
+        const u64 h2v = l_h2[k];
+        const u64 o = atomicCAS((unsigned long long *)(gt + 1), 0ull, (unsigned long long)h2v);
+        if (o != 0 && o != h2v) atomicAdd((unsigned long long *)&a.ctr->collision, 1ull);
+    }
+    if (threadIdx.x == 0) {
+        atomicAdd((unsigned long long *)&a.ctr->total_rows, (unsigned long long)l_rows[0]);
+        atomicAdd((unsigned long long *)&a.ctr->song_rows, (unsigned long long)l_rows[1]);
+        atomicAdd((unsigned long long *)&a.ctr->tokens, (unsigned long long)l_rows[2]);
+        if (l_rows[3]) atomicAdd((unsigned long long *)&a.ctr->collision, (unsigned long long)l_rows[3]);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -496,7 +559,7 @@ __global__ __launch_bounds__(256) void k_wcs_wordlen(const u8 *__restrict__ buf,
         ++l;
     }
     const u64 cnt = g[3];
-    if (h1_fin(h1, l) != g[0] || h2_fin(h2, l) * cnt != g[1])
+    if (h1_fin(h1, l) != g[0] || h2_fin(h2, l) != g[1])
         atomicAdd((unsigned long long *)&ctr->collision, 1ull);
     rank_of[slot] = (u32)i;
     len[i] = l;

@@ -12,6 +12,7 @@
 """
 import os
 import random
+import subprocess
 import sys
 
 import pytest
@@ -125,3 +126,22 @@ def test_wcs_full_size_properties(msa_mod, wcs):
                 wcs.run(sample)
             continue
         assert wcs.run(sample) == exp
+
+
+@pytest.mark.parametrize("name", [c for c in CASES if c in ("basic", "crlf_cr_blank", "zipf_300", "err_missing_col",
+                                                          "err_short_row", "torture_2")])
+def test_wcs_cli_golden(msa_mod, name, tmp_path):
+    """bin/word_count_per_song writes the script's two files and prints its row count."""
+    cli = os.path.join(msa_mod.PKG_DIR, "bin", "word_count_per_song")
+    data, exp = load_case(name)
+    inp = tmp_path / "in.csv"
+    inp.write_bytes(data)
+    out = tmp_path / "out"
+    r = subprocess.run([cli, str(inp), "--output-dir", str(out), "--delimiter", ","], capture_output=True, timeout=120)
+    if exp is None:
+        assert r.returncode != 0
+        return
+    assert r.returncode == 0, r.stderr
+    assert f"Processadas {exp[0]} linhas".encode() in r.stdout
+    assert (out / "word_counts_by_song.csv").read_bytes() == exp[1]
+    assert (out / "word_counts_global.csv").read_bytes() == exp[2]

@@ -1,0 +1,64 @@
+"""Bench of the per-song word counter (DESIGN.md row f): msa_wcs_run over a
+synthetic Zipfian lyric CSV resident in HBM (same generator and size as the
+main bench: 5M songs, ~1.2 GB), one JSON line on stdout.
+
+    python tools/bench_wcs.py [--songs N] [--steps K] [--warmup W] [--no-cpu-baseline]
+
+The timed step is the whole msa_wcs_run (validation, row split, per-row
+tokenise + count, ranking, by-song lines; results left in HBM) -- it syncs
+with the host between phases, so wall-clock around it is the step time.
+cpu_baseline: oracle/wcs_oracle.py (pure-Python restatement of the script,
+kind "port", 1 core) on a bounded sample of the same corpus.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "music-analyst-ai_amd"))
+import msa  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--songs", type=int, default=5_000_000)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    a = ap.parse_args()
+    data = msa.gen_corpus(a.songs, mode="zipf", seed=1)
+    n = len(data)
+    with msa.WordCountPerSong(0) as w:
+        w.load_csv(data)
+        for _ in range(a.warmup):
+            w.count()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            w.count()
+        dt = (time.perf_counter() - t0) / a.steps
+        s = w.summary()
+    out = {
+        "metric": "CSV->per-song word counts GB/s (word_count_per_song.py path)",
+        "value": round(n / dt / 1e9, 3), "unit": "GB/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": round(dt * 1e3, 3), "higher_is_better": True, "dtype": "u8",
+        "data": "synthetic (csrc/msa_gen.c Zipfian lyric CSV, seed 1)",
+        "config": {"workload": f"{a.songs} songs, {n} bytes, resident in HBM", "summary": s},
+    }
+    if not a.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import wcs_oracle  # checker restatement, timed as the CPU baseline only
+
+        sample = msa.gen_corpus(20000, mode="zipf", seed=1)
+        t0 = time.perf_counter()
+        wcs_oracle.word_count_per_song(sample)
+        ct = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": round(len(sample) / ct / 1e9, 6), "unit": "GB/s", "cores": 1, "kind": "port",
+                               "seconds": round(ct, 3),
+                               "sample": f"20000 songs, {len(sample)} bytes, oracle/wcs_oracle.py (pure Python)"}
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
