@@ -305,7 +305,7 @@ struct RowArgs {
     u64 *gtab;      // 4 u64 per slot: key, h2 of the word, ~first (pos << 20 | raw len), count
     u64 gmask;
     u64 glimit;
-    u64 *scratch;   // per-row tables, row r at scratch + row start
+    u64 *scratch;   // per-row work areas, row at scratch + 3 * row start
     u64 *nd;        // distinct words per row
     u64 *spans;     // 4 per row: artist start/end, song start/end (raw)
     WCtr *ctr;
@@ -384,29 +384,22 @@ __device__ __forceinline__ void wcs_row(const RowArgs &a, WgAgg &agg, u64 r) {
     bool in_tok = false, alnum = false, skip = false;
     u32 cps = 0;
     u64 h1 = H1_0, h2 = H2_0, tlen = 0, tstart = 0;
-    u64 *rt = a.scratch + rs;
-    const u32 rcap = (u32)((re - rs) / 2 + 2);
+    // scratch of this row (u64 units, disjoint from every other row's):
+    //   [0, 3*tmax)            token records (h1, h2, ~first) from the byte walk;
+    //                          its front is reused as the u32 order->slot list
+    //   [tmax, tmax + nd)      the row's (word id, count) lines in order
+    //   [3*tmax, +2*ntok)      per-row hash table (id, order, count)
+    u64 *sc = a.scratch + 3 * rs;
+    const u64 tmax = (re - rs) / 4 + 1;
     u32 nd = 0, ntok = 0;
     bool limit = false;
 
     auto tok_end = [&](u64 end) {
-        if (in_tok && cps >= 3 && alnum) {
-            const u64 key = h1_fin(h1, tlen);
-            const u64 slot = g_insert(a, key);
-            if (slot != ~0ull) {
-                word_update(a, agg, slot, h2_fin(h2, tlen), ~((tstart << 20) | (end - tstart)));
-                if (ntok == 0)
-                    for (u32 k = 0; k < rcap; ++k) rt[k] = 0;
-                ++ntok;
-                const u64 id = slot + 1;
-                u32 h = (u32)(((id * 0x9E3779B97F4A7C15ull) >> 32) % rcap);
-                for (;;) {
-                    const u64 v = rt[h];
-                    if (v == 0) { rt[h] = (id << 32) | ((u64)nd << 16) | 1u; ++nd; break; }
-                    if ((v >> 32) == id) { rt[h] = v + 1; break; }
-                    h = h + 1 == rcap ? 0 : h + 1;
-                }
-            }
+        if (in_tok && cps >= 3 && alnum) {  // record only: the walk stays free of memory round trips
+            u64 *t = sc + 3 * (u64)ntok++;
+            t[0] = h1_fin(h1, tlen);
+            t[1] = h2_fin(h2, tlen);
+            t[2] = ~((tstart << 20) | (end - tstart));
         }
         in_tok = false;
     };
@@ -477,12 +470,35 @@ __device__ __forceinline__ void wcs_row(const RowArgs &a, WgAgg &agg, u64 r) {
     if (s == IQ) save(re);  // input ended inside a quoted field
     if (limit) wcs_err(a.ctr, r, E_LIMIT);
     if (!any) { a.nd[r] = 0; return; }  // blank line: DictReader skips it
+    // tokens -> global table (via the workgroup aggregate) and per-row table;
+    // every lane runs the same loop, one iteration per token
+    if (ntok) {
+        const u32 rcap = 2 * ntok;
+        u64 *rt = sc + 3 * tmax;
+        u32 *list = (u32 *)sc;
+        for (u32 k = 0; k < rcap; ++k) rt[k] = 0;
+        for (u32 t = 0; t < ntok; ++t) {
+            const u64 key = sc[3 * t], h2v = sc[3 * t + 1], nfirst = sc[3 * t + 2];
+            const u64 slot = g_insert(a, key);
+            if (slot == ~0ull) continue;  // overflow: the run repeats with a larger table
+            word_update(a, agg, slot, h2v, nfirst);
+            const u64 id = slot + 1;
+            u32 h = (u32)(((id * 0x9E3779B97F4A7C15ull) >> 32) % rcap);
+            for (;;) {
+                const u64 v = rt[h];
+                if (v == 0) { rt[h] = (id << 32) | 1u; list[nd++] = h; break; }
+                if ((v >> 32) == id) { rt[h] = v + 1; break; }
+                h = h + 1 == rcap ? 0 : h + 1;
+            }
+        }
+        for (u32 k = 0; k < nd; ++k) sc[tmax + k] = rt[list[k]];
+    }
     atomicAdd((unsigned long long *)&agg.rows[0], 1ull);
     if (f <= a.need) wcs_err(a.ctr, r, E_SHORT);
     a.nd[r] = nd;
     if (nd) {
         atomicAdd((unsigned long long *)&agg.rows[1], 1ull);
-        atomicAdd((unsigned long long *)&agg.rows[2], (unsigned long long)ntok);
+        atomicAdd((unsigned long long *)&agg.rows[2], (unsigned long long)ntok);  // counted tokens
     }
     u64 *o = a.spans + r * 4;
     o[0] = sp[0]; o[1] = sp[1]; o[2] = sp[2]; o[3] = sp[3];
@@ -586,7 +602,7 @@ __global__ __launch_bounds__(256) void k_wcs_wordblob(const u8 *__restrict__ buf
     if (j != off[i + 1]) atomicAdd((unsigned long long *)&ctr->collision, 1ull);
 }
 
-// by-song lines of row r at poff[r] + order: (rank << 32) | count
+// by-song lines of row r at poff[r] + k: (rank << 32) | count
 __global__ __launch_bounds__(256) void k_wcs_pairs(const u64 *__restrict__ rend, u64 nrows,
                                                    const u64 *__restrict__ nd, const u64 *__restrict__ poff,
                                                    const u64 *__restrict__ scratch, const u32 *__restrict__ rank_of,
@@ -594,14 +610,12 @@ __global__ __launch_bounds__(256) void k_wcs_pairs(const u64 *__restrict__ rend,
     const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x + 2;
     if (r >= nrows || nd[r] == 0) return;
     const u64 rs = rend[r - 1], re = rend[r];
-    const u32 rcap = (u32)((re - rs) / 2 + 2);
-    const u64 *rt = scratch + rs;
+    const u64 *c = scratch + 3 * rs + ((re - rs) / 4 + 1);
     u64 *o = pairs + poff[r];
-    for (u32 k = 0; k < rcap; ++k) {
-        const u64 v = rt[k];
-        if (!v) continue;
-        const u64 id = v >> 32;
-        o[(v >> 16) & 0xFFFFu] = ((u64)rank_of[id - 1] << 32) | (v & 0xFFFFu);
+    const u64 m = nd[r];
+    for (u64 k = 0; k < m; ++k) {
+        const u64 v = c[k];
+        o[k] = ((u64)rank_of[(v >> 32) - 1] << 32) | (v & 0xFFFFFFFFu);
     }
 }
 
@@ -634,7 +648,8 @@ struct msa_wcs {
     u64 gbits = 0;  // global table size of the next run (log2), 0 = auto
     bool have = false;
     // scratch owned by the run
-    void *scr[24] = {nullptr};
+    void *scr[24] = {nullptr};  // grow-only pool: buffers persist across runs
+    u64 scr_cap[24] = {0};
 };
 
 static int wfail(msa_wcs *w, int code, const char *fmt, ...) {
@@ -663,13 +678,25 @@ static hipError_t walloc(T *&p, u64 bytes) {
     return e;
 }
 
-static void wcs_release_results(msa_wcs *w) {
-    void **ps[] = {(void **)&w->d_counts, (void **)&w->d_woff, (void **)&w->d_blob, (void **)&w->d_pairs,
-                   (void **)&w->d_nd, (void **)&w->d_spans};
-    for (void **p : ps) wfree(*p);
-    for (auto &p : w->scr) wfree(p);
-    w->have = false;
+// Pool slot k holds at least `bytes` (contents not preserved on growth).
+template <typename T>
+static hipError_t wpool(msa_wcs *w, int k, u64 bytes, T *&p) {
+    if (bytes == 0) bytes = 16;
+    if (w->scr_cap[k] < bytes) {
+        wfree(w->scr[k]);
+        w->scr_cap[k] = 0;
+        hipError_t e = hipMalloc(&w->scr[k], bytes);
+        if (e != hipSuccess) {
+            w->scr[k] = nullptr;
+            return e;
+        }
+        w->scr_cap[k] = bytes;
+    }
+    p = (T *)w->scr[k];
+    return hipSuccess;
 }
+
+static void wcs_release_results(msa_wcs *w) { w->have = false; }
 
 extern "C" int msa_wcs_create(int device, msa_wcs **out) {
     if (!out) return MSA_ERR_ARG;
@@ -691,7 +718,7 @@ extern "C" void msa_wcs_destroy(msa_wcs *w) {
     if (!w) return;
     (void)hipSetDevice(w->device);
     (void)hipStreamSynchronize(w->stream);
-    wcs_release_results(w);
+    for (auto &p : w->scr) wfree(p);
     wfree((void *&)w->d_buf);
     wfree((void *&)w->d_rend);
     (void)hipStreamDestroy(w->stream);
@@ -807,8 +834,7 @@ extern "C" int msa_wcs_run(msa_wcs *w) {
     const u8 *buf = w->d_buf;
     const u64 n = w->n;
     WCtr *ctr;
-    WCHECK(walloc(ctr, sizeof(WCtr)));
-    w->scr[0] = ctr;
+    WCHECK(wpool(w, 0, sizeof(WCtr), ctr));
     WCtr h0{};
     h0.err = ~0ull;
     WCHECK(hipMemcpyAsync(ctr, &h0, sizeof h0, hipMemcpyHostToDevice, st));
@@ -827,14 +853,14 @@ extern "C" int msa_wcs_run(msa_wcs *w) {
         const u64 nb = (nseg + BSEG - 1) / BSEG;
         u32 *map, *bmap, *sstate, *dfin;
         u64 *cnt6, *cnt, *roff, *bsum, *total;
-        WCHECK(walloc(map, nseg * 4)); w->scr[1] = map;
-        WCHECK(walloc(cnt6, nseg * 8)); w->scr[2] = cnt6;
-        WCHECK(walloc(cnt, nseg * 8)); w->scr[3] = cnt;
-        WCHECK(walloc(roff, nseg * 8)); w->scr[4] = roff;
-        WCHECK(walloc(bmap, nb * 4 + 16)); w->scr[5] = bmap;
-        WCHECK(walloc(sstate, nseg * 4)); w->scr[6] = sstate;
-        WCHECK(walloc(bsum, (nseg / 1024 + 2) * 8)); w->scr[7] = bsum;
-        WCHECK(walloc(total, 16)); w->scr[8] = total;
+        WCHECK(wpool(w, 1, nseg * 4, map));
+        WCHECK(wpool(w, 2, nseg * 8, cnt6));
+        WCHECK(wpool(w, 3, nseg * 8, cnt));
+        WCHECK(wpool(w, 4, nseg * 8, roff));
+        WCHECK(wpool(w, 5, nb * 4 + 16, bmap));
+        WCHECK(wpool(w, 6, nseg * 4, sstate));
+        WCHECK(wpool(w, 7, (nseg / 1024 + 2) * 8, bsum));
+        WCHECK(wpool(w, 8, 16, total));
         dfin = bmap + nb;
         hipLaunchKernelGGL(k_wcs_map, grid1(nseg), dim3(256), 0, st, buf, ds, n, nseg, map, cnt6);
         hipLaunchKernelGGL(k_wcs_state_block, dim3((u32)nb), dim3(BLK), 0, st, (const u32 *)map, nseg, bmap);
@@ -879,11 +905,11 @@ extern "C" int msa_wcs_run(msa_wcs *w) {
     // ---- per-row pass: d_rend[0] = ds, d_rend[k + 1] = end of file row k;
     // per-row arrays are indexed by k + 1 (the header is index 1)
     const u64 R = nrows + 1;
-    WCHECK(walloc(w->d_nd, R * 8));
-    WCHECK(walloc(w->d_spans, R * 32));
+    WCHECK(wpool(w, 18, R * 8, w->d_nd));
+    WCHECK(wpool(w, 19, R * 32, w->d_spans));
     WCHECK(hipMemsetAsync(w->d_nd, 0, R * 8, st));
     u64 *scratch;
-    WCHECK(walloc(scratch, (n + 64) * 8)); w->scr[9] = scratch;
+    WCHECK(wpool(w, 9, (3 * n + 64) * 8, scratch));
     u64 bits = w->gbits;
     if (!bits) {
         bits = 16;
@@ -892,8 +918,7 @@ extern "C" int msa_wcs_run(msa_wcs *w) {
     u64 *gtab = nullptr;
     for (;;) {
         const u64 slots = 1ull << bits;
-        wfree(w->scr[10]);
-        WCHECK(walloc(gtab, slots * 32)); w->scr[10] = gtab;
+        WCHECK(wpool(w, 10, slots * 32, gtab));
         WCHECK(hipMemsetAsync(gtab, 0, slots * 32, st));
         WCHECK(hipMemcpyAsync(ctr, &h0, sizeof h0, hipMemcpyHostToDevice, st));
         RowArgs a;
@@ -918,8 +943,8 @@ extern "C" int msa_wcs_run(msa_wcs *w) {
     u32 *V[3];
     u64 *kmem;
     u32 *vmem;
-    WCHECK(walloc(kmem, (nw + 1) * 8 * 9)); w->scr[11] = kmem;
-    WCHECK(walloc(vmem, (nw + 1) * 4 * 3)); w->scr[12] = vmem;
+    WCHECK(wpool(w, 11, (nw + 1) * 8 * 9, kmem));
+    WCHECK(wpool(w, 12, (nw + 1) * 4 * 3, vmem));
     for (int k = 0; k < 3; ++k) {
         K2[k] = kmem + (u64)(3 * k + 0) * (nw + 1);
         K1[k] = kmem + (u64)(3 * k + 1) * (nw + 1);
@@ -932,13 +957,13 @@ extern "C" int msa_wcs_run(msa_wcs *w) {
     WCHECK(msa_launch_sort(K2, K1, K0, V, nw, &which, st));
     const u32 *order = V[which];
     u32 *rank_of;
-    WCHECK(walloc(rank_of, slots * 4)); w->scr[13] = rank_of;
+    WCHECK(wpool(w, 13, slots * 4, rank_of));
     u64 *wlen, *bsum2, *total2;
-    WCHECK(walloc(wlen, (nw + 1) * 8)); w->scr[14] = wlen;
-    WCHECK(walloc(w->d_counts, (nw + 1) * 4));
-    WCHECK(walloc(w->d_woff, (nw + 1) * 8));
-    WCHECK(walloc(bsum2, ((R > nw ? R : nw) / 1024 + 2) * 8)); w->scr[15] = bsum2;
-    WCHECK(walloc(total2, 16)); w->scr[16] = total2;
+    WCHECK(wpool(w, 14, (nw + 1) * 8, wlen));
+    WCHECK(wpool(w, 20, (nw + 1) * 4, w->d_counts));
+    WCHECK(wpool(w, 21, (nw + 1) * 8, w->d_woff));
+    WCHECK(wpool(w, 15, ((R > nw ? R : nw) / 1024 + 2) * 8, bsum2));
+    WCHECK(wpool(w, 16, 16, total2));
     if (nw) {
         hipLaunchKernelGGL(k_wcs_wordlen, grid1(nw), dim3(256), 0, st, buf, (const u64 *)gtab, order, nw, rank_of, wlen,
                            w->d_counts, ctr);
@@ -950,19 +975,19 @@ extern "C" int msa_wcs_run(msa_wcs *w) {
     u64 blob_len = 0;
     WCHECK(hipMemcpyAsync(&blob_len, w->d_woff + nw, 8, hipMemcpyDeviceToHost, st));
     WCHECK(hipStreamSynchronize(st));
-    WCHECK(walloc(w->d_blob, blob_len + 16));
+    WCHECK(wpool(w, 22, blob_len + 16, w->d_blob));
     if (nw)
         hipLaunchKernelGGL(k_wcs_wordblob, grid1(nw), dim3(256), 0, st, buf, (const u64 *)gtab, order, nw,
                            (const u64 *)w->d_woff, w->d_blob, ctr);
 
     // ---- by-song lines
     u64 *poff;
-    WCHECK(walloc(poff, R * 8)); w->scr[17] = poff;
+    WCHECK(wpool(w, 17, R * 8, poff));
     WCHECK(msa_exclusive_scan(w->d_nd, R, poff, bsum2, total2, st));
     u64 np = 0;
     WCHECK(hipMemcpyAsync(&np, total2, 8, hipMemcpyDeviceToHost, st));
     WCHECK(hipStreamSynchronize(st));
-    WCHECK(walloc(w->d_pairs, np * 8 + 16));
+    WCHECK(wpool(w, 23, np * 8 + 16, w->d_pairs));
     if (R > 2)
         hipLaunchKernelGGL(k_wcs_pairs, grid1(R - 2), dim3(256), 0, st, (const u64 *)w->d_rend, R,
                            (const u64 *)w->d_nd, (const u64 *)poff, (const u64 *)scratch, (const u32 *)rank_of,
