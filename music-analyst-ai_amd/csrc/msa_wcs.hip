@@ -309,6 +309,9 @@ struct RowArgs {
     u64 *nd;        // distinct words per row
     u64 *spans;     // 4 per row: artist start/end, song start/end (raw)
     WCtr *ctr;
+    int ablate;     // timing diagnostics only (MSA_WCS_ABLATE): 1 no token loop, 4 no per-row
+                    // table -- results are wrong when set (never skip the word update: the
+                    // ranking kernels read the first-occurrence spans it writes)
 };
 
 __device__ __forceinline__ u64 g_insert(const RowArgs &a, u64 key) {
@@ -472,7 +475,7 @@ __device__ __forceinline__ void wcs_row(const RowArgs &a, WgAgg &agg, u64 r) {
     if (!any) { a.nd[r] = 0; return; }  // blank line: DictReader skips it
     // tokens -> global table (via the workgroup aggregate) and per-row table;
     // every lane runs the same loop, one iteration per token
-    if (ntok) {
+    if (ntok && !(a.ablate & 1)) {
         const u32 rcap = 2 * ntok;
         u64 *rt = sc + 3 * tmax;
         u32 *list = (u32 *)sc;
@@ -482,6 +485,7 @@ __device__ __forceinline__ void wcs_row(const RowArgs &a, WgAgg &agg, u64 r) {
             const u64 slot = g_insert(a, key);
             if (slot == ~0ull) continue;  // overflow: the run repeats with a larger table
             word_update(a, agg, slot, h2v, nfirst);
+            if (a.ablate & 4) continue;
             const u64 id = slot + 1;
             u32 h = (u32)(((id * 0x9E3779B97F4A7C15ull) >> 32) % rcap);
             for (;;) {
@@ -926,6 +930,7 @@ extern "C" int msa_wcs_run(msa_wcs *w) {
         a.ia = ia; a.isg = isg; a.it = it; a.need = need;
         a.gtab = gtab; a.gmask = slots - 1; a.glimit = slots / 4 * 3;
         a.scratch = scratch; a.nd = w->d_nd; a.spans = w->d_spans; a.ctr = ctr;
+        a.ablate = getenv("MSA_WCS_ABLATE") ? atoi(getenv("MSA_WCS_ABLATE")) : 0;
         if (R > 2) hipLaunchKernelGGL(k_wcs_rows, grid1(R - 2), dim3(256), 0, st, a);
         WCHECK(hipGetLastError());
         WCHECK(hipMemcpyAsync(&hc, ctr, sizeof hc, hipMemcpyDeviceToHost, st));
