@@ -53,6 +53,14 @@ constexpr u32 T_O = PK(IF, IF, IF, IQ, IF, EC);    // anything else
 constexpr u32 T_EOL = PK(SR, SR, SR, IQ, SR, SR);  // end of a line
 constexpr u32 MAP_ID = PK(0, 1, 2, 3, 4, 5);
 #undef PK
+// actions per (byte class, state), 2 bits per state: bit 0 = the byte is
+// added to the field, bit 1 = the field is saved (ends) before it
+#define PA(a, b, c, d, e, f) ((a) | ((b) << 2) | ((c) << 4) | ((d) << 6) | ((e) << 8) | ((f) << 10))
+constexpr u32 A_Q = PA(0, 0, 1, 0, 1, 0);
+constexpr u32 A_D = PA(2, 2, 2, 1, 2, 0);
+constexpr u32 A_NL = PA(0, 2, 2, 1, 2, 0);
+constexpr u32 A_O = PA(1, 1, 1, 1, 1, 0);
+#undef PA
 
 constexpr u32 SEG = 256;        // bytes per lane in the map / emit passes
 constexpr u32 BLK = 256;        // threads per block in the state scan
@@ -282,18 +290,41 @@ __host__ __device__ __forceinline__ bool tok_c3(u32 d) { return d >= 0x80 && d <
 __host__ __device__ __forceinline__ u32 low_ascii(u32 c) { return (c >= 'A' && c <= 'Z') ? c + 32 : c; }
 __host__ __device__ __forceinline__ u32 low_c3(u32 d) { return d <= 0x9E ? d + 32 : d; }
 
-constexpr u64 H1_P = 0x100000001b3ull, H1_0 = 0xcbf29ce484222325ull;
-constexpr u64 H2_P = 0x9E3779B97F4A7C15ull, H2_0 = 0x2545F4914F6CDD1Dull;
-__host__ __device__ __forceinline__ u64 h1_step(u64 h, u32 b) { return (h ^ b) * H1_P; }
-__host__ __device__ __forceinline__ u64 h2_step(u64 h, u32 b) { return (h + b + 0x100u) * H2_P ^ (h >> 29); }
-__host__ __device__ __forceinline__ u64 h1_fin(u64 h, u64 len) {
-    const u64 k = fmix64(h ^ (len * 0xD6E8FEB86659FD93ull));
-    return k ? k : 1;
-}
-__host__ __device__ __forceinline__ u64 h2_fin(u64 h, u64 len) {
-    const u64 k = fmix64(h + len);
-    return k ? k : 1;
-}
+// Word hash: bytes are packed 8 at a time into a u64 and absorbed by two
+// independent mixers (h1 = table key, h2 = check); one multiply pair per 8
+// bytes instead of per byte.
+struct TokHash {
+    u64 h1, h2, acc;
+    u32 nacc, len;
+    __host__ __device__ __forceinline__ void reset() {
+        h1 = 0xcbf29ce484222325ull; h2 = 0x2545F4914F6CDD1Dull; acc = 0; nacc = 0; len = 0;
+    }
+    __host__ __device__ __forceinline__ void absorb() {
+        h1 = (h1 ^ acc) * 0x87c37b91114253d5ull;
+        h1 = (h1 << 31) | (h1 >> 33);
+        h2 = (h2 + acc) * 0x9E3779B97F4A7C15ull;
+        h2 ^= h2 >> 32;
+        acc = 0;
+        nacc = 0;
+    }
+    __host__ __device__ __forceinline__ void add(u32 c) {
+        acc |= (u64)c << (8 * nacc);
+        ++len;
+        if (++nacc == 8) absorb();
+    }
+    __host__ __device__ __forceinline__ u64 key() const {  // h1 of the finished word (nonzero)
+        u64 x = h1;
+        if (nacc) { x = (x ^ acc) * 0x87c37b91114253d5ull; x = (x << 31) | (x >> 33); }
+        const u64 k = fmix64(x ^ ((u64)len * 0xD6E8FEB86659FD93ull));
+        return k ? k : 1;
+    }
+    __host__ __device__ __forceinline__ u64 check() const {  // h2 of the finished word (nonzero)
+        u64 x = h2;
+        if (nacc) { x = (x + acc) * 0x9E3779B97F4A7C15ull; x ^= x >> 32; }
+        const u64 k = fmix64(x + len);
+        return k ? k : 1;
+    }
+};
 
 struct RowArgs {
     const u8 *buf;
@@ -386,7 +417,9 @@ __device__ __forceinline__ void wcs_row(const RowArgs &a, WgAgg &agg, u64 r) {
     // tokenizer over the added characters of field `it`
     bool in_tok = false, alnum = false, skip = false;
     u32 cps = 0;
-    u64 h1 = H1_0, h2 = H2_0, tlen = 0, tstart = 0;
+    TokHash th;
+    th.reset();
+    u64 tstart = 0;
     // scratch of this row (u64 units, disjoint from every other row's):
     //   [0, 3*tmax)            token records (h1, h2, ~first) from the byte walk;
     //                          its front is reused as the u32 order->slot list
@@ -400,8 +433,8 @@ __device__ __forceinline__ void wcs_row(const RowArgs &a, WgAgg &agg, u64 r) {
     auto tok_end = [&](u64 end) {
         if (in_tok && cps >= 3 && alnum) {  // record only: the walk stays free of memory round trips
             u64 *t = sc + 3 * (u64)ntok++;
-            t[0] = h1_fin(h1, tlen);
-            t[1] = h2_fin(h2, tlen);
+            t[0] = th.key();
+            t[1] = th.check();
             t[2] = ~((tstart << 20) | (end - tstart));
         }
         in_tok = false;
@@ -425,46 +458,33 @@ __device__ __forceinline__ void wcs_row(const RowArgs &a, WgAgg &agg, u64 r) {
             if (tok_c3(d)) { lo0 = 0xC3; lo1 = low_c3(d); nb = 2; skip = true; }
         }
         if (!nb) { tok_end(i); return; }
-        if (!in_tok) { in_tok = true; alnum = false; cps = 0; h1 = H1_0; h2 = H2_0; tlen = 0; tstart = i; }
-        h1 = h1_step(h1, lo0); h2 = h2_step(h2, lo0); ++tlen;
-        if (nb == 2) { h1 = h1_step(h1, lo1); h2 = h2_step(h2, lo1); ++tlen; }
+        if (!in_tok) { in_tok = true; alnum = false; cps = 0; th.reset(); tstart = i; }
+        th.add(lo0);
+        if (nb == 2) th.add(lo1);
         alnum |= b != '\'';
         ++cps;
     };
 
     for (u64 i = rs; i < re; ++i) {
         const u32 b = rd.get(i);
-        const bool eol = eol_after(b, i + 1 < a.n ? rd.get(i + 1) : 0u, i, a.n);
-        switch (s) {
-            case SR:
-                if (b == '\r' || b == '\n') { s = EC; break; }
-                s = SF;
-                fstart = i;
-                [[fallthrough]];
-            case SF:
-                if (b == '\r' || b == '\n') { save(i); s = EC; }
-                else if (b == '"') s = IQ;
-                else if (b == ',') { save(i); fstart = i + 1; }
-                else { add(i, b); s = IF; }
-                break;
-            case IF:
-                if (b == '\r' || b == '\n') { save(i); s = EC; }
-                else if (b == ',') { save(i); fstart = i + 1; s = SF; }
-                else add(i, b);
-                break;
-            case IQ:
-                if (b == '"') s = QQ;
-                else add(i, b);
-                break;
-            case QQ:
-                if (b == '"') { add(i, b); s = IQ; }
-                else if (b == ',') { save(i); fstart = i + 1; s = SF; }
-                else if (b == '\r' || b == '\n') { save(i); s = EC; }
-                else { add(i, b); s = IF; }
-                break;
-            default:
-                break;  // EC
+        // end of line: after '\n', after '\r' not followed by '\n', after the last byte
+        bool eol = i + 1 == a.n;
+        if (b == '\n') eol = true;
+        else if (b == '\r' && !eol) eol = rd.get(i + 1) != '\n';
+        // one table step instead of a switch: lanes of a wave sit in different
+        // states, and a divergent switch would run every arm (and every inlined
+        // copy of add/save) for the whole wave
+        const u32 cls = b == '"' ? 0u : (b == ',' ? 1u : ((b == '\r' || b == '\n') ? 2u : 3u));
+        const u32 tnext = cls == 0 ? T_Q : (cls == 1 ? T_D : (cls == 2 ? T_NL : T_O));
+        const u32 tact = cls == 0 ? A_Q : (cls == 1 ? A_D : (cls == 2 ? A_NL : A_O));
+        const u32 act = (tact >> (2 * s)) & 3u;
+        if (s == SR && cls != 2) fstart = i;
+        if (act & 2u) {
+            save(i);
+            if (cls == 1) fstart = i + 1;
         }
+        if (act & 1u) add(i, b);
+        s = step(tnext, s);
         if (eol) {
             if (s == SF || s == IF || s == QQ) save(i + 1);
             if (s != IQ) s = SR;
@@ -566,7 +586,8 @@ __global__ __launch_bounds__(256) void k_wcs_wordlen(const u8 *__restrict__ buf,
     const u64 *g = gtab + (u64)slot * 4;
     const u64 fe = ~g[2];
     const u64 pos = fe >> 20, raw = fe & ((1u << 20) - 1);
-    u64 h1 = H1_0, h2 = H2_0, l = 0;
+    TokHash th;
+    th.reset();
     for (u64 k = 0; k < raw; ++k) {
         const u32 b = buf[pos + k];
         if (b == '"') continue;
@@ -574,12 +595,11 @@ __global__ __launch_bounds__(256) void k_wcs_wordlen(const u8 *__restrict__ buf,
         if (b == 0xC3) c = 0xC3;
         else if (k > 0 && buf[pos + k - 1] == 0xC3) c = low_c3(b);
         else c = low_ascii(b);
-        h1 = h1_step(h1, c);
-        h2 = h2_step(h2, c);
-        ++l;
+        th.add(c);
     }
     const u64 cnt = g[3];
-    if (h1_fin(h1, l) != g[0] || h2_fin(h2, l) != g[1])
+    const u64 l = th.len;
+    if (th.key() != g[0] || th.check() != g[1])
         atomicAdd((unsigned long long *)&ctr->collision, 1ull);
     rank_of[slot] = (u32)i;
     len[i] = l;
