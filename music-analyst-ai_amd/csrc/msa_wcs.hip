@@ -395,8 +395,10 @@ __device__ __forceinline__ void word_update(const RowArgs &a, WgAgg &g, u64 slot
         }
         if (cur != id) continue;
         atomicAdd(&g.cnt[h], 1u);
-        atomicMax((unsigned long long *)&g.first[h], (unsigned long long)nfirst);
-        const u64 o = atomicCAS((unsigned long long *)&g.h2[h], 0ull, (unsigned long long)h2v);
+        // first / h2 change rarely: plain LDS reads filter out most atomics
+        if (nfirst > g.first[h]) atomicMax((unsigned long long *)&g.first[h], (unsigned long long)nfirst);
+        u64 o = g.h2[h];
+        if (o == 0) o = atomicCAS((unsigned long long *)&g.h2[h], 0ull, (unsigned long long)h2v);
         if (o != 0 && o != h2v) atomicAdd((unsigned long long *)&g.rows[3], 1ull);
         return;
     }
