@@ -245,6 +245,19 @@ int msa_wcs_get_summary(msa_wcs *w, msa_wcs_summary *out);
 int msa_wcs_get_csv(msa_wcs *w, int which, char **out, size_t *len);
 int msa_wcs_write_outputs(msa_wcs *w, const char *outdir);
 
+/* Column splitter: the GPU part of /root/reference/scripts/split_csv_columns.py
+ * (main 124-199) on the CSV loaded with msa_wcs_load_csv: csv.reader rows
+ * (delimiter ',', quotechar '"'), every column's file body as csv.writer
+ * writes it (lineterminator "\n", QUOTE_MINIMAL) -- rows after the header
+ * (has_header != 0) or all rows.  ncols = fields of the first row.  The
+ * column splitter and msa_wcs_run share the context: running one invalidates
+ * the other's results.  MSA_ERR_NOHEADER = "CSV vazio.".                    */
+int msa_csvcol_run(msa_wcs *w, int has_header, uint64_t *ncols, uint64_t *nrows);
+/* Header field `col` of the first row (unescaped content), malloc'ed. */
+int msa_csvcol_header(msa_wcs *w, uint64_t col, char **out, size_t *len);
+/* Body bytes of column `col`'s file, malloc'ed (release with msa_free). */
+int msa_csvcol_get(msa_wcs *w, uint64_t col, char **out, size_t *len);
+
 #ifdef __cplusplus
 }
 #endif

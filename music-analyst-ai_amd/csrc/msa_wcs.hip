@@ -32,6 +32,7 @@
 #include <string.h>
 
 #include <string>
+#include <vector>
 
 #include "msa_hip.h"
 #include "msa_internal.h"
@@ -645,6 +646,110 @@ __global__ __launch_bounds__(256) void k_wcs_pairs(const u64 *__restrict__ rend,
     }
 }
 
+// ---------------------------------------------------------------------------
+// Column splitter (/root/reference/scripts/split_csv_columns.py main 124-199):
+// csv.reader rows (blank lines are rows with no fields) -> one file body per
+// column, each value written by csv.writer([value]) with lineterminator "\n",
+// QUOTE_MINIMAL: quoted when it holds ',', '"' or '\n' (quotes doubled), and
+// a lone empty value is written as "".  Fields past ncols are dropped, missing
+// ones are "".  Pass 0 computes each (column, row) output length (+ a quoted
+// flag), pass 1 writes the bytes at the scanned offsets (column-major, so the
+// columns end up contiguous one after another).
+struct ColArgs {
+    const u8 *buf;
+    u64 n;
+    const u64 *rend;
+    u64 first, nrows;  // kernel rows [first, nrows)
+    u64 ncols, R;      // R = rows per column block
+    u64 *len;          // [ncols * R]
+    u8 *quoted;        // [ncols * R]
+    const u64 *off;    // [ncols * R] (pass 1)
+    u8 *out;
+    WCtr *ctr;
+};
+
+template <int PASS>
+__global__ __launch_bounds__(256) void k_csvcol(ColArgs a) {
+    const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x + a.first;
+    if (r >= a.nrows) return;
+    const u64 rs = a.rend[r - 1], re = a.rend[r];
+    const u64 j = r - a.first;  // output row
+    ByteReader rd(a.buf);
+    u32 s = SR, chars = 0;
+    u64 f = 0, clen = 0;
+    bool special = false, limit = false;
+    u8 *dst = nullptr;
+    bool q = false;
+    auto open_field = [&]() {
+        clen = 0;
+        special = false;
+        if (PASS == 1 && f < a.ncols) {
+            const u64 k = f * a.R + j;
+            dst = a.out + a.off[k];
+            q = a.quoted[k] != 0;
+            if (q) *dst++ = '"';
+        }
+    };
+    auto save = [&]() {
+        if (f < a.ncols) {
+            if (PASS == 0) {
+                const u64 k = f * a.R + j;
+                const bool qq = special || clen == 0;  // clen already counts doubled quotes
+                a.len[k] = qq ? clen + 3 : clen + 1;
+                a.quoted[k] = qq;
+            } else {
+                if (q) *dst++ = '"';
+                *dst++ = '\n';
+            }
+        }
+        ++f;
+        chars = 0;
+        open_field();
+    };
+    open_field();
+    bool any = false;
+    for (u64 i = rs; i < re; ++i) {
+        const u32 b = rd.get(i);
+        bool eol = i + 1 == a.n;
+        if (b == '\n') eol = true;
+        else if (b == '\r' && !eol) eol = rd.get(i + 1) != '\n';
+        const u32 cls = b == '"' ? 0u : (b == ',' ? 1u : ((b == '\r' || b == '\n') ? 2u : 3u));
+        const u32 tnext = cls == 0 ? T_Q : (cls == 1 ? T_D : (cls == 2 ? T_NL : T_O));
+        const u32 tact = cls == 0 ? A_Q : (cls == 1 ? A_D : (cls == 2 ? A_NL : A_O));
+        const u32 act = (tact >> (2 * s)) & 3u;
+        if (act & 2u) { save(); any = true; }
+        if (act & 1u) {
+            if ((b & 0xC0) != 0x80 && ++chars > FIELD_LIMIT) limit = true;
+            if (f < a.ncols) {
+                if (PASS == 0) {
+                    clen += 1 + (b == '"');  // a quote is doubled if the value is quoted
+                    special |= b == ',' || b == '"' || b == '\n';
+                } else {
+                    *dst++ = (u8)b;
+                    if (q && b == '"') *dst++ = '"';
+                }
+            }
+        }
+        s = step(tnext, s);
+        if (eol) {
+            if (s == SF || s == IF || s == QQ) { save(); any = true; }
+            if (s != IQ) s = SR;
+        }
+    }
+    if (s == IQ) { save(); any = true; }
+    if (PASS == 0 && limit) wcs_err(a.ctr, r, E_LIMIT);
+    (void)any;
+    // missing fields (and every field of a blank row) are ""
+    for (; f < a.ncols; ++f) {
+        const u64 k = f * a.R + j;
+        if (PASS == 0) { a.len[k] = 3; a.quoted[k] = 1; }
+        else {
+            u8 *d = a.out + a.off[k];
+            d[0] = '"'; d[1] = '"'; d[2] = '\n';
+        }
+    }
+}
+
 inline dim3 grid1(u64 n, u32 t = 256) { return dim3((u32)((n + t - 1) / t)); }
 
 }  // namespace
@@ -673,6 +778,12 @@ struct msa_wcs {
     msa_wcs_summary sum{};
     u64 gbits = 0;  // global table size of the next run (log2), 0 = auto
     bool have = false;
+    // column splitter results
+    u64 cc_ncols = 0, cc_rows = 0;
+    std::vector<std::string> cc_hdr;
+    u64 *d_ccoff = nullptr;  // [ncols * rows + 1]
+    u8 *d_ccout = nullptr;
+    bool cc_have = false;
     // scratch owned by the run
     void *scr[24] = {nullptr};  // grow-only pool: buffers persist across runs
     u64 scr_cap[24] = {0};
@@ -722,7 +833,7 @@ static hipError_t wpool(msa_wcs *w, int k, u64 bytes, T *&p) {
     return hipSuccess;
 }
 
-static void wcs_release_results(msa_wcs *w) { w->have = false; }
+static void wcs_release_results(msa_wcs *w) { w->have = false; w->cc_have = false; }
 
 extern "C" int msa_wcs_create(int device, msa_wcs **out) {
     if (!out) return MSA_ERR_ARG;
@@ -852,10 +963,9 @@ static int wcs_input_error(msa_wcs *w, u64 e) {
     }
 }
 
-extern "C" int msa_wcs_run(msa_wcs *w) {
-    if (!w || !w->d_buf) return MSA_ERR_ARG;
-    WCHECK(hipSetDevice(w->device));
-    wcs_release_results(w);
+// Validation + row ends of the loaded CSV (shared by the per-song counter and
+// the column splitter).  d_rend[0] = ds, d_rend[k + 1] = end of file row k.
+static int wcs_split_rows(msa_wcs *w, WCtr **ctr_out, u64 *ds_out, u64 *nrows_out) {
     hipStream_t st = w->stream;
     const u8 *buf = w->d_buf;
     const u64 n = w->n;
@@ -914,7 +1024,28 @@ extern "C" int msa_wcs_run(msa_wcs *w) {
     WCHECK(hipMemcpyAsync(&hc, ctr, sizeof hc, hipMemcpyDeviceToHost, st));
     WCHECK(hipStreamSynchronize(st));
     if (hc.err != ~0ull) return wcs_input_error(w, hc.err);
+    *ctr_out = ctr;
+    *ds_out = ds;
+    *nrows_out = nrows;
+    return MSA_OK;
+}
+
+
+extern "C" int msa_wcs_run(msa_wcs *w) {
+    if (!w || !w->d_buf) return MSA_ERR_ARG;
+    WCHECK(hipSetDevice(w->device));
+    wcs_release_results(w);
+    hipStream_t st = w->stream;
+    const u8 *buf = w->d_buf;
+    const u64 n = w->n;
+    WCtr *ctr;
+    u64 ds = 0, nrows = 0;
+    int rc0 = wcs_split_rows(w, &ctr, &ds, &nrows);
+    if (rc0) return rc0;
     if (nrows == 0) return wfail(w, MSA_ERR_BADHEADER, "CSV sem colunas esperadas. Campos necessários: artist, song, text.");
+    WCtr h0{};
+    h0.err = ~0ull;
+    WCtr hc{};
 
     // ---- header (host)
     u64 he = 0;
@@ -1198,5 +1329,108 @@ extern "C" int msa_wcs_write_outputs(msa_wcs *w, const char *outdir) {
         free(d);
         if (fclose(f) != 0 || !ok) return wfail(w, MSA_ERR_IO, "write failed: %s", path);
     }
+    return MSA_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Column splitter host side.
+static void row_fields(const u8 *h, u64 len, std::vector<std::string> &out) {
+    out.clear();
+    std::string fld;
+    u32 s = SR;
+    for (u64 i = 0; i < len; ++i) {
+        const u32 b = h[i];
+        const bool eol = b == '\n' || (b == '\r' && (i + 1 >= len || h[i + 1] != '\n')) || i + 1 == len;
+        const u32 cls = b == '"' ? 0u : (b == ',' ? 1u : ((b == '\r' || b == '\n') ? 2u : 3u));
+        const u32 tnext = cls == 0 ? T_Q : (cls == 1 ? T_D : (cls == 2 ? T_NL : T_O));
+        const u32 tact = cls == 0 ? A_Q : (cls == 1 ? A_D : (cls == 2 ? A_NL : A_O));
+        const u32 act = (tact >> (2 * s)) & 3u;
+        if (act & 2u) { out.push_back(fld); fld.clear(); }
+        if (act & 1u) fld.push_back((char)b);
+        s = step(tnext, s);
+        if (eol) {
+            if (s == SF || s == IF || s == QQ) { out.push_back(fld); fld.clear(); }
+            if (s != IQ) s = SR;
+        }
+    }
+    if (s == IQ) out.push_back(fld);
+}
+
+extern "C" int msa_csvcol_run(msa_wcs *w, int has_header, uint64_t *ncols, uint64_t *nrows) {
+    if (!w || !w->d_buf || !ncols || !nrows) return MSA_ERR_ARG;
+    WCHECK(hipSetDevice(w->device));
+    w->cc_have = false;
+    w->have = false;  // the two paths share the context's buffer pool
+    hipStream_t st = w->stream;
+    WCtr *ctr;
+    u64 ds = 0, nr = 0;
+    int rc = wcs_split_rows(w, &ctr, &ds, &nr);
+    if (rc) return rc;
+    if (nr == 0) return wfail(w, MSA_ERR_NOHEADER, "CSV vazio.");
+    u64 he = 0;
+    WCHECK(hipMemcpy(&he, w->d_rend + 1, 8, hipMemcpyDeviceToHost));
+    std::vector<u8> hb(he - ds + 1);
+    if (he > ds) WCHECK(hipMemcpy(hb.data(), w->d_buf + ds, he - ds, hipMemcpyDeviceToHost));
+    row_fields(hb.data(), he - ds, w->cc_hdr);
+    const u64 nc = w->cc_hdr.size();
+    const u64 first = has_header ? 2 : 1;  // kernel row index of the first data row
+    const u64 R = nr + 1 - first;
+    const u64 cells = nc * R;
+    u64 *len, *bsum, *total;
+    u8 *quoted;
+    WCHECK(wpool(w, 9, (cells + 1) * 8, len));
+    WCHECK(wpool(w, 1, cells + 16, quoted));
+    WCHECK(wpool(w, 17, (cells + 1) * 8, w->d_ccoff));
+    WCHECK(wpool(w, 15, (cells / 1024 + 2) * 8, bsum));
+    WCHECK(wpool(w, 16, 16, total));
+    ColArgs a;
+    a.buf = w->d_buf; a.n = w->n; a.rend = w->d_rend; a.first = first; a.nrows = nr + 1;
+    a.ncols = nc; a.R = R; a.len = len; a.quoted = quoted; a.off = w->d_ccoff; a.out = nullptr; a.ctr = ctr;
+    if (cells) {
+        hipLaunchKernelGGL(k_csvcol<0>, grid1(R), dim3(256), 0, st, a);
+        WCHECK(msa_exclusive_scan(len, cells, w->d_ccoff, bsum, total, st));
+        WCHECK(hipMemcpyAsync(w->d_ccoff + cells, total, 8, hipMemcpyDeviceToDevice, st));
+    } else {
+        WCHECK(hipMemsetAsync(w->d_ccoff, 0, 8, st));
+    }
+    u64 outlen = 0;
+    WCHECK(hipMemcpyAsync(&outlen, w->d_ccoff + cells, 8, hipMemcpyDeviceToHost, st));
+    WCtr hc{};
+    WCHECK(hipMemcpyAsync(&hc, ctr, sizeof hc, hipMemcpyDeviceToHost, st));
+    WCHECK(hipStreamSynchronize(st));
+    if (hc.err != ~0ull) return wcs_input_error(w, hc.err);
+    WCHECK(wpool(w, 22, outlen + 16, w->d_ccout));
+    a.out = w->d_ccout;
+    if (cells) hipLaunchKernelGGL(k_csvcol<1>, grid1(R), dim3(256), 0, st, a);
+    WCHECK(hipGetLastError());
+    WCHECK(hipStreamSynchronize(st));
+    w->cc_ncols = nc;
+    w->cc_rows = R;
+    w->cc_have = true;
+    *ncols = nc;
+    *nrows = R;
+    return MSA_OK;
+}
+
+extern "C" int msa_csvcol_header(msa_wcs *w, uint64_t col, char **out, size_t *len) {
+    if (!w || !w->cc_have || col >= w->cc_ncols || !out || !len) return MSA_ERR_ARG;
+    const std::string &h = w->cc_hdr[col];
+    char *p = (char *)malloc(h.size() + 1);
+    memcpy(p, h.data(), h.size());
+    *out = p;
+    *len = h.size();
+    return MSA_OK;
+}
+
+extern "C" int msa_csvcol_get(msa_wcs *w, uint64_t col, char **out, size_t *len) {
+    if (!w || !w->cc_have || col >= w->cc_ncols || !out || !len) return MSA_ERR_ARG;
+    WCHECK(hipSetDevice(w->device));
+    u64 o[2];
+    WCHECK(hipMemcpy(&o[0], w->d_ccoff + col * w->cc_rows, 8, hipMemcpyDeviceToHost));
+    WCHECK(hipMemcpy(&o[1], w->d_ccoff + (col + 1) * w->cc_rows, 8, hipMemcpyDeviceToHost));
+    char *p = (char *)malloc(o[1] - o[0] + 1);
+    if (o[1] > o[0]) WCHECK(hipMemcpy(p, w->d_ccout + o[0], o[1] - o[0], hipMemcpyDeviceToHost));
+    *out = p;
+    *len = o[1] - o[0];
     return MSA_OK;
 }

@@ -45,6 +45,7 @@ EXPORTS = [
     "msa_segment_set", "msa_export_partitions", "msa_export_copy", "msa_import_partitions",
     "msa_wcs_create", "msa_wcs_destroy", "msa_wcs_last_error", "msa_wcs_stream", "msa_wcs_load_csv",
     "msa_wcs_set_table_bits", "msa_wcs_run", "msa_wcs_get_summary", "msa_wcs_get_csv", "msa_wcs_write_outputs",
+    "msa_csvcol_run", "msa_csvcol_header", "msa_csvcol_get",
 ]
 MSA_WCS_GLOBAL = 0
 MSA_WCS_BY_SONG = 1
@@ -157,6 +158,9 @@ def load(path: str = LIB_PATH):
     lib.msa_wcs_get_summary.argtypes = [vp, C.POINTER(_WcsSummary)]
     lib.msa_wcs_get_csv.argtypes = [vp, i, C.POINTER(C.c_void_p), C.POINTER(sz)]
     lib.msa_wcs_write_outputs.argtypes = [vp, C.c_char_p]
+    lib.msa_csvcol_run.argtypes = [vp, i, C.POINTER(u64), C.POINTER(u64)]
+    lib.msa_csvcol_header.argtypes = [vp, u64, C.POINTER(C.c_void_p), C.POINTER(sz)]
+    lib.msa_csvcol_get.argtypes = [vp, u64, C.POINTER(C.c_void_p), C.POINTER(sz)]
     _lib = lib
     return lib
 
@@ -396,6 +400,27 @@ class WordCountPerSong:
 
     def write_outputs(self, outdir: str):
         self._check(self.lib.msa_wcs_write_outputs(self.h, outdir.encode()))
+
+    # ---- column splitter (split_csv_columns.py), same context
+    def split_columns(self, has_header: bool = True) -> Tuple[int, int]:
+        nc, nr = C.c_uint64(), C.c_uint64()
+        self._check(self.lib.msa_csvcol_run(self.h, int(has_header), C.byref(nc), C.byref(nr)))
+        return nc.value, nr.value
+
+    def _take(self, fn, col: int) -> bytes:
+        out = C.c_void_p()
+        n = C.c_size_t()
+        self._check(fn(self.h, col, C.byref(out), C.byref(n)))
+        try:
+            return C.string_at(out, n.value)
+        finally:
+            self.lib.msa_free(out)
+
+    def column_header(self, col: int) -> bytes:
+        return self._take(self.lib.msa_csvcol_header, col)
+
+    def column_body(self, col: int) -> bytes:
+        return self._take(self.lib.msa_csvcol_get, col)
 
     def run(self, data: bytes) -> Tuple[int, bytes, bytes]:
         self.load_csv(data)
