@@ -1,0 +1,102 @@
+"""split_csv_columns on the GPU: host mirror of
+/root/reference/scripts/split_csv_columns.py (same arguments, file naming,
+output bytes and messages) whose data path -- CSV record/field splitting and
+the per-column csv.writer bytes -- runs in libmsa_hip (msa_csvcol_*,
+csrc/msa_wcs.hip).  File naming and the final writes stay on the host, as in
+the script (sanitize_filename 24-28, the name loop 159-174).
+
+    python -m msa.split_columns data.csv [--output-dir D] [--delimiter ,]
+           [--quotechar '"'] [--encoding utf-8-sig] [--no-header] [--force]
+
+Only ',' / '"' are implemented (an explicit --delimiter is required to skip
+csv.Sniffer, 46-66, whose guess the GPU path does not reproduce).
+"""
+from __future__ import annotations
+
+import argparse
+import re
+from pathlib import Path
+from typing import List, Optional
+
+from . import WordCountPerSong
+
+
+def sanitize_filename(name: str, max_len: int = 80) -> str:
+    """split_csv_columns.py:24-28: newlines to spaces, strip, runs of
+    characters outside [\\w\\-. ] to '_', whitespace runs to '_', cut to 80."""
+    s = (name or "").replace("\n", " ").replace("\r", " ").strip()
+    s = re.sub(r"[^\w\-. ]+", "_", s, flags=re.UNICODE)
+    s = re.sub(r"\s+", "_", s)
+    return (s or "col")[:max_len]
+
+
+def _header_line(h: str) -> str:
+    if h == "" or any(c in h for c in ',"\n'):
+        return '"' + h.replace('"', '""') + '"\n'
+    return h + "\n"
+
+
+def split_csv_columns(csv_path: str, output_dir: Optional[str] = None, delimiter: Optional[str] = None,
+                      quotechar: str = '"', encoding: str = "utf-8-sig", no_header: bool = False,
+                      force: bool = False, device: int = 0) -> List[Path]:
+    in_path = Path(csv_path)
+    if not in_path.exists():
+        raise SystemExit(f"Erro: arquivo não encontrado: {in_path}")
+    if delimiter != "," or quotechar != '"':
+        raise SystemExit("only --delimiter ',' with quotechar '\"' is implemented on the GPU path")
+    if encoding.lower().replace("_", "-") not in ("utf-8-sig", "utf-8", "utf8"):
+        raise SystemExit("only UTF-8 input is implemented on the GPU path")
+    base_out = Path(output_dir) if output_dir else in_path.with_suffix("").parent / f"{in_path.stem}_columns"
+    base_out.mkdir(parents=True, exist_ok=True)
+    data = in_path.read_bytes()
+    with WordCountPerSong(device) as w:
+        w.load_csv(data)
+        try:
+            ncols, _ = w.split_columns(has_header=not no_header)
+        except Exception as e:  # MSA_ERR_NOHEADER carries the script's message
+            if "CSV vazio" in str(e):
+                raise SystemExit("CSV vazio.")
+            raise
+        if no_header:
+            headers = [f"col{i + 1}" for i in range(ncols)]
+        else:
+            raw = [w.column_header(i).decode("utf-8") for i in range(ncols)]
+            headers = [h if h.strip() else f"col{i + 1}" for i, h in enumerate(raw)]
+        seen, names = set(), []
+        for i, h in enumerate(headers, start=1):
+            name = sanitize_filename(str(h)) or f"col{i}"
+            cand, k = f"{name}.csv", 2
+            while cand.lower() in seen or ((base_out / cand).exists() and not force):
+                cand = f"{name}_{k}.csv"
+                k += 1
+            seen.add(cand.lower())
+            names.append(cand)
+        bom = "﻿".encode("utf-8") if encoding.lower().replace("_", "-") == "utf-8-sig" else b""
+        for i in range(ncols):
+            with open(base_out / names[i], "wb") as fh:
+                fh.write(bom)
+                if not no_header:
+                    fh.write(_header_line(headers[i]).encode("utf-8"))
+                fh.write(w.column_body(i))
+    print(f"Concluído. {ncols} arquivo(s) gerado(s) em: {base_out}")
+    for name in names:
+        print(f" - {base_out / name}")
+    return [base_out / n for n in names]
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description="Split a CSV into one file per column (GPU data path).")
+    ap.add_argument("csv_path")
+    ap.add_argument("--output-dir", dest="output_dir", default=None)
+    ap.add_argument("--delimiter", dest="delimiter", default=None)
+    ap.add_argument("--quotechar", dest="quotechar", default='"')
+    ap.add_argument("--encoding", dest="encoding", default="utf-8-sig")
+    ap.add_argument("--no-header", dest="no_header", action="store_true")
+    ap.add_argument("--force", dest="force", action="store_true")
+    ap.add_argument("--device", type=int, default=0)
+    a = ap.parse_args(argv)
+    split_csv_columns(a.csv_path, a.output_dir, a.delimiter, a.quotechar, a.encoding, a.no_header, a.force, a.device)
+
+
+if __name__ == "__main__":
+    main()

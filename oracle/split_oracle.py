@@ -1,0 +1,51 @@
+"""CPU oracle for the column splitter -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/ may use this module, and only as the checker; the product path
+(libmsa_hip's msa_csvcol_* entry points, driven by msa/split_columns.py)
+never calls it.
+
+Restates the data part of /root/reference/scripts/split_csv_columns.py
+main (124-199) for an explicit ',' delimiter and '"' quotechar:
+* rows: CPython 3.10 csv.reader (wcs_oracle.csv_rows -- the same _csv state
+  machine; blank lines are rows with no fields, csv.reader yields them);
+* columns: len(first row); each later row contributes row[i] or "" (175-178);
+* each value is written by csv.writer(lineterminator="\\n", QUOTE_MINIMAL)
+  as a one-field row: quoted (quotes doubled) when it holds ',', '"' or
+  '\\n' ('\\r' is NOT quoted with this lineterminator), and a lone empty value
+  is written as "".
+
+Parity: pinned against outputs of the real script in tests/golden/split/
+(tests/golden/make_split_golden.py).
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from wcs_oracle import WcsError, _utf8_check, csv_rows  # noqa: E402,F401
+
+
+def write_value(v: bytes) -> bytes:
+    """csv.writer(...).writerow([v]) with lineterminator '\\n', QUOTE_MINIMAL."""
+    if v == b"" or any(c in v for c in b',"\n'):
+        return b'"' + v.replace(b'"', b'""') + b'"\n'
+    return v + b"\n"
+
+
+def split_columns(data: bytes, has_header: bool = True):
+    """-> (first-row fields, [body bytes of column i]) ; raises WcsError / ValueError("CSV vazio.")."""
+    _utf8_check(data)
+    rows = csv_rows(data)
+    first = next(rows, None)
+    if first is None:
+        raise ValueError("CSV vazio.")
+    nc = len(first)
+    bodies = [[] for _ in range(nc)]
+    if not has_header:
+        for i in range(nc):
+            bodies[i].append(write_value(first[i]))
+    for row in rows:
+        for i in range(nc):
+            bodies[i].append(write_value(row[i] if i < len(row) else b""))
+    return first, [b"".join(b) for b in bodies]

@@ -1,0 +1,75 @@
+#!/usr/bin/env python3
+"""Golden vectors for the column splitter (DESIGN.md row f, second script).
+
+Runs the REAL reference script /root/reference/scripts/split_csv_columns.py
+(in this container only) on deterministic inputs and stores, per case under
+tests/golden/split/<case>/: input.csv, args.txt, the output files under out/
+(names as the script chose them) and stdout.txt -- or error.txt when the
+script exits non-zero.
+
+    python tests/golden/make_split_golden.py
+"""
+import os
+import random
+import shutil
+import subprocess
+import sys
+import tempfile
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+OUT = os.path.join(HERE, "split")
+REF = "/root/reference/scripts/split_csv_columns.py"
+sys.path.insert(0, HERE)
+
+
+def cases():
+    from make_wcs_golden import hand_cases, torture
+
+    c = {}
+    for k, (text, _) in hand_cases().items():
+        c[k] = (text, ["--delimiter", ","])
+    c["no_header"] = ("a,b,c\n1,2\n\n4,5,6,7\n", ["--delimiter", ",", "--no-header"])
+    c["blank_first_no_header"] = ("\nx,y\n", ["--delimiter", ",", "--no-header"])
+    c["dup_and_blank_headers"] = ("a b,a b,  ,A B,é/x\n1,2,3,4,5\n\"q,\"\"r\",\"\",x\ry,\"m\nn\",\n", ["--delimiter", ","])
+    c["cr_values"] = ("h1,h2\n\"a\rb\",c\n", ["--delimiter", ","])
+    for s in range(4):
+        c[f"torture_{s}"] = (torture(500 + s, 120), ["--delimiter", ","])
+    rnd = random.Random(9)
+    rows = ["artist,song,link,text"]
+    words = ["la", "love", "x,y", 'q""q', "nl\nnl"]
+    for i in range(300):
+        lyric = " ".join(rnd.choice(words) for _ in range(rnd.randint(0, 9)))
+        rows.append("A%d,S%d,/l/%d,\"%s\"" % (rnd.randint(0, 40), i, i, lyric))
+    c["lyrics_300"] = ("\n".join(rows) + "\n", ["--delimiter", ","])
+    return c
+
+
+def main():
+    if os.path.isdir(OUT):
+        shutil.rmtree(OUT)
+    os.makedirs(OUT)
+    for name, (text, args) in sorted(cases().items()):
+        d = os.path.join(OUT, name)
+        os.makedirs(d)
+        data = text.encode("utf-8")
+        with open(os.path.join(d, "input.csv"), "wb") as f:
+            f.write(data)
+        with open(os.path.join(d, "args.txt"), "w") as f:
+            f.write(" ".join(args))
+        with tempfile.TemporaryDirectory() as tmp:
+            od = os.path.join(tmp, "cols")
+            r = subprocess.run([sys.executable, REF, os.path.join(d, "input.csv"), "--output-dir", od] + args,
+                               capture_output=True, text=True)
+            if r.returncode != 0:
+                with open(os.path.join(d, "error.txt"), "w") as f:
+                    f.write((r.stderr.strip().splitlines() or ["error"])[-1] + "\n")
+                print(f"{name}: reference error: {(r.stderr.strip().splitlines() or ['?'])[-1]}")
+                continue
+            shutil.copytree(od, os.path.join(d, "out"))
+            with open(os.path.join(d, "stdout.txt"), "w") as f:
+                f.write(r.stdout.splitlines()[0].split(" arquivo")[0] + "\n")
+            print(f"{name}: {sorted(os.listdir(od))}")
+
+
+if __name__ == "__main__":
+    main()
