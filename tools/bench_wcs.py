@@ -27,7 +27,11 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--path", choices=["wcs", "split"], default="wcs",
+                    help="wcs: msa_wcs_run (per-song counts); split: msa_csvcol_run (column files in HBM)")
     a = ap.parse_args()
+    if a.path == "split":
+        return bench_split(a)
     data = msa.gen_corpus(a.songs, mode="zipf", seed=1)
     n = len(data)
     with msa.WordCountPerSong(0) as w:
@@ -57,6 +61,35 @@ def main():
         out["cpu_baseline"] = {"value": round(len(sample) / ct / 1e9, 6), "unit": "GB/s", "cores": 1, "kind": "port",
                                "seconds": round(ct, 3),
                                "sample": f"20000 songs, {len(sample)} bytes, oracle/wcs_oracle.py (pure Python)"}
+    print(json.dumps(out), flush=True)
+
+
+def bench_split(a):
+    data = msa.gen_corpus(a.songs, mode="zipf", seed=1)
+    n = len(data)
+    with msa.WordCountPerSong(0) as w:
+        w.load_csv(data)
+        for _ in range(a.warmup):
+            w.split_columns(True)
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            nc, nr = w.split_columns(True)
+        dt = (time.perf_counter() - t0) / a.steps
+    out = {"metric": "CSV->per-column files GB/s (split_csv_columns.py path)", "value": round(n / dt / 1e9, 3),
+           "unit": "GB/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(dt * 1e3, 3),
+           "higher_is_better": True, "dtype": "u8", "data": "synthetic (csrc/msa_gen.c Zipfian lyric CSV, seed 1)",
+           "config": {"workload": f"{a.songs} songs, {n} bytes, resident in HBM", "columns": nc, "rows": nr}}
+    if not a.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import split_oracle  # checker restatement, timed as the CPU baseline only
+
+        sample = msa.gen_corpus(20000, mode="zipf", seed=1)
+        t0 = time.perf_counter()
+        split_oracle.split_columns(sample, True)
+        ct = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": round(len(sample) / ct / 1e9, 6), "unit": "GB/s", "cores": 1, "kind": "port",
+                               "seconds": round(ct, 3),
+                               "sample": f"20000 songs, {len(sample)} bytes, oracle/split_oracle.py (pure Python)"}
     print(json.dumps(out), flush=True)
 
 
