@@ -678,8 +678,22 @@ __global__ __launch_bounds__(256) void k_csvcol(ColArgs a) {
     u32 s = SR, chars = 0;
     u64 f = 0, clen = 0;
     bool special = false, limit = false;
+    // write combiner: byte stores up to an 8-byte boundary, then whole u64s
     u8 *dst = nullptr;
+    u64 acc = 0;
+    u32 nacc = 0;
     bool q = false;
+    auto put = [&](u32 c) {
+        if (nacc == 0 && ((uintptr_t)dst & 7u) != 0) { *dst++ = (u8)c; return; }
+        acc |= (u64)c << (8 * nacc);
+        if (++nacc == 8) { *(u64 *)dst = acc; dst += 8; acc = 0; nacc = 0; }
+    };
+    auto flush = [&]() {
+        for (u32 k = 0; k < nacc; ++k) dst[k] = (u8)(acc >> (8 * k));
+        dst += nacc;
+        acc = 0;
+        nacc = 0;
+    };
     auto open_field = [&]() {
         clen = 0;
         special = false;
@@ -687,7 +701,7 @@ __global__ __launch_bounds__(256) void k_csvcol(ColArgs a) {
             const u64 k = f * a.R + j;
             dst = a.out + a.off[k];
             q = a.quoted[k] != 0;
-            if (q) *dst++ = '"';
+            if (q) put('"');
         }
     };
     auto save = [&]() {
@@ -698,8 +712,9 @@ __global__ __launch_bounds__(256) void k_csvcol(ColArgs a) {
                 a.len[k] = qq ? clen + 3 : clen + 1;
                 a.quoted[k] = qq;
             } else {
-                if (q) *dst++ = '"';
-                *dst++ = '\n';
+                if (q) put('"');
+                put('\n');
+                flush();
             }
         }
         ++f;
@@ -725,8 +740,8 @@ __global__ __launch_bounds__(256) void k_csvcol(ColArgs a) {
                     clen += 1 + (b == '"');  // a quote is doubled if the value is quoted
                     special |= b == ',' || b == '"' || b == '\n';
                 } else {
-                    *dst++ = (u8)b;
-                    if (q && b == '"') *dst++ = '"';
+                    put(b);
+                    if (q && b == '"') put('"');
                 }
             }
         }
