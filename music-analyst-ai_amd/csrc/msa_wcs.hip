@@ -150,38 +150,76 @@ __device__ __forceinline__ bool eol_after(u32 b, u32 next, u64 i, u64 n) {
     return b == '\n' || (b == '\r' && (i + 1 >= n || next != '\n')) || i + 1 == n;
 }
 
+// Segment walk shared by k_wcs_map and k_wcs_emit.  Only '"', ',', '\r',
+// '\n' (and the last byte of the input) are visited one by one: T_O, the
+// step of every other byte, is idempotent, so a run of ordinary bytes is one
+// T_O step.  SWAR masks over each 16-byte vector find the visited bytes.
+// S: the walker; S::step(t) applies a transfer table, S::eol(i) handles the
+// end of a line after byte i.
+__device__ __forceinline__ u32 mask16(const uint4 &v, u32 c) {
+    return swar_pack4(swar_eq(v.x, c)) | (swar_pack4(swar_eq(v.y, c)) << 4) | (swar_pack4(swar_eq(v.z, c)) << 8) |
+           (swar_pack4(swar_eq(v.w, c)) << 12);
+}
+
+template <typename W>
+__device__ __forceinline__ void seg_walk(const u8 *__restrict__ buf, u64 base, u64 ds, u64 n, W &wk) {
+    for (u32 q = 0; q < SEG / 16; ++q) {
+        const u64 b0 = base + q * 16;
+        if (b0 >= n) break;
+        const uint4 v = *(const uint4 *)(buf + b0);
+        u32 vm = 0xFFFFu;
+        if (b0 < ds) vm &= 0xFFFFu << (u32)(ds - b0);
+        if (b0 + 16 > n) vm &= (1u << (u32)(n - b0)) - 1u;
+        if (!vm) continue;
+        const u32 Q = mask16(v, '"'), D = mask16(v, ','), NL = mask16(v, '\n'), CR = mask16(v, '\r');
+        const u32 S = (Q | D | NL | CR) & vm;
+        const u32 O = vm & ~S;
+        u32 E = S;
+        const bool has_last = b0 + 16 >= n;  // the input's last byte is in this vector
+        const u32 pl = has_last ? (u32)(n - 1 - b0) : 0u;
+        if (has_last && ((vm >> pl) & 1u)) E |= 1u << pl;
+        int prev = -1;
+        while (E) {
+            const u32 p = (u32)__builtin_ctz(E);
+            E &= E - 1;
+            const u32 upto_prev = prev < 0 ? 0u : ((2u << prev) - 1u);
+            if (O & ((1u << p) - 1u) & ~upto_prev) wk.step(T_O);  // ordinary bytes in (prev, p)
+            const u32 c = byte_of(v, p);
+            wk.step(tpk(c));
+            const u64 i = b0 + p;
+            bool eol = i + 1 == n || c == '\n';
+            if (c == '\r' && !eol) eol = (p < 15 ? byte_of(v, p + 1) : (u32)buf[i + 1]) != '\n';
+            if (eol) wk.eol(i);
+            prev = (int)p;
+        }
+        if (O & ~(prev < 0 ? 0u : ((2u << prev) - 1u))) wk.step(T_O);  // ordinary bytes after the last visited one
+    }
+}
+
+struct MapWalker {
+    u32 m;
+    u64 c6;
+    __device__ __forceinline__ void step(u32 t) { m = map_apply(t, m); }
+    __device__ __forceinline__ void eol(u64) {
+#pragma unroll
+        for (u32 k = 0; k < 6; ++k) {
+            const u32 s = (m >> (3 * k)) & 7u;
+            if (s != SR && s != IQ) c6 += 1ull << (9 * k);
+        }
+        m = map_apply(T_EOL, m);
+    }
+};
+
 // Per segment: map over the 6 entering states; row ends per entering state
 // (9 bits each: at most 256 per segment).
 __global__ __launch_bounds__(256) void k_wcs_map(const u8 *__restrict__ buf, u64 ds, u64 n, u64 nseg,
                                                  u32 *__restrict__ map, u64 *__restrict__ cnt6) {
     const u64 seg = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (seg >= nseg) return;
-    const u64 base = seg * SEG;
-    u32 m = MAP_ID;
-    u64 c6 = 0;
-    for (u32 q = 0; q < SEG / 16; ++q) {
-        const u64 b0 = base + q * 16;
-        if (b0 >= n) break;
-        const uint4 v = *(const uint4 *)(buf + b0);
-        for (u32 j = 0; j < 16; ++j) {
-            const u64 i = b0 + j;
-            if (i < ds) continue;
-            if (i >= n) break;
-            const u32 b = byte_of(v, j);
-            m = map_apply(tpk(b), m);
-            const u32 nx = j < 15 ? byte_of(v, j + 1) : buf[i + 1];
-            if (eol_after(b, nx, i, n)) {
-#pragma unroll
-                for (u32 k = 0; k < 6; ++k) {
-                    const u32 s = (m >> (3 * k)) & 7u;
-                    if (s != SR && s != IQ) c6 += 1ull << (9 * k);
-                }
-                m = map_apply(T_EOL, m);
-            }
-        }
-    }
-    map[seg] = m;
-    cnt6[seg] = c6;
+    MapWalker wk{MAP_ID, 0};
+    seg_walk(buf, seg * SEG, ds, n, wk);
+    map[seg] = wk.m;
+    cnt6[seg] = wk.c6;
 }
 
 // Inclusive scan of the 256 thread composites of a block (Hillis-Steele in LDS).
@@ -242,31 +280,24 @@ __global__ __launch_bounds__(BLK) void k_wcs_state_down(const u32 *__restrict__ 
     }
 }
 
+struct EmitWalker {
+    u32 s;
+    u64 o;
+    u64 *rend;
+    __device__ __forceinline__ void step(u32 t) { s = ::step(t, s); }
+    __device__ __forceinline__ void eol(u64 i) {
+        if (s != SR && s != IQ) rend[o++] = i + 1;
+        s = ::step(T_EOL, s);
+    }
+};
+
 __global__ __launch_bounds__(256) void k_wcs_emit(const u8 *__restrict__ buf, u64 ds, u64 n, u64 nseg,
                                                   const u32 *__restrict__ sstate, const u64 *__restrict__ roff,
                                                   u64 *__restrict__ rend) {
     const u64 seg = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (seg >= nseg) return;
-    const u64 base = seg * SEG;
-    u32 s = sstate[seg];
-    u64 o = roff[seg];
-    for (u32 q = 0; q < SEG / 16; ++q) {
-        const u64 b0 = base + q * 16;
-        if (b0 >= n) break;
-        const uint4 v = *(const uint4 *)(buf + b0);
-        for (u32 j = 0; j < 16; ++j) {
-            const u64 i = b0 + j;
-            if (i < ds) continue;
-            if (i >= n) break;
-            const u32 b = byte_of(v, j);
-            s = step(tpk(b), s);
-            const u32 nx = j < 15 ? byte_of(v, j + 1) : buf[i + 1];
-            if (eol_after(b, nx, i, n)) {
-                if (s != SR && s != IQ) rend[o++] = i + 1;
-                s = step(T_EOL, s);
-            }
-        }
-    }
+    EmitWalker wk{sstate[seg], roff[seg], rend};
+    seg_walk(buf, seg * SEG, ds, n, wk);
 }
 
 // ---------------------------------------------------------------------------
