@@ -100,6 +100,11 @@ __device__ __forceinline__ u32 byte_of(const uint4 &v, u32 j) {
     return (w >> (8 * (j & 3))) & 0xFFu;
 }
 
+__device__ __forceinline__ u32 mask16(const uint4 &v, u32 c) {
+    return swar_pack4(swar_eq(v.x, c)) | (swar_pack4(swar_eq(v.y, c)) << 4) | (swar_pack4(swar_eq(v.z, c)) << 8) |
+           (swar_pack4(swar_eq(v.w, c)) << 12);
+}
+
 // ---------------------------------------------------------------------------
 // UTF-8 (strict, as Python's decoder) and NUL check.
 __device__ __forceinline__ u32 lead_len(u32 b) {
@@ -110,6 +115,8 @@ __global__ __launch_bounds__(256) void k_wcs_validate(const u8 *__restrict__ buf
     const u64 base = ((u64)blockIdx.x * blockDim.x + threadIdx.x) * 16;
     if (base >= n) return;
     const uint4 v = *(const uint4 *)(buf + base);
+    // fast path: 16 ASCII bytes without NUL (almost all of a lyrics file)
+    if (base + 16 <= n && !((v.x | v.y | v.z | v.w) & 0x80808080u) && !mask16(v, 0)) return;
     u32 bad = 0;
     for (u32 j = 0; j < 16; ++j) {
         const u64 i = base + j;
@@ -156,11 +163,6 @@ __device__ __forceinline__ bool eol_after(u32 b, u32 next, u64 i, u64 n) {
 // T_O step.  SWAR masks over each 16-byte vector find the visited bytes.
 // S: the walker; S::step(t) applies a transfer table, S::eol(i) handles the
 // end of a line after byte i.
-__device__ __forceinline__ u32 mask16(const uint4 &v, u32 c) {
-    return swar_pack4(swar_eq(v.x, c)) | (swar_pack4(swar_eq(v.y, c)) << 4) | (swar_pack4(swar_eq(v.z, c)) << 8) |
-           (swar_pack4(swar_eq(v.w, c)) << 12);
-}
-
 template <typename W>
 __device__ __forceinline__ void seg_walk(const u8 *__restrict__ buf, u64 base, u64 ds, u64 n, W &wk) {
     for (u32 q = 0; q < SEG / 16; ++q) {
@@ -248,15 +250,33 @@ __global__ __launch_bounds__(BLK) void k_wcs_state_block(const u32 *__restrict__
     if (threadIdx.x == BLK - 1) bmap[blockIdx.x] = x;
 }
 
-// One thread: entering state of every block (nb is small: nseg / 1024).
-__global__ void k_wcs_state_top(u32 *__restrict__ bmap, u64 nb, u32 *__restrict__ final_state) {
+// Entering state of every block: the block maps are staged in LDS by the
+// whole workgroup, then one thread composes them in order (nb = nseg / 1024).
+constexpr u32 TOP_T = 1024, TOP_CHUNK = 16384;
+__global__ __launch_bounds__(TOP_T) void k_wcs_state_top(u32 *__restrict__ bmap, u64 nb, u32 *__restrict__ final_state) {
+    __shared__ u32 sm[TOP_CHUNK];
     u32 s = SR;
-    for (u64 b = 0; b < nb; ++b) {
-        const u32 m = bmap[b];
-        bmap[b] = s;
-        s = step(m, s);
+    for (u64 c0 = 0; c0 < nb; c0 += TOP_CHUNK) {
+        const u32 m = (u32)(nb - c0 < TOP_CHUNK ? nb - c0 : TOP_CHUNK);
+        for (u32 k = threadIdx.x; k < m; k += TOP_T) sm[k] = bmap[c0 + k];
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (u32 k = 0; k < m; ++k) {
+                const u32 t = sm[k];
+                sm[k] = s;
+                s = step(t, s);
+            }
+        }
+        __syncthreads();
+        for (u32 k = threadIdx.x; k < m; k += TOP_T) bmap[c0 + k] = sm[k];
+        __syncthreads();
+        s = __shfl(s, 0);  // every wave needs the carry; wave 0 lane 0 holds it
+        if (threadIdx.x == 0) sm[0] = s;
+        __syncthreads();
+        s = sm[0];
+        __syncthreads();
     }
-    *final_state = s;
+    if (threadIdx.x == 0) *final_state = s;
 }
 
 __global__ __launch_bounds__(BLK) void k_wcs_state_down(const u32 *__restrict__ map, const u64 *__restrict__ cnt6,
@@ -1046,7 +1066,7 @@ static int wcs_split_rows(msa_wcs *w, WCtr **ctr_out, u64 *ds_out, u64 *nrows_ou
         dfin = bmap + nb;
         hipLaunchKernelGGL(k_wcs_map, grid1(nseg), dim3(256), 0, st, buf, ds, n, nseg, map, cnt6);
         hipLaunchKernelGGL(k_wcs_state_block, dim3((u32)nb), dim3(BLK), 0, st, (const u32 *)map, nseg, bmap);
-        hipLaunchKernelGGL(k_wcs_state_top, dim3(1), dim3(1), 0, st, bmap, nb, dfin);
+        hipLaunchKernelGGL(k_wcs_state_top, dim3(1), dim3(TOP_T), 0, st, bmap, nb, dfin);
         hipLaunchKernelGGL(k_wcs_state_down, dim3((u32)nb), dim3(BLK), 0, st, (const u32 *)map, (const u64 *)cnt6,
                            nseg, (const u32 *)bmap, sstate, cnt);
         WCHECK(msa_exclusive_scan(cnt, nseg, roff, bsum, total, st));
