@@ -401,7 +401,7 @@ __device__ __forceinline__ u64 g_insert(const RowArgs &a, u64 key) {
     u64 slot = key & a.gmask;
     for (u64 p = 0; p <= a.gmask; ++p) {
         u64 *k = a.gtab + slot * 4;
-        const u64 cur = __atomic_load_n(k, __ATOMIC_RELAXED);
+        const u64 cur = *k;  // plain (cached) load: a key never changes once set; a stale 0 goes to the CAS
         if (cur == key) return slot;
         if (cur == 0) {
             const u64 old = atomicCAS((unsigned long long *)k, 0ull, (unsigned long long)key);
