@@ -774,6 +774,61 @@ __global__ __launch_bounds__(256) void k_csvcol(ColArgs a) {
     };
     open_field();
     bool any = false;
+    if constexpr (PASS == 0) {
+        // lengths only: quote/comma/CR/LF bytes one by one, every run of other
+        // bytes at once (all of them are added to the field; they never need
+        // quoting or doubling); field-limit characters = non-continuation bytes
+        for (u64 b0 = rs & ~15ull; b0 < re; b0 += 16) {
+            const uint4 v = *(const uint4 *)(a.buf + b0);
+            u32 vm = 0xFFFFu;
+            if (b0 < rs) vm &= 0xFFFFu << (u32)(rs - b0);
+            if (b0 + 16 > re) vm &= (1u << (u32)(re - b0)) - 1u;
+            const u32 S = (mask16(v, '"') | mask16(v, ',') | mask16(v, '\n') | mask16(v, '\r')) & vm;
+            const u32 O = vm & ~S;
+            const u32 W[4] = {v.x, v.y, v.z, v.w};
+            u32 CONT = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) CONT |= swar_pack4(W[k] & ~(W[k] << 1) & 0x80808080u) << (4 * k);
+            u32 E = S;
+            if (b0 + 16 >= a.n && a.n > b0 && ((vm >> (u32)(a.n - 1 - b0)) & 1u)) E |= 1u << (u32)(a.n - 1 - b0);
+            int prev = -1;
+            auto run = [&](u32 m) {
+                if (!m) return;
+                chars += (u32)__popc(m & ~CONT);
+                if (chars > FIELD_LIMIT) limit = true;
+                if (f < a.ncols) clen += (u32)__popc(m);
+                s = step(T_O, s);
+            };
+            while (E) {
+                const u32 p = (u32)__builtin_ctz(E);
+                E &= E - 1;
+                run(O & ((1u << p) - 1u) & ~(prev < 0 ? 0u : ((2u << prev) - 1u)));
+                const u32 b = byte_of(v, p);
+                const u64 i = b0 + p;
+                bool eol = i + 1 == a.n || b == '\n';
+                if (b == '\r' && !eol) eol = (p < 15 ? byte_of(v, p + 1) : (u32)a.buf[i + 1]) != '\n';
+                const u32 cls = b == '"' ? 0u : (b == ',' ? 1u : ((b == '\r' || b == '\n') ? 2u : 3u));
+                const u32 tnext = cls == 0 ? T_Q : (cls == 1 ? T_D : (cls == 2 ? T_NL : T_O));
+                const u32 tact = cls == 0 ? A_Q : (cls == 1 ? A_D : (cls == 2 ? A_NL : A_O));
+                const u32 act = (tact >> (2 * s)) & 3u;
+                if (act & 2u) save();
+                if (act & 1u) {
+                    if ((b & 0xC0) != 0x80 && ++chars > FIELD_LIMIT) limit = true;
+                    if (f < a.ncols) {
+                        clen += 1 + (b == '"');
+                        special |= b == ',' || b == '"' || b == '\n';
+                    }
+                }
+                s = step(tnext, s);
+                if (eol) {
+                    if (s == SF || s == IF || s == QQ) save();
+                    if (s != IQ) s = SR;
+                }
+                prev = (int)p;
+            }
+            run(O & ~(prev < 0 ? 0u : ((2u << prev) - 1u)));
+        }
+    } else
     for (u64 i = rs; i < re; ++i) {
         const u32 b = rd.get(i);
         bool eol = i + 1 == a.n;
