@@ -725,7 +725,6 @@ __global__ __launch_bounds__(256) void k_csvcol(ColArgs a) {
     if (r >= a.nrows) return;
     const u64 rs = a.rend[r - 1], re = a.rend[r];
     const u64 j = r - a.first;  // output row
-    ByteReader rd(a.buf);
     u32 s = SR, chars = 0;
     u64 f = 0, clen = 0;
     bool special = false, limit = false;
@@ -774,10 +773,11 @@ __global__ __launch_bounds__(256) void k_csvcol(ColArgs a) {
     };
     open_field();
     bool any = false;
-    if constexpr (PASS == 0) {
-        // lengths only: quote/comma/CR/LF bytes one by one, every run of other
-        // bytes at once (all of them are added to the field; they never need
-        // quoting or doubling); field-limit characters = non-continuation bytes
+    {
+        // quote/comma/CR/LF bytes one by one, every run of other bytes at once
+        // (all of them are added to the field and never need quoting or
+        // doubling): pass 0 counts them (field-limit characters =
+        // non-continuation bytes), pass 1 copies them through the combiner
         for (u64 b0 = rs & ~15ull; b0 < re; b0 += 16) {
             const uint4 v = *(const uint4 *)(a.buf + b0);
             u32 vm = 0xFFFFu;
@@ -794,9 +794,13 @@ __global__ __launch_bounds__(256) void k_csvcol(ColArgs a) {
             int prev = -1;
             auto run = [&](u32 m) {
                 if (!m) return;
-                chars += (u32)__popc(m & ~CONT);
-                if (chars > FIELD_LIMIT) limit = true;
-                if (f < a.ncols) clen += (u32)__popc(m);
+                if (PASS == 0) {
+                    chars += (u32)__popc(m & ~CONT);
+                    if (chars > FIELD_LIMIT) limit = true;
+                    if (f < a.ncols) clen += (u32)__popc(m);
+                } else if (f < a.ncols) {
+                    for (u32 mm = m; mm; mm &= mm - 1) put(byte_of(v, (u32)__builtin_ctz(mm)));
+                }
                 s = step(T_O, s);
             };
             while (E) {
@@ -815,8 +819,13 @@ __global__ __launch_bounds__(256) void k_csvcol(ColArgs a) {
                 if (act & 1u) {
                     if ((b & 0xC0) != 0x80 && ++chars > FIELD_LIMIT) limit = true;
                     if (f < a.ncols) {
-                        clen += 1 + (b == '"');
-                        special |= b == ',' || b == '"' || b == '\n';
+                        if (PASS == 0) {
+                            clen += 1 + (b == '"');  // a quote is doubled if the value is quoted
+                            special |= b == ',' || b == '"' || b == '\n';
+                        } else {
+                            put(b);
+                            if (q && b == '"') put('"');
+                        }
                     }
                 }
                 s = step(tnext, s);
@@ -827,34 +836,6 @@ __global__ __launch_bounds__(256) void k_csvcol(ColArgs a) {
                 prev = (int)p;
             }
             run(O & ~(prev < 0 ? 0u : ((2u << prev) - 1u)));
-        }
-    } else
-    for (u64 i = rs; i < re; ++i) {
-        const u32 b = rd.get(i);
-        bool eol = i + 1 == a.n;
-        if (b == '\n') eol = true;
-        else if (b == '\r' && !eol) eol = rd.get(i + 1) != '\n';
-        const u32 cls = b == '"' ? 0u : (b == ',' ? 1u : ((b == '\r' || b == '\n') ? 2u : 3u));
-        const u32 tnext = cls == 0 ? T_Q : (cls == 1 ? T_D : (cls == 2 ? T_NL : T_O));
-        const u32 tact = cls == 0 ? A_Q : (cls == 1 ? A_D : (cls == 2 ? A_NL : A_O));
-        const u32 act = (tact >> (2 * s)) & 3u;
-        if (act & 2u) { save(); any = true; }
-        if (act & 1u) {
-            if ((b & 0xC0) != 0x80 && ++chars > FIELD_LIMIT) limit = true;
-            if (f < a.ncols) {
-                if (PASS == 0) {
-                    clen += 1 + (b == '"');  // a quote is doubled if the value is quoted
-                    special |= b == ',' || b == '"' || b == '\n';
-                } else {
-                    put(b);
-                    if (q && b == '"') put('"');
-                }
-            }
-        }
-        s = step(tnext, s);
-        if (eol) {
-            if (s == SF || s == IF || s == QQ) { save(); any = true; }
-            if (s != IQ) s = SR;
         }
     }
     if (s == IQ) { save(); any = true; }
