@@ -685,15 +685,34 @@ __global__ __launch_bounds__(256) void k_wcs_pairs(const u64 *__restrict__ rend,
                                                    const u64 *__restrict__ nd, const u64 *__restrict__ poff,
                                                    const u64 *__restrict__ scratch, const u32 *__restrict__ rank_of,
                                                    u64 *__restrict__ pairs) {
+    // One wave covers 64 consecutive rows and writes their lines [wbeg, wend)
+    // contiguously: lane-strided over the lines, each lane finds the owning
+    // row by a binary search over the lanes' first-line offsets (shuffles), so
+    // stores are coalesced and reads run along each row's compact area.
+    const u32 lane = lane_id();
     const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x + 2;
-    if (r >= nrows || nd[r] == 0) return;
-    const u64 rs = rend[r - 1], re = rend[r];
-    const u64 *c = scratch + 3 * rs + ((re - rs) / 4 + 1);
-    u64 *o = pairs + poff[r];
-    const u64 m = nd[r];
-    for (u64 k = 0; k < m; ++k) {
-        const u64 v = c[k];
-        o[k] = ((u64)rank_of[(v >> 32) - 1] << 32) | (v & 0xFFFFFFFFu);
+    const bool act = r < nrows;
+    const u64 p0 = act ? poff[r] : ~0ull;
+    const u64 cnt = act ? nd[r] : 0;
+    const u64 rs = act ? rend[r - 1] : 0, re = act ? rend[r] : 0;
+    const u64 cbase = act ? 3 * rs + (re - rs) / 4 + 1 : 0;
+    const u64 wbeg = readlane64(p0, 0);
+    if (wbeg == ~0ull) return;  // no row of this wave exists (wave-uniform)
+    u64 wend = act ? p0 + cnt : 0;
+    for (int o = 32; o > 0; o >>= 1) wend = max(wend, (u64)__shfl_xor(wend, o));
+    const u64 iters = (wend - wbeg + 63) / 64;
+    for (u64 it = 0; it < iters; ++it) {
+        const u64 p = wbeg + it * 64 + lane;
+        int l = 0;
+        for (int st = 32; st > 0; st >>= 1) {
+            const u64 v = __shfl(p0, l + st);
+            if (v <= p) l += st;
+        }
+        const u64 k0 = __shfl(p0, l), cb = __shfl(cbase, l);
+        if (p < wend) {
+            const u64 v = scratch[cb + (p - k0)];
+            pairs[p] = ((u64)rank_of[(v >> 32) - 1] << 32) | (v & 0xFFFFFFFFu);
+        }
     }
 }
 
