@@ -388,7 +388,7 @@ struct RowArgs {
     u64 *gtab;      // 4 u64 per slot: key, h2 of the word, ~first (pos << 20 | raw len), count
     u64 gmask;
     u64 glimit;
-    u64 *scratch;   // per-row work areas, row at scratch + 3 * row start
+    u64 *scratch;   // per-row work areas, row at scratch + 2 * row start (3 tmax + 2 ntok <= 2 L)
     u64 *nd;        // distinct words per row
     u64 *spans;     // 4 per row: artist start/end, song start/end (raw)
     WCtr *ctr;
@@ -479,7 +479,7 @@ __device__ __forceinline__ void wcs_row(const RowArgs &a, WgAgg &agg, u64 r) {
     //                          its front is reused as the u32 order->slot list
     //   [tmax, tmax + nd)      the row's (word id, count) lines in order
     //   [3*tmax, +2*ntok)      per-row hash table (id, order, count)
-    u64 *sc = a.scratch + 3 * rs;
+    u64 *sc = a.scratch + 2 * rs;
     const u64 tmax = (re - rs) / 4 + 1;
     u32 nd = 0, ntok = 0;
     bool limit = false;
@@ -695,7 +695,7 @@ __global__ __launch_bounds__(256) void k_wcs_pairs(const u64 *__restrict__ rend,
     const u64 p0 = act ? poff[r] : ~0ull;
     const u64 cnt = act ? nd[r] : 0;
     const u64 rs = act ? rend[r - 1] : 0, re = act ? rend[r] : 0;
-    const u64 cbase = act ? 3 * rs + (re - rs) / 4 + 1 : 0;
+    const u64 cbase = act ? 2 * rs + (re - rs) / 4 + 1 : 0;
     const u64 wbeg = readlane64(p0, 0);
     if (wbeg == ~0ull) return;  // no row of this wave exists (wave-uniform)
     u64 wend = act ? p0 + cnt : 0;
@@ -1187,7 +1187,7 @@ extern "C" int msa_wcs_run(msa_wcs *w) {
     WCHECK(wpool(w, 19, R * 32, w->d_spans));
     WCHECK(hipMemsetAsync(w->d_nd, 0, R * 8, st));
     u64 *scratch;
-    WCHECK(wpool(w, 9, (3 * n + 64) * 8, scratch));
+    WCHECK(wpool(w, 9, (2 * n + 64) * 8, scratch));
     u64 bits = w->gbits;
     if (!bits) {
         bits = 16;
