@@ -72,3 +72,19 @@ def test_split_zipf_vs_oracle(msa_mod):
         # the same context then runs the per-song counter (shared buffer pool)
         w.count()
         assert w.summary()["total_rows"] == 3000
+
+
+def test_split_cli(msa_mod, tmp_path):
+    """`python -m msa.split_columns` (the script's command line) writes the
+    script's files and prints its summary line."""
+    import subprocess
+
+    data, args, exp = load_case("basic")
+    inp = tmp_path / "in.csv"
+    inp.write_bytes(data)
+    od = tmp_path / "cols"
+    r = subprocess.run([sys.executable, "-m", "msa.split_columns", str(inp), "--output-dir", str(od)] + args,
+                       capture_output=True, timeout=120, cwd=msa_mod.PKG_DIR)
+    assert r.returncode == 0, r.stderr
+    assert "Concluído. 4 arquivo(s) gerado(s) em:".encode() in r.stdout
+    assert {p.name: p.read_bytes() for p in od.iterdir()} == exp
