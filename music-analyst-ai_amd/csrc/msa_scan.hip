@@ -51,23 +51,34 @@ __device__ __forceinline__ void wave_sync() {
 // the last terminator as saturating ballot counts (min(popc, 3) per lane; the
 // state saturates at 3), the rest by readlane at that lane (scalar work).
 // Input is loaded two iterations ahead (the buffers are padded).
-// 32 bytes per lane per iteration (2 KiB per wave): the cross-lane ballot work
-// is per iteration, so twice the bytes per lane halves it per byte.
-#define K1_ITER 2048
-__device__ __forceinline__ Classes classify32(uint4 a, uint4 b, u32 vlo, u32 vhi) {
-    const Classes x = classify16(a, vlo), y = classify16(b, vhi);
-    Classes k;
-    k.Q = x.Q | (y.Q << 16); k.C = x.C | (y.C << 16); k.NL = x.NL | (y.NL << 16);
-    k.CR = x.CR | (y.CR << 16); k.Z = x.Z | (y.Z << 16); k.T = x.T | (y.T << 16);
+// 64 bytes per lane per iteration (4 KiB per wave, u64 masks per lane): the
+// cross-lane ballot work is per iteration, so more bytes per lane make it
+// cheaper per byte.
+#define K1_ITER 4096
+struct Classes64 {
+    u64 Q, C, NL, CR, Z;
+};
+__device__ __forceinline__ Classes64 classify64(const uint4 (&v)[4], u64 lpos, u64 end) {
+    Classes64 k{0, 0, 0, 0, 0};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const Classes c = classify16(v[q], valid_mask(lpos + 16 * q, end));
+        k.Q |= (u64)c.Q << (16 * q);
+        k.C |= (u64)c.C << (16 * q);
+        k.NL |= (u64)c.NL << (16 * q);
+        k.CR |= (u64)c.CR << (16 * q);
+        k.Z |= (u64)c.Z << (16 * q);
+    }
     return k;
 }
-__device__ __forceinline__ u32 pxor_excl32(u32 q) {  // bit j = xor of bits < j
-    u32 x = q << 1;
+__device__ __forceinline__ u64 pxor_excl64(u64 q) {  // bit j = xor of bits < j
+    u64 x = q << 1;
     x ^= x << 1;
     x ^= x << 2;
     x ^= x << 4;
     x ^= x << 8;
     x ^= x << 16;
+    x ^= x << 32;
     return x;
 }
 
@@ -82,60 +93,67 @@ __global__ __launch_bounds__(256) void k_chunk_summary(const u8 *__restrict__ bu
         const u64 cend = min(cbase + (u64)MSA_CHUNK, seg_end);
         u32 par = 0, first_nl = 0;
         u32 cr[2] = {0, 0}, nterm[2] = {0, 0}, cc[2] = {0, 0}, zz[2] = {0, 0}, lend[2] = {0, 0};
-        uint4 cur0 = ld16(buf + cbase + lane * 32), cur1 = ld16(buf + cbase + lane * 32 + 16);
+        uint4 cur[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) cur[q] = ld16(buf + cbase + lane * 64 + 16 * q);
         for (u64 ibase = cbase; ibase < cend; ibase += K1_ITER) {
-            const u64 lpos = ibase + lane * 32;
-            // one 2 KiB iteration ahead: reads end < cend + 4096 (MSA_INPUT_PAD)
-            const uint4 nxt0 = ld16(buf + lpos + K1_ITER), nxt1 = ld16(buf + lpos + K1_ITER + 16);
-            const Classes k = classify32(cur0, cur1, valid_mask(lpos, cend), valid_mask(lpos + 16, cend));
-            if (ibase == cbase) first_nl = readlane(k.NL, 0) & 1u;
-            const u64 B = __ballot(__popc(k.Q) & 1u);
+            const u64 lpos = ibase + lane * 64;
+            // one iteration ahead, only inside the chunk: reads end < cend + 4096 (MSA_INPUT_PAD)
+            uint4 nxt[4] = {cur[0], cur[1], cur[2], cur[3]};
+            if (ibase + K1_ITER < cend) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) nxt[q] = ld16(buf + lpos + K1_ITER + 16 * q);
+            }
+            const Classes64 k = classify64(cur, lpos, cend);
+            if (ibase == cbase) first_nl = (u32)(readlane64(k.NL, 0) & 1u);
+            const u64 B = __ballot(__popcll(k.Q) & 1u);
             const u32 pin0 = par ^ (mbcnt(B) & 1u);
-            const u32 inq0 = pxor_excl32(k.Q) ^ (pin0 ? 0xFFFFFFFFu : 0u);
+            const u64 inq0 = pxor_excl64(k.Q) ^ (pin0 ? ~0ull : 0ull);
             par ^= (u32)__popcll(B) & 1u;
             // raw '\n' at the following byte (for the '\r\n' swallow)
             const u64 nb_pos = ibase + K1_ITER;
             const u32 nb_nl = (nb_pos < seg_end && buf[nb_pos] == '\n') ? 1u : 0u;
-            const u32 dn = __shfl_down(k.NL, 1);
-            const u32 nlnext = (k.NL >> 1) | (((lane == 63) ? nb_nl : (dn & 1u)) << 31);
+            const u64 dn = __shfl_down(k.NL, 1);
+            const u64 nlnext = (k.NL >> 1) | ((u64)((lane == 63) ? nb_nl : (u32)(dn & 1u)) << 63);
             const u32 lastb = (u32)(min(ibase + (u64)K1_ITER, cend) - 1 - ibase);
-            const int Lz = (int)(lastb >> 5);
-            const u32 bz = lastb & 31u;
+            const int Lz = (int)(lastb >> 6);
+            const u32 bz = lastb & 63u;
             const u64 Bz = __ballot(k.Z != 0);
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-                const u32 inq = h ? ~inq0 : inq0;
-                const u32 CRu = k.CR & ~inq, NLu = k.NL & ~inq, Cu = k.C & ~inq;
-                const u32 up = __shfl_up(CRu, 1);
-                const u32 pc0 = lane ? ((up >> 31) & 1u) : cr[h];
-                const u32 TERM = CRu | (NLu & ~((CRu << 1) | pc0));
-                const u32 nt = __popc(TERM);
+                const u64 inq = h ? ~inq0 : inq0;
+                const u64 CRu = k.CR & ~inq, NLu = k.NL & ~inq, Cu = k.C & ~inq;
+                const u64 up = __shfl_up(CRu, 1);
+                const u64 pc0 = lane ? ((up >> 63) & 1u) : (u64)cr[h];
+                const u64 TERM = CRu | (NLu & ~((CRu << 1) | pc0));
+                const u32 nt = (u32)__popcll(TERM);
                 u32 totT = 0;
 #pragma unroll
-                for (int b = 0; b < 6; ++b) totT += (u32)__popcll(__ballot((nt >> b) & 1u)) << b;
-                const u32 cq = min((u32)__popc(Cu), 3u);
+                for (int b = 0; b < 7; ++b) totT += (u32)__popcll(__ballot((nt >> b) & 1u)) << b;
+                const u32 cq = min((u32)__popcll(Cu), 3u);
                 const u64 C1 = __ballot(cq >= 1u), C2 = __ballot(cq >= 2u), C3 = __ballot(cq >= 3u);
                 const u64 Bh = __ballot(nt != 0);
                 if (Bh) {
                     const int jl = 63 - __clzll(Bh);
                     const u64 A = (jl == 63) ? 0ull : (~0ull << (jl + 1));  // lanes after jl
-                    const u32 tj = readlane(TERM, jl);
-                    const u32 lt_j = 31u - __clz(tj);
-                    const u32 above = (u32)(0xFFFFFFFFull << (lt_j + 1));
-                    const u32 c_new = (u32)__popc(readlane(Cu, jl) & above) + (u32)__popcll(C1 & A) +
+                    const u64 tj = readlane64(TERM, jl);
+                    const u32 lt_j = 63u - (u32)__clzll(tj);
+                    const u64 above = lt_j == 63 ? 0ull : (~0ull << (lt_j + 1));
+                    const u32 c_new = (u32)__popcll(readlane64(Cu, jl) & above) + (u32)__popcll(C1 & A) +
                                       (u32)__popcll(C2 & A) + (u32)__popcll(C3 & A);
                     cc[h] = min(c_new, 3u);
-                    zz[h] = ((readlane(k.Z, jl) & above) != 0) | ((Bz & A) != 0);
-                    const u32 sw_j = ((readlane(CRu, jl) & readlane(nlnext, jl)) >> lt_j) & 1u;
-                    lend[h] = (u32)(ibase - cbase) + (u32)jl * 32u + lt_j + 1u + sw_j;
+                    zz[h] = ((readlane64(k.Z, jl) & above) != 0) | ((Bz & A) != 0);
+                    const u32 sw_j = (u32)(((readlane64(CRu, jl) & readlane64(nlnext, jl)) >> lt_j) & 1u);
+                    lend[h] = (u32)(ibase - cbase) + (u32)jl * 64u + lt_j + 1u + sw_j;
                 } else {
                     cc[h] = min(cc[h] + (u32)__popcll(C1) + (u32)__popcll(C2) + (u32)__popcll(C3), 3u);
                     zz[h] |= (Bz != 0);
                 }
                 nterm[h] += totT;
-                cr[h] = (readlane(CRu, Lz) >> bz) & 1u;
+                cr[h] = (u32)((readlane64(CRu, Lz) >> bz) & 1u);
             }
-            cur0 = nxt0; cur1 = nxt1;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) cur[q] = nxt[q];
         }
         if (lane == 0) {
             ChunkSum s;
