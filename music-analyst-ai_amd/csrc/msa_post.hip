@@ -628,7 +628,12 @@ __global__ void k_col_collapse(const u8 *__restrict__ buf, const u64 *__restrict
 // skewed: without it the head artists serialise on one HBM counter); the
 // block then adds each distinct key once to the HBM table.
 #define AK_T 256
+#ifndef AK_SLOTS
 #define AK_SLOTS 2048  // 40 KB of LDS: four 256-thread workgroups per CU
+#endif
+#ifndef AK_BLOCKS
+#define AK_BLOCKS 1024
+#endif
 #define AK_LOCAL (1ull << 63)
 __global__ __launch_bounds__(AK_T) void k_artist_key(const u8 *__restrict__ col, const u64 *__restrict__ ar_start,
                                                      u64 nrec, u8 *__restrict__ arena,
@@ -1118,7 +1123,7 @@ hipError_t msa_launch_artist_key(const u8 *col, const u64 *ar_start, u64 nrec, u
                                  u64 alist_cap, Counters *ctr, u64 short_base, hipStream_t s) {
     if (nrec) {
         u64 blocks = (nrec + AK_T - 1) / AK_T;
-        if (blocks > 1024) blocks = 1024;
+        if (blocks > AK_BLOCKS) blocks = AK_BLOCKS;
         hipLaunchKernelGGL(k_artist_key, dim3((u32)blocks), dim3(AK_T), 0, s, col, ar_start, nrec, arena,
                            key_off, key_len, key_slot, atab, amask, alist, alist_cap, ctr, short_base);
         hipLaunchKernelGGL(k_artist_verify, grid1(nrec), dim3(256), 0, s, (const u8 *)arena, key_off, key_len,
