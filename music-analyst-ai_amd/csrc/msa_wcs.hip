@@ -519,30 +519,66 @@ __device__ __forceinline__ void wcs_row(const RowArgs &a, WgAgg &agg, u64 r) {
         ++cps;
     };
 
-    for (u64 i = rs; i < re; ++i) {
-        const u32 b = rd.get(i);
-        // end of line: after '\n', after '\r' not followed by '\n', after the last byte
-        bool eol = i + 1 == a.n;
-        if (b == '\n') eol = true;
-        else if (b == '\r' && !eol) eol = rd.get(i + 1) != '\n';
-        // one table step instead of a switch: lanes of a wave sit in different
-        // states, and a divergent switch would run every arm (and every inlined
-        // copy of add/save) for the whole wave
-        const u32 cls = b == '"' ? 0u : (b == ',' ? 1u : ((b == '\r' || b == '\n') ? 2u : 3u));
-        const u32 tnext = cls == 0 ? T_Q : (cls == 1 ? T_D : (cls == 2 ? T_NL : T_O));
-        const u32 tact = cls == 0 ? A_Q : (cls == 1 ? A_D : (cls == 2 ? A_NL : A_O));
-        const u32 act = (tact >> (2 * s)) & 3u;
-        if (s == SR && cls != 2) fstart = i;
-        if (act & 2u) {
-            save(i);
-            if (cls == 1) fstart = i + 1;
+    // 16-byte SWAR blocks: quote/comma/CR/LF bytes (and the input's last byte)
+    // go through the reader's table step one by one; a run of other bytes is
+    // one (idempotent) T_O step -- its bytes are all added to the field: fed
+    // to the tokenizer in the text field, only counted in the others
+    for (u64 b0 = rs & ~15ull; b0 < re; b0 += 16) {
+        const uint4 v = *(const uint4 *)(a.buf + b0);
+        u32 vm = 0xFFFFu;
+        if (b0 < rs) vm &= 0xFFFFu << (u32)(rs - b0);
+        if (b0 + 16 > re) vm &= (1u << (u32)(re - b0)) - 1u;
+        const u32 S = (mask16(v, '"') | mask16(v, ',') | mask16(v, '\n') | mask16(v, '\r')) & vm;
+        const u32 O = vm & ~S;
+        u32 E = S;
+        if (b0 + 16 >= a.n && a.n > b0 && ((vm >> (u32)(a.n - 1 - b0)) & 1u)) E |= 1u << (u32)(a.n - 1 - b0);
+        auto run = [&](u32 m) {
+            if (!m) return;
+            if (s == SR) fstart = b0 + (u32)__builtin_ctz(m);
+            if (f == a.it) {
+                for (u32 mm = m; mm; mm &= mm - 1) {
+                    const u32 p = (u32)__builtin_ctz(mm);
+                    add(b0 + p, byte_of(v, p));
+                }
+            } else {
+                const u32 W[4] = {v.x, v.y, v.z, v.w};
+                u32 cont = 0;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) cont |= swar_pack4(W[k] & ~(W[k] << 1) & 0x80808080u) << (4 * k);
+                chars += (u32)__popc(m & ~cont);
+                if (chars > FIELD_LIMIT) limit = true;
+            }
+            s = step(T_O, s);
+        };
+        int prev = -1;
+        while (E) {
+            const u32 p = (u32)__builtin_ctz(E);
+            E &= E - 1;
+            run(O & ((1u << p) - 1u) & ~(prev < 0 ? 0u : ((2u << prev) - 1u)));
+            const u32 b = byte_of(v, p);
+            const u64 i = b0 + p;
+            // end of line: after '\n', after '\r' not followed by '\n', after the last byte
+            bool eol = i + 1 == a.n;
+            if (b == '\n') eol = true;
+            else if (b == '\r' && !eol) eol = (p < 15 ? byte_of(v, p + 1) : (u32)a.buf[i + 1]) != '\n';
+            const u32 cls = b == '"' ? 0u : (b == ',' ? 1u : ((b == '\r' || b == '\n') ? 2u : 3u));
+            const u32 tnext = cls == 0 ? T_Q : (cls == 1 ? T_D : (cls == 2 ? T_NL : T_O));
+            const u32 tact = cls == 0 ? A_Q : (cls == 1 ? A_D : (cls == 2 ? A_NL : A_O));
+            const u32 act = (tact >> (2 * s)) & 3u;
+            if (s == SR && cls != 2) fstart = i;
+            if (act & 2u) {
+                save(i);
+                if (cls == 1) fstart = i + 1;
+            }
+            if (act & 1u) add(i, b);
+            s = step(tnext, s);
+            if (eol) {
+                if (s == SF || s == IF || s == QQ) save(i + 1);
+                if (s != IQ) s = SR;
+            }
+            prev = (int)p;
         }
-        if (act & 1u) add(i, b);
-        s = step(tnext, s);
-        if (eol) {
-            if (s == SF || s == IF || s == QQ) save(i + 1);
-            if (s != IQ) s = SR;
-        }
+        run(O & ~(prev < 0 ? 0u : ((2u << prev) - 1u)));
     }
     if (s == IQ) save(re);  // input ended inside a quoted field
     if (limit) wcs_err(a.ctr, r, E_LIMIT);
