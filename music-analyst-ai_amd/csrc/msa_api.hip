@@ -373,9 +373,10 @@ static int ensure_tables(msa_ctx *c) {
 
 // After an overflow: grow exactly the tables that overflowed, to at least
 // twice what the failed run claimed (claim counters keep counting past the
-// list capacity), and at least 8x.
-static void grow_tables(msa_ctx *c) {
-    const u64 f = c->h_ctr.overflow;
+// list capacity), and at least 8x.  `mask` selects the overflow bits of the
+// stage that is retried.
+static void grow_tables(msa_ctx *c, u64 mask = ~0ull) {
+    const u64 f = c->h_ctr.overflow & mask;
     auto grow = [](u32 &lg, u64 claimed) {
         const u32 want = log2_ceil(std::max<u64>(claimed * 4, 1));
         lg = std::max<u32>(lg + 3, want);
@@ -419,6 +420,36 @@ static int clear_tables(msa_ctx *c) {
 static int sync_counters(msa_ctx *c) {
     HIPC(c, hipMemcpyAsync(&c->h_ctr, c->ctr.p, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
     HIPC(c, hipStreamSynchronize(c->stream));
+    return MSA_OK;
+}
+
+// After a failed (overflowed) attempt the tables hold partial counts and their
+// slot lists may be incomplete: zero the whole tables instead of the claimed
+// slots (rare path).
+static int wipe_tables(msa_ctx *c) {
+    struct {
+        DevBuf *tab;
+        u64 slots, *used;
+        u32 w;
+    } t[4] = {{&c->s_tab, c->s_slots, &c->s_used_prev, 2},
+              {&c->m_tab, c->m_slots, &c->m_used_prev, 4},
+              {&c->l_tab, c->lt_slots, &c->lt_used_prev, 4},
+              {&c->a_tab, c->a_slots, &c->a_used_prev, 4}};
+    for (auto &x : t) {
+        if (x.tab->p && x.slots) HIPC(c, hipMemsetAsync(x.tab->p, 0, x.slots * x.w * 8, c->stream));
+        *x.used = 0;
+    }
+    return MSA_OK;
+}
+static int wipe_one(msa_ctx *c, DevBuf &tab, u64 slots, u32 w, u64 &used) {
+    if (tab.p && slots) HIPC(c, hipMemsetAsync(tab.p, 0, slots * w * 8, c->stream));
+    used = 0;
+    return MSA_OK;
+}
+// Zero counter fields on the stream (a stage about to be retried).
+static int reset_ctr(msa_ctx *c, u64 Counters::*f) {
+    Counters *dc = c->ctr.as<Counters>();
+    HIPC(c, hipMemsetAsync(&(dc->*f), 0, 8, c->stream));
     return MSA_OK;
 }
 
@@ -491,7 +522,19 @@ static int split_columns_rest(msa_ctx *c, bool want_text, const std::string &ah,
     return MSA_OK;
 }
 
-static int do_split(msa_ctx *c, int flags) {
+// Word-table overflows of the scan (S/M tables, long-word occurrence list):
+// the split is repeated with grown tables (msa_split_columns' retry loop).
+static const u64 kSplitOvf = OVF_S | OVF_M | OVF_L;
+static int check_split_overflow(msa_ctx *c) {
+    int rc;
+    if ((rc = sync_counters(c))) return rc;
+    if (c->h_ctr.overflow & kSplitOvf)
+        return fail(c, MSA_ERR_CAPACITY, "word table capacity overflow (flags 0x%llx)",
+                    (unsigned long long)c->h_ctr.overflow);
+    return MSA_OK;
+}
+
+static int split_once(msa_ctx *c, int flags) {
     int rc;
     if (!c->in) return fail(c, MSA_ERR_ARG, "no input bound (msa_load_csv / msa_bind_csv)");
     if (c->n == 0 && !c->cont) return fail(c, MSA_ERR_NOHEADER, "Dataset does not contain a header row");
@@ -549,6 +592,7 @@ static int do_split(msa_ctx *c, int flags) {
     }
     if (c->cont) {
         if ((rc = build_word_lists(c))) return rc;
+        if ((rc = check_split_overflow(c))) return rc;
         return split_columns_rest(c, want_text, std::string(), std::string());
     }
     // header record = record 0
@@ -602,7 +646,23 @@ static int do_split(msa_ctx *c, int flags) {
     ah.push_back('\n');
     th.push_back('\n');
     if ((rc = build_word_lists(c))) return rc;
+    if ((rc = check_split_overflow(c))) return rc;
     return split_columns_rest(c, want_text, ah, th);
+}
+
+// The split with ht_resize semantics (parallel_spotify.c:130-132): a table
+// that overflows is grown and the pass repeated, so no input cardinality
+// makes the call fail.
+static int do_split(msa_ctx *c, int flags) {
+    int rc = MSA_OK;
+    for (int attempt = 0; attempt < 12; ++attempt) {
+        rc = split_once(c, flags);
+        if (rc != MSA_ERR_CAPACITY || !(c->h_ctr.overflow & kSplitOvf)) return rc;
+        grow_tables(c, kSplitOvf);
+        if ((rc = ensure_tables(c))) return rc;
+        if ((rc = wipe_tables(c))) return rc;
+    }
+    return rc;
 }
 
 
@@ -642,21 +702,42 @@ static int do_count(msa_ctx *c) {
         prof_end(c, ST_ARTIST_SCAN, (e - b) + c->nrec_a * 16);
     }
     if (fin.rs < e) HIPC(c, hipMemcpyAsync(c->ar_start.as<u64>() + c->nrec_a, &e, 8, hipMemcpyHostToDevice, c->stream));
-    prof_begin(c, ST_ARTIST_KEYS);
-    HIPC(c, msa_launch_artist_key(c->acol.as<u8>(), c->ar_start.as<u64>(), c->nrec_a,
-                                  c->arena.as<u8>(), c->key_off.as<u64>(), c->key_len.as<u32>(), c->key_slot.as<u64>(),
-                                  c->a_tab.as<u64>(), c->a_slots - 1, c->a_list.as<u32>(), c->a_slots / 2,
-                                  c->ctr.as<Counters>(), short_base, c->stream));
-    prof_end(c, ST_ARTIST_KEYS, (e - b) * 2 + c->nrec_a * 48);
-    if ((rc = sync_counters(c))) return rc;
-    // words longer than 16 bytes
+    // artist table: grown and the keying repeated on overflow (ht_resize, 130-132)
+    for (int attempt = 0;; ++attempt) {
+        prof_begin(c, ST_ARTIST_KEYS);
+        HIPC(c, msa_launch_artist_key(c->acol.as<u8>(), c->ar_start.as<u64>(), c->nrec_a,
+                                      c->arena.as<u8>(), c->key_off.as<u64>(), c->key_len.as<u32>(), c->key_slot.as<u64>(),
+                                      c->a_tab.as<u64>(), c->a_slots - 1, c->a_list.as<u32>(), c->a_slots / 2,
+                                      c->ctr.as<Counters>(), short_base, c->stream));
+        prof_end(c, ST_ARTIST_KEYS, (e - b) * 2 + c->nrec_a * 48);
+        if ((rc = sync_counters(c))) return rc;
+        if (!(c->h_ctr.overflow & OVF_A) || attempt >= 12) break;
+        grow_tables(c, OVF_A);
+        if ((rc = ensure_tables(c))) return rc;
+        if ((rc = wipe_one(c, c->a_tab, c->a_slots, 4, c->a_used_prev))) return rc;
+        if ((rc = reset_ctr(c, &Counters::a_claimed))) return rc;
+        if ((rc = reset_ctr(c, &Counters::overflow))) return rc;
+        if ((rc = reset_ctr(c, &Counters::collision))) return rc;
+    }
+    // words longer than 16 bytes (their table grows the same way)
     const u64 nl = std::min<u64>(c->h_ctr.l_occ, c->l_occ_cap);
-    prof_begin(c, ST_LONG_WORDS);
-    HIPC(c, msa_launch_long(c->in, c->n, c->extra.as<u8>(), c->extra_len, c->l_pos.as<u64>(), nl, c->l_len.as<u32>(), c->l_slot.as<u64>(),
-                            c->l_tab.as<u64>(), c->lt_slots - 1, c->l_list.as<u32>(), c->lt_slots / 2,
-                            c->ctr.as<Counters>(), c->stream));
-    prof_end(c, ST_LONG_WORDS, nl * 64);
-    if ((rc = sync_counters(c))) return rc;
+    for (int attempt = 0;; ++attempt) {
+        prof_begin(c, ST_LONG_WORDS);
+        HIPC(c, msa_launch_long(c->in, c->n, c->extra.as<u8>(), c->extra_len, c->l_pos.as<u64>(), nl,
+                                c->l_len.as<u32>(), c->l_slot.as<u64>(), c->l_tab.as<u64>(), c->lt_slots - 1,
+                                c->l_list.as<u32>(), c->lt_slots / 2, c->ctr.as<Counters>(), c->stream));
+        prof_end(c, ST_LONG_WORDS, nl * 64);
+        if ((rc = sync_counters(c))) return rc;
+        if (!(c->h_ctr.overflow & OVF_LT) || attempt >= 12) break;
+        // the artist stage is done: only the long-word table and its counters restart
+        const u64 keep_collision = c->h_ctr.collision;
+        grow_tables(c, OVF_LT);
+        if ((rc = ensure_tables(c))) return rc;
+        if ((rc = wipe_one(c, c->l_tab, c->lt_slots, 4, c->lt_used_prev))) return rc;
+        if ((rc = reset_ctr(c, &Counters::l_claimed))) return rc;
+        if ((rc = reset_ctr(c, &Counters::overflow))) return rc;
+        if (!keep_collision && (rc = reset_ctr(c, &Counters::collision))) return rc;
+    }
     c->s_used_prev = std::min<u64>(c->h_ctr.s_claimed, c->s_slots / 2);
     c->m_used_prev = std::min<u64>(c->h_ctr.m_claimed, c->m_slots / 2);
     c->lt_used_prev = std::min<u64>(c->h_ctr.l_claimed, c->lt_slots / 2);
@@ -903,16 +984,9 @@ int msa_rank(msa_ctx *c) {
 int msa_run(msa_ctx *c, int flags) {
     if (!c) return MSA_ERR_ARG;
     HIPC(c, hipSetDevice(c->device));
-    int rc = MSA_OK;
-    for (int attempt = 0; attempt < 8; ++attempt) {
-        rc = do_split(c, flags);
-        if (!rc) rc = do_count(c);
-        if (rc == MSA_ERR_CAPACITY && c->h_ctr.overflow) {
-            grow_tables(c);
-            continue;
-        }
-        break;
-    }
+    // overflowing tables grow inside each stage (do_split / do_count)
+    int rc = do_split(c, flags);
+    if (!rc) rc = do_count(c);
     if (!rc) rc = do_rank(c);
     return rc;
 }

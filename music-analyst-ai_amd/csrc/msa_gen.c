@@ -247,7 +247,9 @@ static void gen_zipf_like(const msa_gen_params *p, Out *o, int highcard) {
     out_s(o, p->crlf ? "\r\n" : "\n");
     for (uint64_t s = 0; s < p->n_songs; ++s) {
         int q;
-        uint32_t aid = alias_draw(&za, &r);
+        /* highcard: half the songs by a skewed (Zipf 1.1) artist population,
+         * half by one of 2^30 artists -> artist cardinality grows with songs */
+        uint32_t aid = (highcard && rng_below(&r, 2)) ? A + rng_below(&r, 1u << 30) : alias_draw(&za, &r);
         size_t nl = artist_name(aid, name, &q);
         if (q) put_quoted(o, name, nl); else out_put(o, name, nl);
         out_c(o, ',');
@@ -274,11 +276,21 @@ static void gen_zipf_like(const msa_gen_params *p, Out *o, int highcard) {
         for (uint32_t k = 0; k < nw; ++k) {
             uint32_t w;
             if (highcard && rng_below(&r, 2) == 0) {
-                /* unique-ish token: base-36 of a 40-bit random number */
-                uint64_t x = rng_next(&r) & 0xFFFFFFFFFFULL;
+                /* unique-ish token: base-36 digits of random numbers, 60 % of
+                 * them 3..8 bytes (S keys), 30 % 9..16 (M keys), 10 % 17..28
+                 * (long words), so every table class sees high cardinality */
+                const uint32_t cls = rng_below(&r, 10);
+                const int want = cls < 6 ? 3 + (int)rng_below(&r, 6) : (cls < 9 ? 9 + (int)rng_below(&r, 8)
+                                                                              : 17 + (int)rng_below(&r, 12));
                 int t = 0;
-                char tb[16];
-                do { tb[t++] = "abcdefghijklmnopqrstuvwxyz0123456789"[x % 36]; x /= 36; } while (x);
+                char tb[32];
+                while (t < want) {
+                    uint64_t x = rng_next(&r);
+                    for (int d = 0; d < 12 && t < want; ++d) {
+                        tb[t++] = "abcdefghijklmnopqrstuvwxyz0123456789"[x % 36];
+                        x /= 36;
+                    }
+                }
                 if (k && line) out_c(o, ' ');
                 out_put(o, tb, (size_t)t);
                 line++;

@@ -194,7 +194,7 @@ hipError_t msa_launch_exp_count(const ExpSrc &x, u64 n, u32 nparts, u64 *pcnt, u
 hipError_t msa_launch_exp_write(const ExpSrc &x, u64 n, u32 nparts, const u64 *pbase, const u64 *pcnt,
                                 const u64 *pblob, u64 *rcur, u64 *bcur, u8 *out, hipStream_t s) {
     if (n) hipLaunchKernelGGL(k_exp_write, g1(n), dim3(256), 0, s, x, n, nparts, pbase, pcnt, rcur, bcur, out);
-    hipLaunchKernelGGL(k_exp_headers, dim3(1), dim3(64), 0, s, nparts, pbase, pcnt, pblob, out);
+    hipLaunchKernelGGL(k_exp_headers, g1(nparts, 64), dim3(64), 0, s, nparts, pbase, pcnt, pblob, out);
     return hipGetLastError();
 }
 hipError_t msa_launch_imp(const u8 *in, const u64 *blk_off, u32 nblk, u64 *rec_base, u64 nrec_total, const ImpDst &d,

@@ -135,29 +135,23 @@ int main(int argc, char **argv) {
     if ((rc = msa_load_csv(ctx, csv, n))) die(ctx, rc, "load");
     free(csv);
 
-    double t_split0 = now_s();
+    /* Timed region.  The reference brackets its text and artist passes
+     * (parallel_spotify.c:850-851 .. 1000) for compute_time and the merge +
+     * outputs for total_time (1068).  On the GPU the text pass (tokenising and
+     * counting every lyric) runs inside the record/field scan of
+     * msa_split_columns, so the clock starts before it; the split-column FILES
+     * are written after the timed region (their bytes stay on the device
+     * until then), as the reference writes them before its own. */
+    double t0 = now_s();
     rc = msa_split_columns(ctx, MSA_SPLIT_TEXT_COLUMN);
     if (rc == MSA_ERR_NOHEADER) die(ctx, rc, "Dataset does not contain a header row");
     if (rc == MSA_ERR_BADHEADER) die(ctx, rc, "Unable to parse dataset header");
     if (rc) die(ctx, rc, "Failed to split dataset columns");
-    (void)t_split0;
-    msa_summary s;
-    msa_get_summary(ctx, &s);
-    for (int which = 0; which < 2; ++which) {
-        char *col = NULL;
-        size_t cl = 0;
-        if ((rc = msa_get_split_column(ctx, which, &col, &cl))) die(ctx, rc, "split column");
-        snprintf(path, sizeof path, "%s/%s.csv", split_dir, which ? s.text_file : s.artist_file);
-        if (write_all(path, col, cl) != 0) fprintf(stderr, "Failed to create split files in %s\n", split_dir);
-        msa_free(col);
-    }
-
-    /* timed region of the reference: after the split, through the outputs */
-    double t0 = now_s();
     if ((rc = msa_count(ctx))) die(ctx, rc, "count");
     if ((rc = msa_sync(ctx))) die(ctx, rc, "sync");
     double compute = now_s() - t0;
     if ((rc = msa_rank(ctx))) die(ctx, rc, "rank");
+    msa_summary s;
     msa_get_summary(ctx, &s);
 
     snprintf(path, sizeof path, "%s/word_counts.csv", outdir);
@@ -173,6 +167,15 @@ int main(int argc, char **argv) {
     print_top(ctx, MSA_TABLE_WORDS, "", "words");
     print_top(ctx, MSA_TABLE_ARTISTS, " songs", "artists");
     double total = now_s() - t0;
+
+    for (int which = 0; which < 2; ++which) {
+        char *col = NULL;
+        size_t cl = 0;
+        if ((rc = msa_get_split_column(ctx, which, &col, &cl))) die(ctx, rc, "split column");
+        snprintf(path, sizeof path, "%s/%s.csv", split_dir, which ? s.text_file : s.artist_file);
+        if (write_all(path, col, cl) != 0) fprintf(stderr, "Failed to create split files in %s\n", split_dir);
+        msa_free(col);
+    }
 
     snprintf(path, sizeof path, "%s/performance_metrics.json", outdir);
     FILE *mf = fopen(path, "w");

@@ -53,7 +53,8 @@ def read_outputs(outdir):
 def run_oracle(csv_path, outdir, ranks=1, word_limit=0, artist_limit=0):
     """The CPU oracle (C restatement of parallel_spotify.c, virtual np)."""
     if not os.path.exists(ORACLE):
-        pytest.skip("oracle not built (make -C oracle)")
+        # a missing checker must never turn parity tests into skips
+        pytest.fail("oracle/msa_oracle not built (make -C oracle): parity cannot be checked")
     cmd = [ORACLE, csv_path, "--output-dir", outdir, "--ranks", str(ranks)]
     if word_limit:
         cmd += ["--word-limit", str(word_limit)]

@@ -68,7 +68,7 @@ def run_world(tmp_path, data, cuts):
     logs = []
     for p in procs:
         try:
-            o, _ = p.communicate(timeout=100)
+            o, _ = p.communicate(timeout=240)
         except subprocess.TimeoutExpired:
             for q in procs:
                 q.kill()
@@ -142,3 +142,17 @@ def test_sharded_tiny_shards(msa_mod, tmp_path):
     assert words == exp["word_counts.csv"]
     assert artists == exp["top_artists.csv"]
     assert tot["total_words"] == exp["metrics"]["total_words"]
+
+
+@pytest.mark.timeout(300)
+def test_sharded_highcard_every_table_overflows(msa_mod, tmp_path):
+    """2 ranks on the corpus of test_gpu_scale.py whose cardinalities exceed
+    every initial table: each rank's split/count and the merged partitions
+    grow their tables and the result is still the single-process one."""
+    data = msa_mod.gen_corpus(150_000, mode="highcard", seed=31)
+    cuts = cuts_for(data, 2, "in_quotes")
+    words, artists, tot = run_world(tmp_path, data, cuts)
+    exp = expected(tmp_path, data)
+    assert tot == {k: exp["metrics"][k] for k in ("total_songs", "total_words")}
+    assert words == exp["word_counts.csv"]
+    assert artists == exp["top_artists.csv"]

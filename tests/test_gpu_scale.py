@@ -1,0 +1,105 @@
+"""GPU: the configurations the bench claims, and table growth on every entry point.
+
+* configs[2] at full size (5M Zipfian songs, ~1.19 GB resident in HBM, the
+  corpus bench.py times) against the oracle, byte for byte;
+* a high-cardinality corpus sized so that EVERY initial table overflows
+  (> 512K distinct 3..8-byte words, > 131K 9..16-byte words, > 32K distinct
+  long words and > 64K long-word occurrences, > 32K artists), through
+  msa_run, through the separate msa_split_columns / msa_count / msa_rank entry
+  points, and through the drop-in CLI.  The reference grows its tables
+  (ht_resize, /root/reference/src/parallel_spotify.c:101-132) and never fails
+  on cardinality; neither may libmsa_hip.
+The 2-rank sharded world on the same corpus is in test_gpu_dist.py."""
+import os
+import subprocess
+
+import pytest
+
+from conftest import PKG, read_outputs, run_oracle
+from test_gpu_parity import check_against_oracle
+
+pytestmark = pytest.mark.gpu
+CLI = os.path.join(PKG, "bin", "parallel_spotify")
+
+# cardinalities of this corpus (measured with the oracle): S 1.18M, M 683K,
+# long 226K distinct words, 79K artists -- every initial capacity exceeded
+HIGHCARD_SONGS = 150_000
+HIGHCARD_SEED = 31
+
+
+@pytest.fixture(scope="module")
+def ctx(msa_mod):
+    c = msa_mod.Context(0)
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="module")
+def highcard(msa_mod, tmp_path_factory):
+    data = msa_mod.gen_corpus(HIGHCARD_SONGS, mode="highcard", seed=HIGHCARD_SEED)
+    d = tmp_path_factory.mktemp("hc")
+    p = d / "hc.csv"
+    p.write_bytes(data)
+    r = run_oracle(str(p), str(d / "o"), ranks=1)
+    assert r.returncode == 0, r.stderr
+    return data, str(p), read_outputs(str(d / "o"))
+
+
+def test_highcard_overflows_every_table_run(msa_mod, highcard):
+    data, _, exp = highcard
+    with msa_mod.Context(0) as c:  # fresh context: initial (small) capacities
+        c.load_csv(data)
+        c.run(text_column=True)
+        s = c.summary()
+        assert s.n_words > 2_000_000 and s.n_artists > 32_768
+        assert msa_mod.table_csv_bytes(c.ranked(msa_mod.MSA_TABLE_WORDS), "word") == exp["word_counts.csv"]
+        assert msa_mod.table_csv_bytes(c.ranked(msa_mod.MSA_TABLE_ARTISTS), "artist") == exp["top_artists.csv"]
+        assert (s.total_songs, s.total_words) == (exp["metrics"]["total_songs"], exp["metrics"]["total_words"])
+
+
+def test_highcard_overflows_every_table_stages(msa_mod, highcard):
+    """msa_split_columns + msa_count + msa_rank (the CLI's and the sharded
+    driver's call sequence) recover from overflow on their own."""
+    data, _, exp = highcard
+    with msa_mod.Context(0) as c:
+        c.load_csv(data)
+        c.split_columns(True)
+        c.count()
+        c.rank()
+        s = c.summary()
+        assert msa_mod.table_csv_bytes(c.ranked(msa_mod.MSA_TABLE_WORDS), "word") == exp["word_counts.csv"]
+        assert msa_mod.table_csv_bytes(c.ranked(msa_mod.MSA_TABLE_ARTISTS), "artist") == exp["top_artists.csv"]
+        assert s.total_words == exp["metrics"]["total_words"]
+        for k, v in exp["split"].items():
+            which = 0 if k == s.artist_file + ".csv" else 1
+            assert c.split_column(which) == v, k
+
+
+def test_highcard_cli(highcard, tmp_path):
+    _, path, exp = highcard
+    out = tmp_path / "out"
+    p = subprocess.run([CLI, path, "--output-dir", str(out)], capture_output=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    got = read_outputs(str(out))
+    assert got["word_counts.csv"] == exp["word_counts.csv"]
+    assert got["top_artists.csv"] == exp["top_artists.csv"]
+    assert got["split"] == exp["split"]
+    assert got["metrics"]["total_words"] == exp["metrics"]["total_words"]
+
+
+def test_tables_shrink_back_to_small_corpus(msa_mod, highcard, tmp_path):
+    """A context whose tables grew keeps working on the next (small) input."""
+    data, _, _ = highcard
+    with msa_mod.Context(0) as c:
+        c.load_csv(data)
+        c.run(text_column=False)
+        small = msa_mod.gen_corpus(2000, mode="torture", seed=9)
+        check_against_oracle(msa_mod, c, small, tmp_path, "after_grow")
+
+
+@pytest.mark.timeout(600)
+def test_configs2_full_size(msa_mod, ctx, tmp_path):
+    """BASELINE configs[2] exactly as bench.py builds it (5M songs, ~1.19 GB)."""
+    data = msa_mod.gen_corpus(5_000_000, mode="zipf", seed=1, vocab=50000, n_artists=5000, words_per_song=30)
+    assert len(data) > 1_000_000_000
+    check_against_oracle(msa_mod, ctx, data, tmp_path, "configs2")

@@ -23,6 +23,8 @@ def load_case(name):
     if os.path.exists(os.path.join(d, "error.txt")):
         return data, args, None
     od = os.path.join(d, "out")
+    if not os.path.isdir(od):  # the script wrote no file (git keeps no empty directory)
+        return data, args, {}
     return data, args, {n: open(os.path.join(od, n), "rb").read() for n in sorted(os.listdir(od))}
 
 
