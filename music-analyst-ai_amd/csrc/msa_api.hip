@@ -21,6 +21,7 @@ hipError_t msa_launch_summary(const u8 *, u64, u64, u32, ChunkSum *, hipStream_t
 u32 msa_fn_blocks(u32 nchunks);
 hipError_t msa_launch_fn(const ChunkSum *, u64, u32, Fn *, State *, Fn *, const State *, State *, State *, hipStream_t);
 hipError_t msa_launch_scan(const ScanArgs &, int, hipStream_t);
+hipError_t msa_launch_scan_csv(const ScanArgs &, hipStream_t);
 hipError_t msa_exclusive_scan(const u64 *, u64, u64 *, u64 *, u64 *, hipStream_t);
 hipError_t msa_launch_rec_spans(const u8 *, const u64 *, const u32 *, u64, u64, int, u64 *, u64 *, u32 *, u64 *, u64 *,
                                 u32 *, hipStream_t);
@@ -582,7 +583,9 @@ static int split_once(msa_ctx *c, int flags) {
     a.ablate = c->ablate;
     a.first_rec = c->cont ? 0 : 1;
     prof_begin(c, ST_CSV_SCAN);
-    HIPC(c, msa_launch_scan(a, 0, c->stream));
+    // k_scan_csv (msa_k3.hip); MSA_ABLATE bit 64 selects the round-1 kernel (A/B runs)
+    if (c->ablate & 64) HIPC(c, msa_launch_scan(a, 0, c->stream));
+    else HIPC(c, msa_launch_scan_csv(a, c->stream));
     // algorithmic bytes: every CSV byte once + the per-record SoA it writes
     prof_end(c, ST_CSV_SCAN, c->n + c->nrec * (want_text ? 12ull : 8ull));
     // rec_start[nrec] = end of the last record (EOF when it has no terminator)
@@ -1423,3 +1426,18 @@ int msa_import_partitions(msa_ctx *c, int table, const void *src, const uint64_t
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------------ diagnostics
+// Not part of include/msa_hip.h: the per-record arrays of the last split
+// (tools/k3_debug.py compares kernel variants with it).
+extern "C" int msa_debug_records(msa_ctx *c, uint64_t *rec_start, uint32_t *nulrel, uint64_t cap, uint64_t *n) {
+    if (!c || !n) return MSA_ERR_ARG;
+    if (c->stage < 1) return MSA_ERR_ARG;
+    HIPC(c, hipSetDevice(c->device));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    *n = c->nrec;
+    const u64 m = std::min<u64>(cap, c->nrec + 1);
+    if (rec_start && m) HIPC(c, hipMemcpy(rec_start, c->rec_start.p, m * 8, hipMemcpyDeviceToHost));
+    if (nulrel && m) HIPC(c, hipMemcpy(nulrel, c->nulrel.p, m * 4, hipMemcpyDeviceToHost));
+    return MSA_OK;
+}

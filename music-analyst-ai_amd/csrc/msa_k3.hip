@@ -1,0 +1,531 @@
+// msa_k3.hip -- K3 for the CSV: record/field structure, lyric tokens and word
+// counting in one pass over each 16 KiB chunk (reader state at the chunk start
+// from K1/K2, msa_scan.hip).
+//
+// Replaces the byte-serial reader and tokenizer of the reference
+// (read_csv_record, parallel_spotify.c:549-633; parse_csv_line 258-304;
+// process_lyrics 350-394; ht_put 126-149) for the lyric column.
+//
+// Layout of the work (gfx950, wave64):
+//   * a wave moves 4 KiB per iteration; lane l owns the 64 contiguous bytes
+//     [64 l, 64 l + 64) as four dwordx4 loads, so every byte class is a u64
+//     mask per lane and every cross-lane step (quote parity, record index,
+//     comma count) is a handful of ballots per 4 KiB;
+//   * per-record structure is computed per lane segment (between record
+//     terminators) with bit arithmetic, not per byte;
+//   * the iteration's bytes are staged in a per-wave LDS ring; each lane walks
+//     its own token starts, reads the key (<= 16 bytes) from the ring and
+//     counts it in ONE workgroup-wide LDS table of 16-byte keys (4-slot
+//     buckets read with four ds_read_b128); keys the LDS table cannot hold
+//     are batched per wave and inserted into the HBM tables 64 at a time.
+#include "msa_internal.h"
+#include "msa_tables.h"
+
+namespace {
+
+#define Q_T 1024                 // 16 waves: one workgroup per CU
+#define Q_W (Q_T / 64)
+#define Q_BLK 4096               // bytes per wave-iteration
+#define Q_RING (Q_BLK + 32)      // + the next block's first 16 bytes (+ slack)
+#define Q_MISS 64                // deferred HBM inserts per wave (16 B each)
+#define Q_WLDS (Q_RING + Q_MISS * 16)
+#ifndef Q_SLOTS
+#define Q_SLOTS 4064             // LDS word table: 16-byte keys + u32 counts
+#endif
+#define Q_NB (Q_SLOTS / 4)
+#define Q_TAB (Q_SLOTS * 20)
+#define Q_LDS (Q_TAB + Q_W * Q_WLDS)
+static_assert(Q_LDS <= 163840, "K3 LDS exceeds the CU's 160 KiB");
+static_assert(Q_SLOTS % 4 == 0 && Q_TAB % 16 == 0 && Q_WLDS % 16 == 0, "LDS carve-outs stay 16-byte aligned");
+
+// Every key byte of a token is < 0x80 (alnum or '\''), so bit 63 of the
+// second key word is free: it marks a published slot (an S word has k1 == 0).
+#define KMARK 0x8000000000000000ull
+
+__device__ __forceinline__ uint4 ldg16(const u8 *p) { return *reinterpret_cast<const uint4 *>(p); }
+
+// lane l receives lane l+1's value (lane 63: 0) / lane l-1's (lane 0: 0): DPP wave shifts
+__device__ __forceinline__ u32 from_next32(u32 v) { return __builtin_amdgcn_update_dpp(0u, v, 0x130, 0xF, 0xF, false); }
+__device__ __forceinline__ u32 from_prev32(u32 v) { return __builtin_amdgcn_update_dpp(0u, v, 0x138, 0xF, 0xF, false); }
+__device__ __forceinline__ u64 from_next(u64 v) {
+    return ((u64)from_next32((u32)(v >> 32)) << 32) | from_next32((u32)v);
+}
+__device__ __forceinline__ u64 from_prev(u64 v) {
+    return ((u64)from_prev32((u32)(v >> 32)) << 32) | from_prev32((u32)v);
+}
+
+__device__ __forceinline__ u64 bits_lo(u32 n) { return n >= 64 ? ~0ull : ((1ull << n) - 1ull); }  // [0, n)
+__device__ __forceinline__ u64 bits_hi(u32 n) { return n >= 64 ? 0ull : (~0ull << n); }           // [n, 64)
+
+__device__ __forceinline__ void wsync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// 4 packed 0x80-per-byte masks of one dword -> 4 bits
+__device__ __forceinline__ u32 pk4(u32 m) { return (((m >> 7) * 0x00204081u) >> 21) & 0xFu; }
+
+struct Masks {
+    u64 Q, C, NL, CR, Z, T;
+};
+
+// An opaque use/def: the value is computed before this point and not
+// recomputed after it.
+__device__ __forceinline__ void pin64(u64 &x) { asm volatile("" : "+v"(x)); }
+
+// "byte == c" per byte as 0x80 flags (exact: no cross-byte carries)
+__device__ __forceinline__ u32 eq80(u32 x, u32 c) {
+    const u32 y = x ^ (c * 0x01010101u);
+    return ~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y) & 0x80808080u;
+}
+// any byte == c (cheap, may not locate it): the classic has-zero test
+__device__ __forceinline__ u32 has80(u32 x, u32 c) {
+    const u32 y = x ^ (c * 0x01010101u);
+    return (y - 0x01010101u) & ~y & 0x80808080u;
+}
+// 'A'..'Z' -> 'a'..'z' in place (every other byte unchanged, bytes >= 0x80
+// stay >= 0x80) and the token-byte flags of process_lyrics (alnum or '\'')
+__device__ __forceinline__ u32 lower_tok(u32 &x) {
+    const u32 hi = x & 0x80808080u, y = x & 0x7F7F7F7Fu;
+    const u32 up = (y + 0x3F3F3F3Fu) & ~(y + 0x25252525u) & ~hi & 0x80808080u;  // 'A'..'Z'
+    x |= up >> 2;
+    const u32 z = y | (up >> 2);
+    const u32 lo = (z + 0x1F1F1F1Fu) & ~(z + 0x05050505u);                     // 'a'..'z'
+    const u32 dg = (z + 0x50505050u) & ~(z + 0x46464646u);                     // '0'..'9'
+    return (((lo | dg) & ~hi) & 0x80808080u) | eq80(x, '\'');
+}
+
+// Byte classes of the lane's 64 bytes (bit i = byte i; bytes at or past
+// `nvalid` cleared); lower-cases the bytes in place (they feed only the key
+// ring).  '\r' and NUL masks are computed only when the wave's block holds
+// one (a wave-uniform branch).
+__device__ __forceinline__ Masks classify64x(uint4 (&v)[4], u32 nvalid) {
+    Masks k{0, 0, 0, 0, 0, 0};
+    u32 rare = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        u32 w[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            const u32 sh = 16 * q + 4 * d;
+            rare |= has80(w[d], '\r') | has80(w[d], 0);
+            k.Q |= (u64)pk4(eq80(w[d], '"')) << sh;
+            k.C |= (u64)pk4(eq80(w[d], ',')) << sh;
+            k.NL |= (u64)pk4(eq80(w[d], '\n')) << sh;
+            k.T |= (u64)pk4(lower_tok(w[d])) << sh;
+        }
+        v[q] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    if (__ballot(rare != 0)) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const u32 w[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                const u32 sh = 16 * q + 4 * d;
+                k.CR |= (u64)pk4(eq80(w[d], '\r')) << sh;
+                k.Z |= (u64)pk4(eq80(w[d], 0)) << sh;
+            }
+        }
+    }
+    const u64 vm = bits_lo(nvalid);
+    k.Q &= vm; k.C &= vm; k.NL &= vm; k.CR &= vm; k.Z &= vm; k.T &= vm;
+    // materialise the masks here: left alone, the scheduler sinks the byte
+    // tests to their first use (the token phase) and keeps all 64 input bytes
+    // live across the structure code, spilling to scratch
+    pin64(k.Q); pin64(k.C); pin64(k.NL); pin64(k.CR); pin64(k.Z); pin64(k.T);
+    return k;
+}
+
+__device__ __forceinline__ u64 pxor_ex64(u64 q) {  // bit j = parity of bits < j
+    u64 x = q << 1;
+    x ^= x << 1;
+    x ^= x << 2;
+    x ^= x << 4;
+    x ^= x << 8;
+    x ^= x << 16;
+    x ^= x << 32;
+    return x;
+}
+
+// Physical u64 index of logical ring word wi (the chunk swizzle of the ring
+// writes; the tail words 512.. map to themselves).
+__device__ __forceinline__ u32 ring_word(u32 wi) { return wi ^ (((wi >> 5) & 3u) << 1); }
+
+// 128-bit (hi:lo) >> k, low 64 bits, 0 < k < 64
+__device__ __forceinline__ u64 shr128(u64 lo, u64 hi, u32 k) { return (lo >> k) | (hi << (64 - k)); }
+
+// LDS lookup of a 16-byte key (k1 carries KMARK).  Returns the slot or ~0u.
+// Written branch-light: the four slot compares are plain selects; only the
+// (rare, after warm-up) claim of an empty slot takes a divergent path.
+__device__ __forceinline__ u32 lds_find16(ulonglong2 *keys, u64 k0, u64 k1) {
+    u32 h = (u32)k0 * 0x9E3779B1u + (u32)(k0 >> 32) * 0x85EBCA77u + (u32)k1 * 0xC2B2AE3Du + (u32)(k1 >> 32);
+    h ^= h >> 15;
+    h *= 0x2C1B3C6Du;
+    u32 b = __umulhi(h, (u32)Q_NB);
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+        const u32 base = b * 4;
+        const ulonglong2 s0 = keys[base], s1 = keys[base + 1], s2 = keys[base + 2], s3 = keys[base + 3];
+        const bool e0 = (s0.x == k0) & (s0.y == k1), e1 = (s1.x == k0) & (s1.y == k1);
+        const bool e2 = (s2.x == k0) & (s2.y == k1), e3 = (s3.x == k0) & (s3.y == k1);
+        const u32 hit = e0 ? 0u : (e1 ? 1u : (e2 ? 2u : (e3 ? 3u : 4u)));
+        if (hit < 4) return base + hit;
+        u32 i = s0.x == 0 ? 0u : (s1.x == 0 ? 1u : (s2.x == 0 ? 2u : (s3.x == 0 ? 3u : 4u)));
+        for (; i < 4; ++i) {
+            u64 *kp = reinterpret_cast<u64 *>(&keys[base + i]);
+            const u64 old = atomicCAS((unsigned long long *)kp, 0ull, (unsigned long long)k0);
+            if (old == 0) {
+                kp[1] = k1;  // published; a prober that reads 0 moves on
+                return base + i;
+            }
+            if (old == k0 && kp[1] == k1) return base + i;
+        }
+        b = (b + 1 == Q_NB) ? 0 : b + 1;
+    }
+    return ~0u;
+}
+
+__device__ __forceinline__ void hbm_insert16(const ScanArgs &a, u64 k0, u64 k1m, u64 cnt) {
+    if (k1m == KMARK) s_insert<false>(a.s_tab, a.s_mask, k0, cnt, a.s_list, a.s_list_cap, a.ctr);
+    else m_insert<false>(a.m_tab, a.m_mask, k0, k1m & ~KMARK, cnt, a.m_list, a.m_list_cap, a.ctr);
+}
+
+// Deferred HBM inserts, pipelined: a flush hands the wave's LDS miss buffer
+// (<= 64 keys, one per lane) to registers and issues the load of each key's
+// home slot in the HBM table WITHOUT waiting for it; the next flush (or the
+// kernel end) completes them -- a home slot that already holds the key (the
+// Zipf tail, after warm-up) costs one fire-and-forget atomic add, anything
+// else (empty, other key, unpublished) takes the full insert protocol.
+struct Pending {
+    u64 k0, k1m;       // key (k1m == KMARK: 3..8-byte word)
+    ulonglong2 v;      // home slot's first 16 bytes as loaded
+    u64 *slot;         // home slot
+    bool on;
+};
+
+__device__ __forceinline__ void pend_complete(const ScanArgs &a, Pending &p) {
+    if (!p.on) return;
+    const bool sword = p.k1m == KMARK;
+    const bool ok = sword ? (p.v.x == p.k0) : (p.v.x == p.k0 && p.v.y == (p.k1m & ~KMARK));
+    if (ok) atomicAdd((unsigned long long *)(p.slot + (sword ? 1 : 2)), 1ull);
+    else hbm_insert16(a, p.k0, p.k1m, 1);
+    p.on = false;
+}
+
+__device__ __forceinline__ void flush_miss(const ScanArgs &a, const ulonglong2 *miss, u32 n, Pending &p) {
+    wsync();
+    pend_complete(a, p);
+    const u32 lane = lane_id();
+    if (lane < n) {
+        const ulonglong2 x = miss[lane];
+        p.k0 = x.x;
+        p.k1m = x.y;
+        if (x.y == KMARK) p.slot = a.s_tab + 2 * (fmix64(x.x) & a.s_mask);
+        else p.slot = a.m_tab + 4 * (fmix64(x.x ^ fmix64(x.y & ~KMARK)) & a.m_mask);
+        p.v = *reinterpret_cast<const ulonglong2 *>(p.slot);  // consumed at the next flush
+        p.on = true;
+    }
+    wsync();
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(Q_T, 1) void k_scan_csv(ScanArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    ulonglong2 *keys = reinterpret_cast<ulonglong2 *>(smem);
+    u32 *cnts = reinterpret_cast<u32 *>(smem + Q_SLOTS * 16);
+    const u32 lane = lane_id();
+    const u32 wib = threadIdx.x >> 6;
+    unsigned char *wl = smem + Q_TAB + wib * Q_WLDS;
+    u8 *ring = wl;
+    ulonglong2 *miss = reinterpret_cast<ulonglong2 *>(wl + Q_RING);
+    u32 nmiss = 0;  // wave-uniform
+    Pending pend;
+    pend.on = false;
+    pend.k0 = pend.k1m = 0;
+    pend.slot = nullptr;
+    pend.v = make_ulonglong2(0, 0);
+    const u64 lt = (1ull << lane) - 1ull;
+
+    for (u32 i = threadIdx.x; i < Q_SLOTS; i += Q_T) {
+        keys[i] = make_ulonglong2(0, 0);
+        cnts[i] = 0;
+    }
+    __syncthreads();
+
+    const u32 gw = blockIdx.x * Q_W + wib;
+    const u32 nw = gridDim.x * Q_W;
+    u64 words = 0;
+
+    for (u32 c = gw; c < a.nchunks; c += nw) {
+        State st = a.carry[c];
+        const u64 cbase = a.seg_begin + (u64)c * MSA_CHUNK;
+        const u64 cend = min(cbase + (u64)MSA_CHUNK, a.seg_end);
+        u32 prevT = 0;  // the byte before the chunk is a token byte
+        if (cbase > a.seg_begin) {
+            const u32 b = a.buf[cbase - 1];
+            prevT = (u32)(((b | 0x20u) >= 'a' && (b | 0x20u) <= 'z') || (b >= '0' && b <= '9') || b == '\'');
+        }
+        uint4 cur[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) cur[q] = ldg16(a.buf + cbase + lane * 64 + 16 * q);
+
+        for (u64 ib = cbase; ib < cend; ib += Q_BLK) {
+            const u64 lpos = ib + lane * 64;
+            const bool more = ib + Q_BLK < cend;
+            // the 16 bytes after this block (token continuation, "\r\n" swallow):
+            // one uniform 16-byte load, only where they exist (bytes past the
+            // segment end do not count, whatever the padding holds)
+            const u64 tpos = ib + Q_BLK;
+            const uint4 tail = tpos < a.seg_end ? ldg16(a.buf + tpos) : make_uint4(0, 0, 0, 0);
+            const u32 tvm = tpos < a.seg_end ? (a.seg_end - tpos >= 16 ? 0xFFFFu : (1u << (a.seg_end - tpos)) - 1u) : 0u;
+            u32 tw[4] = {tail.x, tail.y, tail.z, tail.w};
+            u32 ttok = 0;
+#pragma unroll
+            for (int d = 0; d < 4; ++d) ttok |= pk4(lower_tok(tw[d])) << (4 * d);
+            ttok &= tvm;
+            const uint4 tail_lc = make_uint4(tw[0], tw[1], tw[2], tw[3]);
+            const u64 rem = cend > lpos ? cend - lpos : 0;
+            const Masks k = classify64x(cur, (u32)min(rem, (u64)64));
+            // stage the block (+ tail) in the wave's ring for key extraction
+            wsync();
+            // swizzled: lane l's 16-byte chunk q sits at chunk 4l + (q ^ ((l >> 2) & 3)),
+            // so lanes whose rows share banks read different banks (ring_word)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                *reinterpret_cast<uint4 *>(ring + lane * 64 + 16 * (q ^ ((lane >> 2) & 3))) = cur[q];
+            if (lane == 0) *reinterpret_cast<uint4 *>(ring + Q_BLK) = tail_lc;
+
+            // the block's bytes now live in the ring and the masks: load the
+            // next block into the same registers (in flight during the rest)
+            if (more) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) cur[q] = ldg16(a.buf + lpos + Q_BLK + 16 * q);
+            }
+
+            // ---- record structure (read_csv_record + parse_csv_line) ----
+            const u64 B = __ballot(__popcll(k.Q) & 1u);
+            const u32 pin = st.p ^ (mbcnt(B) & 1u);
+            const u64 inq = pxor_ex64(k.Q) ^ (pin ? ~0ull : 0ull);
+            const u64 CRu = k.CR & ~inq, NLu = k.NL & ~inq, Cu = k.C & ~inq;
+            // DPP and bpermute read the source lane's register only when that
+            // lane is active: every cross-lane move below runs on all 64 lanes,
+            // the per-lane choice is a select afterwards
+            const u64 CRp = from_prev(CRu) >> 63;
+            const u64 NLn = from_next(k.NL) & 1ull;
+            const u64 pCR = lane ? CRp : (u64)st.cr;
+            const u64 TERM = CRu | (NLu & ~((CRu << 1) | pCR));
+            const u32 tail_nl = ((tail.x & 0xFFu) == '\n' && (tvm & 1u)) ? 1u : 0u;
+            const u64 nNL = lane == 63 ? (u64)tail_nl : NLn;
+            const u64 SW = CRu & ((k.NL >> 1) | (nNL << 63));  // '\r' terminators that swallow a '\n'
+
+            const u32 nt = (u32)__popcll(TERM);
+            const u32 lastT = nt ? 63u - (u32)__clzll(TERM) : 0u;
+            const u64 above = nt ? bits_hi(lastT + 1) : ~0ull;
+            const u32 cq = min((u32)__popcll(Cu & above), 3u);
+            const bool zq = (k.Z & above) != 0;
+            const u64 C1 = __ballot(cq >= 1), C2 = __ballot(cq >= 2), C3 = __ballot(cq >= 3);
+            const u64 Zb = __ballot(zq), Bh = __ballot(nt != 0);
+            const u64 J = Bh & lt;
+            u64 M;
+            u32 cin;
+            bool zin;
+            if (J) {
+                const u32 jl = 63u - (u32)__clzll(J);
+                M = lt & ~bits_lo(jl);
+                cin = 0;
+                zin = (Zb & M) != 0;
+            } else {
+                M = lt;
+                cin = st.c;
+                zin = st.z || ((Zb & M) != 0);
+            }
+            cin = min(cin + (u32)__popcll(C1 & M) + (u32)__popcll(C2 & M) + (u32)__popcll(C3 & M), 3u);
+            // record index at the lane's first byte: prefix of terminator counts
+            const u64 T1 = __ballot(nt >= 1), T2 = __ballot(nt >= 2), T3 = __ballot(nt >= 3);
+            u64 rin = st.rec + (u64)__popcll(T1 & lt) + (u64)__popcll(T2 & lt);
+            if (T3) {  // records shorter than 32 bytes (rare): full prefix of nt
+                u32 tot;
+                rin = st.rec + wave_prefix<7>(nt, tot);
+            }
+            // record start at the lane's first byte (for NUL offsets; only
+            // when a NUL is anywhere in this block's wave)
+            const u64 endp = nt ? lpos + lastT + 1 + ((SW >> lastT) & 1ull) : 0;
+            const u64 Zany = __ballot(k.Z != 0);
+            u64 rsin = st.rs;
+            if (Zany) {  // wave-uniform branch: the shuffle runs on every lane
+                const u64 rsj = __shfl(endp, J ? 63 - __clzll(J) : (int)lane);
+                if (J) rsin = rsj;
+            }
+
+            // per segment of the lane (between terminators): live lyric bytes,
+            // record starts, first NUL
+            u64 live = 0;
+            {
+                u64 E = TERM;
+                u32 lo = 0, cc = cin;
+                bool zz = zin;
+                u64 r = rin, rs = rsin;
+                for (;;) {
+                    const u32 hi = E ? (u32)__ffsll((long long)E) - 1 : 64u;
+                    const u64 seg = bits_hi(lo) & bits_lo(hi);
+                    const u64 zs = k.Z & seg;
+                    if (zs && !zz && a.want_nul && r < a.rec_cap) {
+                        const u32 zp = (u32)__ffsll((long long)zs) - 1;
+                        a.nulrel[r] = (u32)(lpos + zp - rs) + 1u;
+                    }
+                    if (r >= a.first_rec && !zz) {
+                        // commas after a NUL do not count (the C string ends there)
+                        u64 x = Cu & seg & (zs ? bits_lo((u32)__ffsll((long long)zs) - 1) : ~0ull);
+                        u32 from = lo;
+                        bool ok = true;
+                        for (u32 n = cc; n < 3; ++n) {
+                            if (!x) { ok = false; break; }
+                            from = (u32)__ffsll((long long)x);  // one past that comma
+                            x &= x - 1;
+                        }
+                        if (ok) {
+                            u64 lv = bits_hi(from) & bits_lo(hi);
+                            if (zs) lv &= bits_lo((u32)__ffsll((long long)zs) - 1);
+                            live |= lv;
+                        }
+                    }
+                    if (!E) break;
+                    const u64 ns = lpos + hi + 1 + ((SW >> hi) & 1ull);
+                    ++r;
+                    if (r < a.rec_cap) a.rec_start[r] = ns;
+                    rs = ns;
+                    cc = 0;
+                    zz = false;
+                    lo = hi + 1;
+                    E &= E - 1;
+                }
+            }
+            // carry the reader state to the next block (lane 63 has seen every byte)
+            {
+                const u32 cout = nt ? cq : min(cin + cq, 3u);
+                const bool zout = nt ? zq : (zin || zq);
+                st.p ^= (u32)__popcll(B) & 1u;
+                st.cr = readlane((u32)(CRu >> 63), 63);
+                st.c = readlane(cout, 63);
+                st.z = readlane((u32)zout, 63);
+                st.rec = rin + nt;
+                st.rec = readlane64(st.rec, 63);
+                if (Bh) st.rs = readlane64(endp, 63 - __clzll(Bh));
+            }
+
+            // ---- tokens of the lyric field (process_lyrics, 350-394) ----
+            const u64 Tp = from_prev(k.T) >> 63;
+            const u64 tp = lane ? Tp : (u64)prevT;
+            const u64 S0 = k.T & live & ~((k.T << 1) | tp);
+            prevT = readlane((u32)(k.T >> 63), 63);
+            const u64 Tnx = from_next(k.T);
+            const u64 Tn = lane == 63 ? (u64)ttok : Tnx;
+            // runs: rK bit b = bytes b .. b+K-1 are token bytes (w = Tn:T)
+            const u64 w = k.T;
+            const u64 r2 = w & shr128(w, Tn, 1), r2h = Tn & (Tn >> 1);
+            const u64 r3 = r2 & shr128(w, Tn, 2);
+            const u64 r4 = r2 & shr128(r2, r2h, 2), r4h = r2h & (r2h >> 2);
+            const u64 r8 = r4 & shr128(r4, r4h, 4), r8h = r4h & (r4h >> 4);
+            const u64 r9 = r8 & shr128(w, Tn, 8);
+            const u64 r16 = r8 & shr128(r8, r8h, 8);
+            const u64 r17 = r16 & shr128(w, Tn, 16);
+            const u64 sSM = S0 & r3 & ~r17, sL = S0 & r17;
+            words += (u64)__popcll(S0 & r3);
+
+            // long words (> 16 bytes): positions for k_long_insert
+            const u64 BL = __ballot(sL != 0);
+            if (BL) {
+                const u32 nl = (u32)__popcll(sL);
+                u32 tot;
+                const u32 pre = wave_prefix<6>(nl, tot);
+                u64 base = 0;
+                if (lane == 0) base = atomicAdd((unsigned long long *)&a.ctr->l_occ, (unsigned long long)tot);
+                base = readlane64(base, 0) + pre;
+                for (u64 m = sL; m; m &= m - 1) {
+                    const u32 b = (u32)__ffsll((long long)m) - 1;
+                    if (base < a.l_cap) a.l_pos[base] = (lpos + b) | a.lpos_tag;
+                    else atomicOr((unsigned long long *)&a.ctr->overflow, (unsigned long long)OVF_L);
+                    ++base;
+                }
+            }
+
+            // 3..16-byte words: every lane walks its own starts
+            wsync();
+            // diagnostic ablations (MSA_ABLATE; results invalid): 1 no tokens at
+            // all, 2 no walk, 32 walk without LDS table, 4 LDS misses dropped
+            u64 m = (a.ablate & 3) ? 0ull : sSM;
+            while (__ballot(m != 0)) {
+                bool mis = false;
+                u64 k0 = 0, k1 = KMARK;
+                if (m) {
+                    const u32 b = (u32)__ffsll((long long)m) - 1;
+                    m &= m - 1;
+                    // token length (<= 16 here): first non-token bit at or after b,
+                    // from the 32 bits [b, b + 32) of (Tn:T)
+                    const u32 d0 = (u32)w, d1 = (u32)(w >> 32), d2 = (u32)Tn;
+                    const u32 run = __builtin_amdgcn_alignbit(b >= 32 ? d2 : d1, b >= 32 ? d1 : d0, b & 31u);
+                    const u32 len = (u32)__ffs(~run) - 1;  // 3..16
+                    const u32 o = lane * 64 + b;
+                    const u64 *rw = reinterpret_cast<const u64 *>(ring);
+                    const u32 wi = o >> 3, sh = (o & 7u) * 8u;
+                    const u64 w0 = rw[ring_word(wi)], w1 = rw[ring_word(wi + 1)], w2 = rw[ring_word(wi + 2)];
+                    u64 x0 = sh ? ((w0 >> sh) | (w1 << (64 - sh))) : w0;
+                    u64 x1 = sh ? ((w1 >> sh) | (w2 << (64 - sh))) : w1;
+                    if (len < 8) x0 &= bits_lo(8 * len);
+                    x1 = len <= 8 ? 0ull : (x1 & bits_lo(8 * (len - 8)));
+                    k0 = x0;
+                    k1 = x1 | KMARK;
+                    if (a.ablate & 32) {
+                        words += (k0 ^ k1) == 1;  // keep the key build alive
+                    } else {
+                        const u32 slot = lds_find16(keys, k0, k1);
+                        if (slot != ~0u) atomicAdd(&cnts[slot], 1u);
+                        else mis = !(a.ablate & 4);
+                    }
+                }
+                const u64 MB = __ballot(mis);
+                if (MB) {
+                    const u32 nm = (u32)__popcll(MB);
+                    if (nmiss + nm > Q_MISS) {
+                        flush_miss(a, miss, nmiss, pend);
+                        nmiss = 0;
+                    }
+                    if (mis) miss[nmiss + mbcnt(MB)] = make_ulonglong2(k0, k1);
+                    nmiss += nm;
+                }
+            }
+        }
+    }
+    if (nmiss) flush_miss(a, miss, nmiss, pend);
+    pend_complete(a, pend);
+    words = wave_sum64(words);
+    if (lane == 0 && words) atomicAdd((unsigned long long *)&a.ctr->total_words, (unsigned long long)words);
+    __syncthreads();
+    for (u32 i = threadIdx.x; i < Q_SLOTS; i += Q_T) {
+        const u32 n = cnts[i];
+        if (n) {
+            const ulonglong2 kk = keys[i];
+            hbm_insert16(a, kk.x, kk.y, n);
+        }
+    }
+}
+
+static int g_q_cus = 0;
+hipError_t msa_launch_scan_csv(const ScanArgs &a, hipStream_t s) {
+    if (!a.nchunks) return hipSuccess;
+    if (!g_q_cus) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        hipDeviceProp_t p;
+        g_q_cus = (hipGetDeviceProperties(&p, dev) == hipSuccess && p.multiProcessorCount > 0) ? p.multiProcessorCount
+                                                                                                 : 256;
+        (void)hipFuncSetAttribute((const void *)k_scan_csv, hipFuncAttributeMaxDynamicSharedMemorySize, Q_LDS);
+    }
+    u32 blocks = (a.nchunks + Q_W - 1) / Q_W;
+    if (blocks > (u32)g_q_cus) blocks = (u32)g_q_cus;
+    hipLaunchKernelGGL(k_scan_csv, dim3(blocks), dim3(Q_T), Q_LDS, s, a);
+    return hipGetLastError();
+}
