@@ -203,6 +203,16 @@ int msa_segment_copy(msa_ctx *ctx, int piece, uint64_t off, uint64_t len, void *
 /* Process [skip, size) of the piece followed by tail (host or device bytes). */
 int msa_segment_set(msa_ctx *ctx, int piece, uint64_t skip, const void *tail, uint64_t tail_len);
 
+/* The artist pass (parallel_spotify.c:948-998) reads artist.csv with the
+ * record reader.  When no accepted record's artist field holds a '"' outside
+ * a quoted field (and the label has no '\n'), every artist.csv line is one
+ * record and msa_count keys the lines directly.  msa_artist_reader_needed
+ * reports (after msa_split_columns) whether that shortcut is unavailable;
+ * msa_set_artist_reader(ctx, 1) forces the exact reader (a sharded run does
+ * so on every rank when any rank needs it, then resolves MSA_PIECE_ARTISTS). */
+int msa_artist_reader_needed(msa_ctx *ctx, int *needed);
+int msa_set_artist_reader(msa_ctx *ctx, int exact);
+
 /* Serialise the counted table as nparts key-hash partitions (wire format in
  * csrc/msa_merge.hip); part_bytes[p] = bytes of partition p's block.      */
 int msa_export_partitions(msa_ctx *ctx, int table, int nparts, uint64_t *part_bytes);

@@ -24,7 +24,9 @@ hipError_t msa_launch_scan(const ScanArgs &, int, hipStream_t);
 hipError_t msa_launch_scan_csv(const ScanArgs &, hipStream_t);
 hipError_t msa_exclusive_scan(const u64 *, u64, u64 *, u64 *, u64 *, hipStream_t);
 hipError_t msa_launch_rec_spans(const u8 *, const u64 *, const u32 *, u64, u64, int, u64 *, u64 *, u32 *, u64 *, u64 *,
-                                u32 *, hipStream_t);
+                                u32 *, Counters *, const AKeys &, hipStream_t);
+hipError_t msa_launch_artist_count(const u64 *, const u32 *, const u64 *, const u64 *, u64, u64 *, u64, u32 *, u64,
+                                   Counters *, int, hipStream_t);
 hipError_t msa_launch_first_end(const u8 *, u64, u32, u32, u64 *, hipStream_t);
 hipError_t msa_launch_artist_verify(const u8 *, const u64 *, const u32 *, const u64 *, u64, const u64 *, Counters *,
                                     hipStream_t);
@@ -36,8 +38,8 @@ hipError_t msa_launch_exp_write(const ExpSrc &, u64, u32, const u64 *, const u64
 hipError_t msa_launch_imp(const u8 *, const u64 *, u32, u64 *, u64, const ImpDst &, hipStream_t);
 hipError_t msa_launch_col_write(int, const u8 *, const u64 *, const u64 *, const u64 *, const u32 *, u64, u64, u64, u8 *,
                                 hipStream_t);
-hipError_t msa_launch_artist_key(const u8 *, const u64 *, u64, u8 *, u64 *, u32 *, u64 *, u64 *, u64,
-                                 u32 *, u64, Counters *, u64, hipStream_t);
+hipError_t msa_launch_artist_key(const u8 *, const u64 *, const u64 *, const u64 *, u64, u64, u8 *, u64 *, u32 *, u64 *,
+                                 u64 *, u64, u32 *, u64, Counters *, u64, int, int, hipStream_t);
 hipError_t msa_launch_long(const u8 *, u64, const u8 *, u64, const u64 *, u64, u32 *, u64 *, u64 *, u64, u32 *, u64,
                            Counters *, hipStream_t);
 hipError_t msa_launch_word_entries(const EntryArgs &, hipStream_t);
@@ -132,10 +134,17 @@ struct msa_ctx {
     DevBuf acol, alen, aoff, asrc, apairs, tcol, tlen, toff, tsrc, tpairs, scan_bsum, scan_total;
     int cus = 256;
     int ablate = 0;  // MSA_ABLATE: diagnostic kernel ablations (results invalid)
-    u64 acol_len = 0, a_hdr_getline = 0, tcol_len = 0;
+    u64 acol_len = 0, a_hdr_getline = 0, a_hdr_len = 0, tcol_len = 0;
+    // artist pass: true = the exact record reader over artist.csv (forced by
+    // msa_set_artist_reader / an artist piece set for a shard); otherwise the
+    // lines are the records unless the split found an unquoted artist field
+    // holding a '"' (Counters::a_quoted) or the label holds a '\n'
+    bool artist_exact = false;       // msa_set_artist_reader
+    bool artist_piece_set = false;   // msa_segment_set(MSA_PIECE_ARTISTS) since the split
     bool have_tcol = false;
     // artist.csv records + keys
-    DevBuf ar_start, arena, key_off, key_len, key_slot;
+    DevBuf ar_start, arena, key_off, key_len, key_slot, kh1, kh2;
+    u64 a_long_cap = 0;  // long-key area of the lines shortcut (grows when it overflowed)
     u64 nrec_a = 0;
     // tables
     DevBuf s_tab, s_list, m_tab, m_list, l_pos, l_len, l_slot, l_tab, l_list, a_tab, a_list;
@@ -453,6 +462,17 @@ static int reset_ctr(msa_ctx *c, u64 Counters::*f) {
     HIPC(c, hipMemsetAsync(&(dc->*f), 0, 8, c->stream));
     return MSA_OK;
 }
+// Fresh artist table (grown or not) and its counters, for a repeated keying.
+static int ensure_tables(msa_ctx *c);
+static int reset_artist_table(msa_ctx *c) {
+    int rc;
+    if ((rc = ensure_tables(c))) return rc;
+    if ((rc = wipe_one(c, c->a_tab, c->a_slots, 4, c->a_used_prev))) return rc;
+    if ((rc = reset_ctr(c, &Counters::a_claimed))) return rc;
+    if ((rc = reset_ctr(c, &Counters::overflow))) return rc;
+    if ((rc = reset_ctr(c, &Counters::songs))) return rc;  // the lines kernel counts them again
+    return reset_ctr(c, &Counters::collision);
+}
 
 // ------------------------------------------------------------------ stage 1
 static int materialise_column(msa_ctx *c, bool text, const std::string &hdr_line, DevBuf &col, DevBuf &lenb,
@@ -502,13 +522,25 @@ static int split_columns_rest(msa_ctx *c, bool want_text, const std::string &ah,
         HIPC(c, ensure(c->tsrc, nrec * 8));
         HIPC(c, ensure(c->tpairs, nrec * 4));
     }
+    // artist keys for the lines shortcut of the artist pass (msa_count)
+    if (!c->a_long_cap) c->a_long_cap = std::max<u64>(1ull << 20, c->n / 32);
+    const u64 long_base = 32 * (nrec + 2);
+    HIPC(c, ensure(c->arena, long_base + c->a_long_cap));
+    HIPC(c, ensure(c->key_off, (nrec + 2) * 8));
+    HIPC(c, ensure(c->key_len, (nrec + 2) * 4));
+    HIPC(c, ensure(c->kh1, (nrec + 2) * 8));
+    HIPC(c, ensure(c->kh2, (nrec + 2) * 8));
+    AKeys ak{c->arena.as<u8>(), c->key_off.as<u64>(), c->key_len.as<u32>(), c->kh1.as<u64>(), c->kh2.as<u64>(),
+             long_base, c->a_long_cap};
     HIPC(c, msa_launch_rec_spans(c->in, c->rec_start.as<u64>(), c->nulrel.as<u32>(), nrec, c->cont ? 0 : 1,
                                  want_text ? 1 : 0, c->alen.as<u64>(), c->asrc.as<u64>(), c->apairs.as<u32>(),
-                                 c->tlen.as<u64>(), c->tsrc.as<u64>(), c->tpairs.as<u32>(), c->stream));
+                                 c->tlen.as<u64>(), c->tsrc.as<u64>(), c->tpairs.as<u32>(), c->ctr.as<Counters>(), ak,
+                                 c->stream));
     if ((rc = materialise_column(c, false, ah, c->acol, c->alen, c->aoff, c->asrc, c->apairs, &c->acol_len))) return rc;
     prof_end(c, ST_ARTIST_COLUMN, c->acol_len * 2 + c->nrec * 32);
     // compute_header_length (parallel_spotify.c:444-459): getline's end
     c->a_hdr_getline = ah.empty() ? 0 : ah.find('\n') + 1;
+    c->a_hdr_len = ah.size();
     c->a_beg = c->a_hdr_getline;
     c->a_end = c->acol_len;
     c->have_tcol = false;
@@ -541,6 +573,7 @@ static int split_once(msa_ctx *c, int flags) {
     if (c->n == 0 && !c->cont) return fail(c, MSA_ERR_NOHEADER, "Dataset does not contain a header row");
     const bool want_text = (flags & MSA_SPLIT_TEXT_COLUMN) != 0;
     c->merged_w = c->merged_a = false;
+    c->artist_piece_set = false;
     c->extra_len = 0;
     HIPC(c, ensure(c->ctr, sizeof(Counters)));
     if ((rc = clear_tables(c))) return rc;
@@ -670,57 +703,90 @@ static int do_split(msa_ctx *c, int flags) {
 
 
 // ------------------------------------------------------------------ stage 2
+// Artist keying with table growth (ht_resize semantics, 130-132).
+static int artist_keys(msa_ctx *c, const u8 *col, const u64 *ar_start, bool lines, u64 nrec, u64 short_base, u64 bytes) {
+    int rc;
+    for (int attempt = 0;; ++attempt) {
+        prof_begin(c, ST_ARTIST_KEYS);
+        HIPC(c, msa_launch_artist_key(col, ar_start, lines ? c->aoff.as<u64>() : nullptr,
+                                      lines ? c->alen.as<u64>() : nullptr, c->a_hdr_len, nrec, c->arena.as<u8>(),
+                                      c->key_off.as<u64>(), c->key_len.as<u32>(), c->key_slot.as<u64>(),
+                                      c->a_tab.as<u64>(), c->a_slots - 1, c->a_list.as<u32>(), c->a_slots / 2,
+                                      c->ctr.as<Counters>(), short_base, c->cus, c->ablate, c->stream));
+        prof_end(c, ST_ARTIST_KEYS, bytes);
+        if ((rc = sync_counters(c))) return rc;
+        if (!(c->h_ctr.overflow & OVF_A) || attempt >= 12) return MSA_OK;
+        grow_tables(c, OVF_A);
+        if ((rc = reset_artist_table(c))) return rc;
+    }
+}
+
 static int do_count(msa_ctx *c) {
     int rc;
     if (c->stage < 1) return fail(c, MSA_ERR_ARG, "msa_count before msa_split_columns");
-    // artist pass over artist.csv records from its getline header end (or the
-    // segment msa_segment_set chose for a shard)
-    const u64 b = c->a_beg, e = c->a_end;
-    State init{0, b, 0, 0, 0, 0}, fin;
-    if ((rc = run_scan_fn(c, c->acol.as<u8>(), b, e, init, &fin, ST_ARTIST_SUMMARY))) return rc;
-    const u64 nterm = fin.rec;
-    c->nrec_a = nterm + (fin.rs < e ? 1 : 0);
-    const u64 cap = nterm + 2;
-    HIPC(c, ensure(c->ar_start, cap * 8));
-    // arena: keys rewritten by duplicate_field at their artist.csv offsets, then
-    // one aligned 32-byte slot per record for keys built in registers
-    const u64 short_base = (e + 64 + 255) & ~255ull;
-    HIPC(c, ensure(c->arena, short_base + 32 * cap));
-    HIPC(c, ensure(c->key_off, cap * 8));
-    HIPC(c, ensure(c->key_len, cap * 4));
-    HIPC(c, ensure(c->key_slot, cap * 8));
-    HIPC(c, hipMemcpyAsync(c->ar_start.p, &b, 8, hipMemcpyHostToDevice, c->stream));
-    if (e > b) {
-        ScanArgs a{};
-        a.buf = c->acol.as<u8>();
-        a.seg_begin = b;
-        a.seg_end = e;
-        a.nchunks = (u32)((e - b + MSA_CHUNK - 1) / MSA_CHUNK);
-        a.carry = c->carry.as<State>();
-        a.rec_start = c->ar_start.as<u64>();
-        a.rec_cap = cap;
-        a.ctr = c->ctr.as<Counters>();
-        prof_begin(c, ST_ARTIST_SCAN);
-        HIPC(c, msa_launch_scan(a, 1, c->stream));
-        prof_end(c, ST_ARTIST_SCAN, (e - b) + c->nrec_a * 16);
+    // a label with a '\n' (its rest is read as artist records): records != lines
+    bool exact = c->artist_exact || c->artist_piece_set || c->a_hdr_getline < c->a_hdr_len;
+    if (!exact) {
+        // every artist line is one artist.csv record: count the keys k_rec_spans
+        // built (no record reader over artist.csv); the split's a_quoted flag
+        // says whether that held -- if not, start over with the exact reader
+        const u64 nrec = c->nrec;
+        for (int attempt = 0;; ++attempt) {
+            prof_begin(c, ST_ARTIST_KEYS);
+            HIPC(c, msa_launch_artist_count(c->alen.as<u64>(), c->key_len.as<u32>(), c->kh1.as<u64>(),
+                                            c->kh2.as<u64>(), nrec, c->a_tab.as<u64>(), c->a_slots - 1,
+                                            c->a_list.as<u32>(), c->a_slots / 2, c->ctr.as<Counters>(), c->cus,
+                                            c->stream));
+            prof_end(c, ST_ARTIST_KEYS, nrec * 28);
+            if ((rc = sync_counters(c))) return rc;
+            if (!(c->h_ctr.overflow & OVF_A) || attempt >= 12) break;
+            grow_tables(c, OVF_A);
+            if ((rc = reset_artist_table(c))) return rc;
+        }
+        if (c->h_ctr.a_quoted) {
+            if (c->h_ctr.a_quoted & 2) c->a_long_cap = std::max<u64>(c->a_long_cap * 4, c->h_ctr.a_long * 2);
+            exact = true;
+            if ((rc = reset_artist_table(c))) return rc;
+        } else {
+            c->nrec_a = c->h_ctr.songs;
+        }
     }
-    if (fin.rs < e) HIPC(c, hipMemcpyAsync(c->ar_start.as<u64>() + c->nrec_a, &e, 8, hipMemcpyHostToDevice, c->stream));
-    // artist table: grown and the keying repeated on overflow (ht_resize, 130-132)
-    for (int attempt = 0;; ++attempt) {
-        prof_begin(c, ST_ARTIST_KEYS);
-        HIPC(c, msa_launch_artist_key(c->acol.as<u8>(), c->ar_start.as<u64>(), c->nrec_a,
-                                      c->arena.as<u8>(), c->key_off.as<u64>(), c->key_len.as<u32>(), c->key_slot.as<u64>(),
-                                      c->a_tab.as<u64>(), c->a_slots - 1, c->a_list.as<u32>(), c->a_slots / 2,
-                                      c->ctr.as<Counters>(), short_base, c->stream));
-        prof_end(c, ST_ARTIST_KEYS, (e - b) * 2 + c->nrec_a * 48);
-        if ((rc = sync_counters(c))) return rc;
-        if (!(c->h_ctr.overflow & OVF_A) || attempt >= 12) break;
-        grow_tables(c, OVF_A);
-        if ((rc = ensure_tables(c))) return rc;
-        if ((rc = wipe_one(c, c->a_tab, c->a_slots, 4, c->a_used_prev))) return rc;
-        if ((rc = reset_ctr(c, &Counters::a_claimed))) return rc;
-        if ((rc = reset_ctr(c, &Counters::overflow))) return rc;
-        if ((rc = reset_ctr(c, &Counters::collision))) return rc;
+    if (exact) {
+        // the artist pass over artist.csv records from its getline header end (or
+        // the segment msa_segment_set chose for a shard)
+        const u64 b = c->a_beg, e = c->a_end;
+        State init{0, b, 0, 0, 0, 0}, fin;
+        if ((rc = run_scan_fn(c, c->acol.as<u8>(), b, e, init, &fin, ST_ARTIST_SUMMARY))) return rc;
+        const u64 nterm = fin.rec;
+        const u64 nra = nterm + (fin.rs < e ? 1 : 0);
+        const u64 cap = nterm + 2;
+        HIPC(c, ensure(c->ar_start, cap * 8));
+        // arena: keys rewritten by duplicate_field at their artist.csv offsets, then
+        // one aligned 32-byte slot per record for keys built in registers
+        const u64 short_base = (e + 64 + 255) & ~255ull;
+        HIPC(c, ensure(c->arena, short_base + 32 * cap));
+        HIPC(c, ensure(c->key_off, cap * 8));
+        HIPC(c, ensure(c->key_len, cap * 4));
+        HIPC(c, ensure(c->key_slot, cap * 8));
+        HIPC(c, hipMemcpyAsync(c->ar_start.p, &b, 8, hipMemcpyHostToDevice, c->stream));
+        if (e > b) {
+            ScanArgs a{};
+            a.buf = c->acol.as<u8>();
+            a.seg_begin = b;
+            a.seg_end = e;
+            a.nchunks = (u32)((e - b + MSA_CHUNK - 1) / MSA_CHUNK);
+            a.carry = c->carry.as<State>();
+            a.rec_start = c->ar_start.as<u64>();
+            a.rec_cap = cap;
+            a.ctr = c->ctr.as<Counters>();
+            prof_begin(c, ST_ARTIST_SCAN);
+            HIPC(c, msa_launch_scan(a, 1, c->stream));
+            prof_end(c, ST_ARTIST_SCAN, (e - b) + nra * 16);
+        }
+        if (fin.rs < e) HIPC(c, hipMemcpyAsync(c->ar_start.as<u64>() + nra, &e, 8, hipMemcpyHostToDevice, c->stream));
+        c->nrec_a = nra;
+        if ((rc = artist_keys(c, c->acol.as<u8>(), c->ar_start.as<u64>(), false, nra, short_base, (e - b) * 2 + nra * 48)))
+            return rc;
     }
     // words longer than 16 bytes (their table grows the same way)
     const u64 nl = std::min<u64>(c->h_ctr.l_occ, c->l_occ_cap);
@@ -916,7 +982,7 @@ void msa_destroy(msa_ctx *c) {
                      &c->nulrel, &c->acol, &c->alen, &c->aoff, &c->asrc, &c->apairs, &c->tcol, &c->tlen, &c->toff, &c->tsrc, &c->tpairs,
                      &c->scan_bsum, &c->scan_total, &c->ar_start, &c->arena, &c->key_off,
                      &c->key_len, &c->key_slot, &c->s_tab, &c->s_list, &c->m_tab, &c->m_list, &c->l_pos, &c->l_len,
-                     &c->l_slot, &c->l_tab, &c->l_list, &c->a_tab, &c->a_list, &c->ctr};
+                     &c->l_slot, &c->l_tab, &c->l_list, &c->a_tab, &c->a_list, &c->ctr, &c->kh1, &c->kh2};
     for (DevBuf *b : all) release(*b);
     for (Ranked *R : {&c->rw, &c->ra}) {
         for (auto &s : R->K)
@@ -1074,6 +1140,22 @@ int msa_get_split_column(msa_ctx *c, int which, char **out, size_t *len) {
     p[n] = 0;
     *out = p;
     *len = n;
+    return MSA_OK;
+}
+
+int msa_set_artist_reader(msa_ctx *c, int exact) {
+    if (!c) return MSA_ERR_ARG;
+    c->artist_exact = exact != 0;
+    return MSA_OK;
+}
+
+int msa_artist_reader_needed(msa_ctx *c, int *needed) {
+    if (!c || !needed) return MSA_ERR_ARG;
+    if (c->stage < 1) return fail(c, MSA_ERR_ARG, "msa_artist_reader_needed before msa_split_columns");
+    HIPC(c, hipSetDevice(c->device));
+    int rc;
+    if ((rc = sync_counters(c))) return rc;
+    *needed = (c->h_ctr.a_quoted || c->a_hdr_getline < c->a_hdr_len) ? 1 : 0;
     return MSA_OK;
 }
 
@@ -1252,6 +1334,7 @@ int msa_segment_set(msa_ctx *c, int piece, uint64_t skip, const void *tail, uint
         HIPC(c, hipMemsetAsync(c->acol.as<u8>() + c->acol_len + tail_len, 0, MSA_INPUT_PAD, c->stream));
         c->a_beg = b0 + skip;
         c->a_end = c->acol_len + tail_len;
+        c->artist_piece_set = true;  // the piece is read with the exact record reader
     }
     HIPC(c, hipStreamSynchronize(c->stream));
     return MSA_OK;

@@ -247,10 +247,27 @@ struct Counters {
     u64 overflow;    // bitmask of capacity overflows
     u64 collision;   // hash-collision detections
     u64 songs;
-    u64 pad[7];
+    // split: some accepted record's artist field holds a '"' without being a
+    // quoted field, so artist.csv lines may not be artist.csv records (the
+    // artist pass then runs the exact record reader over artist.csv)
+    u64 a_quoted;
+    u64 a_long;      // bytes used in the long-key arena (k_rec_spans)
+    u64 pad[5];
 };
 
 enum { OVF_S = 1, OVF_M = 2, OVF_L = 4, OVF_LT = 8, OVF_A = 16, OVF_REC = 32 };
+
+// Artist keys built by k_rec_spans for the lines shortcut of the artist pass:
+// per record the key bytes (duplicate_field(duplicate_field(field0, 1), 0))
+// in the arena -- a 32-byte slot per record, longer or escaped keys in the
+// long area behind an atomic cursor -- and two independent 64-bit hashes.
+struct AKeys {
+    u8 *arena;
+    u64 *key_off;
+    u32 *key_len;
+    u64 *kh1, *kh2;
+    u64 long_base, long_cap;  // long area = arena + [long_base, long_base + long_cap)
+};
 
 // Arguments of the main scan (K3) and of the ranking-entry builder.
 struct ScanArgs {

@@ -199,8 +199,15 @@ __device__ __forceinline__ u64 win_mask(const Win64 &w) {
     }
     return m;
 }
+// w.q[i] for a run-time i, as selects on single dwords (a select of whole
+// array elements is lowered to a scratch-memory index)
+__device__ __forceinline__ u32 sel_d(u32 i, u32 a, u32 b, u32 c, u32 d) {
+    const u32 lo = (i & 1u) ? b : a, hi = (i & 1u) ? d : c;
+    return (i & 2u) ? hi : lo;
+}
 __device__ __forceinline__ uint4 sel_q(const Win64 &w, u32 i) {
-    return i == 0 ? w.q[0] : (i == 1 ? w.q[1] : (i == 2 ? w.q[2] : w.q[3]));
+    return make_uint4(sel_d(i, w.q[0].x, w.q[1].x, w.q[2].x, w.q[3].x), sel_d(i, w.q[0].y, w.q[1].y, w.q[2].y, w.q[3].y),
+                      sel_d(i, w.q[0].z, w.q[1].z, w.q[2].z, w.q[3].z), sel_d(i, w.q[0].w, w.q[1].w, w.q[2].w, w.q[3].w));
 }
 // 32 window bytes starting at byte `at` (at + len <= 64), bytes >= len zeroed.
 __device__ __forceinline__ void win_take32(const Win64 &w, u32 at, u32 len, uint4 *o0, uint4 *o1) {
@@ -270,6 +277,89 @@ __device__ __forceinline__ u32 quote_pairs(u64 q) {
     return pairs;
 }
 
+// The artist pass's key for one record when artist.csv lines are its records:
+// duplicate_field(line, 0) with line = duplicate_field(field0, 1) (the
+// artist.csv line without its '\n'), i.e. for the trimmed field [as, ae):
+//   quote-free           -> the field itself
+//   quoted "..."         -> trim(collapse(inner))
+//   anything else        -> the general path (byte loop, long area)
+// An unquoted field with a '"' makes the shortcut unavailable (a_quoted is
+// set by the caller), so its key is never used.
+__device__ void artist_key_of(const u8 *__restrict__ buf, const Win64 &w0, u64 b0, u64 as, u64 ae, u64 r,
+                              const AKeys &ak, Counters *ctr) {
+    const u64 n = ae - as;
+    if (n == 0) {
+        ak.key_len[r] = 0;
+        return;
+    }
+    bool quoted;
+    if (ae - b0 <= 64) {  // the field is inside the record's first window
+        const u32 a = (u32)(as - b0), b = (u32)(ae - 1 - b0);
+        const u64 Q = win_mask<1>(w0) & bits_from(a) & bits_below(b + 1);
+        quoted = n >= 2 && ((Q >> a) & 1) && ((Q >> b) & 1);
+        u32 ka = a, kb = b + 1;  // key = window bytes [ka, kb)
+        bool ok = false;
+        if (!Q) {
+            ok = true;
+        } else if (quoted && !(Q & bits_from(a + 1) & bits_below(b))) {
+            const u64 inner = bits_from(a + 1) & bits_below(b);
+            const u64 nsp = inner & ~win_mask<0>(w0);
+            if (!nsp) {
+                ak.key_len[r] = 0;
+                return;
+            }
+            ka = (u32)__ffsll((long long)nsp) - 1;
+            kb = 64u - (u32)__clzll((long long)nsp);
+            ok = true;
+        }
+        if (ok && kb - ka <= 32) {
+            const u32 klen = kb - ka;
+            uint4 k0, k1;
+            win_take32(w0, ka, klen, &k0, &k1);
+            uint4 *dst = reinterpret_cast<uint4 *>(ak.arena + 32 * r);
+            dst[0] = k0;
+            dst[1] = k1;
+            ak.key_off[r] = 32 * r;
+            ak.key_len[r] = klen;
+            const u64 w0 = ((u64)k0.y << 32) | k0.x, w1 = ((u64)k0.w << 32) | k0.z;
+            const u64 w2 = ((u64)k1.y << 32) | k1.x, w3 = ((u64)k1.w << 32) | k1.z;
+            ak.kh1[r] = akey_fold(akey_seed(klen, 0), w0, w1, w2, w3, 0);
+            ak.kh2[r] = akey_fold(akey_seed(klen, 1), w0, w1, w2, w3, 1);
+            return;
+        }
+    } else {
+        quoted = n >= 2 && buf[as] == '"' && buf[ae - 1] == '"';
+    }
+    // general path: the line (collapse "" pairs of an unquoted field), then
+    // duplicate_field(line, 0) in place, in the long area
+    const u64 room = n + 1;
+    const u64 at = atomicAdd((unsigned long long *)&ctr->a_long, (unsigned long long)((room + 15) & ~15ull));
+    if (at + room > ak.long_cap) {  // no room: the shortcut is given up, the exact reader runs
+        atomicOr((unsigned long long *)&ctr->a_quoted, 2ull);
+        ak.key_len[r] = 0;
+        return;
+    }
+    u8 *dst = ak.arena + ak.long_base + at;
+    u64 m = 0;
+    if (quoted) {
+        for (u64 i = as; i < ae; ++i) dst[m++] = buf[i];
+    } else {
+        for (u64 i = as; i < ae; ++i) {
+            const u8 ch = buf[i];
+            if (ch == '"' && i + 1 < ae && buf[i + 1] == '"') ++i;
+            dst[m++] = ch;
+        }
+        while (m > 0 && c_space(dst[m - 1])) --m;  // trim_inplace (the front is non-space)
+    }
+    const Span sp = dup_field(dst, m, 0, dst);
+    ak.key_off[r] = ak.long_base + at + sp.off;
+    ak.key_len[r] = (u32)sp.len;
+    if (sp.len) {
+        ak.kh1[r] = akey_hash_bytes(dst + sp.off, sp.len, 0);
+        ak.kh2[r] = akey_hash_bytes(dst + sp.off, sp.len, 1);
+    }
+}
+
 // Per record (thread): the first three unquoted commas (parse_csv_line,
 // parallel_spotify.c:258-304), then the spans of both column lines
 // (split_dataset_columns 699-714): line = duplicate_field(field, preserve=1)
@@ -287,7 +377,8 @@ __global__ __launch_bounds__(256) void k_rec_spans(const u8 *__restrict__ buf, c
                                                    const u32 *__restrict__ nulrel, u64 nrec, u64 first_rec,
                                                    int want_text, u64 *__restrict__ alen, u64 *__restrict__ asrc,
                                                    u32 *__restrict__ apairs, u64 *__restrict__ tlen,
-                                                   u64 *__restrict__ tsrc, u32 *__restrict__ tpairs) {
+                                                   u64 *__restrict__ tsrc, u32 *__restrict__ tpairs,
+                                                   Counters *ctr, AKeys ak) {
     const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= nrec) return;
     const u64 s = rec_start[r], e = rec_start[r + 1];
@@ -321,6 +412,7 @@ __global__ __launch_bounds__(256) void k_rec_spans(const u8 *__restrict__ buf, c
     }
     if (r < first_rec || nc < 3) {
         alen[r] = 0;
+        ak.key_len[r] = 0;
         if (want_text) tlen[r] = 0;
         return;
     }
@@ -336,20 +428,30 @@ __global__ __launch_bounds__(256) void k_rec_spans(const u8 *__restrict__ buf, c
             } else {
                 const u32 a = (u32)__ffsll((long long)nsp) - 1, b = 63u - (u32)__clzll((long long)nsp);
                 const u64 Q = win_mask<1>(w0) & bits_from(a) & bits_below(b + 1);
-                if (!(b > a && ((Q >> a) & 1) && ((Q >> b) & 1))) pairs = quote_pairs(Q);
+                if (!(b > a && ((Q >> a) & 1) && ((Q >> b) & 1))) {
+                    pairs = quote_pairs(Q);
+                    if (Q) atomicOr((unsigned long long *)&ctr->a_quoted, 1ull);
+                }
                 as = b0 + a;
                 ae = b0 + b + 1;
             }
         } else {
             while (as < ae && c_space(buf[as])) ++as;
             while (ae > as && c_space(buf[ae - 1])) --ae;
-            if (!(ae > as + 1 && buf[as] == '"' && buf[ae - 1] == '"'))
-                for (u64 i = as; i + 1 < ae; ++i)
-                    if (buf[i] == '"' && buf[i + 1] == '"') { ++pairs; ++i; }
+            if (!(ae > as + 1 && buf[as] == '"' && buf[ae - 1] == '"')) {
+                bool anyq = false;
+                for (u64 i = as; i < ae; ++i) {
+                    if (buf[i] != '"') continue;
+                    anyq = true;
+                    if (i + 1 < ae && buf[i + 1] == '"') { ++pairs; ++i; }
+                }
+                if (anyq) atomicOr((unsigned long long *)&ctr->a_quoted, 1ull);
+            }
         }
         alen[r] = (ae - as) - pairs + 1;
         asrc[r] = as;
         apairs[r] = pairs;
+        artist_key_of(buf, w0, b0, as, ae, r, ak, ctr);
     }
     if (want_text) {  // field 3: after the third comma up to the first NUL; the
                       // terminator is part of the record and trimmed as whitespace
@@ -621,109 +723,344 @@ __global__ void k_col_collapse(const u8 *__restrict__ buf, const u64 *__restrict
     dst[len] = '\n';
 }
 
-// Artist pass over artist.csv records: strip EOL, duplicate_field(line, 0),
-// count non-empty names (parallel_spotify.c:986-994).  Key bytes go to the
-// arena at the record's own offset.  Counting is privatised per workgroup in
-// an LDS table keyed by the 64-bit key hash (the artist distribution is
-// skewed: without it the head artists serialise on one HBM counter); the
-// block then adds each distinct key once to the HBM table.
-#define AK_T 256
-#ifndef AK_SLOTS
-#define AK_SLOTS 2048  // 40 KB of LDS: four 256-thread workgroups per CU
-#endif
-#ifndef AK_BLOCKS
-#define AK_BLOCKS 1024
-#endif
+// Artist pass (parallel_spotify.c:948-998): per artist.csv record, strip EOL,
+// duplicate_field(line, 0), count non-empty names.  Records are either the
+// artist.csv records found by the exact reader (ar_start) or -- when every
+// artist line is one artist.csv record (no unquoted artist field holds a
+// '"', checked by k_rec_spans) -- the lines themselves (hdr + line_off[j],
+// line_len[j]; a record without a line has length 0 and is no song).
+//
+// Key bytes go to the arena (<= 32 bytes: an aligned 32-byte slot per record,
+// built in registers; longer / escaped names: at the record's own offset).
+// Counting is privatised in ONE workgroup-wide LDS table per CU (64-bit key
+// hash, 4-slot buckets, 8192 slots); each distinct key is added to the HBM
+// table once per workgroup.  Exactness: every record's bytes are compared
+// with its workgroup's first record of that hash (after the workgroup
+// barrier, so the bytes are visible), and each workgroup's first record with
+// the global representative (k_artist_verify_reps, next launch).
+#define AK_T 1024
+#define AK_SLOTS 8192
+#define AK_NB (AK_SLOTS / 4)
 #define AK_LOCAL (1ull << 63)
-__global__ __launch_bounds__(AK_T) void k_artist_key(const u8 *__restrict__ col, const u64 *__restrict__ ar_start,
-                                                     u64 nrec, u8 *__restrict__ arena,
-                                                     u64 *__restrict__ key_off, u32 *__restrict__ key_len,
-                                                     u64 *__restrict__ key_slot, u64 *atab, u64 amask, u32 *alist,
-                                                     u64 alist_cap, Counters *ctr, u64 short_base) {
-    __shared__ u64 lh[AK_SLOTS];
-    __shared__ u64 lrep[AK_SLOTS];  // first local record; after the flush: global slot
-    __shared__ u32 lc[AK_SLOTS];
-    for (u32 i = threadIdx.x; i < AK_SLOTS; i += AK_T) { lh[i] = 0; lc[i] = 0; }
-    __syncthreads();
-    const u64 stride = (u64)gridDim.x * AK_T;
-    for (u64 j = (u64)blockIdx.x * AK_T + threadIdx.x; j < nrec; j += stride) {
-        const u64 s = ar_start[j];
-        const u64 L = ar_start[j + 1] - s;  // the record incl. its terminator
-        u64 h = 0;
-        u32 klen = 0;
-        bool fast = false;
-        if (L <= 48) {
-            // registers: strip EOL, trim; a line without '"' is its own key
-            const Win64 w = load_win64(col, s);
-            const u32 o = (u32)(s & 15);
-            const u64 fm = bits_from(o) & bits_below(o + (u32)L);
-            const u64 ne = fm & ~win_mask<2>(w);
-            const u32 endp = ne ? 64u - (u32)__clzll((long long)ne) : o;  // past the last non-EOL byte
-            const u64 f2 = fm & bits_below(endp);
-            const u64 nsp = f2 & ~win_mask<0>(w);
-            if (!nsp) {
-                fast = true;  // empty name: a song, not an artist
-            } else if (!(f2 & win_mask<1>(w))) {
-                const u32 a = (u32)__ffsll((long long)nsp) - 1, b = 63u - (u32)__clzll((long long)nsp);
-                if (b - a + 1 <= 32) {
-                    klen = b - a + 1;
-                    uint4 k0, k1;
-                    win_take32(w, a, klen, &k0, &k1);
-                    h = bytes_hash_words(k0, k1, klen);
-                    uint4 *dst = reinterpret_cast<uint4 *>(arena + short_base + 32 * j);
-                    dst[0] = k0;
-                    dst[1] = k1;
-                    key_off[j] = short_base + 32 * j;
-                    fast = true;
-                }
+#define AK_VREP (1ull << 62)   // verify against the HBM table's representative
+#define AK_SLOTMASK ((1ull << 62) - 1)
+static_assert(AK_SLOTS * 16 <= 160 * 1024, "artist LDS table exceeds the CU");
+
+__device__ __forceinline__ bool keys_equal(const u8 *__restrict__ arena, u64 oa, u32 na, u64 ob, u32 nb) {
+    if (na != nb) return false;
+    if (na <= 32 && ((oa | ob) & 15) == 0) {  // aligned 32-byte slots: vector compare
+        const uint4 *pa = reinterpret_cast<const uint4 *>(arena + oa), *pb = reinterpret_cast<const uint4 *>(arena + ob);
+        const uint4 a0 = pa[0], b0 = pb[0];
+        const uint4 a1 = na > 16 ? pa[1] : make_uint4(0, 0, 0, 0), b1 = na > 16 ? pb[1] : make_uint4(0, 0, 0, 0);
+        const u32 x[8] = {a0.x ^ b0.x, a0.y ^ b0.y, a0.z ^ b0.z, a0.w ^ b0.w,
+                          a1.x ^ b1.x, a1.y ^ b1.y, a1.z ^ b1.z, a1.w ^ b1.w};
+        u32 acc = 0;
+#pragma unroll
+        for (u32 k = 0; k < 8; ++k) {
+            const u32 lo = 4 * k;
+            const u32 keep = na <= lo ? 0u : (na >= lo + 4 ? 4u : na - lo);
+            acc |= x[k] & (keep == 4 ? 0xFFFFFFFFu : ((1u << (8 * keep)) - 1u));
+        }
+        return acc == 0;
+    }
+    const u8 *a = arena + oa, *b = arena + ob;
+    for (u32 i = 0; i < na; ++i)
+        if (a[i] != b[i]) return false;
+    return true;
+}
+
+// One artist record (the body of k_artist_key's phase 1).
+template <bool LINES>
+__device__ __forceinline__ void artist_one(u64 j, u64 s, u64 L, const Win64 win, const u8 *__restrict__ col,
+                                           u8 *__restrict__ arena, u64 *__restrict__ key_off,
+                                           u32 *__restrict__ key_len, u64 *__restrict__ key_slot, u64 *atab,
+                                           u64 amask, u32 *alist, u64 alist_cap, Counters *ctr, u64 short_base,
+                                           u64 *lh, u32 *lc, u32 *lrep, u32 &songs) {
+    if (L == 0) {  // no line: not an artist.csv record
+        key_len[j] = 0;
+        key_slot[j] = ~0ull;
+        return;
+    }
+    ++songs;
+    u64 h = 0;
+    u32 klen = 0;
+    bool fast = false;
+    if (L <= 48) {
+        // registers: strip EOL, trim; a line without '"' is its own key
+        const Win64 &w = win;
+        const u32 o = (u32)(s & 15);
+        const u64 fm = bits_from(o) & bits_below(o + (u32)L);
+        const u64 ne = fm & ~win_mask<2>(w);
+        const u32 endp = ne ? 64u - (u32)__clzll((long long)ne) : o;  // past the last non-EOL byte
+        const u64 f2 = fm & bits_below(endp);
+        const u64 nsp = f2 & ~win_mask<0>(w);
+        if (!nsp) {
+            fast = true;  // empty name: a song, not an artist
+        } else if (!(f2 & win_mask<1>(w))) {
+            const u32 a = (u32)__ffsll((long long)nsp) - 1, b = 63u - (u32)__clzll((long long)nsp);
+            if (b - a + 1 <= 32) {
+                klen = b - a + 1;
+                uint4 k0, k1;
+                win_take32(w, a, klen, &k0, &k1);
+                h = bytes_hash_words(k0, k1, klen);
+                uint4 *dst = reinterpret_cast<uint4 *>(arena + short_base + 32 * j);
+                dst[0] = k0;
+                dst[1] = k1;
+                key_off[j] = short_base + 32 * j;
+                fast = true;
             }
         }
-        if (!fast) {
-            u64 n = L;
-            const u8 *p = col + s;
-            while (n > 0 && (p[n - 1] == '\n' || p[n - 1] == '\r')) --n;
-            const Span sp = dup_field(p, n, 0, arena + s);
-            key_off[j] = s + sp.off;
-            klen = (u32)sp.len;
-            if (klen) h = bytes_hash(arena + s + sp.off, sp.len, 0);
+    }
+    if (!fast) {
+        u64 n = L;
+        const u8 *p = col + s;
+        while (n > 0 && (p[n - 1] == '\n' || p[n - 1] == '\r')) --n;
+        const Span sp = dup_field(p, n, 0, arena + s);
+        key_off[j] = s + sp.off;
+        klen = (u32)sp.len;
+        if (klen) h = bytes_hash(arena + s + sp.off, sp.len, 0);
+    }
+    key_len[j] = klen;
+    if (klen == 0) {
+        key_slot[j] = ~0ull;
+        return;
+    }
+    if (h == 0) h = 0x8000000000000000ULL;
+    u32 b = (u32)(((h >> 32) * (u64)AK_NB) >> 32);
+    u64 ks = ~0ull;
+#pragma unroll
+    for (int p = 0; p < 2 && ks == ~0ull; ++p) {
+        const u32 base = b * 4;
+        const ulonglong2 q0 = *reinterpret_cast<const ulonglong2 *>(&lh[base]);
+        const ulonglong2 q1 = *reinterpret_cast<const ulonglong2 *>(&lh[base + 2]);
+        const u64 kk[4] = {q0.x, q0.y, q1.x, q1.y};
+        u32 hit = kk[0] == h ? 0u : (kk[1] == h ? 1u : (kk[2] == h ? 2u : (kk[3] == h ? 3u : 4u)));
+        if (hit < 4) {
+            atomicAdd(&lc[base + hit], 1u);
+            ks = AK_LOCAL | (base + hit);
+            break;
         }
-        key_len[j] = klen;
-        if (klen == 0) {
-            key_slot[j] = ~0ull;
-            continue;
-        }
-        if (h == 0) h = 0x8000000000000000ULL;
-        u32 q = (u32)(h >> 20) & (AK_SLOTS - 1);
-        bool done = false;
-        for (u32 probe = 0; probe < 32; ++probe) {
-            u64 cur = lh[q];
-            if (cur == 0) {
-                cur = atomicCAS((unsigned long long *)&lh[q], 0ull, (unsigned long long)h);
-                if (cur == 0) {
-                    lrep[q] = j;
-                    cur = h;
-                }
-            }
-            if (cur == h) {
-                atomicAdd(&lc[q], 1u);
-                key_slot[j] = AK_LOCAL | q;
-                done = true;
+        for (u32 i = 0; i < 4; ++i) {
+            if (kk[i] != 0) continue;
+            const u64 old = atomicCAS((unsigned long long *)&lh[base + i], 0ull, (unsigned long long)h);
+            if (old == 0) lrep[base + i] = (u32)j;
+            if (old == 0 || old == h) {
+                atomicAdd(&lc[base + i], 1u);
+                ks = AK_LOCAL | (base + i);
                 break;
             }
-            q = (q + 1) & (AK_SLOTS - 1);
         }
-        if (!done) key_slot[j] = h_insert(atab, amask, h, 1, j, alist, alist_cap, &ctr->a_claimed, ctr, OVF_A);
+        b = (b + 1 == AK_NB) ? 0 : b + 1;
     }
+    if (ks == ~0ull) {  // the workgroup's table is full: straight to HBM
+        const u64 g = h_insert(atab, amask, h, 1, j, alist, alist_cap, &ctr->a_claimed, ctr, OVF_A);
+        ks = g == ~0ull ? ~0ull : (g | AK_VREP);
+    }
+    key_slot[j] = ks;
+}
+
+template <bool LINES>
+__global__ __launch_bounds__(AK_T) void k_artist_key(const u8 *__restrict__ col, const u64 *__restrict__ ar_start,
+                                                     const u64 *__restrict__ line_off,
+                                                     const u64 *__restrict__ line_len, u64 hdr, u64 nrec,
+                                                     u8 *__restrict__ arena, u64 *__restrict__ key_off,
+                                                     u32 *__restrict__ key_len, u64 *__restrict__ key_slot, u64 *atab,
+                                                     u64 amask, u32 *alist, u64 alist_cap, Counters *ctr,
+                                                     u64 short_base, int abl) {
+    __shared__ u64 lh[AK_SLOTS];   // key hash; after the flush: the global slot
+    __shared__ u32 lc[AK_SLOTS];   // count
+    __shared__ u32 lrep[AK_SLOTS]; // the workgroup's first record with this hash
+    __shared__ u32 songs_wg;
+    for (u32 i = threadIdx.x; i < AK_SLOTS; i += AK_T) { lh[i] = 0; lc[i] = 0; }
+    if (threadIdx.x == 0) songs_wg = 0;
     __syncthreads();
+    const u64 stride = (u64)gridDim.x * AK_T;
+    u32 songs = 0;
+    // AK_B records per thread and step, their loads issued together (memory-
+    // level parallelism: each record is a chain of dependent loads)
+#define AK_B 2
+    for (u64 jb = (u64)blockIdx.x * AK_T + threadIdx.x; jb < nrec; jb += AK_B * stride) {
+    u64 sB[AK_B], LB[AK_B];
+    Win64 wB[AK_B];
+#pragma unroll
+    for (int u = 0; u < AK_B; ++u) {
+        const u64 j = jb + u * stride;
+        sB[u] = 0;
+        LB[u] = 0;
+        if (j < nrec) {
+            if (LINES) {
+                LB[u] = line_len[j];
+                sB[u] = hdr + line_off[j];
+            } else {
+                sB[u] = ar_start[j];
+                LB[u] = ar_start[j + 1] - sB[u];  // the record incl. its terminator
+            }
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < AK_B; ++u) wB[u] = load_win64(col, sB[u]);  // in bounds for every record (padding)
+#pragma unroll
+    for (int u = 0; u < AK_B; ++u) {
+        const u64 j = jb + u * stride;
+        if (j < nrec)
+            artist_one<LINES>(j, sB[u], LB[u], wB[u], col, arena, key_off, key_len, key_slot, atab, amask, alist,
+                              alist_cap, ctr, short_base, lh, lc, lrep, songs);
+    }
+    }
+    if (LINES && songs) atomicAdd(&songs_wg, songs);
+    __syncthreads();
+    // one HBM insert per distinct key of the workgroup
     for (u32 i = threadIdx.x; i < AK_SLOTS; i += AK_T) {
         const u32 cnt = lc[i];
-        if (cnt) lrep[i] = h_insert(atab, amask, lh[i], cnt, lrep[i], alist, alist_cap, &ctr->a_claimed, ctr, OVF_A);
+        if (cnt) {  // MSA_ABLATE 512: no HBM inserts (diagnostic, results invalid; no slot is used)
+            lh[i] = (abl & 512) ? ~0ull
+                                : h_insert(atab, amask, lh[i], cnt, lrep[i], alist, alist_cap, &ctr->a_claimed, ctr, OVF_A);
+        }
     }
+    if (LINES && threadIdx.x == 0 && songs_wg) atomicAdd((unsigned long long *)&ctr->songs, (unsigned long long)songs_wg);
     __syncthreads();
-    for (u64 j = (u64)blockIdx.x * AK_T + threadIdx.x; j < nrec; j += stride) {
-        const u64 k = key_slot[j];
-        if (k != ~0ull && (k & AK_LOCAL)) key_slot[j] = lrep[k & (AK_SLOTS - 1)];
+    // global slots; every record's bytes against its workgroup representative
+    for (u64 jb = (u64)blockIdx.x * AK_T + threadIdx.x; jb < nrec; jb += AK_B * stride) {
+        u64 kB[AK_B];
+#pragma unroll
+        for (int u = 0; u < AK_B; ++u) kB[u] = jb + u * stride < nrec ? key_slot[jb + u * stride] : ~0ull;
+        u64 oa[AK_B], ob[AK_B];
+        u32 na[AK_B], nb[AK_B];
+        bool cmp[AK_B];
+#pragma unroll
+        for (int u = 0; u < AK_B; ++u) {
+            const u64 j = jb + u * stride, k = kB[u];
+            cmp[u] = false;
+            if (k == ~0ull || !(k & AK_LOCAL)) continue;
+            const u32 q = (u32)(k & (AK_SLOTS - 1));
+            const u64 g = lh[q];
+            if (g == ~0ull) {  // the HBM table overflowed: the run is repeated with a bigger table
+                key_slot[j] = ~0ull;
+                continue;
+            }
+            const u32 rep = lrep[q];
+            if (rep == (u32)j) {
+                key_slot[j] = g | AK_VREP;
+            } else {
+                key_slot[j] = g;
+                cmp[u] = true;
+                oa[u] = key_off[j];
+                na[u] = key_len[j];
+                ob[u] = key_off[rep];
+                nb[u] = key_len[rep];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < AK_B; ++u)
+            if (cmp[u] && !(abl & 256) && !keys_equal(arena, oa[u], na[u], ob[u], nb[u]))
+                atomicAdd((unsigned long long *)&ctr->collision, 1ull);
     }
+}
+
+// The artist pass when artist.csv lines are its records: count the keys
+// k_rec_spans built.  One workgroup per CU counts a contiguous range of
+// records in an LDS table (64-bit hash h1; per slot the count, the sum of the
+// second hashes h2 and the first record); each distinct key then goes to the
+// HBM table once per workgroup, flushes staggered so that the workgroups do
+// not all hit the same keys at once.  A slot whose sum of h2 is not
+// count x h2(first record) holds two different keys: reported, never merged
+// silently (k_artist_h2_check does the same for the HBM table).
+#define AC_T 1024
+#define AC_SLOTS 6144
+#define AC_NB (AC_SLOTS / 4)
+static_assert(AC_SLOTS * 24 + 16 <= 160 * 1024, "artist count LDS exceeds the CU");
+
+__global__ __launch_bounds__(AC_T) void k_artist_count(const u64 *__restrict__ line_len,
+                                                       const u32 *__restrict__ key_len, const u64 *__restrict__ kh1,
+                                                       const u64 *__restrict__ kh2, u64 nrec, u64 *atab, u64 amask,
+                                                       u32 *alist, u64 alist_cap, Counters *ctr) {
+    __shared__ u64 lh[AC_SLOTS];
+    __shared__ u64 lsum[AC_SLOTS];
+    __shared__ u32 lc[AC_SLOTS];
+    __shared__ u32 lrep[AC_SLOTS];
+    __shared__ u32 songs_wg;
+    for (u32 i = threadIdx.x; i < AC_SLOTS; i += AC_T) { lh[i] = 0; lsum[i] = 0; lc[i] = 0; }
+    if (threadIdx.x == 0) songs_wg = 0;
+    __syncthreads();
+    const u64 per = (nrec + gridDim.x - 1) / gridDim.x;
+    const u64 r0 = (u64)blockIdx.x * per, r1 = min(nrec, r0 + per);
+    u32 songs = 0;
+    for (u64 r = r0 + threadIdx.x; r < r1; r += AC_T) {
+        if (!line_len[r]) continue;  // no line: no artist.csv record
+        ++songs;
+        const u32 klen = key_len[r];
+        if (!klen) continue;         // empty name: a song, not an artist
+        u64 h = kh1[r];
+        const u64 h2 = kh2[r];
+        if (h == 0) h = 0x8000000000000000ULL;
+        u32 b = (u32)(((h >> 32) * (u64)AC_NB) >> 32);
+        bool done = false;
+#pragma unroll
+        for (int p = 0; p < 2 && !done; ++p) {
+            const u32 base = b * 4;
+            const ulonglong2 q0 = *reinterpret_cast<const ulonglong2 *>(&lh[base]);
+            const ulonglong2 q1 = *reinterpret_cast<const ulonglong2 *>(&lh[base + 2]);
+            const u64 kk[4] = {q0.x, q0.y, q1.x, q1.y};
+            u32 i = kk[0] == h ? 0u : (kk[1] == h ? 1u : (kk[2] == h ? 2u : (kk[3] == h ? 3u : 4u)));
+            if (i == 4) {
+                for (u32 e = 0; e < 4 && !done; ++e) {
+                    if (kk[e] != 0) continue;
+                    const u64 old = atomicCAS((unsigned long long *)&lh[base + e], 0ull, (unsigned long long)h);
+                    if (old == 0) lrep[base + e] = (u32)(r - r0);
+                    if (old == 0 || old == h) { i = e; done = true; }
+                }
+            } else {
+                done = true;
+            }
+            if (done) {
+                atomicAdd(&lc[base + i], 1u);
+                atomicAdd((unsigned long long *)&lsum[base + i], (unsigned long long)h2);
+            }
+            b = (b + 1 == AC_NB) ? 0 : b + 1;
+        }
+        if (!done)  // the workgroup's table is full: straight to HBM
+            h_insert2(atab, amask, h, 1, r, h2, alist, alist_cap, &ctr->a_claimed, ctr, OVF_A);
+    }
+    if (songs) atomicAdd(&songs_wg, songs);
+    __syncthreads();
+    if (threadIdx.x == 0 && songs_wg) atomicAdd((unsigned long long *)&ctr->songs, (unsigned long long)songs_wg);
+    // flush, each workgroup starting at its own offset in the slot array
+    const u32 rot = (u32)(((u64)blockIdx.x * AC_SLOTS) / gridDim.x);
+    for (u32 t = threadIdx.x; t < AC_SLOTS; t += AC_T) {
+        u32 i = t + rot;
+        if (i >= AC_SLOTS) i -= AC_SLOTS;
+        const u32 cnt = lc[i];
+        if (!cnt) continue;
+        const u64 rep = r0 + lrep[i];
+        if (lsum[i] != (u64)cnt * kh2[rep]) atomicAdd((unsigned long long *)&ctr->collision, 1ull);
+        h_insert2(atab, amask, lh[i], cnt, rep, lsum[i], alist, alist_cap, &ctr->a_claimed, ctr, OVF_A);
+    }
+}
+
+// Every HBM artist entry: sum of h2 == count x h2(representative).
+__global__ void k_artist_h2_check(const u64 *__restrict__ atab, const u32 *__restrict__ alist, u64 cap,
+                                  const u64 *__restrict__ kh2, Counters *ctr) {
+    const u64 e = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= cap || e >= ctr->a_claimed) return;
+    const u64 *slot = atab + 4 * (u64)alist[e];
+    if (slot[3] != slot[1] * kh2[slot[2]]) atomicAdd((unsigned long long *)&ctr->collision, 1ull);
+}
+
+// Workgroup representatives (and records inserted straight into HBM) against
+// the HBM table's representative.
+__global__ void k_artist_verify_reps(const u8 *__restrict__ arena, const u64 *__restrict__ key_off,
+                                     const u32 *__restrict__ key_len, u64 *__restrict__ key_slot, u64 nrec,
+                                     const u64 *__restrict__ atab, Counters *ctr) {
+    const u64 j = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= nrec) return;
+    const u64 k = key_slot[j];
+    if (k == ~0ull || !(k & AK_VREP)) return;
+    const u64 slot = k & AK_SLOTMASK;
+    key_slot[j] = slot;
+    const u64 rep = atab[4 * slot + 2];
+    if (rep == j) return;
+    if (!keys_equal(arena, key_off[j], key_len[j], key_off[rep], key_len[rep]))
+        atomicAdd((unsigned long long *)&ctr->collision, 1ull);
 }
 
 __global__ void k_artist_verify(const u8 *__restrict__ arena, const u64 *__restrict__ key_off,
@@ -1098,10 +1435,11 @@ __global__ void k_blob_write(const u32 *__restrict__ order, u64 n, const u64 *__
 static inline dim3 grid1(u64 n, u32 t = 256) { return dim3((u32)((n + t - 1) / t)); }
 
 hipError_t msa_launch_rec_spans(const u8 *buf, const u64 *rs, const u32 *nul, u64 nrec, u64 first_rec, int text,
-                                u64 *alen, u64 *asrc, u32 *apairs, u64 *tlen, u64 *tsrc, u32 *tpairs, hipStream_t s) {
+                                u64 *alen, u64 *asrc, u32 *apairs, u64 *tlen, u64 *tsrc, u32 *tpairs, Counters *ctr,
+                                const AKeys &ak, hipStream_t s) {
     if (nrec)
         hipLaunchKernelGGL(k_rec_spans, grid1(nrec), dim3(256), 0, s, buf, rs, nul, nrec, first_rec, text, alen, asrc,
-                           apairs, tlen, tsrc, tpairs);
+                           apairs, tlen, tsrc, tpairs, ctr, ak);
     return hipGetLastError();
 }
 hipError_t msa_launch_col_write(int text, const u8 *buf, const u64 *len, const u64 *off, const u64 *src,
@@ -1118,16 +1456,36 @@ hipError_t msa_launch_col_write(int text, const u8 *buf, const u64 *len, const u
     hipLaunchKernelGGL(k_col_collapse, grid1(nrec), dim3(256), 0, s, buf, len, off, src, pairs, nrec, hdr, col);
     return hipGetLastError();
 }
-hipError_t msa_launch_artist_key(const u8 *col, const u64 *ar_start, u64 nrec, u8 *arena,
-                                 u64 *key_off, u32 *key_len, u64 *key_slot, u64 *atab, u64 amask, u32 *alist,
-                                 u64 alist_cap, Counters *ctr, u64 short_base, hipStream_t s) {
+hipError_t msa_launch_artist_key(const u8 *col, const u64 *ar_start, const u64 *line_off, const u64 *line_len, u64 hdr,
+                                 u64 nrec, u8 *arena, u64 *key_off, u32 *key_len, u64 *key_slot, u64 *atab, u64 amask,
+                                 u32 *alist, u64 alist_cap, Counters *ctr, u64 short_base, int cus, int abl,
+                                 hipStream_t s) {
     if (nrec) {
         u64 blocks = (nrec + AK_T - 1) / AK_T;
-        if (blocks > AK_BLOCKS) blocks = AK_BLOCKS;
-        hipLaunchKernelGGL(k_artist_key, dim3((u32)blocks), dim3(AK_T), 0, s, col, ar_start, nrec, arena,
-                           key_off, key_len, key_slot, atab, amask, alist, alist_cap, ctr, short_base);
-        hipLaunchKernelGGL(k_artist_verify, grid1(nrec), dim3(256), 0, s, (const u8 *)arena, key_off, key_len,
+        if (blocks > (u64)cus) blocks = (u64)cus;  // one workgroup (one LDS table) per CU
+        if (line_len)
+            hipLaunchKernelGGL(k_artist_key<true>, dim3((u32)blocks), dim3(AK_T), 0, s, col, ar_start, line_off,
+                               line_len, hdr, nrec, arena, key_off, key_len, key_slot, atab, amask, alist, alist_cap,
+                               ctr, short_base, abl);
+        else
+            hipLaunchKernelGGL(k_artist_key<false>, dim3((u32)blocks), dim3(AK_T), 0, s, col, ar_start, line_off,
+                               line_len, hdr, nrec, arena, key_off, key_len, key_slot, atab, amask, alist, alist_cap,
+                               ctr, short_base, abl);
+        hipLaunchKernelGGL(k_artist_verify_reps, grid1(nrec), dim3(256), 0, s, (const u8 *)arena, key_off, key_len,
                            key_slot, nrec, (const u64 *)atab, ctr);
+    }
+    return hipGetLastError();
+}
+hipError_t msa_launch_artist_count(const u64 *line_len, const u32 *key_len, const u64 *kh1, const u64 *kh2, u64 nrec,
+                                   u64 *atab, u64 amask, u32 *alist, u64 alist_cap, Counters *ctr, int cus,
+                                   hipStream_t s) {
+    if (nrec) {
+        u64 blocks = (nrec + AC_T - 1) / AC_T;
+        if (blocks > (u64)cus) blocks = (u64)cus;
+        hipLaunchKernelGGL(k_artist_count, dim3((u32)blocks), dim3(AC_T), 0, s, line_len, key_len, kh1, kh2, nrec, atab,
+                           amask, alist, alist_cap, ctr);
+        hipLaunchKernelGGL(k_artist_h2_check, grid1(alist_cap), dim3(256), 0, s, (const u64 *)atab, (const u32 *)alist,
+                           alist_cap, kh2, ctr);
     }
     return hipGetLastError();
 }

@@ -128,6 +128,66 @@ __device__ __forceinline__ u64 h_insert(u64 *tab, u64 mask, u64 hash, u64 cnt, u
     return ~0ull;
 }
 
+// Artist-key hashes of the lines shortcut (k_rec_spans -> k_artist_count):
+// two independent 64-bit hashes, each a sum of per-position products of the
+// key's little-endian 8-byte words (zero padded) folded by fmix64 every 32
+// bytes -- cheap enough for one hash pair per record.  The word and byte
+// forms agree for every key.
+__host__ __device__ __forceinline__ u64 akey_fold(u64 h, u64 w0, u64 w1, u64 w2, u64 w3, int second) {
+    if (!second)
+        return fmix64(h + w0 * 0x9E3779B97F4A7C15ULL + w1 * 0xC2B2AE3D27D4EB4FULL + w2 * 0x165667B19E3779F9ULL +
+                      w3 * 0xD6E8FEB86659FD93ULL);
+    return fmix64(h ^ (w0 * 0xFF51AFD7ED558CCDULL + w1 * 0xC4CEB9FE1A85EC53ULL + w2 * 0x9FB21C651E98DF25ULL +
+                       w3 * 0xBF58476D1CE4E5B9ULL));
+}
+__host__ __device__ __forceinline__ u64 akey_seed(u64 n, int second) {
+    return second ? (0x6A09E667F3BCC909ULL ^ (n * 0xBB67AE8584CAA73BULL)) : (n * 0x94D049BB133111EBULL + 0x243F6A8885A308D3ULL);
+}
+__device__ __forceinline__ u64 akey_hash_bytes(const u8 *p, u64 n, int second) {
+    u64 h = akey_seed(n, second);
+    for (u64 b = 0; b < n || b == 0; b += 32) {
+        u64 w[4] = {0, 0, 0, 0};
+        for (u32 i = 0; i < 32 && b + i < n; ++i) w[i >> 3] |= (u64)p[b + i] << (8 * (i & 7));
+        h = akey_fold(h, w[0], w[1], w[2], w[3], second);
+        if (n == 0) break;
+    }
+    return h;
+}
+
+// H-table insert for artist keys with the second hash: sum2 (the sum of h2
+// over the occurrences added) accumulates in the slot's 4th word, so the
+// table can check sum2 == count * h2(rep) afterwards (k_artist_h2_check).
+__device__ __forceinline__ u64 h_insert2(u64 *tab, u64 mask, u64 hash, u64 cnt, u64 rep, u64 sum2, u32 *list,
+                                         u64 list_cap, u64 *claimed, Counters *ctr, u64 ovf_bit) {
+    if (hash == 0) hash = 0x8000000000000000ULL;
+    u64 h = hash & mask;
+    for (u32 probe = 0; probe < MSA_MAX_PROBE; ++probe) {
+        u64 *slot = tab + 4 * h;
+        u64 cur = ld_relaxed(slot);
+        if (cur == 0) {
+            u64 old = atomicCAS((unsigned long long *)slot, 0ull, (unsigned long long)hash);
+            if (old == 0) {
+                __hip_atomic_store(slot + 2, rep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                atomicAdd((unsigned long long *)(slot + 1), (unsigned long long)cnt);
+                atomicAdd((unsigned long long *)(slot + 3), (unsigned long long)sum2);
+                u64 i = atomicAdd((unsigned long long *)claimed, 1ull);
+                if (i < list_cap) list[i] = (u32)h;
+                else atomicOr((unsigned long long *)&ctr->overflow, (unsigned long long)ovf_bit);
+                return h;
+            }
+            cur = old;
+        }
+        if (cur == hash) {
+            atomicAdd((unsigned long long *)(slot + 1), (unsigned long long)cnt);
+            atomicAdd((unsigned long long *)(slot + 3), (unsigned long long)sum2);
+            return h;
+        }
+        h = (h + 1) & mask;
+    }
+    atomicOr((unsigned long long *)&ctr->overflow, (unsigned long long)ovf_bit);
+    return ~0ull;
+}
+
 // 64-bit hash of a byte string (lower-cased when `lower`), for the H-table.
 __device__ __forceinline__ u64 bytes_hash(const u8 *p, u64 n, int lower) {
     u64 h = 0x243F6A8885A308D3ULL ^ (n * 0x9E3779B97F4A7C15ULL);

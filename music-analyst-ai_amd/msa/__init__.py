@@ -42,7 +42,7 @@ EXPORTS = [
     "msa_count", "msa_rank", "msa_run", "msa_get_summary", "msa_get_ranked",
     "msa_write_table_csv", "msa_get_split_column", "msa_set_profiling", "msa_get_profile",
     "msa_set_shard", "msa_piece_size", "msa_shard_function", "msa_shard_head", "msa_segment_copy",
-    "msa_segment_set", "msa_export_partitions", "msa_export_copy", "msa_import_partitions",
+    "msa_segment_set", "msa_artist_reader_needed", "msa_set_artist_reader", "msa_export_partitions", "msa_export_copy", "msa_import_partitions",
     "msa_wcs_create", "msa_wcs_destroy", "msa_wcs_last_error", "msa_wcs_stream", "msa_wcs_load_csv",
     "msa_wcs_set_table_bits", "msa_wcs_run", "msa_wcs_get_summary", "msa_wcs_get_csv", "msa_wcs_write_outputs",
     "msa_csvcol_run", "msa_csvcol_header", "msa_csvcol_get",
@@ -140,6 +140,8 @@ def load(path: str = LIB_PATH):
     lib.msa_shard_head.argtypes = [vp, i, vp, i, C.POINTER(u64), C.POINTER(u64)]
     lib.msa_segment_copy.argtypes = [vp, i, u64, u64, vp]
     lib.msa_segment_set.argtypes = [vp, i, u64, vp, u64]
+    lib.msa_artist_reader_needed.argtypes = [vp, C.POINTER(i)]
+    lib.msa_set_artist_reader.argtypes = [vp, i]
     lib.msa_export_partitions.argtypes = [vp, i, i, C.POINTER(u64)]
     lib.msa_export_copy.argtypes = [vp, vp]
     lib.msa_import_partitions.argtypes = [vp, i, vp, C.POINTER(u64), i]
@@ -284,6 +286,14 @@ class Context:
 
     def segment_set(self, piece: int, skip: int, tail_ptr: int = 0, tail_len: int = 0):
         self._check(self.lib.msa_segment_set(self.h, piece, skip, C.c_void_p(tail_ptr or None), tail_len))
+
+    def artist_reader_needed(self) -> bool:
+        v = C.c_int()
+        self._check(self.lib.msa_artist_reader_needed(self.h, C.byref(v)))
+        return bool(v.value)
+
+    def set_artist_reader(self, exact: bool):
+        self._check(self.lib.msa_set_artist_reader(self.h, int(exact)))
 
     def export_partitions(self, table: int, nparts: int) -> List[int]:
         out = (C.c_uint64 * nparts)()

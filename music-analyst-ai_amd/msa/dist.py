@@ -153,7 +153,13 @@ def run_sharded(ctx, comm: Comm, text_column: bool = True) -> Tuple[int, int]:
     ctx.set_shard(comm.rank == 0)
     resolve_piece(ctx, comm, PIECE_CSV)
     ctx.split_columns(text_column)
-    resolve_piece(ctx, comm, PIECE_ARTISTS)
+    # artist.csv lines are its records on every rank unless some rank's split
+    # says otherwise; then every rank runs the exact reader on resolved pieces
+    if comm.all_reduce_sum([int(ctx.artist_reader_needed())])[0]:
+        ctx.set_artist_reader(True)
+        resolve_piece(ctx, comm, PIECE_ARTISTS)
+    else:
+        ctx.set_artist_reader(False)
     ctx.count()
     s = ctx.summary()
     merge_table(ctx, comm, MSA_TABLE_WORDS)
