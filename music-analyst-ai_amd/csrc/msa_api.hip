@@ -148,6 +148,7 @@ struct msa_ctx {
     u64 nrec_a = 0;
     // tables
     DevBuf s_tab, s_list, m_tab, m_list, l_pos, l_len, l_slot, l_tab, l_list, a_tab, a_list;
+    DevBuf mlog, mlog_n;  // K3's logged LDS-table misses (k_miss_agg)
     u64 s_slots = 0, m_slots = 0, l_occ_cap = 0, lt_slots = 0, a_slots = 0;
     u64 s_used_prev = 0, m_used_prev = 0, lt_used_prev = 0, a_used_prev = 0;
     // Table capacities (log2 slots / occurrence capacity).  They start small --
@@ -615,6 +616,15 @@ static int split_once(msa_ctx *c, int flags) {
     a.want_nul = want_text ? 1 : 0;
     a.ablate = c->ablate;
     a.first_rec = c->cont ? 0 : 1;
+    {  // miss logs: room for about a quarter of the tokens (a full partition falls back to HBM inserts)
+        const u64 parts = (u64)c->cus * MSA_MLOG_PARTS;
+        const u64 entries = std::max<u64>(parts * 1024, c->n / 16);
+        a.mlog_cap = (u32)std::min<u64>(entries / parts, 1u << 30);
+        HIPC(c, ensure(c->mlog, parts * a.mlog_cap * 16));
+        HIPC(c, ensure(c->mlog_n, parts * 4));
+        a.mlog = c->mlog.as<ulonglong2>();
+        a.mlog_n = c->mlog_n.as<u32>();
+    }
     prof_begin(c, ST_CSV_SCAN);
     // k_scan_csv (msa_k3.hip); MSA_ABLATE bit 64 selects the round-1 kernel (A/B runs)
     if (c->ablate & 64) HIPC(c, msa_launch_scan(a, 0, c->stream));
@@ -982,7 +992,7 @@ void msa_destroy(msa_ctx *c) {
                      &c->nulrel, &c->acol, &c->alen, &c->aoff, &c->asrc, &c->apairs, &c->tcol, &c->tlen, &c->toff, &c->tsrc, &c->tpairs,
                      &c->scan_bsum, &c->scan_total, &c->ar_start, &c->arena, &c->key_off,
                      &c->key_len, &c->key_slot, &c->s_tab, &c->s_list, &c->m_tab, &c->m_list, &c->l_pos, &c->l_len,
-                     &c->l_slot, &c->l_tab, &c->l_list, &c->a_tab, &c->a_list, &c->ctr, &c->kh1, &c->kh2};
+                     &c->l_slot, &c->l_tab, &c->l_list, &c->a_tab, &c->a_list, &c->ctr, &c->kh1, &c->kh2, &c->mlog, &c->mlog_n};
     for (DevBuf *b : all) release(*b);
     for (Ranked *R : {&c->rw, &c->ra}) {
         for (auto &s : R->K)

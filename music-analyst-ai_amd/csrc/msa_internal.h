@@ -292,8 +292,15 @@ struct ScanArgs {
     Counters *ctr;
     int want_nul;    // record the first NUL of each record (text column)
     int ablate;
-    u32 first_rec;   // records before this index are not data (the header: 1; a continuation shard: 0)      // diagnostic builds only (MSA_ABLATE env): see msa_scan.hip
+    u32 first_rec;   // records before this index are not data (the header: 1; a continuation shard: 0)
+    // K3 misses of the LDS word table, logged per (workgroup, key partition)
+    // for k_miss_agg (MSA_MLOG_PARTS partitions, mlog_cap entries each)
+    ulonglong2 *mlog;
+    u32 *mlog_n;
+    u32 mlog_cap;      // diagnostic builds only (MSA_ABLATE env): see msa_scan.hip
 };
+
+#define MSA_MLOG_PARTS 16
 
 // A long-token position with this bit set indexes the context's side buffer
 // (text.csv header-label remainder, see do_split) instead of the CSV.

@@ -13,34 +13,34 @@
 //     comma count) is a handful of ballots per 4 KiB;
 //   * per-record structure is computed per lane segment (between record
 //     terminators) with bit arithmetic, not per byte;
-//   * the iteration's bytes are staged in a per-wave LDS ring; each lane walks
-//     its own token starts, reads the key (<= 16 bytes) from the ring and
-//     counts it in ONE workgroup-wide LDS table of 16-byte keys (4-slot
-//     buckets read with four ds_read_b128); keys the LDS table cannot hold
-//     are batched per wave and inserted into the HBM tables 64 at a time.
+//   * the wave's token starts go to a per-wave LDS list; the lanes take them
+//     64 at a time, re-read each key (<= 16 bytes) from the just-loaded input
+//     (L1/L2) and count it in ONE workgroup-wide LDS table of 16-byte keys
+//     (4-slot buckets); keys the LDS table cannot hold are batched per wave
+//     and inserted into the HBM tables asynchronously (pipelined loads).
 #include "msa_internal.h"
 #include "msa_tables.h"
+
+#include <algorithm>
 
 namespace {
 
 #define Q_T 1024                 // 16 waves: one workgroup per CU
 #define Q_W (Q_T / 64)
 #define Q_BLK 4096               // bytes per wave-iteration
-// Q_GKEY 1: token keys are re-read from the input (L1/L2-resident, just
-// loaded) instead of an LDS copy of the block, which leaves the LDS to the
-// word table (7368 instead of 4064 slots: fewer HBM misses)
-#ifndef Q_GKEY
-#define Q_GKEY 1
-#endif
-#define Q_RING (Q_GKEY ? 0 : Q_BLK + 32)  // + the next block's first 16 bytes (+ slack)
-#define Q_MISS 64                // deferred HBM inserts per wave (16 B each)
-#define Q_WLDS (Q_RING + Q_MISS * 16)
+// Token keys are re-read from the input (just loaded: L1/L2) rather than
+// from an LDS copy of the block, which leaves the LDS to the word table and
+// to a per-wave list of the block's token starts: the lanes share the tokens
+// evenly (compaction) instead of each walking its own.
+#define Q_LIST 1024              // token entries per wave-iteration (>= 4 bytes per token)
+#define Q_MISS 32                // deferred HBM inserts per wave (16 B each)
+#define Q_WLDS (Q_LIST * 2 + Q_MISS * 16)
 #ifndef Q_SLOTS
-#define Q_SLOTS (Q_GKEY ? 7368 : 4064)  // LDS word table: 16-byte keys + u32 counts
+#define Q_SLOTS 6140             // LDS word table: 16-byte keys + u32 counts
 #endif
 #define Q_NB (Q_SLOTS / 4)
 #define Q_TAB (Q_SLOTS * 20)
-#define Q_LDS (Q_TAB + Q_W * Q_WLDS)
+#define Q_LDS (Q_TAB + Q_W * Q_WLDS + MSA_MLOG_PARTS * 4)
 static_assert(Q_LDS <= 163840, "K3 LDS exceeds the CU's 160 KiB");
 static_assert(Q_SLOTS % 4 == 0 && Q_TAB % 16 == 0 && Q_WLDS % 16 == 0, "LDS carve-outs stay 16-byte aligned");
 
@@ -103,8 +103,7 @@ __device__ __forceinline__ u32 lower_tok(u32 &x) {
 }
 
 // Byte classes of the lane's 64 bytes (bit i = byte i; bytes at or past
-// `nvalid` cleared); lower-cases the bytes in place (they feed only the key
-// ring).  '\r' and NUL masks are computed only when the wave's block holds
+// `nvalid` cleared).  '\r' and NUL masks are computed only when the wave's block holds
 // one (a wave-uniform branch).
 __device__ __forceinline__ Masks classify64x(uint4 (&v)[4], u32 nvalid) {
     Masks k{0, 0, 0, 0, 0, 0};
@@ -155,10 +154,6 @@ __device__ __forceinline__ u64 pxor_ex64(u64 q) {  // bit j = parity of bits < j
     return x;
 }
 
-// Physical u64 index of logical ring word wi (the chunk swizzle of the ring
-// writes; the tail words 512.. map to themselves).
-__device__ __forceinline__ u32 ring_word(u32 wi) { return wi ^ (((wi >> 5) & 3u) << 1); }
-
 // 128-bit (hi:lo) >> k, low 64 bits, 0 < k < 64
 __device__ __forceinline__ u64 shr128(u64 lo, u64 hi, u32 k) { return (lo >> k) | (hi << (64 - k)); }
 
@@ -198,40 +193,26 @@ __device__ __forceinline__ void hbm_insert16(const ScanArgs &a, u64 k0, u64 k1m,
     else m_insert<false>(a.m_tab, a.m_mask, k0, k1m & ~KMARK, cnt, a.m_list, a.m_list_cap, a.ctr);
 }
 
-// Deferred HBM inserts, pipelined: a flush hands the wave's LDS miss buffer
-// (<= 64 keys, one per lane) to registers and issues the load of each key's
-// home slot in the HBM table WITHOUT waiting for it; the next flush (or the
-// kernel end) completes them -- a home slot that already holds the key (the
-// Zipf tail, after warm-up) costs one fire-and-forget atomic add, anything
-// else (empty, other key, unpublished) takes the full insert protocol.
-struct Pending {
-    u64 k0, k1m;       // key (k1m == KMARK: 3..8-byte word)
-    ulonglong2 v;      // home slot's first 16 bytes as loaded
-    u64 *slot;         // home slot
-    bool on;
-};
-
-__device__ __forceinline__ void pend_complete(const ScanArgs &a, Pending &p) {
-    if (!p.on) return;
-    const bool sword = p.k1m == KMARK;
-    const bool ok = sword ? (p.v.x == p.k0) : (p.v.x == p.k0 && p.v.y == (p.k1m & ~KMARK));
-    if (ok) atomicAdd((unsigned long long *)(p.slot + (sword ? 1 : 2)), 1ull);
-    else hbm_insert16(a, p.k0, p.k1m, 1);
-    p.on = false;
+// Keys the LDS table cannot hold are not counted in HBM one atomic at a
+// time (scattered device-scope atomics run at a few tens of G/s chip-wide and
+// made up a third of the kernel).  They are logged instead: per workgroup and
+// key partition (16 by key hash), plain 16-byte stores behind an LDS cursor;
+// k_miss_agg then counts each partition in LDS and adds each distinct key to
+// the HBM table once per aggregating workgroup.  A full log partition falls
+// back to the direct insert.
+__device__ __forceinline__ u32 mlog_part(u64 k0, u64 k1m) {
+    return (u32)((k0 * 0xD6E8FEB86659FD93ull ^ k1m * 0x9E3779B97F4A7C15ull) >> 60);
 }
 
-__device__ __forceinline__ void flush_miss(const ScanArgs &a, const ulonglong2 *miss, u32 n, Pending &p) {
+__device__ __forceinline__ void flush_miss(const ScanArgs &a, const ulonglong2 *miss, u32 n, u32 *lcur) {
     wsync();
-    pend_complete(a, p);
     const u32 lane = lane_id();
     if (lane < n) {
         const ulonglong2 x = miss[lane];
-        p.k0 = x.x;
-        p.k1m = x.y;
-        if (x.y == KMARK) p.slot = a.s_tab + 2 * (fmix64(x.x) & a.s_mask);
-        else p.slot = a.m_tab + 4 * (fmix64(x.x ^ fmix64(x.y & ~KMARK)) & a.m_mask);
-        p.v = *reinterpret_cast<const ulonglong2 *>(p.slot);  // consumed at the next flush
-        p.on = true;
+        const u32 part = mlog_part(x.x, x.y);
+        const u32 at = atomicAdd(&lcur[part], 1u);
+        if (at < a.mlog_cap) a.mlog[((u64)blockIdx.x * MSA_MLOG_PARTS + part) * a.mlog_cap + at] = x;
+        else hbm_insert16(a, x.x, x.y, 1);
     }
     wsync();
 }
@@ -245,20 +226,17 @@ __global__ __launch_bounds__(Q_T, 1) void k_scan_csv(ScanArgs a) {
     const u32 lane = lane_id();
     const u32 wib = threadIdx.x >> 6;
     unsigned char *wl = smem + Q_TAB + wib * Q_WLDS;
-    u8 *ring = wl;
-    ulonglong2 *miss = reinterpret_cast<ulonglong2 *>(wl + Q_RING);
+    u16 *list = reinterpret_cast<u16 *>(wl);
+    ulonglong2 *miss = reinterpret_cast<ulonglong2 *>(wl + Q_LIST * 2);
     u32 nmiss = 0;  // wave-uniform
-    Pending pend;
-    pend.on = false;
-    pend.k0 = pend.k1m = 0;
-    pend.slot = nullptr;
-    pend.v = make_ulonglong2(0, 0);
     const u64 lt = (1ull << lane) - 1ull;
 
+    u32 *lcur = reinterpret_cast<u32 *>(smem + Q_TAB + Q_W * Q_WLDS);  // log cursors per key partition
     for (u32 i = threadIdx.x; i < Q_SLOTS; i += Q_T) {
         keys[i] = make_ulonglong2(0, 0);
         cnts[i] = 0;
     }
+    if (threadIdx.x < MSA_MLOG_PARTS) lcur[threadIdx.x] = 0;
     __syncthreads();
 
     const u32 gw = blockIdx.x * Q_W + wib;
@@ -292,22 +270,10 @@ __global__ __launch_bounds__(Q_T, 1) void k_scan_csv(ScanArgs a) {
 #pragma unroll
             for (int d = 0; d < 4; ++d) ttok |= pk4(lower_tok(tw[d])) << (4 * d);
             ttok &= tvm;
-            const uint4 tail_lc = make_uint4(tw[0], tw[1], tw[2], tw[3]);
             const u64 rem = cend > lpos ? cend - lpos : 0;
             const Masks k = classify64x(cur, (u32)min(rem, (u64)64));
-            // stage the block (+ tail) in the wave's ring for key extraction
-            wsync();
-            // swizzled: lane l's 16-byte chunk q sits at chunk 4l + (q ^ ((l >> 2) & 3)),
-            // so lanes whose rows share banks read different banks (ring_word)
-            if (!Q_GKEY) {
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    *reinterpret_cast<uint4 *>(ring + lane * 64 + 16 * (q ^ ((lane >> 2) & 3))) = cur[q];
-                if (lane == 0) *reinterpret_cast<uint4 *>(ring + Q_BLK) = tail_lc;
-            }
-
-            // the block's bytes now live in the ring and the masks: load the
-            // next block into the same registers (in flight during the rest)
+            // the block's bytes now live in the masks: load the next block into
+            // the same registers (in flight during the rest)
             if (more) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q) cur[q] = ldg16(a.buf + lpos + Q_BLK + 16 * q);
@@ -459,14 +425,15 @@ __global__ __launch_bounds__(Q_T, 1) void k_scan_csv(ScanArgs a) {
                 }
             }
 
-            // 3..16-byte words: every lane walks its own starts
-            wsync();
-            // diagnostic ablations (MSA_ABLATE; results invalid): 1 no tokens at
-            // all, 2 no walk, 32 walk without LDS table, 4 LDS misses dropped
+            // 3..16-byte words.  The wave's token starts go to its LDS list
+            // (block offset | (length - 3) << 12), then the lanes take them
+            // 64 at a time.  Diagnostic ablations (MSA_ABLATE; results
+            // invalid): 1 no tokens at all, 2 no counting, 32 keys without
+            // the LDS table, 4 LDS misses dropped
             u64 m = (a.ablate & 3) ? 0ull : sSM;
+            u32 ntok;
+            u32 li = wave_prefix<5>((u32)__popcll(m), ntok);
             while (__ballot(m != 0)) {
-                bool mis = false;
-                u64 k0 = 0, k1 = KMARK;
                 if (m) {
                     const u32 b = (u32)__ffsll((long long)m) - 1;
                     m &= m - 1;
@@ -475,30 +442,26 @@ __global__ __launch_bounds__(Q_T, 1) void k_scan_csv(ScanArgs a) {
                     const u32 d0 = (u32)w, d1 = (u32)(w >> 32), d2 = (u32)Tn;
                     const u32 run = __builtin_amdgcn_alignbit(b >= 32 ? d2 : d1, b >= 32 ? d1 : d0, b & 31u);
                     const u32 len = (u32)__ffs(~run) - 1;  // 3..16
-                    const u32 o = lane * 64 + b;
-                    u64 w0, w1, w2;
-                    u32 sh;
-                    if (Q_GKEY) {  // the input itself (just loaded: L1/L2), lower-cased below
-                        const u64 ap = lpos + b;
-                        const u64 *gw = reinterpret_cast<const u64 *>(a.buf + (ap & ~7ull));
-                        w0 = gw[0];
-                        w1 = gw[1];
-                        w2 = gw[2];
-                        sh = (u32)(ap & 7u) * 8u;
-                    } else {
-                        const u64 *rw = reinterpret_cast<const u64 *>(ring);
-                        const u32 wi = o >> 3;
-                        sh = (o & 7u) * 8u;
-                        w0 = rw[ring_word(wi)];
-                        w1 = rw[ring_word(wi + 1)];
-                        w2 = rw[ring_word(wi + 2)];
-                    }
+                    list[li++] = (u16)((lane * 64 + b) | ((len - 3) << 12));
+                }
+            }
+            wsync();
+            for (u32 t0 = 0; t0 < ntok; t0 += 64) {
+                bool mis = false;
+                u64 k0 = 0, k1 = KMARK;
+                if (t0 + lane < ntok) {
+                    const u32 e = list[t0 + lane];
+                    const u32 len = (e >> 12) + 3;
+                    const u64 ap = ib + (e & 4095u);
+                    const u64 *gw = reinterpret_cast<const u64 *>(a.buf + (ap & ~7ull));
+                    const u64 w0 = gw[0], w1 = gw[1], w2 = gw[2];
+                    const u32 sh = (u32)(ap & 7u) * 8u;
                     u64 x0 = sh ? ((w0 >> sh) | (w1 << (64 - sh))) : w0;
                     u64 x1 = sh ? ((w1 >> sh) | (w2 << (64 - sh))) : w1;
                     if (len < 8) x0 &= bits_lo(8 * len);
                     x1 = len <= 8 ? 0ull : (x1 & bits_lo(8 * (len - 8)));
-                    k0 = Q_GKEY ? lower8(x0) : x0;
-                    k1 = (Q_GKEY ? lower8(x1) : x1) | KMARK;
+                    k0 = lower8(x0);
+                    k1 = lower8(x1) | KMARK;
                     if (a.ablate & 32) {
                         words += (k0 ^ k1) == 1;  // keep the key build alive
                     } else {
@@ -511,17 +474,24 @@ __global__ __launch_bounds__(Q_T, 1) void k_scan_csv(ScanArgs a) {
                 if (MB) {
                     const u32 nm = (u32)__popcll(MB);
                     if (nmiss + nm > Q_MISS) {
-                        flush_miss(a, miss, nmiss, pend);
+                        flush_miss(a, miss, nmiss, lcur);
                         nmiss = 0;
                     }
-                    if (mis) miss[nmiss + mbcnt(MB)] = make_ulonglong2(k0, k1);
-                    nmiss += nm;
+                    if (mis) {
+                        const u32 at = nmiss + mbcnt(MB);
+                        if (at < Q_MISS) miss[at] = make_ulonglong2(k0, k1);
+                        else hbm_insert16(a, k0, k1, 1);  // more misses than the buffer holds (> 32 in one pass)
+                    }
+                    nmiss = min(nmiss + nm, (u32)Q_MISS);
                 }
             }
+            wsync();
         }
     }
-    if (nmiss) flush_miss(a, miss, nmiss, pend);
-    pend_complete(a, pend);
+    if (nmiss) flush_miss(a, miss, nmiss, lcur);
+    __syncthreads();
+    if (threadIdx.x < MSA_MLOG_PARTS)
+        a.mlog_n[blockIdx.x * MSA_MLOG_PARTS + threadIdx.x] = min(lcur[threadIdx.x], a.mlog_cap);
     words = wave_sum64(words);
     if (lane == 0 && words) atomicAdd((unsigned long long *)&a.ctr->total_words, (unsigned long long)words);
     __syncthreads();
@@ -530,6 +500,70 @@ __global__ __launch_bounds__(Q_T, 1) void k_scan_csv(ScanArgs a) {
         if (n) {
             const ulonglong2 kk = keys[i];
             hbm_insert16(a, kk.x, kk.y, n);
+        }
+    }
+}
+
+// k_miss_agg: workgroup (partition p, group g) counts partition p of the
+// logs of K3 workgroups g, g + G, ... in an LDS table (the whole LDS: ~8000
+// 16-byte keys), then adds each distinct key once to the HBM tables.
+#define MA_T 1024
+#define MA_SLOTS 8176
+#define MA_NB (MA_SLOTS / 4)
+__device__ __forceinline__ u32 ma_find(ulonglong2 *keys, u64 k0, u64 k1) {
+    u32 h = (u32)k0 * 0x9E3779B1u + (u32)(k0 >> 32) * 0x85EBCA77u + (u32)k1 * 0xC2B2AE3Du + (u32)(k1 >> 32);
+    h ^= h >> 15;
+    h *= 0x2C1B3C6Du;
+    u32 b = __umulhi(h, (u32)MA_NB);
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+        const u32 base = b * 4;
+        const ulonglong2 s0 = keys[base], s1 = keys[base + 1], s2 = keys[base + 2], s3 = keys[base + 3];
+        const bool e0 = (s0.x == k0) & (s0.y == k1), e1 = (s1.x == k0) & (s1.y == k1);
+        const bool e2 = (s2.x == k0) & (s2.y == k1), e3 = (s3.x == k0) & (s3.y == k1);
+        const u32 hit = e0 ? 0u : (e1 ? 1u : (e2 ? 2u : (e3 ? 3u : 4u)));
+        if (hit < 4) return base + hit;
+        u32 i = s0.x == 0 ? 0u : (s1.x == 0 ? 1u : (s2.x == 0 ? 2u : (s3.x == 0 ? 3u : 4u)));
+        for (; i < 4; ++i) {
+            u64 *kp = reinterpret_cast<u64 *>(&keys[base + i]);
+            const u64 old = atomicCAS((unsigned long long *)kp, 0ull, (unsigned long long)k0);
+            if (old == 0) {
+                kp[1] = k1;
+                return base + i;
+            }
+            if (old == k0 && kp[1] == k1) return base + i;
+        }
+        b = (b + 1 == MA_NB) ? 0 : b + 1;
+    }
+    return ~0u;
+}
+
+__global__ __launch_bounds__(MA_T) void k_miss_agg(ScanArgs a, u32 nsrc, u32 groups) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    ulonglong2 *keys = reinterpret_cast<ulonglong2 *>(smem);
+    u32 *cnts = reinterpret_cast<u32 *>(smem + MA_SLOTS * 16);
+    for (u32 i = threadIdx.x; i < MA_SLOTS; i += MA_T) {
+        keys[i] = make_ulonglong2(0, 0);
+        cnts[i] = 0;
+    }
+    __syncthreads();
+    const u32 part = blockIdx.x % MSA_MLOG_PARTS, g = blockIdx.x / MSA_MLOG_PARTS;
+    for (u32 src = g; src < nsrc; src += groups) {
+        const u64 base = ((u64)src * MSA_MLOG_PARTS + part) * a.mlog_cap;
+        const u32 n = a.mlog_n[src * MSA_MLOG_PARTS + part];
+        for (u32 i = threadIdx.x; i < n; i += MA_T) {
+            const ulonglong2 x = a.mlog[base + i];
+            const u32 slot = ma_find(keys, x.x, x.y);
+            if (slot != ~0u) atomicAdd(&cnts[slot], 1u);
+            else hbm_insert16(a, x.x, x.y, 1);
+        }
+    }
+    __syncthreads();
+    for (u32 i = threadIdx.x; i < MA_SLOTS; i += MA_T) {
+        const u32 c = cnts[i];
+        if (c) {
+            const ulonglong2 kk = keys[i];
+            hbm_insert16(a, kk.x, kk.y, c);
         }
     }
 }
@@ -544,9 +578,13 @@ hipError_t msa_launch_scan_csv(const ScanArgs &a, hipStream_t s) {
         g_q_cus = (hipGetDeviceProperties(&p, dev) == hipSuccess && p.multiProcessorCount > 0) ? p.multiProcessorCount
                                                                                                  : 256;
         (void)hipFuncSetAttribute((const void *)k_scan_csv, hipFuncAttributeMaxDynamicSharedMemorySize, Q_LDS);
+        (void)hipFuncSetAttribute((const void *)k_miss_agg, hipFuncAttributeMaxDynamicSharedMemorySize, MA_SLOTS * 20);
     }
     u32 blocks = (a.nchunks + Q_W - 1) / Q_W;
     if (blocks > (u32)g_q_cus) blocks = (u32)g_q_cus;
     hipLaunchKernelGGL(k_scan_csv, dim3(blocks), dim3(Q_T), Q_LDS, s, a);
+    // aggregate the logged misses: 16 partitions x groups, one workgroup per CU
+    const u32 groups = std::max<u32>(1, std::min<u32>(blocks, (u32)g_q_cus / MSA_MLOG_PARTS));
+    hipLaunchKernelGGL(k_miss_agg, dim3(groups * MSA_MLOG_PARTS), dim3(MA_T), MA_SLOTS * 20, s, a, blocks, groups);
     return hipGetLastError();
 }
