@@ -18,7 +18,8 @@
  *   msa_set_shard / msa_shard_function / msa_shard_head / msa_segment_*
  *                       (multi-GPU) the even byte split + re-sync of main
  *                       866-916, done exactly instead of at raw byte offsets
- *   msa_export_partitions / msa_export_copy / msa_import_partitions
+ *   msa_export_partitions / msa_export_ranked / msa_export_copy /
+ *   msa_import_partitions
  *                       send_hash_table 397-410, receive_hash_table 413-432,
  *                       ht_merge 152-158, the merge loop of main 1011-1025
  *   msa_rank            ht_to_array 161-175 + qsort(entry_compare_desc)
@@ -71,6 +72,10 @@ typedef struct {
 
 /* Deterministic synthetic corpus; *out is malloc'ed, release with msa_free. */
 int msa_gen_corpus(const msa_gen_params *p, char **out, size_t *len);
+/* Songs [first_song, first_song + n_songs) of the corpus p describes (the
+ * header row only when first_song is 0): the concatenation of consecutive
+ * ranges is msa_gen_corpus's output.  ZIPF / HIGHCARD only.               */
+int msa_gen_corpus_range(const msa_gen_params *p, uint64_t first_song, uint64_t n_songs, char **out, size_t *len);
 void msa_free(void *p);
 
 /* --------------------------------------------------------------- context */
@@ -216,6 +221,15 @@ int msa_set_artist_reader(msa_ctx *ctx, int exact);
 /* Serialise the counted table as nparts key-hash partitions (wire format in
  * csrc/msa_merge.hip); part_bytes[p] = bytes of partition p's block.      */
 int msa_export_partitions(msa_ctx *ctx, int table, int nparts, uint64_t *part_bytes);
+/* After msa_rank: ranked entries [0, limit) of a table (all when limit is 0)
+ * as ONE block of the same wire format.  A root GPU that imports every GPU's
+ * block (msa_import_partitions, one block per GPU) and calls msa_rank holds
+ * the global ranking -- or its top-limit: the key partitions are disjoint, so
+ * the union of the per-GPU top-limit lists holds the global top-limit.
+ * Replaces rank 0's receive + merge of every rank's table (main 1011-1025)
+ * followed by the final qsort (write_table_csv 325-344).                    */
+int msa_export_ranked(msa_ctx *ctx, int table, uint64_t limit, uint64_t *bytes);
+/* Copy the last export (partitions or ranked block) to dst (host or device). */
 int msa_export_copy(msa_ctx *ctx, void *dst);
 /* Replace the table by the union of the received blocks (counts summed);
  * blk_off[0..nblk] are the blocks' byte offsets in src (last = total).     */

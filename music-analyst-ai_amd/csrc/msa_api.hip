@@ -22,6 +22,7 @@ u32 msa_fn_blocks(u32 nchunks);
 hipError_t msa_launch_fn(const ChunkSum *, u64, u32, Fn *, State *, Fn *, const State *, State *, State *, hipStream_t);
 hipError_t msa_launch_scan(const ScanArgs &, int, hipStream_t);
 hipError_t msa_launch_scan_csv(const ScanArgs &, hipStream_t);
+hipError_t msa_launch_miss_agg(const ScanArgs &, hipStream_t);
 hipError_t msa_exclusive_scan(const u64 *, u64, u64 *, u64 *, u64 *, hipStream_t);
 hipError_t msa_launch_rec_spans(const u8 *, const u64 *, const u32 *, u64, u64, int, u64 *, u64 *, u32 *, u64 *, u64 *,
                                 u32 *, Counters *, const AKeys &, hipStream_t);
@@ -35,6 +36,7 @@ hipError_t msa_launch_long_verify(const u8 *, const u8 *, const u64 *, const u32
 hipError_t msa_launch_exp_count(const ExpSrc &, u64, u32, u64 *, u64 *, hipStream_t);
 hipError_t msa_launch_exp_write(const ExpSrc &, u64, u32, const u64 *, const u64 *, const u64 *, u64 *, u64 *, u8 *,
                                 hipStream_t);
+hipError_t msa_launch_exp_ranked(const u64 *, const u64 *, const u8 *, u64, u64, u8 *, hipStream_t);
 hipError_t msa_launch_imp(const u8 *, const u64 *, u32, u64 *, u64, const ImpDst &, hipStream_t);
 hipError_t msa_launch_col_write(int, const u8 *, const u64 *, const u64 *, const u64 *, const u32 *, u64, u64, u64, u8 *,
                                 hipStream_t);
@@ -90,11 +92,12 @@ enum {
     ST_LONG_WORDS,       // > 16-byte words: hash table + verification
     ST_RANK_WORDS,       // entries + sort + key blob, words
     ST_RANK_ARTISTS,     // the same, artists
+    ST_MISS_AGG,         // K3's logged LDS-table misses -> word tables (k_miss_agg)
     ST_COUNT_
 };
 const char *const kStageName[ST_COUNT_] = {"csv_summary", "csv_scan",    "artist_column", "text_column",
                                            "artist_summary", "artist_scan", "artist_keys",  "long_words",
-                                           "rank_words",  "rank_artists"};
+                                           "rank_words",  "rank_artists", "csv_miss_agg"};
 
 struct ProfStage {
     hipEvent_t a = nullptr, b = nullptr;
@@ -631,6 +634,11 @@ static int split_once(msa_ctx *c, int flags) {
     else HIPC(c, msa_launch_scan_csv(a, c->stream));
     // algorithmic bytes: every CSV byte once + the per-record SoA it writes
     prof_end(c, ST_CSV_SCAN, c->n + c->nrec * (want_text ? 12ull : 8ull));
+    if (!(c->ablate & 64)) {
+        prof_begin(c, ST_MISS_AGG);
+        HIPC(c, msa_launch_miss_agg(a, c->stream));
+        prof_end(c, ST_MISS_AGG, 0);
+    }
     // rec_start[nrec] = end of the last record (EOF when it has no terminator)
     if (fin.rs < c->n) {
         u64 v = c->n;
@@ -1410,6 +1418,26 @@ int msa_export_partitions(msa_ctx *c, int table, int nparts, uint64_t *part_byte
     return MSA_OK;
 }
 
+int msa_export_ranked(msa_ctx *c, int table, uint64_t limit, uint64_t *bytes) {
+    if (!c || !bytes) return MSA_ERR_ARG;
+    if (table != MSA_TABLE_WORDS && table != MSA_TABLE_ARTISTS) return MSA_ERR_ARG;
+    if (c->stage < 3) return fail(c, MSA_ERR_ARG, "msa_export_ranked before msa_rank");
+    HIPC(c, hipSetDevice(c->device));
+    Ranked &R = table == MSA_TABLE_WORDS ? c->rw : c->ra;
+    const u64 n = (limit && limit < R.n) ? limit : R.n;
+    u64 end = R.blob_len;
+    if (n < R.n) HIPC(c, hipMemcpy(&end, R.off.as<u64>() + n, 8, hipMemcpyDeviceToHost));
+    if (end >> 32) return fail(c, MSA_ERR_CAPACITY, "ranked key blob over 4 GiB");
+    const u64 total = 32 + 32 * n + end;
+    HIPC(c, ensure(c->exp_buf, total + 16));
+    HIPC(c, msa_launch_exp_ranked(R.counts.as<u64>(), R.off.as<u64>(), R.blob.as<u8>(), n, end, c->exp_buf.as<u8>(),
+                                  c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    c->exp_bytes = total;
+    *bytes = total;
+    return MSA_OK;
+}
+
 int msa_export_copy(msa_ctx *c, void *dst) {
     if (!c || (c->exp_bytes && !dst)) return MSA_ERR_ARG;
     HIPC(c, hipSetDevice(c->device));
@@ -1521,6 +1549,22 @@ int msa_import_partitions(msa_ctx *c, int table, const void *src, const uint64_t
 }  // extern "C"
 
 // ------------------------------------------------------------ diagnostics
+// Not part of include/msa_hip.h: a run counter by name (tools/ablate.py).
+extern "C" int msa_debug_stat(msa_ctx *c, const char *name, uint64_t *v) {
+    if (!c || !name || !v) return MSA_ERR_ARG;
+    int rc;
+    if ((rc = sync_counters(c))) return rc;
+    const Counters &k = c->h_ctr;
+    const std::string n(name);
+    if (n == "k3_misses") *v = k.k3_misses;
+    else if (n == "total_words") *v = k.total_words;
+    else if (n == "collision") *v = k.collision;
+    else if (n == "a_long") *v = k.a_long;
+    else if (n == "overflow") *v = k.overflow;
+    else return MSA_ERR_ARG;
+    return MSA_OK;
+}
+
 // Not part of include/msa_hip.h: the per-record arrays of the last split
 // (tools/k3_debug.py compares kernel variants with it).
 extern "C" int msa_debug_records(msa_ctx *c, uint64_t *rec_start, uint32_t *nulrel, uint64_t cap, uint64_t *n) {

@@ -16,10 +16,16 @@
  *                       unquoted fields with stray quotes) for parity tests
  *
  * Same (params) -> same bytes, on every machine.  Pure host C, no HIP.
+ * ZIPF / HIGHCARD songs are independent draws (per-song generator state), so
+ * msa_gen_corpus_range produces any song range of a corpus -- each GPU of
+ * configs[3] generates only its own shard -- and large ranges are generated
+ * on several host threads.
  */
+#include <pthread.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 #include "msa_hip.h"
 
@@ -225,31 +231,63 @@ static void put_quoted(Out *o, const char *s, size_t n) {
     out_c(o, '"');
 }
 
-static void gen_zipf_like(const msa_gen_params *p, Out *o, int highcard) {
-    Rng r = {p->seed * 0x9E3779B97F4A7C15ULL + 12345};
-    uint32_t V = p->vocab ? p->vocab : 50000, A = p->n_artists ? p->n_artists : 5000;
-    uint32_t wps = p->words_per_song ? p->words_per_song : 30;
+/* The generation context shared (read-only) by every song: the rendered
+ * vocabulary and the two Zipf samplers. */
+typedef struct {
+    const msa_gen_params *p;
+    int highcard;
+    uint32_t V, A, wps;
     Alias zw, za;
-    if (alias_build(&zw, V, 1.0) || alias_build(&za, A, highcard ? 1.1 : 0.8)) { o->oom = 1; return; }
-    /* pre-render the vocabulary (offset table into one arena) */
-    char *arena = (char *)malloc((size_t)V * 48);
-    uint32_t *off = (uint32_t *)malloc(sizeof(uint32_t) * (V + 1));
-    if (!arena || !off) { o->oom = 1; return; }
+    char *arena;
+    uint32_t *off;
+} ZipfGen;
+
+static int zipf_setup(ZipfGen *g, const msa_gen_params *p, int highcard) {
+    memset(g, 0, sizeof *g);
+    g->p = p;
+    g->highcard = highcard;
+    g->V = p->vocab ? p->vocab : 50000;
+    g->A = p->n_artists ? p->n_artists : 5000;
+    g->wps = p->words_per_song ? p->words_per_song : 30;
+    if (alias_build(&g->zw, g->V, 1.0) || alias_build(&g->za, g->A, highcard ? 1.1 : 0.8)) return -1;
+    g->arena = (char *)malloc((size_t)g->V * 48);
+    g->off = (uint32_t *)malloc(sizeof(uint32_t) * (g->V + 1));
+    if (!g->arena || !g->off) return -1;
     size_t al = 0;
-    for (uint32_t i = 0; i < V; ++i) {
-        off[i] = (uint32_t)al;
-        al += vocab_word(i, arena + al, highcard);
+    for (uint32_t i = 0; i < g->V; ++i) {
+        g->off[i] = (uint32_t)al;
+        al += vocab_word(i, g->arena + al, highcard);
     }
-    off[V] = (uint32_t)al;
+    g->off[g->V] = (uint32_t)al;
+    return 0;
+}
+static void zipf_free(ZipfGen *g) {
+    free(g->arena);
+    free(g->off);
+    alias_free(&g->zw);
+    alias_free(&g->za);
+}
+
+/* Songs [s0, s1): each song draws from its own generator state (a function
+ * of the seed and the song index), so any song range of the corpus can be
+ * generated on its own -- a GPU's shard of a huge corpus, or a thread's. */
+static void zipf_songs(const ZipfGen *g, uint64_t s0, uint64_t s1, Out *o) {
+    const msa_gen_params *p = g->p;
+    const int highcard = g->highcard;
+    const uint32_t A = g->A, wps = g->wps;
     static const char *punct[] = {",", ".", "!", "?", " -", "...", ";", ":", ")", ""};
     char name[256], tmp[64];
-    out_s(o, "artist,song,link,text");
-    out_s(o, p->crlf ? "\r\n" : "\n");
-    for (uint64_t s = 0; s < p->n_songs; ++s) {
+    if (s0 == 0) {
+        out_s(o, "artist,song,link,text");
+        out_s(o, p->crlf ? "\r\n" : "\n");
+    }
+    for (uint64_t s = s0; s < s1; ++s) {
+        Rng r = {p->seed * 0x9E3779B97F4A7C15ULL + 12345 + s * 0xD1342543DE82EF95ULL};
+        (void)rng_next(&r);
         int q;
         /* highcard: half the songs by a skewed (Zipf 1.1) artist population,
          * half by one of 2^30 artists -> artist cardinality grows with songs */
-        uint32_t aid = (highcard && rng_below(&r, 2)) ? A + rng_below(&r, 1u << 30) : alias_draw(&za, &r);
+        uint32_t aid = (highcard && rng_below(&r, 2)) ? A + rng_below(&r, 1u << 30) : alias_draw(&g->za, &r);
         size_t nl = artist_name(aid, name, &q);
         if (q) put_quoted(o, name, nl); else out_put(o, name, nl);
         out_c(o, ',');
@@ -258,9 +296,9 @@ static void gen_zipf_like(const msa_gen_params *p, Out *o, int highcard) {
         int tq = rng_below(&r, 10) == 0;
         if (tq) out_c(o, '"');
         for (uint32_t k = 0; k < tw; ++k) {
-            uint32_t w = alias_draw(&zw, &r);
+            uint32_t w = alias_draw(&g->zw, &r);
             if (k) out_s(o, tq && k == 1 ? ", " : " ");
-            out_put(o, arena + off[w], off[w + 1] - off[w]);
+            out_put(o, g->arena + g->off[w], g->off[w + 1] - g->off[w]);
         }
         if (tq) out_c(o, '"');
         out_s(o, ",/a/");
@@ -296,12 +334,12 @@ static void gen_zipf_like(const msa_gen_params *p, Out *o, int highcard) {
                 line++;
                 continue;
             }
-            w = alias_draw(&zw, &r);
+            w = alias_draw(&g->zw, &r);
             if (k && line) out_c(o, ' ');
             uint32_t deco = rng_below(&r, 64);
             if (deco == 0) out_s(o, "\"\"");
             else if (deco == 1) out_c(o, '(');
-            out_put(o, arena + off[w], off[w + 1] - off[w]);
+            out_put(o, g->arena + g->off[w], g->off[w + 1] - g->off[w]);
             if (deco == 0) out_s(o, "\"\"");
             else if (deco < 12) out_s(o, punct[deco % 10]);
             line++;
@@ -313,10 +351,65 @@ static void gen_zipf_like(const msa_gen_params *p, Out *o, int highcard) {
         out_s(o, "  \n\"");
         out_s(o, p->crlf ? "\r\n" : "\n");
     }
-    free(arena);
-    free(off);
-    alias_free(&zw);
-    alias_free(&za);
+}
+
+typedef struct {
+    const ZipfGen *g;
+    uint64_t s0, s1;
+    Out o;
+} GenJob;
+static void *gen_job(void *arg) {
+    GenJob *j = (GenJob *)arg;
+    zipf_songs(j->g, j->s0, j->s1, &j->o);
+    return NULL;
+}
+
+/* Songs [s0, s1) of the corpus, on up to 16 host threads for large ranges
+ * (same bytes whatever the thread count). */
+static void gen_zipf_like(const msa_gen_params *p, uint64_t s0, uint64_t s1, Out *o, int highcard) {
+    ZipfGen g;
+    if (zipf_setup(&g, p, highcard)) { o->oom = 1; zipf_free(&g); return; }
+    const uint64_t n = s1 - s0;
+    uint64_t nt = n / 200000;
+    long ncpu = sysconf(_SC_NPROCESSORS_ONLN);
+    if (nt > 16) nt = 16;
+    if (ncpu > 0 && nt > (uint64_t)ncpu) nt = (uint64_t)ncpu;
+    if (nt < 2) {
+        zipf_songs(&g, s0, s1, o);
+        zipf_free(&g);
+        return;
+    }
+    GenJob jobs[16];
+    pthread_t th[16];
+    uint64_t started = 0;
+    for (uint64_t t = 0; t < nt; ++t) {
+        memset(&jobs[t].o, 0, sizeof(Out));
+        jobs[t].g = &g;
+        jobs[t].s0 = s0 + n * t / nt;
+        jobs[t].s1 = s0 + n * (t + 1) / nt;
+        if (t == 0 || pthread_create(&th[t], NULL, gen_job, &jobs[t]) != 0) {
+            gen_job(&jobs[t]);  /* thread 0 (and any thread that failed to start) runs here */
+            th[t] = 0;
+        } else {
+            started |= 1ull << t;
+        }
+    }
+    for (uint64_t t = 1; t < nt; ++t)
+        if (started >> t & 1ull) pthread_join(th[t], NULL);
+    size_t tot = 0;
+    for (uint64_t t = 0; t < nt; ++t) {
+        if (jobs[t].o.oom) o->oom = 1;
+        tot += jobs[t].o.n;
+    }
+    if (!o->oom) out_reserve(o, tot);
+    for (uint64_t t = 0; t < nt; ++t) {
+        if (!o->oom) {
+            memcpy(o->p + o->n, jobs[t].o.p, jobs[t].o.n);
+            o->n += jobs[t].o.n;
+        }
+        free(jobs[t].o.p);
+    }
+    zipf_free(&g);
 }
 
 /* CSV syntax torture: every state of the record reader, field splitter and
@@ -374,16 +467,23 @@ static void gen_torture(const msa_gen_params *p, Out *o) {
     }
 }
 
-int msa_gen_corpus(const msa_gen_params *p, char **out, size_t *len) {
+int msa_gen_corpus_range(const msa_gen_params *p, uint64_t first_song, uint64_t n_songs, char **out, size_t *len) {
     if (!p || !out || !len) return -1;
+    if (first_song > p->n_songs || n_songs > p->n_songs - first_song) return -1;
+    if (p->mode == MSA_GEN_TORTURE && (first_song || n_songs != p->n_songs)) return -1;  /* one stream */
     Out o = {0};
     if (p->mode == MSA_GEN_TORTURE) gen_torture(p, &o);
-    else gen_zipf_like(p, &o, p->mode == MSA_GEN_HIGHCARD);
+    else gen_zipf_like(p, first_song, first_song + n_songs, &o, p->mode == MSA_GEN_HIGHCARD);
     if (o.oom) { free(o.p); return -2; }
     if (!o.p) { o.p = (char *)malloc(1); }
     *out = o.p;
     *len = o.n;
     return 0;
+}
+
+int msa_gen_corpus(const msa_gen_params *p, char **out, size_t *len) {
+    if (!p) return -1;
+    return msa_gen_corpus_range(p, 0, p->n_songs, out, len);
 }
 
 void msa_free(void *p) { free(p); }

@@ -252,7 +252,8 @@ struct Counters {
     // artist pass then runs the exact record reader over artist.csv)
     u64 a_quoted;
     u64 a_long;      // bytes used in the long-key arena (k_rec_spans)
-    u64 pad[5];
+    u64 k3_misses;   // K3 LDS-table misses logged for k_miss_agg (diagnostic)
+    u64 pad[4];
 };
 
 enum { OVF_S = 1, OVF_M = 2, OVF_L = 4, OVF_LT = 8, OVF_A = 16, OVF_REC = 32 };
@@ -297,7 +298,7 @@ struct ScanArgs {
     // for k_miss_agg (MSA_MLOG_PARTS partitions, mlog_cap entries each)
     ulonglong2 *mlog;
     u32 *mlog_n;
-    u32 mlog_cap;      // diagnostic builds only (MSA_ABLATE env): see msa_scan.hip
+    u32 mlog_cap;
 };
 
 #define MSA_MLOG_PARTS 16

@@ -551,6 +551,7 @@ __global__ __launch_bounds__(MA_T) void k_miss_agg(ScanArgs a, u32 nsrc, u32 gro
     for (u32 src = g; src < nsrc; src += groups) {
         const u64 base = ((u64)src * MSA_MLOG_PARTS + part) * a.mlog_cap;
         const u32 n = a.mlog_n[src * MSA_MLOG_PARTS + part];
+        if (threadIdx.x == 0 && n) atomicAdd((unsigned long long *)&a.ctr->k3_misses, (unsigned long long)n);
         for (u32 i = threadIdx.x; i < n; i += MA_T) {
             const ulonglong2 x = a.mlog[base + i];
             const u32 slot = ma_find(keys, x.x, x.y);
@@ -569,8 +570,7 @@ __global__ __launch_bounds__(MA_T) void k_miss_agg(ScanArgs a, u32 nsrc, u32 gro
 }
 
 static int g_q_cus = 0;
-hipError_t msa_launch_scan_csv(const ScanArgs &a, hipStream_t s) {
-    if (!a.nchunks) return hipSuccess;
+static u32 scan_blocks(const ScanArgs &a) {
     if (!g_q_cus) {
         int dev = 0;
         (void)hipGetDevice(&dev);
@@ -580,10 +580,19 @@ hipError_t msa_launch_scan_csv(const ScanArgs &a, hipStream_t s) {
         (void)hipFuncSetAttribute((const void *)k_scan_csv, hipFuncAttributeMaxDynamicSharedMemorySize, Q_LDS);
         (void)hipFuncSetAttribute((const void *)k_miss_agg, hipFuncAttributeMaxDynamicSharedMemorySize, MA_SLOTS * 20);
     }
-    u32 blocks = (a.nchunks + Q_W - 1) / Q_W;
-    if (blocks > (u32)g_q_cus) blocks = (u32)g_q_cus;
-    hipLaunchKernelGGL(k_scan_csv, dim3(blocks), dim3(Q_T), Q_LDS, s, a);
-    // aggregate the logged misses: 16 partitions x groups, one workgroup per CU
+    const u32 blocks = (a.nchunks + Q_W - 1) / Q_W;
+    return blocks > (u32)g_q_cus ? (u32)g_q_cus : blocks;
+}
+hipError_t msa_launch_scan_csv(const ScanArgs &a, hipStream_t s) {
+    if (!a.nchunks) return hipSuccess;
+    hipLaunchKernelGGL(k_scan_csv, dim3(scan_blocks(a)), dim3(Q_T), Q_LDS, s, a);
+    return hipGetLastError();
+}
+// after k_scan_csv on the same stream: fold the logged misses, 16 partitions x
+// groups, one workgroup per CU
+hipError_t msa_launch_miss_agg(const ScanArgs &a, hipStream_t s) {
+    if (!a.nchunks) return hipSuccess;
+    const u32 blocks = scan_blocks(a);
     const u32 groups = std::max<u32>(1, std::min<u32>(blocks, (u32)g_q_cus / MSA_MLOG_PARTS));
     hipLaunchKernelGGL(k_miss_agg, dim3(groups * MSA_MLOG_PARTS), dim3(MA_T), MA_SLOTS * 20, s, a, blocks, groups);
     return hipGetLastError();

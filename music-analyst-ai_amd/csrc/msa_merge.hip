@@ -185,6 +185,40 @@ __global__ void k_imp_insert(const u8 *in, const u64 *blk_off, const u64 *rec_ba
 }
 
 // ---------------------------------------------------------------------------
+// Ranked export: entries [0, n) of a ranked table (rank order) as ONE block of
+// the wire format above, so that a root GPU can import the blocks of every
+// GPU (disjoint key partitions) and rank their union -- the global ranking, or
+// its top-k when every GPU sent its own top-k.  The blob is the ranked key
+// blob itself (keys unpadded; the importer reads long keys byte by byte).
+__global__ void k_exp_ranked(const u64 *__restrict__ counts, const u64 *__restrict__ off, const u8 *__restrict__ blob,
+                             u64 n, u64 blob_end, u8 *__restrict__ out) {
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) {
+        u64 *h = reinterpret_cast<u64 *>(out);
+        h[0] = n;
+        h[1] = blob_end;
+        h[2] = 0;
+        h[3] = 0;
+    }
+    if (i >= n) return;
+    const u64 o = off[i], e = (i + 1 < n) ? off[i + 1] : blob_end;
+    const u32 len = (u32)(e - o);
+    u64 k0 = 0, k1 = 0;
+    if (len <= 16) {
+        for (u32 k = 0; k < len; ++k) {
+            const u64 ch = blob[o + k];
+            if (k < 8) k0 |= ch << (8 * k);
+            else k1 |= ch << (8 * (k - 8));
+        }
+    }
+    u64 *rec = reinterpret_cast<u64 *>(out + 32 + 32 * i);
+    rec[0] = counts[i];
+    rec[1] = (u64)len | (o << 32);
+    rec[2] = k0;
+    rec[3] = k1;
+}
+
+// ---------------------------------------------------------------------------
 static inline dim3 g1(u64 n, u32 t = 256) { return dim3((u32)((n + t - 1) / t)); }
 
 hipError_t msa_launch_exp_count(const ExpSrc &x, u64 n, u32 nparts, u64 *pcnt, u64 *pblob, hipStream_t s) {
@@ -201,5 +235,11 @@ hipError_t msa_launch_imp(const u8 *in, const u64 *blk_off, u32 nblk, u64 *rec_b
                           hipStream_t s) {
     hipLaunchKernelGGL(k_imp_index, dim3(1), dim3(64), 0, s, in, blk_off, nblk, rec_base);
     if (nrec_total) hipLaunchKernelGGL(k_imp_insert, g1(nrec_total), dim3(256), 0, s, in, blk_off, rec_base, nblk, d);
+    return hipGetLastError();
+}
+hipError_t msa_launch_exp_ranked(const u64 *counts, const u64 *off, const u8 *blob, u64 n, u64 blob_end, u8 *out,
+                                 hipStream_t s) {
+    hipLaunchKernelGGL(k_exp_ranked, g1(n ? n : 1), dim3(256), 0, s, counts, off, blob, n, blob_end, out);
+    if (blob_end) (void)hipMemcpyAsync(out + 32 + 32 * n, blob, blob_end, hipMemcpyDeviceToDevice, s);
     return hipGetLastError();
 }

@@ -58,17 +58,47 @@ __device__ __forceinline__ void wave_sync() {
 struct Classes64 {
     u64 Q, C, NL, CR, Z;
 };
+// "byte == c" per byte as 0x80 flags (exact) / "some byte == c" (cheap)
+__device__ __forceinline__ u32 k1_eq80(u32 x, u32 c) {
+    const u32 y = x ^ (c * 0x01010101u);
+    return ~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y) & 0x80808080u;
+}
+__device__ __forceinline__ u32 k1_has80(u32 x, u32 c) {
+    const u32 y = x ^ (c * 0x01010101u);
+    return (y - 0x01010101u) & ~y & 0x80808080u;
+}
+// The lane's 64 bytes: '"', ',' and '\n' always; '\r' and NUL only when the
+// wave's 4 KiB hold one (a cheap has-byte test, then a wave-uniform branch).
 __device__ __forceinline__ Classes64 classify64(const uint4 (&v)[4], u64 lpos, u64 end) {
     Classes64 k{0, 0, 0, 0, 0};
+    u32 rare = 0;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        const Classes c = classify16(v[q], valid_mask(lpos + 16 * q, end));
-        k.Q |= (u64)c.Q << (16 * q);
-        k.C |= (u64)c.C << (16 * q);
-        k.NL |= (u64)c.NL << (16 * q);
-        k.CR |= (u64)c.CR << (16 * q);
-        k.Z |= (u64)c.Z << (16 * q);
+        const u32 w[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            const u32 sh = 16 * q + 4 * d;
+            rare |= k1_has80(w[d], '\r') | k1_has80(w[d], 0);
+            k.Q |= (u64)swar_pack4(k1_eq80(w[d], '"')) << sh;
+            k.C |= (u64)swar_pack4(k1_eq80(w[d], ',')) << sh;
+            k.NL |= (u64)swar_pack4(k1_eq80(w[d], '\n')) << sh;
+        }
     }
+    if (__ballot(rare != 0)) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const u32 w[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                const u32 sh = 16 * q + 4 * d;
+                k.CR |= (u64)swar_pack4(k1_eq80(w[d], '\r')) << sh;
+                k.Z |= (u64)swar_pack4(k1_eq80(w[d], 0)) << sh;
+            }
+        }
+    }
+    const u64 r = lpos < end ? end - lpos : 0;
+    const u64 vm = r >= 64 ? ~0ull : ((1ull << r) - 1ull);
+    k.Q &= vm; k.C &= vm; k.NL &= vm; k.CR &= vm; k.Z &= vm;
     return k;
 }
 __device__ __forceinline__ u64 pxor_excl64(u64 q) {  // bit j = xor of bits < j

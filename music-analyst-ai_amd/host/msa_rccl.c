@@ -1,0 +1,171 @@
+/*
+ * msa_rccl.c -- the RCCL transport of the C host's rank layer (msa_ranks.h):
+ * one rank per GPU, device buffers, RCCL over xGMI.
+ *
+ *   all-gather   ncclAllGather of the (small) control data -- shard transfer
+ *                functions, piece sizes, heads, partition sizes, timings;
+ *   all-to-all-v one ncclGroupStart/End of ncclSend + ncclRecv per peer:
+ *                the head bytes of records cut by a shard boundary, the
+ *                key-hash partitions of the count tables, the ranked blocks
+ *                gathered to rank 0 (replacing send_hash_table /
+ *                receive_hash_table, parallel_spotify.c:397-432).
+ * The communicator is set up with the ncclUniqueId rank 0 publishes in the
+ * launcher's shared block.  Every operation runs on the transport's own HIP
+ * stream and is complete when it returns (libmsa_hip reads the buffers on its
+ * stream right after).
+ */
+#include <fcntl.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <unistd.h>
+
+#include <hip/hip_runtime_api.h>
+#include <rccl/rccl.h>
+
+#include "msa_ranks.h"
+
+typedef struct {
+    ncclComm_t comm;
+    hipStream_t stream;
+    void *scratch;
+    size_t scratch_bytes;
+} RcclImpl;
+
+#define NCCL_OK(x, what)                                                                          \
+    do {                                                                                          \
+        ncclResult_t r_ = (x);                                                                    \
+        if (r_ != ncclSuccess) {                                                                  \
+            fprintf(stderr, "rank %d: %s: %s\n", t->rank, what, ncclGetErrorString(r_));          \
+            return -1;                                                                            \
+        }                                                                                         \
+    } while (0)
+#define HIP_OK(x, what)                                                                           \
+    do {                                                                                          \
+        hipError_t e_ = (x);                                                                      \
+        if (e_ != hipSuccess) {                                                                   \
+            fprintf(stderr, "rank %d: %s: %s\n", t->rank, what, hipGetErrorString(e_));           \
+            return -1;                                                                            \
+        }                                                                                         \
+    } while (0)
+
+static int rc_allgather(msa_tr *t, const void *in, size_t bytes, void *out) {
+    RcclImpl *im = (RcclImpl *)t->impl;
+    const size_t need = bytes * (size_t)t->world;
+    if (need > im->scratch_bytes) {
+        if (im->scratch) (void)hipFree(im->scratch);
+        im->scratch = NULL;
+        HIP_OK(hipMalloc(&im->scratch, need), "hipMalloc");
+        im->scratch_bytes = need;
+    }
+    char *sc = (char *)im->scratch;
+    HIP_OK(hipMemcpyAsync(sc + bytes * (size_t)t->rank, in, bytes, hipMemcpyHostToDevice, im->stream), "copy in");
+    NCCL_OK(ncclAllGather(sc + bytes * (size_t)t->rank, sc, bytes, ncclUint8, im->comm, im->stream), "ncclAllGather");
+    HIP_OK(hipMemcpyAsync(out, sc, need, hipMemcpyDeviceToHost, im->stream), "copy out");
+    HIP_OK(hipStreamSynchronize(im->stream), "sync");
+    return 0;
+}
+
+static int rc_alltoallv(msa_tr *t, const void *send, const uint64_t *sc, void *recv, const uint64_t *rc) {
+    RcclImpl *im = (RcclImpl *)t->impl;
+    uint64_t so = 0, ro = 0;
+    NCCL_OK(ncclGroupStart(), "ncclGroupStart");
+    for (int p = 0; p < t->world; ++p) {
+        if (sc[p]) NCCL_OK(ncclSend((const char *)send + so, sc[p], ncclUint8, p, im->comm, im->stream), "ncclSend");
+        if (rc[p]) NCCL_OK(ncclRecv((char *)recv + ro, rc[p], ncclUint8, p, im->comm, im->stream), "ncclRecv");
+        so += sc[p];
+        ro += rc[p];
+    }
+    NCCL_OK(ncclGroupEnd(), "ncclGroupEnd");
+    HIP_OK(hipStreamSynchronize(im->stream), "sync");
+    return 0;
+}
+
+static void *rc_alloc(msa_tr *t, size_t n) {
+    void *p = NULL;
+    if (hipMalloc(&p, n ? n : 1) != hipSuccess) {
+        fprintf(stderr, "rank %d: hipMalloc(%zu) failed\n", t->rank, n);
+        return NULL;
+    }
+    return p;
+}
+static void rc_release(msa_tr *t, void *p) {
+    (void)t;
+    if (p) (void)hipFree(p);
+}
+static void rc_destroy(msa_tr *t) {
+    RcclImpl *im = (RcclImpl *)t->impl;
+    if (im) {
+        if (im->comm) ncclCommDestroy(im->comm);
+        if (im->scratch) (void)hipFree(im->scratch);
+        if (im->stream) (void)hipStreamDestroy(im->stream);
+        free(im);
+    }
+    free(t);
+}
+
+/* RCCL prints its version banner on stdout at initialisation; the CLI's
+ * stdout is the reference's summary, byte for byte, so the banner goes to
+ * stderr instead. */
+static int stdout_to_stderr(void) {
+    fflush(stdout);
+    const int saved = dup(1);
+    if (saved >= 0) dup2(2, 1);
+    return saved;
+}
+static void stdout_restore(int saved) {
+    fflush(stdout);
+    if (saved >= 0) {
+        dup2(saved, 1);
+        close(saved);
+    }
+}
+
+msa_tr *msa_tr_rccl(msa_shared *sh, int rank, int world, int device) {
+    msa_tr *t = calloc(1, sizeof *t);
+    RcclImpl *im = calloc(1, sizeof *im);
+    if (!t || !im) { free(t); free(im); return NULL; }
+    t->rank = rank;
+    t->world = world;
+    t->kind = "rccl";
+    t->allgather = rc_allgather;
+    t->alltoallv = rc_alltoallv;
+    t->alloc = rc_alloc;
+    t->release = rc_release;
+    t->destroy = rc_destroy;
+    t->sh = sh;
+    t->impl = im;
+    ncclUniqueId id;
+    _Static_assert(sizeof(ncclUniqueId) <= 128, "ncclUniqueId fits the shared blob");
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&im->stream, hipStreamNonBlocking) != hipSuccess) {
+        fprintf(stderr, "rank %d: cannot use GPU %d\n", rank, device);
+        rc_destroy(t);
+        return NULL;
+    }
+    const int saved = stdout_to_stderr();
+    msa_tr *res = t;
+    if (rank == 0) {
+        if (ncclGetUniqueId(&id) != ncclSuccess) {
+            fprintf(stderr, "rank 0: ncclGetUniqueId failed\n");
+            rc_destroy(t);
+            stdout_restore(saved);
+            return NULL;
+        }
+        memcpy(msa_shared_blob(sh), &id, sizeof id);
+    }
+    if (msa_shared_barrier(sh)) {  /* the id is published */
+        rc_destroy(t);
+        stdout_restore(saved);
+        return NULL;
+    }
+    memcpy(&id, msa_shared_blob(sh), sizeof id);
+    const ncclResult_t r = ncclCommInitRank(&im->comm, world, id, rank);
+    if (r != ncclSuccess) {
+        fprintf(stderr, "rank %d: ncclCommInitRank: %s\n", rank, ncclGetErrorString(r));
+        im->comm = NULL;
+        rc_destroy(t);
+        res = NULL;
+    }
+    stdout_restore(saved);
+    return res;
+}

@@ -37,12 +37,12 @@ PROF_MAX = 16
 
 # Every symbol include/msa_hip.h declares (tests check the .so exports them).
 EXPORTS = [
-    "msa_gen_corpus", "msa_free", "msa_create", "msa_destroy", "msa_last_error",
+    "msa_gen_corpus", "msa_gen_corpus_range", "msa_free", "msa_create", "msa_destroy", "msa_last_error",
     "msa_stream", "msa_sync", "msa_load_csv", "msa_bind_csv", "msa_split_columns",
     "msa_count", "msa_rank", "msa_run", "msa_get_summary", "msa_get_ranked",
     "msa_write_table_csv", "msa_get_split_column", "msa_set_profiling", "msa_get_profile",
     "msa_set_shard", "msa_piece_size", "msa_shard_function", "msa_shard_head", "msa_segment_copy",
-    "msa_segment_set", "msa_artist_reader_needed", "msa_set_artist_reader", "msa_export_partitions", "msa_export_copy", "msa_import_partitions",
+    "msa_segment_set", "msa_artist_reader_needed", "msa_set_artist_reader", "msa_export_partitions", "msa_export_ranked", "msa_export_copy", "msa_import_partitions",
     "msa_wcs_create", "msa_wcs_destroy", "msa_wcs_last_error", "msa_wcs_stream", "msa_wcs_load_csv",
     "msa_wcs_set_table_bits", "msa_wcs_run", "msa_wcs_get_summary", "msa_wcs_get_csv", "msa_wcs_write_outputs",
     "msa_csvcol_run", "msa_csvcol_header", "msa_csvcol_get",
@@ -113,6 +113,7 @@ def load(path: str = LIB_PATH):
     lib = C.CDLL(path)
     vp, sz, u64, i = C.c_void_p, C.c_size_t, C.c_uint64, C.c_int
     lib.msa_gen_corpus.argtypes = [C.POINTER(_GenParams), C.POINTER(C.c_void_p), C.POINTER(sz)]
+    lib.msa_gen_corpus_range.argtypes = [C.POINTER(_GenParams), u64, u64, C.POINTER(C.c_void_p), C.POINTER(sz)]
     lib.msa_free.argtypes = [vp]
     lib.msa_free.restype = None
     lib.msa_create.argtypes = [i, C.POINTER(vp)]
@@ -144,6 +145,7 @@ def load(path: str = LIB_PATH):
     lib.msa_set_artist_reader.argtypes = [vp, i]
     lib.msa_export_partitions.argtypes = [vp, i, i, C.POINTER(u64)]
     lib.msa_export_copy.argtypes = [vp, vp]
+    lib.msa_export_ranked.argtypes = [vp, i, u64, C.POINTER(u64)]
     lib.msa_import_partitions.argtypes = [vp, i, vp, C.POINTER(u64), i]
     lib.msa_set_profiling.argtypes = [vp, i]
     lib.msa_get_profile.argtypes = [vp, C.POINTER(_Profile), i]
@@ -168,13 +170,20 @@ def load(path: str = LIB_PATH):
 
 
 def gen_corpus(n_songs: int, mode: str = "zipf", seed: int = 1, vocab: int = 50000, n_artists: int = 5000,
-               words_per_song: int = 30, crlf: bool = False) -> bytes:
-    """Deterministic synthetic corpus (csrc/msa_gen.c) -- host code, no GPU."""
+               words_per_song: int = 30, crlf: bool = False, first_song: int = 0,
+               count: Optional[int] = None) -> bytes:
+    """Deterministic synthetic corpus (csrc/msa_gen.c) -- host code, no GPU.
+    With first_song / count: only songs [first_song, first_song + count) of the
+    n_songs-song corpus (header only in the range starting at song 0)."""
     lib = load()
     p = _GenParams(seed, n_songs, vocab, n_artists, words_per_song, GEN_MODES[mode], int(crlf))
     out = C.c_void_p()
     n = C.c_size_t()
-    rc = lib.msa_gen_corpus(C.byref(p), C.byref(out), C.byref(n))
+    if count is None and first_song == 0:
+        rc = lib.msa_gen_corpus(C.byref(p), C.byref(out), C.byref(n))
+    else:
+        cnt = n_songs - first_song if count is None else count
+        rc = lib.msa_gen_corpus_range(C.byref(p), first_song, cnt, C.byref(out), C.byref(n))
     if rc:
         raise MsaError(rc, "corpus generation failed")
     try:
@@ -299,6 +308,12 @@ class Context:
         out = (C.c_uint64 * nparts)()
         self._check(self.lib.msa_export_partitions(self.h, table, nparts, out))
         return list(out)
+
+    def export_ranked(self, table: int, limit: int = 0) -> int:
+        """Serialise ranked entries [0, limit) (all: 0) as one wire block; returns its bytes."""
+        n = C.c_uint64()
+        self._check(self.lib.msa_export_ranked(self.h, table, limit, C.byref(n)))
+        return n.value
 
     def export_copy(self, dst_ptr: int):
         self._check(self.lib.msa_export_copy(self.h, C.c_void_p(dst_ptr)))

@@ -20,12 +20,11 @@ It replaces the reference's MPI data flow (/root/reference/src/parallel_spotify.
   and every rank merges and ranks its own key range; rank 0 then gathers the
   ranked partitions (or their top-k).
 
-The routing logic (`head_owners`, `tail_plan`, `merge_ranked`) is plain Python
+The routing logic (`head_owners`, `tail_plan`) is plain Python
 so it is tested on CPU with a gloo world (tests/test_dist.py).
 """
 from __future__ import annotations
 
-import heapq
 from typing import Callable, List, Optional, Sequence, Tuple
 
 import torch
@@ -60,13 +59,6 @@ def tail_plan(rank: int, heads: Sequence[int], sizes: Sequence[int]) -> Tuple[Li
         if owners[r] == rank:
             recv[r] = heads[r]
     return send, recv
-
-
-def merge_ranked(parts: Sequence[Sequence[Tuple[bytes, int]]]) -> List[Tuple[bytes, int]]:
-    """k-way merge of per-rank ranked lists in entry_compare_desc order
-    (parallel_spotify.c:178-188: count descending, then strcmp of the keys).
-    The key partitions are disjoint, so this is the global ranking."""
-    return list(heapq.merge(*parts, key=lambda kv: (-kv[1], kv[0])))
 
 
 # ----------------------------------------------------------------- exchange
@@ -169,29 +161,31 @@ def run_sharded(ctx, comm: Comm, text_column: bool = True) -> Tuple[int, int]:
     return songs, words
 
 
-def gather_ranked(ctx, comm: Comm, table: int, topk: Optional[int] = None) -> Optional[List[Tuple[bytes, int]]]:
-    """Rank 0 receives every rank's ranked partition (or its top-k) and merges
-    them into the global ranking; other ranks return None."""
-    mine = ctx.ranked(table, 0, topk)
-    blob = b"".join(len(k).to_bytes(4, "little") + c.to_bytes(8, "little") + k for k, c in mine)
-    sizes = [row[0] for row in comm.all_gather_u64([len(blob)])]
-    width = max(1, max(sizes))
-    t = torch.zeros(width, dtype=torch.uint8, device=comm.device)
-    if blob:
-        t[: len(blob)].copy_(torch.frombuffer(bytearray(blob), dtype=torch.uint8))
-    out = [torch.empty_like(t) for _ in range(comm.world)]
-    dist.all_gather(out, t, group=comm.group)
+def gather_ranked(ctx, comm: Comm, topk: Optional[int] = None,
+                  tables: Sequence[int] = (MSA_TABLE_WORDS, MSA_TABLE_ARTISTS)) -> bool:
+    """Device-side final gather: every rank serialises its ranked partition
+    (or its top-k) with msa_export_ranked, one all-to-all moves the blocks to
+    rank 0 (RCCL: GPU to GPU), and rank 0 imports their union and ranks it --
+    the key partitions are disjoint, so that is the global ranking (its top-k
+    when each rank sent its own top-k).  Returns True on rank 0, whose context
+    then holds the global ranked tables (ctx.ranked / msa_write_table_csv).
+    Replaces rank 0's receive + merge of every rank's table
+    (parallel_spotify.c:1011-1025) and the final qsort (325-344)."""
+    got = []
+    for t in tables:
+        nbytes = ctx.export_ranked(t, topk or 0)
+        send = torch.empty(max(1, nbytes), dtype=torch.uint8, device=comm.device)
+        ctx.export_copy(send.data_ptr())
+        counts = [0] * comm.world
+        counts[0] = nbytes
+        recv, recv_counts = comm.alltoallv(send, counts)
+        got.append((t, recv, recv_counts))
     if comm.rank != 0:
-        return None
-    parts = []
-    for o, n in zip(out, sizes):
-        raw = bytes(o.cpu().numpy().tobytes()[:n])
-        lst, i = [], 0
-        while i < n:
-            kl = int.from_bytes(raw[i:i + 4], "little")
-            cnt = int.from_bytes(raw[i + 4:i + 12], "little")
-            lst.append((raw[i + 12:i + 12 + kl], cnt))
-            i += 12 + kl
-        parts.append(lst)
-    merged = merge_ranked(parts)
-    return merged[:topk] if topk else merged
+        return False
+    for t, recv, recv_counts in got:
+        offs = [0]
+        for c in recv_counts:
+            offs.append(offs[-1] + c)
+        ctx.import_partitions(t, recv.data_ptr(), offs)
+    ctx.rank()
+    return True

@@ -1,7 +1,7 @@
 """CPU: the multi-GPU routing and exchange logic of msa/dist.py with a gloo
 world of 2-3 processes.  The GPU kernels are replaced by a small host stand-in
 (FakeCtx) so that the boundary plan, the head exchange, the partitioned merge
-and the final ranked gather are exercised exactly as on RCCL; the GPU-backed
+and the final ranked gather (full and top-k) are exercised exactly as on RCCL; the GPU-backed
 version of the same flow is tests/test_gpu_dist.py."""
 import ctypes
 import hashlib
@@ -30,13 +30,6 @@ def test_tail_plan():
     assert mdist.tail_plan(0, heads, sizes) == ([0, 0, 0], [0, 10, 4])
     assert mdist.tail_plan(1, heads, sizes) == ([10, 0, 0], [0, 0, 0])
     assert mdist.tail_plan(2, heads, sizes) == ([4, 0, 0], [0, 0, 0])
-
-
-def test_merge_ranked_is_entry_compare_desc():
-    a = [(b"the", 9), (b"abc", 3), (b"zed", 3)]
-    b = [(b"you", 9), (b"abd", 3), (b"a", 1)]
-    got = mdist.merge_ranked([a, b])
-    assert got == sorted(a + b, key=lambda kv: (-kv[1], kv[0]))
 
 
 # ------------------------------------------------------------ host stand-in
@@ -110,8 +103,15 @@ class FakeCtx:
     def export_copy(self, dst):
         ctypes.memmove(dst, self.exported, len(self.exported))
 
+    def export_ranked(self, table, limit):
+        r = self.ranked(table, 0, limit or None)
+        self.exported = b"".join(len(k).to_bytes(4, "little") + c.to_bytes(8, "little") + k for k, c in r)
+        return len(self.exported)
+
     def import_partitions(self, table, src, offs):
+        # like msa_import_partitions: the table becomes the union of the blocks
         raw = ctypes.string_at(src, offs[-1]) if offs[-1] else b""
+        self.merged = {}
         i = 0
         while i < len(raw):
             kl = int.from_bytes(raw[i:i + 4], "little")
@@ -119,6 +119,9 @@ class FakeCtx:
             k = raw[i + 12:i + 12 + kl]
             self.merged[k] = self.merged.get(k, 0) + c
             i += 12 + kl
+
+    def rank(self):
+        pass
 
     def ranked(self, table, first=0, count=None):
         r = sorted(self.merged.items(), key=lambda kv: (-kv[1], kv[0]))
@@ -140,9 +143,15 @@ def _worker(rank, world, port, data, cuts, q):
             counts[r] = counts.get(r, 0) + 1
         ctx.set_counts(counts)
         mdist.merge_table(ctx, comm, 0)
-        ranked = mdist.gather_ranked(ctx, comm, 0)
+        top = ctx.ranked(0, 0, 3)  # this rank's partition
+        root = mdist.gather_ranked(ctx, comm, tables=(0,))
+        ranked = ctx.ranked(0) if root else None
         tot = comm.all_reduce_sum([len(recs)])
-        q.put((rank, seg, ranked, tot))
+        # top-k gather: each rank sends its top 3, the root ranks the union
+        ctx.merged = dict(top)
+        mdist.gather_ranked(ctx, comm, topk=3, tables=(0,))
+        top3 = ctx.ranked(0, 0, 3) if root else None
+        q.put((rank, seg, ranked, tot, top3))
     finally:
         dist.destroy_process_group()
 
@@ -175,8 +184,8 @@ def test_gloo_world_resolves_and_merges(cuts_kind):
         p.start()
     res = {}
     for _ in range(world):
-        r, seg, ranked, tot = q.get(timeout=60)
-        res[r] = (seg, ranked, tot)
+        r, seg, ranked, tot, top3 = q.get(timeout=60)
+        res[r] = (seg, ranked, tot, top3)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -187,4 +196,7 @@ def test_gloo_world_resolves_and_merges(cuts_kind):
     expect = {}
     for r in whole:
         expect[r] = expect.get(r, 0) + 1
-    assert res[0][1] == sorted(expect.items(), key=lambda kv: (-kv[1], kv[0]))
+    full = sorted(expect.items(), key=lambda kv: (-kv[1], kv[0]))
+    assert res[0][1] == full
+    assert res[0][3] == full[:3]
+    assert all(res[r][1] is None for r in range(1, world))

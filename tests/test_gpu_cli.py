@@ -51,3 +51,67 @@ def test_cli_errors(case, msg, tmp_path):
                        capture_output=True, timeout=120)
     assert p.returncode != 0
     assert msg in p.stderr
+
+
+# ------------------------------------------------------------------ ranks
+# --processes N: N rank processes (host shared-memory transport when they
+# share the box's one GPU; RCCL with one GPU per rank).  Results must equal
+# the single-process reference for every N -- the reference's own depend on
+# -np (tests/test_oracle.py::test_reference_is_np_dependent).
+@pytest.mark.parametrize("case,procs", [("zipf_small", 2), ("zipf_small", 3), ("torture_3", 2), ("torture_17", 4),
+                                        ("zipf_crlf", 3), ("nul_bytes", 2), ("long_words", 2),
+                                        ("multiline_artist_header", 2), ("quotes_everywhere", 3), ("header_only", 2),
+                                        ("highcard_small", 4), ("cr_only", 2)])
+def test_cli_processes_match_single(case, procs, tmp_path):
+    if case not in CASES:
+        pytest.skip(f"no golden case {case}")
+    res, files = golden(case, 1)
+    out = tmp_path / "out"
+    p = subprocess.run([CLI, os.path.join(GOLDEN, case, "input.csv"), "--output-dir", str(out),
+                        "--processes", str(procs)], capture_output=True, timeout=180)
+    assert p.returncode == 0, p.stderr
+    got = read_outputs(str(out))
+    assert got["metrics"] == {"processes": procs, "total_songs": res["total_songs"], "total_words": res["total_words"]}
+    assert got["word_counts.csv"] == files["word_counts.csv"]
+    assert got["top_artists.csv"] == files["top_artists.csv"]
+    assert got["split"] == files["split"]
+    assert p.stdout.decode("latin-1") == res["stdout"]
+
+
+def test_cli_rank_path_rccl_world_of_one(tmp_path):
+    """The RCCL transport end to end on the box's one GPU (a world of one:
+    communicator init, all-gathers, send/recv to self)."""
+    case = "zipf_small"
+    res, files = golden(case, 1)
+    out = tmp_path / "out"
+    env = dict(os.environ, MSA_RANK_PATH="1", MSA_TRANSPORT="rccl")
+    p = subprocess.run([CLI, os.path.join(GOLDEN, case, "input.csv"), "--output-dir", str(out)],
+                       capture_output=True, timeout=180, env=env)
+    assert p.returncode == 0, p.stderr
+    got = read_outputs(str(out))
+    assert got["word_counts.csv"] == files["word_counts.csv"]
+    assert got["top_artists.csv"] == files["top_artists.csv"]
+    assert got["split"] == files["split"]
+    assert p.stdout.decode("latin-1") == res["stdout"]
+
+
+def test_cli_processes_limits(tmp_path):
+    case = "zipf_small"
+    res, files = golden(case, 1)
+    out = tmp_path / "out"
+    p = subprocess.run([CLI, os.path.join(GOLDEN, case, "input.csv"), "--output-dir", str(out), "--processes", "3",
+                        "--word-limit", "7", "--artist-limit", "3"], capture_output=True, timeout=180)
+    assert p.returncode == 0, p.stderr
+    assert open(out / "word_counts.csv", "rb").read() == b"\n".join(files["word_counts.csv"].split(b"\n")[:8]) + b"\n"
+    assert open(out / "top_artists.csv", "rb").read() == b"\n".join(files["top_artists.csv"].split(b"\n")[:4]) + b"\n"
+    assert p.stdout.decode("latin-1") == res["stdout"]
+
+
+@pytest.mark.parametrize("case,msg", [("empty_file", b"Dataset does not contain a header row"),
+                                      ("bad_header", b"Unable to parse dataset header")])
+def test_cli_processes_errors(case, msg, tmp_path):
+    """A failing rank ends the whole job (the others may wait in a collective)."""
+    p = subprocess.run([CLI, os.path.join(GOLDEN, case, "input.csv"), "--output-dir", str(tmp_path / "o"),
+                        "--processes", "2"], capture_output=True, timeout=120)
+    assert p.returncode != 0
+    assert msg in p.stderr

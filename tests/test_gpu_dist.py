@@ -31,9 +31,9 @@ ctx = msa.Context(0)
 ctx.load_csv(data[lo:hi])
 comm = mdist.Comm()
 songs, words = mdist.run_sharded(ctx, comm, text_column=False)
-w = mdist.gather_ranked(ctx, comm, msa.MSA_TABLE_WORDS)
-a = mdist.gather_ranked(ctx, comm, msa.MSA_TABLE_ARTISTS)
-if rank == 0:
+if mdist.gather_ranked(ctx, comm):
+    w = ctx.ranked(msa.MSA_TABLE_WORDS)
+    a = ctx.ranked(msa.MSA_TABLE_ARTISTS)
     out = os.environ["MSA_OUT"]
     open(out + ".words", "wb").write(msa.table_csv_bytes(w, "word"))
     open(out + ".artists", "wb").write(msa.table_csv_bytes(a, "artist"))

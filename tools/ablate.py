@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
-"""Diagnostic: time K3 (k_scan_main<0>) under kernel ablations (MSA_ABLATE bits,
-see msa_scan.hip).  Results of ablated runs are wrong by design; only the
+"""Diagnostic: time K3 (k_scan_csv) under kernel ablations (MSA_ABLATE bits,
+see msa_k3.hip), with its LDS-table miss count.  Results of ablated runs are wrong by design; only the
 stage times are read.  Usage: python tools/ablate.py [songs] [bits ...]"""
+import ctypes as C
 import os
 import sys
 
@@ -23,4 +24,10 @@ for b in bits:
             c.run()
         p = c.profile(reset=True)
         st = {k: round(v["ms"] / v["launches"], 3) for k, v in p.items()}
-        print(f"ablate={b:2d} csv_scan={st.get('csv_scan')} ms  all={st}", flush=True)
+        lib = msa.load()
+        lib.msa_debug_stat.argtypes = [C.c_void_p, C.c_char_p, C.POINTER(C.c_uint64)]
+        mv, tw = C.c_uint64(), C.c_uint64()
+        lib.msa_debug_stat(c.h, b"k3_misses", C.byref(mv))
+        lib.msa_debug_stat(c.h, b"total_words", C.byref(tw))
+        print(f"ablate={b:2d} csv_scan={st.get('csv_scan')} ms  misses={mv.value} of {tw.value} words  all={st}",
+              flush=True)

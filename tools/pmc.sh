@@ -1,17 +1,29 @@
 #!/usr/bin/env bash
 # PMC passes over bench.py (run ON the GPU box, from the repo root), one
-# rocprofv3 run per counter group, as MI355X_MICROARCH.md prescribes:
-#   pass 1  FETCH_SIZE            (TCC: 3 slots)
-#   pass 2  WRITE_SIZE            (TCC: 2 slots)
-#   pass 3  SQ counters of K3     (8 SQ slots)
-# Then tools/pmc_summary.py folds them into profiles/pmc_scan_main.json.
+# rocprofv3 run per counter group, as MI355X_MICROARCH.md prescribes
+# (FETCH_SIZE takes 3 TCC slots, WRITE_SIZE 2: never in one pass):
+#   fetch   FETCH_SIZE
+#   write   WRITE_SIZE
+#   sq      8 SQ counters (waves, cycles, VALU/LDS instructions, LDS bank conflicts, waits)
+#   atomic  TCC_ATOMIC_sum TCC_EA0_ATOMIC_sum (L2 / memory-side atomics),
+#           TA_FLAT_ATOMIC_WAVEFRONTS_sum TA_BUFFER_ATOMIC_WAVEFRONTS_sum (issued),
+#           SQ_INSTS_LDS_ATOMIC
+# tools/pmc_summary.py then folds them, per kernel, into $OUT/pmc.json stamped
+# with the sha256 of the libmsa_hip.so that ran (copy it to
+# profiles/pmc_scan_main.json; bench.py only attaches `traffic` when the stamp
+# matches the library it loaded).
 set -euo pipefail
 export TMPDIR=/tmp
 OUT=${1:-gpurun_out/pmc}
 STEPS=${STEPS:-1}
 mkdir -p "$OUT"
 B=(python3 bench.py --steps "$STEPS" --warmup 1 --no-cpu-baseline)
-timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- "${B[@]}" > "$OUT/fetch.log" 2>&1
-timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- "${B[@]}" > "$OUT/write.log" 2>&1
-timeout -s KILL 150 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_ANY --output-format csv -d "$OUT/sq" -o run -- "${B[@]}" > "$OUT/sq.log" 2>&1
+pass() {  # name counters...
+  local name=$1; shift
+  timeout -s KILL 150 rocprofv3 --pmc "$@" --output-format csv -d "$OUT/$name" -o run -- "${B[@]}" > "$OUT/$name.log" 2>&1
+}
+pass fetch FETCH_SIZE
+pass write WRITE_SIZE
+pass sq SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_ANY
+pass atomic TCC_ATOMIC_sum TCC_EA0_ATOMIC_sum TA_FLAT_ATOMIC_WAVEFRONTS_sum TA_BUFFER_ATOMIC_WAVEFRONTS_sum SQ_INSTS_LDS_ATOMIC
 python3 tools/pmc_summary.py "$OUT"

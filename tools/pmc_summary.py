@@ -1,35 +1,61 @@
 #!/usr/bin/env python3
-"""Fold the rocprofv3 PMC passes of tools/pmc.sh into profiles/pmc_scan_main.json.
+"""Fold the rocprofv3 PMC passes of tools/pmc.sh into OUT/pmc.json (copied to
+profiles/pmc_scan_main.json).
 
-HBM bytes per K3 launch = (2 x FETCH_SIZE + WRITE_SIZE) x 1024: rocprofv3 reports
-both in KiB, and on gfx950 FETCH_SIZE counts exactly half of a wide (16 B/lane)
-coalesced streaming read (MI355X_MICROARCH.md, HBM section) -- K3 reads the CSV
-that way.  The SQ pass is summarised as-is (per launch means)."""
+Per kernel of the bench step, per launch (mean over dispatches):
+  hbm_bytes   = (2 x FETCH_SIZE + WRITE_SIZE) x 1024.  rocprofv3 reports both in
+                KiB; on gfx950 FETCH_SIZE counts exactly half of a wide (16 B/lane)
+                coalesced streaming read (MI355X_MICROARCH.md, HBM section).  The
+                correction is exact for k_scan_csv / k_chunk_summary (dwordx4 per
+                lane streams); for gather-type kernels fetch_raw_bytes is given too.
+  atomics     TCC_ATOMIC_sum (atomics reaching the L2), TCC_EA0_ATOMIC_sum
+                (atomics leaving the L2 to memory), TA_*_ATOMIC_WAVEFRONTS_sum
+                (atomic wave instructions issued), SQ_INSTS_LDS_ATOMIC
+  sq          SQ_LDS_BANK_CONFLICT (cycles), SQ_INSTS_LDS, waits, ...
+The file is stamped with the sha256 of the libmsa_hip.so in this tree and with
+the bench line the passes ran (input bytes, K3 algorithmic bytes)."""
 import csv
 import glob
+import hashlib
 import json
 import os
 import sys
 
-KERNEL = "k_scan_main<0>"
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(REPO, "music-analyst-ai_amd", "libmsa_hip.so")
+KERNELS = ["k_scan_csv", "k_miss_agg", "k_chunk_summary", "k_rec_spans", "k_col_gather", "k_col_lines",
+           "k_artist_count", "k_tile_sort", "k_merge_pass"]
+PASSES = ["fetch", "write", "sq", "atomic"]
 
 
-def rows(d):
-    out = []
-    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
-        with open(f) as fh:
-            out.extend(csv.DictReader(fh))
-    return out
+def lib_sha256(path=LIB):
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for b in iter(lambda: f.read(1 << 20), b""):
+            h.update(b)
+    return h.hexdigest()
 
 
-def per_launch(d, counter):
-    vals = {}
-    for r in rows(d):
-        if KERNEL not in r.get("Kernel_Name", "") or r.get("Counter_Name") != counter:
-            continue
-        key = r.get("Dispatch_Id") or r.get("Correlation_Id")
-        vals[key] = vals.get(key, 0.0) + float(r["Counter_Value"])
-    return (sum(vals.values()) / len(vals), len(vals)) if vals else (None, 0)
+def short(name):
+    for k in KERNELS:
+        if name.startswith(k + "(") or name.startswith(k + "<") or name == k:
+            return k
+    return None
+
+
+def collect(out):
+    acc = {}  # kernel -> counter -> {dispatch: value}
+    for p in PASSES:
+        for f in glob.glob(os.path.join(out, p, "**", "*counter_collection.csv"), recursive=True):
+            with open(f) as fh:
+                for r in csv.DictReader(fh):
+                    k = short(r.get("Kernel_Name", ""))
+                    if not k:
+                        continue
+                    key = (p, r.get("Dispatch_Id") or r.get("Correlation_Id"))
+                    c = acc.setdefault(k, {}).setdefault(r["Counter_Name"], {})
+                    c[key] = c.get(key, 0.0) + float(r["Counter_Value"])
+    return {k: {c: sum(v.values()) / len(v) for c, v in cs.items()} for k, cs in acc.items()}
 
 
 def bench_line(log):
@@ -44,29 +70,35 @@ def bench_line(log):
 
 def main():
     out = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
-    fetch, nf = per_launch(os.path.join(out, "fetch"), "FETCH_SIZE")
-    write, nw = per_launch(os.path.join(out, "write"), "WRITE_SIZE")
-    sq = {}
-    for c in ("SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_WAIT_INST_LDS",
-              "SQ_LDS_BANK_CONFLICT", "SQ_WAIT_ANY"):
-        v, _ = per_launch(os.path.join(out, "sq"), c)
-        sq[c] = v
+    per = collect(out)
+    kernels = {}
+    for k, c in per.items():
+        e = {"counters": c}
+        if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+            e["hbm_bytes_per_launch"] = int((2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024)
+            e["fetch_raw_bytes_per_launch"] = int(c["FETCH_SIZE"] * 1024)
+            e["write_bytes_per_launch"] = int(c["WRITE_SIZE"] * 1024)
+        kernels[k] = e
     b = bench_line(os.path.join(out, "fetch.log"))
     res = {
-        "kernel": KERNEL,
+        "lib_sha256": lib_sha256(),
         "input_bytes": b["config"]["bytes_per_gpu"] if b else None,
+        "roofline_kernel": "k_scan_csv",
         "alg_bytes_per_launch": b["roofline"]["alg_bytes_per_launch"] if b else None,
-        "fetch_size_kib_per_launch": fetch,
-        "write_size_kib_per_launch": write,
-        "launches_seen": {"fetch": nf, "write": nw},
-        "hbm_bytes_per_launch": int((2 * fetch + write) * 1024) if fetch is not None and write is not None else None,
         "correction": "hbm = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE halves 16B/lane streams)",
-        "sq_per_launch": sq,
+        "command": "tools/pmc.sh: rocprofv3 --pmc <group> -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline",
+        "kernels": kernels,
     }
-    # written next to the passes (gpurun_out/ travels back); copy to profiles/
-    with open(os.path.join(out, "pmc_scan_main.json"), "w") as f:
+    k3 = kernels.get("k_scan_csv", {})
+    if res["alg_bytes_per_launch"] and k3.get("hbm_bytes_per_launch"):
+        res["traffic_over_alg"] = round(k3["hbm_bytes_per_launch"] / res["alg_bytes_per_launch"], 3)
+    with open(os.path.join(out, "pmc.json"), "w") as f:
         json.dump(res, f, indent=1)
-    print(json.dumps(res, indent=1))
+    for k, e in sorted(kernels.items()):
+        print(k, json.dumps({x: round(y, 1) for x, y in e["counters"].items()}))
+        if "hbm_bytes_per_launch" in e:
+            print("   hbm bytes/launch", e["hbm_bytes_per_launch"])
+    print("traffic_over_alg", res.get("traffic_over_alg"))
 
 
 if __name__ == "__main__":
