@@ -169,6 +169,13 @@ def load(path: str = LIB_PATH):
     return lib
 
 
+def _bytes_at(ptr, n: int) -> bytes:
+    """bytes of a malloc'ed C buffer (ctypes.string_at truncates sizes to 32 bits)."""
+    if n == 0:
+        return b""
+    return bytes((C.c_ubyte * n).from_address(ptr.value if isinstance(ptr, C.c_void_p) else ptr))
+
+
 def gen_corpus(n_songs: int, mode: str = "zipf", seed: int = 1, vocab: int = 50000, n_artists: int = 5000,
                words_per_song: int = 30, crlf: bool = False, first_song: int = 0,
                count: Optional[int] = None) -> bytes:
@@ -187,7 +194,7 @@ def gen_corpus(n_songs: int, mode: str = "zipf", seed: int = 1, vocab: int = 500
     if rc:
         raise MsaError(rc, "corpus generation failed")
     try:
-        return C.string_at(out, n.value)
+        return _bytes_at(out, n.value)
     finally:
         lib.msa_free(out)
 
@@ -352,7 +359,7 @@ class Context:
         n = C.c_size_t()
         self._check(self.lib.msa_get_split_column(self.h, which, C.byref(out), C.byref(n)))
         try:
-            return C.string_at(out, n.value)
+            return _bytes_at(out, n.value)
         finally:
             self.lib.msa_free(out)
 
@@ -419,7 +426,7 @@ class WordCountPerSong:
         n = C.c_size_t()
         self._check(self.lib.msa_wcs_get_csv(self.h, which, C.byref(out), C.byref(n)))
         try:
-            return C.string_at(out, n.value)
+            return _bytes_at(out, n.value)
         finally:
             self.lib.msa_free(out)
 
@@ -437,7 +444,7 @@ class WordCountPerSong:
         n = C.c_size_t()
         self._check(fn(self.h, col, C.byref(out), C.byref(n)))
         try:
-            return C.string_at(out, n.value)
+            return _bytes_at(out, n.value)
         finally:
             self.lib.msa_free(out)
 

@@ -103,3 +103,14 @@ def test_configs2_full_size(msa_mod, ctx, tmp_path):
     data = msa_mod.gen_corpus(5_000_000, mode="zipf", seed=1, vocab=50000, n_artists=5000, words_per_song=30)
     assert len(data) > 1_000_000_000
     check_against_oracle(msa_mod, ctx, data, tmp_path, "configs2")
+
+
+@pytest.mark.timeout(900)
+def test_corpus_over_4gib(msa_mod, tmp_path):
+    """A 20M-song corpus (~4.7 GB > 2^32 bytes) on one GPU against the oracle:
+    no 32-bit byte offset anywhere in the pipeline (at N = 2 the configs[3]
+    shards are ~12 GB per GPU)."""
+    data = msa_mod.gen_corpus(20_000_000, mode="zipf", seed=1, vocab=50000, n_artists=5000, words_per_song=30)
+    assert len(data) > (1 << 32)
+    with msa_mod.Context(0) as c:
+        check_against_oracle(msa_mod, c, data, tmp_path, "over4g")
