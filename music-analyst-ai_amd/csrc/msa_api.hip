@@ -48,6 +48,14 @@ hipError_t msa_launch_word_entries(const EntryArgs &, hipStream_t);
 hipError_t msa_launch_list_build(const u64 *, u64, u32, u32 *, u64, u64 *, Counters *, u64, hipStream_t);
 hipError_t msa_launch_artist_entries(const u64 *, const u32 *, u64, const u8 *, const u64 *, const u32 *, u64 *, u64 *,
                                      u64 *, u32 *, u64 *, u64 *, hipStream_t);
+u64 msa_radix_scratch_bytes(u64 n);
+hipError_t msa_radix_sort(u64 *const[3], u64 *const[3], u64 *const[3], u32 *const[3], u64, int *, u8 *, hipStream_t);
+hipError_t msa_launch_tie_mark(const u64 *, const u64 *, const u64 *, u64, u64 *, u64 *, hipStream_t);
+hipError_t msa_launch_tie_build(const u64 *, const u64 *, const u64 *, const u64 *, u64, const u32 *, const u64 *, u32,
+                                const u64 *,
+                                const u8 *, const u8 *, const u64 *, const u32 *, const u8 *, const u64 *, const u32 *,
+                                u64 *, u64 *, u64 *, u32 *, u32 *, u64 *, hipStream_t);
+hipError_t msa_launch_tie_apply(const u32 *, const u32 *, const u64 *, u64, u32 *, u32 *, u64 *, hipStream_t);
 hipError_t msa_launch_sort(u64 *const[3], u64 *const[3], u64 *const[3], u32 *const[3], u64, int *, hipStream_t);
 hipError_t msa_launch_fixup(const u64 *, const u64 *, const u64 *, const u32 *, u64, const u64 *, const u8 *,
                             const u8 *, const u64 *, const u32 *, const u8 *, const u64 *, const u32 *, u32 *, hipStream_t);
@@ -137,6 +145,11 @@ struct msa_ctx {
     DevBuf acol, alen, aoff, asrc, apairs, tcol, tlen, toff, tsrc, tpairs, scan_bsum, scan_total;
     int cus = 256;
     int ablate = 0;  // MSA_ABLATE: diagnostic kernel ablations (results invalid)
+    int sort_mode = 0;  // MSA_SORT: 0 by size, 1 merge sort, 2 radix sort
+    DevBuf sort_scratch;
+    // tie refinement of the radix path: per-level marks/scans, the subset's
+    // three key sets + values, and its order positions
+    DevBuf t_head, t_tie, t_runid, t_tpos, t_bsum, t_total, t_K[3][3], t_V[3], t_Vn, t_Pn, t_Vc, t_Pc;
     u64 acol_len = 0, a_hdr_getline = 0, a_hdr_len = 0, tcol_len = 0;
     // artist pass: true = the exact record reader over artist.csv (forced by
     // msa_set_artist_reader / an artist piece set for a shard); otherwise the
@@ -844,6 +857,69 @@ static int do_count(msa_ctx *c) {
 }
 
 // ------------------------------------------------------------------ stage 3
+static const u64 kRadixMin = 1ull << 18;
+
+// Order of entries equal in (count, first 16 key bytes), radix path: round r
+// re-sorts the tied entries by (their run, key bytes [16 r, 16 r + 16)) with
+// the radix sort, until no two adjacent keys are equal (keys are distinct).
+static int refine_ties(msa_ctx *c, Ranked &R, int cur, const u8 *wbuf, const u8 *wextra, const u8 *arena,
+                       const u64 *key_off, const u32 *key_len) {
+    const u64 n = R.n;
+    HIPC(c, hipMemcpyAsync(R.order.p, R.V[cur].p, n * 4, hipMemcpyDeviceToDevice, c->stream));
+    for (DevBuf *b : {&c->t_head, &c->t_tie, &c->t_runid, &c->t_tpos}) HIPC(c, ensure(*b, n * 8));
+    HIPC(c, ensure(c->t_bsum, ((n + 1023) / 1024 + 1) * 8));
+    HIPC(c, ensure(c->t_total, 64));
+    const u64 *K2 = R.K[cur][0].as<u64>(), *K1 = R.K[cur][1].as<u64>(), *K0 = R.K[cur][2].as<u64>();
+    const u32 *Vc = R.V[cur].as<u32>();
+    const u64 *Pc = nullptr;
+    u64 mc = n;
+    for (u32 r = 1; r < 4096; ++r) {
+        HIPC(c, msa_launch_tie_mark(K2, K1, K0, mc, c->t_head.as<u64>(), c->t_tie.as<u64>(), c->stream));
+        HIPC(c, msa_exclusive_scan(c->t_head.as<u64>(), mc, c->t_runid.as<u64>(), c->t_bsum.as<u64>(),
+                                   c->t_total.as<u64>(), c->stream));
+        HIPC(c, msa_exclusive_scan(c->t_tie.as<u64>(), mc, c->t_tpos.as<u64>(), c->t_bsum.as<u64>(),
+                                   c->t_total.as<u64>(), c->stream));
+        u64 m = 0;
+        HIPC(c, hipMemcpyAsync(&m, c->t_total.p, 8, hipMemcpyDeviceToHost, c->stream));
+        HIPC(c, hipStreamSynchronize(c->stream));
+        if (c->ablate & 4096) fprintf(stderr, "refine_ties: n %llu round %u ties %llu\n", (unsigned long long)n, r,
+                                      (unsigned long long)m);
+        if (!m) return MSA_OK;
+        for (int s = 0; s < 3; ++s) {
+            for (int k = 0; k < 3; ++k) HIPC(c, ensure(c->t_K[s][k], m * 8));
+            HIPC(c, ensure(c->t_V[s], m * 4));
+        }
+        HIPC(c, ensure(c->t_Vn, m * 4));
+        HIPC(c, ensure(c->t_Pn, m * 8));
+        HIPC(c, ensure(c->t_Vc, m * 4));
+        HIPC(c, ensure(c->t_Pc, m * 8));
+        u64 *k2[3], *k1[3], *k0[3];
+        u32 *vv[3];
+        for (int s = 0; s < 3; ++s) {
+            k2[s] = c->t_K[s][0].as<u64>();
+            k1[s] = c->t_K[s][1].as<u64>();
+            k0[s] = c->t_K[s][2].as<u64>();
+            vv[s] = c->t_V[s].as<u32>();
+        }
+        HIPC(c, msa_launch_tie_build(c->t_runid.as<u64>(), c->t_head.as<u64>(), c->t_tie.as<u64>(), c->t_tpos.as<u64>(),
+                                     mc, Vc, Pc, r,
+                                     R.ref.as<u64>(), wbuf, wextra, c->l_pos.as<u64>(), c->l_len.as<u32>(), arena,
+                                     key_off, key_len, k2[0], k1[0], k0[0], vv[0], c->t_Vn.as<u32>(),
+                                     c->t_Pn.as<u64>(), c->stream));
+        int o = 1;
+        HIPC(c, msa_radix_sort(k2, k1, k0, vv, m, &o, c->sort_scratch.as<u8>(), c->stream));
+        HIPC(c, msa_launch_tie_apply(vv[o], c->t_Vn.as<u32>(), c->t_Pn.as<u64>(), m, R.order.as<u32>(),
+                                     c->t_Vc.as<u32>(), c->t_Pc.as<u64>(), c->stream));
+        K2 = k2[o];
+        K1 = k1[o];
+        K0 = k0[o];
+        Vc = c->t_Vc.as<u32>();
+        Pc = c->t_Pc.as<u64>();
+        mc = m;
+    }
+    return fail(c, MSA_ERR_COLLISION, "tie refinement did not converge (equal keys in one table)");
+}
+
 static int sort_and_blob(msa_ctx *c, Ranked &R, const u8 *wbuf, const u8 *wextra, const u8 *arena, const u64 *key_off,
                          const u32 *key_len) {
     const u64 n = R.n;
@@ -865,11 +941,20 @@ static int sort_and_blob(msa_ctx *c, Ranked &R, const u8 *wbuf, const u8 *wextra
         vv[s] = R.V[s].as<u32>();
     }
     int cur = 1;
-    HIPC(c, msa_launch_sort(k2, k1, k0, vv, n, &cur, c->stream));
+    // large tables: LSD radix sort (msa_sort.hip); small ones: LDS bitonic
+    // tiles + merge passes (launch-bound sizes).  MSA_SORT=radix|merge forces one.
     HIPC(c, ensure(R.order, n * 4));
-    HIPC(c, msa_launch_fixup(R.K[cur][0].as<u64>(), R.K[cur][1].as<u64>(), R.K[cur][2].as<u64>(), R.V[cur].as<u32>(),
-                             n, R.ref.as<u64>(), wbuf, wextra, c->l_pos.as<u64>(), c->l_len.as<u32>(), arena, key_off,
-                             key_len, R.order.as<u32>(), c->stream));
+    if (c->sort_mode == 2 || (c->sort_mode == 0 && n >= kRadixMin)) {
+        HIPC(c, ensure(c->sort_scratch, msa_radix_scratch_bytes(n)));
+        HIPC(c, msa_radix_sort(k2, k1, k0, vv, n, &cur, c->sort_scratch.as<u8>(), c->stream));
+        int rc;
+        if ((rc = refine_ties(c, R, cur, wbuf, wextra, arena, key_off, key_len))) return rc;
+    } else {
+        HIPC(c, msa_launch_sort(k2, k1, k0, vv, n, &cur, c->stream));
+        HIPC(c, msa_launch_fixup(R.K[cur][0].as<u64>(), R.K[cur][1].as<u64>(), R.K[cur][2].as<u64>(),
+                                 R.V[cur].as<u32>(), n, R.ref.as<u64>(), wbuf, wextra, c->l_pos.as<u64>(),
+                                 c->l_len.as<u32>(), arena, key_off, key_len, R.order.as<u32>(), c->stream));
+    }
     // key blob in rank order
     HIPC(c, ensure(R.len, n * 8));
     HIPC(c, ensure(R.off, (n + 1) * 8));
@@ -979,6 +1064,7 @@ int msa_create(int device, msa_ctx **out) {
     msa_ctx *c = new msa_ctx();
     c->device = device;
     if (const char *ab = getenv("MSA_ABLATE")) c->ablate = atoi(ab);
+    if (const char *so = getenv("MSA_SORT")) c->sort_mode = !strcmp(so, "merge") ? 1 : (!strcmp(so, "radix") ? 2 : 0);
     {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
@@ -1000,7 +1086,9 @@ void msa_destroy(msa_ctx *c) {
                      &c->nulrel, &c->acol, &c->alen, &c->aoff, &c->asrc, &c->apairs, &c->tcol, &c->tlen, &c->toff, &c->tsrc, &c->tpairs,
                      &c->scan_bsum, &c->scan_total, &c->ar_start, &c->arena, &c->key_off,
                      &c->key_len, &c->key_slot, &c->s_tab, &c->s_list, &c->m_tab, &c->m_list, &c->l_pos, &c->l_len,
-                     &c->l_slot, &c->l_tab, &c->l_list, &c->a_tab, &c->a_list, &c->ctr, &c->kh1, &c->kh2, &c->mlog, &c->mlog_n};
+                     &c->l_slot, &c->l_tab, &c->l_list, &c->a_tab, &c->a_list, &c->ctr, &c->kh1, &c->kh2, &c->mlog, &c->mlog_n, &c->sort_scratch,
+                     &c->t_head, &c->t_tie, &c->t_runid, &c->t_tpos, &c->t_bsum, &c->t_total, &c->t_Vn, &c->t_Pn,
+                     &c->t_Vc, &c->t_Pc};
     for (DevBuf *b : all) release(*b);
     for (Ranked *R : {&c->rw, &c->ra}) {
         for (auto &s : R->K)
@@ -1009,6 +1097,9 @@ void msa_destroy(msa_ctx *c) {
         DevBuf *rb[] = {&R->ref, &R->cnt, &R->order, &R->len, &R->off, &R->blob, &R->counts};
         for (DevBuf *b : rb) release(*b);
     }
+    for (auto &s : c->t_K)
+        for (auto &k : s) release(k);
+    for (auto &v : c->t_V) release(v);
     for (ProfStage &s : c->ps) {
         if (s.a) (void)hipEventDestroy(s.a);
         if (s.b) (void)hipEventDestroy(s.b);

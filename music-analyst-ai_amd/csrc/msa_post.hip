@@ -1378,6 +1378,75 @@ __global__ void k_tie_fixup(const u64 *__restrict__ K2, const u64 *__restrict__ 
 }
 
 // ---------------------------------------------------------------------------
+// Tie refinement (radix path): instead of comparing every pair of a tie run,
+// the tied entries are sorted again by (run, next 16 key bytes), round after
+// round, until no two adjacent keys are equal.  A run of thousands of artists
+// sharing 16 bytes and a count (configs[4]) costs one small radix sort, not
+// run^2 string compares.
+__global__ void k_tie_mark(const u64 *__restrict__ K2, const u64 *__restrict__ K1, const u64 *__restrict__ K0, u64 n,
+                           u64 *__restrict__ head, u64 *__restrict__ tie) {
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const u64 a2 = K2[i], a1 = K1[i], a0 = K0[i];
+    const bool eq_prev = i > 0 && K2[i - 1] == a2 && K1[i - 1] == a1 && K0[i - 1] == a0;
+    const bool eq_next = i + 1 < n && K2[i + 1] == a2 && K1[i + 1] == a1 && K0[i + 1] == a0;
+    head[i] = eq_prev ? 0 : 1;
+    tie[i] = (eq_prev || eq_next) ? 1 : 0;
+}
+
+// key bytes [16 r, 16 r + 16) of an entry as two big-endian words (zero past its end)
+__device__ __forceinline__ void key16_round(u64 refv, u32 r, const u8 *buf, const u8 *extra, const u64 *l_pos,
+                                            const u32 *l_len, const u8 *arena, const u64 *key_off,
+                                            const u32 *key_len, u64 *hi, u64 *lo) {
+    const u8 *p;
+    u64 n;
+    int lower;
+    key_bytes(refv, 0, 0, buf, extra, l_pos, l_len, arena, key_off, key_len, &p, &n, &lower);
+    const u64 skip = 16ull * r;
+    if (!p || n <= skip) {  // S/M keys end within their first 16 bytes
+        *hi = 0;
+        *lo = 0;
+        return;
+    }
+    be16(p + skip, n - skip, lower, hi, lo);
+}
+
+// runid = exclusive scan of head (+ head: run index of each entry), tpos = exclusive
+// scan of tie; entry i of the current level (value Vc[i], order position
+// Pc ? Pc[i] : i) goes to slot tpos[i] of the next level's subset
+__global__ void k_tie_build(const u64 *__restrict__ runid, const u64 *__restrict__ head, const u64 *__restrict__ tie,
+                            const u64 *__restrict__ tpos,
+                            u64 mc, const u32 *__restrict__ Vc, const u64 *__restrict__ Pc, u32 r,
+                            const u64 *__restrict__ ref, const u8 *buf, const u8 *extra, const u64 *l_pos,
+                            const u32 *l_len, const u8 *arena, const u64 *key_off, const u32 *key_len,
+                            u64 *__restrict__ K2n, u64 *__restrict__ K1n, u64 *__restrict__ K0n,
+                            u32 *__restrict__ Vid, u32 *__restrict__ Vn, u64 *__restrict__ Pn) {
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= mc || !tie[i]) return;
+    const u64 j = tpos[i];
+    const u32 e = Vc[i];
+    u64 hi, lo;
+    key16_round(ref[e], r, buf, extra, l_pos, l_len, arena, key_off, key_len, &hi, &lo);
+    K2n[j] = runid[i] + head[i];  // inclusive count of run heads: the same for every entry of a run
+    K1n[j] = hi;
+    K0n[j] = lo;
+    Vid[j] = (u32)j;
+    Vn[j] = e;
+    Pn[j] = Pc ? Pc[i] : i;
+}
+
+// the subset sorted (perm): its entries take the same order positions, in order
+__global__ void k_tie_apply(const u32 *__restrict__ perm, const u32 *__restrict__ Vn, const u64 *__restrict__ Pn,
+                            u64 m, u32 *__restrict__ order, u32 *__restrict__ Vc, u64 *__restrict__ Pc) {
+    const u64 j = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= m) return;
+    const u32 e = Vn[perm[j]];
+    order[Pn[j]] = e;
+    Vc[j] = e;
+    Pc[j] = Pn[j];
+}
+
+// ---------------------------------------------------------------------------
 // Ranked key blob: lengths, then bytes (in rank order).
 __device__ __forceinline__ u64 entry_key_len(u64 ref, u64 k1, u64 k0, const u32 *l_len, const u32 *key_len) {
     const u32 kind = (u32)(ref >> 60);
@@ -1567,5 +1636,25 @@ hipError_t msa_launch_blob(const u32 *order, u64 n, const u64 *ref, const u64 *K
     }
     hipLaunchKernelGGL(k_blob_write, grid1(n), dim3(256), 0, s, order, n, ref, K1u, K0u, cnt, buf, extra, l_pos, l_len, arena,
                        key_off, key_len, (const u64 *)off, blob, counts_out);
+    return hipGetLastError();
+}
+
+hipError_t msa_launch_tie_mark(const u64 *K2, const u64 *K1, const u64 *K0, u64 n, u64 *head, u64 *tie, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_tie_mark, grid1(n), dim3(256), 0, s, K2, K1, K0, n, head, tie);
+    return hipGetLastError();
+}
+hipError_t msa_launch_tie_build(const u64 *runid, const u64 *head, const u64 *tie, const u64 *tpos, u64 mc, const u32 *Vc,
+                                const u64 *Pc,
+                                u32 r, const u64 *ref, const u8 *buf, const u8 *extra, const u64 *l_pos,
+                                const u32 *l_len, const u8 *arena, const u64 *key_off, const u32 *key_len, u64 *K2n,
+                                u64 *K1n, u64 *K0n, u32 *Vid, u32 *Vn, u64 *Pn, hipStream_t s) {
+    if (mc)
+        hipLaunchKernelGGL(k_tie_build, grid1(mc), dim3(256), 0, s, runid, head, tie, tpos, mc, Vc, Pc, r, ref, buf, extra,
+                           l_pos, l_len, arena, key_off, key_len, K2n, K1n, K0n, Vid, Vn, Pn);
+    return hipGetLastError();
+}
+hipError_t msa_launch_tie_apply(const u32 *perm, const u32 *Vn, const u64 *Pn, u64 m, u32 *order, u32 *Vc, u64 *Pc,
+                                hipStream_t s) {
+    if (m) hipLaunchKernelGGL(k_tie_apply, grid1(m), dim3(256), 0, s, perm, Vn, Pn, m, order, Vc, Pc);
     return hipGetLastError();
 }

@@ -15,7 +15,7 @@ import subprocess
 
 import pytest
 
-from conftest import PKG, read_outputs, run_oracle
+from conftest import GOLDEN, PKG, read_outputs, run_oracle
 from test_gpu_parity import check_against_oracle
 
 pytestmark = pytest.mark.gpu
@@ -114,3 +114,23 @@ def test_corpus_over_4gib(msa_mod, tmp_path):
     assert len(data) > (1 << 32)
     with msa_mod.Context(0) as c:
         check_against_oracle(msa_mod, c, data, tmp_path, "over4g")
+
+
+@pytest.mark.parametrize("sort", ["radix", "merge"])
+def test_sort_designs_agree(msa_mod, tmp_path, sort, monkeypatch):
+    """Both ranking sorts, forced on every table size (MSA_SORT): the radix
+    sort on the small torture tables (ties, empty and 16-byte-prefix-sharing
+    keys) and the merge sort on the high-cardinality tables."""
+    monkeypatch.setenv("MSA_SORT", sort)
+    data = msa_mod.gen_corpus(1500, mode="torture", seed=5) if sort == "radix" else None
+    with msa_mod.Context(0) as c:
+        if sort == "radix":
+            check_against_oracle(msa_mod, c, data, tmp_path, "sort_radix_torture")
+            small = msa_mod.gen_corpus(3000, mode="highcard", seed=8, vocab=20000)
+            check_against_oracle(msa_mod, c, small, tmp_path, "sort_radix_hc")
+            for case in ("shared_prefix_ties", "long_words", "quotes_everywhere"):  # 16-byte-prefix tie runs
+                raw = open(os.path.join(GOLDEN, case, "input.csv"), "rb").read()
+                check_against_oracle(msa_mod, c, raw, tmp_path, f"sort_radix_{case}")
+        else:
+            big = msa_mod.gen_corpus(HIGHCARD_SONGS, mode="highcard", seed=HIGHCARD_SEED)
+            check_against_oracle(msa_mod, c, big, tmp_path, "sort_merge_hc")
