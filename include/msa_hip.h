@@ -260,6 +260,12 @@ void msa_wcs_destroy(msa_wcs *w);
 const char *msa_wcs_last_error(const msa_wcs *w);
 void *msa_wcs_stream(msa_wcs *w);
 int msa_wcs_load_csv(msa_wcs *w, const void *host_csv, size_t n);
+/* The reader's field delimiter (default ','): the script's --delimiter, or
+ * what csv.Sniffer guesses on its 65536-character sample (detect_delimiter,
+ * word_count_per_song.py:42-49; split_csv_columns.py:48-66).  One ASCII
+ * byte other than '"', CR, LF and NUL; MSA_ERR_ARG otherwise.  Also the
+ * column splitter's writer delimiter (QUOTE_MINIMAL quoting).              */
+int msa_wcs_set_delimiter(msa_wcs *w, int delimiter);
 /* log2 of the word-table slots of the next run (0 = sized from the input;
  * the table grows by itself when it fills). */
 int msa_wcs_set_table_bits(msa_wcs *w, int bits);

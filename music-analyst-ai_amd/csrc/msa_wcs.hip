@@ -83,8 +83,8 @@ struct WCtr {
     u64 listed;
 };
 
-__host__ __device__ __forceinline__ u32 tpk(u32 b) {
-    return b == '"' ? T_Q : (b == ',' ? T_D : ((b == '\r' || b == '\n') ? T_NL : T_O));
+__host__ __device__ __forceinline__ u32 tpk(u32 b, u32 d) {  // d: the delimiter byte
+    return b == '"' ? T_Q : (b == d ? T_D : ((b == '\r' || b == '\n') ? T_NL : T_O));
 }
 __host__ __device__ __forceinline__ u32 step(u32 t, u32 s) { return (t >> (3 * s)) & 7u; }
 __device__ __forceinline__ u32 map_apply(u32 t, u32 m) {  // m then t
@@ -164,7 +164,7 @@ __device__ __forceinline__ bool eol_after(u32 b, u32 next, u64 i, u64 n) {
 // S: the walker; S::step(t) applies a transfer table, S::eol(i) handles the
 // end of a line after byte i.
 template <typename W>
-__device__ __forceinline__ void seg_walk(const u8 *__restrict__ buf, u64 base, u64 ds, u64 n, W &wk) {
+__device__ __forceinline__ void seg_walk(const u8 *__restrict__ buf, u64 base, u64 ds, u64 n, u32 delim, W &wk) {
     for (u32 q = 0; q < SEG / 16; ++q) {
         const u64 b0 = base + q * 16;
         if (b0 >= n) break;
@@ -173,7 +173,7 @@ __device__ __forceinline__ void seg_walk(const u8 *__restrict__ buf, u64 base, u
         if (b0 < ds) vm &= 0xFFFFu << (u32)(ds - b0);
         if (b0 + 16 > n) vm &= (1u << (u32)(n - b0)) - 1u;
         if (!vm) continue;
-        const u32 Q = mask16(v, '"'), D = mask16(v, ','), NL = mask16(v, '\n'), CR = mask16(v, '\r');
+        const u32 Q = mask16(v, '"'), D = mask16(v, delim), NL = mask16(v, '\n'), CR = mask16(v, '\r');
         const u32 S = (Q | D | NL | CR) & vm;
         const u32 O = vm & ~S;
         u32 E = S;
@@ -187,7 +187,7 @@ __device__ __forceinline__ void seg_walk(const u8 *__restrict__ buf, u64 base, u
             const u32 upto_prev = prev < 0 ? 0u : ((2u << prev) - 1u);
             if (O & ((1u << p) - 1u) & ~upto_prev) wk.step(T_O);  // ordinary bytes in (prev, p)
             const u32 c = byte_of(v, p);
-            wk.step(tpk(c));
+            wk.step(tpk(c, delim));
             const u64 i = b0 + p;
             bool eol = i + 1 == n || c == '\n';
             if (c == '\r' && !eol) eol = (p < 15 ? byte_of(v, p + 1) : (u32)buf[i + 1]) != '\n';
@@ -214,12 +214,12 @@ struct MapWalker {
 
 // Per segment: map over the 6 entering states; row ends per entering state
 // (9 bits each: at most 256 per segment).
-__global__ __launch_bounds__(256) void k_wcs_map(const u8 *__restrict__ buf, u64 ds, u64 n, u64 nseg,
+__global__ __launch_bounds__(256) void k_wcs_map(const u8 *__restrict__ buf, u64 ds, u64 n, u64 nseg, u32 delim,
                                                  u32 *__restrict__ map, u64 *__restrict__ cnt6) {
     const u64 seg = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (seg >= nseg) return;
     MapWalker wk{MAP_ID, 0};
-    seg_walk(buf, seg * SEG, ds, n, wk);
+    seg_walk(buf, seg * SEG, ds, n, delim, wk);
     map[seg] = wk.m;
     cnt6[seg] = wk.c6;
 }
@@ -311,13 +311,13 @@ struct EmitWalker {
     }
 };
 
-__global__ __launch_bounds__(256) void k_wcs_emit(const u8 *__restrict__ buf, u64 ds, u64 n, u64 nseg,
+__global__ __launch_bounds__(256) void k_wcs_emit(const u8 *__restrict__ buf, u64 ds, u64 n, u64 nseg, u32 delim,
                                                   const u32 *__restrict__ sstate, const u64 *__restrict__ roff,
                                                   u64 *__restrict__ rend) {
     const u64 seg = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (seg >= nseg) return;
     EmitWalker wk{sstate[seg], roff[seg], rend};
-    seg_walk(buf, seg * SEG, ds, n, wk);
+    seg_walk(buf, seg * SEG, ds, n, delim, wk);
 }
 
 // ---------------------------------------------------------------------------
@@ -385,6 +385,7 @@ struct RowArgs {
     u64 ds;
     u64 nrows;
     u32 ia, isg, it, need;
+    u32 delim;      // the field delimiter byte (',' unless sniffed / given otherwise)
     u64 *gtab;      // 4 u64 per slot: key, h2 of the word, ~first (pos << 20 | raw len), count
     u64 gmask;
     u64 glimit;
@@ -528,7 +529,7 @@ __device__ __forceinline__ void wcs_row(const RowArgs &a, WgAgg &agg, u64 r) {
         u32 vm = 0xFFFFu;
         if (b0 < rs) vm &= 0xFFFFu << (u32)(rs - b0);
         if (b0 + 16 > re) vm &= (1u << (u32)(re - b0)) - 1u;
-        const u32 S = (mask16(v, '"') | mask16(v, ',') | mask16(v, '\n') | mask16(v, '\r')) & vm;
+        const u32 S = (mask16(v, '"') | mask16(v, a.delim) | mask16(v, '\n') | mask16(v, '\r')) & vm;
         const u32 O = vm & ~S;
         u32 E = S;
         if (b0 + 16 >= a.n && a.n > b0 && ((vm >> (u32)(a.n - 1 - b0)) & 1u)) E |= 1u << (u32)(a.n - 1 - b0);
@@ -561,7 +562,7 @@ __device__ __forceinline__ void wcs_row(const RowArgs &a, WgAgg &agg, u64 r) {
             bool eol = i + 1 == a.n;
             if (b == '\n') eol = true;
             else if (b == '\r' && !eol) eol = (p < 15 ? byte_of(v, p + 1) : (u32)a.buf[i + 1]) != '\n';
-            const u32 cls = b == '"' ? 0u : (b == ',' ? 1u : ((b == '\r' || b == '\n') ? 2u : 3u));
+            const u32 cls = b == '"' ? 0u : (b == a.delim ? 1u : ((b == '\r' || b == '\n') ? 2u : 3u));
             const u32 tnext = cls == 0 ? T_Q : (cls == 1 ? T_D : (cls == 2 ? T_NL : T_O));
             const u32 tact = cls == 0 ? A_Q : (cls == 1 ? A_D : (cls == 2 ? A_NL : A_O));
             const u32 act = (tact >> (2 * s)) & 3u;
@@ -772,6 +773,7 @@ struct ColArgs {
     const u64 *off;    // [ncols * R] (pass 1)
     u8 *out;
     WCtr *ctr;
+    u32 delim;         // field delimiter of the reader and of the writer's quoting
 };
 
 template <int PASS>
@@ -838,7 +840,7 @@ __global__ __launch_bounds__(256) void k_csvcol(ColArgs a) {
             u32 vm = 0xFFFFu;
             if (b0 < rs) vm &= 0xFFFFu << (u32)(rs - b0);
             if (b0 + 16 > re) vm &= (1u << (u32)(re - b0)) - 1u;
-            const u32 S = (mask16(v, '"') | mask16(v, ',') | mask16(v, '\n') | mask16(v, '\r')) & vm;
+            const u32 S = (mask16(v, '"') | mask16(v, a.delim) | mask16(v, '\n') | mask16(v, '\r')) & vm;
             const u32 O = vm & ~S;
             const u32 W[4] = {v.x, v.y, v.z, v.w};
             u32 CONT = 0;
@@ -866,7 +868,7 @@ __global__ __launch_bounds__(256) void k_csvcol(ColArgs a) {
                 const u64 i = b0 + p;
                 bool eol = i + 1 == a.n || b == '\n';
                 if (b == '\r' && !eol) eol = (p < 15 ? byte_of(v, p + 1) : (u32)a.buf[i + 1]) != '\n';
-                const u32 cls = b == '"' ? 0u : (b == ',' ? 1u : ((b == '\r' || b == '\n') ? 2u : 3u));
+                const u32 cls = b == '"' ? 0u : (b == a.delim ? 1u : ((b == '\r' || b == '\n') ? 2u : 3u));
                 const u32 tnext = cls == 0 ? T_Q : (cls == 1 ? T_D : (cls == 2 ? T_NL : T_O));
                 const u32 tact = cls == 0 ? A_Q : (cls == 1 ? A_D : (cls == 2 ? A_NL : A_O));
                 const u32 act = (tact >> (2 * s)) & 3u;
@@ -876,7 +878,7 @@ __global__ __launch_bounds__(256) void k_csvcol(ColArgs a) {
                     if (f < a.ncols) {
                         if (PASS == 0) {
                             clen += 1 + (b == '"');  // a quote is doubled if the value is quoted
-                            special |= b == ',' || b == '"' || b == '\n';
+                            special |= b == a.delim || b == '"' || b == '\n';
                         } else {
                             put(b);
                             if (q && b == '"') put('"');
@@ -934,6 +936,7 @@ struct msa_wcs {
     u64 *d_spans = nullptr;
     msa_wcs_summary sum{};
     u64 gbits = 0;  // global table size of the next run (log2), 0 = auto
+    u32 delim = ',';  // field delimiter (msa_wcs_set_delimiter: the script's --delimiter or csv.Sniffer's guess)
     bool have = false;
     // column splitter results
     u64 cc_ncols = 0, cc_rows = 0;
@@ -1038,6 +1041,15 @@ extern "C" int msa_wcs_load_csv(msa_wcs *w, const void *host_csv, size_t n) {
     return MSA_OK;
 }
 
+// The field delimiter of the reader (and of the column splitter's writer):
+// one ASCII byte other than '"', '\r', '\n' and NUL.  Invalidates results.
+extern "C" int msa_wcs_set_delimiter(msa_wcs *w, int delim) {
+    if (!w || delim <= 0 || delim > 127 || delim == '"' || delim == '\r' || delim == '\n') return MSA_ERR_ARG;
+    if ((u32)delim != w->delim) wcs_release_results(w);
+    w->delim = (u32)delim;
+    return MSA_OK;
+}
+
 extern "C" int msa_wcs_set_table_bits(msa_wcs *w, int bits) {
     if (!w || bits < 0 || bits > 31) return MSA_ERR_ARG;
     w->gbits = (u64)bits;
@@ -1071,12 +1083,12 @@ static int parse_header(msa_wcs *w, const u8 *h, u64 len, u32 *ia, u32 *isg, u32
             case SF:
                 if (b == '\r' || b == '\n') { save(); s = EC; }
                 else if (b == '"') s = IQ;
-                else if (b == ',') save();
+                else if (b == w->delim) save();
                 else { fld[fl++] = (char)b; s = IF; }
                 break;
             case IF:
                 if (b == '\r' || b == '\n') { save(); s = EC; }
-                else if (b == ',') { save(); s = SF; }
+                else if (b == w->delim) { save(); s = SF; }
                 else fld[fl++] = (char)b;
                 break;
             case IQ:
@@ -1085,7 +1097,7 @@ static int parse_header(msa_wcs *w, const u8 *h, u64 len, u32 *ia, u32 *isg, u32
                 break;
             case QQ:
                 if (b == '"') { fld[fl++] = '"'; s = IQ; }
-                else if (b == ',') { save(); s = SF; }
+                else if (b == w->delim) { save(); s = SF; }
                 else if (b == '\r' || b == '\n') { save(); s = EC; }
                 else { fld[fl++] = (char)b; s = IF; }
                 break;
@@ -1155,7 +1167,7 @@ static int wcs_split_rows(msa_wcs *w, WCtr **ctr_out, u64 *ds_out, u64 *nrows_ou
         WCHECK(wpool(w, 7, (nseg / 1024 + 2) * 8, bsum));
         WCHECK(wpool(w, 8, 16, total));
         dfin = bmap + nb;
-        hipLaunchKernelGGL(k_wcs_map, grid1(nseg), dim3(256), 0, st, buf, ds, n, nseg, map, cnt6);
+        hipLaunchKernelGGL(k_wcs_map, grid1(nseg), dim3(256), 0, st, buf, ds, n, nseg, w->delim, map, cnt6);
         hipLaunchKernelGGL(k_wcs_state_block, dim3((u32)nb), dim3(BLK), 0, st, (const u32 *)map, nseg, bmap);
         hipLaunchKernelGGL(k_wcs_state_top, dim3(1), dim3(TOP_T), 0, st, bmap, nb, dfin);
         hipLaunchKernelGGL(k_wcs_state_down, dim3((u32)nb), dim3(BLK), 0, st, (const u32 *)map, (const u64 *)cnt6,
@@ -1173,7 +1185,7 @@ static int wcs_split_rows(msa_wcs *w, WCtr **ctr_out, u64 *ds_out, u64 *nrows_ou
         }
         // rend[-1] = ds: rows are [rend[r-1], rend[r]) with d_rend shifted by one
         WCHECK(hipMemcpyAsync(w->d_rend, &ds, 8, hipMemcpyHostToDevice, st));
-        hipLaunchKernelGGL(k_wcs_emit, grid1(nseg), dim3(256), 0, st, buf, ds, n, nseg, (const u32 *)sstate,
+        hipLaunchKernelGGL(k_wcs_emit, grid1(nseg), dim3(256), 0, st, buf, ds, n, nseg, w->delim, (const u32 *)sstate,
                            (const u64 *)roff, w->d_rend + 1);
         if (fin == IQ) WCHECK(hipMemcpyAsync(w->d_rend + nrows, &n, 8, hipMemcpyHostToDevice, st));
     }
@@ -1237,7 +1249,7 @@ extern "C" int msa_wcs_run(msa_wcs *w) {
         WCHECK(hipMemcpyAsync(ctr, &h0, sizeof h0, hipMemcpyHostToDevice, st));
         RowArgs a;
         a.buf = buf; a.n = n; a.rend = w->d_rend; a.ds = ds; a.nrows = R;
-        a.ia = ia; a.isg = isg; a.it = it; a.need = need;
+        a.ia = ia; a.isg = isg; a.it = it; a.need = need; a.delim = w->delim;
         a.gtab = gtab; a.gmask = slots - 1; a.glimit = slots / 4 * 3;
         a.scratch = scratch; a.nd = w->d_nd; a.spans = w->d_spans; a.ctr = ctr;
         a.ablate = getenv("MSA_WCS_ABLATE") ? atoi(getenv("MSA_WCS_ABLATE")) : 0;
@@ -1491,14 +1503,14 @@ extern "C" int msa_wcs_write_outputs(msa_wcs *w, const char *outdir) {
 
 // ---------------------------------------------------------------------------
 // Column splitter host side.
-static void row_fields(const u8 *h, u64 len, std::vector<std::string> &out) {
+static void row_fields(const u8 *h, u64 len, u32 delim, std::vector<std::string> &out) {
     out.clear();
     std::string fld;
     u32 s = SR;
     for (u64 i = 0; i < len; ++i) {
         const u32 b = h[i];
         const bool eol = b == '\n' || (b == '\r' && (i + 1 >= len || h[i + 1] != '\n')) || i + 1 == len;
-        const u32 cls = b == '"' ? 0u : (b == ',' ? 1u : ((b == '\r' || b == '\n') ? 2u : 3u));
+        const u32 cls = b == '"' ? 0u : (b == delim ? 1u : ((b == '\r' || b == '\n') ? 2u : 3u));
         const u32 tnext = cls == 0 ? T_Q : (cls == 1 ? T_D : (cls == 2 ? T_NL : T_O));
         const u32 tact = cls == 0 ? A_Q : (cls == 1 ? A_D : (cls == 2 ? A_NL : A_O));
         const u32 act = (tact >> (2 * s)) & 3u;
@@ -1528,7 +1540,7 @@ extern "C" int msa_csvcol_run(msa_wcs *w, int has_header, uint64_t *ncols, uint6
     WCHECK(hipMemcpy(&he, w->d_rend + 1, 8, hipMemcpyDeviceToHost));
     std::vector<u8> hb(he - ds + 1);
     if (he > ds) WCHECK(hipMemcpy(hb.data(), w->d_buf + ds, he - ds, hipMemcpyDeviceToHost));
-    row_fields(hb.data(), he - ds, w->cc_hdr);
+    row_fields(hb.data(), he - ds, w->delim, w->cc_hdr);
     const u64 nc = w->cc_hdr.size();
     const u64 first = has_header ? 2 : 1;  // kernel row index of the first data row
     const u64 R = nr + 1 - first;
@@ -1543,6 +1555,7 @@ extern "C" int msa_csvcol_run(msa_wcs *w, int has_header, uint64_t *ncols, uint6
     ColArgs a;
     a.buf = w->d_buf; a.n = w->n; a.rend = w->d_rend; a.first = first; a.nrows = nr + 1;
     a.ncols = nc; a.R = R; a.len = len; a.quoted = quoted; a.off = w->d_ccoff; a.out = nullptr; a.ctr = ctr;
+    a.delim = w->delim;
     if (cells) {
         hipLaunchKernelGGL(k_csvcol<0>, grid1(R), dim3(256), 0, st, a);
         WCHECK(msa_exclusive_scan(len, cells, w->d_ccoff, bsum, total, st));

@@ -2,14 +2,17 @@
  * word_count_per_song -- drop-in CLI for /root/reference/scripts/
  * word_count_per_song.py (main 102-155) on libmsa_hip's GPU path (msa_wcs_*).
  *
- *   word_count_per_song <csv> [--output-dir D] [--delimiter ,]
+ *   word_count_per_song <csv> [--output-dir D] [--delimiter C]
  *                       [--encoding utf-8-sig] [--workers N]
  *
  * Writes D/word_counts_global.csv and D/word_counts_by_song.csv (default D =
  * output/serial_word_counts) and prints the script's three lines.  --workers
- * is accepted and ignored (the GPU replaces the thread pool, 132-133).  Only
- * the ',' delimiter and UTF-8 input are implemented (what detect_delimiter
- * 42-49 yields on this dataset); others are refused.
+ * is accepted and ignored (the GPU replaces the thread pool, 132-133).
+ * Without --delimiter the delimiter is detect_delimiter's (42-49):
+ * csv.Sniffer on the first 65536 characters, ',' when it fails (msa_sniff.c
+ * restates the stdlib's Sniffer).  The GPU reader takes any one-byte ASCII
+ * delimiter but '"', CR, LF; a sniffed or given delimiter outside that set,
+ * and encodings other than UTF-8, are refused.
  */
 #define _POSIX_C_SOURCE 200809L
 #include <errno.h>
@@ -19,6 +22,7 @@
 #include <sys/stat.h>
 
 #include "msa_hip.h"
+#include "msa_sniff.h"
 
 static int mkdirs(const char *path) {
     char tmp[4096];
@@ -64,17 +68,18 @@ int main(int argc, char **argv) {
         else if (!strcmp(argv[i], "--workers") && i + 1 < argc) ++i;
         else if (!csv) csv = argv[i];
         else {
-            fprintf(stderr, "usage: %s <csv> [--output-dir D] [--delimiter ,] [--encoding utf-8-sig]\n", argv[0]);
+            fprintf(stderr, "usage: %s <csv> [--output-dir D] [--delimiter C] [--encoding utf-8-sig]\n", argv[0]);
             return 2;
         }
     }
     if (!csv) {
-        fprintf(stderr, "usage: %s <csv> [--output-dir D] [--delimiter ,] [--encoding utf-8-sig]\n", argv[0]);
+        fprintf(stderr, "usage: %s <csv> [--output-dir D] [--delimiter C] [--encoding utf-8-sig]\n", argv[0]);
         return 2;
     }
-    if (delim && strcmp(delim, ",") != 0) {
-        fprintf(stderr, "only the ',' delimiter is implemented on the GPU path\n");
-        return 2;
+    if (delim && strlen(delim) != 1) {
+        /* csv.DictReader(delimiter=...) raises TypeError: "delimiter" must be a 1-character string */
+        fprintf(stderr, "TypeError: \"delimiter\" must be a 1-character string\n");
+        return 1;
     }
     if (strcmp(enc, "utf-8-sig") != 0 && strcmp(enc, "utf-8") != 0 && strcmp(enc, "utf8") != 0) {
         fprintf(stderr, "only UTF-8 input is implemented on the GPU path\n");
@@ -101,13 +106,33 @@ int main(int argc, char **argv) {
         fprintf(stderr, "--encoding utf-8 with a BOM is not implemented on the GPU path (use utf-8-sig)\n");
         return 2;
     }
+    uint32_t dch = delim ? (unsigned char)delim[0] : ',';
+    if (!delim) {  /* detect_delimiter(fh.read(65536)) */
+        uint32_t *cps = malloc(65536 * sizeof *cps);
+        const long k = msa_sniff_sample((const unsigned char *)data, n, cps, 65536);
+        if (k < 0) {
+            fprintf(stderr, "UnicodeDecodeError: 'utf-8' codec can't decode the first 65536 characters of %s\n", csv);
+            free(cps);
+            free(data);
+            return 1;
+        }
+        const msa_sniff_result sr = msa_sniff(cps, (size_t)k);
+        free(cps);
+        dch = sr.ok ? sr.delimiter : ',';
+    }
+    if (dch == 0 || dch > 127 || dch == '"' || dch == '\r' || dch == '\n') {
+        fprintf(stderr, "delimiter U+%04X is not implemented on the GPU path\n", (unsigned)dch);
+        free(data);
+        return 2;
+    }
     msa_wcs *w = NULL;
     int rc = msa_wcs_create(0, &w);
     if (rc) {
         fprintf(stderr, "msa_wcs_create failed (%d): no GPU visible\n", rc);
         return 1;
     }
-    rc = msa_wcs_load_csv(w, data, n);
+    rc = msa_wcs_set_delimiter(w, (int)dch);
+    if (!rc) rc = msa_wcs_load_csv(w, data, n);
     free(data);
     if (!rc) rc = msa_wcs_run(w);
     if (!rc) rc = msa_wcs_write_outputs(w, outdir);

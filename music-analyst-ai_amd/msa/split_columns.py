@@ -8,8 +8,11 @@ the script (sanitize_filename 24-28, the name loop 159-174).
     python -m msa.split_columns data.csv [--output-dir D] [--delimiter ,]
            [--quotechar '"'] [--encoding utf-8-sig] [--no-header] [--force]
 
-Only ',' / '"' are implemented (an explicit --delimiter is required to skip
-csv.Sniffer, 46-66, whose guess the GPU path does not reproduce).
+Without --delimiter the dialect is detect_csv_params' (46-66): the stdlib's
+csv.Sniffer on the first 65536 characters (msa/sniff.py), ',' when it fails.
+The GPU reader takes any one-byte ASCII delimiter but '"', CR, LF, with
+quotechar '"'; a sniffed skipinitialspace dialect is refused (not implemented
+on the GPU path), as are other delimiters and quotechars.
 """
 from __future__ import annotations
 
@@ -19,6 +22,7 @@ from pathlib import Path
 from typing import List, Optional
 
 from . import WordCountPerSong
+from .sniff import detect_csv_params, gpu_supported, read_sample
 
 
 def sanitize_filename(name: str, max_len: int = 80) -> str:
@@ -30,8 +34,9 @@ def sanitize_filename(name: str, max_len: int = 80) -> str:
     return (s or "col")[:max_len]
 
 
-def _header_line(h: str) -> str:
-    if h == "" or any(c in h for c in ',"\n'):
+def _header_line(h: str, delimiter: str = ",") -> str:
+    """csv.writer(QUOTE_MINIMAL, lineterminator "\n").writerow([h])"""
+    if h == "" or any(c in h for c in (delimiter, '"', "\n")):
         return '"' + h.replace('"', '""') + '"\n'
     return h + "\n"
 
@@ -42,14 +47,19 @@ def split_csv_columns(csv_path: str, output_dir: Optional[str] = None, delimiter
     in_path = Path(csv_path)
     if not in_path.exists():
         raise SystemExit(f"Erro: arquivo não encontrado: {in_path}")
-    if delimiter != "," or quotechar != '"':
-        raise SystemExit("only --delimiter ',' with quotechar '\"' is implemented on the GPU path")
     if encoding.lower().replace("_", "-") not in ("utf-8-sig", "utf-8", "utf8"):
         raise SystemExit("only UTF-8 input is implemented on the GPU path")
+    skipinitialspace = False
+    if not delimiter:  # detect_csv_params: csv.Sniffer on the script's sample
+        delimiter, skipinitialspace = detect_csv_params(read_sample(str(in_path), encoding))
+    if quotechar != '"' or not gpu_supported(delimiter) or skipinitialspace:
+        raise SystemExit(f"dialect delimiter={delimiter!r} quotechar={quotechar!r} "
+                         f"skipinitialspace={skipinitialspace} is not implemented on the GPU path")
     base_out = Path(output_dir) if output_dir else in_path.with_suffix("").parent / f"{in_path.stem}_columns"
     base_out.mkdir(parents=True, exist_ok=True)
     data = in_path.read_bytes()
     with WordCountPerSong(device) as w:
+        w.set_delimiter(delimiter)
         w.load_csv(data)
         try:
             ncols, _ = w.split_columns(has_header=not no_header)
@@ -76,7 +86,7 @@ def split_csv_columns(csv_path: str, output_dir: Optional[str] = None, delimiter
             with open(base_out / names[i], "wb") as fh:
                 fh.write(bom)
                 if not no_header:
-                    fh.write(_header_line(headers[i]).encode("utf-8"))
+                    fh.write(_header_line(headers[i], delimiter).encode("utf-8"))
                 fh.write(w.column_body(i))
     print(f"Concluído. {ncols} arquivo(s) gerado(s) em: {base_out}")
     for name in names:

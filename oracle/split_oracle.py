@@ -5,7 +5,8 @@ Only tests/ may use this module, and only as the checker; the product path
 never calls it.
 
 Restates the data part of /root/reference/scripts/split_csv_columns.py
-main (124-199) for an explicit ',' delimiter and '"' quotechar:
+main (124-199) for a given delimiter (the script's --delimiter or its
+csv.Sniffer guess, default ',') and '"' quotechar:
 * rows: CPython 3.10 csv.reader (wcs_oracle.csv_rows -- the same _csv state
   machine; blank lines are rows with no fields, csv.reader yields them);
 * columns: len(first row); each later row contributes row[i] or "" (175-178);
@@ -26,17 +27,18 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from wcs_oracle import WcsError, _utf8_check, csv_rows  # noqa: E402,F401
 
 
-def write_value(v: bytes) -> bytes:
+def write_value(v: bytes, delim: bytes = b",") -> bytes:
     """csv.writer(...).writerow([v]) with lineterminator '\\n', QUOTE_MINIMAL."""
-    if v == b"" or any(c in v for c in b',"\n'):
+    if v == b"" or any(c in v for c in delim + b'"\n'):
         return b'"' + v.replace(b'"', b'""') + b'"\n'
     return v + b"\n"
 
 
-def split_columns(data: bytes, has_header: bool = True):
+def split_columns(data: bytes, has_header: bool = True, delimiter: str = ","):
     """-> (first-row fields, [body bytes of column i]) ; raises WcsError / ValueError("CSV vazio.")."""
     _utf8_check(data)
-    rows = csv_rows(data)
+    d = delimiter.encode()
+    rows = csv_rows(data, ord(delimiter))
     first = next(rows, None)
     if first is None:
         raise ValueError("CSV vazio.")
@@ -44,8 +46,8 @@ def split_columns(data: bytes, has_header: bool = True):
     bodies = [[] for _ in range(nc)]
     if not has_header:
         for i in range(nc):
-            bodies[i].append(write_value(first[i]))
+            bodies[i].append(write_value(first[i], d))
     for row in rows:
         for i in range(nc):
-            bodies[i].append(write_value(row[i] if i < len(row) else b""))
+            bodies[i].append(write_value(row[i] if i < len(row) else b"", d))
     return first, [b"".join(b) for b in bodies]

@@ -70,3 +70,31 @@ def msa_mod():
 
     msa.load()
     return msa
+
+
+def golden_delimiter(case_dir):
+    """The delimiter the reference script ran a golden case with: its
+    --delimiter, else what its csv.Sniffer picked on the 65536-character
+    sample (the stdlib class the script calls, via msa/sniff.py)."""
+    args = open(os.path.join(case_dir, "args.txt")).read().split()
+    if "--delimiter" in args:
+        return args[args.index("--delimiter") + 1]
+    from msa.sniff import detect_delimiter, read_sample
+
+    try:
+        return detect_delimiter(read_sample(os.path.join(case_dir, "input.csv")))
+    except UnicodeDecodeError:
+        return ","
+
+
+def golden_dialect(case_dir):
+    """(delimiter, skipinitialspace) of split_csv_columns.py's detect_csv_params."""
+    args = open(os.path.join(case_dir, "args.txt")).read().split()
+    if "--delimiter" in args:
+        return args[args.index("--delimiter") + 1], False
+    from msa.sniff import detect_csv_params, read_sample
+
+    try:
+        return detect_csv_params(read_sample(os.path.join(case_dir, "input.csv")))
+    except UnicodeDecodeError:
+        return ",", False

@@ -41,6 +41,14 @@ def cases():
         lyric = " ".join(rnd.choice(words) for _ in range(rnd.randint(0, 9)))
         rows.append("A%d,S%d,/l/%d,\"%s\"" % (rnd.randint(0, 40), i, i, lyric))
     c["lyrics_300"] = ("\n".join(rows) + "\n", ["--delimiter", ","])
+    # no --delimiter: the script's detect_csv_params (csv.Sniffer) decides
+    from make_wcs_golden import sniffed_cases
+
+    for k, (text, _) in sniffed_cases().items():
+        c[k] = (text, [])
+    # a sniffed skipinitialspace dialect (", " after every delimiter): the GPU
+    # path refuses it (not implemented); the golden records what the script does
+    c["sniff_skipinitialspace"] = ('a, b, c\n"x", "y", "z"\n"1", "2", "3"\n', [])
     return c
 
 

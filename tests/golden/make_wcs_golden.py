@@ -19,6 +19,7 @@ import sys
 import tempfile
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+# inputs WITHOUT --delimiter (args.txt empty) exercise the script's csv.Sniffer
 OUT = os.path.join(HERE, "wcs")
 REF = "/root/reference/scripts/word_count_per_song.py"
 sys.path.insert(0, os.path.join(HERE, "..", "..", "music-analyst-ai_amd"))
@@ -78,8 +79,45 @@ def zipf(n, seed, crlf=False):
     return msa.gen_corpus(n, mode="zipf", seed=seed, crlf=crlf).decode("utf-8")
 
 
+def sniffed_cases():
+    """Inputs run WITHOUT --delimiter: the script's detect_delimiter (csv.Sniffer
+    on the first 65536 characters) picks the delimiter."""
+    rnd = random.Random(77)
+    words = ["love", "the", "naïve", "don't", "you", "Über", "night", "ÇA", "x", "rock'n'roll"]
+
+    def lyric(d):
+        body = " ".join(rnd.choice(words) for _ in range(rnd.randint(1, 12)))
+        if rnd.random() < 0.5:
+            body = body.replace(" ", d + " ", 1) + ", yeah"
+        return '"' + body.replace('"', '""') + '\n' + rnd.choice(words) + '"'
+
+    c = {}
+    for name, d in (("sniff_semicolon", ";"), ("sniff_tab", "\t"), ("sniff_pipe", "|"), ("sniff_colon", ":")):
+        rows = [d.join(["artist", "song", "link", "text"])]
+        for i in range(60):
+            rows.append(d.join([f"Artist {i % 7}", f"Song {i}", f"/l/{i}", lyric(d)]))
+        c[name] = ("\n".join(rows) + "\n", [])
+    # unquoted, space separated: the frequency heuristic (_guess_delimiter) decides
+    c["sniff_space_unquoted"] = ("artist song text\n" + "".join(f"A{i} S{i} word{i % 5}\n" for i in range(40)), [])
+    # no quotes, no consistent character: sniff raises, ',' is used
+    c["sniff_fails"] = ("artist,song,link,text\nA,S,/l,some words here, and more\nB,T\n"
+                        "C,U,/l,x,y,z,w,v\nsingle\n", [])
+    # the generated lyric corpus with ';' (the shape of the real dataset)
+    import msa
+
+    z = msa.gen_corpus(150, mode="zipf", seed=5).decode("utf-8")
+    out, q = [], False
+    for ch in z:  # ',' -> ';' outside quotes
+        if ch == '"':
+            q = not q
+        out.append(";" if (ch == "," and not q) else ch)
+    c["sniff_zipf_semicolon"] = ("".join(out), [])
+    return c
+
+
 def main():
     cases = hand_cases()
+    cases.update(sniffed_cases())
     for s in range(6):
         cases[f"torture_{s}"] = (torture(100 + s, 150), ["--delimiter", ","])
     cases["zipf_300"] = (zipf(300, 3), [])

@@ -21,7 +21,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(HERE, "..", "oracle"))
 sys.path.insert(0, os.path.join(HERE, "golden"))
 import wcs_oracle  # noqa: E402
-from test_wcs_oracle import CASES, load_case  # noqa: E402
+from conftest import golden_delimiter  # noqa: E402
+from test_wcs_oracle import CASES, GOLD, load_case  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
@@ -36,11 +37,15 @@ def wcs(msa_mod):
 @pytest.mark.parametrize("name", CASES)
 def test_wcs_golden(msa_mod, wcs, name):
     data, exp = load_case(name)
-    if exp is None:
-        with pytest.raises(msa_mod.MsaError):
-            wcs.run(data)
-        return
-    assert wcs.run(data) == exp
+    wcs.set_delimiter(golden_delimiter(os.path.join(GOLD, name)))
+    try:
+        if exp is None:
+            with pytest.raises(msa_mod.MsaError):
+                wcs.run(data)
+            return
+        assert wcs.run(data) == exp
+    finally:
+        wcs.set_delimiter(",")
 
 
 def _torture(seed, n):
@@ -129,15 +134,18 @@ def test_wcs_full_size_properties(msa_mod, wcs):
 
 
 @pytest.mark.parametrize("name", [c for c in CASES if c in ("basic", "crlf_cr_blank", "zipf_300", "err_missing_col",
-                                                          "err_short_row", "torture_2")])
+                                                          "err_short_row", "torture_2") or c.startswith("sniff_")])
 def test_wcs_cli_golden(msa_mod, name, tmp_path):
-    """bin/word_count_per_song writes the script's two files and prints its row count."""
+    """bin/word_count_per_song writes the script's two files and prints its row
+    count -- invoked like the golden run: with its --delimiter, or without one
+    (the CLI's own csv.Sniffer restatement then picks it, as the script did)."""
     cli = os.path.join(msa_mod.PKG_DIR, "bin", "word_count_per_song")
     data, exp = load_case(name)
+    args = open(os.path.join(GOLD, name, "args.txt")).read().split()
     inp = tmp_path / "in.csv"
     inp.write_bytes(data)
     out = tmp_path / "out"
-    r = subprocess.run([cli, str(inp), "--output-dir", str(out), "--delimiter", ","], capture_output=True, timeout=120)
+    r = subprocess.run([cli, str(inp), "--output-dir", str(out)] + args, capture_output=True, timeout=120)
     if exp is None:
         assert r.returncode != 0
         return

@@ -8,6 +8,7 @@ import pytest
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(HERE, "..", "oracle"))
 import wcs_oracle  # noqa: E402
+from conftest import golden_delimiter, golden_dialect  # noqa: E402,F401
 
 GOLD = os.path.join(HERE, "golden", "wcs")
 CASES = sorted(os.listdir(GOLD))
@@ -25,11 +26,12 @@ def load_case(name):
 @pytest.mark.parametrize("name", CASES)
 def test_oracle_matches_reference(name):
     data, exp = load_case(name)
+    d = golden_delimiter(os.path.join(GOLD, name))
     if exp is None:
         with pytest.raises(wcs_oracle.WcsError):
-            wcs_oracle.word_count_per_song(data)
+            wcs_oracle.word_count_per_song(data, d)
         return
-    assert wcs_oracle.word_count_per_song(data) == exp
+    assert wcs_oracle.word_count_per_song(data, d) == exp
 
 
 def test_oracle_refuses_bad_bytes():
