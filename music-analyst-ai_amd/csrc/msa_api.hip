@@ -38,8 +38,8 @@ hipError_t msa_launch_exp_write(const ExpSrc &, u64, u32, const u64 *, const u64
                                 hipStream_t);
 hipError_t msa_launch_exp_ranked(const u64 *, const u64 *, const u8 *, u64, u64, u8 *, hipStream_t);
 hipError_t msa_launch_imp(const u8 *, const u64 *, u32, u64 *, u64, const ImpDst &, hipStream_t);
-hipError_t msa_launch_col_write(int, const u8 *, const u64 *, const u64 *, const u64 *, const u32 *, u64, u64, u64, u8 *,
-                                hipStream_t);
+hipError_t msa_launch_col_write(int, const u8 *, const u64 *, const u64 *, const u64 *, const u32 *, u64, u64,
+                                const u64 *, u8 *, hipStream_t);
 hipError_t msa_launch_artist_key(const u8 *, const u64 *, const u64 *, const u64 *, u64, u64, u8 *, u64 *, u32 *, u64 *,
                                  u64 *, u64, u32 *, u64, Counters *, u64, int, int, hipStream_t);
 hipError_t msa_launch_long(const u8 *, u64, const u8 *, u64, const u64 *, u64, u32 *, u64 *, u64 *, u64, u32 *, u64,
@@ -61,7 +61,7 @@ hipError_t msa_launch_fixup(const u64 *, const u64 *, const u64 *, const u32 *, 
                             const u8 *, const u64 *, const u32 *, const u8 *, const u64 *, const u32 *, u32 *, hipStream_t);
 hipError_t msa_launch_blob(const u32 *, u64, const u64 *, const u64 *, const u64 *, const u64 *, const u8 *,
                            const u8 *, const u64 *, const u32 *, const u8 *, const u64 *, const u32 *, u64 *, u64 *, u64 *, u64 *,
-                           u8 *, u64 *, hipStream_t, int);
+                           u8 *, u64 *, u64, hipStream_t, int);
 
 // ---------------------------------------------------------------------------
 namespace {
@@ -72,11 +72,18 @@ struct DevBuf {
     template <class T> T *as() const { return reinterpret_cast<T *>(p); }
 };
 
+struct BlobArgs {  // key sources of the last blob pass (for a rewrite after growth)
+    const u8 *wbuf, *wextra, *arena;
+    const u64 *key_off;
+    const u32 *key_len;
+};
 struct Ranked {
     DevBuf K[3][3];  // [set][k2,k1,k0]: set 0 = input, 1/2 = ping-pong
     DevBuf V[3];
     DevBuf ref, cnt, order, len, off, blob, counts;
-    u64 n = 0, blob_len = 0;
+    u64 n = 0, blob_len = 0, blob_cap = 0;
+    bool blob_pending = false;  // blob_len not read back yet (do_rank's sync)
+    BlobArgs pending{};
     std::vector<u64> h_counts, h_off;
     std::vector<char> h_blob;
     bool host_valid = false;
@@ -147,10 +154,13 @@ struct msa_ctx {
     int ablate = 0;  // MSA_ABLATE: diagnostic kernel ablations (results invalid)
     int sort_mode = 0;  // MSA_SORT: 0 by size, 1 merge sort, 2 radix sort
     DevBuf sort_scratch;
+    DevBuf blob_tot;  // the two tables' key-blob lengths (device), read back once per msa_rank
     // tie refinement of the radix path: per-level marks/scans, the subset's
     // three key sets + values, and its order positions
     DevBuf t_head, t_tie, t_runid, t_tpos, t_bsum, t_total, t_K[3][3], t_V[3], t_Vn, t_Pn, t_Vc, t_Pc;
     u64 acol_len = 0, a_hdr_getline = 0, a_hdr_len = 0, tcol_len = 0;
+    u64 col_hdr[2] = {0, 0};        // header-line bytes of artist.csv / text.csv
+    bool col_lens_pending = false;  // acol_len, tcol_len, a_end not read back yet
     // artist pass: true = the exact record reader over artist.csv (forced by
     // msa_set_artist_reader / an artist piece set for a shard); otherwise the
     // lines are the records unless the split found an unquoted artist field
@@ -444,11 +454,22 @@ static int clear_tables(msa_ctx *c) {
     return MSA_OK;
 }
 
+// Every read-back of the run counters also settles the column lengths the
+// split left on the device.
+static void take_col_lens(msa_ctx *c) {
+    if (!c->col_lens_pending) return;
+    c->acol_len = c->col_hdr[0] + c->h_ctr.col_body[0];
+    c->tcol_len = c->have_tcol ? c->col_hdr[1] + c->h_ctr.col_body[1] : 0;
+    c->a_end = c->acol_len;
+    c->col_lens_pending = false;
+}
 static int sync_counters(msa_ctx *c) {
     HIPC(c, hipMemcpyAsync(&c->h_ctr, c->ctr.p, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
     HIPC(c, hipStreamSynchronize(c->stream));
+    take_col_lens(c);
     return MSA_OK;
 }
+static int resolve_col_lens(msa_ctx *c) { return c->col_lens_pending ? sync_counters(c) : MSA_OK; }
 
 // After a failed (overflowed) attempt the tables hold partial counts and their
 // slot lists may be incomplete: zero the whole tables instead of the claimed
@@ -492,24 +513,22 @@ static int reset_artist_table(msa_ctx *c) {
 }
 
 // ------------------------------------------------------------------ stage 1
+// The column's length stays on the device (no host round trip): every line is
+// at most as long as its record, so header + input bytes bound the column;
+// the length lands in Counters::col_body[text] and reaches the host with the
+// next counter read-back (col_lens_pending).
 static int materialise_column(msa_ctx *c, bool text, const std::string &hdr_line, DevBuf &col, DevBuf &lenb,
-                              DevBuf &offb, DevBuf &srcb, DevBuf &pairsb, u64 *col_len) {
+                              DevBuf &offb, DevBuf &srcb, DevBuf &pairsb) {
     const u64 nrec = c->nrec;
     HIPC(c, ensure(offb, nrec * 8));
     HIPC(c, ensure(c->scan_bsum, ((nrec + 1023) / 1024 + 1) * 8));
     HIPC(c, ensure(c->scan_total, 64));
-    HIPC(c, msa_exclusive_scan(lenb.as<u64>(), nrec, offb.as<u64>(), c->scan_bsum.as<u64>(), c->scan_total.as<u64>(),
-                               c->stream));
-    u64 body = 0;
-    HIPC(c, hipMemcpyAsync(&body, c->scan_total.p, 8, hipMemcpyDeviceToHost, c->stream));
-    HIPC(c, hipStreamSynchronize(c->stream));
-    const u64 total = hdr_line.size() + body;
-    HIPC(c, ensure(col, total + MSA_INPUT_PAD));
+    u64 *body_p = &c->ctr.as<Counters>()->col_body[text ? 1 : 0];
+    HIPC(c, msa_exclusive_scan(lenb.as<u64>(), nrec, offb.as<u64>(), c->scan_bsum.as<u64>(), body_p, c->stream));
+    HIPC(c, ensure(col, hdr_line.size() + c->n + 1 + MSA_INPUT_PAD));
     HIPC(c, hipMemcpyAsync(col.p, hdr_line.data(), hdr_line.size(), hipMemcpyHostToDevice, c->stream));
-    HIPC(c, hipMemsetAsync(col.as<char>() + total, 0, MSA_INPUT_PAD, c->stream));
-    HIPC(c, msa_launch_col_write(text ? 1 : 0, c->in, lenb.as<u64>(), offb.as<u64>(), srcb.as<u64>(), pairsb.as<u32>(), nrec,
-                                 hdr_line.size(), body, col.as<u8>(), c->stream));
-    *col_len = total;
+    HIPC(c, msa_launch_col_write(text ? 1 : 0, c->in, lenb.as<u64>(), offb.as<u64>(), srcb.as<u64>(), pairsb.as<u32>(),
+                                 nrec, hdr_line.size(), body_p, col.as<u8>(), c->stream));
     return MSA_OK;
 }
 
@@ -553,19 +572,20 @@ static int split_columns_rest(msa_ctx *c, bool want_text, const std::string &ah,
                                  want_text ? 1 : 0, c->alen.as<u64>(), c->asrc.as<u64>(), c->apairs.as<u32>(),
                                  c->tlen.as<u64>(), c->tsrc.as<u64>(), c->tpairs.as<u32>(), c->ctr.as<Counters>(), ak,
                                  c->stream));
-    if ((rc = materialise_column(c, false, ah, c->acol, c->alen, c->aoff, c->asrc, c->apairs, &c->acol_len))) return rc;
-    prof_end(c, ST_ARTIST_COLUMN, c->acol_len * 2 + c->nrec * 32);
+    if ((rc = materialise_column(c, false, ah, c->acol, c->alen, c->aoff, c->asrc, c->apairs))) return rc;
+    prof_end(c, ST_ARTIST_COLUMN, c->nrec * 16 * 2 + c->nrec * 32);  // ~16-byte artist lines
     // compute_header_length (parallel_spotify.c:444-459): getline's end
     c->a_hdr_getline = ah.empty() ? 0 : ah.find('\n') + 1;
     c->a_hdr_len = ah.size();
     c->a_beg = c->a_hdr_getline;
-    c->a_end = c->acol_len;
+    c->col_hdr[0] = ah.size();
+    c->col_hdr[1] = th.size();
+    c->col_lens_pending = true;  // acol_len / tcol_len / a_end: from the next counter read-back
     c->have_tcol = false;
     if (want_text) {
         prof_begin(c, ST_TEXT_COLUMN);
-        if ((rc = materialise_column(c, true, th, c->tcol, c->tlen, c->toff, c->tsrc, c->tpairs, &c->tcol_len)))
-            return rc;
-        prof_end(c, ST_TEXT_COLUMN, c->tcol_len * 2 + c->nrec * 40);
+        if ((rc = materialise_column(c, true, th, c->tcol, c->tlen, c->toff, c->tsrc, c->tpairs))) return rc;
+        prof_end(c, ST_TEXT_COLUMN, c->n * 2 + c->nrec * 40);  // ~ the text column read + written
         c->have_tcol = true;
     }
     c->stage = 1;
@@ -575,9 +595,9 @@ static int split_columns_rest(msa_ctx *c, bool want_text, const std::string &ah,
 // Word-table overflows of the scan (S/M tables, long-word occurrence list):
 // the split is repeated with grown tables (msa_split_columns' retry loop).
 static const u64 kSplitOvf = OVF_S | OVF_M | OVF_L;
-static int check_split_overflow(msa_ctx *c) {
+static int check_split_overflow(msa_ctx *c, bool read_back = true) {
     int rc;
-    if ((rc = sync_counters(c))) return rc;
+    if (read_back && (rc = sync_counters(c))) return rc;
     if (c->h_ctr.overflow & kSplitOvf)
         return fail(c, MSA_ERR_CAPACITY, "word table capacity overflow (flags 0x%llx)",
                     (unsigned long long)c->h_ctr.overflow);
@@ -591,6 +611,7 @@ static int split_once(msa_ctx *c, int flags) {
     const bool want_text = (flags & MSA_SPLIT_TEXT_COLUMN) != 0;
     c->merged_w = c->merged_a = false;
     c->artist_piece_set = false;
+    c->col_lens_pending = false;
     c->extra_len = 0;
     HIPC(c, ensure(c->ctr, sizeof(Counters)));
     if ((rc = clear_tables(c))) return rc;
@@ -657,22 +678,30 @@ static int split_once(msa_ctx *c, int flags) {
         u64 v = c->n;
         HIPC(c, hipMemcpyAsync(c->rec_start.as<u64>() + c->nrec, &v, 8, hipMemcpyHostToDevice, c->stream));
     }
-    if (c->cont) {
-        if ((rc = build_word_lists(c))) return rc;
-        if ((rc = check_split_overflow(c))) return rc;
-        return split_columns_rest(c, want_text, std::string(), std::string());
-    }
-    // header record = record 0
+    // one read-back after the scan: the counters (table overflow, long-word
+    // occurrences) and -- for the first shard -- the header record's end plus
+    // the input's first bytes (the header, almost always)
+    if ((rc = build_word_lists(c))) return rc;
+    HIPC(c, hipMemcpyAsync(&c->h_ctr, c->ctr.p, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
     u64 hend = c->n;
-    if (nterm > 0) {
-        // record 0 = [0, start of record 1), terminator included: parse_csv_line strips
-        // trailing '\n' / '\r' itself (parallel_spotify.c:267-270, h_parse_header)
-        HIPC(c, hipMemcpyAsync(&hend, c->rec_start.as<u64>() + 1, 8, hipMemcpyDeviceToHost, c->stream));
+    static const u64 kHead = 4096;
+    std::vector<unsigned char> hdr(std::min<u64>(c->n, kHead) + 1);
+    if (!c->cont) {
+        if (nterm > 0) HIPC(c, hipMemcpyAsync(&hend, c->rec_start.as<u64>() + 1, 8, hipMemcpyDeviceToHost, c->stream));
+        if (c->n) HIPC(c, hipMemcpyAsync(hdr.data(), c->in, std::min<u64>(c->n, kHead), hipMemcpyDeviceToHost, c->stream));
     }
     HIPC(c, hipStreamSynchronize(c->stream));
+    if (c->cont) {
+        if ((rc = check_split_overflow(c, false))) return rc;
+        return split_columns_rest(c, want_text, std::string(), std::string());
+    }
+    // header record = record 0 = [0, start of record 1), terminator included:
+    // parse_csv_line strips trailing '\n' / '\r' itself (parallel_spotify.c:267-270, h_parse_header)
     if (hend > c->n) hend = c->n;
-    std::vector<unsigned char> hdr(hend + 1);
-    if (hend) HIPC(c, hipMemcpy(hdr.data(), c->in, hend, hipMemcpyDeviceToHost));
+    if (hend > kHead) {  // a header longer than the bytes read with the counters
+        hdr.resize(hend + 1);
+        HIPC(c, hipMemcpy(hdr.data(), c->in, hend, hipMemcpyDeviceToHost));
+    }
     std::string al, tl;
     if (!h_parse_header(hdr.data(), hend, al, tl)) return fail(c, MSA_ERR_BADHEADER, "Unable to parse dataset header");
     memset(c->sum.artist_label, 0, 128);
@@ -706,14 +735,18 @@ static int split_once(msa_ctx *c, int flags) {
             f.carry = d_zero;
             f.lpos_tag = MSA_POS_EXTRA;
             HIPC(c, msa_launch_scan(f, 2, c->stream));
+            // the remainder's words may be new keys: list the tables again
+            if ((rc = reset_ctr(c, &Counters::s_claimed))) return rc;
+            if ((rc = reset_ctr(c, &Counters::m_claimed))) return rc;
+            if ((rc = build_word_lists(c))) return rc;
+            if ((rc = sync_counters(c))) return rc;
         }
     }
     std::string ah = c->sum.artist_label[0] ? c->sum.artist_label : "Artists";
     std::string th = c->sum.text_label[0] ? c->sum.text_label : "Texts";
     ah.push_back('\n');
     th.push_back('\n');
-    if ((rc = build_word_lists(c))) return rc;
-    if ((rc = check_split_overflow(c))) return rc;
+    if ((rc = check_split_overflow(c, false))) return rc;
     return split_columns_rest(c, want_text, ah, th);
 }
 
@@ -752,15 +785,37 @@ static int artist_keys(msa_ctx *c, const u8 *col, const u64 *ar_start, bool line
     }
 }
 
+// Long words (> 16 bytes): table of their occurrences recorded by the scan.
+static void launch_long_words(msa_ctx *c, u64 nl) {
+    prof_begin(c, ST_LONG_WORDS);
+    (void)msa_launch_long(c->in, c->n, c->extra.as<u8>(), c->extra_len, c->l_pos.as<u64>(), nl, c->l_len.as<u32>(),
+                          c->l_slot.as<u64>(), c->l_tab.as<u64>(), c->lt_slots - 1, c->l_list.as<u32>(),
+                          c->lt_slots / 2, c->ctr.as<Counters>(), c->stream);
+    prof_end(c, ST_LONG_WORDS, nl * 64);
+}
+// A long-word pass that has to run again (the artist stage restarted and its
+// counter reset dropped the pass's overflow / collision flags): its table and
+// claim count start over; the flags are raised again by the new pass.
+static int wipe_long_table(msa_ctx *c) {
+    int rc;
+    if ((rc = wipe_one(c, c->l_tab, c->lt_slots, 4, c->lt_used_prev))) return rc;
+    return reset_ctr(c, &Counters::l_claimed);
+}
+
 static int do_count(msa_ctx *c) {
     int rc;
     if (c->stage < 1) return fail(c, MSA_ERR_ARG, "msa_count before msa_split_columns");
     // a label with a '\n' (its rest is read as artist records): records != lines
     bool exact = c->artist_exact || c->artist_piece_set || c->a_hdr_getline < c->a_hdr_len;
+    const u64 nl = std::min<u64>(c->h_ctr.l_occ, c->l_occ_cap);  // final since the split's read-back
+    bool long_ok = false;   // the long-word pass ran and its flags are in h_ctr
+    bool long_ran = false;  // the long-word table holds a pass's counts
     if (!exact) {
         // every artist line is one artist.csv record: count the keys k_rec_spans
-        // built (no record reader over artist.csv); the split's a_quoted flag
-        // says whether that held -- if not, start over with the exact reader
+        // built (no record reader over artist.csv); the long-word table goes in
+        // the same launch sequence, and ONE counter read-back settles both (and
+        // the column lengths).  The split's a_quoted flag says whether the
+        // shortcut held -- if not, start over with the exact reader.
         const u64 nrec = c->nrec;
         for (int attempt = 0;; ++attempt) {
             prof_begin(c, ST_ARTIST_KEYS);
@@ -769,20 +824,27 @@ static int do_count(msa_ctx *c) {
                                             c->a_list.as<u32>(), c->a_slots / 2, c->ctr.as<Counters>(), c->cus,
                                             c->stream));
             prof_end(c, ST_ARTIST_KEYS, nrec * 28);
+            if (attempt == 0) {
+                launch_long_words(c, nl);
+                long_ran = true;
+            }
             if ((rc = sync_counters(c))) return rc;
+            long_ok = attempt == 0;
             if (!(c->h_ctr.overflow & OVF_A) || attempt >= 12) break;
             grow_tables(c, OVF_A);
-            if ((rc = reset_artist_table(c))) return rc;
+            if ((rc = reset_artist_table(c))) return rc;  // clears overflow + collision: the long stage reruns
         }
         if (c->h_ctr.a_quoted) {
             if (c->h_ctr.a_quoted & 2) c->a_long_cap = std::max<u64>(c->a_long_cap * 4, c->h_ctr.a_long * 2);
             exact = true;
+            long_ok = false;
             if ((rc = reset_artist_table(c))) return rc;
         } else {
             c->nrec_a = c->h_ctr.songs;
         }
     }
     if (exact) {
+        if ((rc = resolve_col_lens(c))) return rc;
         // the artist pass over artist.csv records from its getline header end (or
         // the segment msa_segment_set chose for a shard)
         const u64 b = c->a_beg, e = c->a_end;
@@ -820,14 +882,14 @@ static int do_count(msa_ctx *c) {
             return rc;
     }
     // words longer than 16 bytes (their table grows the same way)
-    const u64 nl = std::min<u64>(c->h_ctr.l_occ, c->l_occ_cap);
     for (int attempt = 0;; ++attempt) {
-        prof_begin(c, ST_LONG_WORDS);
-        HIPC(c, msa_launch_long(c->in, c->n, c->extra.as<u8>(), c->extra_len, c->l_pos.as<u64>(), nl,
-                                c->l_len.as<u32>(), c->l_slot.as<u64>(), c->l_tab.as<u64>(), c->lt_slots - 1,
-                                c->l_list.as<u32>(), c->lt_slots / 2, c->ctr.as<Counters>(), c->stream));
-        prof_end(c, ST_LONG_WORDS, nl * 64);
-        if ((rc = sync_counters(c))) return rc;
+        if (!long_ok) {
+            if (long_ran && attempt == 0 && (rc = wipe_long_table(c))) return rc;
+            launch_long_words(c, nl);
+            long_ran = true;
+            if ((rc = sync_counters(c))) return rc;
+        }
+        long_ok = false;
         if (!(c->h_ctr.overflow & OVF_LT) || attempt >= 12) break;
         // the artist stage is done: only the long-word table and its counters restart
         const u64 keep_collision = c->h_ctr.collision;
@@ -921,9 +983,10 @@ static int refine_ties(msa_ctx *c, Ranked &R, int cur, const u8 *wbuf, const u8 
 }
 
 static int sort_and_blob(msa_ctx *c, Ranked &R, const u8 *wbuf, const u8 *wextra, const u8 *arena, const u64 *key_off,
-                         const u32 *key_len) {
+                         const u32 *key_len, int slot, u64 est) {
     const u64 n = R.n;
     R.host_valid = false;
+    R.blob_pending = n != 0;
     if (n == 0) {
         R.blob_len = 0;
         return MSA_OK;
@@ -964,14 +1027,19 @@ static int sort_and_blob(msa_ctx *c, Ranked &R, const u8 *wbuf, const u8 *wextra
     HIPC(c, msa_launch_blob(R.order.as<u32>(), n, R.ref.as<u64>(), R.K[0][1].as<u64>(), R.K[0][2].as<u64>(),
                             R.cnt.as<u64>(), wbuf, wextra, c->l_pos.as<u64>(), c->l_len.as<u32>(), arena, key_off, key_len,
                             R.len.as<u64>(), R.off.as<u64>(), c->scan_bsum.as<u64>(), c->scan_total.as<u64>(), nullptr,
-                            nullptr, c->stream, 0));
-    HIPC(c, hipMemcpyAsync(&R.blob_len, c->scan_total.p, 8, hipMemcpyDeviceToHost, c->stream));
-    HIPC(c, hipStreamSynchronize(c->stream));
-    HIPC(c, ensure(R.blob, R.blob_len + 16));
+                            nullptr, 0, c->stream, 0));
+    // the blob length stays on the device until do_rank's one sync: the blob is
+    // sized from what the host knows (the last run's length, or an estimate)
+    // and k_blob_write skips keys past that capacity (do_rank redoes them)
+    HIPC(c, ensure(c->blob_tot, 64));
+    HIPC(c, hipMemcpyAsync(c->blob_tot.as<u64>() + slot, c->scan_total.p, 8, hipMemcpyDeviceToDevice, c->stream));
+    HIPC(c, ensure(R.blob, std::max<u64>(est, R.blob_len) + 16));
+    R.blob_cap = R.blob.cap - 16;
     HIPC(c, msa_launch_blob(R.order.as<u32>(), n, R.ref.as<u64>(), R.K[0][1].as<u64>(), R.K[0][2].as<u64>(),
                             R.cnt.as<u64>(), wbuf, wextra, c->l_pos.as<u64>(), c->l_len.as<u32>(), arena, key_off, key_len,
                             R.len.as<u64>(), R.off.as<u64>(), c->scan_bsum.as<u64>(), c->scan_total.as<u64>(),
-                            R.blob.as<u8>(), R.counts.as<u64>(), c->stream, 1));
+                            R.blob.as<u8>(), R.counts.as<u64>(), R.blob_cap, c->stream, 1));
+    R.pending = BlobArgs{wbuf, wextra, arena, key_off, key_len};
     return MSA_OK;
 }
 
@@ -1011,7 +1079,8 @@ static int do_rank(msa_ctx *c) {
     }
     const u8 *wbuf = c->merged_w ? c->imp_w.as<u8>() : c->in;
     const u8 *wextra = c->merged_w ? c->imp_w.as<u8>() : c->extra.as<u8>();
-    if ((rc = sort_and_blob(c, W, wbuf, wextra, nullptr, nullptr, nullptr))) return rc;
+    const u64 west = c->h_ctr.s_claimed * 8 + c->h_ctr.m_claimed * 16 + c->h_ctr.l_claimed * 48;
+    if ((rc = sort_and_blob(c, W, wbuf, wextra, nullptr, nullptr, nullptr, 0, west))) return rc;
     prof_end(c, ST_RANK_WORDS, W.n * 64 + W.blob_len);
     // artists
     Ranked &A = c->ra;
@@ -1029,9 +1098,33 @@ static int do_rank(msa_ctx *c) {
                                           A.cnt.as<u64>(), c->stream));
     }
     const u8 *aarena = c->merged_a ? c->imp_a.as<u8>() : c->arena.as<u8>();
-    if ((rc = sort_and_blob(c, A, wbuf, wextra, aarena, c->key_off.as<u64>(), c->key_len.as<u32>()))) return rc;
+    if ((rc = sort_and_blob(c, A, wbuf, wextra, aarena, c->key_off.as<u64>(), c->key_len.as<u32>(), 1, A.n * 32)))
+        return rc;
     prof_end(c, ST_RANK_ARTISTS, A.n * 64 + A.blob_len);
+    // the one read-back of the ranking: both blob lengths; a blob that did not
+    // fit the capacity it was written with is grown and written again
+    u64 tot[2] = {0, 0};
+    if (W.blob_pending || A.blob_pending)
+        HIPC(c, hipMemcpyAsync(tot, c->blob_tot.p, sizeof tot, hipMemcpyDeviceToHost, c->stream));
     HIPC(c, hipStreamSynchronize(c->stream));
+    bool again = false;
+    for (int t = 0; t < 2; ++t) {
+        Ranked &R = t ? A : W;
+        if (!R.blob_pending) continue;
+        R.blob_pending = false;
+        R.blob_len = tot[t];
+        if (R.blob_len <= R.blob_cap) continue;
+        HIPC(c, ensure(R.blob, R.blob_len + 16));
+        R.blob_cap = R.blob.cap - 16;
+        const BlobArgs &b = R.pending;
+        HIPC(c, msa_launch_blob(R.order.as<u32>(), R.n, R.ref.as<u64>(), R.K[0][1].as<u64>(), R.K[0][2].as<u64>(),
+                                R.cnt.as<u64>(), b.wbuf, b.wextra, c->l_pos.as<u64>(), c->l_len.as<u32>(), b.arena,
+                                b.key_off, b.key_len, R.len.as<u64>(), R.off.as<u64>(), c->scan_bsum.as<u64>(),
+                                c->scan_total.as<u64>(), R.blob.as<u8>(), R.counts.as<u64>(), R.blob_cap, c->stream,
+                                1));
+        again = true;
+    }
+    if (again) HIPC(c, hipStreamSynchronize(c->stream));
     c->stage = 3;
     return MSA_OK;
 }
@@ -1086,7 +1179,7 @@ void msa_destroy(msa_ctx *c) {
                      &c->nulrel, &c->acol, &c->alen, &c->aoff, &c->asrc, &c->apairs, &c->tcol, &c->tlen, &c->toff, &c->tsrc, &c->tpairs,
                      &c->scan_bsum, &c->scan_total, &c->ar_start, &c->arena, &c->key_off,
                      &c->key_len, &c->key_slot, &c->s_tab, &c->s_list, &c->m_tab, &c->m_list, &c->l_pos, &c->l_len,
-                     &c->l_slot, &c->l_tab, &c->l_list, &c->a_tab, &c->a_list, &c->ctr, &c->kh1, &c->kh2, &c->mlog, &c->mlog_n, &c->sort_scratch,
+                     &c->l_slot, &c->l_tab, &c->l_list, &c->a_tab, &c->a_list, &c->ctr, &c->kh1, &c->kh2, &c->mlog, &c->mlog_n, &c->sort_scratch, &c->blob_tot,
                      &c->t_head, &c->t_tie, &c->t_runid, &c->t_tpos, &c->t_bsum, &c->t_total, &c->t_Vn, &c->t_Pn,
                      &c->t_Vc, &c->t_Pc};
     for (DevBuf *b : all) release(*b);
@@ -1240,6 +1333,8 @@ int msa_get_split_column(msa_ctx *c, int which, char **out, size_t *len) {
     if (which == 1 && !c->have_tcol)
         return fail(c, MSA_ERR_ARG, "text column not materialised (pass MSA_SPLIT_TEXT_COLUMN)");
     HIPC(c, hipSetDevice(c->device));
+    int rc;
+    if ((rc = resolve_col_lens(c))) return rc;
     const DevBuf &b = which ? c->tcol : c->acol;
     const u64 n = which ? c->tcol_len : c->acol_len;
     char *p = (char *)malloc(n + 1);
@@ -1311,6 +1406,8 @@ static int piece_of(msa_ctx *c, int piece, const u8 **base, u64 *len) {
     }
     if (piece == MSA_PIECE_ARTISTS) {
         if (c->stage < 1) return fail(c, MSA_ERR_ARG, "artist piece before msa_split_columns");
+        int rc;
+        if ((rc = resolve_col_lens(c))) return rc;
         *base = c->acol.as<u8>() + c->a_hdr_getline;
         *len = c->acol_len - c->a_hdr_getline;
         return MSA_OK;

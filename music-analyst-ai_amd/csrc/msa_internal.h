@@ -253,7 +253,8 @@ struct Counters {
     u64 a_quoted;
     u64 a_long;      // bytes used in the long-key arena (k_rec_spans)
     u64 k3_misses;   // K3 LDS-table misses logged for k_miss_agg (diagnostic)
-    u64 pad[4];
+    u64 col_body[2]; // artist.csv / text.csv body bytes (the line-offset scans' totals)
+    u64 pad[2];
 };
 
 enum { OVF_S = 1, OVF_M = 2, OVF_L = 4, OVF_LT = 8, OVF_A = 16, OVF_REC = 32 };

@@ -7,6 +7,7 @@
 //     LDS, then merge passes by rank -- with an exact strcmp fix-up of the
 //     rare equal-prefix runs: the order of entry_compare_desc (178-188)
 //   * generic exclusive scan (u64)
+#include "msa_hip.h"
 #include "msa_internal.h"
 #include "msa_tables.h"
 
@@ -489,9 +490,10 @@ __global__ __launch_bounds__(256) void k_rec_spans(const u8 *__restrict__ buf, c
 __global__ __launch_bounds__(CG_T) void k_col_gather(const u8 *__restrict__ buf, const u64 *__restrict__ line_len,
                                                      const u64 *__restrict__ line_off,
                                                      const u64 *__restrict__ span_src,
-                                                     const u32 *__restrict__ span_pairs, u64 nrec, u64 hdr, u64 body,
-                                                     u8 *__restrict__ col) {
+                                                     const u32 *__restrict__ span_pairs, u64 nrec, u64 hdr,
+                                                     const u64 *__restrict__ body_p, u8 *__restrict__ col) {
     __shared__ u64 w_off[CG_T + 1], w_src[CG_T];
+    const u64 body = *body_p;  // column body bytes (the scan's total, left on the device)
     __shared__ u32 smap[CG_MAXS];  // slot -> line holding the slot's first byte
     __shared__ u32 tmax[CG_T];
     const u64 r0 = (u64)blockIdx.x * CG_T;
@@ -669,8 +671,9 @@ __device__ __forceinline__ void put_line(P dst, const u8 *__restrict__ buf, u64 
 
 __global__ __launch_bounds__(CL_T) void k_col_lines(const u8 *__restrict__ buf, const u64 *__restrict__ line_len,
                                                     const u64 *__restrict__ line_off, const u64 *__restrict__ span_src,
-                                                    const u32 *__restrict__ span_pairs, u64 nrec, u64 hdr, u64 body,
-                                                    u8 *__restrict__ col) {
+                                                    const u32 *__restrict__ span_pairs, u64 nrec, u64 hdr,
+                                                    const u64 *__restrict__ body_p, u8 *__restrict__ col) {
+    const u64 body = *body_p;
     __shared__ __attribute__((aligned(16))) u8 st[CL_LDS];
     const u64 r0 = (u64)blockIdx.x * CL_T;
     const u32 t = threadIdx.x;
@@ -1475,15 +1478,20 @@ __global__ void k_blob_write(const u32 *__restrict__ order, u64 n, const u64 *__
                              const u64 *__restrict__ K1u, const u64 *__restrict__ K0u, const u64 *__restrict__ cnt,
                              const u8 *buf, const u8 *extra, const u64 *l_pos, const u32 *l_len, const u8 *arena,
                              const u64 *key_off, const u32 *key_len, const u64 *__restrict__ off,
-                             u8 *__restrict__ blob, u64 *__restrict__ counts_out) {
+                             const u64 *__restrict__ len, u8 *__restrict__ blob, u64 *__restrict__ counts_out,
+                             u64 blob_cap) {
     const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const u32 e = order[i];
     const u64 r = ref[e];
     const u32 kind = (u32)(r >> 60);
     const u64 idx = r & ((1ull << 60) - 1);
-    u8 *dst = blob + off[i];
     counts_out[i] = cnt[e];
+    // the blob was sized before its length came back to the host: a key that
+    // does not fit is skipped (the host sees the total, grows the blob and
+    // writes it again)
+    if (off[i] + len[i] > blob_cap) return;
+    u8 *dst = blob + off[i];
     if (kind == KIND_L) {
         const u8 *p = tok_at(buf, extra, l_pos[idx]);
         for (u32 k = 0; k < l_len[idx]; ++k) dst[k] = (u8)lower1(p[k]);
@@ -1511,16 +1519,23 @@ hipError_t msa_launch_rec_spans(const u8 *buf, const u64 *rs, const u32 *nul, u6
                            apairs, tlen, tsrc, tpairs, ctr, ak);
     return hipGetLastError();
 }
+// body_p: the column body length on the device (the offsets' scan total);
+// the PAD bytes after the column are zeroed here too
+__global__ void k_zero_tail(u8 *__restrict__ col, u64 hdr, const u64 *__restrict__ body_p, u32 pad) {
+    const u64 at = hdr + *body_p;
+    for (u32 k = threadIdx.x; k < pad; k += blockDim.x) col[at + k] = 0;
+}
 hipError_t msa_launch_col_write(int text, const u8 *buf, const u64 *len, const u64 *off, const u64 *src,
-                                const u32 *pairs, u64 nrec, u64 hdr, u64 body, u8 *col, hipStream_t s) {
-    if (!nrec || !body) return hipSuccess;
+                                const u32 *pairs, u64 nrec, u64 hdr, const u64 *body_p, u8 *col, hipStream_t s) {
+    hipLaunchKernelGGL(k_zero_tail, dim3(1), dim3(256), 0, s, col, hdr, body_p, (u32)MSA_INPUT_PAD);
+    if (!nrec) return hipGetLastError();
     if (!text) {
         hipLaunchKernelGGL(k_col_lines, dim3((u32)((nrec + CL_T - 1) / CL_T)), dim3(CL_T), 0, s, buf, len, off, src,
-                           pairs, nrec, hdr, body, col);
+                           pairs, nrec, hdr, body_p, col);
         return hipGetLastError();
     }
     const u64 groups = (nrec + CG_T - 1) / CG_T;
-    hipLaunchKernelGGL(k_col_gather, dim3((u32)groups), dim3(CG_T), 0, s, buf, len, off, src, pairs, nrec, hdr, body,
+    hipLaunchKernelGGL(k_col_gather, dim3((u32)groups), dim3(CG_T), 0, s, buf, len, off, src, pairs, nrec, hdr, body_p,
                        col);
     hipLaunchKernelGGL(k_col_collapse, grid1(nrec), dim3(256), 0, s, buf, len, off, src, pairs, nrec, hdr, col);
     return hipGetLastError();
@@ -1628,14 +1643,14 @@ hipError_t msa_launch_fixup(const u64 *K2, const u64 *K1, const u64 *K0, const u
 hipError_t msa_launch_blob(const u32 *order, u64 n, const u64 *ref, const u64 *K1u, const u64 *K0u, const u64 *cnt,
                            const u8 *buf, const u8 *extra, const u64 *l_pos, const u32 *l_len, const u8 *arena, const u64 *key_off,
                            const u32 *key_len, u64 *len, u64 *off, u64 *bsum, u64 *total, u8 *blob, u64 *counts_out,
-                           hipStream_t s, int phase) {
+                           u64 blob_cap, hipStream_t s, int phase) {
     if (!n) return hipSuccess;
     if (phase == 0) {
         hipLaunchKernelGGL(k_blob_len, grid1(n), dim3(256), 0, s, order, n, ref, K1u, K0u, l_len, key_len, len);
         return msa_exclusive_scan(len, n, off, bsum, total, s);
     }
     hipLaunchKernelGGL(k_blob_write, grid1(n), dim3(256), 0, s, order, n, ref, K1u, K0u, cnt, buf, extra, l_pos, l_len, arena,
-                       key_off, key_len, (const u64 *)off, blob, counts_out);
+                       key_off, key_len, (const u64 *)off, (const u64 *)len, blob, counts_out, blob_cap);
     return hipGetLastError();
 }
 

@@ -59,6 +59,31 @@ static char *read_file(const char *path, size_t *len) {
     return b;
 }
 
+/* os.fspath(Path(p)) (POSIX pathlib): repeated slashes and "." components
+ * collapse, a trailing slash goes, ".." stays, exactly two leading slashes
+ * are kept, "" becomes "." -- the script prints its paths this way (148-155). */
+static void path_norm(const char *p, char *out, size_t cap) {
+    size_t o = 0;
+    const size_t n = strlen(p);
+    if (n >= 2 && p[0] == '/' && p[1] == '/' && (n == 2 || p[2] != '/')) { out[o++] = '/'; out[o++] = '/'; }
+    else if (n >= 1 && p[0] == '/') out[o++] = '/';
+    const size_t root = o;
+    for (size_t i = 0; i < n;) {
+        while (i < n && p[i] == '/') ++i;
+        size_t j = i;
+        while (j < n && p[j] != '/') ++j;
+        const size_t len = j - i;
+        if (len && !(len == 1 && p[i] == '.') && o + len + 2 < cap) {
+            if (o > root) out[o++] = '/';
+            memcpy(out + o, p + i, len);
+            o += len;
+        }
+        i = j;
+    }
+    if (o == 0) out[o++] = '.';
+    out[o] = 0;
+}
+
 int main(int argc, char **argv) {
     const char *csv = NULL, *outdir = "output/serial_word_counts", *delim = NULL, *enc = "utf-8-sig";
     for (int i = 1; i < argc; ++i) {
@@ -144,8 +169,16 @@ int main(int argc, char **argv) {
     msa_wcs_summary s;
     msa_wcs_get_summary(w, &s);
     msa_wcs_destroy(w);
-    printf("Concluído. Processadas %llu linhas. Arquivos gerados em %s\n", (unsigned long long)s.total_rows, outdir);
-    printf(" - %s/word_counts_global.csv\n", outdir);
-    printf(" - %s/word_counts_by_song.csv\n", outdir);
+    char shown[4096];
+    path_norm(outdir, shown, sizeof shown);
+    const char *sep = strcmp(shown, "/") && strcmp(shown, "//") ? "/" : "";
+    printf("Concluído. Processadas %llu linhas. Arquivos gerados em %s\n", (unsigned long long)s.total_rows, shown);
+    if (!strcmp(shown, ".")) {  /* Path(".") / "x" is "x" */
+        printf(" - word_counts_global.csv\n");
+        printf(" - word_counts_by_song.csv\n");
+    } else {
+        printf(" - %s%sword_counts_global.csv\n", shown, sep);
+        printf(" - %s%sword_counts_by_song.csv\n", shown, sep);
+    }
     return 0;
 }

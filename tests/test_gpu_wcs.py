@@ -153,3 +153,21 @@ def test_wcs_cli_golden(msa_mod, name, tmp_path):
     assert f"Processadas {exp[0]} linhas".encode() in r.stdout
     assert (out / "word_counts_by_song.csv").read_bytes() == exp[1]
     assert (out / "word_counts_global.csv").read_bytes() == exp[2]
+
+
+@pytest.mark.parametrize("outdir", ["out/", "./out", "out//sub/", "./out/./sub", "."])
+def test_wcs_cli_prints_paths_like_pathlib(msa_mod, outdir, tmp_path):
+    """The script prints os.fspath(Path(output_dir)) (word_count_per_song.py:148-155)."""
+    from pathlib import Path
+
+    cli = os.path.join(msa_mod.PKG_DIR, "bin", "word_count_per_song")
+    data, exp = load_case("basic")
+    inp = tmp_path / "in.csv"
+    inp.write_bytes(data)
+    r = subprocess.run([cli, str(inp), "--output-dir", outdir, "--delimiter", ","], capture_output=True, timeout=120,
+                       cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr
+    od = Path(outdir)
+    want = (f"Concluído. Processadas {exp[0]} linhas. Arquivos gerados em {os.fspath(od)}\n"
+            f" - {os.fspath(od / 'word_counts_global.csv')}\n - {os.fspath(od / 'word_counts_by_song.csv')}\n")
+    assert r.stdout.decode() == want
