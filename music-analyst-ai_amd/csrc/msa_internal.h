@@ -142,8 +142,22 @@ __device__ __forceinline__ u32 swar_eq(u32 x, u32 byte) {
 __device__ __forceinline__ u32 swar_ge7(u32 y7, u32 c) {  // y7 bytes < 0x80; 0x80 where byte >= c
     return (y7 + (0x80u - c) * 0x01010101u) & 0x80808080u;
 }
-// 0x80-per-byte mask -> 4-bit mask (byte j -> bit j)
-__device__ __forceinline__ u32 swar_pack4(u32 m) { return (((m >> 7) * 0x00204081u) >> 21) & 0xFu; }
+// 0x80-per-byte mask -> 4-bit mask (byte j -> bit j): one v_dot4_u32_u8 (the
+// bytes weighted 1, 2, 4, 8), not a 32-bit multiply (quarter rate)
+__device__ __forceinline__ u32 swar_pack4(u32 m) { return __builtin_amdgcn_udot4(m, 0x08040201u, 0u, false) >> 7; }
+// Two dwords of 0x80 flags -> 128 x (8-bit mask): bytes of a -> bits 0..3, of
+// b -> bits 4..7 (two chained dot4s)
+__device__ __forceinline__ u32 swar_pack8x128(u32 a, u32 b) {
+    return __builtin_amdgcn_udot4(b, 0x80402010u, __builtin_amdgcn_udot4(a, 0x08040201u, 0u, false), false);
+}
+// Byte k (0..7) of a 64-bit mask kept as two dwords, from swar_pack8x128
+__device__ __forceinline__ void swar_put8(u32 &lo, u32 &hi, int k, u32 p128) {
+    const int s = 8 * (k & 3) - 7;
+    const u32 v = s < 0 ? (p128 >> 7) : (p128 << s);
+    if (k < 4) lo |= v;
+    else hi |= v;
+}
+__device__ __forceinline__ u64 mk64(u32 lo, u32 hi) { return ((u64)hi << 32) | lo; }
 
 // Token byte of process_lyrics (parallel_spotify.c:359): isalnum (C locale) or '\''.
 __device__ __forceinline__ u32 swar_tok(u32 x) {

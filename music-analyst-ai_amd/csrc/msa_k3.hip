@@ -25,7 +25,9 @@
 
 namespace {
 
+#ifndef Q_T
 #define Q_T 1024                 // 16 waves: one workgroup per CU
+#endif
 #define Q_W (Q_T / 64)
 #define Q_BLK 4096               // bytes per wave-iteration
 // Token keys are re-read from the input (just loaded: L1/L2) rather than
@@ -35,8 +37,8 @@ namespace {
 #define Q_LIST 1024              // token entries per wave-iteration (>= 4 bytes per token)
 #define Q_MISS 32                // deferred HBM inserts per wave (16 B each)
 #define Q_WLDS (Q_LIST * 2 + Q_MISS * 16)
-#ifndef Q_SLOTS
-#define Q_SLOTS 6140             // LDS word table: 16-byte keys + u32 counts
+#ifndef Q_SLOTS                  // LDS word table: 16-byte keys + u32 counts (the rest of the CU's LDS)
+#define Q_SLOTS (((163840 - Q_W * (Q_LIST * 2 + Q_MISS * 16) - MSA_MLOG_PARTS * 4) / 20) & ~3)
 #endif
 #define Q_NB (Q_SLOTS / 4)
 #define Q_TAB (Q_SLOTS * 20)
@@ -47,6 +49,10 @@ static_assert(Q_SLOTS % 4 == 0 && Q_TAB % 16 == 0 && Q_WLDS % 16 == 0, "LDS carv
 // Every key byte of a token is < 0x80 (alnum or '\''), so bit 63 of the
 // second key word is free: it marks a published slot (an S word has k1 == 0).
 #define KMARK 0x8000000000000000ull
+
+#ifndef K3_ROT
+#define K3_ROT 0
+#endif
 
 __device__ __forceinline__ uint4 ldg16(const u8 *p) { return *reinterpret_cast<const uint4 *>(p); }
 
@@ -108,31 +114,38 @@ __device__ __forceinline__ u32 lower_tok(u32 &x) {
 __device__ __forceinline__ Masks classify64x(uint4 (&v)[4], u32 nvalid) {
     Masks k{0, 0, 0, 0, 0, 0};
     u32 rare = 0;
+    u32 q0 = 0, q1 = 0, c0 = 0, c1 = 0, n0 = 0, n1 = 0, t0 = 0, t1 = 0;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         u32 w[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
 #pragma unroll
-        for (int d = 0; d < 4; ++d) {
-            const u32 sh = 16 * q + 4 * d;
-            rare |= has80(w[d], '\r') | has80(w[d], 0);
-            k.Q |= (u64)pk4(eq80(w[d], '"')) << sh;
-            k.C |= (u64)pk4(eq80(w[d], ',')) << sh;
-            k.NL |= (u64)pk4(eq80(w[d], '\n')) << sh;
-            k.T |= (u64)pk4(lower_tok(w[d])) << sh;
+        for (int d = 0; d < 4; ++d) rare |= has80(w[d], '\r') | has80(w[d], 0);
+        // dwords in pairs: byte k = 2q + h of each 64-bit mask (dot4 packing)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int kb = 2 * q + h;
+            u32 &a = w[2 * h], &b = w[2 * h + 1];
+            swar_put8(q0, q1, kb, swar_pack8x128(eq80(a, '"'), eq80(b, '"')));
+            swar_put8(c0, c1, kb, swar_pack8x128(eq80(a, ','), eq80(b, ',')));
+            swar_put8(n0, n1, kb, swar_pack8x128(eq80(a, '\n'), eq80(b, '\n')));
+            swar_put8(t0, t1, kb, swar_pack8x128(lower_tok(a), lower_tok(b)));
         }
-        v[q] = make_uint4(w[0], w[1], w[2], w[3]);
     }
+    k.Q = mk64(q0, q1); k.C = mk64(c0, c1); k.NL = mk64(n0, n1); k.T = mk64(t0, t1);
     if (__ballot(rare != 0)) {
+        u32 r0 = 0, r1 = 0, z0 = 0, z1 = 0;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const u32 w[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
 #pragma unroll
-            for (int d = 0; d < 4; ++d) {
-                const u32 sh = 16 * q + 4 * d;
-                k.CR |= (u64)pk4(eq80(w[d], '\r')) << sh;
-                k.Z |= (u64)pk4(eq80(w[d], 0)) << sh;
+            for (int h = 0; h < 2; ++h) {
+                const int kb = 2 * q + h;
+                swar_put8(r0, r1, kb, swar_pack8x128(eq80(w[2 * h], '\r'), eq80(w[2 * h + 1], '\r')));
+                swar_put8(z0, z1, kb, swar_pack8x128(eq80(w[2 * h], 0), eq80(w[2 * h + 1], 0)));
             }
         }
+        k.CR = mk64(r0, r1);
+        k.Z = mk64(z0, z1);
     }
     const u64 vm = bits_lo(nvalid);
     k.Q &= vm; k.C &= vm; k.NL &= vm; k.CR &= vm; k.Z &= vm; k.T &= vm;
@@ -165,23 +178,33 @@ __device__ __forceinline__ u32 lds_find16(ulonglong2 *keys, u64 k0, u64 k1) {
     h ^= h >> 15;
     h *= 0x2C1B3C6Du;
     u32 b = __umulhi(h, (u32)Q_NB);
+#if K3_ROT
+    // the four slot reads of a bucket start at a key-dependent slot: a
+    // ds_read_b128 lane group (16 lanes) then spreads over 16 positions of the
+    // 256-byte bank row instead of the 4 that bucket alignment alone gives
+    const u32 ro = h & 3u;
+#else
+    const u32 ro = 0;
+#endif
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
         const u32 base = b * 4;
-        const ulonglong2 s0 = keys[base], s1 = keys[base + 1], s2 = keys[base + 2], s3 = keys[base + 3];
+        const ulonglong2 s0 = keys[base + (ro & 3u)], s1 = keys[base + ((ro + 1) & 3u)];
+        const ulonglong2 s2 = keys[base + ((ro + 2) & 3u)], s3 = keys[base + ((ro + 3) & 3u)];
         const bool e0 = (s0.x == k0) & (s0.y == k1), e1 = (s1.x == k0) & (s1.y == k1);
         const bool e2 = (s2.x == k0) & (s2.y == k1), e3 = (s3.x == k0) & (s3.y == k1);
         const u32 hit = e0 ? 0u : (e1 ? 1u : (e2 ? 2u : (e3 ? 3u : 4u)));
-        if (hit < 4) return base + hit;
+        if (hit < 4) return base + ((ro + hit) & 3u);
         u32 i = s0.x == 0 ? 0u : (s1.x == 0 ? 1u : (s2.x == 0 ? 2u : (s3.x == 0 ? 3u : 4u)));
         for (; i < 4; ++i) {
-            u64 *kp = reinterpret_cast<u64 *>(&keys[base + i]);
+            const u32 sl = base + ((ro + i) & 3u);
+            u64 *kp = reinterpret_cast<u64 *>(&keys[sl]);
             const u64 old = atomicCAS((unsigned long long *)kp, 0ull, (unsigned long long)k0);
             if (old == 0) {
                 kp[1] = k1;  // published; a prober that reads 0 moves on
-                return base + i;
+                return sl;
             }
-            if (old == k0 && kp[1] == k1) return base + i;
+            if (old == k0 && kp[1] == k1) return sl;
         }
         b = (b + 1 == Q_NB) ? 0 : b + 1;
     }
@@ -429,7 +452,7 @@ __global__ __launch_bounds__(Q_T, 1) void k_scan_csv(ScanArgs a) {
             // (block offset | (length - 3) << 12), then the lanes take them
             // 64 at a time.  Diagnostic ablations (MSA_ABLATE; results
             // invalid): 1 no tokens at all, 2 no counting, 32 keys without
-            // the LDS table, 4 LDS misses dropped
+            // the LDS table, 4 LDS misses dropped, 128 keys not re-read from memory
             u64 m = (a.ablate & 3) ? 0ull : sSM;
             u32 ntok;
             u32 li = wave_prefix<5>((u32)__popcll(m), ntok);
@@ -454,7 +477,14 @@ __global__ __launch_bounds__(Q_T, 1) void k_scan_csv(ScanArgs a) {
                     const u32 len = (e >> 12) + 3;
                     const u64 ap = ib + (e & 4095u);
                     const u64 *gw = reinterpret_cast<const u64 *>(a.buf + (ap & ~7ull));
-                    const u64 w0 = gw[0], w1 = gw[1], w2 = gw[2];
+                    u64 w0, w1, w2;
+                    if (a.ablate & 128) {  // diagnostic: keys made up from the list entry (no re-read)
+                        w0 = (u64)e * 0x9E3779B97F4A7C15ull & 0x7F7F7F7F7F7F7F7Full;
+                        w1 = w0 >> 3;
+                        w2 = 0;
+                    } else {
+                        w0 = gw[0]; w1 = gw[1]; w2 = gw[2];
+                    }
                     const u32 sh = (u32)(ap & 7u) * 8u;
                     u64 x0 = sh ? ((w0 >> sh) | (w1 << (64 - sh))) : w0;
                     u64 x1 = sh ? ((w1 >> sh) | (w2 << (64 - sh))) : w1;
@@ -515,23 +545,30 @@ __device__ __forceinline__ u32 ma_find(ulonglong2 *keys, u64 k0, u64 k1) {
     h ^= h >> 15;
     h *= 0x2C1B3C6Du;
     u32 b = __umulhi(h, (u32)MA_NB);
+#if K3_ROT
+    const u32 ro = h & 3u;  // key-dependent first slot (bank spread, as lds_find16)
+#else
+    const u32 ro = 0;
+#endif
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
         const u32 base = b * 4;
-        const ulonglong2 s0 = keys[base], s1 = keys[base + 1], s2 = keys[base + 2], s3 = keys[base + 3];
+        const ulonglong2 s0 = keys[base + (ro & 3u)], s1 = keys[base + ((ro + 1) & 3u)];
+        const ulonglong2 s2 = keys[base + ((ro + 2) & 3u)], s3 = keys[base + ((ro + 3) & 3u)];
         const bool e0 = (s0.x == k0) & (s0.y == k1), e1 = (s1.x == k0) & (s1.y == k1);
         const bool e2 = (s2.x == k0) & (s2.y == k1), e3 = (s3.x == k0) & (s3.y == k1);
         const u32 hit = e0 ? 0u : (e1 ? 1u : (e2 ? 2u : (e3 ? 3u : 4u)));
-        if (hit < 4) return base + hit;
+        if (hit < 4) return base + ((ro + hit) & 3u);
         u32 i = s0.x == 0 ? 0u : (s1.x == 0 ? 1u : (s2.x == 0 ? 2u : (s3.x == 0 ? 3u : 4u)));
         for (; i < 4; ++i) {
-            u64 *kp = reinterpret_cast<u64 *>(&keys[base + i]);
+            const u32 sl = base + ((ro + i) & 3u);
+            u64 *kp = reinterpret_cast<u64 *>(&keys[sl]);
             const u64 old = atomicCAS((unsigned long long *)kp, 0ull, (unsigned long long)k0);
             if (old == 0) {
                 kp[1] = k1;
-                return base + i;
+                return sl;
             }
-            if (old == k0 && kp[1] == k1) return base + i;
+            if (old == k0 && kp[1] == k1) return sl;
         }
         b = (b + 1 == MA_NB) ? 0 : b + 1;
     }

@@ -72,29 +72,36 @@ __device__ __forceinline__ u32 k1_has80(u32 x, u32 c) {
 __device__ __forceinline__ Classes64 classify64(const uint4 (&v)[4], u64 lpos, u64 end) {
     Classes64 k{0, 0, 0, 0, 0};
     u32 rare = 0;
+    u32 q0 = 0, q1 = 0, c0 = 0, c1 = 0, n0 = 0, n1 = 0;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const u32 w[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
 #pragma unroll
-        for (int d = 0; d < 4; ++d) {
-            const u32 sh = 16 * q + 4 * d;
-            rare |= k1_has80(w[d], '\r') | k1_has80(w[d], 0);
-            k.Q |= (u64)swar_pack4(k1_eq80(w[d], '"')) << sh;
-            k.C |= (u64)swar_pack4(k1_eq80(w[d], ',')) << sh;
-            k.NL |= (u64)swar_pack4(k1_eq80(w[d], '\n')) << sh;
+        for (int d = 0; d < 4; ++d) rare |= k1_has80(w[d], '\r') | k1_has80(w[d], 0);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {  // dword pairs: byte 2q + h of each mask
+            const int kb = 2 * q + h;
+            const u32 a = w[2 * h], b = w[2 * h + 1];
+            swar_put8(q0, q1, kb, swar_pack8x128(k1_eq80(a, '"'), k1_eq80(b, '"')));
+            swar_put8(c0, c1, kb, swar_pack8x128(k1_eq80(a, ','), k1_eq80(b, ',')));
+            swar_put8(n0, n1, kb, swar_pack8x128(k1_eq80(a, '\n'), k1_eq80(b, '\n')));
         }
     }
+    k.Q = mk64(q0, q1); k.C = mk64(c0, c1); k.NL = mk64(n0, n1);
     if (__ballot(rare != 0)) {
+        u32 r0 = 0, r1 = 0, z0 = 0, z1 = 0;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const u32 w[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
 #pragma unroll
-            for (int d = 0; d < 4; ++d) {
-                const u32 sh = 16 * q + 4 * d;
-                k.CR |= (u64)swar_pack4(k1_eq80(w[d], '\r')) << sh;
-                k.Z |= (u64)swar_pack4(k1_eq80(w[d], 0)) << sh;
+            for (int h = 0; h < 2; ++h) {
+                const int kb = 2 * q + h;
+                swar_put8(r0, r1, kb, swar_pack8x128(k1_eq80(w[2 * h], '\r'), k1_eq80(w[2 * h + 1], '\r')));
+                swar_put8(z0, z1, kb, swar_pack8x128(k1_eq80(w[2 * h], 0), k1_eq80(w[2 * h + 1], 0)));
             }
         }
+        k.CR = mk64(r0, r1);
+        k.Z = mk64(z0, z1);
     }
     const u64 r = lpos < end ? end - lpos : 0;
     const u64 vm = r >= 64 ? ~0ull : ((1ull << r) - 1ull);
