@@ -636,6 +636,7 @@ static int split_once(msa_ctx *c, int flags) {
     a.seg_end = c->n;
     a.nchunks = (u32)((c->n + MSA_CHUNK - 1) / MSA_CHUNK);
     a.carry = c->carry.as<State>();
+    a.sums = c->sums.as<ChunkSum>();  // from run_scan_fn over the same [0, n)
     a.rec_start = c->rec_start.as<u64>();
     a.nulrel = c->nulrel.as<u32>();
     a.rec_cap = cap;
@@ -733,6 +734,7 @@ static int split_once(msa_ctx *c, int flags) {
             f.seg_end = c->extra_len;
             f.nchunks = 1;
             f.carry = d_zero;
+            f.sums = nullptr;
             f.lpos_tag = MSA_POS_EXTRA;
             HIPC(c, msa_launch_scan(f, 2, c->stream));
             // the remainder's words may be new keys: list the tables again

@@ -50,6 +50,7 @@ struct Fn {
 // K1 output per chunk: the chunk's function for hypotheses p=0 / p=1 with
 // cr=0 (the cr=1 entry is derived from first_nl).  Packed flags word:
 //   [15:0] nterm  [17:16] c  [18] z  [19] cr_out  [20] parity  [21] first_nl
+//   [22] the chunk holds a '\r' or NUL byte (both hypotheses)
 struct ChunkSum {
     u32 h[2];
     u32 last_end[2];  // offset in chunk just past the last terminator
@@ -158,6 +159,20 @@ __device__ __forceinline__ void swar_put8(u32 &lo, u32 &hi, int k, u32 p128) {
     else hi |= v;
 }
 __device__ __forceinline__ u64 mk64(u32 lo, u32 hi) { return ((u64)hi << 32) | lo; }
+
+// The same tests with x7 = x & 0x7F7F7F7F shared by every class of one dword:
+// "byte == c" (c < 0x80) is one v_xad_u32 + one v_bitop3_b32, and the token
+// class of process_lyrics (isalnum or '\'', parallel_spotify.c:359) a dozen ops.
+__device__ __forceinline__ u32 eq80x(u32 x, u32 x7, u32 c) {
+    const u32 t = (x7 ^ (c * 0x01010101u)) + 0x7F7F7F7Fu;  // bit 7 of a byte: low 7 bits != c
+    return ~(t | x) & 0x80808080u;
+}
+__device__ __forceinline__ u32 tok80x(u32 x, u32 x7) {
+    const u32 z = x7 | 0x20202020u;                           // case folded
+    const u32 al = (z + 0x1F1F1F1Fu) & ~(z + 0x05050505u);    // 'a'..'z'
+    const u32 dg = (x7 + 0x50505050u) & ~(x7 + 0x46464646u);  // '0'..'9'
+    return ((al | dg) & ~x & 0x80808080u) | eq80x(x, x7, '\'');
+}
 
 // Token byte of process_lyrics (parallel_spotify.c:359): isalnum (C locale) or '\''.
 __device__ __forceinline__ u32 swar_tok(u32 x) {
@@ -304,6 +319,9 @@ struct ScanArgs {
     u64 m_list_cap;
     u64 *l_pos;
     u64 l_cap;
+    // K1's chunk summaries of this segment (bit 22 of h[0]: the chunk holds a
+    // '\r' or NUL), or null: test every block
+    const ChunkSum *sums;
     u64 lpos_tag;    // OR'ed into recorded long-token positions (MSA_POS_EXTRA: the side buffer)
     Counters *ctr;
     int want_nul;    // record the first NUL of each record (text column)

@@ -111,7 +111,7 @@ __device__ __forceinline__ u32 lower_tok(u32 &x) {
 // Byte classes of the lane's 64 bytes (bit i = byte i; bytes at or past
 // `nvalid` cleared).  '\r' and NUL masks are computed only when the wave's block holds
 // one (a wave-uniform branch).
-__device__ __forceinline__ Masks classify64x(uint4 (&v)[4], u32 nvalid) {
+__device__ __forceinline__ Masks classify64x(uint4 (&v)[4], u32 nvalid, bool test_rare) {
     Masks k{0, 0, 0, 0, 0, 0};
     u32 rare = 0;
     u32 q0 = 0, q1 = 0, c0 = 0, c1 = 0, n0 = 0, n1 = 0, t0 = 0, t1 = 0;
@@ -119,16 +119,18 @@ __device__ __forceinline__ Masks classify64x(uint4 (&v)[4], u32 nvalid) {
     for (int q = 0; q < 4; ++q) {
         u32 w[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
 #pragma unroll
-        for (int d = 0; d < 4; ++d) rare |= has80(w[d], '\r') | has80(w[d], 0);
+        for (int d = 0; d < 4; ++d)
+            if (test_rare) rare |= has80(w[d], '\r') | has80(w[d], 0);
         // dwords in pairs: byte k = 2q + h of each 64-bit mask (dot4 packing)
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const int kb = 2 * q + h;
-            u32 &a = w[2 * h], &b = w[2 * h + 1];
-            swar_put8(q0, q1, kb, swar_pack8x128(eq80(a, '"'), eq80(b, '"')));
-            swar_put8(c0, c1, kb, swar_pack8x128(eq80(a, ','), eq80(b, ',')));
-            swar_put8(n0, n1, kb, swar_pack8x128(eq80(a, '\n'), eq80(b, '\n')));
-            swar_put8(t0, t1, kb, swar_pack8x128(lower_tok(a), lower_tok(b)));
+            const u32 a = w[2 * h], b = w[2 * h + 1];
+            const u32 a7 = a & 0x7F7F7F7Fu, b7 = b & 0x7F7F7F7Fu;
+            swar_put8(q0, q1, kb, swar_pack8x128(eq80x(a, a7, '"'), eq80x(b, b7, '"')));
+            swar_put8(c0, c1, kb, swar_pack8x128(eq80x(a, a7, ','), eq80x(b, b7, ',')));
+            swar_put8(n0, n1, kb, swar_pack8x128(eq80x(a, a7, '\n'), eq80x(b, b7, '\n')));
+            swar_put8(t0, t1, kb, swar_pack8x128(tok80x(a, a7), tok80x(b, b7)));
         }
     }
     k.Q = mk64(q0, q1); k.C = mk64(c0, c1); k.NL = mk64(n0, n1); k.T = mk64(t0, t1);
@@ -268,6 +270,8 @@ __global__ __launch_bounds__(Q_T, 1) void k_scan_csv(ScanArgs a) {
 
     for (u32 c = gw; c < a.nchunks; c += nw) {
         State st = a.carry[c];
+        // K1 saw no '\r' / NUL in this chunk: their masks stay empty
+        const bool rare_chunk = !a.sums || ((a.sums[c].h[0] >> 22) & 1u);
         const u64 cbase = a.seg_begin + (u64)c * MSA_CHUNK;
         const u64 cend = min(cbase + (u64)MSA_CHUNK, a.seg_end);
         u32 prevT = 0;  // the byte before the chunk is a token byte
@@ -294,7 +298,7 @@ __global__ __launch_bounds__(Q_T, 1) void k_scan_csv(ScanArgs a) {
             for (int d = 0; d < 4; ++d) ttok |= pk4(lower_tok(tw[d])) << (4 * d);
             ttok &= tvm;
             const u64 rem = cend > lpos ? cend - lpos : 0;
-            const Masks k = classify64x(cur, (u32)min(rem, (u64)64));
+            const Masks k = classify64x(cur, (u32)min(rem, (u64)64), rare_chunk);
             // the block's bytes now live in the masks: load the next block into
             // the same registers (in flight during the rest)
             if (more) {

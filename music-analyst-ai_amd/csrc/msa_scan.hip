@@ -57,6 +57,7 @@ __device__ __forceinline__ void wave_sync() {
 #define K1_ITER 4096
 struct Classes64 {
     u64 Q, C, NL, CR, Z;
+    bool rare;  // the wave's 4 KiB hold a '\r' or NUL (CR / Z computed)
 };
 // "byte == c" per byte as 0x80 flags (exact) / "some byte == c" (cheap)
 __device__ __forceinline__ u32 k1_eq80(u32 x, u32 c) {
@@ -70,7 +71,7 @@ __device__ __forceinline__ u32 k1_has80(u32 x, u32 c) {
 // The lane's 64 bytes: '"', ',' and '\n' always; '\r' and NUL only when the
 // wave's 4 KiB hold one (a cheap has-byte test, then a wave-uniform branch).
 __device__ __forceinline__ Classes64 classify64(const uint4 (&v)[4], u64 lpos, u64 end) {
-    Classes64 k{0, 0, 0, 0, 0};
+    Classes64 k{0, 0, 0, 0, 0, false};
     u32 rare = 0;
     u32 q0 = 0, q1 = 0, c0 = 0, c1 = 0, n0 = 0, n1 = 0;
 #pragma unroll
@@ -82,9 +83,10 @@ __device__ __forceinline__ Classes64 classify64(const uint4 (&v)[4], u64 lpos, u
         for (int h = 0; h < 2; ++h) {  // dword pairs: byte 2q + h of each mask
             const int kb = 2 * q + h;
             const u32 a = w[2 * h], b = w[2 * h + 1];
-            swar_put8(q0, q1, kb, swar_pack8x128(k1_eq80(a, '"'), k1_eq80(b, '"')));
-            swar_put8(c0, c1, kb, swar_pack8x128(k1_eq80(a, ','), k1_eq80(b, ',')));
-            swar_put8(n0, n1, kb, swar_pack8x128(k1_eq80(a, '\n'), k1_eq80(b, '\n')));
+            const u32 a7 = a & 0x7F7F7F7Fu, b7 = b & 0x7F7F7F7Fu;
+            swar_put8(q0, q1, kb, swar_pack8x128(eq80x(a, a7, '"'), eq80x(b, b7, '"')));
+            swar_put8(c0, c1, kb, swar_pack8x128(eq80x(a, a7, ','), eq80x(b, b7, ',')));
+            swar_put8(n0, n1, kb, swar_pack8x128(eq80x(a, a7, '\n'), eq80x(b, b7, '\n')));
         }
     }
     k.Q = mk64(q0, q1); k.C = mk64(c0, c1); k.NL = mk64(n0, n1);
@@ -102,6 +104,7 @@ __device__ __forceinline__ Classes64 classify64(const uint4 (&v)[4], u64 lpos, u
         }
         k.CR = mk64(r0, r1);
         k.Z = mk64(z0, z1);
+        k.rare = true;
     }
     const u64 r = lpos < end ? end - lpos : 0;
     const u64 vm = r >= 64 ? ~0ull : ((1ull << r) - 1ull);
@@ -128,7 +131,7 @@ __global__ __launch_bounds__(256) void k_chunk_summary(const u8 *__restrict__ bu
     for (u32 c = gw; c < nchunks; c += nw) {
         const u64 cbase = seg_begin + (u64)c * MSA_CHUNK;
         const u64 cend = min(cbase + (u64)MSA_CHUNK, seg_end);
-        u32 par = 0, first_nl = 0;
+        u32 par = 0, first_nl = 0, anyrare = 0;
         u32 cr[2] = {0, 0}, nterm[2] = {0, 0}, cc[2] = {0, 0}, zz[2] = {0, 0}, lend[2] = {0, 0};
         uint4 cur[4];
 #pragma unroll
@@ -142,6 +145,7 @@ __global__ __launch_bounds__(256) void k_chunk_summary(const u8 *__restrict__ bu
                 for (int q = 0; q < 4; ++q) nxt[q] = ld16(buf + lpos + K1_ITER + 16 * q);
             }
             const Classes64 k = classify64(cur, lpos, cend);
+            anyrare |= k.rare ? 1u : 0u;
             if (ibase == cbase) first_nl = (u32)(readlane64(k.NL, 0) & 1u);
             const u64 B = __ballot(__popcll(k.Q) & 1u);
             const u32 pin0 = par ^ (mbcnt(B) & 1u);
@@ -195,7 +199,7 @@ __global__ __launch_bounds__(256) void k_chunk_summary(const u8 *__restrict__ bu
         if (lane == 0) {
             ChunkSum s;
             for (int h = 0; h < 2; ++h) {
-                s.h[h] = nterm[h] | (cc[h] << 16) | (zz[h] << 18) | (cr[h] << 19) | (par << 20) | (first_nl << 21);
+                s.h[h] = nterm[h] | (cc[h] << 16) | (zz[h] << 18) | (cr[h] << 19) | (par << 20) | (first_nl << 21) | (anyrare << 22);
                 s.last_end[h] = lend[h];
             }
             out[c] = s;
