@@ -473,25 +473,41 @@ __global__ __launch_bounds__(Q_T, 1) void k_scan_csv(ScanArgs a) {
                 }
             }
             wsync();
+            // Keys are re-read from the block (L2) as five dwords from the
+            // token's dword; the next 64 tokens' loads are issued before this
+            // batch is probed, so their latency hides behind the LDS work.
+            u32 en = 0;
+            uint4 kv = make_uint4(0, 0, 0, 0);
+            u32 k4 = 0;
+            if (lane < ntok) {
+                en = list[lane];
+                const u32 *gp = reinterpret_cast<const u32 *>(a.buf + ((ib + (en & 4095u)) & ~3ull));
+                kv = *reinterpret_cast<const uint4 *>(gp);
+                k4 = gp[4];
+            }
             for (u32 t0 = 0; t0 < ntok; t0 += 64) {
                 bool mis = false;
                 u64 k0 = 0, k1 = KMARK;
+                const u32 e = en;
+                const uint4 v = kv;
+                const u32 v4 = k4;
+                if (t0 + 64 + lane < ntok) {
+                    en = list[t0 + 64 + lane];
+                    const u32 *gp = reinterpret_cast<const u32 *>(a.buf + ((ib + (en & 4095u)) & ~3ull));
+                    kv = *reinterpret_cast<const uint4 *>(gp);
+                    k4 = gp[4];
+                }
                 if (t0 + lane < ntok) {
-                    const u32 e = list[t0 + lane];
                     const u32 len = (e >> 12) + 3;
-                    const u64 ap = ib + (e & 4095u);
-                    const u64 *gw = reinterpret_cast<const u64 *>(a.buf + (ap & ~7ull));
-                    u64 w0, w1, w2;
+                    const u32 sh = (u32)(ib + (e & 4095u)) & 3u;
+                    u64 x0, x1;
                     if (a.ablate & 128) {  // diagnostic: keys made up from the list entry (no re-read)
-                        w0 = (u64)e * 0x9E3779B97F4A7C15ull & 0x7F7F7F7F7F7F7F7Full;
-                        w1 = w0 >> 3;
-                        w2 = 0;
+                        x0 = (u64)e * 0x9E3779B97F4A7C15ull & 0x7F7F7F7F7F7F7F7Full;
+                        x1 = x0 >> 3;
                     } else {
-                        w0 = gw[0]; w1 = gw[1]; w2 = gw[2];
+                        x0 = mk64(__builtin_amdgcn_alignbyte(v.y, v.x, sh), __builtin_amdgcn_alignbyte(v.z, v.y, sh));
+                        x1 = mk64(__builtin_amdgcn_alignbyte(v.w, v.z, sh), __builtin_amdgcn_alignbyte(v4, v.w, sh));
                     }
-                    const u32 sh = (u32)(ap & 7u) * 8u;
-                    u64 x0 = sh ? ((w0 >> sh) | (w1 << (64 - sh))) : w0;
-                    u64 x1 = sh ? ((w1 >> sh) | (w2 << (64 - sh))) : w1;
                     if (len < 8) x0 &= bits_lo(8 * len);
                     x1 = len <= 8 ? 0ull : (x1 & bits_lo(8 * (len - 8)));
                     k0 = lower8(x0);
