@@ -25,7 +25,8 @@ hipError_t msa_launch_scan_csv(const ScanArgs &, hipStream_t);
 hipError_t msa_launch_miss_agg(const ScanArgs &, hipStream_t);
 hipError_t msa_exclusive_scan(const u64 *, u64, u64 *, u64 *, u64 *, hipStream_t);
 hipError_t msa_launch_rec_spans(const u8 *, const u64 *, const u32 *, u64, u64, int, u64 *, u64 *, u32 *, u64 *, u64 *,
-                                u32 *, Counters *, const AKeys &, hipStream_t);
+                                u32 *, Counters *, const AKeys &, const u64 *, const u64 *, const u64 *, u64 *, int,
+                                hipStream_t);
 hipError_t msa_launch_artist_count(const u64 *, const u32 *, const u64 *, const u64 *, u64, u64 *, u64, u32 *, u64,
                                    Counters *, int, hipStream_t);
 hipError_t msa_launch_first_end(const u8 *, u64, u32, u32, u64 *, hipStream_t);
@@ -143,6 +144,8 @@ struct msa_ctx {
     DevBuf sums, carry, btot, bstate, small;  // small: Fn total + 2 States + ...
     // CSV records
     DevBuf rec_start, nulrel;  // rec_start[nrec] = end of the last record
+    DevBuf f0, tss, tse, span_fix;  // K3's per-record span events (k_rec_fast), listed exact-path records
+    bool spans = false;             // the last scan recorded f0 / tss / tse
     u64 nrec = 0, rec_cap = 0;
     bool have_text_arrays = false;
     // side buffer: text.csv header-label remainder read back as lyrics
@@ -568,10 +571,12 @@ static int split_columns_rest(msa_ctx *c, bool want_text, const std::string &ah,
     HIPC(c, ensure(c->kh2, (nrec + 2) * 8));
     AKeys ak{c->arena.as<u8>(), c->key_off.as<u64>(), c->key_len.as<u32>(), c->kh1.as<u64>(), c->kh2.as<u64>(),
              long_base, c->a_long_cap};
+    if (c->spans) HIPC(c, ensure(c->span_fix, (nrec + 1) * 8));
     HIPC(c, msa_launch_rec_spans(c->in, c->rec_start.as<u64>(), c->nulrel.as<u32>(), nrec, c->cont ? 0 : 1,
                                  want_text ? 1 : 0, c->alen.as<u64>(), c->asrc.as<u64>(), c->apairs.as<u32>(),
                                  c->tlen.as<u64>(), c->tsrc.as<u64>(), c->tpairs.as<u32>(), c->ctr.as<Counters>(), ak,
-                                 c->stream));
+                                 c->spans ? c->f0.as<u64>() : nullptr, c->tss.as<u64>(), c->tse.as<u64>(),
+                                 c->span_fix.as<u64>(), c->ablate, c->stream));
     if ((rc = materialise_column(c, false, ah, c->acol, c->alen, c->aoff, c->asrc, c->apairs))) return rc;
     prof_end(c, ST_ARTIST_COLUMN, c->nrec * 16 * 2 + c->nrec * 32);  // ~16-byte artist lines
     // compute_header_length (parallel_spotify.c:444-459): getline's end
@@ -624,6 +629,9 @@ static int split_once(msa_ctx *c, int flags) {
     const u64 cap = nterm + 2;
     HIPC(c, ensure(c->rec_start, cap * 8));
     HIPC(c, ensure(c->nulrel, cap * 4));
+    HIPC(c, ensure(c->f0, cap * 8));
+    HIPC(c, ensure(c->tss, cap * 8));
+    HIPC(c, ensure(c->tse, cap * 8));
     c->rec_cap = cap;
     if (want_text) HIPC(c, hipMemsetAsync(c->nulrel.p, 0, cap * 4, c->stream));
     u64 zero = 0;
@@ -640,6 +648,10 @@ static int split_once(msa_ctx *c, int flags) {
     a.rec_start = c->rec_start.as<u64>();
     a.nulrel = c->nulrel.as<u32>();
     a.rec_cap = cap;
+    a.f0 = c->f0.as<u64>();
+    a.tss = c->tss.as<u64>();
+    a.tse = c->tse.as<u64>();
+    c->spans = !(c->ablate & 64);  // the round-1 kernel records no spans
     a.s_tab = c->s_tab.as<u64>();
     a.s_mask = c->s_slots - 1;
     a.s_list = c->s_list.as<u32>();
@@ -678,6 +690,8 @@ static int split_once(msa_ctx *c, int flags) {
     if (fin.rs < c->n) {
         u64 v = c->n;
         HIPC(c, hipMemcpyAsync(c->rec_start.as<u64>() + c->nrec, &v, 8, hipMemcpyHostToDevice, c->stream));
+        u64 fx = SPAN_FIX;  // no terminator: k_rec_fast leaves the last record to the exact path
+        HIPC(c, hipMemcpyAsync(c->tse.as<u64>() + c->nrec - 1, &fx, 8, hipMemcpyHostToDevice, c->stream));
     }
     // one read-back after the scan: the counters (table overflow, long-word
     // occurrences) and -- for the first shard -- the header record's end plus
@@ -1178,7 +1192,7 @@ void msa_destroy(msa_ctx *c) {
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     DevBuf *all[] = {&c->in_own, &c->sums, &c->carry, &c->btot, &c->bstate, &c->small, &c->rec_start, &c->extra, &c->exp_buf, &c->exp_meta, &c->imp_w, &c->imp_a, &c->imp_meta,
-                     &c->nulrel, &c->acol, &c->alen, &c->aoff, &c->asrc, &c->apairs, &c->tcol, &c->tlen, &c->toff, &c->tsrc, &c->tpairs,
+                     &c->nulrel, &c->f0, &c->tss, &c->tse, &c->span_fix, &c->acol, &c->alen, &c->aoff, &c->asrc, &c->apairs, &c->tcol, &c->tlen, &c->toff, &c->tsrc, &c->tpairs,
                      &c->scan_bsum, &c->scan_total, &c->ar_start, &c->arena, &c->key_off,
                      &c->key_len, &c->key_slot, &c->s_tab, &c->s_list, &c->m_tab, &c->m_list, &c->l_pos, &c->l_len,
                      &c->l_slot, &c->l_tab, &c->l_list, &c->a_tab, &c->a_list, &c->ctr, &c->kh1, &c->kh2, &c->mlog, &c->mlog_n, &c->sort_scratch, &c->blob_tot,
@@ -1751,6 +1765,7 @@ extern "C" int msa_debug_stat(msa_ctx *c, const char *name, uint64_t *v) {
     else if (n == "collision") *v = k.collision;
     else if (n == "a_long") *v = k.a_long;
     else if (n == "overflow") *v = k.overflow;
+    else if (n == "span_fix") *v = k.span_fix;
     else return MSA_ERR_ARG;
     return MSA_OK;
 }

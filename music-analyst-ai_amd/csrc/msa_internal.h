@@ -283,7 +283,8 @@ struct Counters {
     u64 a_long;      // bytes used in the long-key arena (k_rec_spans)
     u64 k3_misses;   // K3 LDS-table misses logged for k_miss_agg (diagnostic)
     u64 col_body[2]; // artist.csv / text.csv body bytes (the line-offset scans' totals)
-    u64 pad[2];
+    u64 span_fix;    // records k_rec_fast hands to k_rec_fix (the exact per-record path)
+    u64 pad;
 };
 
 enum { OVF_S = 1, OVF_M = 2, OVF_L = 4, OVF_LT = 8, OVF_A = 16, OVF_REC = 32 };
@@ -309,6 +310,11 @@ struct ScanArgs {
     u64 *rec_start;
     u32 *nulrel;
     u64 rec_cap;
+    // per record, for the column spans (k_rec_fast): f0 = position of field
+    // 0's comma; tss = start of field 3 (| SPAN_Q: it is a '"'); tse = the
+    // record's terminator (| SPAN_Q: the byte before is a '"', | SPAN_NUL /
+    // SPAN_NOLINE)
+    u64 *f0, *tss, *tse;
     u64 *s_tab;
     u64 s_mask;
     u32 *s_list;
@@ -335,6 +341,12 @@ struct ScanArgs {
 };
 
 #define MSA_MLOG_PARTS 16
+
+#define SPAN_Q (1ull << 63)
+#define SPAN_NUL (1ull << 62)
+#define SPAN_NOLINE (1ull << 61)
+#define SPAN_FIX (1ull << 60)   // set by the host on an unterminated last record
+#define SPAN_POS ((1ull << 60) - 1)
 
 // A long-token position with this bit set indexes the context's side buffer
 // (text.csv header-label remainder, see do_split) instead of the CSV.

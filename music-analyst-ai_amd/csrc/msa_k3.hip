@@ -275,9 +275,11 @@ __global__ __launch_bounds__(Q_T, 1) void k_scan_csv(ScanArgs a) {
         const u64 cbase = a.seg_begin + (u64)c * MSA_CHUNK;
         const u64 cend = min(cbase + (u64)MSA_CHUNK, a.seg_end);
         u32 prevT = 0;  // the byte before the chunk is a token byte
+        u32 prevQ = 0;  // ... is a '"'
         if (cbase > a.seg_begin) {
             const u32 b = a.buf[cbase - 1];
             prevT = (u32)(((b | 0x20u) >= 'a' && (b | 0x20u) <= 'z') || (b >= '0' && b <= '9') || b == '\'');
+            prevQ = (u32)(b == '"');
         }
         uint4 cur[4];
 #pragma unroll
@@ -320,6 +322,12 @@ __global__ __launch_bounds__(Q_T, 1) void k_scan_csv(ScanArgs a) {
             const u64 TERM = CRu | (NLu & ~((CRu << 1) | pCR));
             const u32 tail_nl = ((tail.x & 0xFFu) == '\n' && (tvm & 1u)) ? 1u : 0u;
             const u64 nNL = lane == 63 ? (u64)tail_nl : NLn;
+            // '"' at the byte after the lane (text start after a comma at byte
+            // 63) and at the byte before it (text end before a terminator at byte 0)
+            const u32 tail_q = ((tail.x & 0xFFu) == '"' && (tvm & 1u)) ? 1u : 0u;
+            const u64 Qnx = from_next(k.Q) & 1ull, Qpv = from_prev(k.Q) >> 63;
+            const u32 qnext = lane == 63 ? tail_q : (u32)Qnx;
+            const u32 qprev = lane ? (u32)Qpv : prevQ;
             const u64 SW = CRu & ((k.NL >> 1) | (nNL << 63));  // '\r' terminators that swallow a '\n'
 
             const u32 nt = (u32)__popcll(TERM);
@@ -377,23 +385,37 @@ __global__ __launch_bounds__(Q_T, 1) void k_scan_csv(ScanArgs a) {
                         const u32 zp = (u32)__ffsll((long long)zs) - 1;
                         a.nulrel[r] = (u32)(lpos + zp - rs) + 1u;
                     }
+                    bool ok = false;  // the record's third comma is at or before this segment's end
                     if (r >= a.first_rec && !zz) {
                         // commas after a NUL do not count (the C string ends there)
                         u64 x = Cu & seg & (zs ? bits_lo((u32)__ffsll((long long)zs) - 1) : ~0ull);
                         u32 from = lo;
-                        bool ok = true;
+                        ok = true;
                         for (u32 n = cc; n < 3; ++n) {
                             if (!x) { ok = false; break; }
                             from = (u32)__ffsll((long long)x);  // one past that comma
                             x &= x - 1;
+                            // field 0 ends here (artist span for k_rec_fast)
+                            if (n == 0 && r < a.rec_cap) a.f0[r] = lpos + from - 1;
                         }
                         if (ok) {
                             u64 lv = bits_hi(from) & bits_lo(hi);
                             if (zs) lv &= bits_lo((u32)__ffsll((long long)zs) - 1);
                             live |= lv;
+                            if (cc < 3 && r < a.rec_cap) {  // field 3 starts here; '"' there?
+                                const u32 q = from < 64 ? (u32)(k.Q >> from) & 1u : qnext;
+                                a.tss[r] = (lpos + from) | (q ? SPAN_Q : 0ull);
+                            }
                         }
                     }
                     if (!E) break;
+                    if (r < a.rec_cap) {  // the record ends at this terminator
+                        const u32 q = hi ? (u32)(k.Q >> (hi - 1)) & 1u : qprev;
+                        u64 fl = q ? SPAN_Q : 0ull;
+                        if (zz || zs) fl |= SPAN_NUL;  // the C string ends before: exact path
+                        else if (!ok) fl |= SPAN_NOLINE;  // header, or < 3 commas (parse_csv_line fails)
+                        a.tse[r] = (lpos + hi) | fl;
+                    }
                     const u64 ns = lpos + hi + 1 + ((SW >> hi) & 1ull);
                     ++r;
                     if (r < a.rec_cap) a.rec_start[r] = ns;
@@ -422,6 +444,7 @@ __global__ __launch_bounds__(Q_T, 1) void k_scan_csv(ScanArgs a) {
             const u64 tp = lane ? Tp : (u64)prevT;
             const u64 S0 = k.T & live & ~((k.T << 1) | tp);
             prevT = readlane((u32)(k.T >> 63), 63);
+            prevQ = readlane((u32)(k.Q >> 63), 63);
             const u64 Tnx = from_next(k.T);
             const u64 Tn = lane == 63 ? (u64)ttok : Tnx;
             // runs: rK bit b = bytes b .. b+K-1 are token bytes (w = Tn:T)

@@ -278,6 +278,80 @@ __device__ __forceinline__ u32 quote_pairs(u64 q) {
     return pairs;
 }
 
+// Any '"' in bytes [as, as + n): 16-byte pieces, SWAR test.
+__device__ __forceinline__ bool field_has_quote(const u8 *__restrict__ buf, u64 as, u64 n) {
+    for (u64 b = 0; b < n; b += 16) {
+        const uint4 c = load16u(buf, as + b);
+        const u32 m = swar_pack4(swar_eq(c.x, '"')) | (swar_pack4(swar_eq(c.y, '"')) << 4) |
+                      (swar_pack4(swar_eq(c.z, '"')) << 8) | (swar_pack4(swar_eq(c.w, '"')) << 12);
+        const u64 left = n - b;
+        if (m & (left >= 16 ? 0xFFFFu : ((1u << left) - 1u))) return true;
+    }
+    return false;
+}
+
+// 8 dwords = 32 bytes; bytes moved up by o (0..31) positions, the top ones
+// dropped: a barrel shifter (16 / 8 / 4 bytes by selects, then v_alignbyte).
+__device__ __forceinline__ void v32_shl(u32 (&d)[8], u32 o) {
+#pragma unroll
+    for (int k = 7; k >= 0; --k) d[k] = (o & 16) ? (k >= 4 ? d[k - 4] : 0u) : d[k];
+#pragma unroll
+    for (int k = 7; k >= 0; --k) d[k] = (o & 8) ? (k >= 2 ? d[k - 2] : 0u) : d[k];
+#pragma unroll
+    for (int k = 7; k >= 0; --k) d[k] = (o & 4) ? (k >= 1 ? d[k - 1] : 0u) : d[k];
+    const u32 sh = o & 3u;
+    if (sh) {
+#pragma unroll
+        for (int k = 7; k >= 1; --k) d[k] = __builtin_amdgcn_alignbyte(d[k], d[k - 1], 4 - sh);
+        d[0] <<= 8 * sh;
+    }
+}
+
+// Key of a quoted artist field whose outer quotes are window bytes a < b:
+// duplicate_field(line, 0) = trim(collapse(inner)), built in registers (the
+// "" pairs' second quotes dropped, the kept runs shifted into place).  False
+// when the key is longer than 32 bytes.
+__device__ bool quoted_key_window(const Win64 &w, u32 a, u32 b, uint4 *k0, uint4 *k1, u32 *klen) {
+    const u64 IM = bits_from(a + 1) & bits_below(b);
+    u64 R = 0;
+    for (u64 q = win_mask<1>(w) & IM; q;) {  // greedy pairs: runs of quotes
+        const u32 st = (u32)__ffsll((long long)q) - 1;
+        const u64 rest = ~(q >> st);
+        const u32 rl = rest ? (u32)__ffsll((long long)rest) - 1 : 64u - st;
+        const u64 run = bits_below(rl) << st;
+        R |= run & ((st & 1u) ? 0x5555555555555555ull : 0xAAAAAAAAAAAAAAAAull);
+        q &= ~run;
+    }
+    u64 K = IM & ~R;
+    const u64 NS = K & ~win_mask<0>(w);
+    if (!NS) {
+        *klen = 0;
+        return true;
+    }
+    K &= bits_from((u32)__ffsll((long long)NS) - 1) & bits_below(64u - (u32)__clzll((long long)NS));
+    const u32 n = (u32)__popcll(K);
+    if (n > 32) return false;
+    u32 out[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    u32 o = 0;
+    while (K) {
+        const u32 rs = (u32)__ffsll((long long)K) - 1;
+        const u64 rest = ~(K >> rs);
+        const u32 rl = rest ? (u32)__ffsll((long long)rest) - 1 : 64u - rs;
+        uint4 t0, t1;
+        win_take32(w, rs, rl, &t0, &t1);
+        u32 t[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
+        v32_shl(t, o);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) out[k] |= t[k];
+        o += rl;
+        K &= ~(bits_below(rl) << rs);
+    }
+    *k0 = make_uint4(out[0], out[1], out[2], out[3]);
+    *k1 = make_uint4(out[4], out[5], out[6], out[7]);
+    *klen = n;
+    return true;
+}
+
 // The artist pass's key for one record when artist.csv lines are its records:
 // duplicate_field(line, 0) with line = duplicate_field(field0, 1) (the
 // artist.csv line without its '\n'), i.e. for the trimmed field [as, ae):
@@ -287,22 +361,30 @@ __device__ __forceinline__ u32 quote_pairs(u64 q) {
 // An unquoted field with a '"' makes the shortcut unavailable (a_quoted is
 // set by the caller), so its key is never used.
 __device__ void artist_key_of(const u8 *__restrict__ buf, const Win64 &w0, u64 b0, u64 as, u64 ae, u64 r,
-                              const AKeys &ak, Counters *ctr) {
+                              const AKeys &ak, Counters *ctr, int ab = 0) {
     const u64 n = ae - as;
     if (n == 0) {
         ak.key_len[r] = 0;
         return;
     }
-    bool quoted;
+    bool quoted, plain = false;
     if (ae - b0 <= 64) {  // the field is inside the record's first window
         const u32 a = (u32)(as - b0), b = (u32)(ae - 1 - b0);
         const u64 Q = win_mask<1>(w0) & bits_from(a) & bits_below(b + 1);
         quoted = n >= 2 && ((Q >> a) & 1) && ((Q >> b) & 1);
+        plain = !Q;
         u32 ka = a, kb = b + 1;  // key = window bytes [ka, kb)
         bool ok = false;
+        uint4 k0, k1;
+        u32 klen = 0;
         if (!Q) {
             ok = true;
-        } else if (quoted && !(Q & bits_from(a + 1) & bits_below(b))) {
+        } else if (!quoted) {
+            // an unquoted field holding a '"': the shortcut is off (the caller
+            // raised a_quoted), this key is never read
+            ak.key_len[r] = 0;
+            return;
+        } else if (!(Q & bits_from(a + 1) & bits_below(b))) {
             const u64 inner = bits_from(a + 1) & bits_below(b);
             const u64 nsp = inner & ~win_mask<0>(w0);
             if (!nsp) {
@@ -312,24 +394,83 @@ __device__ void artist_key_of(const u8 *__restrict__ buf, const Win64 &w0, u64 b
             ka = (u32)__ffsll((long long)nsp) - 1;
             kb = 64u - (u32)__clzll((long long)nsp);
             ok = true;
+        } else if (quoted_key_window(w0, a, b, &k0, &k1, &klen)) {  // inner quotes
+            if (!klen) {
+                ak.key_len[r] = 0;
+                return;
+            }
+            ok = true;
+            ka = 0;
+            kb = klen;  // k0 / k1 hold the key already
         }
         if (ok && kb - ka <= 32) {
-            const u32 klen = kb - ka;
-            uint4 k0, k1;
-            win_take32(w0, ka, klen, &k0, &k1);
+            if (!klen) {
+                klen = kb - ka;
+                win_take32(w0, ka, klen, &k0, &k1);
+            }
             uint4 *dst = reinterpret_cast<uint4 *>(ak.arena + 32 * r);
-            dst[0] = k0;
-            dst[1] = k1;
+            if (ab & 16384) {  // diagnostic: the key built and hashed, one store
+                const u64 w0 = ((u64)k0.y << 32) | k0.x, w1 = ((u64)k0.w << 32) | k0.z;
+                const u64 w2 = ((u64)k1.y << 32) | k1.x, w3 = ((u64)k1.w << 32) | k1.z;
+                ak.kh1[r] = akey_fold(akey_seed(klen, 0), w0, w1, w2, w3, 0) ^
+                            akey_fold(akey_seed(klen, 1), w0, w1, w2, w3, 1);
+                return;
+            }
+            if (!(ab & 8192)) {
+                dst[0] = k0;
+                dst[1] = k1;
+            }
             ak.key_off[r] = 32 * r;
             ak.key_len[r] = klen;
             const u64 w0 = ((u64)k0.y << 32) | k0.x, w1 = ((u64)k0.w << 32) | k0.z;
             const u64 w2 = ((u64)k1.y << 32) | k1.x, w3 = ((u64)k1.w << 32) | k1.z;
-            ak.kh1[r] = akey_fold(akey_seed(klen, 0), w0, w1, w2, w3, 0);
-            ak.kh2[r] = akey_fold(akey_seed(klen, 1), w0, w1, w2, w3, 1);
+            if (ab & 2048) {
+                ak.kh1[r] = w0 ^ w1 ^ w2 ^ w3;
+                ak.kh2[r] = w0;
+            } else {
+                ak.kh1[r] = akey_fold(akey_seed(klen, 0), w0, w1, w2, w3, 0);
+                ak.kh2[r] = akey_fold(akey_seed(klen, 1), w0, w1, w2, w3, 1);
+            }
             return;
         }
     } else {
         quoted = n >= 2 && buf[as] == '"' && buf[ae - 1] == '"';
+    }
+    // A field without any '"' (the long names of the synthetic corpora): its
+    // line and key are the trimmed field itself.  Copied to the long area in
+    // 16-byte pieces and hashed per 32 bytes as akey_hash_bytes does -- the
+    // byte loops below cost a dependent load per byte, and a wave waits for
+    // its slowest lane.
+    if (!plain && !quoted) plain = !field_has_quote(buf, as, n);
+    if (plain) {
+        const u64 room32 = (n + 31) & ~31ull;
+        const u64 at = atomicAdd((unsigned long long *)&ctr->a_long, (unsigned long long)room32);
+        if (at + room32 > ak.long_cap) {
+            atomicOr((unsigned long long *)&ctr->a_quoted, 2ull);
+            ak.key_len[r] = 0;
+            return;
+        }
+        uint4 *dst = reinterpret_cast<uint4 *>(ak.arena + ak.long_base + at);
+        u64 h1 = akey_seed(n, 0), h2 = akey_seed(n, 1);
+        for (u64 b = 0; b < n; b += 32) {
+            uint4 c0 = load16u(buf, as + b), c1 = load16u(buf, as + b + 16);
+            const u64 left = n - b;
+            if (left < 32) {
+                c0 = bytes_blend(make_uint4(0, 0, 0, 0), c0, 0, (u32)min(left, (u64)16));
+                c1 = left > 16 ? bytes_blend(make_uint4(0, 0, 0, 0), c1, 0, (u32)(left - 16)) : make_uint4(0, 0, 0, 0);
+            }
+            dst[b / 16] = c0;
+            dst[b / 16 + 1] = c1;
+            const u64 w0 = ((u64)c0.y << 32) | c0.x, w1 = ((u64)c0.w << 32) | c0.z;
+            const u64 w2 = ((u64)c1.y << 32) | c1.x, w3 = ((u64)c1.w << 32) | c1.z;
+            h1 = akey_fold(h1, w0, w1, w2, w3, 0);
+            h2 = akey_fold(h2, w0, w1, w2, w3, 1);
+        }
+        ak.key_off[r] = ak.long_base + at;
+        ak.key_len[r] = (u32)n;
+        ak.kh1[r] = h1;
+        ak.kh2[r] = h2;
+        return;
     }
     // general path: the line (collapse "" pairs of an unquoted field), then
     // duplicate_field(line, 0) in place, in the long area
@@ -374,14 +515,78 @@ __device__ void artist_key_of(const u8 *__restrict__ buf, const Win64 &w0, u64 b
 // (four dwordx4 loads) with the quote parity carried; a NUL ends the C string
 // the reference splits, so commas after it do not count.  The artist field
 // (<= 48 bytes) is trimmed and its pairs counted in the first window.
-__global__ __launch_bounds__(256) void k_rec_spans(const u8 *__restrict__ buf, const u64 *__restrict__ rec_start,
-                                                   const u32 *__restrict__ nulrel, u64 nrec, u64 first_rec,
-                                                   int want_text, u64 *__restrict__ alen, u64 *__restrict__ asrc,
-                                                   u32 *__restrict__ apairs, u64 *__restrict__ tlen,
-                                                   u64 *__restrict__ tsrc, u32 *__restrict__ tpairs,
-                                                   Counters *ctr, AKeys ak) {
-    const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= nrec) return;
+struct SpanOut {
+    u64 *alen, *asrc;
+    u32 *apairs;
+    u64 *tlen, *tsrc;
+    u32 *tpairs;
+};
+
+// Artist line span of record r = field 0 = [s, s + f0) (w0 = the 64-byte
+// window at s & ~15), and the artist key of the lines shortcut.
+__device__ __forceinline__ void rec_artist(const u8 *__restrict__ buf, const Win64 &w0, u64 s, u32 f0, u64 r,
+                                           const SpanOut &o, Counters *ctr, const AKeys &ak, bool no_key = false,
+                                           int ab = 0) {
+    const u64 b0 = s & ~15ull;
+    u64 as = s, ae = s + f0;
+    u32 pairs = 0;
+    if (f0 <= 48) {
+        const u32 o16 = (u32)(s & 15);
+        const u64 fm = bits_from(o16) & bits_below(o16 + f0);
+        const u64 nsp = fm & ~win_mask<0>(w0);
+        if (!nsp) {
+            ae = as;
+        } else {
+            const u32 a = (u32)__ffsll((long long)nsp) - 1, b = 63u - (u32)__clzll((long long)nsp);
+            const u64 Q = win_mask<1>(w0) & bits_from(a) & bits_below(b + 1);
+            if (!(b > a && ((Q >> a) & 1) && ((Q >> b) & 1))) {
+                pairs = quote_pairs(Q);
+                if (Q) atomicOr((unsigned long long *)&ctr->a_quoted, 1ull);
+            }
+            as = b0 + a;
+            ae = b0 + b + 1;
+        }
+    } else {
+        while (as < ae && c_space(buf[as])) ++as;
+        while (ae > as && c_space(buf[ae - 1])) --ae;
+        if (!(ae > as + 1 && buf[as] == '"' && buf[ae - 1] == '"') && field_has_quote(buf, as, ae - as)) {
+            bool anyq = false;
+            for (u64 i = as; i < ae; ++i) {
+                if (buf[i] != '"') continue;
+                anyq = true;
+                if (i + 1 < ae && buf[i + 1] == '"') { ++pairs; ++i; }
+            }
+            if (anyq) atomicOr((unsigned long long *)&ctr->a_quoted, 1ull);
+        }
+    }
+    o.alen[r] = (ae - as) - pairs + 1;
+    o.asrc[r] = as;
+    o.apairs[r] = pairs;
+    if (!no_key) artist_key_of(buf, w0, b0, as, ae, r, ak, ctr, ab);
+}
+
+__device__ __forceinline__ void rec_noline(u64 r, int want_text, const SpanOut &o, const AKeys &ak) {
+    o.alen[r] = 0;
+    ak.key_len[r] = 0;
+    if (want_text) o.tlen[r] = 0;
+}
+
+// Per record, the exact path: the first three commas (parse_csv_line,
+// parallel_spotify.c:258-304), then the spans of both column lines
+// (split_dataset_columns 699-714): line = duplicate_field(field, preserve=1)
+// + '\n'.  After the outer trim a quoted field -- every lyric of the real
+// corpus -- is copied raw; an unquoted one has its "" pairs collapsed and
+// needs no second trim (its first and last bytes are non-space and a
+// collapsed pair yields '"').  Outputs per record: line length (0 = no line:
+// the header, or a record parse_csv_line rejects), source offset, pairs.
+//
+// Commas: record-local (a record starts outside quotes), 64-byte windows
+// (four dwordx4 loads) with the quote parity carried; a NUL ends the C string
+// the reference splits, so commas after it do not count.  The artist field
+// (<= 48 bytes) is trimmed and its pairs counted in the first window.
+__device__ void rec_full(const u8 *__restrict__ buf, const u64 *__restrict__ rec_start,
+                         const u32 *__restrict__ nulrel, u64 r, u64 first_rec, int want_text, const SpanOut &o,
+                         Counters *ctr, const AKeys &ak) {
     const u64 s = rec_start[r], e = rec_start[r + 1];
     const u64 b0 = s & ~15ull;
     const Win64 w0 = load_win64(buf, s);
@@ -412,48 +617,10 @@ __global__ __launch_bounds__(256) void k_rec_spans(const u8 *__restrict__ buf, c
         if (nc >= 3 || Z) break;
     }
     if (r < first_rec || nc < 3) {
-        alen[r] = 0;
-        ak.key_len[r] = 0;
-        if (want_text) tlen[r] = 0;
+        rec_noline(r, want_text, o, ak);
         return;
     }
-    {  // artist: field 0 = [s, s + f0)
-        u64 as = s, ae = s + f0;
-        u32 pairs = 0;
-        if (f0 <= 48) {
-            const u32 o = (u32)(s & 15);
-            const u64 fm = bits_from(o) & bits_below(o + f0);
-            const u64 nsp = fm & ~win_mask<0>(w0);
-            if (!nsp) {
-                ae = as;
-            } else {
-                const u32 a = (u32)__ffsll((long long)nsp) - 1, b = 63u - (u32)__clzll((long long)nsp);
-                const u64 Q = win_mask<1>(w0) & bits_from(a) & bits_below(b + 1);
-                if (!(b > a && ((Q >> a) & 1) && ((Q >> b) & 1))) {
-                    pairs = quote_pairs(Q);
-                    if (Q) atomicOr((unsigned long long *)&ctr->a_quoted, 1ull);
-                }
-                as = b0 + a;
-                ae = b0 + b + 1;
-            }
-        } else {
-            while (as < ae && c_space(buf[as])) ++as;
-            while (ae > as && c_space(buf[ae - 1])) --ae;
-            if (!(ae > as + 1 && buf[as] == '"' && buf[ae - 1] == '"')) {
-                bool anyq = false;
-                for (u64 i = as; i < ae; ++i) {
-                    if (buf[i] != '"') continue;
-                    anyq = true;
-                    if (i + 1 < ae && buf[i + 1] == '"') { ++pairs; ++i; }
-                }
-                if (anyq) atomicOr((unsigned long long *)&ctr->a_quoted, 1ull);
-            }
-        }
-        alen[r] = (ae - as) - pairs + 1;
-        asrc[r] = as;
-        apairs[r] = pairs;
-        artist_key_of(buf, w0, b0, as, ae, r, ak, ctr);
-    }
+    rec_artist(buf, w0, s, f0, r, o, ctr, ak);
     if (want_text) {  // field 3: after the third comma up to the first NUL; the
                       // terminator is part of the record and trimmed as whitespace
         u64 ts = s + f3, te = e;
@@ -465,10 +632,75 @@ __global__ __launch_bounds__(256) void k_rec_spans(const u8 *__restrict__ buf, c
         if (!(te > ts + 1 && buf[ts] == '"' && buf[te - 1] == '"'))
             for (u64 i = ts; i + 1 < te; ++i)
                 if (buf[i] == '"' && buf[i + 1] == '"') { ++pairs; ++i; }
-        tlen[r] = (te - ts) - pairs + 1;
-        tsrc[r] = ts;
-        tpairs[r] = pairs;
+        o.tlen[r] = (te - ts) - pairs + 1;
+        o.tsrc[r] = ts;
+        o.tpairs[r] = pairs;
     }
+}
+
+// Thread per record, every record on the exact path (A/B runs with the
+// round-1 scan kernel, which records no spans).
+__global__ __launch_bounds__(256) void k_rec_spans(const u8 *__restrict__ buf, const u64 *__restrict__ rec_start,
+                                                   const u32 *__restrict__ nulrel, u64 nrec, u64 first_rec,
+                                                   int want_text, SpanOut o, Counters *ctr, AKeys ak) {
+    const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < nrec) rec_full(buf, rec_start, nulrel, r, first_rec, want_text, o, ctr, ak);
+}
+
+// Thread per record, from what K3 recorded (f0 / tss / tse): no comma search
+// and no reads at the record's end.  The common record -- field 3 opens with
+// a '"' right after its comma and the record's terminator follows a '"' --
+// has the text line [tss, tse) copied raw (duplicate_field keeps a quoted
+// field as is); the artist span comes from the record's first window.  Every
+// other record (unquoted or space-padded lyrics, a NUL, the unterminated last
+// record) is listed for k_rec_fix, the exact path.
+__global__ __launch_bounds__(256) void k_rec_fast(const u8 *__restrict__ buf, const u64 *__restrict__ rec_start,
+                                                  const u64 *__restrict__ f0p, const u64 *__restrict__ tss,
+                                                  const u64 *__restrict__ tse, u64 nrec, u64 first_rec,
+                                                  int want_text, SpanOut o, Counters *ctr, AKeys ak,
+                                                  u64 *__restrict__ fix, int ablate) {
+    const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nrec) return;
+    const u64 E = tse[r];
+    if (r < first_rec || (E & (SPAN_NOLINE | SPAN_NUL | SPAN_FIX)) == SPAN_NOLINE) {
+        rec_noline(r, want_text, o, ak);
+        return;
+    }
+    const u64 S = tss[r];
+    const u64 ts = S & SPAN_POS, te = E & SPAN_POS;
+    const bool quoted = (S & SPAN_Q) && (E & SPAN_Q) && te >= ts + 2;
+    if ((E & (SPAN_NUL | SPAN_FIX)) || (want_text && !quoted)) {
+        const u64 at = atomicAdd((unsigned long long *)&ctr->span_fix, 1ull);
+        fix[at] = r;
+        return;
+    }
+    const u64 s = rec_start[r];
+    // diagnostic ablations (results invalid): 256 no artist span, 512 no artist
+    // window / key, 1024 no artist key
+    if (ablate & 256) {
+        o.alen[r] = 0;
+    } else if (ablate & 512) {
+        o.alen[r] = f0p[r] - s + 1;
+        o.asrc[r] = s;
+        o.apairs[r] = 0;
+    } else {
+        const Win64 w0 = load_win64(buf, s);
+        rec_artist(buf, w0, s, (u32)(f0p[r] - s), r, o, ctr, ak, (ablate & 1024) != 0, ablate);
+    }
+    if (want_text) {
+        o.tlen[r] = te - ts + 1;
+        o.tsrc[r] = ts;
+        o.tpairs[r] = 0;
+    }
+}
+
+// The records k_rec_fast listed, on the exact path (count on the device).
+__global__ __launch_bounds__(256) void k_rec_fix(const u8 *__restrict__ buf, const u64 *__restrict__ rec_start,
+                                                 const u32 *__restrict__ nulrel, u64 first_rec, int want_text,
+                                                 SpanOut o, Counters *ctr, AKeys ak, const u64 *__restrict__ fix) {
+    const u64 n = *(volatile const u64 *)&ctr->span_fix;
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x)
+        rec_full(buf, rec_start, nulrel, fix[i], first_rec, want_text, o, ctr, ak);
 }
 
 // Segmented gather.  A workgroup owns 256 consecutive lines (their metadata
@@ -1513,10 +1745,19 @@ static inline dim3 grid1(u64 n, u32 t = 256) { return dim3((u32)((n + t - 1) / t
 
 hipError_t msa_launch_rec_spans(const u8 *buf, const u64 *rs, const u32 *nul, u64 nrec, u64 first_rec, int text,
                                 u64 *alen, u64 *asrc, u32 *apairs, u64 *tlen, u64 *tsrc, u32 *tpairs, Counters *ctr,
-                                const AKeys &ak, hipStream_t s) {
-    if (nrec)
-        hipLaunchKernelGGL(k_rec_spans, grid1(nrec), dim3(256), 0, s, buf, rs, nul, nrec, first_rec, text, alen, asrc,
-                           apairs, tlen, tsrc, tpairs, ctr, ak);
+                                const AKeys &ak, const u64 *f0, const u64 *tss, const u64 *tse, u64 *fix,
+                                int ablate, hipStream_t s) {
+    const SpanOut o{alen, asrc, apairs, tlen, tsrc, tpairs};
+    if (!nrec) return hipSuccess;
+    if (!f0) {
+        hipLaunchKernelGGL(k_rec_spans, grid1(nrec), dim3(256), 0, s, buf, rs, nul, nrec, first_rec, text, o, ctr, ak);
+        return hipGetLastError();
+    }
+    hipLaunchKernelGGL(k_rec_fast, grid1(nrec), dim3(256), 0, s, buf, rs, f0, tss, tse, nrec, first_rec, text, o, ctr,
+                       ak, fix, ablate);
+    // the listed records: a fixed grid, the count read on the device
+    const u64 fb = (nrec + 255) / 256 < 1024 ? (nrec + 255) / 256 : 1024;
+    hipLaunchKernelGGL(k_rec_fix, dim3((u32)fb), dim3(256), 0, s, buf, rs, nul, first_rec, text, o, ctr, ak, fix);
     return hipGetLastError();
 }
 // body_p: the column body length on the device (the offsets' scan total);

@@ -3,6 +3,7 @@ CPU oracle on the same inputs -- byte-identical word_counts.csv, top_artists.csv
 split column files and totals (reference semantics of `mpirun -np 1`,
 /root/reference/src/parallel_spotify.c)."""
 import os
+import random
 
 import pytest
 
@@ -92,6 +93,55 @@ EDGE = {
 @pytest.mark.parametrize("name", sorted(EDGE))
 def test_edge_cases(msa_mod, ctx, tmp_path, name):
     check_against_oracle(msa_mod, ctx, EDGE[name], tmp_path, name)
+
+
+def fuzz_fields(seed, n=4000):
+    """Records whose artist / lyric fields stress the column-span paths: quoted
+    names with "" pairs, padding spaces and tabs inside and outside the quotes,
+    names past 32 and 48 bytes, unquoted and space-padded lyrics, lyrics that
+    end right after a quote, records with fewer than four fields."""
+    rng = random.Random(seed)
+    bits = ["a", "Bo", "x y", '"', '""', " ", "  ", "\t", "Zed", "q", "0", "'", "é"]
+    out = ["artist,song,link,text\n"]
+    for i in range(n):
+        name = "".join(rng.choice(bits) for _ in range(rng.choice([0, 1, 2, 4, 8, 14, 22])))
+        r = rng.random()
+        if r < 0.6:
+            art = " " * rng.randint(0, 2) + '"' + name.replace('"', '""') + '"' + " " * rng.randint(0, 2)
+        elif r < 0.95:
+            art = name.replace('"', "").replace(",", "")
+        else:
+            art = name  # unquoted with quotes: the exact artist reader
+        words = " ".join(rng.choice(["love", "You", "don't", "la", "xx", "a", "Go!", "quoted\"s"])
+                         for _ in range(rng.randint(0, 9)))
+        t = rng.random()
+        if t < 0.5:
+            text = '"' + words.replace('"', '""') + '"'
+        elif t < 0.7:
+            text = " " * rng.randint(1, 3) + '"' + words.replace('"', '""') + '"' + " " * rng.randint(1, 3)
+        elif t < 0.85:
+            text = words.replace('"', "").replace(",", " ")
+        elif t < 0.95:
+            text = '"' + words.replace('"', '""') + '\n' + words.replace('"', "") + '"'
+        else:
+            text = '""'
+        if rng.random() < 0.03:
+            out.append(f"{art},s{i}\n")  # too few fields
+        else:
+            out.append(f"{art},s{i},/l/{i},{text}" + rng.choice(["\n", "\r\n", "\n"]))
+    return "".join(out).encode()
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3, 4])
+def test_fuzz_fields(msa_mod, ctx, tmp_path, seed):
+    check_against_oracle(msa_mod, ctx, fuzz_fields(seed), tmp_path, f"fuzz{seed}")
+
+
+def test_fuzz_fields_quote_free_artists(msa_mod, ctx, tmp_path):
+    """The same without unquoted quote-bearing names: the artist lines shortcut
+    stays on, so the in-register quoted-key path decides the artist table."""
+    data = b"\n".join(l for l in fuzz_fields(9).split(b"\n") if not (l[:1] != b'"' and b'"' in l.split(b",")[0]))
+    check_against_oracle(msa_mod, ctx, data, tmp_path, "fuzz_qf")
 
 
 def test_empty_file_fails_loudly(msa_mod, ctx):

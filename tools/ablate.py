@@ -29,5 +29,7 @@ for b in bits:
         mv, tw = C.c_uint64(), C.c_uint64()
         lib.msa_debug_stat(c.h, b"k3_misses", C.byref(mv))
         lib.msa_debug_stat(c.h, b"total_words", C.byref(tw))
-        print(f"ablate={b:2d} csv_scan={st.get('csv_scan')} ms  misses={mv.value} of {tw.value} words  all={st}",
+        fx = C.c_uint64()
+        lib.msa_debug_stat(c.h, b"span_fix", C.byref(fx))
+        print(f"ablate={b:2d} csv_scan={st.get('csv_scan')} ms  misses={mv.value} of {tw.value} words  span_fix={fx.value}  all={st}",
               flush=True)

@@ -23,7 +23,7 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(REPO, "music-analyst-ai_amd", "libmsa_hip.so")
-KERNELS = ["k_scan_csv", "k_miss_agg", "k_chunk_summary", "k_rec_spans", "k_col_gather", "k_col_lines",
+KERNELS = ["k_scan_csv", "k_miss_agg", "k_chunk_summary", "k_rec_spans", "k_rec_fast", "k_rec_fix", "k_col_gather", "k_col_lines",
            "k_artist_count", "k_tile_sort", "k_merge_pass"]
 PASSES = ["fetch", "write", "sq", "atomic"]
 
