@@ -28,7 +28,7 @@ hipError_t msa_launch_rec_spans(const u8 *, const u64 *, const u32 *, u64, u64, 
                                 u32 *, Counters *, const AKeys &, const u64 *, const u64 *, const u64 *, u64 *, int,
                                 hipStream_t);
 hipError_t msa_launch_artist_count(const u64 *, const u32 *, const u64 *, const u64 *, u64, u64 *, u64, u32 *, u64,
-                                   Counters *, int, hipStream_t);
+                                   Counters *, int, int, ulonglong2 *, u32 *, u32, hipStream_t);
 hipError_t msa_launch_first_end(const u8 *, u64, u32, u32, u64 *, hipStream_t);
 hipError_t msa_launch_artist_verify(const u8 *, const u64 *, const u32 *, const u64 *, u64, const u64 *, Counters *,
                                     hipStream_t);
@@ -40,7 +40,7 @@ hipError_t msa_launch_exp_write(const ExpSrc &, u64, u32, const u64 *, const u64
 hipError_t msa_launch_exp_ranked(const u64 *, const u64 *, const u8 *, u64, u64, u8 *, hipStream_t);
 hipError_t msa_launch_imp(const u8 *, const u64 *, u32, u64 *, u64, const ImpDst &, hipStream_t);
 hipError_t msa_launch_col_write(int, const u8 *, const u64 *, const u64 *, const u64 *, const u32 *, u64, u64,
-                                const u64 *, u8 *, hipStream_t);
+                                const u64 *, u8 *, const u8 *, const u64 *, const u32 *, hipStream_t);
 hipError_t msa_launch_artist_key(const u8 *, const u64 *, const u64 *, const u64 *, u64, u64, u8 *, u64 *, u32 *, u64 *,
                                  u64 *, u64, u32 *, u64, Counters *, u64, int, int, hipStream_t);
 hipError_t msa_launch_long(const u8 *, u64, const u8 *, u64, const u64 *, u64, u32 *, u64 *, u64 *, u64, u32 *, u64,
@@ -144,6 +144,7 @@ struct msa_ctx {
     DevBuf sums, carry, btot, bstate, small;  // small: Fn total + 2 States + ...
     // CSV records
     DevBuf rec_start, nulrel;  // rec_start[nrec] = end of the last record
+    DevBuf alog, alog_n;            // artist count flush logs (k_artist_merge)
     DevBuf f0, tss, tse, span_fix;  // K3's per-record span events (k_rec_fast), listed exact-path records
     bool spans = false;             // the last scan recorded f0 / tss / tse
     u64 nrec = 0, rec_cap = 0;
@@ -530,8 +531,11 @@ static int materialise_column(msa_ctx *c, bool text, const std::string &hdr_line
     HIPC(c, msa_exclusive_scan(lenb.as<u64>(), nrec, offb.as<u64>(), c->scan_bsum.as<u64>(), body_p, c->stream));
     HIPC(c, ensure(col, hdr_line.size() + c->n + 1 + MSA_INPUT_PAD));
     HIPC(c, hipMemcpyAsync(col.p, hdr_line.data(), hdr_line.size(), hipMemcpyHostToDevice, c->stream));
+    // the artist column reads lines equal to their keys from the arena k_rec_fast filled
+    const bool keys = !text && c->spans;
     HIPC(c, msa_launch_col_write(text ? 1 : 0, c->in, lenb.as<u64>(), offb.as<u64>(), srcb.as<u64>(), pairsb.as<u32>(),
-                                 nrec, hdr_line.size(), body_p, col.as<u8>(), c->stream));
+                                 nrec, hdr_line.size(), body_p, col.as<u8>(), keys ? c->arena.as<u8>() : nullptr,
+                                 c->key_off.as<u64>(), c->key_len.as<u32>(), c->stream));
     return MSA_OK;
 }
 
@@ -833,11 +837,19 @@ static int do_count(msa_ctx *c) {
         // the column lengths).  The split's a_quoted flag says whether the
         // shortcut held -- if not, start over with the exact reader.
         const u64 nrec = c->nrec;
+        // flush logs of the per-CU tables: (workgroup, 16 partitions) x cap
+        // entries of 32 B; a workgroup holds <= min(6144, its records) keys
+        const u64 wgs = std::max<u64>(1, std::min<u64>((nrec + 1023) / 1024, (u64)c->cus));  // k_artist_count's grid
+        const u64 per_wg = (nrec + wgs - 1) / wgs;
+        const u32 alog_cap = (u32)std::min<u64>(1024, std::max<u64>(64, per_wg / 8));
+        HIPC(c, ensure(c->alog, (size_t)c->cus * 16 * alog_cap * 32));
+        HIPC(c, ensure(c->alog_n, (size_t)c->cus * 16 * 4));
         for (int attempt = 0;; ++attempt) {
             prof_begin(c, ST_ARTIST_KEYS);
             HIPC(c, msa_launch_artist_count(c->alen.as<u64>(), c->key_len.as<u32>(), c->kh1.as<u64>(),
                                             c->kh2.as<u64>(), nrec, c->a_tab.as<u64>(), c->a_slots - 1,
                                             c->a_list.as<u32>(), c->a_slots / 2, c->ctr.as<Counters>(), c->cus,
+                                            c->ablate, c->alog.as<ulonglong2>(), c->alog_n.as<u32>(), alog_cap,
                                             c->stream));
             prof_end(c, ST_ARTIST_KEYS, nrec * 28);
             if (attempt == 0) {
@@ -1192,7 +1204,7 @@ void msa_destroy(msa_ctx *c) {
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     DevBuf *all[] = {&c->in_own, &c->sums, &c->carry, &c->btot, &c->bstate, &c->small, &c->rec_start, &c->extra, &c->exp_buf, &c->exp_meta, &c->imp_w, &c->imp_a, &c->imp_meta,
-                     &c->nulrel, &c->f0, &c->tss, &c->tse, &c->span_fix, &c->acol, &c->alen, &c->aoff, &c->asrc, &c->apairs, &c->tcol, &c->tlen, &c->toff, &c->tsrc, &c->tpairs,
+                     &c->nulrel, &c->f0, &c->tss, &c->tse, &c->span_fix, &c->alog, &c->alog_n, &c->acol, &c->alen, &c->aoff, &c->asrc, &c->apairs, &c->tcol, &c->tlen, &c->toff, &c->tsrc, &c->tpairs,
                      &c->scan_bsum, &c->scan_total, &c->ar_start, &c->arena, &c->key_off,
                      &c->key_len, &c->key_slot, &c->s_tab, &c->s_list, &c->m_tab, &c->m_list, &c->l_pos, &c->l_len,
                      &c->l_slot, &c->l_tab, &c->l_list, &c->a_tab, &c->a_list, &c->ctr, &c->kh1, &c->kh2, &c->mlog, &c->mlog_n, &c->sort_scratch, &c->blob_tot,

@@ -281,7 +281,7 @@ struct Counters {
     // artist pass then runs the exact record reader over artist.csv)
     u64 a_quoted;
     u64 a_long;      // bytes used in the long-key arena (k_rec_spans)
-    u64 k3_misses;   // K3 LDS-table misses logged for k_miss_agg (diagnostic)
+    u64 k3_misses;   // K3 log entries folded by k_miss_agg: LDS-table misses + flushed table entries (diagnostic)
     u64 col_body[2]; // artist.csv / text.csv body bytes (the line-offset scans' totals)
     u64 span_fix;    // records k_rec_fast hands to k_rec_fix (the exact per-record path)
     u64 pad;

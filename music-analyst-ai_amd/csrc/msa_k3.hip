@@ -229,6 +229,26 @@ __device__ __forceinline__ u32 mlog_part(u64 k0, u64 k1m) {
     return (u32)((k0 * 0xD6E8FEB86659FD93ull ^ k1m * 0x9E3779B97F4A7C15ull) >> 60);
 }
 
+// The workgroup's LDS table is flushed into the same logs at the end of the
+// scan (k_miss_agg then inserts each distinct key once per aggregating
+// workgroup, not once per scan workgroup): a flushed entry carries its count
+// (1..32767) in the bytes' free high bits -- bit 7 of every key byte (token
+// bytes are < 0x80) except KMARK.  A logged miss has none set: count 1.
+#define MLOG_CMAX 32767u
+__device__ __forceinline__ u64 spread8(u32 c) {  // bit j of c -> bit 8j + 7
+    u64 r = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r |= (u64)((c >> j) & 1u) << (8 * j + 7);
+    return r;
+}
+__device__ __forceinline__ u32 gather8(u64 x) {  // bit 8j + 7 -> bit j
+    u32 r = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r |= (u32)((x >> (8 * j + 7)) & 1u) << j;
+    return r;
+}
+#define MLOG_KEYBITS 0x7F7F7F7F7F7F7F7Full
+
 __device__ __forceinline__ void flush_miss(const ScanArgs &a, const ulonglong2 *miss, u32 n, u32 *lcur) {
     wsync();
     const u32 lane = lane_id();
@@ -562,19 +582,27 @@ __global__ __launch_bounds__(Q_T, 1) void k_scan_csv(ScanArgs a) {
         }
     }
     if (nmiss) flush_miss(a, miss, nmiss, lcur);
-    __syncthreads();
-    if (threadIdx.x < MSA_MLOG_PARTS)
-        a.mlog_n[blockIdx.x * MSA_MLOG_PARTS + threadIdx.x] = min(lcur[threadIdx.x], a.mlog_cap);
     words = wave_sum64(words);
     if (lane == 0 && words) atomicAdd((unsigned long long *)&a.ctr->total_words, (unsigned long long)words);
     __syncthreads();
-    for (u32 i = threadIdx.x; i < Q_SLOTS; i += Q_T) {
-        const u32 n = cnts[i];
-        if (n) {
-            const ulonglong2 kk = keys[i];
-            hbm_insert16(a, kk.x, kk.y, n);
+    // the LDS table into the logs, counts encoded (full partitions: HBM inserts)
+    for (u32 i = threadIdx.x; i < Q_SLOTS && !(a.ablate & 32768); i += Q_T) {  // 32768: no flush (diagnostic)
+        u32 n = cnts[i];
+        if (!n) continue;
+        const ulonglong2 kk = keys[i];
+        const u32 part = mlog_part(kk.x, kk.y);
+        const u64 base = ((u64)blockIdx.x * MSA_MLOG_PARTS + part) * a.mlog_cap;
+        while (n) {
+            const u32 c = min(n, MLOG_CMAX);
+            const u32 at = atomicAdd(&lcur[part], 1u);
+            if (at < a.mlog_cap) a.mlog[base + at] = make_ulonglong2(kk.x | spread8(c), kk.y | spread8(c >> 8));
+            else hbm_insert16(a, kk.x, kk.y, c);
+            n -= c;
         }
     }
+    __syncthreads();
+    if (threadIdx.x < MSA_MLOG_PARTS)
+        a.mlog_n[blockIdx.x * MSA_MLOG_PARTS + threadIdx.x] = min(lcur[threadIdx.x], a.mlog_cap);
 }
 
 // k_miss_agg: workgroup (partition p, group g) counts partition p of the
@@ -588,11 +616,10 @@ __device__ __forceinline__ u32 ma_find(ulonglong2 *keys, u64 k0, u64 k1) {
     h ^= h >> 15;
     h *= 0x2C1B3C6Du;
     u32 b = __umulhi(h, (u32)MA_NB);
-#if K3_ROT
-    const u32 ro = h & 3u;  // key-dependent first slot (bank spread, as lds_find16)
-#else
-    const u32 ro = 0;
-#endif
+    // the four slot reads start at a key-dependent slot: a ds_read_b128 lane
+    // group spreads over 16 positions of the bank row, not 4 (measured: the
+    // aggregation 0.22 -> 0.19 ms; in K3's table it did not pay)
+    const u32 ro = h & 3u;
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
         const u32 base = b * 4;
@@ -634,9 +661,11 @@ __global__ __launch_bounds__(MA_T) void k_miss_agg(ScanArgs a, u32 nsrc, u32 gro
         if (threadIdx.x == 0 && n) atomicAdd((unsigned long long *)&a.ctr->k3_misses, (unsigned long long)n);
         for (u32 i = threadIdx.x; i < n; i += MA_T) {
             const ulonglong2 x = a.mlog[base + i];
-            const u32 slot = ma_find(keys, x.x, x.y);
-            if (slot != ~0u) atomicAdd(&cnts[slot], 1u);
-            else hbm_insert16(a, x.x, x.y, 1);
+            const u32 c = gather8(x.x) | ((gather8(x.y) & 0x7Fu) << 8);
+            const u64 k0 = x.x & MLOG_KEYBITS, k1 = x.y & (MLOG_KEYBITS | KMARK);
+            const u32 slot = ma_find(keys, k0, k1);
+            if (slot != ~0u) atomicAdd(&cnts[slot], c ? c : 1u);
+            else hbm_insert16(a, k0, k1, c ? c : 1u);
         }
     }
     __syncthreads();

@@ -873,8 +873,19 @@ __global__ __launch_bounds__(CG_T) void k_col_gather(const u8 *__restrict__ buf,
 #define CL_T 256
 #define CL_LDS 16384
 template <typename P>
-__device__ __forceinline__ void put_line(P dst, const u8 *__restrict__ buf, u64 s, u64 len, u32 pairs) {
-    if (!pairs && (s & 15) + len <= 64) {
+__device__ __forceinline__ void put_line(P dst, const u8 *__restrict__ buf, u64 s, u64 len, u32 pairs,
+                                         const uint4 *__restrict__ key32 = nullptr) {
+    if (key32) {  // the line is the record's artist key: its 32-byte arena slot (dense, just written)
+        const uint4 x0 = key32[0], x1 = key32[1];
+        const u32 d[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+        for (u32 k = 0; k < 8; ++k) {
+            if (4 * k >= len) break;
+#pragma unroll
+            for (u32 b = 0; b < 4; ++b)
+                if (4 * k + b < len) dst[4 * k + b] = (u8)(d[k] >> (8 * b));
+        }
+    } else if (!pairs && (s & 15) + len <= 64) {
         const Win64 w = load_win64(buf, s);
         const u32 o = (u32)(s & 15);
         uint4 x0, x1, y0, y1;
@@ -904,7 +915,9 @@ __device__ __forceinline__ void put_line(P dst, const u8 *__restrict__ buf, u64 
 __global__ __launch_bounds__(CL_T) void k_col_lines(const u8 *__restrict__ buf, const u64 *__restrict__ line_len,
                                                     const u64 *__restrict__ line_off, const u64 *__restrict__ span_src,
                                                     const u32 *__restrict__ span_pairs, u64 nrec, u64 hdr,
-                                                    const u64 *__restrict__ body_p, u8 *__restrict__ col) {
+                                                    const u64 *__restrict__ body_p, u8 *__restrict__ col,
+                                                    const u8 *__restrict__ arena, const u64 *__restrict__ key_off,
+                                                    const u32 *__restrict__ key_len) {
     const u64 body = *body_p;
     __shared__ __attribute__((aligned(16))) u8 st[CL_LDS];
     const u64 r0 = (u64)blockIdx.x * CL_T;
@@ -919,8 +932,12 @@ __global__ __launch_bounds__(CL_T) void k_col_lines(const u8 *__restrict__ buf, 
     if (r < nrec) {
         const u64 L = line_len[r];
         if (L) {
-            if (staged) put_line(st + lead + (line_off[r] - B0), buf, span_src[r], L - 1, span_pairs[r]);
-            else put_line(col + hdr + line_off[r], buf, span_src[r], L - 1, span_pairs[r]);
+            // an artist line equal to its key (same length: nothing stripped,
+            // nothing collapsed) is read from the key's arena slot
+            const uint4 *k32 = (arena && key_off[r] == 32 * r && (u64)key_len[r] + 1 == L)
+                                   ? reinterpret_cast<const uint4 *>(arena + 32 * r) : nullptr;
+            if (staged) put_line(st + lead + (line_off[r] - B0), buf, span_src[r], L - 1, span_pairs[r], k32);
+            else put_line(col + hdr + line_off[r], buf, span_src[r], L - 1, span_pairs[r], k32);
         }
     }
     if (!staged) return;
@@ -1202,13 +1219,16 @@ __global__ __launch_bounds__(AK_T) void k_artist_key(const u8 *__restrict__ col,
 // silently (k_artist_h2_check does the same for the HBM table).
 #define AC_T 1024
 #define AC_SLOTS 6144
+#define AC_PARTS 16       // hash partitions of the flush logs (k_artist_merge)
 #define AC_NB (AC_SLOTS / 4)
 static_assert(AC_SLOTS * 24 + 16 <= 160 * 1024, "artist count LDS exceeds the CU");
 
 __global__ __launch_bounds__(AC_T) void k_artist_count(const u64 *__restrict__ line_len,
                                                        const u32 *__restrict__ key_len, const u64 *__restrict__ kh1,
                                                        const u64 *__restrict__ kh2, u64 nrec, u64 *atab, u64 amask,
-                                                       u32 *alist, u64 alist_cap, Counters *ctr) {
+                                                       u32 *alist, u64 alist_cap, Counters *ctr, int ablate,
+                                                       ulonglong2 *__restrict__ alog, u32 *__restrict__ alog_n,
+                                                       u32 alog_cap) {
     __shared__ u64 lh[AC_SLOTS];
     __shared__ u64 lsum[AC_SLOTS];
     __shared__ u32 lc[AC_SLOTS];
@@ -1259,17 +1279,71 @@ __global__ __launch_bounds__(AC_T) void k_artist_count(const u64 *__restrict__ l
     if (songs) atomicAdd(&songs_wg, songs);
     __syncthreads();
     if (threadIdx.x == 0 && songs_wg) atomicAdd((unsigned long long *)&ctr->songs, (unsigned long long)songs_wg);
-    // flush, each workgroup starting at its own offset in the slot array
-    const u32 rot = (u32)(((u64)blockIdx.x * AC_SLOTS) / gridDim.x);
-    for (u32 t = threadIdx.x; t < AC_SLOTS; t += AC_T) {
-        u32 i = t + rot;
-        if (i >= AC_SLOTS) i -= AC_SLOTS;
+    // flush: every workgroup holds the Zipf head of the artists, so the entries
+    // go to per-(workgroup, hash partition) logs and k_artist_merge inserts
+    // each distinct key once per merging workgroup (a full log partition:
+    // straight to HBM)
+    __shared__ u32 lcur[AC_PARTS];
+    if (threadIdx.x < AC_PARTS) lcur[threadIdx.x] = 0;
+    __syncthreads();
+    for (u32 i = threadIdx.x; i < AC_SLOTS && !(ablate & 65536); i += AC_T) {  // 65536: no flush (diagnostic)
         const u32 cnt = lc[i];
         if (!cnt) continue;
         const u64 rep = r0 + lrep[i];
         if (lsum[i] != (u64)cnt * kh2[rep]) atomicAdd((unsigned long long *)&ctr->collision, 1ull);
-        h_insert2(atab, amask, lh[i], cnt, rep, lsum[i], alist, alist_cap, &ctr->a_claimed, ctr, OVF_A);
+        const u32 part = (u32)(lh[i] >> 60) & (AC_PARTS - 1);
+        const u32 at = atomicAdd(&lcur[part], 1u);
+        if (at < alog_cap) {
+            ulonglong2 *e = alog + 2 * (((u64)blockIdx.x * AC_PARTS + part) * alog_cap + at);
+            e[0] = make_ulonglong2(lh[i], (u64)cnt);
+            e[1] = make_ulonglong2(lsum[i], rep);
+        } else {
+            h_insert2(atab, amask, lh[i], cnt, rep, lsum[i], alist, alist_cap, &ctr->a_claimed, ctr, OVF_A);
+        }
     }
+    __syncthreads();
+    if (threadIdx.x < AC_PARTS) alog_n[blockIdx.x * AC_PARTS + threadIdx.x] = min(lcur[threadIdx.x], alog_cap);
+}
+
+// Workgroup (partition p, group g) folds partition p of the artist logs of
+// count workgroups g, g + G, ... in LDS (counts and h2 sums added, the lowest
+// representative kept), then adds each distinct hash to the HBM table once.
+#define AM_T 1024
+#define AM_SLOTS 4096
+__global__ __launch_bounds__(AM_T) void k_artist_merge(const ulonglong2 *__restrict__ alog,
+                                                       const u32 *__restrict__ alog_n, u32 alog_cap, u32 nsrc,
+                                                       u32 groups, u64 *atab, u64 amask, u32 *alist, u64 alist_cap,
+                                                       Counters *ctr) {
+    __shared__ u64 mh[AM_SLOTS], mc[AM_SLOTS], ms[AM_SLOTS], mr[AM_SLOTS];
+    for (u32 i = threadIdx.x; i < AM_SLOTS; i += AM_T) { mh[i] = 0; mc[i] = 0; ms[i] = 0; mr[i] = ~0ull; }
+    __syncthreads();
+    const u32 part = blockIdx.x % AC_PARTS, g = blockIdx.x / AC_PARTS;
+    for (u32 src = g; src < nsrc; src += groups) {
+        const u32 n = alog_n[src * AC_PARTS + part];
+        const ulonglong2 *e = alog + 2 * ((u64)src * AC_PARTS + part) * alog_cap;
+        for (u32 i = threadIdx.x; i < n; i += AM_T) {
+            const ulonglong2 x = e[2 * i], y = e[2 * i + 1];  // (hash, count), (h2 sum, representative)
+            u32 b = (u32)((x.x * 0x9E3779B97F4A7C15ull) >> 52) & (AM_SLOTS - 1);
+            bool done = false;
+            for (u32 p = 0; p < 64 && !done; ++p, b = (b + 1) & (AM_SLOTS - 1)) {
+                u64 cur = mh[b];
+                if (cur == 0) {
+                    const u64 old = atomicCAS((unsigned long long *)&mh[b], 0ull, (unsigned long long)x.x);
+                    cur = old ? old : x.x;
+                }
+                if (cur == x.x) {
+                    atomicAdd((unsigned long long *)&mc[b], (unsigned long long)x.y);
+                    atomicAdd((unsigned long long *)&ms[b], (unsigned long long)y.x);
+                    atomicMin((unsigned long long *)&mr[b], (unsigned long long)y.y);
+                    done = true;
+                }
+            }
+            if (!done) h_insert2(atab, amask, x.x, x.y, y.y, y.x, alist, alist_cap, &ctr->a_claimed, ctr, OVF_A);
+        }
+    }
+    __syncthreads();
+    for (u32 i = threadIdx.x; i < AM_SLOTS; i += AM_T)
+        if (mc[i]) h_insert2(atab, amask, mh[i], mc[i], mr[i], ms[i], alist, alist_cap, &ctr->a_claimed, ctr, OVF_A);
 }
 
 // Every HBM artist entry: sum of h2 == count x h2(representative).
@@ -1767,12 +1841,13 @@ __global__ void k_zero_tail(u8 *__restrict__ col, u64 hdr, const u64 *__restrict
     for (u32 k = threadIdx.x; k < pad; k += blockDim.x) col[at + k] = 0;
 }
 hipError_t msa_launch_col_write(int text, const u8 *buf, const u64 *len, const u64 *off, const u64 *src,
-                                const u32 *pairs, u64 nrec, u64 hdr, const u64 *body_p, u8 *col, hipStream_t s) {
+                                const u32 *pairs, u64 nrec, u64 hdr, const u64 *body_p, u8 *col, const u8 *arena,
+                                const u64 *key_off, const u32 *key_len, hipStream_t s) {
     hipLaunchKernelGGL(k_zero_tail, dim3(1), dim3(256), 0, s, col, hdr, body_p, (u32)MSA_INPUT_PAD);
     if (!nrec) return hipGetLastError();
     if (!text) {
         hipLaunchKernelGGL(k_col_lines, dim3((u32)((nrec + CL_T - 1) / CL_T)), dim3(CL_T), 0, s, buf, len, off, src,
-                           pairs, nrec, hdr, body_p, col);
+                           pairs, nrec, hdr, body_p, col, arena, key_off, key_len);
         return hipGetLastError();
     }
     const u64 groups = (nrec + CG_T - 1) / CG_T;
@@ -1803,12 +1878,17 @@ hipError_t msa_launch_artist_key(const u8 *col, const u64 *ar_start, const u64 *
 }
 hipError_t msa_launch_artist_count(const u64 *line_len, const u32 *key_len, const u64 *kh1, const u64 *kh2, u64 nrec,
                                    u64 *atab, u64 amask, u32 *alist, u64 alist_cap, Counters *ctr, int cus,
-                                   hipStream_t s) {
+                                   int ablate, ulonglong2 *alog, u32 *alog_n, u32 alog_cap, hipStream_t s) {
     if (nrec) {
         u64 blocks = (nrec + AC_T - 1) / AC_T;
         if (blocks > (u64)cus) blocks = (u64)cus;
         hipLaunchKernelGGL(k_artist_count, dim3((u32)blocks), dim3(AC_T), 0, s, line_len, key_len, kh1, kh2, nrec, atab,
-                           amask, alist, alist_cap, ctr);
+                           amask, alist, alist_cap, ctr, ablate, alog, alog_n, alog_cap);
+        u32 groups = (u32)cus / AC_PARTS;
+        if (groups > (u32)blocks) groups = (u32)blocks;
+        if (groups < 1) groups = 1;
+        hipLaunchKernelGGL(k_artist_merge, dim3(groups * AC_PARTS), dim3(AM_T), 0, s, (const ulonglong2 *)alog,
+                           (const u32 *)alog_n, alog_cap, (u32)blocks, groups, atab, amask, alist, alist_cap, ctr);
         hipLaunchKernelGGL(k_artist_h2_check, grid1(alist_cap), dim3(256), 0, s, (const u64 *)atab, (const u32 *)alist,
                            alist_cap, kh2, ctr);
     }
