@@ -24,6 +24,8 @@ hipError_t msa_launch_scan(const ScanArgs &, int, hipStream_t);
 hipError_t msa_launch_scan_csv(const ScanArgs &, hipStream_t);
 hipError_t msa_launch_miss_agg(const ScanArgs &, hipStream_t);
 hipError_t msa_exclusive_scan(const u64 *, u64, u64 *, u64 *, u64 *, hipStream_t);
+hipError_t msa_exclusive_scan2(const u64 *, u64, u64 *, u64 *, u64 *, const u64 *, u64, u64 *, u64 *, u64 *,
+                               hipStream_t);
 hipError_t msa_launch_rec_spans(const u8 *, const u64 *, const u32 *, u64, u64, int, u64 *, u64 *, u32 *, u64 *, u64 *,
                                 u32 *, Counters *, const AKeys &, const u64 *, const u64 *, const u64 *, u64 *, int,
                                 hipStream_t);
@@ -521,14 +523,26 @@ static int reset_artist_table(msa_ctx *c) {
 // at most as long as its record, so header + input bytes bound the column;
 // the length lands in Counters::col_body[text] and reaches the host with the
 // next counter read-back (col_lens_pending).
+// Line offsets of both columns: one scan launch sequence over both length
+// arrays (the bodies' totals stay on the device, Counters::col_body).
+static int scan_columns(msa_ctx *c, bool text) {
+    const u64 nrec = c->nrec;
+    const u64 nbb = (nrec + 1023) / 1024 + 1;
+    HIPC(c, ensure(c->aoff, nrec * 8));
+    if (text) HIPC(c, ensure(c->toff, nrec * 8));
+    HIPC(c, ensure(c->scan_bsum, 2 * nbb * 8));
+    u64 *body = c->ctr.as<Counters>()->col_body;
+    u64 *bs = c->scan_bsum.as<u64>();
+    HIPC(c, msa_exclusive_scan2(c->alen.as<u64>(), nrec, c->aoff.as<u64>(), bs, &body[0],
+                                text ? c->tlen.as<u64>() : nullptr, nrec, c->toff.as<u64>(), bs + nbb, &body[1],
+                                c->stream));
+    return MSA_OK;
+}
+
 static int materialise_column(msa_ctx *c, bool text, const std::string &hdr_line, DevBuf &col, DevBuf &lenb,
                               DevBuf &offb, DevBuf &srcb, DevBuf &pairsb) {
     const u64 nrec = c->nrec;
-    HIPC(c, ensure(offb, nrec * 8));
-    HIPC(c, ensure(c->scan_bsum, ((nrec + 1023) / 1024 + 1) * 8));
-    HIPC(c, ensure(c->scan_total, 64));
-    u64 *body_p = &c->ctr.as<Counters>()->col_body[text ? 1 : 0];
-    HIPC(c, msa_exclusive_scan(lenb.as<u64>(), nrec, offb.as<u64>(), c->scan_bsum.as<u64>(), body_p, c->stream));
+    u64 *body_p = &c->ctr.as<Counters>()->col_body[text ? 1 : 0];  // from scan_columns
     HIPC(c, ensure(col, hdr_line.size() + c->n + 1 + MSA_INPUT_PAD));
     HIPC(c, hipMemcpyAsync(col.p, hdr_line.data(), hdr_line.size(), hipMemcpyHostToDevice, c->stream));
     // the artist column reads lines equal to their keys from the arena k_rec_fast filled
@@ -581,6 +595,7 @@ static int split_columns_rest(msa_ctx *c, bool want_text, const std::string &ah,
                                  c->tlen.as<u64>(), c->tsrc.as<u64>(), c->tpairs.as<u32>(), c->ctr.as<Counters>(), ak,
                                  c->spans ? c->f0.as<u64>() : nullptr, c->tss.as<u64>(), c->tse.as<u64>(),
                                  c->span_fix.as<u64>(), c->ablate, c->stream));
+    if ((rc = scan_columns(c, want_text))) return rc;
     if ((rc = materialise_column(c, false, ah, c->acol, c->alen, c->aoff, c->asrc, c->apairs))) return rc;
     prof_end(c, ST_ARTIST_COLUMN, c->nrec * 16 * 2 + c->nrec * 32);  // ~16-byte artist lines
     // compute_header_length (parallel_spotify.c:444-459): getline's end

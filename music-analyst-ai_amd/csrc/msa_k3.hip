@@ -288,6 +288,12 @@ __global__ __launch_bounds__(Q_T, 1) void k_scan_csv(ScanArgs a) {
     const u32 nw = gridDim.x * Q_W;
     u64 words = 0;
 
+    // a chunk's first block is loaded during the previous chunk's last block
+    uint4 cur[4];
+    if (gw < a.nchunks) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) cur[q] = ldg16(a.buf + a.seg_begin + (u64)gw * MSA_CHUNK + lane * 64 + 16 * q);
+    }
     for (u32 c = gw; c < a.nchunks; c += nw) {
         State st = a.carry[c];
         // K1 saw no '\r' / NUL in this chunk: their masks stay empty
@@ -301,9 +307,6 @@ __global__ __launch_bounds__(Q_T, 1) void k_scan_csv(ScanArgs a) {
             prevT = (u32)(((b | 0x20u) >= 'a' && (b | 0x20u) <= 'z') || (b >= '0' && b <= '9') || b == '\'');
             prevQ = (u32)(b == '"');
         }
-        uint4 cur[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) cur[q] = ldg16(a.buf + cbase + lane * 64 + 16 * q);
 
         for (u64 ib = cbase; ib < cend; ib += Q_BLK) {
             const u64 lpos = ib + lane * 64;
@@ -326,6 +329,10 @@ __global__ __launch_bounds__(Q_T, 1) void k_scan_csv(ScanArgs a) {
             if (more) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q) cur[q] = ldg16(a.buf + lpos + Q_BLK + 16 * q);
+            } else if (c + nw < a.nchunks) {  // the wave's next chunk
+                const u64 nb = a.seg_begin + (u64)(c + nw) * MSA_CHUNK + lane * 64;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) cur[q] = ldg16(a.buf + nb + 16 * q);
             }
 
             // ---- record structure (read_csv_record + parse_csv_line) ----

@@ -7,6 +7,8 @@
 //     LDS, then merge passes by rank -- with an exact strcmp fix-up of the
 //     rare equal-prefix runs: the order of entry_compare_desc (178-188)
 //   * generic exclusive scan (u64)
+#include <algorithm>
+
 #include "msa_hip.h"
 #include "msa_internal.h"
 #include "msa_tables.h"
@@ -20,18 +22,31 @@ __device__ __forceinline__ u64 bswap64(u64 x) { return __builtin_bswap64(x); }
 }  // namespace
 
 // ---------------------------------------------------------------------------
-// generic exclusive scan over u64 (3 phases)
+// generic exclusive scan over u64 (3 phases), for up to two arrays at once
+// (blockIdx.y picks the array: both column line-length arrays in one launch
+// sequence)
 #define SCAN_T 256
 #define SCAN_PER 4
 #define SCAN_TILE (SCAN_T * SCAN_PER)
 
-__global__ __launch_bounds__(SCAN_T) void k_scan_reduce(const u64 *__restrict__ in, u64 n, u64 *__restrict__ bsum) {
+struct ScanJob {
+    const u64 *in;
+    u64 *out, *bsum, *total;
+    u64 n;
+};
+struct ScanJobs {
+    ScanJob j[2];
+};
+
+__global__ __launch_bounds__(SCAN_T) void k_scan_reduce(ScanJobs js) {
+    const ScanJob &J = js.j[blockIdx.y];
     __shared__ u64 red[SCAN_T / 64];
     const u64 base = (u64)blockIdx.x * SCAN_TILE;
+    if (base >= J.n) return;
     u64 s = 0;
     for (int i = 0; i < SCAN_PER; ++i) {
         const u64 idx = base + (u64)i * SCAN_T + threadIdx.x;
-        if (idx < n) s += in[idx];
+        if (idx < J.n) s += J.in[idx];
     }
     s = wave_sum64(s);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
@@ -39,38 +54,46 @@ __global__ __launch_bounds__(SCAN_T) void k_scan_reduce(const u64 *__restrict__ 
     if (threadIdx.x == 0) {
         u64 t = 0;
         for (int w = 0; w < SCAN_T / 64; ++w) t += red[w];
-        bsum[blockIdx.x] = t;
+        J.bsum[blockIdx.x] = t;
     }
 }
 
-__global__ __launch_bounds__(SCAN_T) void k_scan_top(u64 *__restrict__ bsum, u64 nb, u64 *__restrict__ total) {
-    __shared__ u64 part[SCAN_T];
+// exclusive scan of the block sums in place: per-thread runs, then a block
+// scan of the run totals (wave shuffles + wave totals)
+__global__ __launch_bounds__(SCAN_T) void k_scan_top(ScanJobs js) {
+    const ScanJob &J = js.j[blockIdx.y];
+    if (!J.n) return;
+    __shared__ u64 wtot[SCAN_T / 64];
+    const u64 nb = (J.n + SCAN_TILE - 1) / SCAN_TILE;
     const u64 per = (nb + SCAN_T - 1) / SCAN_T;
     const u64 a = min(nb, (u64)threadIdx.x * per), b = min(nb, a + per);
     u64 s = 0;
-    for (u64 i = a; i < b; ++i) s += bsum[i];
-    part[threadIdx.x] = s;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        u64 acc = 0;
-        for (int i = 0; i < SCAN_T; ++i) { u64 v = part[i]; part[i] = acc; acc += v; }
-        if (total) *total = acc;
+    for (u64 i = a; i < b; ++i) s += J.bsum[i];
+    const u32 lane = lane_id(), w = threadIdx.x >> 6;
+    u64 x = s;  // inclusive wave scan
+    for (int o = 1; o < 64; o <<= 1) {
+        const u64 y = __shfl_up(x, o);
+        if (lane >= (u32)o) x += y;
     }
+    if (lane == 63) wtot[w] = x;
     __syncthreads();
-    u64 acc = part[threadIdx.x];
-    for (u64 i = a; i < b; ++i) { u64 v = bsum[i]; bsum[i] = acc; acc += v; }
+    u64 acc = x - s;
+    for (u32 i = 0; i < w; ++i) acc += wtot[i];
+    if (threadIdx.x == SCAN_T - 1 && J.total) *J.total = acc + s;
+    for (u64 i = a; i < b; ++i) { const u64 v = J.bsum[i]; J.bsum[i] = acc; acc += v; }
 }
 
-__global__ __launch_bounds__(SCAN_T) void k_scan_down(const u64 *__restrict__ in, u64 n, const u64 *__restrict__ bsum,
-                                                     u64 *__restrict__ out) {
+__global__ __launch_bounds__(SCAN_T) void k_scan_down(ScanJobs js) {
+    const ScanJob &J = js.j[blockIdx.y];
     __shared__ u64 wsum[SCAN_T / 64];
     const u64 base = (u64)blockIdx.x * SCAN_TILE;
+    if (base >= J.n) return;
     const u32 lane = lane_id(), w = threadIdx.x >> 6;
     // thread t owns elements base + t*SCAN_PER .. +SCAN_PER (blocked)
     u64 v[SCAN_PER], s = 0;
     for (int i = 0; i < SCAN_PER; ++i) {
         const u64 idx = base + (u64)threadIdx.x * SCAN_PER + i;
-        v[i] = idx < n ? in[idx] : 0;
+        v[i] = idx < J.n ? J.in[idx] : 0;
         s += v[i];
     }
     // inclusive wave scan of s
@@ -81,26 +104,39 @@ __global__ __launch_bounds__(SCAN_T) void k_scan_down(const u64 *__restrict__ in
     }
     if (lane == 63) wsum[w] = x;
     __syncthreads();
-    u64 pre = bsum[blockIdx.x];
+    u64 pre = J.bsum[blockIdx.x];
     for (u32 i = 0; i < w; ++i) pre += wsum[i];
     pre += x - s;
     for (int i = 0; i < SCAN_PER; ++i) {
         const u64 idx = base + (u64)threadIdx.x * SCAN_PER + i;
-        if (idx < n) out[idx] = pre;
+        if (idx < J.n) J.out[idx] = pre;
         pre += v[i];
     }
 }
 
-hipError_t msa_exclusive_scan(const u64 *in, u64 n, u64 *out, u64 *bsum_scratch, u64 *total, hipStream_t s) {
-    if (n == 0) {
-        if (total) return hipMemsetAsync(total, 0, sizeof(u64), s);
-        return hipSuccess;
-    }
-    const u64 nb = (n + SCAN_TILE - 1) / SCAN_TILE;
-    hipLaunchKernelGGL(k_scan_reduce, dim3((u32)nb), dim3(SCAN_T), 0, s, in, n, bsum_scratch);
-    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(SCAN_T), 0, s, bsum_scratch, nb, total);
-    hipLaunchKernelGGL(k_scan_down, dim3((u32)nb), dim3(SCAN_T), 0, s, in, n, bsum_scratch, out);
+// Exclusive scans of one or two u64 arrays (in2 null: one), totals to the
+// device; bsum scratch: (n + 1023) / 1024 entries per array.
+hipError_t msa_exclusive_scan2(const u64 *in, u64 n, u64 *out, u64 *bsum, u64 *total, const u64 *in2, u64 n2,
+                               u64 *out2, u64 *bsum2, u64 *total2, hipStream_t s) {
+    ScanJobs js{};
+    js.j[0] = ScanJob{in, out, bsum, total, n};
+    js.j[1] = ScanJob{in2, out2, bsum2, total2, in2 ? n2 : 0};
+    const u32 ny = in2 ? 2 : 1;
+    for (u32 k = 0; k < ny; ++k)
+        if (js.j[k].n == 0 && js.j[k].total) {
+            hipError_t e = hipMemsetAsync(js.j[k].total, 0, sizeof(u64), s);
+            if (e != hipSuccess) return e;
+        }
+    const u64 nmax = std::max(js.j[0].n, js.j[1].n);
+    if (nmax == 0) return hipSuccess;
+    const u64 nb = (nmax + SCAN_TILE - 1) / SCAN_TILE;
+    hipLaunchKernelGGL(k_scan_reduce, dim3((u32)nb, ny), dim3(SCAN_T), 0, s, js);
+    hipLaunchKernelGGL(k_scan_top, dim3(1, ny), dim3(SCAN_T), 0, s, js);
+    hipLaunchKernelGGL(k_scan_down, dim3((u32)nb, ny), dim3(SCAN_T), 0, s, js);
     return hipGetLastError();
+}
+hipError_t msa_exclusive_scan(const u64 *in, u64 n, u64 *out, u64 *bsum_scratch, u64 *total, hipStream_t s) {
+    return msa_exclusive_scan2(in, n, out, bsum_scratch, total, nullptr, 0, nullptr, nullptr, nullptr, s);
 }
 
 // ---------------------------------------------------------------------------
@@ -780,7 +816,7 @@ __global__ __launch_bounds__(CG_T) void k_col_gather(const u8 *__restrict__ buf,
     // slots in batches of CG_B per thread: every single-line slot's loads of
     // the batch are issued before the first store (memory-level parallelism)
 #ifndef CG_B
-#define CG_B 4
+#define CG_B 2
 #endif
     for (u64 s0 = t; s0 < nslots; s0 += (u64)CG_B * CG_T) {
         uint4 va[CG_B];

@@ -128,21 +128,28 @@ __global__ __launch_bounds__(256) void k_chunk_summary(const u8 *__restrict__ bu
     const u32 lane = lane_id();
     const u32 gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const u32 nw = (gridDim.x * blockDim.x) >> 6;
+    uint4 cur[4];  // a chunk's first block: loaded during the previous chunk's last one
+    if (gw < nchunks) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) cur[q] = ld16(buf + seg_begin + (u64)gw * MSA_CHUNK + lane * 64 + 16 * q);
+    }
     for (u32 c = gw; c < nchunks; c += nw) {
         const u64 cbase = seg_begin + (u64)c * MSA_CHUNK;
         const u64 cend = min(cbase + (u64)MSA_CHUNK, seg_end);
         u32 par = 0, first_nl = 0, anyrare = 0;
         u32 cr[2] = {0, 0}, nterm[2] = {0, 0}, cc[2] = {0, 0}, zz[2] = {0, 0}, lend[2] = {0, 0};
-        uint4 cur[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) cur[q] = ld16(buf + cbase + lane * 64 + 16 * q);
         for (u64 ibase = cbase; ibase < cend; ibase += K1_ITER) {
             const u64 lpos = ibase + lane * 64;
-            // one iteration ahead, only inside the chunk: reads end < cend + 4096 (MSA_INPUT_PAD)
+            // one iteration ahead: the chunk's next block, else the wave's next
+            // chunk (reads end < cend + 4096, MSA_INPUT_PAD)
             uint4 nxt[4] = {cur[0], cur[1], cur[2], cur[3]};
             if (ibase + K1_ITER < cend) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q) nxt[q] = ld16(buf + lpos + K1_ITER + 16 * q);
+            } else if (c + nw < nchunks) {
+                const u64 nb = seg_begin + (u64)(c + nw) * MSA_CHUNK + lane * 64;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) nxt[q] = ld16(buf + nb + 16 * q);
             }
             const Classes64 k = classify64(cur, lpos, cend);
             anyrare |= k.rare ? 1u : 0u;
@@ -243,29 +250,42 @@ __global__ __launch_bounds__(FN_T) void k_fn_reduce(const ChunkSum *__restrict__
 __global__ __launch_bounds__(FN_T) void k_fn_top(const Fn *__restrict__ btot, u32 nb, u64 seg_begin,
                                                  const State *__restrict__ init, State *__restrict__ bstate,
                                                  Fn *__restrict__ total) {
+    // tiles of FN_T block totals: an inclusive scan in LDS per tile (as
+    // k_fn_down), the state carried from tile to tile -- one element per
+    // thread, no per-thread serial composition (that one lived in scratch)
     __shared__ Fn sh[2][FN_T];
+    __shared__ State carry_s;
+    __shared__ Fn tot_s;
     const u32 t = threadIdx.x;
-    const u32 per = (nb + FN_T - 1) / FN_T;
-    const u32 a = min(nb, t * per), b = min(nb, a + per);
-    Fn f = fn_identity(seg_begin);
-    for (u32 i = a; i < b; ++i) f = fn_compose(f, btot[i]);
-    sh[0][t] = f;
-    __syncthreads();
-    u32 cur = 0;
-    for (u32 off = 1; off < FN_T; off <<= 1) {  // inclusive scan of the runs, ping-pong buffers
-        Fn g = sh[cur][t];
-        if (t >= off) g = fn_compose(sh[cur][t - off], g);
-        sh[cur ^ 1][t] = g;
-        cur ^= 1;
+    if (t == 0) {
+        carry_s = *init;
+        tot_s = fn_identity(seg_begin);
+    }
+    for (u32 base = 0; base < nb; base += FN_T) {
+        const u32 i = base + t;
+        sh[0][t] = i < nb ? btot[i] : fn_identity(seg_begin);
+        __syncthreads();
+        u32 cur = 0;
+        for (u32 off = 1; off < FN_T; off <<= 1) {  // inclusive scan, ping-pong buffers
+            const u32 src = (t >= off) ? t - off : t;
+            Fn g = fn_compose(sh[cur][src], sh[cur][t]);
+            if (t < off) g = sh[cur][t];
+            sh[cur ^ 1][t] = g;
+            cur ^= 1;
+            __syncthreads();
+        }
+        const State s0 = carry_s;
+        State s = s0;
+        if (t > 0) s = fn_apply(s0, sh[cur][t - 1]);
+        if (i < nb) bstate[i] = s;
+        __syncthreads();  // every thread has read carry_s
+        if (t == FN_T - 1) {
+            carry_s = fn_apply(s0, sh[cur][t]);
+            if (total) tot_s = fn_compose(tot_s, sh[cur][t]);
+        }
         __syncthreads();
     }
-    State s = *init;
-    if (t > 0) s = fn_apply(s, sh[cur][t - 1]);
-    if (t == FN_T - 1 && total) *total = sh[cur][t];
-    for (u32 i = a; i < b; ++i) {
-        bstate[i] = s;
-        s = fn_apply(s, btot[i]);
-    }
+    if (t == 0 && total) *total = tot_s;
 }
 
 __global__ __launch_bounds__(FN_T) void k_fn_down(const ChunkSum *__restrict__ sums, u64 seg_begin, u32 nchunks,
