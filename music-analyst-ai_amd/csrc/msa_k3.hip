@@ -37,14 +37,33 @@ namespace {
 #define Q_LIST 1024              // token entries per wave-iteration (>= 4 bytes per token)
 #define Q_MISS 32                // deferred HBM inserts per wave (16 B each)
 #define Q_WLDS (Q_LIST * 2 + Q_MISS * 16)
-#ifndef Q_SLOTS                  // LDS word table: 16-byte keys + u32 counts (the rest of the CU's LDS)
-#define Q_SLOTS (((163840 - Q_W * (Q_LIST * 2 + Q_MISS * 16) - MSA_MLOG_PARTS * 4) / 20) & ~3)
+// LDS word tables: S = 3..8-byte words (92 % of the tokens of lyric text) as
+// single u64 keys (12 bytes a slot, 4-slot buckets read as two ds_read_b128),
+// optionally M = 9..16-byte words as 16-byte keys (20 bytes a slot).
+// Measured on configs[2] (csv_scan + k_miss_agg): S and M listed apart with a
+// 1024-slot M table 1.95 ms, mixed 1.99, mixed without an M table (M words
+// logged for k_miss_agg, the S table takes the whole LDS) 1.82.
+// K3_MIXED: one token list (S and M words mixed in a batch); the M lanes of
+// a batch probe the M table (or, with Q_MSLOTS 0, go straight to the miss
+// logs).  Otherwise S and M words are listed apart and probed in batches of
+// their own.
+#ifndef K3_MIXED
+#define K3_MIXED 1
 #endif
-#define Q_NB (Q_SLOTS / 4)
-#define Q_TAB (Q_SLOTS * 20)
+#ifndef Q_MSLOTS
+#define Q_MSLOTS 0
+#endif
+#define Q_MTAB (Q_MSLOTS * 20)
+#ifndef Q_SSLOTS                 // the rest of the CU's LDS
+#define Q_SSLOTS (((163840 - Q_MTAB - Q_W * (Q_LIST * 2 + Q_MISS * 16) - MSA_MLOG_PARTS * 4) / 12) & ~31)
+#endif
+#define Q_SNB (Q_SSLOTS / 4)
+#define Q_MNB (Q_MSLOTS / 4)
+#define Q_TAB (Q_SSLOTS * 12 + Q_MTAB)
 #define Q_LDS (Q_TAB + Q_W * Q_WLDS + MSA_MLOG_PARTS * 4)
 static_assert(Q_LDS <= 163840, "K3 LDS exceeds the CU's 160 KiB");
-static_assert(Q_SLOTS % 4 == 0 && Q_TAB % 16 == 0 && Q_WLDS % 16 == 0, "LDS carve-outs stay 16-byte aligned");
+static_assert(Q_SSLOTS % 32 == 0 && Q_MSLOTS % 4 == 0 && Q_TAB % 16 == 0 && Q_WLDS % 16 == 0,
+              "LDS carve-outs stay 16-byte aligned");
 
 // Every key byte of a token is < 0x80 (alnum or '\''), so bit 63 of the
 // second key word is free: it marks a published slot (an S word has k1 == 0).
@@ -172,6 +191,29 @@ __device__ __forceinline__ u64 pxor_ex64(u64 q) {  // bit j = parity of bits < j
 // 128-bit (hi:lo) >> k, low 64 bits, 0 < k < 64
 __device__ __forceinline__ u64 shr128(u64 lo, u64 hi, u32 k) { return (lo >> k) | (hi << (64 - k)); }
 
+// LDS lookup of an S key (3..8 bytes, nonzero).  Returns the slot or ~0u.
+__device__ __forceinline__ u32 lds_find8(u64 *skeys, u64 k0) {
+    u32 h = (u32)k0 * 0x9E3779B1u ^ (u32)(k0 >> 32) * 0x85EBCA77u;
+    h ^= h >> 15;
+    h *= 0x2C1B3C6Du;
+    u32 b = __umulhi(h, (u32)Q_SNB);
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+        const u32 base = b * 4;
+        const ulonglong2 s01 = *reinterpret_cast<const ulonglong2 *>(&skeys[base]);
+        const ulonglong2 s23 = *reinterpret_cast<const ulonglong2 *>(&skeys[base + 2]);
+        const u32 hit = s01.x == k0 ? 0u : (s01.y == k0 ? 1u : (s23.x == k0 ? 2u : (s23.y == k0 ? 3u : 4u)));
+        if (hit < 4) return base + hit;
+        u32 i = s01.x == 0 ? 0u : (s01.y == 0 ? 1u : (s23.x == 0 ? 2u : (s23.y == 0 ? 3u : 4u)));
+        for (; i < 4; ++i) {
+            const u64 old = atomicCAS((unsigned long long *)&skeys[base + i], 0ull, (unsigned long long)k0);
+            if (old == 0 || old == k0) return base + i;
+        }
+        b = (b + 1 == Q_SNB) ? 0 : b + 1;
+    }
+    return ~0u;
+}
+
 // LDS lookup of a 16-byte key (k1 carries KMARK).  Returns the slot or ~0u.
 // Written branch-light: the four slot compares are plain selects; only the
 // (rare, after warm-up) claim of an empty slot takes a divergent path.
@@ -179,7 +221,7 @@ __device__ __forceinline__ u32 lds_find16(ulonglong2 *keys, u64 k0, u64 k1) {
     u32 h = (u32)k0 * 0x9E3779B1u + (u32)(k0 >> 32) * 0x85EBCA77u + (u32)k1 * 0xC2B2AE3Du + (u32)(k1 >> 32);
     h ^= h >> 15;
     h *= 0x2C1B3C6Du;
-    u32 b = __umulhi(h, (u32)Q_NB);
+    u32 b = __umulhi(h, (u32)Q_MNB);
 #if K3_ROT
     // the four slot reads of a bucket start at a key-dependent slot: a
     // ds_read_b128 lane group (16 lanes) then spreads over 16 positions of the
@@ -208,7 +250,7 @@ __device__ __forceinline__ u32 lds_find16(ulonglong2 *keys, u64 k0, u64 k1) {
             }
             if (old == k0 && kp[1] == k1) return sl;
         }
-        b = (b + 1 == Q_NB) ? 0 : b + 1;
+        b = (b + 1 == Q_MNB) ? 0 : b + 1;
     }
     return ~0u;
 }
@@ -266,8 +308,10 @@ __device__ __forceinline__ void flush_miss(const ScanArgs &a, const ulonglong2 *
 
 __global__ __launch_bounds__(Q_T, 1) void k_scan_csv(ScanArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    ulonglong2 *keys = reinterpret_cast<ulonglong2 *>(smem);
-    u32 *cnts = reinterpret_cast<u32 *>(smem + Q_SLOTS * 16);
+    u64 *skeys = reinterpret_cast<u64 *>(smem);
+    u32 *scnts = reinterpret_cast<u32 *>(smem + Q_SSLOTS * 8);
+    ulonglong2 *keys = reinterpret_cast<ulonglong2 *>(smem + Q_SSLOTS * 12);
+    u32 *cnts = reinterpret_cast<u32 *>(smem + Q_SSLOTS * 12 + Q_MSLOTS * 16);
     const u32 lane = lane_id();
     const u32 wib = threadIdx.x >> 6;
     unsigned char *wl = smem + Q_TAB + wib * Q_WLDS;
@@ -277,7 +321,11 @@ __global__ __launch_bounds__(Q_T, 1) void k_scan_csv(ScanArgs a) {
     const u64 lt = (1ull << lane) - 1ull;
 
     u32 *lcur = reinterpret_cast<u32 *>(smem + Q_TAB + Q_W * Q_WLDS);  // log cursors per key partition
-    for (u32 i = threadIdx.x; i < Q_SLOTS; i += Q_T) {
+    for (u32 i = threadIdx.x; i < Q_SSLOTS; i += Q_T) {
+        skeys[i] = 0;
+        scnts[i] = 0;
+    }
+    for (u32 i = threadIdx.x; i < Q_MSLOTS; i += Q_T) {
         keys[i] = make_ulonglong2(0, 0);
         cnts[i] = 0;
     }
@@ -482,7 +530,8 @@ __global__ __launch_bounds__(Q_T, 1) void k_scan_csv(ScanArgs a) {
             const u64 r8 = r4 & shr128(r4, r4h, 4), r8h = r4h & (r4h >> 4);
             const u64 r16 = r8 & shr128(r8, r8h, 8);
             const u64 r17 = r16 & shr128(w, Tn, 16);
-            const u64 sSM = S0 & r3 & ~r17, sL = S0 & r17;
+            const u64 r9 = r8 & shr128(w, Tn, 8);
+            const u64 sS = S0 & r3 & ~r9, sM = S0 & r9 & ~r17, sL = S0 & r17;
             words += (u64)__popcll(S0 & r3);
 
             // long words (> 16 bytes): positions for k_long_insert
@@ -503,13 +552,21 @@ __global__ __launch_bounds__(Q_T, 1) void k_scan_csv(ScanArgs a) {
             }
 
             // 3..16-byte words.  The wave's token starts go to its LDS list
-            // (block offset | (length - 3) << 12), then the lanes take them
-            // 64 at a time.  Diagnostic ablations (MSA_ABLATE; results
-            // invalid): 1 no tokens at all, 2 no counting, 32 keys without
-            // the LDS table, 4 LDS misses dropped, 128 keys not re-read from memory
-            u64 m = (a.ablate & 3) ? 0ull : sSM;
-            u32 ntok;
-            u32 li = wave_prefix<5>((u32)__popcll(m), ntok);
+            // (block offset | (length - 3) << 12): S words from the front, M
+            // words from the back; then the lanes take them 64 at a time, S
+            // and M batches apart (each probes its own table).  Diagnostic
+            // ablations (MSA_ABLATE; results invalid): 1 no tokens at all, 2
+            // no counting, 32 keys without the LDS tables, 4 LDS misses
+            // dropped, 128 keys not re-read from memory
+            u64 m = (a.ablate & 3) ? 0ull : (sS | sM);
+            u32 nS, nM;
+#if K3_MIXED
+            u32 liS = wave_prefix<5>((u32)__popcll(m), nS), liM = 0;
+            nM = 0;
+#else
+            u32 liS = wave_prefix<5>((u32)__popcll(sS & m), nS);
+            u32 liM = wave_prefix<5>((u32)__popcll(sM & m), nM);
+#endif
             while (__ballot(m != 0)) {
                 if (m) {
                     const u32 b = (u32)__ffsll((long long)m) - 1;
@@ -519,35 +576,51 @@ __global__ __launch_bounds__(Q_T, 1) void k_scan_csv(ScanArgs a) {
                     const u32 d0 = (u32)w, d1 = (u32)(w >> 32), d2 = (u32)Tn;
                     const u32 run = __builtin_amdgcn_alignbit(b >= 32 ? d2 : d1, b >= 32 ? d1 : d0, b & 31u);
                     const u32 len = (u32)__ffs(~run) - 1;  // 3..16
-                    list[li++] = (u16)((lane * 64 + b) | ((len - 3) << 12));
+                    const u16 ent = (u16)((lane * 64 + b) | ((len - 3) << 12));
+                    if (K3_MIXED || len <= 8) list[liS++] = ent;
+                    else list[Q_LIST - 1 - liM++] = ent;
                 }
             }
             wsync();
-            // Keys are re-read from the block (L2) as five dwords from the
-            // token's dword; the next 64 tokens' loads are issued before this
-            // batch is probed, so their latency hides behind the LDS work.
+            // Keys are re-read from the block (L2) as dwords from the token's
+            // dword; the next 64 tokens' loads are issued before this batch is
+            // probed, so their latency hides behind the LDS work.  Batches
+            // 0 .. nbS-1 are S words, the rest M words.
+            const u32 nbS = (nS + 63) >> 6, nbM = (nM + 63) >> 6;
+            auto entry = [&](u32 bt, u32 i) -> u32 {  // list index of lane i of batch bt, or ~0u
+                if (bt < nbS) return (bt * 64 + i < nS) ? bt * 64 + i : ~0u;
+                const u32 k = (bt - nbS) * 64 + i;
+                return k < nM ? Q_LIST - 1 - k : ~0u;
+            };
             u32 en = 0;
             uint4 kv = make_uint4(0, 0, 0, 0);
             u32 k4 = 0;
-            if (lane < ntok) {
-                en = list[lane];
-                const u32 *gp = reinterpret_cast<const u32 *>(a.buf + ((ib + (en & 4095u)) & ~3ull));
-                kv = *reinterpret_cast<const uint4 *>(gp);
-                k4 = gp[4];
+            {
+                const u32 ix = nbS + nbM ? entry(0, lane) : ~0u;
+                if (ix != ~0u) {
+                    en = list[ix];
+                    const u32 *gp = reinterpret_cast<const u32 *>(a.buf + ((ib + (en & 4095u)) & ~3ull));
+                    kv = *reinterpret_cast<const uint4 *>(gp);
+                    k4 = gp[4];
+                }
             }
-            for (u32 t0 = 0; t0 < ntok; t0 += 64) {
+            for (u32 bt = 0; bt < nbS + nbM; ++bt) {
                 bool mis = false;
                 u64 k0 = 0, k1 = KMARK;
                 const u32 e = en;
                 const uint4 v = kv;
                 const u32 v4 = k4;
-                if (t0 + 64 + lane < ntok) {
-                    en = list[t0 + 64 + lane];
-                    const u32 *gp = reinterpret_cast<const u32 *>(a.buf + ((ib + (en & 4095u)) & ~3ull));
-                    kv = *reinterpret_cast<const uint4 *>(gp);
-                    k4 = gp[4];
+                const bool have = entry(bt, lane) != ~0u;
+                if (bt + 1 < nbS + nbM) {
+                    const u32 ix = entry(bt + 1, lane);
+                    if (ix != ~0u) {
+                        en = list[ix];
+                        const u32 *gp = reinterpret_cast<const u32 *>(a.buf + ((ib + (en & 4095u)) & ~3ull));
+                        kv = *reinterpret_cast<const uint4 *>(gp);
+                        k4 = gp[4];
+                    }
                 }
-                if (t0 + lane < ntok) {
+                if (have) {
                     const u32 len = (e >> 12) + 3;
                     const u32 sh = (u32)(ib + (e & 4095u)) & 3u;
                     u64 x0, x1;
@@ -564,10 +637,16 @@ __global__ __launch_bounds__(Q_T, 1) void k_scan_csv(ScanArgs a) {
                     k1 = lower8(x1) | KMARK;
                     if (a.ablate & 32) {
                         words += (k0 ^ k1) == 1;  // keep the key build alive
-                    } else {
+                    } else if (K3_MIXED ? len <= 8 : bt < nbS) {  // separate lists: wave-uniform
+                        const u32 slot = lds_find8(skeys, k0);
+                        if (slot != ~0u) atomicAdd(&scnts[slot], 1u);
+                        else mis = !(a.ablate & 4);
+                    } else if (Q_MSLOTS) {
                         const u32 slot = lds_find16(keys, k0, k1);
                         if (slot != ~0u) atomicAdd(&cnts[slot], 1u);
                         else mis = !(a.ablate & 4);
+                    } else {
+                        mis = !(a.ablate & 4);
                     }
                 }
                 const u64 MB = __ballot(mis);
@@ -593,10 +672,10 @@ __global__ __launch_bounds__(Q_T, 1) void k_scan_csv(ScanArgs a) {
     if (lane == 0 && words) atomicAdd((unsigned long long *)&a.ctr->total_words, (unsigned long long)words);
     __syncthreads();
     // the LDS table into the logs, counts encoded (full partitions: HBM inserts)
-    for (u32 i = threadIdx.x; i < Q_SLOTS && !(a.ablate & 32768); i += Q_T) {  // 32768: no flush (diagnostic)
-        u32 n = cnts[i];
+    for (u32 i = threadIdx.x; i < Q_SSLOTS + Q_MSLOTS && !(a.ablate & 32768); i += Q_T) {  // 32768: no flush
+        u32 n = i < Q_SSLOTS ? scnts[i] : cnts[i - Q_SSLOTS];
         if (!n) continue;
-        const ulonglong2 kk = keys[i];
+        const ulonglong2 kk = i < Q_SSLOTS ? make_ulonglong2(skeys[i], KMARK) : keys[i - Q_SSLOTS];
         const u32 part = mlog_part(kk.x, kk.y);
         const u64 base = ((u64)blockIdx.x * MSA_MLOG_PARTS + part) * a.mlog_cap;
         while (n) {
@@ -666,13 +745,25 @@ __global__ __launch_bounds__(MA_T) void k_miss_agg(ScanArgs a, u32 nsrc, u32 gro
         const u64 base = ((u64)src * MSA_MLOG_PARTS + part) * a.mlog_cap;
         const u32 n = a.mlog_n[src * MSA_MLOG_PARTS + part];
         if (threadIdx.x == 0 && n) atomicAdd((unsigned long long *)&a.ctr->k3_misses, (unsigned long long)n);
-        for (u32 i = threadIdx.x; i < n; i += MA_T) {
-            const ulonglong2 x = a.mlog[base + i];
-            const u32 c = gather8(x.x) | ((gather8(x.y) & 0x7Fu) << 8);
-            const u64 k0 = x.x & MLOG_KEYBITS, k1 = x.y & (MLOG_KEYBITS | KMARK);
-            const u32 slot = ma_find(keys, k0, k1);
-            if (slot != ~0u) atomicAdd(&cnts[slot], c ? c : 1u);
-            else hbm_insert16(a, k0, k1, c ? c : 1u);
+        // four entries per thread in flight: their loads are issued before
+        // the first LDS probe
+        for (u32 i0 = threadIdx.x; i0 < n; i0 += 4 * MA_T) {
+            ulonglong2 xs[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const u32 i = i0 + q * MA_T;
+                xs[q] = i < n ? a.mlog[base + i] : make_ulonglong2(0, 0);
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if (i0 + q * MA_T >= n) break;
+                const ulonglong2 x = xs[q];
+                const u32 c = gather8(x.x) | ((gather8(x.y) & 0x7Fu) << 8);
+                const u64 k0 = x.x & MLOG_KEYBITS, k1 = x.y & (MLOG_KEYBITS | KMARK);
+                const u32 slot = ma_find(keys, k0, k1);
+                if (slot != ~0u) atomicAdd(&cnts[slot], c ? c : 1u);
+                else hbm_insert16(a, k0, k1, c ? c : 1u);
+            }
         }
     }
     __syncthreads();
