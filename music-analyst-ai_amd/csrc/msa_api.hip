@@ -196,6 +196,17 @@ struct msa_ctx {
     Ranked rw, ra;
     msa_summary sum{};
     int stage = 0;  // 0 none, 1 split, 2 counted, 3 ranked
+    // text.csv is written on a side stream, overlapping the artist pass and
+    // the ranking (nothing downstream of the split reads it); every entry
+    // point that could touch its buffers joins it first (join_side)
+    hipStream_t side = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    bool side_pending = false;
+    // text.csv is launched after the counting (it shares the CUs badly with
+    // the per-CU artist tables): on the side stream during the ranking, or on
+    // the library stream by the first entry point that needs it
+    bool text_deferred = false;
+    std::string text_hdr;
     // profiling
     bool prof = false;
     ProfStage ps[ST_COUNT_];
@@ -213,7 +224,7 @@ static void prof_harvest(msa_ctx *c, int id) {
     }
     s.pending = false;
 }
-static void prof_begin(msa_ctx *c, int id) {
+static void prof_begin(msa_ctx *c, int id, hipStream_t st = nullptr) {
     if (!c->prof) return;
     ProfStage &s = c->ps[id];
     prof_harvest(c, id);
@@ -221,14 +232,43 @@ static void prof_begin(msa_ctx *c, int id) {
         (void)hipEventCreate(&s.a);
         (void)hipEventCreate(&s.b);
     }
-    (void)hipEventRecord(s.a, c->stream);
+    (void)hipEventRecord(s.a, st ? st : c->stream);
 }
-static void prof_end(msa_ctx *c, int id, u64 bytes) {
+static void prof_end(msa_ctx *c, int id, u64 bytes, hipStream_t st = nullptr) {
     if (!c->prof) return;
     ProfStage &s = c->ps[id];
-    (void)hipEventRecord(s.b, c->stream);
+    (void)hipEventRecord(s.b, st ? st : c->stream);
     s.pend_bytes = bytes;
     s.pending = true;
+}
+
+// The side stream starts after everything enqueued on the main stream so far.
+static hipError_t fork_side(msa_ctx *c) {
+    hipError_t e = hipEventRecord(c->ev_fork, c->stream);
+    if (e == hipSuccess) e = hipStreamWaitEvent(c->side, c->ev_fork, 0);
+    return e;
+}
+static int materialise_column(msa_ctx *c, bool text, const std::string &hdr_line, DevBuf &col, DevBuf &lenb,
+                              DevBuf &offb, DevBuf &srcb, DevBuf &pairsb, hipStream_t st);
+// The deferred text.csv pass on stream st.
+static hipError_t launch_text(msa_ctx *c, hipStream_t st) {
+    c->text_deferred = false;
+    prof_begin(c, ST_TEXT_COLUMN, st);
+    if (materialise_column(c, true, c->text_hdr, c->tcol, c->tlen, c->toff, c->tsrc, c->tpairs, st))
+        return hipErrorUnknown;
+    prof_end(c, ST_TEXT_COLUMN, c->n * 2 + c->nrec * 40, st);  // ~ the text column read + written
+    return hipGetLastError();
+}
+// Everything the library owes on its stream: a text.csv pass not launched
+// yet runs there, one on the side stream is waited for (enqueued, no host wait).
+static hipError_t join_side(msa_ctx *c) {
+    if (c->text_deferred) {
+        const hipError_t e = launch_text(c, c->stream);
+        if (e != hipSuccess) return e;
+    }
+    if (!c->side_pending) return hipSuccess;
+    c->side_pending = false;
+    return hipStreamWaitEvent(c->stream, c->ev_join, 0);
 }
 
 static int fail(msa_ctx *c, int code, const char *fmt, ...) {
@@ -540,16 +580,15 @@ static int scan_columns(msa_ctx *c, bool text) {
 }
 
 static int materialise_column(msa_ctx *c, bool text, const std::string &hdr_line, DevBuf &col, DevBuf &lenb,
-                              DevBuf &offb, DevBuf &srcb, DevBuf &pairsb) {
+                              DevBuf &offb, DevBuf &srcb, DevBuf &pairsb, hipStream_t st) {
     const u64 nrec = c->nrec;
     u64 *body_p = &c->ctr.as<Counters>()->col_body[text ? 1 : 0];  // from scan_columns
-    HIPC(c, ensure(col, hdr_line.size() + c->n + 1 + MSA_INPUT_PAD));
-    HIPC(c, hipMemcpyAsync(col.p, hdr_line.data(), hdr_line.size(), hipMemcpyHostToDevice, c->stream));
+    HIPC(c, hipMemcpyAsync(col.p, hdr_line.data(), hdr_line.size(), hipMemcpyHostToDevice, st));
     // the artist column reads lines equal to their keys from the arena k_rec_fast filled
     const bool keys = !text && c->spans;
     HIPC(c, msa_launch_col_write(text ? 1 : 0, c->in, lenb.as<u64>(), offb.as<u64>(), srcb.as<u64>(), pairsb.as<u32>(),
                                  nrec, hdr_line.size(), body_p, col.as<u8>(), keys ? c->arena.as<u8>() : nullptr,
-                                 c->key_off.as<u64>(), c->key_len.as<u32>(), c->stream));
+                                 c->key_off.as<u64>(), c->key_len.as<u32>(), st));
     return MSA_OK;
 }
 
@@ -596,7 +635,8 @@ static int split_columns_rest(msa_ctx *c, bool want_text, const std::string &ah,
                                  c->spans ? c->f0.as<u64>() : nullptr, c->tss.as<u64>(), c->tse.as<u64>(),
                                  c->span_fix.as<u64>(), c->ablate, c->stream));
     if ((rc = scan_columns(c, want_text))) return rc;
-    if ((rc = materialise_column(c, false, ah, c->acol, c->alen, c->aoff, c->asrc, c->apairs))) return rc;
+    HIPC(c, ensure(c->acol, ah.size() + c->n + 1 + MSA_INPUT_PAD));
+    if ((rc = materialise_column(c, false, ah, c->acol, c->alen, c->aoff, c->asrc, c->apairs, c->stream))) return rc;
     prof_end(c, ST_ARTIST_COLUMN, c->nrec * 16 * 2 + c->nrec * 32);  // ~16-byte artist lines
     // compute_header_length (parallel_spotify.c:444-459): getline's end
     c->a_hdr_getline = ah.empty() ? 0 : ah.find('\n') + 1;
@@ -606,10 +646,10 @@ static int split_columns_rest(msa_ctx *c, bool want_text, const std::string &ah,
     c->col_hdr[1] = th.size();
     c->col_lens_pending = true;  // acol_len / tcol_len / a_end: from the next counter read-back
     c->have_tcol = false;
-    if (want_text) {
-        prof_begin(c, ST_TEXT_COLUMN);
-        if ((rc = materialise_column(c, true, th, c->tcol, c->tlen, c->toff, c->tsrc, c->tpairs))) return rc;
-        prof_end(c, ST_TEXT_COLUMN, c->n * 2 + c->nrec * 40);  // ~ the text column read + written
+    if (want_text) {  // deferred (see msa_ctx::text_deferred)
+        HIPC(c, ensure(c->tcol, th.size() + c->n + 1 + MSA_INPUT_PAD));
+        c->text_hdr = th;
+        c->text_deferred = true;
         c->have_tcol = true;
     }
     c->stage = 1;
@@ -630,6 +670,8 @@ static int check_split_overflow(msa_ctx *c, bool read_back = true) {
 
 static int split_once(msa_ctx *c, int flags) {
     int rc;
+    c->text_deferred = false;  // superseded by this split
+    HIPC(c, join_side(c));     // a text column pass in flight reads buffers this one rewrites
     if (!c->in) return fail(c, MSA_ERR_ARG, "no input bound (msa_load_csv / msa_bind_csv)");
     if (c->n == 0 && !c->cont) return fail(c, MSA_ERR_NOHEADER, "Dataset does not contain a header row");
     const bool want_text = (flags & MSA_SPLIT_TEXT_COLUMN) != 0;
@@ -1089,6 +1131,12 @@ static int sort_and_blob(msa_ctx *c, Ranked &R, const u8 *wbuf, const u8 *wextra
 static int do_rank(msa_ctx *c) {
     int rc;
     if (c->stage < 2) return fail(c, MSA_ERR_ARG, "msa_rank before msa_count");
+    if (c->text_deferred) {  // text.csv on the side stream, beside the (latency-bound) ranking
+        HIPC(c, fork_side(c));
+        HIPC(c, launch_text(c, c->side));
+        HIPC(c, hipEventRecord(c->ev_join, c->side));
+        c->side_pending = true;
+    }
     // words
     Ranked &W = c->rw;
     W.n = c->sum.n_words;
@@ -1206,7 +1254,10 @@ int msa_create(int device, msa_ctx **out) {
         if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
             c->cus = prop.multiProcessorCount;
     }
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
         delete c;
         return MSA_ERR_HIP;
     }
@@ -1217,6 +1268,7 @@ int msa_create(int device, msa_ctx **out) {
 void msa_destroy(msa_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
+    (void)join_side(c);
     (void)hipStreamSynchronize(c->stream);
     DevBuf *all[] = {&c->in_own, &c->sums, &c->carry, &c->btot, &c->bstate, &c->small, &c->rec_start, &c->extra, &c->exp_buf, &c->exp_meta, &c->imp_w, &c->imp_a, &c->imp_meta,
                      &c->nulrel, &c->f0, &c->tss, &c->tse, &c->span_fix, &c->alog, &c->alog_n, &c->acol, &c->alen, &c->aoff, &c->asrc, &c->apairs, &c->tcol, &c->tlen, &c->toff, &c->tsrc, &c->tpairs,
@@ -1240,6 +1292,9 @@ void msa_destroy(msa_ctx *c) {
         if (s.a) (void)hipEventDestroy(s.a);
         if (s.b) (void)hipEventDestroy(s.b);
     }
+    (void)hipEventDestroy(c->ev_fork);
+    (void)hipEventDestroy(c->ev_join);
+    (void)hipStreamDestroy(c->side);
     (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -1249,6 +1304,7 @@ void *msa_stream(msa_ctx *c) { return c ? (void *)c->stream : nullptr; }
 
 int msa_sync(msa_ctx *c) {
     if (!c) return MSA_ERR_ARG;
+    HIPC(c, join_side(c));
     HIPC(c, hipStreamSynchronize(c->stream));
     return MSA_OK;
 }
@@ -1256,6 +1312,8 @@ int msa_sync(msa_ctx *c) {
 int msa_load_csv(msa_ctx *c, const void *host, size_t n) {
     if (!c || (!host && n)) return MSA_ERR_ARG;
     HIPC(c, hipSetDevice(c->device));
+    HIPC(c, join_side(c));
+    HIPC(c, hipStreamSynchronize(c->stream));  // nothing in flight reads the old input
     HIPC(c, ensure(c->in_own, n + MSA_INPUT_PAD));
     if (n) HIPC(c, hipMemcpy(c->in_own.p, host, n, hipMemcpyHostToDevice));
     HIPC(c, hipMemset(c->in_own.as<char>() + n, 0, MSA_INPUT_PAD));
@@ -1269,6 +1327,7 @@ int msa_load_csv(msa_ctx *c, const void *host, size_t n) {
 
 int msa_bind_csv(msa_ctx *c, const void *dev, size_t n) {
     if (!c || (!dev && n)) return MSA_ERR_ARG;
+    HIPC(c, join_side(c));
     c->in = reinterpret_cast<const u8 *>(dev);
     c->n = n;
     c->in_base = c->in;
@@ -1302,6 +1361,8 @@ int msa_run(msa_ctx *c, int flags) {
     int rc = do_split(c, flags);
     if (!rc) rc = do_count(c);
     if (!rc) rc = do_rank(c);
+    const hipError_t e = join_side(c);  // a later sync on the library stream covers text.csv
+    if (!rc && e != hipSuccess) rc = fail(c, MSA_ERR_HIP, "HIP error %s", hipGetErrorString(e));
     return rc;
 }
 
@@ -1372,6 +1433,7 @@ int msa_write_table_csv(msa_ctx *c, int table, const char *path, const char *key
 
 int msa_get_split_column(msa_ctx *c, int which, char **out, size_t *len) {
     if (!c || !out || !len || (which != 0 && which != 1)) return MSA_ERR_ARG;
+    HIPC(c, join_side(c));  // text.csv (side stream) may still read the buffers this touches
     if (c->stage < 1) return fail(c, MSA_ERR_ARG, "msa_get_split_column before msa_split_columns");
     if (which == 1 && !c->have_tcol)
         return fail(c, MSA_ERR_ARG, "text column not materialised (pass MSA_SPLIT_TEXT_COLUMN)");
@@ -1392,6 +1454,7 @@ int msa_get_split_column(msa_ctx *c, int which, char **out, size_t *len) {
 
 int msa_set_artist_reader(msa_ctx *c, int exact) {
     if (!c) return MSA_ERR_ARG;
+    HIPC(c, join_side(c));  // text.csv (side stream) may still read the buffers this touches
     c->artist_exact = exact != 0;
     return MSA_OK;
 }
@@ -1435,6 +1498,7 @@ static_assert(sizeof(msa_shard_fn) == sizeof(Fn), "msa_shard_fn mirrors Fn");
 
 int msa_set_shard(msa_ctx *c, int first) {
     if (!c) return MSA_ERR_ARG;
+    HIPC(c, join_side(c));  // text.csv (side stream) may still read the buffers this touches
     c->cont = first == 0;
     return MSA_OK;
 }
@@ -1460,6 +1524,7 @@ static int piece_of(msa_ctx *c, int piece, const u8 **base, u64 *len) {
 
 int msa_piece_size(msa_ctx *c, int piece, uint64_t *len) {
     if (!c || !len) return MSA_ERR_ARG;
+    HIPC(c, join_side(c));  // text.csv (side stream) may still read the buffers this touches
     const u8 *base;
     u64 n;
     int rc;
@@ -1470,6 +1535,7 @@ int msa_piece_size(msa_ctx *c, int piece, uint64_t *len) {
 
 int msa_shard_function(msa_ctx *c, int piece, msa_shard_fn *out) {
     if (!c || !out) return MSA_ERR_ARG;
+    HIPC(c, join_side(c));  // text.csv (side stream) may still read the buffers this touches
     HIPC(c, hipSetDevice(c->device));
     const u8 *base;
     u64 len;
@@ -1488,6 +1554,7 @@ int msa_shard_function(msa_ctx *c, int piece, msa_shard_fn *out) {
 int msa_shard_head(msa_ctx *c, int piece, const msa_shard_fn *before, int nbefore, const uint64_t *sizes,
                    uint64_t *head) {
     if (!c || !head || nbefore < 0 || (nbefore && (!before || !sizes))) return MSA_ERR_ARG;
+    HIPC(c, join_side(c));  // text.csv (side stream) may still read the buffers this touches
     HIPC(c, hipSetDevice(c->device));
     const u8 *base;
     u64 len;
@@ -1526,6 +1593,7 @@ int msa_shard_head(msa_ctx *c, int piece, const msa_shard_fn *before, int nbefor
 
 int msa_segment_copy(msa_ctx *c, int piece, uint64_t off, uint64_t len, void *dst) {
     if (!c || (len && !dst)) return MSA_ERR_ARG;
+    HIPC(c, join_side(c));  // text.csv (side stream) may still read the buffers this touches
     HIPC(c, hipSetDevice(c->device));
     const u8 *base;
     u64 plen;
@@ -1555,6 +1623,7 @@ static hipError_t grow_keep(DevBuf &b, size_t bytes, size_t keep, hipStream_t s)
 
 int msa_segment_set(msa_ctx *c, int piece, uint64_t skip, const void *tail, uint64_t tail_len) {
     if (!c || (tail_len && !tail)) return MSA_ERR_ARG;
+    HIPC(c, join_side(c));  // text.csv (side stream) may still read the buffers this touches
     HIPC(c, hipSetDevice(c->device));
     const u8 *base;
     u64 len;
@@ -1621,6 +1690,7 @@ static void fill_exp_src(msa_ctx *c, int table, ExpSrc &x, u64 *n) {
 
 int msa_export_partitions(msa_ctx *c, int table, int nparts, uint64_t *part_bytes) {
     if (!c || nparts < 1 || nparts > 4096 || !part_bytes) return MSA_ERR_ARG;
+    HIPC(c, join_side(c));  // text.csv (side stream) may still read the buffers this touches
     if (table != MSA_TABLE_WORDS && table != MSA_TABLE_ARTISTS) return MSA_ERR_ARG;
     if (c->stage < 2) return fail(c, MSA_ERR_ARG, "msa_export_partitions before msa_count");
     HIPC(c, hipSetDevice(c->device));
@@ -1651,6 +1721,7 @@ int msa_export_partitions(msa_ctx *c, int table, int nparts, uint64_t *part_byte
 
 int msa_export_ranked(msa_ctx *c, int table, uint64_t limit, uint64_t *bytes) {
     if (!c || !bytes) return MSA_ERR_ARG;
+    HIPC(c, join_side(c));  // text.csv (side stream) may still read the buffers this touches
     if (table != MSA_TABLE_WORDS && table != MSA_TABLE_ARTISTS) return MSA_ERR_ARG;
     if (c->stage < 3) return fail(c, MSA_ERR_ARG, "msa_export_ranked before msa_rank");
     HIPC(c, hipSetDevice(c->device));
@@ -1671,6 +1742,7 @@ int msa_export_ranked(msa_ctx *c, int table, uint64_t limit, uint64_t *bytes) {
 
 int msa_export_copy(msa_ctx *c, void *dst) {
     if (!c || (c->exp_bytes && !dst)) return MSA_ERR_ARG;
+    HIPC(c, join_side(c));  // text.csv (side stream) may still read the buffers this touches
     HIPC(c, hipSetDevice(c->device));
     if (c->exp_bytes) HIPC(c, hipMemcpyAsync(dst, c->exp_buf.p, c->exp_bytes, hipMemcpyDefault, c->stream));
     HIPC(c, hipStreamSynchronize(c->stream));
@@ -1689,6 +1761,7 @@ static int clear_one(msa_ctx *c, DevBuf &tab, DevBuf &list, u64 &used, u32 w) {
 
 int msa_import_partitions(msa_ctx *c, int table, const void *src, const uint64_t *blk_off, int nblk) {
     if (!c || !blk_off || nblk < 1) return MSA_ERR_ARG;
+    HIPC(c, join_side(c));  // text.csv (side stream) may still read the buffers this touches
     if (table != MSA_TABLE_WORDS && table != MSA_TABLE_ARTISTS) return MSA_ERR_ARG;
     if (c->stage < 2) return fail(c, MSA_ERR_ARG, "msa_import_partitions before msa_count");
     HIPC(c, hipSetDevice(c->device));
@@ -1801,6 +1874,7 @@ extern "C" int msa_debug_stat(msa_ctx *c, const char *name, uint64_t *v) {
 // (tools/k3_debug.py compares kernel variants with it).
 extern "C" int msa_debug_records(msa_ctx *c, uint64_t *rec_start, uint32_t *nulrel, uint64_t cap, uint64_t *n) {
     if (!c || !n) return MSA_ERR_ARG;
+    HIPC(c, join_side(c));  // text.csv (side stream) may still read the buffers this touches
     if (c->stage < 1) return MSA_ERR_ARG;
     HIPC(c, hipSetDevice(c->device));
     HIPC(c, hipStreamSynchronize(c->stream));

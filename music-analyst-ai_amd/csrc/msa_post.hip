@@ -720,8 +720,19 @@ __global__ __launch_bounds__(256) void k_rec_fast(const u8 *__restrict__ buf, co
         o.asrc[r] = s;
         o.apairs[r] = 0;
     } else {
-        const Win64 w0 = load_win64(buf, s);
-        rec_artist(buf, w0, s, (u32)(f0p[r] - s), r, o, ctr, ak, (ablate & 1024) != 0, ablate);
+        // the window's second half only when field 0 reaches into it
+        const u64 f0 = f0p[r] - s;
+        const uint4 *p = reinterpret_cast<const uint4 *>(buf + (s & ~15ull));
+        Win64 w0;
+        w0.q[0] = p[0];
+        w0.q[1] = p[1];
+        if ((s & 15) + f0 > 32) {
+            w0.q[2] = p[2];
+            w0.q[3] = p[3];
+        } else {
+            w0.q[2] = w0.q[3] = make_uint4(0, 0, 0, 0);
+        }
+        rec_artist(buf, w0, s, (u32)f0, r, o, ctr, ak, (ablate & 1024) != 0, ablate);
     }
     if (want_text) {
         o.tlen[r] = te - ts + 1;
