@@ -66,6 +66,27 @@ def test_wcs_zipf_vs_oracle(msa_mod, wcs, seed, crlf):
     assert wcs.run(data) == wcs_oracle.word_count_per_song(data)
 
 
+def _fuzz_text(seed, n=600):
+    """Lyrics mixing ASCII, the two-byte Latin-1 letters (upper / lower case, ß,
+    the excluded × and ÷), other UTF-8 (é in NFD, ’, emoji), apostrophes and
+    escaped quotes at every offset of the 16-byte blocks the tokenizer walks."""
+    import random
+    rng = random.Random(seed)
+    bits = ["a", "Zz", "'", "don't", "ÀÉÎ", "àéî", "ß", "Þþ", "×", "÷", "e\u0301", "’", "😀", "ÿ", "1", "Ü",
+            " ", "  ", ",", ".", '"', "x" * 15, "ÉÉÉÉÉÉÉÉ", "ö'", "\t"]
+    rows = ["artist,song,link,text"]
+    for i in range(n):
+        text = "".join(rng.choice(bits) for _ in range(rng.randint(0, 40)))
+        rows.append(f'A{i % 7},S{i},/l/{i},"' + text.replace('"', '""') + '"')
+    return ("\n".join(rows) + "\n").encode("utf-8")
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3, 4])
+def test_wcs_fuzz_tokens_vs_oracle(wcs, seed):
+    data = _fuzz_text(seed)
+    assert wcs.run(data) == wcs_oracle.word_count_per_song(data)
+
+
 def test_wcs_table_growth(msa_mod):
     """A 2^4-slot word table overflows; the run grows it and repeats."""
     data = msa_mod.gen_corpus(800, mode="highcard", seed=21, vocab=20000)
