@@ -741,7 +741,8 @@ static int split_once(msa_ctx *c, int flags) {
     if (c->ablate & 64) HIPC(c, msa_launch_scan(a, 0, c->stream));
     else HIPC(c, msa_launch_scan_csv(a, c->stream));
     // algorithmic bytes: every CSV byte once + the per-record SoA it writes
-    prof_end(c, ST_CSV_SCAN, c->n + c->nrec * (want_text ? 12ull : 8ull));
+    // (rec_start 8, nulrel 4 with the text column, the span events f0 / tss / tse 24)
+    prof_end(c, ST_CSV_SCAN, c->n + c->nrec * ((want_text ? 12ull : 8ull) + (c->spans ? 24ull : 0ull)));
     if (!(c->ablate & 64)) {
         prof_begin(c, ST_MISS_AGG);
         HIPC(c, msa_launch_miss_agg(a, c->stream));
