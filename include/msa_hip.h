@@ -85,7 +85,11 @@ typedef struct msa_ctx msa_ctx;
 int msa_create(int device, msa_ctx **out);
 void msa_destroy(msa_ctx *ctx);
 const char *msa_last_error(const msa_ctx *ctx);
-/* The HIP stream (hipStream_t) every kernel of this context runs on. */
+/* The HIP stream (hipStream_t) this context's work is ordered on.  text.csv
+ * (MSA_SPLIT_TEXT_COLUMN) is written on a second, internal stream during the
+ * ranking; msa_run and every entry point that reads it enqueue a wait for it
+ * on this stream, so work queued here after msa_run -- and msa_sync -- sees
+ * every result. */
 void *msa_stream(msa_ctx *ctx);
 int msa_sync(msa_ctx *ctx);
 

@@ -207,6 +207,10 @@ struct msa_ctx {
     // the library stream by the first entry point that needs it
     bool text_deferred = false;
     std::string text_hdr;
+    // pinned read-back area: the counters, states and header bytes a run reads
+    // back are copied here asynchronously and waited for with one sync
+    // (pageable destinations made every copy a round trip of its own)
+    unsigned char *pin = nullptr;
     // profiling
     bool prof = false;
     ProfStage ps[ST_COUNT_];
@@ -370,6 +374,10 @@ static void h_sanitize(const std::string &in, char *out) {
 // ------------------------------------------------------------------- scanning
 // Scan a byte segment [b, e) of `buf`: K1 + K2 (+ K3 in `mode`).  Returns the
 // reader state at the end of the segment in *fin.
+// pin layout: [0, 512) Counters, [512, 1024) a state / small values, [1024, 1024 + kPinHead) header bytes
+static const u64 kPinSmall = 512, kPinHead = 4096, kPinBytes = 1024 + kPinHead;
+static_assert(sizeof(Counters) <= 512 && sizeof(State) <= 512, "pinned read-back layout");
+
 static int run_scan_fn(msa_ctx *c, const u8 *buf, u64 b, u64 e, State init, State *fin, int stage_id) {
     const u64 len = e > b ? e - b : 0;
     const u32 nch = (u32)((len + MSA_CHUNK - 1) / MSA_CHUNK);
@@ -388,8 +396,9 @@ static int run_scan_fn(msa_ctx *c, const u8 *buf, u64 b, u64 e, State init, Stat
         HIPC(c, msa_launch_fn(c->sums.as<ChunkSum>(), b, nch, c->btot.as<Fn>(), c->bstate.as<State>(), total, d_init,
                               c->carry.as<State>(), d_fin, c->stream));
         prof_end(c, stage_id, len);
-        HIPC(c, hipMemcpyAsync(fin, d_fin, sizeof(State), hipMemcpyDeviceToHost, c->stream));
+        HIPC(c, hipMemcpyAsync(c->pin + kPinSmall, d_fin, sizeof(State), hipMemcpyDeviceToHost, c->stream));
         HIPC(c, hipStreamSynchronize(c->stream));
+        memcpy(fin, c->pin + kPinSmall, sizeof(State));
     } else {
         *fin = init;
     }
@@ -510,8 +519,9 @@ static void take_col_lens(msa_ctx *c) {
     c->col_lens_pending = false;
 }
 static int sync_counters(msa_ctx *c) {
-    HIPC(c, hipMemcpyAsync(&c->h_ctr, c->ctr.p, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipMemcpyAsync(c->pin, c->ctr.p, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
     HIPC(c, hipStreamSynchronize(c->stream));
+    memcpy(&c->h_ctr, c->pin, sizeof(Counters));
     take_col_lens(c);
     return MSA_OK;
 }
@@ -759,15 +769,22 @@ static int split_once(msa_ctx *c, int flags) {
     // occurrences) and -- for the first shard -- the header record's end plus
     // the input's first bytes (the header, almost always)
     if ((rc = build_word_lists(c))) return rc;
-    HIPC(c, hipMemcpyAsync(&c->h_ctr, c->ctr.p, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipMemcpyAsync(c->pin, c->ctr.p, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
     u64 hend = c->n;
-    static const u64 kHead = 4096;
+    static const u64 kHead = kPinHead;
     std::vector<unsigned char> hdr(std::min<u64>(c->n, kHead) + 1);
     if (!c->cont) {
-        if (nterm > 0) HIPC(c, hipMemcpyAsync(&hend, c->rec_start.as<u64>() + 1, 8, hipMemcpyDeviceToHost, c->stream));
-        if (c->n) HIPC(c, hipMemcpyAsync(hdr.data(), c->in, std::min<u64>(c->n, kHead), hipMemcpyDeviceToHost, c->stream));
+        if (nterm > 0)
+            HIPC(c, hipMemcpyAsync(c->pin + kPinSmall, c->rec_start.as<u64>() + 1, 8, hipMemcpyDeviceToHost, c->stream));
+        if (c->n)
+            HIPC(c, hipMemcpyAsync(c->pin + 1024, c->in, std::min<u64>(c->n, kHead), hipMemcpyDeviceToHost, c->stream));
     }
     HIPC(c, hipStreamSynchronize(c->stream));
+    memcpy(&c->h_ctr, c->pin, sizeof(Counters));
+    if (!c->cont) {
+        if (nterm > 0) memcpy(&hend, c->pin + kPinSmall, 8);
+        if (c->n) memcpy(hdr.data(), c->pin + 1024, std::min<u64>(c->n, kHead));
+    }
     if (c->cont) {
         if ((rc = check_split_overflow(c, false))) return rc;
         return split_columns_rest(c, want_text, std::string(), std::string());
@@ -1197,8 +1214,9 @@ static int do_rank(msa_ctx *c) {
     // fit the capacity it was written with is grown and written again
     u64 tot[2] = {0, 0};
     if (W.blob_pending || A.blob_pending)
-        HIPC(c, hipMemcpyAsync(tot, c->blob_tot.p, sizeof tot, hipMemcpyDeviceToHost, c->stream));
+        HIPC(c, hipMemcpyAsync(c->pin + kPinSmall, c->blob_tot.p, sizeof tot, hipMemcpyDeviceToHost, c->stream));
     HIPC(c, hipStreamSynchronize(c->stream));
+    if (W.blob_pending || A.blob_pending) memcpy(tot, c->pin + kPinSmall, sizeof tot);
     bool again = false;
     for (int t = 0; t < 2; ++t) {
         Ranked &R = t ? A : W;
@@ -1258,7 +1276,8 @@ int msa_create(int device, msa_ctx **out) {
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
+        hipHostMalloc((void **)&c->pin, kPinBytes, hipHostMallocDefault) != hipSuccess) {
         delete c;
         return MSA_ERR_HIP;
     }
@@ -1293,6 +1312,7 @@ void msa_destroy(msa_ctx *c) {
         if (s.a) (void)hipEventDestroy(s.a);
         if (s.b) (void)hipEventDestroy(s.b);
     }
+    (void)hipHostFree(c->pin);
     (void)hipEventDestroy(c->ev_fork);
     (void)hipEventDestroy(c->ev_join);
     (void)hipStreamDestroy(c->side);
