@@ -111,11 +111,12 @@ enum {
     ST_RANK_WORDS,       // entries + sort + key blob, words
     ST_RANK_ARTISTS,     // the same, artists
     ST_MISS_AGG,         // K3's logged LDS-table misses -> word tables (k_miss_agg)
+    ST_REC_SPANS,        // both columns' line spans + artist keys (k_rec_fast / k_rec_fix) + offset scans
     ST_COUNT_
 };
 const char *const kStageName[ST_COUNT_] = {"csv_summary", "csv_scan",    "artist_column", "text_column",
                                            "artist_summary", "artist_scan", "artist_keys",  "long_words",
-                                           "rank_words",  "rank_artists", "csv_miss_agg"};
+                                           "rank_words",  "rank_artists", "csv_miss_agg", "rec_spans"};
 
 struct ProfStage {
     hipEvent_t a = nullptr, b = nullptr;
@@ -262,6 +263,17 @@ static hipError_t launch_text(msa_ctx *c, hipStream_t st) {
         return hipErrorUnknown;
     prof_end(c, ST_TEXT_COLUMN, c->n * 2 + c->nrec * 40, st);  // ~ the text column read + written
     return hipGetLastError();
+}
+// The deferred text.csv pass on the side stream, after what is enqueued on
+// the library stream so far (its artist-table kernels need whole CUs' LDS:
+// the pass starts behind them).
+static hipError_t start_text_side(msa_ctx *c) {
+    if (!c->text_deferred) return hipSuccess;
+    hipError_t e = fork_side(c);
+    if (e == hipSuccess) e = launch_text(c, c->side);
+    if (e == hipSuccess) e = hipEventRecord(c->ev_join, c->side);
+    if (e == hipSuccess) c->side_pending = true;
+    return e;
 }
 // Everything the library owes on its stream: a text.csv pass not launched
 // yet runs there, one on the side stream is waited for (enqueued, no host wait).
@@ -615,10 +627,12 @@ static int build_word_lists(msa_ctx *c) {
 
 // Column materialisation after the scan.  ah / th are the header lines of
 // artist.csv / text.csv (empty for a continuation shard).
-static int split_columns_rest(msa_ctx *c, bool want_text, const std::string &ah, const std::string &th) {
+// Line spans of both columns and the artist keys, then the offset scans: they
+// depend on the scan alone, so they are enqueued before its read-back (the
+// host's header work overlaps them).
+static int launch_spans(msa_ctx *c, bool want_text) {
     int rc;
-    prof_begin(c, ST_ARTIST_COLUMN);
-    // line spans of both columns in one pass over the records
+    prof_begin(c, ST_REC_SPANS);
     const u64 nrec = c->nrec;
     HIPC(c, ensure(c->alen, nrec * 8));
     HIPC(c, ensure(c->asrc, nrec * 8));
@@ -645,9 +659,16 @@ static int split_columns_rest(msa_ctx *c, bool want_text, const std::string &ah,
                                  c->spans ? c->f0.as<u64>() : nullptr, c->tss.as<u64>(), c->tse.as<u64>(),
                                  c->span_fix.as<u64>(), c->ablate, c->stream));
     if ((rc = scan_columns(c, want_text))) return rc;
+    prof_end(c, ST_REC_SPANS, nrec * 136);  // ~36 B read + 100 B written per record
+    return MSA_OK;
+}
+
+static int split_columns_rest(msa_ctx *c, bool want_text, const std::string &ah, const std::string &th) {
+    int rc;
+    prof_begin(c, ST_ARTIST_COLUMN);
     HIPC(c, ensure(c->acol, ah.size() + c->n + 1 + MSA_INPUT_PAD));
     if ((rc = materialise_column(c, false, ah, c->acol, c->alen, c->aoff, c->asrc, c->apairs, c->stream))) return rc;
-    prof_end(c, ST_ARTIST_COLUMN, c->nrec * 16 * 2 + c->nrec * 32);  // ~16-byte artist lines
+    prof_end(c, ST_ARTIST_COLUMN, c->nrec * 16 * 2);  // ~16-byte artist lines read + written
     // compute_header_length (parallel_spotify.c:444-459): getline's end
     c->a_hdr_getline = ah.empty() ? 0 : ah.find('\n') + 1;
     c->a_hdr_len = ah.size();
@@ -765,6 +786,7 @@ static int split_once(msa_ctx *c, int flags) {
         u64 fx = SPAN_FIX;  // no terminator: k_rec_fast leaves the last record to the exact path
         HIPC(c, hipMemcpyAsync(c->tse.as<u64>() + c->nrec - 1, &fx, 8, hipMemcpyHostToDevice, c->stream));
     }
+    if ((rc = launch_spans(c, want_text))) return rc;
     // one read-back after the scan: the counters (table overflow, long-word
     // occurrences) and -- for the first shard -- the header record's end plus
     // the input's first bytes (the header, almost always)
@@ -930,6 +952,7 @@ static int do_count(msa_ctx *c) {
             if (attempt == 0) {
                 launch_long_words(c, nl);
                 long_ran = true;
+                HIPC(c, start_text_side(c));  // text.csv beside this read-back and the ranking
             }
             if ((rc = sync_counters(c))) return rc;
             long_ok = attempt == 0;
@@ -1149,12 +1172,7 @@ static int sort_and_blob(msa_ctx *c, Ranked &R, const u8 *wbuf, const u8 *wextra
 static int do_rank(msa_ctx *c) {
     int rc;
     if (c->stage < 2) return fail(c, MSA_ERR_ARG, "msa_rank before msa_count");
-    if (c->text_deferred) {  // text.csv on the side stream, beside the (latency-bound) ranking
-        HIPC(c, fork_side(c));
-        HIPC(c, launch_text(c, c->side));
-        HIPC(c, hipEventRecord(c->ev_join, c->side));
-        c->side_pending = true;
-    }
+    HIPC(c, start_text_side(c));
     // words
     Ranked &W = c->rw;
     W.n = c->sum.n_words;
