@@ -696,6 +696,10 @@ static int check_split_overflow(msa_ctx *c, bool read_back = true) {
     if (c->h_ctr.overflow & kSplitOvf)
         return fail(c, MSA_ERR_CAPACITY, "word table capacity overflow (flags 0x%llx)",
                     (unsigned long long)c->h_ctr.overflow);
+    // the S/M slots this split claimed: the next split clears them even when no
+    // msa_count ran in between
+    c->s_used_prev = std::min<u64>(c->h_ctr.s_claimed, c->s_slots / 2);
+    c->m_used_prev = std::min<u64>(c->h_ctr.m_claimed, c->m_slots / 2);
     return MSA_OK;
 }
 

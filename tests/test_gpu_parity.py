@@ -144,6 +144,47 @@ def test_fuzz_fields_quote_free_artists(msa_mod, ctx, tmp_path):
     check_against_oracle(msa_mod, ctx, data, tmp_path, "fuzz_qf")
 
 
+def test_text_column_stage_orders(msa_mod, ctx, tmp_path):
+    """text.csv is written on a side stream (launched with the artist pass or
+    the ranking, or by the entry point that first needs it): every order of
+    the stage calls -- and a new input before the old pass finished -- still
+    gives the oracle's columns and tables."""
+    a = msa_mod.gen_corpus(3000, mode="zipf", seed=41)
+    b = msa_mod.gen_corpus(2500, mode="torture", seed=42)
+    exp = {}
+    for name, data in (("a", a), ("b", b)):
+        path = tmp_path / f"{name}.csv"
+        path.write_bytes(data)
+        r = run_oracle(str(path), str(tmp_path / f"o_{name}"), ranks=1)
+        assert r.returncode == 0, r.stderr
+        exp[name] = read_outputs(str(tmp_path / f"o_{name}"))
+
+    def check_split(name):
+        s = ctx.summary()
+        assert ctx.split_column(0) == exp[name]["split"][s.artist_file + ".csv"]
+        assert ctx.split_column(1) == exp[name]["split"][s.text_file + ".csv"]
+
+    def check_tables(name):
+        assert msa_mod.table_csv_bytes(ctx.ranked(msa_mod.MSA_TABLE_WORDS), "word") == exp[name]["word_counts.csv"]
+        assert msa_mod.table_csv_bytes(ctx.ranked(msa_mod.MSA_TABLE_ARTISTS), "artist") == exp[name]["top_artists.csv"]
+
+    ctx.load_csv(a)
+    ctx.split_columns(text_column=True)
+    check_split("a")                        # split only: the entry point launches it
+    ctx.load_csv(b)
+    ctx.split_columns(text_column=True)
+    ctx.count()                             # launched beside the artist pass
+    check_split("b")
+    ctx.rank()
+    check_tables("b")
+    ctx.load_csv(a)
+    ctx.run(text_column=True)               # joined at the end of the run
+    ctx.load_csv(b)                         # a new input right after
+    ctx.run(text_column=True)
+    check_split("b")
+    check_tables("b")
+
+
 def test_empty_file_fails_loudly(msa_mod, ctx):
     ctx.load_csv(b"")
     with pytest.raises(msa_mod.MsaError) as e:
