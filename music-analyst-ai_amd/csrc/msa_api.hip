@@ -926,6 +926,7 @@ static int wipe_long_table(msa_ctx *c) {
 static int do_count(msa_ctx *c) {
     int rc;
     if (c->stage < 1) return fail(c, MSA_ERR_ARG, "msa_count before msa_split_columns");
+    if (c->stage >= 2) return MSA_OK;  // already counted: the tables are final (a second pass would add twice)
     // a label with a '\n' (its rest is read as artist records): records != lines
     bool exact = c->artist_exact || c->artist_piece_set || c->a_hdr_getline < c->a_hdr_len;
     const u64 nl = std::min<u64>(c->h_ctr.l_occ, c->l_occ_cap);  // final since the split's read-back

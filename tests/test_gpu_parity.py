@@ -177,6 +177,9 @@ def test_text_column_stage_orders(msa_mod, ctx, tmp_path):
     check_split("b")
     ctx.rank()
     check_tables("b")
+    ctx.count()                             # a second count changes nothing
+    ctx.rank()
+    check_tables("b")
     ctx.load_csv(a)
     ctx.run(text_column=True)               # joined at the end of the run
     ctx.load_csv(b)                         # a new input right after
