@@ -694,8 +694,15 @@ __global__ __launch_bounds__(Q_T, 1) void k_scan_csv(ScanArgs a) {
 // k_miss_agg: workgroup (partition p, group g) counts partition p of the
 // logs of K3 workgroups g, g + G, ... in an LDS table (the whole LDS: ~8000
 // 16-byte keys), then adds each distinct key once to the HBM tables.
+#ifndef MA_T
 #define MA_T 1024
+#endif
+#ifndef MA_SLOTS
 #define MA_SLOTS 8176
+#endif
+#ifndef MA_FLY
+#define MA_FLY 4  // log entries in flight per thread
+#endif
 #define MA_NB (MA_SLOTS / 4)
 __device__ __forceinline__ u32 ma_find(ulonglong2 *keys, u64 k0, u64 k1) {
     u32 h = (u32)k0 * 0x9E3779B1u + (u32)(k0 >> 32) * 0x85EBCA77u + (u32)k1 * 0xC2B2AE3Du + (u32)(k1 >> 32);
@@ -747,15 +754,15 @@ __global__ __launch_bounds__(MA_T) void k_miss_agg(ScanArgs a, u32 nsrc, u32 gro
         if (threadIdx.x == 0 && n) atomicAdd((unsigned long long *)&a.ctr->k3_misses, (unsigned long long)n);
         // four entries per thread in flight: their loads are issued before
         // the first LDS probe
-        for (u32 i0 = threadIdx.x; i0 < n; i0 += 4 * MA_T) {
-            ulonglong2 xs[4];
+        for (u32 i0 = threadIdx.x; i0 < n; i0 += MA_FLY * MA_T) {
+            ulonglong2 xs[MA_FLY];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
+            for (int q = 0; q < MA_FLY; ++q) {
                 const u32 i = i0 + q * MA_T;
                 xs[q] = i < n ? a.mlog[base + i] : make_ulonglong2(0, 0);
             }
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
+            for (int q = 0; q < MA_FLY; ++q) {
                 if (i0 + q * MA_T >= n) break;
                 const ulonglong2 x = xs[q];
                 const u32 c = gather8(x.x) | ((gather8(x.y) & 0x7Fu) << 8);
@@ -800,7 +807,10 @@ hipError_t msa_launch_scan_csv(const ScanArgs &a, hipStream_t s) {
 hipError_t msa_launch_miss_agg(const ScanArgs &a, hipStream_t s) {
     if (!a.nchunks) return hipSuccess;
     const u32 blocks = scan_blocks(a);
-    const u32 groups = std::max<u32>(1, std::min<u32>(blocks, (u32)g_q_cus / MSA_MLOG_PARTS));
+#ifndef MA_GROUP_MUL
+#define MA_GROUP_MUL 1  // aggregating workgroups per CU
+#endif
+    const u32 groups = std::max<u32>(1, std::min<u32>(blocks, MA_GROUP_MUL * (u32)g_q_cus / MSA_MLOG_PARTS));
     hipLaunchKernelGGL(k_miss_agg, dim3(groups * MSA_MLOG_PARTS), dim3(MA_T), MA_SLOTS * 20, s, a, blocks, groups);
     return hipGetLastError();
 }
