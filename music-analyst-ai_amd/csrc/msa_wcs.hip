@@ -81,6 +81,7 @@ struct WCtr {
     u64 overflow;
     u64 collision;
     u64 listed;
+    u64 fallback;   // rows k_wcs_wrows left to the per-thread walk
 };
 
 __host__ __device__ __forceinline__ u32 tpk(u32 b, u32 d) {  // d: the delimiter byte
@@ -393,6 +394,8 @@ struct RowArgs {
     u64 *nd;        // distinct words per row
     u64 *spans;     // 4 per row: artist start/end, song start/end (raw)
     WCtr *ctr;
+    const u64 *rows;  // k_wcs_rows: the rows to walk (null: every row)
+    u64 *fb;          // k_wcs_wrows: rows it leaves to k_wcs_rows
     int ablate;     // timing diagnostics only (MSA_WCS_ABLATE): 1 no token loop, 4 no per-row
                     // table -- results are wrong when set (never skip the word update: the
                     // ranking kernels read the first-occurrence spans it writes)
@@ -628,8 +631,295 @@ __global__ __launch_bounds__(256) void k_wcs_rows(RowArgs a) {
     WgAgg agg{l_id, l_cnt, l_h2, l_first, l_rows};
     // row k of the file spans [rend[k], rend[k+1]); kernel index r = k + 1,
     // r = 1 is the header row
-    const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x + 2;
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    const u64 r = a.rows ? (i < a.ctr->fallback ? a.rows[i] : a.nrows) : i + 2;
     if (r < a.nrows) wcs_row(a, agg, r);
+    __syncthreads();
+    for (u32 k = threadIdx.x; k < LW; k += blockDim.x) {
+        const u32 id = l_id[k];
+        if (!id) continue;
+        u64 *gt = a.gtab + (u64)(id - 1) * 4;
+        atomicAdd((unsigned long long *)(gt + 3), (unsigned long long)l_cnt[k]);
+        atomicMax((unsigned long long *)(gt + 2), (unsigned long long)l_first[k]);
+        const u64 h2v = l_h2[k];
+        const u64 o = atomicCAS((unsigned long long *)(gt + 1), 0ull, (unsigned long long)h2v);
+        if (o != 0 && o != h2v) atomicAdd((unsigned long long *)&a.ctr->collision, 1ull);
+    }
+    if (threadIdx.x == 0) {
+        atomicAdd((unsigned long long *)&a.ctr->total_rows, (unsigned long long)l_rows[0]);
+        atomicAdd((unsigned long long *)&a.ctr->song_rows, (unsigned long long)l_rows[1]);
+        atomicAdd((unsigned long long *)&a.ctr->tokens, (unsigned long long)l_rows[2]);
+        if (l_rows[3]) atomicAdd((unsigned long long *)&a.ctr->collision, (unsigned long long)l_rows[3]);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Wave-per-row pass (the common case; k_wcs_rows walks what it leaves).
+// A wave takes WR_ROWS consecutive rows; a row of at most one 1 KiB window
+// (16 bytes per lane) is classified with SWAR masks.  Its quoting is
+// "standard" when every '"' sits where the reader's quote parity predicts a
+// structural or doubled quote:
+//   * a quote outside quotes (parity 0) follows the row start, a delimiter or
+//     another quote (the second of a doubled pair),
+//   * a quote inside quotes is followed by a quote, a delimiter, an end of line
+//     or the row end,
+//   * the row ends outside quotes, and ends of line outside quotes are only
+//     the row's own terminator.
+// Then parity 0 <=> the reader is outside a quoted field, the fields are
+// split by the delimiters at parity 0, no quote lies inside a token (so a
+// token's raw span is its bytes), and every quote is a token separator like
+// the character it stands for.  Other rows (and rows over 1 KiB or with more
+// than WR_TCAP token runs) go to the fallback list, before anything of theirs
+// is committed.  Tokens: one lane per token (start / end from LDS) hashes its
+// lower-cased bytes (same TokHash as k_wcs_rows), claims the global slot and
+// updates the workgroup aggregate; the row's Counter is a per-wave LDS table
+// (count, first occurrence), written out in first-occurrence order.
+constexpr u32 WR_W = 8, WR_ROWS = 64, WR_TCAP = 192, WR_DCAP = 256;
+struct WrWave {
+    u32 row[264];          // the row window (1 KiB) + 32 bytes of zeros
+    u32 dkey[WR_DCAP];     // word id (slot + 1)
+    u32 dcnt[WR_DCAP];
+    u32 dfirst[WR_DCAP];   // order of the first token
+    u16 ts[WR_TCAP], te[WR_TCAP];
+    u32 fpos[8];           // start / end of the artist, song, text fields
+};
+
+__device__ __forceinline__ u32 wr_mask(u64 lb, u64 lo, u64 hi) {  // bits j with lb + j in [lo, hi)
+    const u64 a = lo > lb ? (lo - lb < 16 ? lo - lb : 16) : 0;
+    const u64 b = hi > lb ? (hi - lb < 16 ? hi - lb : 16) : 0;
+    return ((1u << b) - 1u) & ~((1u << a) - 1u);
+}
+__device__ __forceinline__ u32 pack16(const u32 m[4]) {
+    return swar_pack4(m[0]) | (swar_pack4(m[1]) << 4) | (swar_pack4(m[2]) << 8) | (swar_pack4(m[3]) << 12);
+}
+// 0x80 per byte in [0x41, 0x5A] or [0x80, 0x9E] (the bytes a token lower-cases by + 0x20)
+__device__ __forceinline__ u32 swar_upper(u32 x) {
+    const u32 x7 = x & 0x7F7F7F7Fu;
+    const u32 up = (x7 + 0x3F3F3F3Fu) & ~(x7 + 0x25252525u) & ~x;
+    const u32 c3 = ~(x7 + 0x61616161u) & x;
+    return (up | c3) & 0x80808080u;
+}
+
+// returns false (nothing written) when the row needs the per-thread walk
+__device__ __forceinline__ bool wr_row(const RowArgs &a, WgAgg &agg, WrWave &W, u64 r, u64 rs, u64 re, uint4 v,
+                                       u64 &n_rows, u64 &n_song, u64 &n_tok) {
+    const u32 lane = lane_id();
+    const u64 base = rs & ~15ull;
+    if (re - base > 1024) return false;
+    const u64 lb = base + 16 * lane;
+    const u32 V = wr_mask(lb, rs, re);
+    const u32 w[4] = {v.x, v.y, v.z, v.w};
+    u32 mq[4], md[4], me[4], mt[4], mc3[4], m2[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const u32 x = w[k], x7 = x & 0x7F7F7F7Fu;
+        mq[k] = eq80x(x, x7, '"');
+        md[k] = eq80x(x, x7, a.delim);
+        me[k] = eq80x(x, x7, '\n') | eq80x(x, x7, '\r');
+        mt[k] = tok80x(x, x7);
+        mc3[k] = swar_eq(x, 0xC3);
+        // second byte of a token 0xC3 pair: 0x80..0xBF minus 0x97 / 0xB7
+        m2[k] = x & ~(x << 1) & 0x80808080u & ~swar_eq(x, 0x97) & ~swar_eq(x, 0xB7);
+    }
+    const u32 Q = pack16(mq) & V, D = pack16(md) & V, E = pack16(me) & V;
+    const u32 C3 = pack16(mc3) & V, T2 = pack16(m2) & V, TA = pack16(mt) & V;
+    // neighbours: bit 15 of the lane below, bit 0 of the lane above
+    const u32 lo_bits = (D >> 15) | ((Q >> 15) << 1) | ((C3 >> 15) << 2);
+    const u32 hi_bits = (Q & 1u) | ((D & 1u) << 1) | ((E & 1u) << 2) | ((T2 & 1u) << 3);
+    u32 pb = __shfl_up(lo_bits, 1), nb = __shfl_down(hi_bits, 1);
+    if (lane == 0) pb = 0;
+    if (lane == 63) nb = 0;
+    // quote parity before each byte
+    const u64 qodd = __ballot(__popc(Q) & 1u);
+    const u32 carry = (u32)__popcll(qodd & ((1ull << lane) - 1ull)) & 1u;
+    const u32 P = pxor_excl16(Q) ^ (carry ? 0xFFFFu : 0u);
+    const u32 sbit = wr_mask(lb, rs, rs + 1), ebit = wr_mask(lb, re - 1, re);
+    const u32 prevD = (D << 1) | (pb & 1u), prevQ = (Q << 1) | ((pb >> 1) & 1u);
+    const u32 nextQ = (Q >> 1) | ((nb & 1u) << 15), nextD = (D >> 1) | (((nb >> 1) & 1u) << 15);
+    const u32 nextE = (E >> 1) | (((nb >> 2) & 1u) << 15);
+    const u32 E0 = E & ~P;
+    u32 bad = (Q & ~P & ~(prevD | prevQ | sbit)) | (Q & P & ~(nextQ | nextD | nextE | ebit));
+    bad |= E0 & ~(ebit | wr_mask(lb, re - 2, re - 1));
+    if (__ballot(bad != 0) || (__popcll(qodd) & 1)) return false;
+    // blank line (only its terminator): DictReader skips it
+    if (__ballot((E0 & sbit) != 0)) {
+        if (lane == 0) a.nd[r] = 0;
+        return true;
+    }
+    // fields: delimiters outside quotes
+    const u32 D0 = D & ~P;
+    u32 nd0;
+    const u32 dpre = wave_prefix<5>((u32)__popc(D0), nd0);
+    const u64 e0 = __ballot(E0 != 0);
+    const u64 feol = e0 ? readlane64(lb + (u32)__builtin_ctz(E0 ? E0 : 1u), (int)__builtin_ctzll(e0)) : re;
+    const u32 fi[3] = {a.ia, a.isg, a.it};
+    if (lane < 6) {
+        const u32 fl = lane < 2 ? a.ia : (lane < 4 ? a.isg : a.it);
+        W.fpos[lane] = (lane & 1) ? (u32)(feol - base) : (fl == 0 ? (u32)(rs - base) : 0u);
+    }
+    __builtin_amdgcn_wave_barrier();
+    for (u32 m = D0, j = dpre; m; m &= m - 1, ++j) {
+        const u32 pos = (u32)(lb - base) + (u32)__builtin_ctz(m);
+#pragma unroll
+        for (int f = 0; f < 3; ++f) {
+            if (j + 1 == fi[f]) W.fpos[2 * f] = pos + 1;
+            if (j == fi[f]) W.fpos[2 * f + 1] = pos;
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    const u32 nf = nd0 + 1;
+    const u64 ts = base + W.fpos[4], te = base + W.fpos[5];
+    // token bytes of the text field (a 0xC3 pair counts when its second byte does)
+    const u32 R = nf > a.it ? wr_mask(lb, ts, te) : 0u;
+    const u32 lead = C3 & ((T2 >> 1) | (((nb >> 3) & 1u) << 15));
+    const u32 sec = T2 & ((C3 << 1) | ((pb >> 2) & 1u));
+    const u32 TB = (TA | lead | sec) & R;
+    u32 pt = __shfl_up(TB >> 15, 1), nt = __shfl_down(TB & 1u, 1);
+    if (lane == 0) pt = 0;
+    if (lane == 63) nt = 0;
+    const u32 TS = TB & ~((TB << 1) | pt), TE = TB & ~((TB >> 1) | (nt << 15));
+    u32 ntok;
+    const u32 tpre = wave_prefix<5>((u32)__popc(TS), ntok);
+    if (ntok > WR_TCAP) return false;
+    // ---- committed from here on
+    {
+        u32 *row = W.row;
+        row[4 * lane] = v.x; row[4 * lane + 1] = v.y; row[4 * lane + 2] = v.z; row[4 * lane + 3] = v.w;
+        if (lane < 8) row[256 + lane] = 0;
+    }
+    for (u32 m = TS, j = tpre; m; m &= m - 1, ++j) W.ts[j] = (u16)((u32)(lb - base) + (u32)__builtin_ctz(m));
+    u32 tot_e;  // the k-th end closes the k-th start
+    const u32 je = wave_prefix<5>((u32)__popc(TE), tot_e);
+    for (u32 m = TE, j = je; m; m &= m - 1, ++j) W.te[j] = (u16)((u32)(lb - base) + (u32)__builtin_ctz(m) + 1u);
+    for (u32 k = lane; k < WR_DCAP; k += 64) { W.dkey[k] = 0; W.dcnt[k] = 0; W.dfirst[k] = ~0u; }
+    __builtin_amdgcn_wave_barrier();
+    // tokens, one per lane
+    u32 nval = 0;
+    for (u32 t0 = 0; t0 < ntok; t0 += 64) {
+        const u32 t = t0 + lane;
+        bool ok = false;
+        u64 key = 0, h2v = 0;
+        u32 s = 0, len = 0;
+        if (t < ntok) {
+            s = W.ts[t];
+            len = W.te[t] - s;
+            TokHash th;
+            th.reset();
+            th.len = len;
+            u32 c3 = 0;
+            bool alnum = false;
+            for (u32 o = 0; o < len; o += 8) {
+                const u32 q = (s + o) >> 2, sh = (s + o) & 3u;
+                const u32 w0 = W.row[q], w1 = W.row[q + 1], w2 = W.row[q + 2];
+                u32 x0 = __builtin_amdgcn_alignbyte(w1, w0, sh), x1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
+                const u32 nbt = len - o < 8 ? len - o : 8;
+                const u32 k0 = nbt >= 4 ? 0xFFFFFFFFu : ((1u << (8 * nbt)) - 1u);
+                const u32 k1 = nbt >= 8 ? 0xFFFFFFFFu : (nbt <= 4 ? 0u : ((1u << (8 * (nbt - 4))) - 1u));
+                x0 &= k0;
+                x1 &= k1;
+                c3 += __popc(swar_eq(x0, 0xC3) & k0 & 0x80808080u) + __popc(swar_eq(x1, 0xC3) & k1 & 0x80808080u);
+                alnum |= ((~swar_eq(x0, '\'') & k0) | (~swar_eq(x1, '\'') & k1)) & 0x80808080u;
+                x0 |= swar_upper(x0) >> 2;
+                x1 |= swar_upper(x1) >> 2;
+                th.acc = ((u64)x1 << 32) | x0;
+                if (nbt == 8) th.absorb();
+                else th.nacc = nbt;
+            }
+            ok = alnum && len - c3 >= 3;
+            if (ok) { key = th.key(); h2v = th.check(); }
+        }
+        const u64 okm = __ballot(ok);
+        const u32 ord = nval + mbcnt(okm);
+        nval += (u32)__popcll(okm);
+        u32 h = 0xFFFFu;
+        if (ok) {
+            const u64 slot = g_insert(a, key);
+            if (slot != ~0ull) {  // else overflow: the run repeats with a larger table
+                word_update(a, agg, slot, h2v, ~(((base + s) << 20) | (u64)len));
+                const u32 id = (u32)slot + 1;
+                h = (id * 0x9E3779B1u) >> 24;
+                for (;;) {
+                    u32 cur = W.dkey[h];
+                    if (cur == 0) {
+                        const u32 old = atomicCAS(&W.dkey[h], 0u, id);
+                        cur = old == 0 ? id : old;
+                    }
+                    if (cur == id) break;
+                    h = (h + 1) & (WR_DCAP - 1);
+                }
+                atomicAdd(&W.dcnt[h], 1u);
+                atomicMin(&W.dfirst[h], ord);
+            }
+        }
+        if (t < ntok) { W.ts[t] = (u16)h; W.te[t] = (u16)ord; }
+    }
+    __builtin_amdgcn_wave_barrier();
+    // the row's (word id, count) lines in first-occurrence order
+    u64 *lines = a.scratch + 2 * rs + (re - rs) / 4 + 1;
+    u32 nd = 0;
+    for (u32 t0 = 0; t0 < ntok; t0 += 64) {
+        const u32 t = t0 + lane;
+        bool lead_t = false;
+        u32 h = 0;
+        if (t < ntok) {
+            h = W.ts[t];
+            lead_t = h != 0xFFFFu && W.dfirst[h] == W.te[t];
+        }
+        const u64 lm = __ballot(lead_t);
+        if (lead_t) lines[nd + mbcnt(lm)] = ((u64)W.dkey[h] << 32) | W.dcnt[h];
+        nd += (u32)__popcll(lm);
+    }
+    if (lane == 0) {
+        if (nf <= a.need) wcs_err(a.ctr, r, E_SHORT);
+        a.nd[r] = nd;
+        u64 *o = a.spans + r * 4;
+        o[0] = base + W.fpos[0]; o[1] = base + W.fpos[1]; o[2] = base + W.fpos[2]; o[3] = base + W.fpos[3];
+    }
+    ++n_rows;
+    if (nd) { ++n_song; n_tok += nval; }
+    __builtin_amdgcn_wave_barrier();
+    return true;
+}
+
+__global__ __launch_bounds__(WR_W * 64) void k_wcs_wrows(RowArgs a) {
+    __shared__ u32 l_id[LW], l_cnt[LW];
+    __shared__ u64 l_h2[LW], l_first[LW], l_rows[4];
+    __shared__ WrWave l_w[WR_W];
+    for (u32 k = threadIdx.x; k < LW; k += blockDim.x) { l_id[k] = 0; l_cnt[k] = 0; l_h2[k] = 0; l_first[k] = 0; }
+    if (threadIdx.x < 4) l_rows[threadIdx.x] = 0;
+    __syncthreads();
+    WgAgg agg{l_id, l_cnt, l_h2, l_first, l_rows};
+    const u32 lane = lane_id(), wv = threadIdx.x >> 6;
+    WrWave &W = l_w[wv];
+    const u64 r0 = 2 + ((u64)blockIdx.x * WR_W + wv) * WR_ROWS;
+    u64 n_rows = 0, n_song = 0, n_tok = 0;
+    if (r0 < a.nrows) {
+        const u64 rl = a.nrows - r0 < WR_ROWS ? a.nrows : r0 + WR_ROWS;
+        // lane k: start of row r0 + k (= end of row r0 + k - 1); the last end apart
+        const u64 mys = r0 + lane < rl ? a.rend[r0 - 1 + lane] : 0;
+        const u64 last = a.rend[rl - 1];
+        u64 rs = readlane64(mys, 0), re = rl > r0 + 1 ? readlane64(mys, 1) : last;
+        uint4 v = *(const uint4 *)(a.buf + (rs & ~15ull) + 16 * lane);
+        for (u64 r = r0; r < rl; ++r) {
+            // the next row's window is in flight while this one is processed
+            const u32 k = (u32)(r - r0);
+            const u64 ns = re, ne = r + 2 < rl ? readlane64(mys, (int)k + 2) : last;
+            uint4 nv = make_uint4(0, 0, 0, 0);
+            if (r + 1 < rl) nv = *(const uint4 *)(a.buf + (ns & ~15ull) + 16 * lane);
+            if (!wr_row(a, agg, W, r, rs, re, v, n_rows, n_song, n_tok) && lane == 0) {
+                const u64 i = atomicAdd((unsigned long long *)&a.ctr->fallback, 1ull);
+                a.fb[i] = r;
+            }
+            rs = ns;
+            re = ne;
+            v = nv;
+        }
+    }
+    if (lane == 0 && n_rows) {
+        atomicAdd((unsigned long long *)&l_rows[0], (unsigned long long)n_rows);
+        atomicAdd((unsigned long long *)&l_rows[1], (unsigned long long)n_song);
+        atomicAdd((unsigned long long *)&l_rows[2], (unsigned long long)n_tok);
+    }
     __syncthreads();
     for (u32 k = threadIdx.x; k < LW; k += blockDim.x) {
         const u32 id = l_id[k];
@@ -945,8 +1235,8 @@ struct msa_wcs {
     u8 *d_ccout = nullptr;
     bool cc_have = false;
     // scratch owned by the run
-    void *scr[24] = {nullptr};  // grow-only pool: buffers persist across runs
-    u64 scr_cap[24] = {0};
+    void *scr[26] = {nullptr};  // grow-only pool: buffers persist across runs
+    u64 scr_cap[26] = {0};
 };
 
 static int wfail(msa_wcs *w, int code, const char *fmt, ...) {
@@ -1236,6 +1526,8 @@ extern "C" int msa_wcs_run(msa_wcs *w) {
     WCHECK(hipMemsetAsync(w->d_nd, 0, R * 8, st));
     u64 *scratch;
     WCHECK(wpool(w, 9, (2 * n + 64) * 8, scratch));
+    u64 *fb;
+    WCHECK(wpool(w, 24, R * 8, fb));
     u64 bits = w->gbits;
     if (!bits) {
         bits = 16;
@@ -1253,7 +1545,25 @@ extern "C" int msa_wcs_run(msa_wcs *w) {
         a.gtab = gtab; a.gmask = slots - 1; a.glimit = slots / 4 * 3;
         a.scratch = scratch; a.nd = w->d_nd; a.spans = w->d_spans; a.ctr = ctr;
         a.ablate = getenv("MSA_WCS_ABLATE") ? atoi(getenv("MSA_WCS_ABLATE")) : 0;
-        if (R > 2) hipLaunchKernelGGL(k_wcs_rows, grid1(R - 2), dim3(256), 0, st, a);
+        a.rows = nullptr;
+        a.fb = fb;
+        // wave per row first; the rows it leaves (long, unusual quoting, many
+        // token runs) are walked one thread per row (ablate bit 8: all of them)
+        if (R > 2 && !(a.ablate & 8)) {
+            const u64 per = (u64)WR_W * WR_ROWS;
+            hipLaunchKernelGGL(k_wcs_wrows, dim3((u32)((R - 2 + per - 1) / per)), dim3(WR_W * 64), 0, st, a);
+            WCHECK(hipGetLastError());
+            WCHECK(hipMemcpyAsync(&hc, ctr, sizeof hc, hipMemcpyDeviceToHost, st));
+            WCHECK(hipStreamSynchronize(st));
+            if (getenv("MSA_WCS_DEBUG")) fprintf(stderr, "k_wcs_wrows: %llu of %llu rows left to k_wcs_rows\n",
+                                                 (unsigned long long)hc.fallback, (unsigned long long)(R - 2));
+            if (hc.fallback) {
+                a.rows = fb;
+                hipLaunchKernelGGL(k_wcs_rows, grid1(hc.fallback), dim3(256), 0, st, a);
+            }
+        } else if (R > 2) {
+            hipLaunchKernelGGL(k_wcs_rows, grid1(R - 2), dim3(256), 0, st, a);
+        }
         WCHECK(hipGetLastError());
         WCHECK(hipMemcpyAsync(&hc, ctr, sizeof hc, hipMemcpyDeviceToHost, st));
         WCHECK(hipStreamSynchronize(st));
