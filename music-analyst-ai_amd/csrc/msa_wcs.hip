@@ -397,26 +397,40 @@ struct RowArgs {
     const u64 *rows;  // k_wcs_rows: the rows to walk (null: every row)
     u64 *fb;          // k_wcs_wrows: rows it leaves to k_wcs_rows
     int ablate;     // timing diagnostics only (MSA_WCS_ABLATE): 1 no token loop, 4 no per-row
-                    // table -- results are wrong when set (never skip the word update: the
-                    // ranking kernels read the first-occurrence spans it writes)
+                    // table, 8 no wave-per-row pass, 16 (wave pass) no global slot claim (no
+                    // words: nothing to rank), 32 neither the claim nor the workgroup aggregate
+                    // -- results are wrong when set
 };
 
-__device__ __forceinline__ u64 g_insert(const RowArgs &a, u64 key) {
+// The token's h2 against its slot's (set once by the first CAS); a second,
+// independent 64-bit hash, so a mismatch is a 64-bit h1 collision.
+__device__ __forceinline__ void h2_check(const RowArgs &a, u64 *gt, u64 seen, u64 h2v) {
+    if (seen == 0) seen = atomicCAS((unsigned long long *)(gt + 1), 0ull, (unsigned long long)h2v);
+    if (seen != 0 && seen != h2v) atomicAdd((unsigned long long *)&a.ctr->collision, 1ull);
+}
+// Global slot of a word: `cur` = the (key, h2) pair at key & gmask, loaded by
+// the caller (its load can be in flight while the caller does LDS work).
+__device__ __forceinline__ ulonglong2 g_probe(const RowArgs &a, u64 key) {
+    return *(const ulonglong2 *)(a.gtab + (key & a.gmask) * 4);  // plain (cached) load: a key never
+                                                                 // changes once set; a stale 0 goes to the CAS
+}
+__device__ __forceinline__ u64 g_insert(const RowArgs &a, u64 key, u64 h2v, ulonglong2 cur) {
     u64 slot = key & a.gmask;
     for (u64 p = 0; p <= a.gmask; ++p) {
         u64 *k = a.gtab + slot * 4;
-        const u64 cur = *k;  // plain (cached) load: a key never changes once set; a stale 0 goes to the CAS
-        if (cur == key) return slot;
-        if (cur == 0) {
+        if (cur.x == key) { h2_check(a, k, cur.y, h2v); return slot; }
+        if (cur.x == 0) {
             const u64 old = atomicCAS((unsigned long long *)k, 0ull, (unsigned long long)key);
             if (old == 0) {
                 const u64 d = atomicAdd((unsigned long long *)&a.ctr->distinct, 1ull);
                 if (d >= a.glimit) atomicOr((unsigned long long *)&a.ctr->overflow, (unsigned long long)OVF_G);
+                h2_check(a, k, 0, h2v);
                 return slot;
             }
-            if (old == key) return slot;
+            if (old == key) { h2_check(a, k, 0, h2v); return slot; }
         }
         slot = (slot + 1) & a.gmask;
+        cur = *(const ulonglong2 *)(a.gtab + slot * 4);
     }
     atomicOr((unsigned long long *)&a.ctr->overflow, (unsigned long long)OVF_G);
     return ~0ull;
@@ -428,22 +442,22 @@ __device__ __forceinline__ void wcs_err(WCtr *ctr, u64 row, u32 code) {
 
 // Workgroup-private aggregation of the global word updates (the Zipf head
 // would otherwise serialise every token on a few device-scope atomics): per
-// word seen by the workgroup, LDS holds the count, the max of ~first and the
-// first token's h2 (a second, independent 64-bit hash: every token's h2 must
-// equal it, which catches 64-bit h1 collisions).  Flushed once per workgroup.
+// word seen by the workgroup, LDS holds the count and the max of ~first.
+// Flushed once per workgroup.  (The h2 check is g_insert's.)
 constexpr u32 LW = 2048, LW_PROBE = 8;
 struct WgAgg {
     u32 *id;
     u32 *cnt;
-    u64 *h2;
     u64 *first;
-    u64 *rows;  // [0] rows, [1] song rows, [2] tokens, [3] collisions
+    u64 *rows;  // [0] rows, [1] song rows, [2] tokens
 };
 
-__device__ __forceinline__ void word_update(const RowArgs &a, WgAgg &g, u64 slot, u64 h2v, u64 nfirst) {
+template <u32 N = LW>
+__device__ __forceinline__ void word_update(const RowArgs &a, WgAgg &g, u64 slot, u64 nfirst) {
+    static_assert((N & (N - 1)) == 0 && N >= 256, "LDS aggregate size");
     const u32 id = (u32)slot + 1;
-    u32 h = (id * 0x9E3779B1u) >> 21;
-    for (u32 p = 0; p < LW_PROBE; ++p, h = (h + 1) & (LW - 1)) {
+    u32 h = (id * 0x9E3779B1u) >> (32 - __builtin_ctz(N));
+    for (u32 p = 0; p < LW_PROBE; ++p, h = (h + 1) & (N - 1)) {
         u32 cur = g.id[h];
         if (cur == 0) {
             const u32 old = atomicCAS(&g.id[h], 0u, id);
@@ -451,18 +465,29 @@ __device__ __forceinline__ void word_update(const RowArgs &a, WgAgg &g, u64 slot
         }
         if (cur != id) continue;
         atomicAdd(&g.cnt[h], 1u);
-        // first / h2 change rarely: plain LDS reads filter out most atomics
+        // first changes rarely: a plain LDS read filters out most atomics
         if (nfirst > g.first[h]) atomicMax((unsigned long long *)&g.first[h], (unsigned long long)nfirst);
-        u64 o = g.h2[h];
-        if (o == 0) o = atomicCAS((unsigned long long *)&g.h2[h], 0ull, (unsigned long long)h2v);
-        if (o != 0 && o != h2v) atomicAdd((unsigned long long *)&g.rows[3], 1ull);
         return;
     }
     u64 *gt = a.gtab + slot * 4;  // LDS table full here: straight to HBM
     atomicAdd((unsigned long long *)(gt + 3), 1ull);
     atomicMax((unsigned long long *)(gt + 2), (unsigned long long)nfirst);
-    const u64 o = atomicCAS((unsigned long long *)(gt + 1), 0ull, (unsigned long long)h2v);
-    if (o != 0 && o != h2v) atomicAdd((unsigned long long *)&a.ctr->collision, 1ull);
+}
+
+// flush of a workgroup's aggregate
+__device__ __forceinline__ void agg_flush(const RowArgs &a, const WgAgg &g, u32 n) {
+    for (u32 k = threadIdx.x; k < n; k += blockDim.x) {
+        const u32 id = g.id[k];
+        if (!id) continue;
+        u64 *gt = a.gtab + (u64)(id - 1) * 4;
+        atomicAdd((unsigned long long *)(gt + 3), (unsigned long long)g.cnt[k]);
+        atomicMax((unsigned long long *)(gt + 2), (unsigned long long)g.first[k]);
+    }
+    if (threadIdx.x == 0) {
+        atomicAdd((unsigned long long *)&a.ctr->total_rows, (unsigned long long)g.rows[0]);
+        atomicAdd((unsigned long long *)&a.ctr->song_rows, (unsigned long long)g.rows[1]);
+        atomicAdd((unsigned long long *)&a.ctr->tokens, (unsigned long long)g.rows[2]);
+    }
 }
 
 __device__ __forceinline__ void wcs_row(const RowArgs &a, WgAgg &agg, u64 r) {
@@ -596,9 +621,9 @@ __device__ __forceinline__ void wcs_row(const RowArgs &a, WgAgg &agg, u64 r) {
         for (u32 k = 0; k < rcap; ++k) rt[k] = 0;
         for (u32 t = 0; t < ntok; ++t) {
             const u64 key = sc[3 * t], h2v = sc[3 * t + 1], nfirst = sc[3 * t + 2];
-            const u64 slot = g_insert(a, key);
+            const u64 slot = g_insert(a, key, h2v, g_probe(a, key));
             if (slot == ~0ull) continue;  // overflow: the run repeats with a larger table
-            word_update(a, agg, slot, h2v, nfirst);
+            word_update(a, agg, slot, nfirst);
             if (a.ablate & 4) continue;
             const u64 id = slot + 1;
             u32 h = (u32)(((id * 0x9E3779B97F4A7C15ull) >> 32) % rcap);
@@ -624,33 +649,18 @@ __device__ __forceinline__ void wcs_row(const RowArgs &a, WgAgg &agg, u64 r) {
 
 __global__ __launch_bounds__(256) void k_wcs_rows(RowArgs a) {
     __shared__ u32 l_id[LW], l_cnt[LW];
-    __shared__ u64 l_h2[LW], l_first[LW], l_rows[4];
-    for (u32 k = threadIdx.x; k < LW; k += blockDim.x) { l_id[k] = 0; l_cnt[k] = 0; l_h2[k] = 0; l_first[k] = 0; }
+    __shared__ u64 l_first[LW], l_rows[4];
+    for (u32 k = threadIdx.x; k < LW; k += blockDim.x) { l_id[k] = 0; l_cnt[k] = 0; l_first[k] = 0; }
     if (threadIdx.x < 4) l_rows[threadIdx.x] = 0;
     __syncthreads();
-    WgAgg agg{l_id, l_cnt, l_h2, l_first, l_rows};
+    WgAgg agg{l_id, l_cnt, l_first, l_rows};
     // row k of the file spans [rend[k], rend[k+1]); kernel index r = k + 1,
     // r = 1 is the header row
     const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     const u64 r = a.rows ? (i < a.ctr->fallback ? a.rows[i] : a.nrows) : i + 2;
     if (r < a.nrows) wcs_row(a, agg, r);
     __syncthreads();
-    for (u32 k = threadIdx.x; k < LW; k += blockDim.x) {
-        const u32 id = l_id[k];
-        if (!id) continue;
-        u64 *gt = a.gtab + (u64)(id - 1) * 4;
-        atomicAdd((unsigned long long *)(gt + 3), (unsigned long long)l_cnt[k]);
-        atomicMax((unsigned long long *)(gt + 2), (unsigned long long)l_first[k]);
-        const u64 h2v = l_h2[k];
-        const u64 o = atomicCAS((unsigned long long *)(gt + 1), 0ull, (unsigned long long)h2v);
-        if (o != 0 && o != h2v) atomicAdd((unsigned long long *)&a.ctr->collision, 1ull);
-    }
-    if (threadIdx.x == 0) {
-        atomicAdd((unsigned long long *)&a.ctr->total_rows, (unsigned long long)l_rows[0]);
-        atomicAdd((unsigned long long *)&a.ctr->song_rows, (unsigned long long)l_rows[1]);
-        atomicAdd((unsigned long long *)&a.ctr->tokens, (unsigned long long)l_rows[2]);
-        if (l_rows[3]) atomicAdd((unsigned long long *)&a.ctr->collision, (unsigned long long)l_rows[3]);
-    }
+    agg_flush(a, agg, LW);
 }
 
 // ---------------------------------------------------------------------------
@@ -674,14 +684,45 @@ __global__ __launch_bounds__(256) void k_wcs_rows(RowArgs a) {
 // lower-cased bytes (same TokHash as k_wcs_rows), claims the global slot and
 // updates the workgroup aggregate; the row's Counter is a per-wave LDS table
 // (count, first occurrence), written out in first-occurrence order.
-constexpr u32 WR_W = 8, WR_ROWS = 64, WR_TCAP = 192, WR_DCAP = 256;
+#ifndef WR_LW
+#define WR_LW 1024  // workgroup aggregate of k_wcs_wrows (two workgroups per CU)
+#endif
+#ifndef WR_WAVES
+#define WR_WAVES 8  // waves per workgroup
+#endif
+#ifndef WR_PIPE
+#define WR_PIPE 0   // 1: the front half of row r runs before the back half of row r - 1
+#endif
+#ifndef WR_OCC
+#define WR_OCC 0    // waves per SIMD the register budget is held to (0: the compiler's choice)
+#endif
+constexpr u32 WR_W = WR_WAVES, WR_ROWS = 64, WR_TCAP = 64, WR_DCAP = 128;
+// A row's Counter (its words' keys, global slots, counts, first tokens): two
+// per wave, the row in the front half and the row in the back half.
+struct WrTable {
+    u64 key[WR_DCAP];
+    u32 slot[WR_DCAP];
+    u32 cnt[WR_DCAP];
+    u32 first[WR_DCAP];
+};
 struct WrWave {
+    WrTable tab[2];
     u32 row[264];          // the row window (1 KiB) + 32 bytes of zeros
-    u32 dkey[WR_DCAP];     // word id (slot + 1)
-    u32 dcnt[WR_DCAP];
-    u32 dfirst[WR_DCAP];   // order of the first token
     u16 ts[WR_TCAP], te[WR_TCAP];
     u32 fpos[8];           // start / end of the artist, song, text fields
+};
+// What the back half of a row needs from its front half: the row (uniform)
+// and this lane's token (one token per lane).
+struct WrRow {
+    u64 r, rs, re;
+    u32 span[4];           // artist / song start, end (offsets from base)
+    u64 base;
+    u32 nf, nval;
+    u64 key, h2v;
+    ulonglong2 cur;        // the (key, h2) probe of the global table, in flight
+    u32 sl;                // token start (offset from base) << 11 | length
+    u32 h, ord;
+    bool ok;
 };
 
 __device__ __forceinline__ u32 wr_mask(u64 lb, u64 lo, u64 hi) {  // bits j with lb + j in [lo, hi)
@@ -700,29 +741,31 @@ __device__ __forceinline__ u32 swar_upper(u32 x) {
     return (up | c3) & 0x80808080u;
 }
 
-// returns false (nothing written) when the row needs the per-thread walk
-__device__ __forceinline__ bool wr_row(const RowArgs &a, WgAgg &agg, WrWave &W, u64 r, u64 rs, u64 re, uint4 v,
-                                       u64 &n_rows, u64 &n_song, u64 &n_tok) {
+enum : int { WR_FALLBACK = 0, WR_BLANK = 1, WR_OK = 2 };
+// Front half: classify, split, tokenize, hash, count into the row table T,
+// and issue the global-table probe.  Nothing global is written; WR_FALLBACK
+// leaves the row to the per-thread walk.
+__device__ __forceinline__ int wr_front(const RowArgs &a, WrWave &W, WrTable &T, u64 r, u64 rs, u64 re, uint4 v,
+                                        WrRow &o) {
     const u32 lane = lane_id();
     const u64 base = rs & ~15ull;
-    if (re - base > 1024) return false;
+    if (re - base > 1024) return WR_FALLBACK;
     const u64 lb = base + 16 * lane;
     const u32 V = wr_mask(lb, rs, re);
     const u32 w[4] = {v.x, v.y, v.z, v.w};
-    u32 mq[4], md[4], me[4], mt[4], mc3[4], m2[4];
+    u32 Q = 0, D = 0, E = 0, C3 = 0, T2 = 0, TA = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const u32 x = w[k], x7 = x & 0x7F7F7F7Fu;
-        mq[k] = eq80x(x, x7, '"');
-        md[k] = eq80x(x, x7, a.delim);
-        me[k] = eq80x(x, x7, '\n') | eq80x(x, x7, '\r');
-        mt[k] = tok80x(x, x7);
-        mc3[k] = swar_eq(x, 0xC3);
+        Q |= swar_pack4(eq80x(x, x7, '"')) << (4 * k);
+        D |= swar_pack4(eq80x(x, x7, a.delim)) << (4 * k);
+        E |= swar_pack4(eq80x(x, x7, '\n') | eq80x(x, x7, '\r')) << (4 * k);
+        TA |= swar_pack4(tok80x(x, x7)) << (4 * k);
+        C3 |= swar_pack4(swar_eq(x, 0xC3)) << (4 * k);
         // second byte of a token 0xC3 pair: 0x80..0xBF minus 0x97 / 0xB7
-        m2[k] = x & ~(x << 1) & 0x80808080u & ~swar_eq(x, 0x97) & ~swar_eq(x, 0xB7);
+        T2 |= swar_pack4(x & ~(x << 1) & 0x80808080u & ~swar_eq(x, 0x97) & ~swar_eq(x, 0xB7)) << (4 * k);
     }
-    const u32 Q = pack16(mq) & V, D = pack16(md) & V, E = pack16(me) & V;
-    const u32 C3 = pack16(mc3) & V, T2 = pack16(m2) & V, TA = pack16(mt) & V;
+    Q &= V; D &= V; E &= V; C3 &= V; T2 &= V; TA &= V;
     // neighbours: bit 15 of the lane below, bit 0 of the lane above
     const u32 lo_bits = (D >> 15) | ((Q >> 15) << 1) | ((C3 >> 15) << 2);
     const u32 hi_bits = (Q & 1u) | ((D & 1u) << 1) | ((E & 1u) << 2) | ((T2 & 1u) << 3);
@@ -740,12 +783,9 @@ __device__ __forceinline__ bool wr_row(const RowArgs &a, WgAgg &agg, WrWave &W, 
     const u32 E0 = E & ~P;
     u32 bad = (Q & ~P & ~(prevD | prevQ | sbit)) | (Q & P & ~(nextQ | nextD | nextE | ebit));
     bad |= E0 & ~(ebit | wr_mask(lb, re - 2, re - 1));
-    if (__ballot(bad != 0) || (__popcll(qodd) & 1)) return false;
+    if (__ballot(bad != 0) || (__popcll(qodd) & 1)) return WR_FALLBACK;
     // blank line (only its terminator): DictReader skips it
-    if (__ballot((E0 & sbit) != 0)) {
-        if (lane == 0) a.nd[r] = 0;
-        return true;
-    }
+    if (__ballot((E0 & sbit) != 0)) return WR_BLANK;
     // fields: delimiters outside quotes
     const u32 D0 = D & ~P;
     u32 nd0;
@@ -778,117 +818,125 @@ __device__ __forceinline__ bool wr_row(const RowArgs &a, WgAgg &agg, WrWave &W, 
     if (lane == 0) pt = 0;
     if (lane == 63) nt = 0;
     const u32 TS = TB & ~((TB << 1) | pt), TE = TB & ~((TB >> 1) | (nt << 15));
-    u32 ntok;
+    u32 ntok, tot_e;
     const u32 tpre = wave_prefix<5>((u32)__popc(TS), ntok);
-    if (ntok > WR_TCAP) return false;
-    // ---- committed from here on
+    if (ntok > WR_TCAP) return WR_FALLBACK;
+    const u32 je = wave_prefix<5>((u32)__popc(TE), tot_e);  // the k-th end closes the k-th start
     {
         u32 *row = W.row;
         row[4 * lane] = v.x; row[4 * lane + 1] = v.y; row[4 * lane + 2] = v.z; row[4 * lane + 3] = v.w;
         if (lane < 8) row[256 + lane] = 0;
     }
     for (u32 m = TS, j = tpre; m; m &= m - 1, ++j) W.ts[j] = (u16)((u32)(lb - base) + (u32)__builtin_ctz(m));
-    u32 tot_e;  // the k-th end closes the k-th start
-    const u32 je = wave_prefix<5>((u32)__popc(TE), tot_e);
     for (u32 m = TE, j = je; m; m &= m - 1, ++j) W.te[j] = (u16)((u32)(lb - base) + (u32)__builtin_ctz(m) + 1u);
-    for (u32 k = lane; k < WR_DCAP; k += 64) { W.dkey[k] = 0; W.dcnt[k] = 0; W.dfirst[k] = ~0u; }
+    for (u32 k = lane; k < WR_DCAP; k += 64) { T.key[k] = 0; T.cnt[k] = 0; T.first[k] = ~0u; }
     __builtin_amdgcn_wave_barrier();
-    // tokens, one per lane
-    u32 nval = 0;
-    for (u32 t0 = 0; t0 < ntok; t0 += 64) {
-        const u32 t = t0 + lane;
-        bool ok = false;
-        u64 key = 0, h2v = 0;
-        u32 s = 0, len = 0;
-        if (t < ntok) {
-            s = W.ts[t];
-            len = W.te[t] - s;
-            TokHash th;
-            th.reset();
-            th.len = len;
-            u32 c3 = 0;
-            bool alnum = false;
-            for (u32 o = 0; o < len; o += 8) {
-                const u32 q = (s + o) >> 2, sh = (s + o) & 3u;
-                const u32 w0 = W.row[q], w1 = W.row[q + 1], w2 = W.row[q + 2];
-                u32 x0 = __builtin_amdgcn_alignbyte(w1, w0, sh), x1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
-                const u32 nbt = len - o < 8 ? len - o : 8;
-                const u32 k0 = nbt >= 4 ? 0xFFFFFFFFu : ((1u << (8 * nbt)) - 1u);
-                const u32 k1 = nbt >= 8 ? 0xFFFFFFFFu : (nbt <= 4 ? 0u : ((1u << (8 * (nbt - 4))) - 1u));
-                x0 &= k0;
-                x1 &= k1;
-                c3 += __popc(swar_eq(x0, 0xC3) & k0 & 0x80808080u) + __popc(swar_eq(x1, 0xC3) & k1 & 0x80808080u);
-                alnum |= ((~swar_eq(x0, '\'') & k0) | (~swar_eq(x1, '\'') & k1)) & 0x80808080u;
-                x0 |= swar_upper(x0) >> 2;
-                x1 |= swar_upper(x1) >> 2;
-                th.acc = ((u64)x1 << 32) | x0;
-                if (nbt == 8) th.absorb();
-                else th.nacc = nbt;
-            }
-            ok = alnum && len - c3 >= 3;
-            if (ok) { key = th.key(); h2v = th.check(); }
+    // this lane's token: lower-cased bytes hashed 8 at a time (TokHash)
+    bool ok = false;
+    u64 key = 0, h2v = 0;
+    u32 s = 0, len = 0;
+    if (lane < ntok) {
+        s = W.ts[lane];
+        len = W.te[lane] - s;
+        TokHash th;
+        th.reset();
+        th.len = len;
+        u32 c3 = 0;
+        bool alnum = false;
+        for (u32 off = 0; off < len; off += 8) {
+            const u32 q = (s + off) >> 2, sh = (s + off) & 3u;
+            const u32 w0 = W.row[q], w1 = W.row[q + 1], w2 = W.row[q + 2];
+            u32 x0 = __builtin_amdgcn_alignbyte(w1, w0, sh), x1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
+            const u32 nbt = len - off < 8 ? len - off : 8;
+            const u32 k0 = nbt >= 4 ? 0xFFFFFFFFu : ((1u << (8 * nbt)) - 1u);
+            const u32 k1 = nbt >= 8 ? 0xFFFFFFFFu : (nbt <= 4 ? 0u : ((1u << (8 * (nbt - 4))) - 1u));
+            x0 &= k0;
+            x1 &= k1;
+            c3 += __popc(swar_eq(x0, 0xC3) & k0 & 0x80808080u) + __popc(swar_eq(x1, 0xC3) & k1 & 0x80808080u);
+            alnum |= ((~swar_eq(x0, '\'') & k0) | (~swar_eq(x1, '\'') & k1)) & 0x80808080u;
+            x0 |= swar_upper(x0) >> 2;
+            x1 |= swar_upper(x1) >> 2;
+            th.acc = ((u64)x1 << 32) | x0;
+            if (nbt == 8) th.absorb();
+            else th.nacc = nbt;
         }
-        const u64 okm = __ballot(ok);
-        const u32 ord = nval + mbcnt(okm);
-        nval += (u32)__popcll(okm);
-        u32 h = 0xFFFFu;
-        if (ok) {
-            const u64 slot = g_insert(a, key);
-            if (slot != ~0ull) {  // else overflow: the run repeats with a larger table
-                word_update(a, agg, slot, h2v, ~(((base + s) << 20) | (u64)len));
-                const u32 id = (u32)slot + 1;
-                h = (id * 0x9E3779B1u) >> 24;
-                for (;;) {
-                    u32 cur = W.dkey[h];
-                    if (cur == 0) {
-                        const u32 old = atomicCAS(&W.dkey[h], 0u, id);
-                        cur = old == 0 ? id : old;
-                    }
-                    if (cur == id) break;
-                    h = (h + 1) & (WR_DCAP - 1);
-                }
-                atomicAdd(&W.dcnt[h], 1u);
-                atomicMin(&W.dfirst[h], ord);
+        ok = alnum && len - c3 >= 3;
+        if (ok) { key = th.key(); h2v = th.check(); }
+    }
+    const u64 okm = __ballot(ok);
+    o.ord = mbcnt(okm);
+    o.nval = (u32)__popcll(okm);
+    o.h = 0;
+    if (ok) {
+        if (!(a.ablate & 48)) o.cur = g_probe(a, key);  // in flight until the back half
+        u32 h = (u32)(key >> 40) & (WR_DCAP - 1);
+        for (;;) {
+            u64 c = T.key[h];
+            if (c == 0) {
+                const u64 old = atomicCAS((unsigned long long *)&T.key[h], 0ull, (unsigned long long)key);
+                c = old == 0 ? key : old;
             }
+            if (c == key) break;
+            h = (h + 1) & (WR_DCAP - 1);
         }
-        if (t < ntok) { W.ts[t] = (u16)h; W.te[t] = (u16)ord; }
+        atomicAdd(&T.cnt[h], 1u);
+        atomicMin(&T.first[h], o.ord);
+        o.h = h;
+    }
+    o.ok = ok;
+    o.key = key;
+    o.h2v = h2v;
+    o.sl = (s << 11) | len;
+    o.r = r; o.rs = rs; o.re = re; o.base = base; o.nf = nf;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o.span[k] = __builtin_amdgcn_readfirstlane(W.fpos[k]);
+    return WR_OK;
+}
+
+// Back half: global slots, workgroup aggregate, the row's lines, nd, spans.
+__device__ __forceinline__ void wr_back(const RowArgs &a, WgAgg &agg, WrTable &T, const WrRow &o, u64 &n_rows,
+                                        u64 &n_song, u64 &n_tok) {
+    const u32 lane = lane_id();
+    if (o.ok) {
+        const u64 slot = (a.ablate & 48) ? (o.key & a.gmask) : g_insert(a, o.key, o.h2v, o.cur);
+        if (slot != ~0ull) {  // else overflow: the run repeats with a larger table
+            if (!(a.ablate & 32))
+                word_update<WR_LW>(a, agg, slot, ~(((o.base + (o.sl >> 11)) << 20) | (u64)(o.sl & 2047u)));
+            T.slot[o.h] = (u32)slot;  // the same value from every token of the word
+        }
     }
     __builtin_amdgcn_wave_barrier();
     // the row's (word id, count) lines in first-occurrence order
-    u64 *lines = a.scratch + 2 * rs + (re - rs) / 4 + 1;
-    u32 nd = 0;
-    for (u32 t0 = 0; t0 < ntok; t0 += 64) {
-        const u32 t = t0 + lane;
-        bool lead_t = false;
-        u32 h = 0;
-        if (t < ntok) {
-            h = W.ts[t];
-            lead_t = h != 0xFFFFu && W.dfirst[h] == W.te[t];
-        }
-        const u64 lm = __ballot(lead_t);
-        if (lead_t) lines[nd + mbcnt(lm)] = ((u64)W.dkey[h] << 32) | W.dcnt[h];
-        nd += (u32)__popcll(lm);
+    const bool lead_t = o.ok && T.first[o.h] == o.ord;
+    const u64 lm = __ballot(lead_t);
+    if (lead_t) {
+        u64 *lines = a.scratch + 2 * o.rs + (o.re - o.rs) / 4 + 1;
+        lines[mbcnt(lm)] = ((u64)(T.slot[o.h] + 1) << 32) | T.cnt[o.h];
     }
+    const u32 nd = (u32)__popcll(lm);
     if (lane == 0) {
-        if (nf <= a.need) wcs_err(a.ctr, r, E_SHORT);
-        a.nd[r] = nd;
-        u64 *o = a.spans + r * 4;
-        o[0] = base + W.fpos[0]; o[1] = base + W.fpos[1]; o[2] = base + W.fpos[2]; o[3] = base + W.fpos[3];
+        if (o.nf <= a.need) wcs_err(a.ctr, o.r, E_SHORT);
+        a.nd[o.r] = nd;
+        u64 *sp = a.spans + o.r * 4;
+        sp[0] = o.base + o.span[0]; sp[1] = o.base + o.span[1]; sp[2] = o.base + o.span[2]; sp[3] = o.base + o.span[3];
     }
     ++n_rows;
-    if (nd) { ++n_song; n_tok += nval; }
+    if (nd) { ++n_song; n_tok += o.nval; }
     __builtin_amdgcn_wave_barrier();
-    return true;
 }
 
+#if WR_OCC
+__global__ __launch_bounds__(WR_W * 64) __attribute__((amdgpu_waves_per_eu(WR_OCC, WR_OCC))) void k_wcs_wrows(RowArgs a) {
+#else
 __global__ __launch_bounds__(WR_W * 64) void k_wcs_wrows(RowArgs a) {
-    __shared__ u32 l_id[LW], l_cnt[LW];
-    __shared__ u64 l_h2[LW], l_first[LW], l_rows[4];
+#endif
+    __shared__ u32 l_id[WR_LW], l_cnt[WR_LW];
+    __shared__ u64 l_first[WR_LW], l_rows[4];
     __shared__ WrWave l_w[WR_W];
-    for (u32 k = threadIdx.x; k < LW; k += blockDim.x) { l_id[k] = 0; l_cnt[k] = 0; l_h2[k] = 0; l_first[k] = 0; }
+    for (u32 k = threadIdx.x; k < WR_LW; k += blockDim.x) { l_id[k] = 0; l_cnt[k] = 0; l_first[k] = 0; }
     if (threadIdx.x < 4) l_rows[threadIdx.x] = 0;
     __syncthreads();
-    WgAgg agg{l_id, l_cnt, l_h2, l_first, l_rows};
+    WgAgg agg{l_id, l_cnt, l_first, l_rows};
     const u32 lane = lane_id(), wv = threadIdx.x >> 6;
     WrWave &W = l_w[wv];
     const u64 r0 = 2 + ((u64)blockIdx.x * WR_W + wv) * WR_ROWS;
@@ -900,20 +948,44 @@ __global__ __launch_bounds__(WR_W * 64) void k_wcs_wrows(RowArgs a) {
         const u64 last = a.rend[rl - 1];
         u64 rs = readlane64(mys, 0), re = rl > r0 + 1 ? readlane64(mys, 1) : last;
         uint4 v = *(const uint4 *)(a.buf + (rs & ~15ull) + 16 * lane);
+        // software pipeline: the front half of row r (its global probes go out)
+        // runs before the back half of row r - 1 (whose probes have landed and
+        // whose stores come after them)
+        WrRow prev;
+        bool pending = false;
+        u32 fb = 0;  // the free table
         for (u64 r = r0; r < rl; ++r) {
-            // the next row's window is in flight while this one is processed
             const u32 k = (u32)(r - r0);
             const u64 ns = re, ne = r + 2 < rl ? readlane64(mys, (int)k + 2) : last;
             uint4 nv = make_uint4(0, 0, 0, 0);
             if (r + 1 < rl) nv = *(const uint4 *)(a.buf + (ns & ~15ull) + 16 * lane);
-            if (!wr_row(a, agg, W, r, rs, re, v, n_rows, n_song, n_tok) && lane == 0) {
-                const u64 i = atomicAdd((unsigned long long *)&a.ctr->fallback, 1ull);
-                a.fb[i] = r;
+            WrRow cur;
+            const int st = wr_front(a, W, W.tab[fb], r, rs, re, v, cur);
+#if WR_PIPE
+            if (pending) wr_back(a, agg, W.tab[fb ^ 1], prev, n_rows, n_song, n_tok);
+            pending = false;
+            if (st == WR_OK) {
+                prev = cur;
+                pending = true;
+                fb ^= 1;
+            } else if (lane == 0) {
+#else
+            if (st == WR_OK) {
+                wr_back(a, agg, W.tab[fb], cur, n_rows, n_song, n_tok);
+            } else if (lane == 0) {
+#endif
+                if (st == WR_BLANK) {
+                    a.nd[r] = 0;
+                } else {
+                    const u64 i = atomicAdd((unsigned long long *)&a.ctr->fallback, 1ull);
+                    a.fb[i] = r;
+                }
             }
             rs = ns;
             re = ne;
             v = nv;
         }
+        if (pending) wr_back(a, agg, W.tab[fb ^ 1], prev, n_rows, n_song, n_tok);
     }
     if (lane == 0 && n_rows) {
         atomicAdd((unsigned long long *)&l_rows[0], (unsigned long long)n_rows);
@@ -921,22 +993,7 @@ __global__ __launch_bounds__(WR_W * 64) void k_wcs_wrows(RowArgs a) {
         atomicAdd((unsigned long long *)&l_rows[2], (unsigned long long)n_tok);
     }
     __syncthreads();
-    for (u32 k = threadIdx.x; k < LW; k += blockDim.x) {
-        const u32 id = l_id[k];
-        if (!id) continue;
-        u64 *gt = a.gtab + (u64)(id - 1) * 4;
-        atomicAdd((unsigned long long *)(gt + 3), (unsigned long long)l_cnt[k]);
-        atomicMax((unsigned long long *)(gt + 2), (unsigned long long)l_first[k]);
-        const u64 h2v = l_h2[k];
-        const u64 o = atomicCAS((unsigned long long *)(gt + 1), 0ull, (unsigned long long)h2v);
-        if (o != 0 && o != h2v) atomicAdd((unsigned long long *)&a.ctr->collision, 1ull);
-    }
-    if (threadIdx.x == 0) {
-        atomicAdd((unsigned long long *)&a.ctr->total_rows, (unsigned long long)l_rows[0]);
-        atomicAdd((unsigned long long *)&a.ctr->song_rows, (unsigned long long)l_rows[1]);
-        atomicAdd((unsigned long long *)&a.ctr->tokens, (unsigned long long)l_rows[2]);
-        if (l_rows[3]) atomicAdd((unsigned long long *)&a.ctr->collision, (unsigned long long)l_rows[3]);
-    }
+    agg_flush(a, agg, WR_LW);
 }
 
 // ---------------------------------------------------------------------------
