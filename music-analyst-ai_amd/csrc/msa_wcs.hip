@@ -116,8 +116,21 @@ __global__ __launch_bounds__(256) void k_wcs_validate(const u8 *__restrict__ buf
     const u64 base = ((u64)blockIdx.x * blockDim.x + threadIdx.x) * 16;
     if (base >= n) return;
     const uint4 v = *(const uint4 *)(buf + base);
-    // fast path: 16 ASCII bytes without NUL (almost all of a lyrics file)
-    if (base + 16 <= n && !((v.x | v.y | v.z | v.w) & 0x80808080u) && !mask16(v, 0)) return;
+    // fast path: 16 bytes without NUL of ASCII and whole 2-byte sequences (lead
+    // C2..DF, then a continuation byte) -- almost all of a lyrics file
+    if (base + 16 <= n && !mask16(v, 0)) {
+        if (!((v.x | v.y | v.z | v.w) & 0x80808080u)) return;
+        const u32 w[4] = {v.x, v.y, v.z, v.w};
+        u32 X = 0, L2 = 0, C = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const u32 x = w[k], x7 = x & 0x7F7F7F7Fu;
+            X |= swar_pack4(x & 0x80808080u) << (4 * k);
+            L2 |= swar_pack4((x7 + 0x3E3E3E3Eu) & ~(x7 + 0x20202020u) & x & 0x80808080u) << (4 * k);
+            C |= swar_pack4(x & ~(x << 1) & 0x80808080u) << (4 * k);
+        }
+        if (!(X & ~(L2 | C)) && C == ((L2 << 1) & 0xFFFFu) && !(L2 & 0x8000u)) return;
+    }
     u32 bad = 0;
     for (u32 j = 0; j < 16; ++j) {
         const u64 i = base + j;
@@ -664,74 +677,62 @@ __global__ __launch_bounds__(256) void k_wcs_rows(RowArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Wave-per-row pass (the common case; k_wcs_rows walks what it leaves).
-// A wave takes WR_ROWS consecutive rows; a row of at most one 1 KiB window
-// (16 bytes per lane) is classified with SWAR masks.  Its quoting is
-// "standard" when every '"' sits where the reader's quote parity predicts a
-// structural or doubled quote:
+// Wave-per-window pass (the common case; k_wcs_rows walks what it leaves).
+// A wave takes WR_ROWS consecutive rows and cuts them into windows: as many
+// whole rows (at most WR_M) as fit in 1 KiB from the first row's 16-byte
+// aligned start, 16 bytes per lane, classified with SWAR masks.  A row's
+// quoting is "standard" when every '"' sits where the reader's quote parity
+// predicts a structural or doubled quote:
 //   * a quote outside quotes (parity 0) follows the row start, a delimiter or
 //     another quote (the second of a doubled pair),
 //   * a quote inside quotes is followed by a quote, a delimiter, an end of line
 //     or the row end,
-//   * the row ends outside quotes, and ends of line outside quotes are only
-//     the row's own terminator.
+//   * the row starts and ends outside quotes, and ends of line outside quotes
+//     are only the row's own terminator.
 // Then parity 0 <=> the reader is outside a quoted field, the fields are
 // split by the delimiters at parity 0, no quote lies inside a token (so a
 // token's raw span is its bytes), and every quote is a token separator like
-// the character it stands for.  Other rows (and rows over 1 KiB or with more
-// than WR_TCAP token runs) go to the fallback list, before anything of theirs
-// is committed.  Tokens: one lane per token (start / end from LDS) hashes its
+// the character it stands for.  Other rows (and rows over 1 KiB, or all rows
+// of a window with more than WR_TCAP token runs) go to the fallback list,
+// before anything of theirs is committed.  Per-row values (delimiter counts,
+// field bounds, flags) are reduced through small LDS arrays indexed by the
+// row's place in the window (row-start bits + prefix counts give a byte's
+// row).  Tokens: one lane per token (start / end from LDS) hashes its
 // lower-cased bytes (same TokHash as k_wcs_rows), claims the global slot and
-// updates the workgroup aggregate; the row's Counter is a per-wave LDS table
-// (count, first occurrence), written out in first-occurrence order.
+// updates the workgroup aggregate; the rows' Counters share one per-wave LDS
+// table keyed by (row, h1) -- the row in h1's top 5 bits, so two words of one
+// window merge only if their 64-bit keys agree in the other 59 -- written out
+// in first-occurrence order.
 #ifndef WR_LW
-#define WR_LW 1024  // workgroup aggregate of k_wcs_wrows (two workgroups per CU)
+#define WR_LW 1024  // workgroup aggregate of k_wcs_wrows
 #endif
 #ifndef WR_WAVES
-#define WR_WAVES 8  // waves per workgroup
+#define WR_WAVES 4  // waves per workgroup
 #endif
-#ifndef WR_PIPE
-#define WR_PIPE 0   // 1: the front half of row r runs before the back half of row r - 1
-#endif
-#ifndef WR_OCC
-#define WR_OCC 0    // waves per SIMD the register budget is held to (0: the compiler's choice)
-#endif
-constexpr u32 WR_W = WR_WAVES, WR_ROWS = 64, WR_TCAP = 64, WR_DCAP = 128;
-// A row's Counter (its words' keys, global slots, counts, first tokens): two
-// per wave, the row in the front half and the row in the back half.
-struct WrTable {
-    u64 key[WR_DCAP];
-    u32 slot[WR_DCAP];
-    u32 cnt[WR_DCAP];
-    u32 first[WR_DCAP];
-};
+constexpr u32 WR_W = WR_WAVES, WR_ROWS = 64, WR_M = 32, WR_TCAP = 192, WR_DCAP = 256;
 struct WrWave {
-    WrTable tab[2];
-    u32 row[264];          // the row window (1 KiB) + 32 bytes of zeros
+    u64 key[WR_DCAP];      // (row, h1)
+    u32 slot[WR_DCAP];     // its global slot
+    u32 cnt[WR_DCAP];
+    u32 first[WR_DCAP];    // order of the first token
+    u32 row[264];          // the window (1 KiB) + 32 bytes of zeros
+    u32 rbits[64];         // row-start bits per lane
+    u32 tgl[64];           // text-field start / end toggles per lane
     u16 ts[WR_TCAP], te[WR_TCAP];
-    u32 fpos[8];           // start / end of the artist, song, text fields
-};
-// What the back half of a row needs from its front half: the row (uniform)
-// and this lane's token (one token per lane).
-struct WrRow {
-    u64 r, rs, re;
-    u32 span[4];           // artist / song start, end (offsets from base)
-    u64 base;
-    u32 nf, nval;
-    u64 key, h2v;
-    ulonglong2 cur;        // the (key, h2) probe of the global table, in flight
-    u32 sl;                // token start (offset from base) << 11 | length
-    u32 h, ord;
-    bool ok;
+    // per row of the window
+    u32 db[WR_M + 1];      // delimiters outside quotes before the row ([m]: all)
+    u32 flag[WR_M];        // 1 bad, 2 blank, 4 odd quote parity at the row start
+    u32 eol[WR_M];         // first end-of-line byte outside quotes, else the row end
+    u32 fp[WR_M][6];       // start / end of the artist, song, text fields
+    u32 lb[WR_M];          // rank of the row's first line in the window
+    u32 nd[WR_M];          // its lines
+    u32 nv[WR_M];          // its counted tokens
 };
 
 __device__ __forceinline__ u32 wr_mask(u64 lb, u64 lo, u64 hi) {  // bits j with lb + j in [lo, hi)
     const u64 a = lo > lb ? (lo - lb < 16 ? lo - lb : 16) : 0;
     const u64 b = hi > lb ? (hi - lb < 16 ? hi - lb : 16) : 0;
     return ((1u << b) - 1u) & ~((1u << a) - 1u);
-}
-__device__ __forceinline__ u32 pack16(const u32 m[4]) {
-    return swar_pack4(m[0]) | (swar_pack4(m[1]) << 4) | (swar_pack4(m[2]) << 8) | (swar_pack4(m[3]) << 12);
 }
 // 0x80 per byte in [0x41, 0x5A] or [0x80, 0x9E] (the bytes a token lower-cases by + 0x20)
 __device__ __forceinline__ u32 swar_upper(u32 x) {
@@ -740,18 +741,42 @@ __device__ __forceinline__ u32 swar_upper(u32 x) {
     const u32 c3 = ~(x7 + 0x61616161u) & x;
     return (up | c3) & 0x80808080u;
 }
+__device__ __forceinline__ u64 shfl64(u64 x, u32 l) {
+    return ((u64)(u32)__shfl((int)(x >> 32), (int)l) << 32) | (u32)__shfl((int)(u32)x, (int)l);
+}
 
-enum : int { WR_FALLBACK = 0, WR_BLANK = 1, WR_OK = 2 };
-// Front half: classify, split, tokenize, hash, count into the row table T,
-// and issue the global-table probe.  Nothing global is written; WR_FALLBACK
-// leaves the row to the per-thread walk.
-__device__ __forceinline__ int wr_front(const RowArgs &a, WrWave &W, WrTable &T, u64 r, u64 rs, u64 re, uint4 v,
-                                        WrRow &o) {
+struct WrCount {
+    u64 rows, song, tok;
+};
+
+// One window: rows i .. i + m - 1 of the wave's set (row i + j owned by lane j),
+// bytes [base, base + 1024) in v.  rsj / rej: the owner lane's row bounds.
+__device__ __forceinline__ void wr_window(const RowArgs &a, WgAgg &agg, WrWave &W, u64 r_first, u32 m, u64 base,
+                                          u64 rsj, u64 rej, uint4 v, WrCount &cnt) {
     const u32 lane = lane_id();
-    const u64 base = rs & ~15ull;
-    if (re - base > 1024) return WR_FALLBACK;
     const u64 lb = base + 16 * lane;
-    const u32 V = wr_mask(lb, rs, re);
+    const u64 ws = readlane64(rsj, 0), we = readlane64(rej, (int)m - 1);
+    const u32 V = wr_mask(lb, ws, we);
+    const bool own = lane < m;
+    const u32 fi[3] = {a.ia, a.isg, a.it};
+    // ---- row starts, per-row defaults
+    W.rbits[lane] = 0;
+    W.tgl[lane] = 0;
+    __builtin_amdgcn_wave_barrier();
+    if (own) {
+        const u32 o = (u32)(rsj - base);
+        atomicOr(&W.rbits[o >> 4], 1u << (o & 15));
+        W.flag[lane] = 0;
+        W.eol[lane] = (u32)(rej - base);
+        W.nd[lane] = 0;
+        W.nv[lane] = 0;
+        W.lb[lane] = ~0u;
+#pragma unroll
+        for (int f = 0; f < 3; ++f) { W.fp[lane][2 * f] = fi[f] == 0 ? o : 0u; W.fp[lane][2 * f + 1] = ~0u; }
+    }
+    __builtin_amdgcn_wave_barrier();
+    const u32 RB = W.rbits[lane];
+    // ---- classes
     const u32 w[4] = {v.x, v.y, v.z, v.w};
     u32 Q = 0, D = 0, E = 0, C3 = 0, T2 = 0, TA = 0;
 #pragma unroll
@@ -766,9 +791,9 @@ __device__ __forceinline__ int wr_front(const RowArgs &a, WrWave &W, WrTable &T,
         T2 |= swar_pack4(x & ~(x << 1) & 0x80808080u & ~swar_eq(x, 0x97) & ~swar_eq(x, 0xB7)) << (4 * k);
     }
     Q &= V; D &= V; E &= V; C3 &= V; T2 &= V; TA &= V;
-    // neighbours: bit 15 of the lane below, bit 0 of the lane above
+    // neighbours: bit 15 of the lane below, bits 0-1 of the lane above
     const u32 lo_bits = (D >> 15) | ((Q >> 15) << 1) | ((C3 >> 15) << 2);
-    const u32 hi_bits = (Q & 1u) | ((D & 1u) << 1) | ((E & 1u) << 2) | ((T2 & 1u) << 3);
+    const u32 hi_bits = (Q & 1u) | ((D & 1u) << 1) | ((E & 1u) << 2) | ((T2 & 1u) << 3) | ((RB & 3u) << 4);
     u32 pb = __shfl_up(lo_bits, 1), nb = __shfl_down(hi_bits, 1);
     if (lane == 0) pb = 0;
     if (lane == 63) nb = 0;
@@ -776,41 +801,69 @@ __device__ __forceinline__ int wr_front(const RowArgs &a, WrWave &W, WrTable &T,
     const u64 qodd = __ballot(__popc(Q) & 1u);
     const u32 carry = (u32)__popcll(qodd & ((1ull << lane) - 1ull)) & 1u;
     const u32 P = pxor_excl16(Q) ^ (carry ? 0xFFFFu : 0u);
-    const u32 sbit = wr_mask(lb, rs, rs + 1), ebit = wr_mask(lb, re - 1, re);
+    // last and second-to-last byte of each row
+    const u32 END = (((RB >> 1) | (((nb >> 4) & 1u) << 15)) & V) | wr_mask(lb, we - 1, we);
+    const u32 END2 = (((RB >> 2) | (((nb >> 4) & 3u) << 14)) & V) | wr_mask(lb, we - 2, we - 1);
     const u32 prevD = (D << 1) | (pb & 1u), prevQ = (Q << 1) | ((pb >> 1) & 1u);
     const u32 nextQ = (Q >> 1) | ((nb & 1u) << 15), nextD = (D >> 1) | (((nb >> 1) & 1u) << 15);
     const u32 nextE = (E >> 1) | (((nb >> 2) & 1u) << 15);
-    const u32 E0 = E & ~P;
-    u32 bad = (Q & ~P & ~(prevD | prevQ | sbit)) | (Q & P & ~(nextQ | nextD | nextE | ebit));
-    bad |= E0 & ~(ebit | wr_mask(lb, re - 2, re - 1));
-    if (__ballot(bad != 0) || (__popcll(qodd) & 1)) return WR_FALLBACK;
-    // blank line (only its terminator): DictReader skips it
-    if (__ballot((E0 & sbit) != 0)) return WR_BLANK;
-    // fields: delimiters outside quotes
-    const u32 D0 = D & ~P;
-    u32 nd0;
-    const u32 dpre = wave_prefix<5>((u32)__popc(D0), nd0);
-    const u64 e0 = __ballot(E0 != 0);
-    const u64 feol = e0 ? readlane64(lb + (u32)__builtin_ctz(E0 ? E0 : 1u), (int)__builtin_ctzll(e0)) : re;
-    const u32 fi[3] = {a.ia, a.isg, a.it};
-    if (lane < 6) {
-        const u32 fl = lane < 2 ? a.ia : (lane < 4 ? a.isg : a.it);
-        W.fpos[lane] = (lane & 1) ? (u32)(feol - base) : (fl == 0 ? (u32)(rs - base) : 0u);
+    const u32 E0 = E & ~P, D0 = D & ~P;
+    const u32 bad = (Q & ~P & ~(prevD | prevQ | RB)) | (Q & P & ~(nextQ | nextD | nextE | END)) |
+                    (E0 & ~(END | END2));
+    // a byte's row: rows started at or before it
+    u32 nrows_tot, nd_tot;
+    const u32 rpre = wave_prefix<6>((u32)__popc(RB), nrows_tot);
+    const u32 dpre = wave_prefix<5>((u32)__popc(D0), nd_tot);
+    for (u32 mm = bad; mm; mm &= mm - 1) {
+        const u32 b = (u32)__builtin_ctz(mm);
+        atomicOr(&W.flag[rpre + __popc(RB & ((2u << b) - 1u)) - 1], 1u);
     }
+    for (u32 mm = RB, j = rpre; mm; mm &= mm - 1, ++j) {
+        const u32 b = (u32)__builtin_ctz(mm);
+        const u32 fl = (((P >> b) & 1u) << 2) | (((E0 >> b) & 1u) << 1);
+        if (fl) atomicOr(&W.flag[j], fl);
+        W.db[j] = dpre + __popc(D0 & ((1u << b) - 1u));
+    }
+    if (lane == 0) W.db[m] = nd_tot;
     __builtin_amdgcn_wave_barrier();
-    for (u32 m = D0, j = dpre; m; m &= m - 1, ++j) {
-        const u32 pos = (u32)(lb - base) + (u32)__builtin_ctz(m);
+    // ---- fields
+    for (u32 mm = D0, g = dpre; mm; mm &= mm - 1, ++g) {
+        const u32 b = (u32)__builtin_ctz(mm);
+        const u32 j = rpre + __popc(RB & ((2u << b) - 1u)) - 1;
+        const u32 idx = g - W.db[j], pos = 16 * lane + b;
 #pragma unroll
         for (int f = 0; f < 3; ++f) {
-            if (j + 1 == fi[f]) W.fpos[2 * f] = pos + 1;
-            if (j == fi[f]) W.fpos[2 * f + 1] = pos;
+            if (idx + 1 == fi[f]) W.fp[j][2 * f] = pos + 1;
+            if (idx == fi[f]) W.fp[j][2 * f + 1] = pos;
+        }
+    }
+    for (u32 mm = E0; mm; mm &= mm - 1) {
+        const u32 b = (u32)__builtin_ctz(mm);
+        atomicMin(&W.eol[rpre + __popc(RB & ((2u << b) - 1u)) - 1], 16 * lane + b);
+    }
+    __builtin_amdgcn_wave_barrier();
+    u32 nf = 0, rflag = 0;
+    if (own) {
+        const u32 fl = W.flag[lane];
+        const bool odd_end = lane + 1 < m ? (W.flag[lane + 1] & 4u) != 0 : (__popcll(qodd) & 1) != 0;
+        rflag = ((fl & 5u) || odd_end) ? 1u : (fl & 2u);
+        nf = W.db[lane + 1] - W.db[lane] + 1;
+        const u32 eo = W.eol[lane];
+#pragma unroll
+        for (int f = 0; f < 3; ++f)
+            if (W.fp[lane][2 * f + 1] == ~0u) W.fp[lane][2 * f + 1] = eo;
+        if (rflag == 0 && nf > a.it) {
+            const u32 ts = W.fp[lane][4], te = W.fp[lane][5];
+            atomicXor(&W.tgl[ts >> 4], 1u << (ts & 15));
+            if (te < 1024) atomicXor(&W.tgl[te >> 4], 1u << (te & 15));
         }
     }
     __builtin_amdgcn_wave_barrier();
-    const u32 nf = nd0 + 1;
-    const u64 ts = base + W.fpos[4], te = base + W.fpos[5];
-    // token bytes of the text field (a 0xC3 pair counts when its second byte does)
-    const u32 R = nf > a.it ? wr_mask(lb, ts, te) : 0u;
+    // ---- tokens of the text fields
+    u32 R = W.tgl[lane];
+    const u32 tcarry = (u32)__popcll(__ballot(__popc(R) & 1u) & ((1ull << lane) - 1ull)) & 1u;
+    R ^= R << 1; R ^= R << 2; R ^= R << 4; R ^= R << 8;
+    R = (R ^ (tcarry ? 0xFFFFu : 0u)) & V;
     const u32 lead = C3 & ((T2 >> 1) | (((nb >> 3) & 1u) << 15));
     const u32 sec = T2 & ((C3 << 1) | ((pb >> 2) & 1u));
     const u32 TB = (TA | lead | sec) & R;
@@ -820,116 +873,147 @@ __device__ __forceinline__ int wr_front(const RowArgs &a, WrWave &W, WrTable &T,
     const u32 TS = TB & ~((TB << 1) | pt), TE = TB & ~((TB >> 1) | (nt << 15));
     u32 ntok, tot_e;
     const u32 tpre = wave_prefix<5>((u32)__popc(TS), ntok);
-    if (ntok > WR_TCAP) return WR_FALLBACK;
-    const u32 je = wave_prefix<5>((u32)__popc(TE), tot_e);  // the k-th end closes the k-th start
-    {
-        u32 *row = W.row;
-        row[4 * lane] = v.x; row[4 * lane + 1] = v.y; row[4 * lane + 2] = v.z; row[4 * lane + 3] = v.w;
-        if (lane < 8) row[256 + lane] = 0;
-    }
-    for (u32 m = TS, j = tpre; m; m &= m - 1, ++j) W.ts[j] = (u16)((u32)(lb - base) + (u32)__builtin_ctz(m));
-    for (u32 m = TE, j = je; m; m &= m - 1, ++j) W.te[j] = (u16)((u32)(lb - base) + (u32)__builtin_ctz(m) + 1u);
-    for (u32 k = lane; k < WR_DCAP; k += 64) { T.key[k] = 0; T.cnt[k] = 0; T.first[k] = ~0u; }
-    __builtin_amdgcn_wave_barrier();
-    // this lane's token: lower-cased bytes hashed 8 at a time (TokHash)
-    bool ok = false;
-    u64 key = 0, h2v = 0;
-    u32 s = 0, len = 0;
-    if (lane < ntok) {
-        s = W.ts[lane];
-        len = W.te[lane] - s;
-        TokHash th;
-        th.reset();
-        th.len = len;
-        u32 c3 = 0;
-        bool alnum = false;
-        for (u32 off = 0; off < len; off += 8) {
-            const u32 q = (s + off) >> 2, sh = (s + off) & 3u;
-            const u32 w0 = W.row[q], w1 = W.row[q + 1], w2 = W.row[q + 2];
-            u32 x0 = __builtin_amdgcn_alignbyte(w1, w0, sh), x1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
-            const u32 nbt = len - off < 8 ? len - off : 8;
-            const u32 k0 = nbt >= 4 ? 0xFFFFFFFFu : ((1u << (8 * nbt)) - 1u);
-            const u32 k1 = nbt >= 8 ? 0xFFFFFFFFu : (nbt <= 4 ? 0u : ((1u << (8 * (nbt - 4))) - 1u));
-            x0 &= k0;
-            x1 &= k1;
-            c3 += __popc(swar_eq(x0, 0xC3) & k0 & 0x80808080u) + __popc(swar_eq(x1, 0xC3) & k1 & 0x80808080u);
-            alnum |= ((~swar_eq(x0, '\'') & k0) | (~swar_eq(x1, '\'') & k1)) & 0x80808080u;
-            x0 |= swar_upper(x0) >> 2;
-            x1 |= swar_upper(x1) >> 2;
-            th.acc = ((u64)x1 << 32) | x0;
-            if (nbt == 8) th.absorb();
-            else th.nacc = nbt;
+    const bool over = ntok > WR_TCAP;  // every row of the window to the fallback
+    u32 nval = 0, nlead = 0;
+    if (!over) {
+        const u32 je = wave_prefix<5>((u32)__popc(TE), tot_e);  // the k-th end closes the k-th start
+        W.row[4 * lane] = v.x; W.row[4 * lane + 1] = v.y; W.row[4 * lane + 2] = v.z; W.row[4 * lane + 3] = v.w;
+        if (lane < 8) W.row[256 + lane] = 0;
+        for (u32 mm = TS, j = tpre; mm; mm &= mm - 1, ++j) {
+            const u32 b = (u32)__builtin_ctz(mm);
+            W.ts[j] = (u16)((16 * lane + b) | ((rpre + __popc(RB & ((2u << b) - 1u)) - 1) << 10));
         }
-        ok = alnum && len - c3 >= 3;
-        if (ok) { key = th.key(); h2v = th.check(); }
-    }
-    const u64 okm = __ballot(ok);
-    o.ord = mbcnt(okm);
-    o.nval = (u32)__popcll(okm);
-    o.h = 0;
-    if (ok) {
-        if (!(a.ablate & 48)) o.cur = g_probe(a, key);  // in flight until the back half
-        u32 h = (u32)(key >> 40) & (WR_DCAP - 1);
-        for (;;) {
-            u64 c = T.key[h];
-            if (c == 0) {
-                const u64 old = atomicCAS((unsigned long long *)&T.key[h], 0ull, (unsigned long long)key);
-                c = old == 0 ? key : old;
+        for (u32 mm = TE, j = je; mm; mm &= mm - 1, ++j) W.te[j] = (u16)(16 * lane + (u32)__builtin_ctz(mm) + 1u);
+        for (u32 k = lane; k < WR_DCAP; k += 64) { W.key[k] = 0; W.cnt[k] = 0; W.first[k] = ~0u; }
+        __builtin_amdgcn_wave_barrier();
+        // one token per lane: lower-cased bytes hashed 8 at a time (TokHash)
+        for (u32 t0 = 0; t0 < ntok; t0 += 64) {
+            const u32 t = t0 + lane;
+            bool ok = false;
+            u64 key = 0, h2v = 0;
+            u32 s = 0, len = 0, rj = 0;
+            if (t < ntok) {
+                const u32 tsv = W.ts[t];
+                s = tsv & 1023u;
+                rj = tsv >> 10;
+                len = W.te[t] - s;
+                TokHash th;
+                th.reset();
+                th.len = len;
+                u32 c3 = 0;
+                bool alnum = false;
+                for (u32 off = 0; off < len; off += 8) {
+                    const u32 q = (s + off) >> 2, sh = (s + off) & 3u;
+                    const u32 w0 = W.row[q], w1 = W.row[q + 1], w2 = W.row[q + 2];
+                    u32 x0 = __builtin_amdgcn_alignbyte(w1, w0, sh), x1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
+                    const u32 nbt = len - off < 8 ? len - off : 8;
+                    const u32 k0 = nbt >= 4 ? 0xFFFFFFFFu : ((1u << (8 * nbt)) - 1u);
+                    const u32 k1 = nbt >= 8 ? 0xFFFFFFFFu : (nbt <= 4 ? 0u : ((1u << (8 * (nbt - 4))) - 1u));
+                    x0 &= k0;
+                    x1 &= k1;
+                    c3 += __popc(swar_eq(x0, 0xC3) & k0 & 0x80808080u) + __popc(swar_eq(x1, 0xC3) & k1 & 0x80808080u);
+                    alnum |= ((~swar_eq(x0, '\'') & k0) | (~swar_eq(x1, '\'') & k1)) & 0x80808080u;
+                    x0 |= swar_upper(x0) >> 2;
+                    x1 |= swar_upper(x1) >> 2;
+                    th.acc = ((u64)x1 << 32) | x0;
+                    if (nbt == 8) th.absorb();
+                    else th.nacc = nbt;
+                }
+                ok = alnum && len - c3 >= 3;
+                if (ok) { key = th.key(); h2v = th.check(); }
             }
-            if (c == key) break;
-            h = (h + 1) & (WR_DCAP - 1);
+            const u64 okm = __ballot(ok);
+            const u32 ord = nval + mbcnt(okm);
+            nval += (u32)__popcll(okm);
+            u32 h = 0;
+            if (ok) {
+                const ulonglong2 cur = (a.ablate & 48) ? ulonglong2{0, 0} : g_probe(a, key);  // in flight
+                const u64 rk = (key & ~(31ull << 59)) | ((u64)rj << 59);
+                h = (u32)(rk >> 40) & (WR_DCAP - 1);
+                for (;;) {
+                    u64 c = W.key[h];
+                    if (c == 0) {
+                        const u64 old = atomicCAS((unsigned long long *)&W.key[h], 0ull, (unsigned long long)rk);
+                        c = old == 0 ? rk : old;
+                    }
+                    if (c == rk) break;
+                    h = (h + 1) & (WR_DCAP - 1);
+                }
+                atomicAdd(&W.cnt[h], 1u);
+                atomicMin(&W.first[h], ord);
+                atomicAdd(&W.nv[rj], 1u);
+                const u64 slot = (a.ablate & 48) ? (key & a.gmask) : g_insert(a, key, h2v, cur);
+                if (slot != ~0ull) {  // else overflow: the run repeats with a larger table
+                    if (!(a.ablate & 32)) word_update<WR_LW>(a, agg, slot, ~(((base + s) << 20) | (u64)len));
+                    W.slot[h] = (u32)slot;  // the same value from every token of the word
+                }
+            }
+            if (t < ntok) { W.ts[t] = (u16)(h | (rj << 10)); W.te[t] = (u16)(ok ? ord : 0xFFFFu); }
         }
-        atomicAdd(&T.cnt[h], 1u);
-        atomicMin(&T.first[h], o.ord);
-        o.h = h;
+        __builtin_amdgcn_wave_barrier();
+        // leaders (first tokens of a word in a row): window rank, row base, row count
+        for (u32 t0 = 0; t0 < ntok; t0 += 64) {
+            const u32 t = t0 + lane;
+            bool ld = false;
+            u32 rj = 0;
+            if (t < ntok) {
+                const u32 tsv = W.ts[t], ord = W.te[t];
+                rj = tsv >> 10;
+                ld = ord != 0xFFFFu && W.first[tsv & 1023u] == ord;
+            }
+            const u64 lm = __ballot(ld);
+            if (ld) {
+                atomicMin(&W.lb[rj], nlead + mbcnt(lm));
+                atomicAdd(&W.nd[rj], 1u);
+            }
+            nlead += (u32)__popcll(lm);
+        }
+        __builtin_amdgcn_wave_barrier();
+        // the rows' (word id, count) lines in first-occurrence order
+        u32 nl = 0;
+        for (u32 t0 = 0; t0 < ntok; t0 += 64) {
+            const u32 t = t0 + lane;
+            bool ld = false;
+            u32 rj = 0, h = 0;
+            if (t < ntok) {
+                const u32 tsv = W.ts[t], ord = W.te[t];
+                rj = tsv >> 10;
+                h = tsv & 1023u;
+                ld = ord != 0xFFFFu && W.first[h] == ord;
+            }
+            const u64 lm = __ballot(ld);
+            const u64 r_s = shfl64(rsj, rj), r_e = shfl64(rej, rj);
+            if (ld) {
+                u64 *lines = a.scratch + 2 * r_s + (r_e - r_s) / 4 + 1;
+                lines[nl + mbcnt(lm) - W.lb[rj]] = ((u64)(W.slot[h] + 1) << 32) | W.cnt[h];
+            }
+            nl += (u32)__popcll(lm);
+        }
+        __builtin_amdgcn_wave_barrier();
     }
-    o.ok = ok;
-    o.key = key;
-    o.h2v = h2v;
-    o.sl = (s << 11) | len;
-    o.r = r; o.rs = rs; o.re = re; o.base = base; o.nf = nf;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) o.span[k] = __builtin_amdgcn_readfirstlane(W.fpos[k]);
-    return WR_OK;
-}
-
-// Back half: global slots, workgroup aggregate, the row's lines, nd, spans.
-__device__ __forceinline__ void wr_back(const RowArgs &a, WgAgg &agg, WrTable &T, const WrRow &o, u64 &n_rows,
-                                        u64 &n_song, u64 &n_tok) {
-    const u32 lane = lane_id();
-    if (o.ok) {
-        const u64 slot = (a.ablate & 48) ? (o.key & a.gmask) : g_insert(a, o.key, o.h2v, o.cur);
-        if (slot != ~0ull) {  // else overflow: the run repeats with a larger table
-            if (!(a.ablate & 32))
-                word_update<WR_LW>(a, agg, slot, ~(((o.base + (o.sl >> 11)) << 20) | (u64)(o.sl & 2047u)));
-            T.slot[o.h] = (u32)slot;  // the same value from every token of the word
+    // ---- per row: fallback, blank, or nd / spans / counters
+    if (own) {
+        const u64 r = r_first + lane;
+        if (rflag == 1 || (over && rflag == 0)) {
+            const u64 i = atomicAdd((unsigned long long *)&a.ctr->fallback, 1ull);
+            a.fb[i] = r;
+        } else if (rflag == 2) {
+            a.nd[r] = 0;
+        } else {
+            if (nf <= a.need) wcs_err(a.ctr, r, E_SHORT);
+            const u32 nd = W.nd[lane];
+            a.nd[r] = nd;
+            u64 *sp = a.spans + r * 4;
+            sp[0] = base + W.fp[lane][0]; sp[1] = base + W.fp[lane][1];
+            sp[2] = base + W.fp[lane][2]; sp[3] = base + W.fp[lane][3];
+            ++cnt.rows;
+            if (nd) { ++cnt.song; cnt.tok += W.nv[lane]; }
         }
     }
     __builtin_amdgcn_wave_barrier();
-    // the row's (word id, count) lines in first-occurrence order
-    const bool lead_t = o.ok && T.first[o.h] == o.ord;
-    const u64 lm = __ballot(lead_t);
-    if (lead_t) {
-        u64 *lines = a.scratch + 2 * o.rs + (o.re - o.rs) / 4 + 1;
-        lines[mbcnt(lm)] = ((u64)(T.slot[o.h] + 1) << 32) | T.cnt[o.h];
-    }
-    const u32 nd = (u32)__popcll(lm);
-    if (lane == 0) {
-        if (o.nf <= a.need) wcs_err(a.ctr, o.r, E_SHORT);
-        a.nd[o.r] = nd;
-        u64 *sp = a.spans + o.r * 4;
-        sp[0] = o.base + o.span[0]; sp[1] = o.base + o.span[1]; sp[2] = o.base + o.span[2]; sp[3] = o.base + o.span[3];
-    }
-    ++n_rows;
-    if (nd) { ++n_song; n_tok += o.nval; }
-    __builtin_amdgcn_wave_barrier();
 }
 
-#if WR_OCC
-__global__ __launch_bounds__(WR_W * 64) __attribute__((amdgpu_waves_per_eu(WR_OCC, WR_OCC))) void k_wcs_wrows(RowArgs a) {
-#else
 __global__ __launch_bounds__(WR_W * 64) void k_wcs_wrows(RowArgs a) {
-#endif
     __shared__ u32 l_id[WR_LW], l_cnt[WR_LW];
     __shared__ u64 l_first[WR_LW], l_rows[4];
     __shared__ WrWave l_w[WR_W];
@@ -940,57 +1024,58 @@ __global__ __launch_bounds__(WR_W * 64) void k_wcs_wrows(RowArgs a) {
     const u32 lane = lane_id(), wv = threadIdx.x >> 6;
     WrWave &W = l_w[wv];
     const u64 r0 = 2 + ((u64)blockIdx.x * WR_W + wv) * WR_ROWS;
-    u64 n_rows = 0, n_song = 0, n_tok = 0;
+    WrCount cnt{0, 0, 0};
     if (r0 < a.nrows) {
-        const u64 rl = a.nrows - r0 < WR_ROWS ? a.nrows : r0 + WR_ROWS;
-        // lane k: start of row r0 + k (= end of row r0 + k - 1); the last end apart
-        const u64 mys = r0 + lane < rl ? a.rend[r0 - 1 + lane] : 0;
-        const u64 last = a.rend[rl - 1];
-        u64 rs = readlane64(mys, 0), re = rl > r0 + 1 ? readlane64(mys, 1) : last;
-        uint4 v = *(const uint4 *)(a.buf + (rs & ~15ull) + 16 * lane);
-        // software pipeline: the front half of row r (its global probes go out)
-        // runs before the back half of row r - 1 (whose probes have landed and
-        // whose stores come after them)
-        WrRow prev;
-        bool pending = false;
-        u32 fb = 0;  // the free table
-        for (u64 r = r0; r < rl; ++r) {
-            const u32 k = (u32)(r - r0);
-            const u64 ns = re, ne = r + 2 < rl ? readlane64(mys, (int)k + 2) : last;
-            uint4 nv = make_uint4(0, 0, 0, 0);
-            if (r + 1 < rl) nv = *(const uint4 *)(a.buf + (ns & ~15ull) + 16 * lane);
-            WrRow cur;
-            const int st = wr_front(a, W, W.tab[fb], r, rs, re, v, cur);
-#if WR_PIPE
-            if (pending) wr_back(a, agg, W.tab[fb ^ 1], prev, n_rows, n_song, n_tok);
-            pending = false;
-            if (st == WR_OK) {
-                prev = cur;
-                pending = true;
-                fb ^= 1;
-            } else if (lane == 0) {
-#else
-            if (st == WR_OK) {
-                wr_back(a, agg, W.tab[fb], cur, n_rows, n_song, n_tok);
-            } else if (lane == 0) {
-#endif
-                if (st == WR_BLANK) {
-                    a.nd[r] = 0;
-                } else {
-                    const u64 i = atomicAdd((unsigned long long *)&a.ctr->fallback, 1ull);
-                    a.fb[i] = r;
+        const u32 nr = (u32)(a.nrows - r0 < WR_ROWS ? a.nrows - r0 : WR_ROWS);
+        // lane k: row r0 + k spans [s_k, e_k)
+        const u64 s_k = lane < nr ? a.rend[r0 - 1 + lane] : 0;
+        const u64 e_k = lane < nr ? a.rend[r0 + lane] : 0;
+        // window starting at row i: rows i .. i + m - 1 (every one ends within
+        // 1 KiB of the first's aligned start, at most WR_M)
+        auto window = [&](u32 i, u64 &wbase) -> u32 {
+            wbase = readlane64(s_k, (int)i) & ~15ull;
+            const bool fit = lane >= i && lane < nr && lane < i + WR_M && e_k - wbase <= 1024;
+            const u64 nf = ~__ballot(fit) >> i;  // first row past the window
+            return nf ? (u32)__builtin_ctzll(nf) : 64u - i;
+        };
+        u32 i = 0;
+        u64 base;
+        u32 m = window(0, base);
+        uint4 v = *(const uint4 *)(a.buf + base + 16 * lane);
+        while (i < nr) {
+            if (m == 0) {  // a row over 1 KiB
+                if (lane == 0) {
+                    const u64 k = atomicAdd((unsigned long long *)&a.ctr->fallback, 1ull);
+                    a.fb[k] = r0 + i;
                 }
+                i += 1;
+                if (i < nr) { m = window(i, base); v = *(const uint4 *)(a.buf + base + 16 * lane); }
+                continue;
             }
-            rs = ns;
-            re = ne;
-            v = nv;
+            // the next window's bytes are in flight while this one is processed
+            const u32 i2 = i + m;
+            u64 base2 = 0;
+            u32 m2 = 0;
+            uint4 v2 = make_uint4(0, 0, 0, 0);
+            if (i2 < nr) {
+                m2 = window(i2, base2);
+                v2 = *(const uint4 *)(a.buf + base2 + 16 * lane);
+            }
+            const u32 src = i + (lane < m ? lane : 0);
+            wr_window(a, agg, W, r0 + i, m, base, shfl64(s_k, src), shfl64(e_k, src), v, cnt);
+            i = i2;
+            base = base2;
+            m = m2;
+            v = v2;
         }
-        if (pending) wr_back(a, agg, W.tab[fb ^ 1], prev, n_rows, n_song, n_tok);
     }
-    if (lane == 0 && n_rows) {
-        atomicAdd((unsigned long long *)&l_rows[0], (unsigned long long)n_rows);
-        atomicAdd((unsigned long long *)&l_rows[1], (unsigned long long)n_song);
-        atomicAdd((unsigned long long *)&l_rows[2], (unsigned long long)n_tok);
+    cnt.rows = wave_sum64(cnt.rows);
+    cnt.song = wave_sum64(cnt.song);
+    cnt.tok = wave_sum64(cnt.tok);
+    if (lane == 0 && cnt.rows) {
+        atomicAdd((unsigned long long *)&l_rows[0], (unsigned long long)cnt.rows);
+        atomicAdd((unsigned long long *)&l_rows[1], (unsigned long long)cnt.song);
+        atomicAdd((unsigned long long *)&l_rows[2], (unsigned long long)cnt.tok);
     }
     __syncthreads();
     agg_flush(a, agg, WR_LW);
@@ -1588,7 +1673,7 @@ extern "C" int msa_wcs_run(msa_wcs *w) {
     u64 bits = w->gbits;
     if (!bits) {
         bits = 16;
-        while (bits < 28 && (1ull << bits) < n / 256) ++bits;
+        while (bits < 28 && (1ull << bits) < n / 1024) ++bits;  // regrown (the run repeats) past 3/4 full
     }
     u64 *gtab = nullptr;
     for (;;) {
