@@ -709,6 +709,9 @@ __global__ __launch_bounds__(256) void k_wcs_rows(RowArgs a) {
 #ifndef WR_WAVES
 #define WR_WAVES 4  // waves per workgroup
 #endif
+#ifndef WR_GPC
+#define WR_GPC 3    // resident workgroups per CU (LDS: 3 x 52 KiB)
+#endif
 constexpr u32 WR_W = WR_WAVES, WR_ROWS = 64, WR_M = 32, WR_TCAP = 192, WR_DCAP = 256;
 struct WrWave {
     u64 key[WR_DCAP];      // (row, h1)
@@ -1023,9 +1026,10 @@ __global__ __launch_bounds__(WR_W * 64) void k_wcs_wrows(RowArgs a) {
     WgAgg agg{l_id, l_cnt, l_first, l_rows};
     const u32 lane = lane_id(), wv = threadIdx.x >> 6;
     WrWave &W = l_w[wv];
-    const u64 r0 = 2 + ((u64)blockIdx.x * WR_W + wv) * WR_ROWS;
     WrCount cnt{0, 0, 0};
-    if (r0 < a.nrows) {
+    for (u64 blk = (u64)blockIdx.x * WR_W + wv;; blk += (u64)gridDim.x * WR_W) {
+        const u64 r0 = 2 + blk * WR_ROWS;
+        if (r0 >= a.nrows) break;
         const u32 nr = (u32)(a.nrows - r0 < WR_ROWS ? a.nrows - r0 : WR_ROWS);
         // lane k: row r0 + k spans [s_k, e_k)
         const u64 s_k = lane < nr ? a.rend[r0 - 1 + lane] : 0;
@@ -1349,6 +1353,7 @@ inline dim3 grid1(u64 n, u32 t = 256) { return dim3((u32)((n + t - 1) / t)); }
 // Host side.
 struct msa_wcs {
     int device = 0;
+    int cus = 0;  // compute units (k_wcs_wrows runs WR_GPC workgroups per CU)
     hipStream_t stream = nullptr;
     char err[512] = {0};
     // input
@@ -1435,6 +1440,8 @@ extern "C" int msa_wcs_create(int device, msa_wcs **out) {
     if (hipSetDevice(device) != hipSuccess) return MSA_ERR_HIP;
     msa_wcs *w = new msa_wcs();
     w->device = device;
+    if (hipDeviceGetAttribute(&w->cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || w->cus < 1)
+        w->cus = 1;
     if (hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking) != hipSuccess) {
         delete w;
         return MSA_ERR_HIP;
@@ -1692,8 +1699,12 @@ extern "C" int msa_wcs_run(msa_wcs *w) {
         // wave per row first; the rows it leaves (long, unusual quoting, many
         // token runs) are walked one thread per row (ablate bit 8: all of them)
         if (R > 2 && !(a.ablate & 8)) {
-            const u64 per = (u64)WR_W * WR_ROWS;
-            hipLaunchKernelGGL(k_wcs_wrows, dim3((u32)((R - 2 + per - 1) / per)), dim3(WR_W * 64), 0, st, a);
+            // persistent workgroups: each keeps its LDS aggregate over many
+            // row blocks, so the flush (device-scope atomics on the Zipf head)
+            // happens a few hundred times, not once per 256 rows
+            const u64 per = (u64)WR_W * WR_ROWS, blocks = (R - 2 + per - 1) / per;
+            const u64 g = (u64)w->cus * WR_GPC;
+            hipLaunchKernelGGL(k_wcs_wrows, dim3((u32)(blocks < g ? blocks : g)), dim3(WR_W * 64), 0, st, a);
             WCHECK(hipGetLastError());
             WCHECK(hipMemcpyAsync(&hc, ctr, sizeof hc, hipMemcpyDeviceToHost, st));
             WCHECK(hipStreamSynchronize(st));
