@@ -704,13 +704,13 @@ __global__ __launch_bounds__(256) void k_wcs_rows(RowArgs a) {
 // window merge only if their 64-bit keys agree in the other 59 -- written out
 // in first-occurrence order.
 #ifndef WR_LW
-#define WR_LW 2048  // workgroup aggregate of k_wcs_wrows (1024 at 3 workgroups per CU: 14.2 vs 12.7 ms)
+#define WR_LW 4096  // workgroup aggregate of k_wcs_wrows (2048 at 2 workgroups per CU 12.66 ms, 1024 at 3: 14.2)
 #endif
 #ifndef WR_WAVES
-#define WR_WAVES 4  // waves per workgroup
+#define WR_WAVES 8  // waves per workgroup
 #endif
 #ifndef WR_GPC
-#define WR_GPC 2    // resident workgroups per CU (LDS: 2 x 68 KiB)
+#define WR_GPC 1    // resident workgroups per CU (LDS: 136 KiB)
 #endif
 constexpr u32 WR_W = WR_WAVES, WR_ROWS = 64, WR_M = 32, WR_TCAP = 192, WR_DCAP = 256;
 struct WrWave {
