@@ -707,10 +707,10 @@ __global__ __launch_bounds__(256) void k_wcs_rows(RowArgs a) {
 #define WR_LW 4096  // workgroup aggregate of k_wcs_wrows (2048 at 2 workgroups per CU 12.66 ms, 1024 at 3: 14.2)
 #endif
 #ifndef WR_WAVES
-#define WR_WAVES 8  // waves per workgroup
+#define WR_WAVES 10  // waves per workgroup (LDS: 10 x 9 KiB + the 64 KiB aggregate; 8 waves: 12.28 vs 11.67 ms)
 #endif
 #ifndef WR_GPC
-#define WR_GPC 1    // resident workgroups per CU (LDS: 136 KiB)
+#define WR_GPC 1    // resident workgroups per CU (LDS: 152 KiB)
 #endif
 constexpr u32 WR_W = WR_WAVES, WR_ROWS = 64, WR_M = 32, WR_TCAP = 192, WR_DCAP = 256;
 struct WrWave {
