@@ -77,6 +77,10 @@ int msa_gen_corpus(const msa_gen_params *p, char **out, size_t *len);
  * ranges is msa_gen_corpus's output.  ZIPF / HIGHCARD only.               */
 int msa_gen_corpus_range(const msa_gen_params *p, uint64_t first_song, uint64_t n_songs, char **out, size_t *len);
 void msa_free(void *p);
+/* Identity of this build: the first 16 hex digits of the sha256 of the kernel
+ * sources, headers and compile flags it was built from (the same for every
+ * rebuild of the same sources).  PMC passes are stamped with it. */
+const char *msa_build_id(void);
 
 /* --------------------------------------------------------------- context */
 
@@ -256,6 +260,8 @@ typedef struct {
     uint64_t total_tokens; /* tokens counted                                  */
     uint64_t n_words;      /* distinct words = word_counts_global.csv lines   */
     uint64_t n_pairs;      /* word_counts_by_song.csv lines                   */
+    uint64_t fallback_rows;/* rows the wave-per-window walk left to the       */
+                           /* thread-per-row walk (long / unusual rows)       */
 } msa_wcs_summary;
 enum { MSA_WCS_GLOBAL = 0, MSA_WCS_BY_SONG = 1 };
 

@@ -857,7 +857,9 @@ __device__ __forceinline__ void wr_window(const RowArgs &a, WgAgg &agg, WrWave &
             if (W.fp[lane][2 * f + 1] == ~0u) W.fp[lane][2 * f + 1] = eo;
         if (rflag == 0 && nf > a.it) {
             const u32 ts = W.fp[lane][4], te = W.fp[lane][5];
-            atomicXor(&W.tgl[ts >> 4], 1u << (ts & 15));
+            // a last row without a newline can end at window byte 1023 with
+            // an empty text field: then ts == 1024, outside the window
+            if (ts < 1024) atomicXor(&W.tgl[ts >> 4], 1u << (ts & 15));
             if (te < 1024) atomicXor(&W.tgl[te >> 4], 1u << (te & 15));
         }
     }
@@ -887,7 +889,7 @@ __device__ __forceinline__ void wr_window(const RowArgs &a, WgAgg &agg, WrWave &
             W.ts[j] = (u16)((16 * lane + b) | ((rpre + __popc(RB & ((2u << b) - 1u)) - 1) << 10));
         }
         for (u32 mm = TE, j = je; mm; mm &= mm - 1, ++j) W.te[j] = (u16)(16 * lane + (u32)__builtin_ctz(mm) + 1u);
-        for (u32 k = lane; k < WR_DCAP; k += 64) { W.key[k] = 0; W.cnt[k] = 0; W.first[k] = ~0u; }
+        for (u32 k = lane; k < WR_DCAP; k += 64) { W.key[k] = 0; W.cnt[k] = 0; W.first[k] = ~0u; W.slot[k] = ~0u; }
         __builtin_amdgcn_wave_barrier();
         // one token per lane: lower-cased bytes hashed 8 at a time (TokHash)
         for (u32 t0 = 0; t0 < ntok; t0 += 64) {
@@ -948,7 +950,12 @@ __device__ __forceinline__ void wr_window(const RowArgs &a, WgAgg &agg, WrWave &
                 const u64 slot = (a.ablate & 48) ? (key & a.gmask) : g_insert(a, key, h2v, cur);
                 if (slot != ~0ull) {  // else overflow: the run repeats with a larger table
                     if (!(a.ablate & 32)) word_update<WR_LW>(a, agg, slot, ~(((base + s) << 20) | (u64)len));
-                    W.slot[h] = (u32)slot;  // the same value from every token of the word
+                    // the same value from every token of the word; two words
+                    // whose (row, h1) keys agree in the window's 59 hash bits
+                    // but that own different global slots are a collision
+                    // (detected and reported, like the global h1 check)
+                    const u32 prev = atomicCAS(&W.slot[h], ~0u, (u32)slot);
+                    if (prev != ~0u && prev != (u32)slot) atomicAdd((unsigned long long *)&a.ctr->collision, 1ull);
                 }
             }
             if (t < ntok) { W.ts[t] = (u16)(h | (rj << 10)); W.te[t] = (u16)(ok ? ord : 0xFFFFu); }
@@ -1361,6 +1368,7 @@ struct msa_wcs {
     u64 n = 0, cap = 0;
     // rows
     u64 nrows = 0;  // incl. header
+    u64 fallback_rows = 0;  // last run: rows left to k_wcs_rows
     u64 *d_rend = nullptr;
     u64 rend_cap = 0;
     // results (device)
@@ -1710,11 +1718,13 @@ extern "C" int msa_wcs_run(msa_wcs *w) {
             WCHECK(hipStreamSynchronize(st));
             if (getenv("MSA_WCS_DEBUG")) fprintf(stderr, "k_wcs_wrows: %llu of %llu rows left to k_wcs_rows\n",
                                                  (unsigned long long)hc.fallback, (unsigned long long)(R - 2));
+            w->fallback_rows = hc.fallback;
             if (hc.fallback) {
                 a.rows = fb;
                 hipLaunchKernelGGL(k_wcs_rows, grid1(hc.fallback), dim3(256), 0, st, a);
             }
         } else if (R > 2) {
+            w->fallback_rows = R - 2;
             hipLaunchKernelGGL(k_wcs_rows, grid1(R - 2), dim3(256), 0, st, a);
         }
         WCHECK(hipGetLastError());
@@ -1796,6 +1806,7 @@ extern "C" int msa_wcs_run(msa_wcs *w) {
     w->sum.total_tokens = hc.tokens;
     w->sum.n_words = nw;
     w->sum.n_pairs = np;
+    w->sum.fallback_rows = w->fallback_rows;
     w->have = true;
     return MSA_OK;
 }

@@ -37,7 +37,7 @@ PROF_MAX = 16
 
 # Every symbol include/msa_hip.h declares (tests check the .so exports them).
 EXPORTS = [
-    "msa_gen_corpus", "msa_gen_corpus_range", "msa_free", "msa_create", "msa_destroy", "msa_last_error",
+    "msa_gen_corpus", "msa_gen_corpus_range", "msa_free", "msa_build_id", "msa_create", "msa_destroy", "msa_last_error",
     "msa_stream", "msa_sync", "msa_load_csv", "msa_bind_csv", "msa_split_columns",
     "msa_count", "msa_rank", "msa_run", "msa_get_summary", "msa_get_ranked",
     "msa_write_table_csv", "msa_get_split_column", "msa_set_profiling", "msa_get_profile",
@@ -97,7 +97,8 @@ class _Profile(C.Structure):
 
 
 class _WcsSummary(C.Structure):
-    _fields_ = [(n, C.c_uint64) for n in ("total_rows", "song_rows", "total_tokens", "n_words", "n_pairs")]
+    _fields_ = [(n, C.c_uint64) for n in ("total_rows", "song_rows", "total_tokens", "n_words", "n_pairs",
+                                                   "fallback_rows")]
 
 
 _lib = None
@@ -116,6 +117,8 @@ def load(path: str = LIB_PATH):
     lib.msa_gen_corpus_range.argtypes = [C.POINTER(_GenParams), u64, u64, C.POINTER(C.c_void_p), C.POINTER(sz)]
     lib.msa_free.argtypes = [vp]
     lib.msa_free.restype = None
+    lib.msa_build_id.argtypes = []
+    lib.msa_build_id.restype = C.c_char_p
     lib.msa_create.argtypes = [i, C.POINTER(vp)]
     lib.msa_destroy.argtypes = [vp]
     lib.msa_destroy.restype = None
@@ -168,6 +171,11 @@ def load(path: str = LIB_PATH):
     lib.msa_csvcol_get.argtypes = [vp, u64, C.POINTER(C.c_void_p), C.POINTER(sz)]
     _lib = lib
     return lib
+
+
+def build_id() -> str:
+    """msa_build_id(): hash of the sources + flags this libmsa_hip.so was built from."""
+    return load().msa_build_id().decode()
 
 
 def _bytes_at(ptr, n: int) -> bytes:

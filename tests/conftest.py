@@ -50,7 +50,20 @@ def read_outputs(outdir):
     return out
 
 
-def run_oracle(csv_path, outdir, ranks=1, word_limit=0, artist_limit=0):
+def files_equal(a, b, chunk=1 << 24):
+    """Byte-for-byte comparison of two (possibly multi-GB) files."""
+    if os.path.getsize(a) != os.path.getsize(b):
+        return False
+    with open(a, "rb") as fa, open(b, "rb") as fb:
+        while True:
+            x, y = fa.read(chunk), fb.read(chunk)
+            if x != y:
+                return False
+            if not x:
+                return True
+
+
+def run_oracle(csv_path, outdir, ranks=1, word_limit=0, artist_limit=0, timeout=300):
     """The CPU oracle (C restatement of parallel_spotify.c, virtual np)."""
     if not os.path.exists(ORACLE):
         # a missing checker must never turn parity tests into skips
@@ -60,7 +73,7 @@ def run_oracle(csv_path, outdir, ranks=1, word_limit=0, artist_limit=0):
         cmd += ["--word-limit", str(word_limit)]
     if artist_limit:
         cmd += ["--artist-limit", str(artist_limit)]
-    p = subprocess.run(cmd, capture_output=True, timeout=300)
+    p = subprocess.run(cmd, capture_output=True, timeout=timeout)
     return p
 
 
@@ -98,3 +111,25 @@ def golden_dialect(case_dir):
         return detect_csv_params(read_sample(os.path.join(case_dir, "input.csv")))
     except UnicodeDecodeError:
         return ",", False
+
+
+# BASELINE configs[3]'s corpus family at a size one GPU box holds twice over:
+# 20M songs of the bench generator (~4.7 GB > 2^32 bytes).  Written once per
+# session with its oracle outputs (np = 1); test_gpu_scale.py runs it on one
+# context, test_gpu_dist.py as sharded worlds (Python driver and C host).
+C3_SONGS = 20_000_000
+
+
+@pytest.fixture(scope="session")
+def configs3_corpus(msa_mod, tmp_path_factory):
+    d = tmp_path_factory.mktemp("c3")
+    path = str(d / "c3.csv")
+    data = msa_mod.gen_corpus(C3_SONGS, mode="zipf", seed=1, vocab=50000, n_artists=5000, words_per_song=30)
+    assert len(data) > (1 << 32)
+    with open(path, "wb") as f:
+        f.write(data)
+    del data
+    od = str(d / "o")
+    r = run_oracle(path, od, ranks=1, timeout=600)
+    assert r.returncode == 0, r.stderr
+    return path, od

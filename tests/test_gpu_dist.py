@@ -12,7 +12,7 @@ import sys
 
 import pytest
 
-from conftest import PKG, REPO, read_outputs, run_oracle
+from conftest import PKG, REPO, files_equal, read_outputs, run_oracle
 
 pytestmark = pytest.mark.gpu
 
@@ -24,11 +24,14 @@ import msa
 from msa import dist as mdist
 rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
 dist.init_process_group("gloo", rank=rank, world_size=world)
-data = open(os.environ["MSA_CSV"], "rb").read()
 cuts = json.loads(os.environ["MSA_CUTS"])
 lo, hi = cuts[rank], cuts[rank + 1]
+with open(os.environ["MSA_CSV"], "rb") as f:  # this rank's byte range only
+    f.seek(lo)
+    data = f.read(hi - lo)
 ctx = msa.Context(0)
-ctx.load_csv(data[lo:hi])
+ctx.load_csv(data)
+del data
 comm = mdist.Comm()
 songs, words = mdist.run_sharded(ctx, comm, text_column=False)
 if mdist.gather_ranked(ctx, comm):
@@ -51,9 +54,10 @@ def free_port():
     return p
 
 
-def run_world(tmp_path, data, cuts):
-    csv = tmp_path / "in.csv"
-    csv.write_bytes(data)
+def run_world(tmp_path, data, cuts, csv=None, timeout=240):
+    if csv is None:
+        csv = tmp_path / "in.csv"
+        csv.write_bytes(data)
     script = tmp_path / "worker.py"
     script.write_text(WORKER)
     out = str(tmp_path / "res")
@@ -68,7 +72,7 @@ def run_world(tmp_path, data, cuts):
     logs = []
     for p in procs:
         try:
-            o, _ = p.communicate(timeout=240)
+            o, _ = p.communicate(timeout=timeout)
         except subprocess.TimeoutExpired:
             for q in procs:
                 q.kill()
@@ -156,3 +160,65 @@ def test_sharded_highcard_every_table_overflows(msa_mod, tmp_path):
     assert tot == {k: exp["metrics"][k] for k in ("total_songs", "total_words")}
     assert words == exp["word_counts.csv"]
     assert artists == exp["top_artists.csv"]
+
+
+# ---- BASELINE configs[3]'s shape: ONE logical multi-GB corpus (20M songs,
+# ~4.7 GB, conftest.configs3_corpus) sharded over several ranks.  On this
+# one-GPU box the ranks share the GPU; the exchanges go through host memory
+# (gloo / the C host's shared-memory transport) instead of RCCL over xGMI --
+# the data flow, boundaries and merge are the ones an 8-GPU node runs.
+def file_cuts(path, world):
+    """Cuts just after the opening quote of a lyric near every n*r/world."""
+    n = os.path.getsize(path)
+    cs = [0]
+    with open(path, "rb") as f:
+        for r in range(1, world):
+            f.seek(n * r // world)
+            w = f.read(1 << 16)
+            cs.append(n * r // world + w.index(b',"') + 2)
+    return cs + [n]
+
+
+@pytest.mark.timeout(900)
+def test_configs3_two_ranks_cut_in_quotes(msa_mod, configs3_corpus, tmp_path):
+    """2 ranks (Python driver over torch.distributed) on the 4.7 GB corpus, the
+    cut inside a quoted lyric: exact boundary exchange, key-hash all-to-all
+    merge, device-side gather -- identical to the oracle at np = 1."""
+    path, od = configs3_corpus
+    words, artists, tot = run_world(tmp_path, None, file_cuts(path, 2), csv=path, timeout=600)
+    exp = read_outputs_tables(od)
+    assert tot == {k: exp["metrics"][k] for k in ("total_songs", "total_words")}
+    assert words == exp["word_counts.csv"]
+    assert artists == exp["top_artists.csv"]
+
+
+def read_outputs_tables(od):
+    with open(os.path.join(od, "performance_metrics.json")) as f:
+        m = json.load(f)
+    return {"word_counts.csv": open(os.path.join(od, "word_counts.csv"), "rb").read(),
+            "top_artists.csv": open(os.path.join(od, "top_artists.csv"), "rb").read(),
+            "metrics": {k: m[k] for k in ("total_songs", "total_words")}}
+
+
+@pytest.mark.timeout(900)
+def test_configs3_c_host_four_ranks_shm(configs3_corpus, tmp_path):
+    """The drop-in C host with --processes 4 (MSA_TRANSPORT=shm: four ranks on
+    the one GPU) on the 4.7 GB corpus: every output file identical to the
+    oracle's at np = 1, performance_metrics.json reports 4 processes."""
+    path, od = configs3_corpus
+    cli = os.path.join(PKG, "bin", "parallel_spotify")
+    out = tmp_path / "out"
+    env = dict(os.environ, MSA_TRANSPORT="shm")
+    p = subprocess.run([cli, path, "--output-dir", str(out), "--processes", "4"], capture_output=True, timeout=800,
+                       env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    for f in ("word_counts.csv", "top_artists.csv"):
+        assert files_equal(str(out / f), os.path.join(od, f)), f
+    names = sorted(os.listdir(os.path.join(od, "split_columns")))
+    assert sorted(os.listdir(out / "split_columns")) == names
+    for n in names:
+        assert files_equal(str(out / "split_columns" / n), os.path.join(od, "split_columns", n)), n
+    with open(out / "performance_metrics.json") as f:
+        m = json.load(f)
+    e = read_outputs_tables(od)["metrics"]
+    assert m["processes"] == 4 and (m["total_songs"], m["total_words"]) == (e["total_songs"], e["total_words"])

@@ -15,7 +15,7 @@ import subprocess
 
 import pytest
 
-from conftest import GOLDEN, PKG, read_outputs, run_oracle
+from conftest import GOLDEN, PKG, files_equal, read_outputs, run_oracle
 from test_gpu_parity import check_against_oracle
 
 pytestmark = pytest.mark.gpu
@@ -105,15 +105,92 @@ def test_configs2_full_size(msa_mod, ctx, tmp_path):
     check_against_oracle(msa_mod, ctx, data, tmp_path, "configs2")
 
 
+def check_files_against_oracle(msa_mod, c, od, tmp_path):
+    """The context's ranked tables (written by msa_write_table_csv), split
+    columns and totals against the oracle's output directory, byte for byte."""
+    s = c.summary()
+    words, artists = str(tmp_path / "w.csv"), str(tmp_path / "a.csv")
+    c.write_table_csv(msa_mod.MSA_TABLE_WORDS, words, "word")
+    c.write_table_csv(msa_mod.MSA_TABLE_ARTISTS, artists, "artist")
+    assert files_equal(words, os.path.join(od, "word_counts.csv")), "word_counts.csv differs"
+    assert files_equal(artists, os.path.join(od, "top_artists.csv")), "top_artists.csv differs"
+    for which, name in ((0, s.artist_file), (1, s.text_file)):
+        with open(os.path.join(od, "split_columns", name + ".csv"), "rb") as f:
+            assert c.split_column(which) == f.read(), f"split column {name}.csv differs"
+    m = read_metrics(od)
+    assert (s.total_songs, s.total_words) == (m["total_songs"], m["total_words"])
+    return s
+
+
+def read_metrics(od):
+    import json
+
+    with open(os.path.join(od, "performance_metrics.json")) as f:
+        return json.load(f)
+
+
 @pytest.mark.timeout(900)
-def test_corpus_over_4gib(msa_mod, tmp_path):
-    """A 20M-song corpus (~4.7 GB > 2^32 bytes) on one GPU against the oracle:
-    no 32-bit byte offset anywhere in the pipeline (at N = 2 the configs[3]
-    shards are ~12 GB per GPU)."""
-    data = msa_mod.gen_corpus(20_000_000, mode="zipf", seed=1, vocab=50000, n_artists=5000, words_per_song=30)
-    assert len(data) > (1 << 32)
+def test_corpus_over_4gib(msa_mod, configs3_corpus, tmp_path):
+    """A 20M-song corpus (~4.7 GB > 2^32 bytes; configs[3]'s corpus family) on
+    one GPU against the oracle: no 32-bit byte offset anywhere in the pipeline
+    (at N = 2 the configs[3] shards are ~12 GB per GPU)."""
+    path, od = configs3_corpus
+    with open(path, "rb") as f:
+        data = f.read()
     with msa_mod.Context(0) as c:
-        check_against_oracle(msa_mod, c, data, tmp_path, "over4g")
+        c.load_csv(data)
+        del data
+        c.run(text_column=True)
+        check_files_against_oracle(msa_mod, c, od, tmp_path)
+
+
+# BASELINE configs[4]: the adversarial high-cardinality corpus at full scale.
+# highcard seed 4 at 4.1M songs holds > 50M distinct words and > 1.7M artists
+# (skewed); every table grows several times (the reference's ht_resize,
+# parallel_spotify.c:101-132), the miss logs overflow into direct inserts, the
+# ranking runs the radix sort with 16-byte-prefix tie refinement.
+C4_SONGS = 4_100_000
+
+
+@pytest.fixture(scope="module")
+def configs4(msa_mod, tmp_path_factory):
+    d = tmp_path_factory.mktemp("c4")
+    path = str(d / "c4.csv")
+    data = msa_mod.gen_corpus(C4_SONGS, mode="highcard", seed=4)
+    with open(path, "wb") as f:
+        f.write(data)
+    od = str(d / "o")
+    r = run_oracle(path, od, ranks=1, timeout=600)
+    assert r.returncode == 0, r.stderr
+    return data, path, od
+
+
+@pytest.mark.timeout(900)
+def test_configs4_run(msa_mod, configs4, tmp_path):
+    data, _, od = configs4
+    with msa_mod.Context(0) as c:  # fresh context: every table starts small
+        c.load_csv(data)
+        c.run(text_column=True)
+        s = check_files_against_oracle(msa_mod, c, od, tmp_path)
+        assert s.n_words >= 50_000_000 and s.n_artists > 1_000_000
+
+
+@pytest.mark.timeout(900)
+def test_configs4_cli(configs4, tmp_path):
+    """The drop-in CLI on the same corpus: word_counts.csv, top_artists.csv and
+    both split-column files identical to the oracle's."""
+    _, path, od = configs4
+    out = tmp_path / "out"
+    p = subprocess.run([CLI, path, "--output-dir", str(out)], capture_output=True, timeout=600)
+    assert p.returncode == 0, p.stderr
+    for f in ("word_counts.csv", "top_artists.csv"):
+        assert files_equal(str(out / f), os.path.join(od, f)), f
+    names = sorted(os.listdir(os.path.join(od, "split_columns")))
+    assert sorted(os.listdir(out / "split_columns")) == names
+    for n in names:
+        assert files_equal(str(out / "split_columns" / n), os.path.join(od, "split_columns", n)), n
+    m, e = read_metrics(str(out)), read_metrics(od)
+    assert (m["total_songs"], m["total_words"]) == (e["total_songs"], e["total_words"])
 
 
 @pytest.mark.parametrize("sort", ["radix", "merge"])

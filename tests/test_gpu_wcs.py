@@ -192,3 +192,89 @@ def test_wcs_cli_prints_paths_like_pathlib(msa_mod, outdir, tmp_path):
     want = (f"Concluído. Processadas {exp[0]} linhas. Arquivos gerados em {os.fspath(od)}\n"
             f" - {os.fspath(od / 'word_counts_global.csv')}\n - {os.fspath(od / 'word_counts_by_song.csv')}\n")
     assert r.stdout.decode() == want
+
+
+# ---- k_wcs_wrows (wave per window of whole rows) at its boundaries: every
+# input runs twice, once with the default path and once with every row on the
+# thread-per-row walk (MSA_WCS_ABLATE=8); both must equal the oracle, and the
+# summary says how many rows the window walk left to the per-row walk.
+def _window_edges(seed):
+    """Rows sized around the window's 1 KiB span (row ends at offsets 1008..1040
+    of a 16-byte aligned start, rows over 1 KiB), windows of 32 tiny rows,
+    windows with more than 192 token runs, the text as the FIRST column, and a
+    last row with no newline ending in an empty text field."""
+    rng = random.Random(seed)
+    text_first = seed % 2 == 1
+    rows = ["text,artist,song,link" if text_first else "artist,song,link,text"]
+
+    def row(i, text):
+        t = '"' + text.replace('"', '""') + '"' if rng.random() < 0.5 or "\n" in text or "," in text else text
+        return f"{t},A{i % 5},S{i},/l/{i}" if text_first else f"A{i % 5},S{i},/l/{i},{t}"
+
+    i = 0
+    for _ in range(60):
+        kind = rng.randrange(5)
+        if kind == 0:      # one row whose end sweeps the window's last bytes
+            n = rng.randrange(1000, 1045)
+            words = []
+            while sum(len(w) + 1 for w in words) < n:
+                words.append(rng.choice(["alpha", "be", "gamma", "don't", "x", "zeta", "ÀÉÎ", "night"]))
+            rows.append(row(i, " ".join(words)[:n]))
+        elif kind == 1:    # a run of tiny rows (windows of WR_M = 32 rows)
+            for _ in range(rng.randrange(30, 70)):
+                rows.append(row(i, rng.choice(["ok", "yes yes", "", "la la la", "hey"])))
+                i += 1
+        elif kind == 2:    # > 192 token runs in one window
+            rows.append(row(i, " ".join(rng.choice("abcdefgh") for _ in range(rng.randrange(300, 700)))))
+        elif kind == 3:    # a row over 1 KiB
+            rows.append(row(i, ("long words keep going " * rng.randrange(50, 120)).strip()))
+        else:              # padding rows of random length shift the alignment
+            rows.append(row(i, "pad " * rng.randrange(1, 40) + "end"))
+        i += 1
+    body = "\n".join(rows) + "\n"
+    # the last row: no newline, its text field empty (ends with the delimiter)
+    body += "Z,S9,/l/9," if not text_first else ",Z,S9,/l/9"
+    return body.encode("utf-8")
+
+
+def _run_both(msa_mod, wcs, data, monkeypatch):
+    monkeypatch.delenv("MSA_WCS_ABLATE", raising=False)
+    got = wcs.run(data)
+    fb = wcs.summary()["fallback_rows"]
+    monkeypatch.setenv("MSA_WCS_ABLATE", "8")
+    try:
+        walked = wcs.run(data)
+        assert wcs.summary()["fallback_rows"] > 0  # every row on the per-row walk
+    finally:
+        monkeypatch.delenv("MSA_WCS_ABLATE", raising=False)
+    return got, walked, fb
+
+
+@pytest.mark.parametrize("seed", range(1, 9))
+def test_wcs_window_edges_both_paths(msa_mod, wcs, seed, monkeypatch):
+    data = _window_edges(seed)
+    exp = wcs_oracle.word_count_per_song(data)
+    got, walked, fb = _run_both(msa_mod, wcs, data, monkeypatch)
+    assert walked == exp
+    assert got == exp
+    assert fb > 0  # rows over 1 KiB / windows over WR_TCAP token runs took the per-row walk
+
+
+def test_wcs_window_walk_takes_every_plain_row(msa_mod, wcs, monkeypatch):
+    """Plain Zipf input: the window walk settles every row itself."""
+    data = msa_mod.gen_corpus(3000, mode="zipf", seed=77, vocab=4000)
+    got, walked, fb = _run_both(msa_mod, wcs, data, monkeypatch)
+    assert got == walked == wcs_oracle.word_count_per_song(data)
+    assert fb == 0
+
+
+@pytest.mark.parametrize("shift", range(0, 48, 3))
+def test_wcs_row_end_sweeps_window_end(msa_mod, wcs, shift, monkeypatch):
+    """A first row of 1000 + shift bytes ends at every offset around byte 1023
+    of its window; the short rows after it follow at every alignment."""
+    hdr = "artist,song,link,text\n"
+    first = "A,S0,/l/0," + ("word " * 400)[: 1000 + shift - len("A,S0,/l/0,") - 1] + "\n"
+    rest = "".join(f"A,S{i},/l/{i},tiny row {i} words\n" for i in range(1, 40))
+    data = (hdr + first + rest).encode()
+    got, walked, _ = _run_both(msa_mod, wcs, data, monkeypatch)
+    assert got == walked == wcs_oracle.word_count_per_song(data)

@@ -12,28 +12,26 @@ Per kernel of the bench step, per launch (mean over dispatches):
                 (atomics leaving the L2 to memory), TA_*_ATOMIC_WAVEFRONTS_sum
                 (atomic wave instructions issued), SQ_INSTS_LDS_ATOMIC
   sq          SQ_LDS_BANK_CONFLICT (cycles), SQ_INSTS_LDS, waits, ...
-The file is stamped with the sha256 of the libmsa_hip.so in this tree and with
-the bench line the passes ran (input bytes, K3 algorithmic bytes)."""
+The file is stamped with the build id of the libmsa_hip.so in this tree
+(msa_build_id(): hash of the kernel sources + flags, stable across rebuilds)
+and with the bench line the passes ran (input bytes, K3 algorithmic bytes)."""
 import csv
 import glob
-import hashlib
 import json
 import os
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB = os.path.join(REPO, "music-analyst-ai_amd", "libmsa_hip.so")
+sys.path.insert(0, os.path.join(REPO, "music-analyst-ai_amd"))
 KERNELS = ["k_scan_csv", "k_miss_agg", "k_chunk_summary", "k_rec_spans", "k_rec_fast", "k_rec_fix", "k_col_gather", "k_col_lines",
            "k_artist_count", "k_tile_sort", "k_merge_pass"]
 PASSES = ["fetch", "write", "sq", "atomic"]
 
 
-def lib_sha256(path=LIB):
-    h = hashlib.sha256()
-    with open(path, "rb") as f:
-        for b in iter(lambda: f.read(1 << 20), b""):
-            h.update(b)
-    return h.hexdigest()
+def build_id():
+    import msa  # ctypes only: no GPU call
+
+    return msa.build_id()
 
 
 def short(name):
@@ -81,7 +79,7 @@ def main():
         kernels[k] = e
     b = bench_line(os.path.join(out, "fetch.log"))
     res = {
-        "lib_sha256": lib_sha256(),
+        "build_id": build_id(),
         "input_bytes": b["config"]["bytes_per_gpu"] if b else None,
         "roofline_kernel": "k_scan_csv",
         "alg_bytes_per_launch": b["roofline"]["alg_bytes_per_launch"] if b else None,
