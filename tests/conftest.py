@@ -24,8 +24,44 @@ if PKG not in sys.path:
     sys.path.insert(0, PKG)
 
 
+_CONFIG = None
+
+
 def pytest_configure(config):
+    global _CONFIG
+    _CONFIG = config
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs libmsa_hip kernels)")
+
+
+def say(msg):
+    """A line on the terminal now, past pytest's output capture: long fixture
+    work (multi-GB corpora, their oracle runs) shows progress instead of
+    looking hung."""
+    capman = _CONFIG.pluginmanager.getplugin("capturemanager") if _CONFIG else None
+    if capman is None:
+        print(msg, flush=True)
+        return
+    with capman.global_and_fixture_disabled():
+        print(msg, flush=True)
+
+
+def run_with_heartbeat(cmd, timeout, what, every=30, env=None):
+    """subprocess.run(cmd) that prints a progress line every `every` seconds."""
+    import time
+
+    t0 = time.time()
+    with subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, env=env) as p:
+        while True:
+            try:
+                out, err = p.communicate(timeout=every)
+                break
+            except subprocess.TimeoutExpired:
+                if time.time() - t0 > timeout:
+                    p.kill()
+                    p.communicate()
+                    raise
+                say(f"  [{what}: {time.time() - t0:.0f} s]")
+    return subprocess.CompletedProcess(cmd, p.returncode, out, err)
 
 
 def _read(path):
@@ -73,8 +109,7 @@ def run_oracle(csv_path, outdir, ranks=1, word_limit=0, artist_limit=0, timeout=
         cmd += ["--word-limit", str(word_limit)]
     if artist_limit:
         cmd += ["--artist-limit", str(artist_limit)]
-    p = subprocess.run(cmd, capture_output=True, timeout=timeout)
-    return p
+    return run_with_heartbeat(cmd, timeout, "oracle " + os.path.basename(csv_path))
 
 
 @pytest.fixture(scope="session")

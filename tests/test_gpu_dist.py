@@ -12,7 +12,7 @@ import sys
 
 import pytest
 
-from conftest import PKG, REPO, files_equal, read_outputs, run_oracle
+from conftest import PKG, REPO, files_equal, read_outputs, run_oracle, run_with_heartbeat
 
 pytestmark = pytest.mark.gpu
 
@@ -209,8 +209,8 @@ def test_configs3_c_host_four_ranks_shm(configs3_corpus, tmp_path):
     cli = os.path.join(PKG, "bin", "parallel_spotify")
     out = tmp_path / "out"
     env = dict(os.environ, MSA_TRANSPORT="shm")
-    p = subprocess.run([cli, path, "--output-dir", str(out), "--processes", "4"], capture_output=True, timeout=800,
-                       env=env)
+    p = run_with_heartbeat([cli, path, "--output-dir", str(out), "--processes", "4"], 800, "parallel_spotify -np 4",
+                           env=env)
     assert p.returncode == 0, p.stderr[-3000:]
     for f in ("word_counts.csv", "top_artists.csv"):
         assert files_equal(str(out / f), os.path.join(od, f)), f

@@ -15,7 +15,7 @@ import subprocess
 
 import pytest
 
-from conftest import GOLDEN, PKG, files_equal, read_outputs, run_oracle
+from conftest import GOLDEN, PKG, files_equal, read_outputs, run_oracle, run_with_heartbeat
 from test_gpu_parity import check_against_oracle
 
 pytestmark = pytest.mark.gpu
@@ -181,7 +181,7 @@ def test_configs4_cli(configs4, tmp_path):
     both split-column files identical to the oracle's."""
     _, path, od = configs4
     out = tmp_path / "out"
-    p = subprocess.run([CLI, path, "--output-dir", str(out)], capture_output=True, timeout=600)
+    p = run_with_heartbeat([CLI, path, "--output-dir", str(out)], 600, "parallel_spotify configs[4]")
     assert p.returncode == 0, p.stderr
     for f in ("word_counts.csv", "top_artists.csv"):
         assert files_equal(str(out / f), os.path.join(od, f)), f

@@ -9,11 +9,17 @@ set -eo pipefail
 export TMPDIR=/tmp
 D=gpurun_out/${1:-final}
 mkdir -p $D
-timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 600 --timeout-method thread > $D/gpu_tests.log 2>&1
+# test failures (rc 1) are reported and the measurements still run; anything
+# else (a crash, a time limit) ends the script here
+rc=0
+timeout -k 10 1000 python -u -m pytest tests -m gpu -v --durations=15 --timeout 600 --timeout-method thread \
+    > $D/gpu_tests.log 2>&1 || rc=$?
+echo "pytest rc $rc"
+[ $rc -le 1 ] || exit $rc
 timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $D/smoke.log 2>&1
 bash tools/pmc.sh $D/pmc
 cp $D/pmc/pmc.json profiles/pmc_scan_main.json
 timeout -k 10 300 python -u bench.py > $D/bench.json 2> $D/bench.err
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $D/prof -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline > $D/prof.log 2>&1
 timeout -k 10 300 python -u tools/bench_wcs.py > $D/bench_wcs.json 2> $D/bench_wcs.err
-echo done
+echo done; exit $rc
