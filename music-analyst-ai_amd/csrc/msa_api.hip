@@ -84,6 +84,7 @@ struct Ranked {
     DevBuf K[3][3];  // [set][k2,k1,k0]: set 0 = input, 1/2 = ping-pong
     DevBuf V[3];
     DevBuf ref, cnt, order, len, off, blob, counts;
+    DevBuf scan_bsum, scan_total;  // the blob offsets' scan scratch (the two tables rank concurrently)
     u64 n = 0, blob_len = 0, blob_cap = 0;
     bool blob_pending = false;  // blob_len not read back yet (do_rank's sync)
     BlobArgs pending{};
@@ -202,6 +203,10 @@ struct msa_ctx {
     // point that could touch its buffers joins it first (join_side)
     hipStream_t side = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    // the artist table is ranked on a stream of its own beside the word table
+    // (both small-table sorts are launch/latency-bound chains)
+    hipStream_t rank2 = nullptr;
+    hipEvent_t ev_r2_fork = nullptr, ev_r2_join = nullptr;
     bool side_pending = false;
     // text.csv is launched after the counting (it shares the CUs badly with
     // the per-CU artist tables): on the side stream during the ranking, or on
@@ -1113,8 +1118,12 @@ static int refine_ties(msa_ctx *c, Ranked &R, int cur, const u8 *wbuf, const u8 
     return fail(c, MSA_ERR_COLLISION, "tie refinement did not converge (equal keys in one table)");
 }
 
+static bool small_sort(const msa_ctx *c, u64 n) { return c->sort_mode == 1 || (c->sort_mode == 0 && n < kRadixMin); }
+
+// Sort + key blob of one table on stream st (the radix path -- large tables --
+// reads back tie counts and runs on the library stream only).
 static int sort_and_blob(msa_ctx *c, Ranked &R, const u8 *wbuf, const u8 *wextra, const u8 *arena, const u64 *key_off,
-                         const u32 *key_len, int slot, u64 est) {
+                         const u32 *key_len, int slot, u64 est, hipStream_t st) {
     const u64 n = R.n;
     R.host_valid = false;
     R.blob_pending = n != 0;
@@ -1138,38 +1147,39 @@ static int sort_and_blob(msa_ctx *c, Ranked &R, const u8 *wbuf, const u8 *wextra
     // large tables: LSD radix sort (msa_sort.hip); small ones: LDS bitonic
     // tiles + merge passes (launch-bound sizes).  MSA_SORT=radix|merge forces one.
     HIPC(c, ensure(R.order, n * 4));
-    if (c->sort_mode == 2 || (c->sort_mode == 0 && n >= kRadixMin)) {
+    if (!small_sort(c, n)) {
+        if (st != c->stream) return fail(c, MSA_ERR_ARG, "radix ranking runs on the library stream");
         HIPC(c, ensure(c->sort_scratch, msa_radix_scratch_bytes(n)));
         HIPC(c, msa_radix_sort(k2, k1, k0, vv, n, &cur, c->sort_scratch.as<u8>(), c->stream));
         int rc;
         if ((rc = refine_ties(c, R, cur, wbuf, wextra, arena, key_off, key_len))) return rc;
     } else {
-        HIPC(c, msa_launch_sort(k2, k1, k0, vv, n, &cur, c->stream));
+        HIPC(c, msa_launch_sort(k2, k1, k0, vv, n, &cur, st));
         HIPC(c, msa_launch_fixup(R.K[cur][0].as<u64>(), R.K[cur][1].as<u64>(), R.K[cur][2].as<u64>(),
                                  R.V[cur].as<u32>(), n, R.ref.as<u64>(), wbuf, wextra, c->l_pos.as<u64>(),
-                                 c->l_len.as<u32>(), arena, key_off, key_len, R.order.as<u32>(), c->stream));
+                                 c->l_len.as<u32>(), arena, key_off, key_len, R.order.as<u32>(), st));
     }
     // key blob in rank order
     HIPC(c, ensure(R.len, n * 8));
     HIPC(c, ensure(R.off, (n + 1) * 8));
     HIPC(c, ensure(R.counts, n * 8));
-    HIPC(c, ensure(c->scan_total, 64));
-    HIPC(c, ensure(c->scan_bsum, ((n + 1023) / 1024 + 1) * 8));
+    HIPC(c, ensure(R.scan_total, 64));
+    HIPC(c, ensure(R.scan_bsum, ((n + 1023) / 1024 + 1) * 8));
     HIPC(c, msa_launch_blob(R.order.as<u32>(), n, R.ref.as<u64>(), R.K[0][1].as<u64>(), R.K[0][2].as<u64>(),
                             R.cnt.as<u64>(), wbuf, wextra, c->l_pos.as<u64>(), c->l_len.as<u32>(), arena, key_off, key_len,
-                            R.len.as<u64>(), R.off.as<u64>(), c->scan_bsum.as<u64>(), c->scan_total.as<u64>(), nullptr,
-                            nullptr, 0, c->stream, 0));
+                            R.len.as<u64>(), R.off.as<u64>(), R.scan_bsum.as<u64>(), R.scan_total.as<u64>(), nullptr,
+                            nullptr, 0, st, 0));
     // the blob length stays on the device until do_rank's one sync: the blob is
     // sized from what the host knows (the last run's length, or an estimate)
     // and k_blob_write skips keys past that capacity (do_rank redoes them)
     HIPC(c, ensure(c->blob_tot, 64));
-    HIPC(c, hipMemcpyAsync(c->blob_tot.as<u64>() + slot, c->scan_total.p, 8, hipMemcpyDeviceToDevice, c->stream));
+    HIPC(c, hipMemcpyAsync(c->blob_tot.as<u64>() + slot, R.scan_total.p, 8, hipMemcpyDeviceToDevice, st));
     HIPC(c, ensure(R.blob, std::max<u64>(est, R.blob_len) + 16));
     R.blob_cap = R.blob.cap - 16;
     HIPC(c, msa_launch_blob(R.order.as<u32>(), n, R.ref.as<u64>(), R.K[0][1].as<u64>(), R.K[0][2].as<u64>(),
                             R.cnt.as<u64>(), wbuf, wextra, c->l_pos.as<u64>(), c->l_len.as<u32>(), arena, key_off, key_len,
-                            R.len.as<u64>(), R.off.as<u64>(), c->scan_bsum.as<u64>(), c->scan_total.as<u64>(),
-                            R.blob.as<u8>(), R.counts.as<u64>(), R.blob_cap, c->stream, 1));
+                            R.len.as<u64>(), R.off.as<u64>(), R.scan_bsum.as<u64>(), R.scan_total.as<u64>(),
+                            R.blob.as<u8>(), R.counts.as<u64>(), R.blob_cap, st, 1));
     R.pending = BlobArgs{wbuf, wextra, arena, key_off, key_len};
     return MSA_OK;
 }
@@ -1212,12 +1222,19 @@ static int do_rank(msa_ctx *c) {
     const u8 *wbuf = c->merged_w ? c->imp_w.as<u8>() : c->in;
     const u8 *wextra = c->merged_w ? c->imp_w.as<u8>() : c->extra.as<u8>();
     const u64 west = c->h_ctr.s_claimed * 8 + c->h_ctr.m_claimed * 16 + c->h_ctr.l_claimed * 48;
-    if ((rc = sort_and_blob(c, W, wbuf, wextra, nullptr, nullptr, nullptr, 0, west))) return rc;
-    prof_end(c, ST_RANK_WORDS, W.n * 64 + W.blob_len);
-    // artists
+    // artists: on their own stream beside the words when both tables take the
+    // small-table sort (a chain of short latency-bound launches each)
     Ranked &A = c->ra;
     A.n = c->sum.n_artists;
-    prof_begin(c, ST_RANK_ARTISTS);
+    const bool conc = small_sort(c, W.n) && small_sort(c, A.n) && A.n;
+    hipStream_t ast = conc ? c->rank2 : c->stream;
+    if (conc) {
+        HIPC(c, hipEventRecord(c->ev_r2_fork, c->stream));
+        HIPC(c, hipStreamWaitEvent(c->rank2, c->ev_r2_fork, 0));
+    }
+    if ((rc = sort_and_blob(c, W, wbuf, wextra, nullptr, nullptr, nullptr, 0, west, c->stream))) return rc;
+    prof_end(c, ST_RANK_WORDS, W.n * 64 + W.blob_len);
+    prof_begin(c, ST_RANK_ARTISTS, ast);
     if (A.n) {
         for (int k = 0; k < 3; ++k) HIPC(c, ensure(A.K[0][k], A.n * 8));
         HIPC(c, ensure(A.V[0], A.n * 4));
@@ -1227,12 +1244,17 @@ static int do_rank(msa_ctx *c) {
                                           c->merged_a ? c->imp_a.as<u8>() : c->arena.as<u8>(),
                                           c->key_off.as<u64>(), c->key_len.as<u32>(), A.K[0][0].as<u64>(),
                                           A.K[0][1].as<u64>(), A.K[0][2].as<u64>(), A.V[0].as<u32>(), A.ref.as<u64>(),
-                                          A.cnt.as<u64>(), c->stream));
+                                          A.cnt.as<u64>(), ast));
     }
     const u8 *aarena = c->merged_a ? c->imp_a.as<u8>() : c->arena.as<u8>();
-    if ((rc = sort_and_blob(c, A, wbuf, wextra, aarena, c->key_off.as<u64>(), c->key_len.as<u32>(), 1, A.n * 32)))
+    if ((rc = sort_and_blob(c, A, wbuf, wextra, aarena, c->key_off.as<u64>(), c->key_len.as<u32>(), 1, A.n * 32,
+                            ast)))
         return rc;
-    prof_end(c, ST_RANK_ARTISTS, A.n * 64 + A.blob_len);
+    prof_end(c, ST_RANK_ARTISTS, A.n * 64 + A.blob_len, ast);
+    if (conc) {
+        HIPC(c, hipEventRecord(c->ev_r2_join, c->rank2));
+        HIPC(c, hipStreamWaitEvent(c->stream, c->ev_r2_join, 0));
+    }
     // the one read-back of the ranking: both blob lengths; a blob that did not
     // fit the capacity it was written with is grown and written again
     u64 tot[2] = {0, 0};
@@ -1252,8 +1274,8 @@ static int do_rank(msa_ctx *c) {
         const BlobArgs &b = R.pending;
         HIPC(c, msa_launch_blob(R.order.as<u32>(), R.n, R.ref.as<u64>(), R.K[0][1].as<u64>(), R.K[0][2].as<u64>(),
                                 R.cnt.as<u64>(), b.wbuf, b.wextra, c->l_pos.as<u64>(), c->l_len.as<u32>(), b.arena,
-                                b.key_off, b.key_len, R.len.as<u64>(), R.off.as<u64>(), c->scan_bsum.as<u64>(),
-                                c->scan_total.as<u64>(), R.blob.as<u8>(), R.counts.as<u64>(), R.blob_cap, c->stream,
+                                b.key_off, b.key_len, R.len.as<u64>(), R.off.as<u64>(), R.scan_bsum.as<u64>(),
+                                R.scan_total.as<u64>(), R.blob.as<u8>(), R.counts.as<u64>(), R.blob_cap, c->stream,
                                 1));
         again = true;
     }
@@ -1298,6 +1320,9 @@ int msa_create(int device, msa_ctx **out) {
     }
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->rank2, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_r2_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_r2_join, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
         hipHostMalloc((void **)&c->pin, kPinBytes, hipHostMallocDefault) != hipSuccess) {
@@ -1325,7 +1350,8 @@ void msa_destroy(msa_ctx *c) {
         for (auto &s : R->K)
             for (auto &k : s) release(k);
         for (auto &v : R->V) release(v);
-        DevBuf *rb[] = {&R->ref, &R->cnt, &R->order, &R->len, &R->off, &R->blob, &R->counts};
+        DevBuf *rb[] = {&R->ref, &R->cnt, &R->order, &R->len, &R->off, &R->blob, &R->counts, &R->scan_bsum,
+                        &R->scan_total};
         for (DevBuf *b : rb) release(*b);
     }
     for (auto &s : c->t_K)
@@ -1338,7 +1364,10 @@ void msa_destroy(msa_ctx *c) {
     (void)hipHostFree(c->pin);
     (void)hipEventDestroy(c->ev_fork);
     (void)hipEventDestroy(c->ev_join);
+    (void)hipEventDestroy(c->ev_r2_fork);
+    (void)hipEventDestroy(c->ev_r2_join);
     (void)hipStreamDestroy(c->side);
+    (void)hipStreamDestroy(c->rank2);
     (void)hipStreamDestroy(c->stream);
     delete c;
 }

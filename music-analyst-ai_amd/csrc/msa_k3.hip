@@ -37,43 +37,65 @@ namespace {
 #define Q_LIST 1024              // token entries per wave-iteration (>= 4 bytes per token)
 #define Q_MISS 32                // deferred HBM inserts per wave (16 B each)
 #define Q_WLDS (Q_LIST * 2 + Q_MISS * 16)
-// LDS word tables: S = 3..8-byte words (92 % of the tokens of lyric text) as
-// single u64 keys (12 bytes a slot, 4-slot buckets read as two ds_read_b128),
-// optionally M = 9..16-byte words as 16-byte keys (20 bytes a slot).
-// Measured on configs[2] (csv_scan + k_miss_agg): S and M listed apart with a
-// 1024-slot M table 1.95 ms, mixed 1.99, mixed without an M table (M words
-// logged for k_miss_agg, the S table takes the whole LDS) 1.82.
-// K3_MIXED: one token list (S and M words mixed in a batch); the M lanes of
-// a batch probe the M table (or, with Q_MSLOTS 0, go straight to the miss
-// logs).  Otherwise S and M words are listed apart and probed in batches of
-// their own.
-#ifndef K3_MIXED
-#define K3_MIXED 1
-#endif
-#ifndef Q_MSLOTS
-#define Q_MSLOTS 0
-#endif
-#define Q_MTAB (Q_MSLOTS * 20)
+// LDS word table: 3..8-byte words (92 % of the tokens of lyric text) as
+// single u64 keys (12 bytes a slot, 4-slot buckets read as two ds_read_b128);
+// 9..16-byte words are logged for k_miss_agg.  Measured on configs[2]
+// (csv_scan + k_miss_agg, round 2): S and M words listed apart with a 1024-slot
+// M table 1.95 ms, mixed with an M table 1.99, mixed without an M table (the S
+// table takes the whole LDS) 1.82 -- the design kept.
 #ifndef Q_SSLOTS                 // the rest of the CU's LDS
-#define Q_SSLOTS (((163840 - Q_MTAB - Q_W * (Q_LIST * 2 + Q_MISS * 16) - MSA_MLOG_PARTS * 4) / 12) & ~31)
+#define Q_SSLOTS (((163840 - Q_W * (Q_LIST * 2 + Q_MISS * 16) - MSA_MLOG_PARTS * 4) / 12) & ~31)
 #endif
 #define Q_SNB (Q_SSLOTS / 4)
-#define Q_MNB (Q_MSLOTS / 4)
-#define Q_TAB (Q_SSLOTS * 12 + Q_MTAB)
+#define Q_TAB (Q_SSLOTS * 12)
 #define Q_LDS (Q_TAB + Q_W * Q_WLDS + MSA_MLOG_PARTS * 4)
 static_assert(Q_LDS <= 163840, "K3 LDS exceeds the CU's 160 KiB");
-static_assert(Q_SSLOTS % 32 == 0 && Q_MSLOTS % 4 == 0 && Q_TAB % 16 == 0 && Q_WLDS % 16 == 0,
+static_assert(Q_SNB < 4096, "lds_find8 scales 20 hash bits by Q_SNB in 32 bits");
+static_assert(Q_SSLOTS % 32 == 0 && Q_TAB % 16 == 0 && Q_WLDS % 16 == 0,
               "LDS carve-outs stay 16-byte aligned");
 
 // Every key byte of a token is < 0x80 (alnum or '\''), so bit 63 of the
 // second key word is free: it marks a published slot (an S word has k1 == 0).
 #define KMARK 0x8000000000000000ull
 
-#ifndef K3_ROT
-#define K3_ROT 0
+// diagnostic ablations of tools/ablate.py (MSA_ABLATE bits) are compiled in
+// only with -DK3_ABLATE=1: the production kernel carries no test of them
+#ifndef K3_ABLATE
+#define K3_ABLATE 0
 #endif
 
+// Lower-cases token bytes ('0'..'9', 'A'..'Z', 'a'..'z', '\'', or zero
+// padding): of those only 'A'..'Z' have bit 6 set and bit 5 clear, so setting
+// bit 5 wherever bit 6 is set is the whole mapping
+__device__ __forceinline__ u64 lower_tok8(u64 x) { return x | ((x >> 1) & 0x2020202020202020ull); }
+
 __device__ __forceinline__ uint4 ldg16(const u8 *p) { return *reinterpret_cast<const uint4 *>(p); }
+// a wave-uniform read of data no kernel writes while this one runs: through
+// the constant address space, i.e. a scalar load (counted in lgkmcnt, so it
+// does not wait behind the wave's vector loads)
+#ifndef K3_SLOAD
+#define K3_SLOAD 1
+#endif
+#if K3_SLOAD
+template <class T>
+__device__ __forceinline__ const __attribute__((address_space(4))) T *sload(const T *p) {
+    return (const __attribute__((address_space(4))) T *)(size_t)p;
+}
+#else
+template <class T>
+__device__ __forceinline__ const T *sload(const T *p) { return p; }
+#endif
+__device__ __forceinline__ State sload_state(const State *p) {
+    const auto q = sload(p);
+    State s;
+    s.rec = q->rec;
+    s.rs = q->rs;
+    s.p = q->p;
+    s.cr = q->cr;
+    s.c = q->c;
+    s.z = q->z;
+    return s;
+}
 
 // lane l receives lane l+1's value (lane 63: 0) / lane l-1's (lane 0: 0): DPP wave shifts
 __device__ __forceinline__ u32 from_next32(u32 v) { return __builtin_amdgcn_update_dpp(0u, v, 0x130, 0xF, 0xF, false); }
@@ -193,10 +215,15 @@ __device__ __forceinline__ u64 shr128(u64 lo, u64 hi, u32 k) { return (lo >> k) 
 
 // LDS lookup of an S key (3..8 bytes, nonzero).  Returns the slot or ~0u.
 __device__ __forceinline__ u32 lds_find8(u64 *skeys, u64 k0) {
-    u32 h = (u32)k0 * 0x9E3779B1u ^ (u32)(k0 >> 32) * 0x85EBCA77u;
-    h ^= h >> 15;
-    h *= 0x2C1B3C6Du;
-    u32 b = __umulhi(h, (u32)Q_SNB);
+    // full-rate 24-bit multiplies only (v_mul_u32_u24; the 32-bit ones are
+    // quarter rate); the bucket is the top 20 bits scaled to Q_SNB (< 2^12)
+    // (HIP's __umul24 returns int: the products are taken as u32 before any shift)
+    const u32 lo = (u32)k0, hi = (u32)(k0 >> 32);
+    u32 t = lo + ((hi << 13) | (hi >> 19));
+    t ^= t >> 17;
+    u32 h = (u32)__umul24(t, 0x9E3779u);
+    h ^= h >> 13;
+    u32 b = (u32)__umul24(h >> 12, (u32)Q_SNB) >> 20;
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
         const u32 base = b * 4;
@@ -210,47 +237,6 @@ __device__ __forceinline__ u32 lds_find8(u64 *skeys, u64 k0) {
             if (old == 0 || old == k0) return base + i;
         }
         b = (b + 1 == Q_SNB) ? 0 : b + 1;
-    }
-    return ~0u;
-}
-
-// LDS lookup of a 16-byte key (k1 carries KMARK).  Returns the slot or ~0u.
-// Written branch-light: the four slot compares are plain selects; only the
-// (rare, after warm-up) claim of an empty slot takes a divergent path.
-__device__ __forceinline__ u32 lds_find16(ulonglong2 *keys, u64 k0, u64 k1) {
-    u32 h = (u32)k0 * 0x9E3779B1u + (u32)(k0 >> 32) * 0x85EBCA77u + (u32)k1 * 0xC2B2AE3Du + (u32)(k1 >> 32);
-    h ^= h >> 15;
-    h *= 0x2C1B3C6Du;
-    u32 b = __umulhi(h, (u32)Q_MNB);
-#if K3_ROT
-    // the four slot reads of a bucket start at a key-dependent slot: a
-    // ds_read_b128 lane group (16 lanes) then spreads over 16 positions of the
-    // 256-byte bank row instead of the 4 that bucket alignment alone gives
-    const u32 ro = h & 3u;
-#else
-    const u32 ro = 0;
-#endif
-#pragma unroll
-    for (int p = 0; p < 2; ++p) {
-        const u32 base = b * 4;
-        const ulonglong2 s0 = keys[base + (ro & 3u)], s1 = keys[base + ((ro + 1) & 3u)];
-        const ulonglong2 s2 = keys[base + ((ro + 2) & 3u)], s3 = keys[base + ((ro + 3) & 3u)];
-        const bool e0 = (s0.x == k0) & (s0.y == k1), e1 = (s1.x == k0) & (s1.y == k1);
-        const bool e2 = (s2.x == k0) & (s2.y == k1), e3 = (s3.x == k0) & (s3.y == k1);
-        const u32 hit = e0 ? 0u : (e1 ? 1u : (e2 ? 2u : (e3 ? 3u : 4u)));
-        if (hit < 4) return base + ((ro + hit) & 3u);
-        u32 i = s0.x == 0 ? 0u : (s1.x == 0 ? 1u : (s2.x == 0 ? 2u : (s3.x == 0 ? 3u : 4u)));
-        for (; i < 4; ++i) {
-            const u32 sl = base + ((ro + i) & 3u);
-            u64 *kp = reinterpret_cast<u64 *>(&keys[sl]);
-            const u64 old = atomicCAS((unsigned long long *)kp, 0ull, (unsigned long long)k0);
-            if (old == 0) {
-                kp[1] = k1;  // published; a prober that reads 0 moves on
-                return sl;
-            }
-            if (old == k0 && kp[1] == k1) return sl;
-        }
-        b = (b + 1 == Q_MNB) ? 0 : b + 1;
     }
     return ~0u;
 }
@@ -310,8 +296,6 @@ __global__ __launch_bounds__(Q_T, 1) void k_scan_csv(ScanArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     u64 *skeys = reinterpret_cast<u64 *>(smem);
     u32 *scnts = reinterpret_cast<u32 *>(smem + Q_SSLOTS * 8);
-    ulonglong2 *keys = reinterpret_cast<ulonglong2 *>(smem + Q_SSLOTS * 12);
-    u32 *cnts = reinterpret_cast<u32 *>(smem + Q_SSLOTS * 12 + Q_MSLOTS * 16);
     const u32 lane = lane_id();
     const u32 wib = threadIdx.x >> 6;
     unsigned char *wl = smem + Q_TAB + wib * Q_WLDS;
@@ -325,33 +309,41 @@ __global__ __launch_bounds__(Q_T, 1) void k_scan_csv(ScanArgs a) {
         skeys[i] = 0;
         scnts[i] = 0;
     }
-    for (u32 i = threadIdx.x; i < Q_MSLOTS; i += Q_T) {
-        keys[i] = make_ulonglong2(0, 0);
-        cnts[i] = 0;
-    }
     if (threadIdx.x < MSA_MLOG_PARTS) lcur[threadIdx.x] = 0;
     __syncthreads();
 
-    const u32 gw = blockIdx.x * Q_W + wib;
+    // wave-uniform chunk walk (scalar registers; the chunk-start values below
+    // come through scalar loads, which do not wait behind the vector prefetch)
+    const u32 gw = __builtin_amdgcn_readfirstlane(blockIdx.x * Q_W + wib);
     const u32 nw = gridDim.x * Q_W;
     u64 words = 0;
 
-    // a chunk's first block is loaded during the previous chunk's last block
+    // Software pipeline: the next block (the wave's next chunk's first block
+    // after a chunk's last one) and the 16 bytes after THAT block are loaded
+    // while the current block is processed.  Every iteration issues the same
+    // five loads (a dummy re-read of the current block where there is no next
+    // one), so the compiler's vmcnt for the block stays the loop-top wait: no
+    // load the current block's structure or token phase waits for was issued
+    // after the prefetch (vmcnt drains in issue order).
     uint4 cur[4];
+    uint4 tl = make_uint4(0, 0, 0, 0);  // the 16 bytes after the current block
     if (gw < a.nchunks) {
+        const u64 b0 = a.seg_begin + (u64)gw * MSA_CHUNK;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) cur[q] = ldg16(a.buf + a.seg_begin + (u64)gw * MSA_CHUNK + lane * 64 + 16 * q);
+        for (int q = 0; q < 4; ++q) cur[q] = ldg16(a.buf + b0 + lane * 64 + 16 * q);
+        tl = ldg16(a.buf + (b0 + Q_BLK < a.seg_end ? b0 + Q_BLK : b0));
     }
     for (u32 c = gw; c < a.nchunks; c += nw) {
-        State st = a.carry[c];
+        State st = sload_state(a.carry + c);
         // K1 saw no '\r' / NUL in this chunk: their masks stay empty
-        const bool rare_chunk = !a.sums || ((a.sums[c].h[0] >> 22) & 1u);
+        const bool rare_chunk = !a.sums || ((*sload(&a.sums[c].h[0]) >> 22) & 1u);
         const u64 cbase = a.seg_begin + (u64)c * MSA_CHUNK;
         const u64 cend = min(cbase + (u64)MSA_CHUNK, a.seg_end);
         u32 prevT = 0;  // the byte before the chunk is a token byte
         u32 prevQ = 0;  // ... is a '"'
         if (cbase > a.seg_begin) {
-            const u32 b = a.buf[cbase - 1];
+            const u64 pa = cbase - 1;
+            const u32 b = (*sload(reinterpret_cast<const u32 *>(a.buf + (pa & ~3ull))) >> (8 * (pa & 3))) & 0xFFu;
             prevT = (u32)(((b | 0x20u) >= 'a' && (b | 0x20u) <= 'z') || (b >= '0' && b <= '9') || b == '\'');
             prevQ = (u32)(b == '"');
         }
@@ -359,11 +351,11 @@ __global__ __launch_bounds__(Q_T, 1) void k_scan_csv(ScanArgs a) {
         for (u64 ib = cbase; ib < cend; ib += Q_BLK) {
             const u64 lpos = ib + lane * 64;
             const bool more = ib + Q_BLK < cend;
-            // the 16 bytes after this block (token continuation, "\r\n" swallow):
-            // one uniform 16-byte load, only where they exist (bytes past the
-            // segment end do not count, whatever the padding holds)
+            // the 16 bytes after this block (token continuation, "\r\n" swallow),
+            // loaded with the block; only bytes before the segment end count,
+            // whatever the padding holds
             const u64 tpos = ib + Q_BLK;
-            const uint4 tail = tpos < a.seg_end ? ldg16(a.buf + tpos) : make_uint4(0, 0, 0, 0);
+            const uint4 tail = tl;
             const u32 tvm = tpos < a.seg_end ? (a.seg_end - tpos >= 16 ? 0xFFFFu : (1u << (a.seg_end - tpos)) - 1u) : 0u;
             u32 tw[4] = {tail.x, tail.y, tail.z, tail.w};
             u32 ttok = 0;
@@ -372,15 +364,19 @@ __global__ __launch_bounds__(Q_T, 1) void k_scan_csv(ScanArgs a) {
             ttok &= tvm;
             const u64 rem = cend > lpos ? cend - lpos : 0;
             const Masks k = classify64x(cur, (u32)min(rem, (u64)64), rare_chunk);
-            // the block's bytes now live in the masks: load the next block into
-            // the same registers (in flight during the rest)
-            if (more) {
+            // the block's bytes now live in the masks: load the next block (and
+            // its tail) into the same registers, in flight during the rest
+            {
+                const u64 nbb = more ? ib + Q_BLK
+                                     : (c + nw < a.nchunks ? a.seg_begin + (u64)(c + nw) * MSA_CHUNK : ib);
 #pragma unroll
-                for (int q = 0; q < 4; ++q) cur[q] = ldg16(a.buf + lpos + Q_BLK + 16 * q);
-            } else if (c + nw < a.nchunks) {  // the wave's next chunk
-                const u64 nb = a.seg_begin + (u64)(c + nw) * MSA_CHUNK + lane * 64;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) cur[q] = ldg16(a.buf + nb + 16 * q);
+                for (int q = 0; q < 4; ++q) cur[q] = ldg16(a.buf + nbb + lane * 64 + 16 * q);
+                // the tail's address is made opaque (a VGPR the compiler cannot
+                // prove uniform): left uniform, its value is moved to scalar
+                // registers right away -- a wait on the load in this iteration
+                u64 ta = nbb + Q_BLK < a.seg_end ? nbb + Q_BLK : nbb;
+                pin64(ta);
+                tl = ldg16(a.buf + ta);
             }
 
             // ---- record structure (read_csv_record + parse_csv_line) ----
@@ -552,21 +548,15 @@ __global__ __launch_bounds__(Q_T, 1) void k_scan_csv(ScanArgs a) {
             }
 
             // 3..16-byte words.  The wave's token starts go to its LDS list
-            // (block offset | (length - 3) << 12): S words from the front, M
-            // words from the back; then the lanes take them 64 at a time, S
-            // and M batches apart (each probes its own table).  Diagnostic
-            // ablations (MSA_ABLATE; results invalid): 1 no tokens at all, 2
-            // no counting, 32 keys without the LDS tables, 4 LDS misses
-            // dropped, 128 keys not re-read from memory
-            u64 m = (a.ablate & 3) ? 0ull : (sS | sM);
-            u32 nS, nM;
-#if K3_MIXED
-            u32 liS = wave_prefix<5>((u32)__popcll(m), nS), liM = 0;
-            nM = 0;
-#else
-            u32 liS = wave_prefix<5>((u32)__popcll(sS & m), nS);
-            u32 liM = wave_prefix<5>((u32)__popcll(sM & m), nM);
-#endif
+            // (block offset | (length - 3) << 12); then the lanes take them 64
+            // at a time: 3..8-byte words probe the LDS table, 9..16-byte words
+            // go to the miss logs.  Diagnostic ablations (K3_ABLATE builds,
+            // MSA_ABLATE; results invalid): 1 no tokens at all, 2 no counting,
+            // 32 keys without the LDS table, 4 LDS misses dropped, 128 keys not
+            // re-read from memory
+            u64 m = (K3_ABLATE && (a.ablate & 3)) ? 0ull : (sS | sM);
+            u32 nS;
+            u32 li = wave_prefix<5>((u32)__popcll(m), nS);
             while (__ballot(m != 0)) {
                 if (m) {
                     const u32 b = (u32)__ffsll((long long)m) - 1;
@@ -576,77 +566,59 @@ __global__ __launch_bounds__(Q_T, 1) void k_scan_csv(ScanArgs a) {
                     const u32 d0 = (u32)w, d1 = (u32)(w >> 32), d2 = (u32)Tn;
                     const u32 run = __builtin_amdgcn_alignbit(b >= 32 ? d2 : d1, b >= 32 ? d1 : d0, b & 31u);
                     const u32 len = (u32)__ffs(~run) - 1;  // 3..16
-                    const u16 ent = (u16)((lane * 64 + b) | ((len - 3) << 12));
-                    if (K3_MIXED || len <= 8) list[liS++] = ent;
-                    else list[Q_LIST - 1 - liM++] = ent;
+                    list[li++] = (u16)((lane * 64 + b) | ((len - 3) << 12));
                 }
             }
             wsync();
             // Keys are re-read from the block (L2) as dwords from the token's
             // dword; the next 64 tokens' loads are issued before this batch is
-            // probed, so their latency hides behind the LDS work.  Batches
-            // 0 .. nbS-1 are S words, the rest M words.
-            const u32 nbS = (nS + 63) >> 6, nbM = (nM + 63) >> 6;
-            auto entry = [&](u32 bt, u32 i) -> u32 {  // list index of lane i of batch bt, or ~0u
-                if (bt < nbS) return (bt * 64 + i < nS) ? bt * 64 + i : ~0u;
-                const u32 k = (bt - nbS) * 64 + i;
-                return k < nM ? Q_LIST - 1 - k : ~0u;
-            };
+            // probed, so their latency hides behind the LDS work.
+            const u32 nb = (nS + 63) >> 6;
             u32 en = 0;
             uint4 kv = make_uint4(0, 0, 0, 0);
             u32 k4 = 0;
-            {
-                const u32 ix = nbS + nbM ? entry(0, lane) : ~0u;
-                if (ix != ~0u) {
-                    en = list[ix];
-                    const u32 *gp = reinterpret_cast<const u32 *>(a.buf + ((ib + (en & 4095u)) & ~3ull));
-                    kv = *reinterpret_cast<const uint4 *>(gp);
-                    k4 = gp[4];
-                }
+            if (lane < nS) {
+                en = list[lane];
+                const u32 *gp = reinterpret_cast<const u32 *>(a.buf + ((ib + (en & 4095u)) & ~3ull));
+                kv = *reinterpret_cast<const uint4 *>(gp);
+                k4 = gp[4];
             }
-            for (u32 bt = 0; bt < nbS + nbM; ++bt) {
+            for (u32 bt = 0; bt < nb; ++bt) {
                 bool mis = false;
                 u64 k0 = 0, k1 = KMARK;
                 const u32 e = en;
                 const uint4 v = kv;
                 const u32 v4 = k4;
-                const bool have = entry(bt, lane) != ~0u;
-                if (bt + 1 < nbS + nbM) {
-                    const u32 ix = entry(bt + 1, lane);
-                    if (ix != ~0u) {
-                        en = list[ix];
-                        const u32 *gp = reinterpret_cast<const u32 *>(a.buf + ((ib + (en & 4095u)) & ~3ull));
-                        kv = *reinterpret_cast<const uint4 *>(gp);
-                        k4 = gp[4];
-                    }
+                const bool have = bt * 64 + lane < nS;
+                if ((bt + 1) * 64 + lane < nS) {
+                    en = list[(bt + 1) * 64 + lane];
+                    const u32 *gp = reinterpret_cast<const u32 *>(a.buf + ((ib + (en & 4095u)) & ~3ull));
+                    kv = *reinterpret_cast<const uint4 *>(gp);
+                    k4 = gp[4];
                 }
                 if (have) {
                     const u32 len = (e >> 12) + 3;
                     const u32 sh = (u32)(ib + (e & 4095u)) & 3u;
-                    u64 x0, x1;
-                    if (a.ablate & 128) {  // diagnostic: keys made up from the list entry (no re-read)
+                    u64 x0 = mk64(__builtin_amdgcn_alignbyte(v.y, v.x, sh), __builtin_amdgcn_alignbyte(v.z, v.y, sh));
+                    u64 x1 = mk64(__builtin_amdgcn_alignbyte(v.w, v.z, sh), __builtin_amdgcn_alignbyte(v4, v.w, sh));
+                    if (K3_ABLATE && (a.ablate & 128)) {  // diagnostic: keys made up from the list entry (no re-read)
                         x0 = (u64)e * 0x9E3779B97F4A7C15ull & 0x7F7F7F7F7F7F7F7Full;
                         x1 = x0 >> 3;
-                    } else {
-                        x0 = mk64(__builtin_amdgcn_alignbyte(v.y, v.x, sh), __builtin_amdgcn_alignbyte(v.z, v.y, sh));
-                        x1 = mk64(__builtin_amdgcn_alignbyte(v.w, v.z, sh), __builtin_amdgcn_alignbyte(v4, v.w, sh));
                     }
-                    if (len < 8) x0 &= bits_lo(8 * len);
-                    x1 = len <= 8 ? 0ull : (x1 & bits_lo(8 * (len - 8)));
-                    k0 = lower8(x0);
-                    k1 = lower8(x1) | KMARK;
-                    if (a.ablate & 32) {
+                    // the token's bytes only (selects, no branches), lower-cased
+                    const u32 nbits = 8 * len;  // 24..128
+                    x0 &= bits_lo(nbits);
+                    x1 = nbits <= 64 ? 0ull : (x1 & bits_lo(nbits - 64));
+                    k0 = lower_tok8(x0);
+                    k1 = lower_tok8(x1) | KMARK;
+                    if (K3_ABLATE && (a.ablate & 32)) {
                         words += (k0 ^ k1) == 1;  // keep the key build alive
-                    } else if (K3_MIXED ? len <= 8 : bt < nbS) {  // separate lists: wave-uniform
+                    } else if (len <= 8) {
                         const u32 slot = lds_find8(skeys, k0);
                         if (slot != ~0u) atomicAdd(&scnts[slot], 1u);
-                        else mis = !(a.ablate & 4);
-                    } else if (Q_MSLOTS) {
-                        const u32 slot = lds_find16(keys, k0, k1);
-                        if (slot != ~0u) atomicAdd(&cnts[slot], 1u);
-                        else mis = !(a.ablate & 4);
+                        else mis = !(K3_ABLATE && (a.ablate & 4));
                     } else {
-                        mis = !(a.ablate & 4);
+                        mis = !(K3_ABLATE && (a.ablate & 4));
                     }
                 }
                 const u64 MB = __ballot(mis);
@@ -672,10 +644,10 @@ __global__ __launch_bounds__(Q_T, 1) void k_scan_csv(ScanArgs a) {
     if (lane == 0 && words) atomicAdd((unsigned long long *)&a.ctr->total_words, (unsigned long long)words);
     __syncthreads();
     // the LDS table into the logs, counts encoded (full partitions: HBM inserts)
-    for (u32 i = threadIdx.x; i < Q_SSLOTS + Q_MSLOTS && !(a.ablate & 32768); i += Q_T) {  // 32768: no flush
-        u32 n = i < Q_SSLOTS ? scnts[i] : cnts[i - Q_SSLOTS];
+    for (u32 i = threadIdx.x; i < Q_SSLOTS && !(K3_ABLATE && (a.ablate & 32768)); i += Q_T) {  // 32768: no flush
+        u32 n = scnts[i];
         if (!n) continue;
-        const ulonglong2 kk = i < Q_SSLOTS ? make_ulonglong2(skeys[i], KMARK) : keys[i - Q_SSLOTS];
+        const ulonglong2 kk = make_ulonglong2(skeys[i], KMARK);
         const u32 part = mlog_part(kk.x, kk.y);
         const u64 base = ((u64)blockIdx.x * MSA_MLOG_PARTS + part) * a.mlog_cap;
         while (n) {

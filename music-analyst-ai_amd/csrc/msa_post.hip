@@ -1701,7 +1701,9 @@ __device__ int full_cmp(u64 refa, u64 refb, u64 k1, u64 k0, const u8 *buf, const
     if (!pa) { pa = tmp; na = 0; while (na < 16 && tmp[na]) ++na; la = 0; }
     if (!pb) { pb = tmp; nb = 0; while (nb < 16 && tmp[nb]) ++nb; lb = 0; }
     const u64 m = na < nb ? na : nb;
-    for (u64 i = 0; i < m; ++i) {
+    // tied entries agree in (k1, k0) = their first 16 key bytes, zero padded;
+    // key bytes are never 0, so the first min(16, na, nb) bytes are equal
+    for (u64 i = m < 16 ? m : 16; i < m; ++i) {
         u32 x = pa[i], y = pb[i];
         if (la) x = lower1(x);
         if (lb) y = lower1(y);

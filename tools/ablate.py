@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
 """Diagnostic: time K3 (k_scan_csv) under kernel ablations (MSA_ABLATE bits,
-see msa_k3.hip), with its LDS-table miss count.  Results of ablated runs are wrong by design; only the
+see msa_k3.hip), with its LDS-table miss count.  K3's ablation bits are
+compiled in only with -DK3_ABLATE=1 (`make variant V=abl FLAGS=-DK3_ABLATE=1`,
+then MSA_LIB=.../libmsa_hip_abl.so); bit 0 (no ablation) times any build.  Results of ablated runs are wrong by design; only the
 stage times are read.  Usage: python tools/ablate.py [songs] [bits ...]"""
 import ctypes as C
 import os
