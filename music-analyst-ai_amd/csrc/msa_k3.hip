@@ -331,7 +331,12 @@ __global__ __launch_bounds__(Q_T, 1) void k_scan_csv(ScanArgs a) {
         const u64 b0 = a.seg_begin + (u64)gw * MSA_CHUNK;
 #pragma unroll
         for (int q = 0; q < 4; ++q) cur[q] = ldg16(a.buf + b0 + lane * 64 + 16 * q);
-        tl = ldg16(a.buf + (b0 + Q_BLK < a.seg_end ? b0 + Q_BLK : b0));
+        // a vector load: a uniform address here (no store before it) would
+        // become a scalar load, which drops the low address bits -- and
+        // a.buf is a view of the input at any alignment
+        u64 ta = b0 + Q_BLK < a.seg_end ? b0 + Q_BLK : b0;
+        pin64(ta);
+        tl = ldg16(a.buf + ta);
     }
     for (u32 c = gw; c < a.nchunks; c += nw) {
         State st = sload_state(a.carry + c);
@@ -342,8 +347,9 @@ __global__ __launch_bounds__(Q_T, 1) void k_scan_csv(ScanArgs a) {
         u32 prevT = 0;  // the byte before the chunk is a token byte
         u32 prevQ = 0;  // ... is a '"'
         if (cbase > a.seg_begin) {
-            const u64 pa = cbase - 1;
-            const u32 b = (*sload(reinterpret_cast<const u32 *>(a.buf + (pa & ~3ull))) >> (8 * (pa & 3))) & 0xFFu;
+            // the dword holding the byte (a.buf is a view: any alignment)
+            const size_t pa = (size_t)(a.buf + cbase - 1);
+            const u32 b = (*sload(reinterpret_cast<const u32 *>(pa & ~(size_t)3)) >> (8 * (pa & 3))) & 0xFFu;
             prevT = (u32)(((b | 0x20u) >= 'a' && (b | 0x20u) <= 'z') || (b >= '0' && b <= '9') || b == '\'');
             prevQ = (u32)(b == '"');
         }
@@ -374,6 +380,7 @@ __global__ __launch_bounds__(Q_T, 1) void k_scan_csv(ScanArgs a) {
                 // the tail's address is made opaque (a VGPR the compiler cannot
                 // prove uniform): left uniform, its value is moved to scalar
                 // registers right away -- a wait on the load in this iteration
+                // (and a scalar load would drop the low address bits)
                 u64 ta = nbb + Q_BLK < a.seg_end ? nbb + Q_BLK : nbb;
                 pin64(ta);
                 tl = ldg16(a.buf + ta);

@@ -46,6 +46,10 @@ struct msa_tr {
     void *(*alloc)(msa_tr *t, size_t bytes);
     void (*release)(msa_tr *t, void *p);
     void (*destroy)(msa_tr *t);
+    /* optional (rccl): enqueue the exchanges on this HIP stream -- the rank's
+     * libmsa_hip stream (msa_stream), so that exports, exchanges and imports
+     * are stream-ordered and released buffers are reused without a wait */
+    void (*set_stream)(msa_tr *t, void *stream);
     msa_shared *sh;
     void *impl;
 };

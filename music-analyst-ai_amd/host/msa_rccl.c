@@ -10,9 +10,13 @@
  *                gathered to rank 0 (replacing send_hash_table /
  *                receive_hash_table, parallel_spotify.c:397-432).
  * The communicator is set up with the ncclUniqueId rank 0 publishes in the
- * launcher's shared block.  Every operation runs on the transport's own HIP
- * stream and is complete when it returns (libmsa_hip reads the buffers on its
- * stream right after).
+ * launcher's shared block.  Once the rank's libmsa_hip context exists, the
+ * collectives are enqueued on the library's own stream (set_stream): the
+ * export kernels, the exchange and the import kernels are stream-ordered, so
+ * an all-to-all returns without a host wait, and transport buffers come from
+ * a pool of device buffers kept for the job (a released buffer is reused by a
+ * later exchange on the same stream: no hipMalloc / hipFree per collective).
+ * The all-gather of control data ends with a copy to the host and one wait.
  */
 #include <fcntl.h>
 #include <stdio.h>
@@ -25,11 +29,19 @@
 
 #include "msa_ranks.h"
 
+#define POOL_N 16
+typedef struct {
+    void *p;
+    size_t cap;
+    int used;
+} PoolBuf;
 typedef struct {
     ncclComm_t comm;
-    hipStream_t stream;
+    hipStream_t own;     /* until set_stream */
+    hipStream_t stream;  /* where every collective is enqueued */
     void *scratch;
     size_t scratch_bytes;
+    PoolBuf pool[POOL_N]; /* every transport buffer of the job, in use or free */
 } RcclImpl;
 
 #define NCCL_OK(x, what)                                                                          \
@@ -77,28 +89,69 @@ static int rc_alltoallv(msa_tr *t, const void *send, const uint64_t *sc, void *r
         ro += rc[p];
     }
     NCCL_OK(ncclGroupEnd(), "ncclGroupEnd");
-    HIP_OK(hipStreamSynchronize(im->stream), "sync");
+    /* on the library's stream the consumers are ordered after the exchange */
+    if (im->stream == im->own) HIP_OK(hipStreamSynchronize(im->stream), "sync");
     return 0;
 }
 
+/* Transport buffers: every device buffer the job allocated stays in the pool
+ * (in use or free); an exchange takes the smallest free one that fits, else
+ * a new one rounded up to 2 MiB so that growing exchanges reuse it.  A free
+ * buffer's last readers were enqueued on the same stream as its next writer. */
 static void *rc_alloc(msa_tr *t, size_t n) {
+    RcclImpl *im = (RcclImpl *)t->impl;
+    int best = -1, empty = -1, spare = -1;
+    for (int i = 0; i < POOL_N; ++i) {
+        PoolBuf *b = &im->pool[i];
+        if (!b->p) { if (empty < 0) empty = i; continue; }
+        if (b->used) continue;
+        if (b->cap >= n && (best < 0 || b->cap < im->pool[best].cap)) best = i;
+        if (spare < 0 || b->cap < im->pool[spare].cap) spare = i;
+    }
+    if (best >= 0) {
+        im->pool[best].used = 1;
+        return im->pool[best].p;
+    }
+    if (empty < 0) {  /* pool full: the smallest free buffer makes room */
+        if (spare < 0) {
+            fprintf(stderr, "rank %d: more than %d transport buffers in use\n", t->rank, POOL_N);
+            return NULL;
+        }
+        (void)hipStreamSynchronize(im->stream);
+        (void)hipFree(im->pool[spare].p);
+        im->pool[spare].p = NULL;
+        empty = spare;
+    }
+    const size_t cap = ((n ? n : 1) + ((size_t)2 << 20) - 1) & ~(((size_t)2 << 20) - 1);
     void *p = NULL;
-    if (hipMalloc(&p, n ? n : 1) != hipSuccess) {
-        fprintf(stderr, "rank %d: hipMalloc(%zu) failed\n", t->rank, n);
+    if (hipMalloc(&p, cap) != hipSuccess) {
+        fprintf(stderr, "rank %d: hipMalloc(%zu) failed\n", t->rank, cap);
         return NULL;
     }
+    im->pool[empty].p = p;
+    im->pool[empty].cap = cap;
+    im->pool[empty].used = 1;
     return p;
 }
 static void rc_release(msa_tr *t, void *p) {
-    (void)t;
-    if (p) (void)hipFree(p);
+    RcclImpl *im = (RcclImpl *)t->impl;
+    for (int i = 0; p && i < POOL_N; ++i)
+        if (im->pool[i].p == p) im->pool[i].used = 0;
+}
+static void rc_set_stream(msa_tr *t, void *stream) {
+    RcclImpl *im = (RcclImpl *)t->impl;
+    (void)hipStreamSynchronize(im->stream);
+    im->stream = stream ? (hipStream_t)stream : im->own;
 }
 static void rc_destroy(msa_tr *t) {
     RcclImpl *im = (RcclImpl *)t->impl;
     if (im) {
+        if (im->stream) (void)hipStreamSynchronize(im->stream);
         if (im->comm) ncclCommDestroy(im->comm);
         if (im->scratch) (void)hipFree(im->scratch);
-        if (im->stream) (void)hipStreamDestroy(im->stream);
+        for (int i = 0; i < POOL_N; ++i)
+            if (im->pool[i].p) (void)hipFree(im->pool[i].p);
+        if (im->own) (void)hipStreamDestroy(im->own);
         free(im);
     }
     free(t);
@@ -133,15 +186,17 @@ msa_tr *msa_tr_rccl(msa_shared *sh, int rank, int world, int device) {
     t->alloc = rc_alloc;
     t->release = rc_release;
     t->destroy = rc_destroy;
+    t->set_stream = rc_set_stream;
     t->sh = sh;
     t->impl = im;
     ncclUniqueId id;
     _Static_assert(sizeof(ncclUniqueId) <= 128, "ncclUniqueId fits the shared blob");
-    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&im->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&im->own, hipStreamNonBlocking) != hipSuccess) {
         fprintf(stderr, "rank %d: cannot use GPU %d\n", rank, device);
         rc_destroy(t);
         return NULL;
     }
+    im->stream = im->own;
     const int saved = stdout_to_stderr();
     msa_tr *res = t;
     if (rank == 0) {

@@ -381,6 +381,9 @@ static int rank_main(int rank, int world, msa_shared *sh, void *arg) {
     if (!part) { fprintf(stderr, "rank %d: cannot read %s\n", rank, o->dataset); return EXIT_FAILURE; }
     int rc = msa_create(device, &R->ctx);
     if (rc) { fprintf(stderr, "rank %d: libmsa_hip: cannot open GPU %d (code %d)\n", rank, device, rc); return 2; }
+    /* RCCL exchanges on the library's stream: stream-ordered with the export /
+     * import kernels around them (no host wait per exchange) */
+    if (t->set_stream) t->set_stream(t, msa_stream(R->ctx));
     TRY(msa_set_shard(R->ctx, rank == 0), "set shard");
     TRY(msa_load_csv(R->ctx, part, len), "load");
     free(part);
@@ -448,6 +451,7 @@ static int rank_main(int rank, int world, msa_shared *sh, void *arg) {
     TRY_T(t->allgather(t, &compute, sizeof compute, all_c), "all-gather of timings");
     TRY_T(t->allgather(t, &total, sizeof total, all_t), "all-gather of timings");
     if (rank == 0) write_metrics(o, world, (long long)songs, (long long)words, all_c, all_t);
+    if (t->set_stream) t->set_stream(t, NULL);  /* the library's stream ends with its context */
     msa_destroy(R->ctx);
     t->destroy(t);
     return EXIT_SUCCESS;
