@@ -276,6 +276,18 @@ int msa_wcs_load_csv(msa_wcs *w, const void *host_csv, size_t n);
  * byte other than '"', CR, LF and NUL; MSA_ERR_ARG otherwise.  Also the
  * column splitter's writer delimiter (QUOTE_MINIMAL quoting).              */
 int msa_wcs_set_delimiter(msa_wcs *w, int delimiter);
+/* The column splitter's quoting: split_csv_columns.py's --quotechar
+ * (90-95, used by detect_csv_params 48-66 for its reader and writer) and the
+ * sniffed dialect's skipinitialspace (58).  quotechar: one ASCII byte other
+ * than the delimiter, CR, LF and NUL (default '"').  msa_wcs_run (the
+ * per-song counter, whose csv.DictReader reads the default dialect) refuses
+ * anything but the default.                                                 */
+int msa_wcs_set_quoting(msa_wcs *w, int quotechar, int skipinitialspace);
+/* The scripts' --encoding (word_count_per_song.py:63-66,111;
+ * split_csv_columns.py:97-101,130): utf8_sig = 1, "utf-8-sig" (default),
+ * drops a leading BOM; 0, "utf-8", keeps it as the first field's first
+ * character (U+FEFF in the first header name).                             */
+int msa_wcs_set_encoding(msa_wcs *w, int utf8_sig);
 /* log2 of the word-table slots of the next run (0 = sized from the input;
  * the table grows by itself when it fills). */
 int msa_wcs_set_table_bits(msa_wcs *w, int bits);

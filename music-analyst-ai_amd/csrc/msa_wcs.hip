@@ -52,6 +52,11 @@ constexpr u32 T_D = PK(SF, SF, SF, IQ, SF, EC);    // ','
 constexpr u32 T_NL = PK(EC, EC, EC, IQ, EC, EC);   // '\r' or '\n'
 constexpr u32 T_O = PK(IF, IF, IF, IQ, IF, EC);    // anything else
 constexpr u32 T_EOL = PK(SR, SR, SR, IQ, SR, SR);  // end of a line
+// ' ' with skipinitialspace (the column splitter's sniffed dialect): ignored
+// at a field's start (START_FIELD tests it before the delimiter), otherwise an
+// ordinary byte; when ' ' is also the delimiter it moves as T_D but saves no
+// field at a field's start
+constexpr u32 T_SP = PK(SF, SF, IF, IQ, IF, EC);
 constexpr u32 MAP_ID = PK(0, 1, 2, 3, 4, 5);
 #undef PK
 // actions per (byte class, state), 2 bits per state: bit 0 = the byte is
@@ -61,6 +66,8 @@ constexpr u32 A_Q = PA(0, 0, 1, 0, 1, 0);
 constexpr u32 A_D = PA(2, 2, 2, 1, 2, 0);
 constexpr u32 A_NL = PA(0, 2, 2, 1, 2, 0);
 constexpr u32 A_O = PA(1, 1, 1, 1, 1, 0);
+constexpr u32 A_SP = PA(0, 0, 1, 1, 1, 0);
+constexpr u32 A_SPD = PA(0, 0, 2, 1, 2, 0);
 #undef PA
 
 constexpr u32 SEG = 256;        // bytes per lane in the map / emit passes
@@ -84,9 +91,27 @@ struct WCtr {
     u64 fallback;   // rows k_wcs_wrows left to the per-thread walk
 };
 
-__host__ __device__ __forceinline__ u32 tpk(u32 b, u32 d) {  // d: the delimiter byte
-    return b == '"' ? T_Q : (b == d ? T_D : ((b == '\r' || b == '\n') ? T_NL : T_O));
+// The reader's dialect: delimiter, quotechar (default '"'), skipinitialspace.
+// The per-song counter always reads the default dialect with its delimiter.
+struct Dia {
+    u32 delim, quote, skip;
+};
+// byte class in the precedence of _csv.c's START_FIELD: quotechar, then a
+// skipped space, then the delimiter, CR/LF, anything else
+enum : u32 { C_Q = 0, C_D = 1, C_NL = 2, C_O = 3, C_SP = 4, C_SPD = 5 };
+__host__ __device__ __forceinline__ u32 cls_of(u32 b, const Dia &d) {
+    if (b == d.quote) return C_Q;
+    if (b == ' ' && d.skip) return b == d.delim ? C_SPD : C_SP;
+    if (b == d.delim) return C_D;
+    return (b == '\r' || b == '\n') ? C_NL : C_O;
 }
+__host__ __device__ __forceinline__ u32 cls_next(u32 c) {
+    return c == C_Q ? T_Q : (c == C_D || c == C_SPD ? T_D : (c == C_NL ? T_NL : (c == C_SP ? T_SP : T_O)));
+}
+__host__ __device__ __forceinline__ u32 cls_act(u32 c) {
+    return c == C_Q ? A_Q : (c == C_D ? A_D : (c == C_NL ? A_NL : (c == C_SP ? A_SP : (c == C_SPD ? A_SPD : A_O))));
+}
+__host__ __device__ __forceinline__ u32 tpk(u32 b, const Dia &d) { return cls_next(cls_of(b, d)); }
 __host__ __device__ __forceinline__ u32 step(u32 t, u32 s) { return (t >> (3 * s)) & 7u; }
 __device__ __forceinline__ u32 map_apply(u32 t, u32 m) {  // m then t
     u32 r = 0;
@@ -178,7 +203,7 @@ __device__ __forceinline__ bool eol_after(u32 b, u32 next, u64 i, u64 n) {
 // S: the walker; S::step(t) applies a transfer table, S::eol(i) handles the
 // end of a line after byte i.
 template <typename W>
-__device__ __forceinline__ void seg_walk(const u8 *__restrict__ buf, u64 base, u64 ds, u64 n, u32 delim, W &wk) {
+__device__ __forceinline__ void seg_walk(const u8 *__restrict__ buf, u64 base, u64 ds, u64 n, Dia dia, W &wk) {
     for (u32 q = 0; q < SEG / 16; ++q) {
         const u64 b0 = base + q * 16;
         if (b0 >= n) break;
@@ -187,8 +212,8 @@ __device__ __forceinline__ void seg_walk(const u8 *__restrict__ buf, u64 base, u
         if (b0 < ds) vm &= 0xFFFFu << (u32)(ds - b0);
         if (b0 + 16 > n) vm &= (1u << (u32)(n - b0)) - 1u;
         if (!vm) continue;
-        const u32 Q = mask16(v, '"'), D = mask16(v, delim), NL = mask16(v, '\n'), CR = mask16(v, '\r');
-        const u32 S = (Q | D | NL | CR) & vm;
+        const u32 Q = mask16(v, dia.quote), D = mask16(v, dia.delim), NL = mask16(v, '\n'), CR = mask16(v, '\r');
+        const u32 S = (Q | D | NL | CR | (dia.skip ? mask16(v, ' ') : 0u)) & vm;
         const u32 O = vm & ~S;
         u32 E = S;
         const bool has_last = b0 + 16 >= n;  // the input's last byte is in this vector
@@ -201,7 +226,7 @@ __device__ __forceinline__ void seg_walk(const u8 *__restrict__ buf, u64 base, u
             const u32 upto_prev = prev < 0 ? 0u : ((2u << prev) - 1u);
             if (O & ((1u << p) - 1u) & ~upto_prev) wk.step(T_O);  // ordinary bytes in (prev, p)
             const u32 c = byte_of(v, p);
-            wk.step(tpk(c, delim));
+            wk.step(tpk(c, dia));
             const u64 i = b0 + p;
             bool eol = i + 1 == n || c == '\n';
             if (c == '\r' && !eol) eol = (p < 15 ? byte_of(v, p + 1) : (u32)buf[i + 1]) != '\n';
@@ -228,12 +253,12 @@ struct MapWalker {
 
 // Per segment: map over the 6 entering states; row ends per entering state
 // (9 bits each: at most 256 per segment).
-__global__ __launch_bounds__(256) void k_wcs_map(const u8 *__restrict__ buf, u64 ds, u64 n, u64 nseg, u32 delim,
+__global__ __launch_bounds__(256) void k_wcs_map(const u8 *__restrict__ buf, u64 ds, u64 n, u64 nseg, Dia dia,
                                                  u32 *__restrict__ map, u64 *__restrict__ cnt6) {
     const u64 seg = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (seg >= nseg) return;
     MapWalker wk{MAP_ID, 0};
-    seg_walk(buf, seg * SEG, ds, n, delim, wk);
+    seg_walk(buf, seg * SEG, ds, n, dia, wk);
     map[seg] = wk.m;
     cnt6[seg] = wk.c6;
 }
@@ -325,13 +350,13 @@ struct EmitWalker {
     }
 };
 
-__global__ __launch_bounds__(256) void k_wcs_emit(const u8 *__restrict__ buf, u64 ds, u64 n, u64 nseg, u32 delim,
+__global__ __launch_bounds__(256) void k_wcs_emit(const u8 *__restrict__ buf, u64 ds, u64 n, u64 nseg, Dia dia,
                                                   const u32 *__restrict__ sstate, const u64 *__restrict__ roff,
                                                   u64 *__restrict__ rend) {
     const u64 seg = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (seg >= nseg) return;
     EmitWalker wk{sstate[seg], roff[seg], rend};
-    seg_walk(buf, seg * SEG, ds, n, delim, wk);
+    seg_walk(buf, seg * SEG, ds, n, dia, wk);
 }
 
 // ---------------------------------------------------------------------------
@@ -1216,7 +1241,7 @@ struct ColArgs {
     const u64 *off;    // [ncols * R] (pass 1)
     u8 *out;
     WCtr *ctr;
-    u32 delim;         // field delimiter of the reader and of the writer's quoting
+    Dia dia;           // the reader's dialect; the writer quotes with its delimiter and quotechar
 };
 
 template <int PASS>
@@ -1251,7 +1276,7 @@ __global__ __launch_bounds__(256) void k_csvcol(ColArgs a) {
             const u64 k = f * a.R + j;
             dst = a.out + a.off[k];
             q = a.quoted[k] != 0;
-            if (q) put('"');
+            if (q) put(a.dia.quote);
         }
     };
     auto save = [&]() {
@@ -1262,7 +1287,7 @@ __global__ __launch_bounds__(256) void k_csvcol(ColArgs a) {
                 a.len[k] = qq ? clen + 3 : clen + 1;
                 a.quoted[k] = qq;
             } else {
-                if (q) put('"');
+                if (q) put(a.dia.quote);
                 put('\n');
                 flush();
             }
@@ -1283,7 +1308,8 @@ __global__ __launch_bounds__(256) void k_csvcol(ColArgs a) {
             u32 vm = 0xFFFFu;
             if (b0 < rs) vm &= 0xFFFFu << (u32)(rs - b0);
             if (b0 + 16 > re) vm &= (1u << (u32)(re - b0)) - 1u;
-            const u32 S = (mask16(v, '"') | mask16(v, a.delim) | mask16(v, '\n') | mask16(v, '\r')) & vm;
+            const u32 S = (mask16(v, a.dia.quote) | mask16(v, a.dia.delim) | mask16(v, '\n') | mask16(v, '\r') |
+                           (a.dia.skip ? mask16(v, ' ') : 0u)) & vm;
             const u32 O = vm & ~S;
             const u32 W[4] = {v.x, v.y, v.z, v.w};
             u32 CONT = 0;
@@ -1311,20 +1337,19 @@ __global__ __launch_bounds__(256) void k_csvcol(ColArgs a) {
                 const u64 i = b0 + p;
                 bool eol = i + 1 == a.n || b == '\n';
                 if (b == '\r' && !eol) eol = (p < 15 ? byte_of(v, p + 1) : (u32)a.buf[i + 1]) != '\n';
-                const u32 cls = b == '"' ? 0u : (b == a.delim ? 1u : ((b == '\r' || b == '\n') ? 2u : 3u));
-                const u32 tnext = cls == 0 ? T_Q : (cls == 1 ? T_D : (cls == 2 ? T_NL : T_O));
-                const u32 tact = cls == 0 ? A_Q : (cls == 1 ? A_D : (cls == 2 ? A_NL : A_O));
-                const u32 act = (tact >> (2 * s)) & 3u;
+                const u32 cls = cls_of(b, a.dia);
+                const u32 tnext = cls_next(cls);
+                const u32 act = (cls_act(cls) >> (2 * s)) & 3u;
                 if (act & 2u) save();
                 if (act & 1u) {
                     if ((b & 0xC0) != 0x80 && ++chars > FIELD_LIMIT) limit = true;
                     if (f < a.ncols) {
                         if (PASS == 0) {
-                            clen += 1 + (b == '"');  // a quote is doubled if the value is quoted
-                            special |= b == a.delim || b == '"' || b == '\n';
+                            clen += 1 + (b == a.dia.quote);  // a quotechar is doubled if the value is quoted
+                            special |= b == a.dia.delim || b == a.dia.quote || b == '\n';
                         } else {
                             put(b);
-                            if (q && b == '"') put('"');
+                            if (q && b == a.dia.quote) put(a.dia.quote);
                         }
                     }
                 }
@@ -1347,7 +1372,7 @@ __global__ __launch_bounds__(256) void k_csvcol(ColArgs a) {
         if (PASS == 0) { a.len[k] = 3; a.quoted[k] = 1; }
         else {
             u8 *d = a.out + a.off[k];
-            d[0] = '"'; d[1] = '"'; d[2] = '\n';
+            d[0] = (u8)a.dia.quote; d[1] = (u8)a.dia.quote; d[2] = '\n';
         }
     }
 }
@@ -1382,6 +1407,10 @@ struct msa_wcs {
     msa_wcs_summary sum{};
     u64 gbits = 0;  // global table size of the next run (log2), 0 = auto
     u32 delim = ',';  // field delimiter (msa_wcs_set_delimiter: the script's --delimiter or csv.Sniffer's guess)
+    u32 quote = '"';  // quotechar and skipinitialspace (msa_wcs_set_quoting): the column splitter's dialect
+    u32 skipsp = 0;
+    bool keep_bom = false;  // msa_wcs_set_encoding: "utf-8" keeps a leading BOM as data ("utf-8-sig" drops it)
+    Dia dia() const { return Dia{delim, quote, skipsp}; }
     bool have = false;
     // column splitter results
     u64 cc_ncols = 0, cc_rows = 0;
@@ -1491,9 +1520,33 @@ extern "C" int msa_wcs_load_csv(msa_wcs *w, const void *host_csv, size_t n) {
 // The field delimiter of the reader (and of the column splitter's writer):
 // one ASCII byte other than '"', '\r', '\n' and NUL.  Invalidates results.
 extern "C" int msa_wcs_set_delimiter(msa_wcs *w, int delim) {
-    if (!w || delim <= 0 || delim > 127 || delim == '"' || delim == '\r' || delim == '\n') return MSA_ERR_ARG;
+    if (!w || delim <= 0 || delim > 127 || (u32)delim == w->quote || delim == '\r' || delim == '\n') return MSA_ERR_ARG;
     if ((u32)delim != w->delim) wcs_release_results(w);
     w->delim = (u32)delim;
+    return MSA_OK;
+}
+
+// The column splitter's quoting (split_csv_columns.py --quotechar, 90-95, and
+// the sniffed skipinitialspace of detect_csv_params, 58): one ASCII byte other
+// than the delimiter, CR, LF and NUL.  The per-song counter reads the default
+// dialect only (msa_wcs_run refuses another).  Invalidates results.
+extern "C" int msa_wcs_set_quoting(msa_wcs *w, int quotechar, int skipinitialspace) {
+    if (!w || quotechar <= 0 || quotechar > 127 || (u32)quotechar == w->delim || quotechar == '\r' ||
+        quotechar == '\n')
+        return MSA_ERR_ARG;
+    if ((u32)quotechar != w->quote || (u32)(skipinitialspace != 0) != w->skipsp) wcs_release_results(w);
+    w->quote = (u32)quotechar;
+    w->skipsp = skipinitialspace != 0;
+    return MSA_OK;
+}
+
+// The scripts' --encoding: utf8_sig = 1 ("utf-8-sig", their default) drops a
+// leading BOM; 0 ("utf-8") keeps it as the first field's first character.
+// Invalidates results.
+extern "C" int msa_wcs_set_encoding(msa_wcs *w, int utf8_sig) {
+    if (!w) return MSA_ERR_ARG;
+    if ((utf8_sig == 0) != w->keep_bom) wcs_release_results(w);
+    w->keep_bom = utf8_sig == 0;
     return MSA_OK;
 }
 
@@ -1595,7 +1648,7 @@ static int wcs_split_rows(msa_wcs *w, WCtr **ctr_out, u64 *ds_out, u64 *nrows_ou
     u8 bom[3] = {0, 0, 0};
     if (n >= 3) WCHECK(hipMemcpyAsync(bom, buf, 3, hipMemcpyDeviceToHost, st));
     WCHECK(hipStreamSynchronize(st));
-    const u64 ds = (n >= 3 && bom[0] == 0xEF && bom[1] == 0xBB && bom[2] == 0xBF) ? 3 : 0;
+    const u64 ds = (!w->keep_bom && n >= 3 && bom[0] == 0xEF && bom[1] == 0xBB && bom[2] == 0xBF) ? 3 : 0;
 
     // ---- rows
     const u64 nseg = (n + SEG - 1) / SEG;
@@ -1614,7 +1667,7 @@ static int wcs_split_rows(msa_wcs *w, WCtr **ctr_out, u64 *ds_out, u64 *nrows_ou
         WCHECK(wpool(w, 7, (nseg / 1024 + 2) * 8, bsum));
         WCHECK(wpool(w, 8, 16, total));
         dfin = bmap + nb;
-        hipLaunchKernelGGL(k_wcs_map, grid1(nseg), dim3(256), 0, st, buf, ds, n, nseg, w->delim, map, cnt6);
+        hipLaunchKernelGGL(k_wcs_map, grid1(nseg), dim3(256), 0, st, buf, ds, n, nseg, w->dia(), map, cnt6);
         hipLaunchKernelGGL(k_wcs_state_block, dim3((u32)nb), dim3(BLK), 0, st, (const u32 *)map, nseg, bmap);
         hipLaunchKernelGGL(k_wcs_state_top, dim3(1), dim3(TOP_T), 0, st, bmap, nb, dfin);
         hipLaunchKernelGGL(k_wcs_state_down, dim3((u32)nb), dim3(BLK), 0, st, (const u32 *)map, (const u64 *)cnt6,
@@ -1632,7 +1685,7 @@ static int wcs_split_rows(msa_wcs *w, WCtr **ctr_out, u64 *ds_out, u64 *nrows_ou
         }
         // rend[-1] = ds: rows are [rend[r-1], rend[r]) with d_rend shifted by one
         WCHECK(hipMemcpyAsync(w->d_rend, &ds, 8, hipMemcpyHostToDevice, st));
-        hipLaunchKernelGGL(k_wcs_emit, grid1(nseg), dim3(256), 0, st, buf, ds, n, nseg, w->delim, (const u32 *)sstate,
+        hipLaunchKernelGGL(k_wcs_emit, grid1(nseg), dim3(256), 0, st, buf, ds, n, nseg, w->dia(), (const u32 *)sstate,
                            (const u64 *)roff, w->d_rend + 1);
         if (fin == IQ) WCHECK(hipMemcpyAsync(w->d_rend + nrows, &n, 8, hipMemcpyHostToDevice, st));
     }
@@ -1649,6 +1702,8 @@ static int wcs_split_rows(msa_wcs *w, WCtr **ctr_out, u64 *ds_out, u64 *nrows_ou
 
 extern "C" int msa_wcs_run(msa_wcs *w) {
     if (!w || !w->d_buf) return MSA_ERR_ARG;
+    if (w->quote != '"' || w->skipsp)  // csv.DictReader(fh, delimiter=...): the default dialect otherwise
+        return wfail(w, MSA_ERR_ARG, "the per-song counter reads quotechar '\"' without skipinitialspace");
     WCHECK(hipSetDevice(w->device));
     wcs_release_results(w);
     hipStream_t st = w->stream;
@@ -1977,17 +2032,16 @@ extern "C" int msa_wcs_write_outputs(msa_wcs *w, const char *outdir) {
 
 // ---------------------------------------------------------------------------
 // Column splitter host side.
-static void row_fields(const u8 *h, u64 len, u32 delim, std::vector<std::string> &out) {
+static void row_fields(const u8 *h, u64 len, const Dia &dia, std::vector<std::string> &out) {
     out.clear();
     std::string fld;
     u32 s = SR;
     for (u64 i = 0; i < len; ++i) {
         const u32 b = h[i];
         const bool eol = b == '\n' || (b == '\r' && (i + 1 >= len || h[i + 1] != '\n')) || i + 1 == len;
-        const u32 cls = b == '"' ? 0u : (b == delim ? 1u : ((b == '\r' || b == '\n') ? 2u : 3u));
-        const u32 tnext = cls == 0 ? T_Q : (cls == 1 ? T_D : (cls == 2 ? T_NL : T_O));
-        const u32 tact = cls == 0 ? A_Q : (cls == 1 ? A_D : (cls == 2 ? A_NL : A_O));
-        const u32 act = (tact >> (2 * s)) & 3u;
+        const u32 cls = cls_of(b, dia);
+        const u32 tnext = cls_next(cls);
+        const u32 act = (cls_act(cls) >> (2 * s)) & 3u;
         if (act & 2u) { out.push_back(fld); fld.clear(); }
         if (act & 1u) fld.push_back((char)b);
         s = step(tnext, s);
@@ -2014,7 +2068,7 @@ extern "C" int msa_csvcol_run(msa_wcs *w, int has_header, uint64_t *ncols, uint6
     WCHECK(hipMemcpy(&he, w->d_rend + 1, 8, hipMemcpyDeviceToHost));
     std::vector<u8> hb(he - ds + 1);
     if (he > ds) WCHECK(hipMemcpy(hb.data(), w->d_buf + ds, he - ds, hipMemcpyDeviceToHost));
-    row_fields(hb.data(), he - ds, w->delim, w->cc_hdr);
+    row_fields(hb.data(), he - ds, w->dia(), w->cc_hdr);
     const u64 nc = w->cc_hdr.size();
     const u64 first = has_header ? 2 : 1;  // kernel row index of the first data row
     const u64 R = nr + 1 - first;
@@ -2029,7 +2083,7 @@ extern "C" int msa_csvcol_run(msa_wcs *w, int has_header, uint64_t *ncols, uint6
     ColArgs a;
     a.buf = w->d_buf; a.n = w->n; a.rend = w->d_rend; a.first = first; a.nrows = nr + 1;
     a.ncols = nc; a.R = R; a.len = len; a.quoted = quoted; a.off = w->d_ccoff; a.out = nullptr; a.ctr = ctr;
-    a.delim = w->delim;
+    a.dia = w->dia();
     if (cells) {
         hipLaunchKernelGGL(k_csvcol<0>, grid1(R), dim3(256), 0, st, a);
         WCHECK(msa_exclusive_scan(len, cells, w->d_ccoff, bsum, total, st));

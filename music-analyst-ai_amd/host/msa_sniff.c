@@ -20,9 +20,9 @@
 
 #include "msa_unicode_word.h"
 
-long msa_sniff_sample(const unsigned char *b, size_t n, uint32_t *cps, size_t max_chars) {
+long msa_sniff_sample(const unsigned char *b, size_t n, int utf8_sig, uint32_t *cps, size_t max_chars) {
     size_t i = 0, k = 0;
-    if (n >= 3 && b[0] == 0xEF && b[1] == 0xBB && b[2] == 0xBF) i = 3;
+    if (utf8_sig && n >= 3 && b[0] == 0xEF && b[1] == 0xBB && b[2] == 0xBF) i = 3;  /* "utf-8" keeps U+FEFF */
     while (i < n && k < max_chars) {
         const uint32_t c = b[i];
         uint32_t cp, need, lo = 0x80, hi = 0xBF;

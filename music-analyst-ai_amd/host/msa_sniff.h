@@ -20,11 +20,12 @@ typedef struct {
     int skipinitialspace;
 } msa_sniff_result;
 
-/* Decode the script's sample from the raw file bytes: skip a UTF-8 BOM, take
- * up to max_chars code points.  Returns the number of code points written to
+/* Decode the script's sample from the raw file bytes: skip a UTF-8 BOM when
+ * utf8_sig ("utf-8-sig"; "utf-8" keeps it as U+FEFF), take up to max_chars
+ * code points.  Returns the number of code points written to
  * cps (capacity max_chars), or -1 when the bytes are not valid UTF-8 within
  * the sample (the script's read() raises UnicodeDecodeError). */
-long msa_sniff_sample(const unsigned char *bytes, size_t n, uint32_t *cps, size_t max_chars);
+long msa_sniff_sample(const unsigned char *bytes, size_t n, int utf8_sig, uint32_t *cps, size_t max_chars);
 
 msa_sniff_result msa_sniff(const uint32_t *s, size_t n);
 

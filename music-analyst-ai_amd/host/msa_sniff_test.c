@@ -21,7 +21,7 @@ int main(int argc, char **argv) {
         }
         fclose(f);
         uint32_t *cps = malloc(65536 * sizeof *cps);
-        const long k = msa_sniff_sample(b, n, cps, 65536);
+        const long k = msa_sniff_sample(b, n, 1, cps, 65536);
         if (k < 0) printf("decode-error\n");
         else {
             const msa_sniff_result r = msa_sniff(cps, (size_t)k);

@@ -12,7 +12,9 @@
  * csv.Sniffer on the first 65536 characters, ',' when it fails (msa_sniff.c
  * restates the stdlib's Sniffer).  The GPU reader takes any one-byte ASCII
  * delimiter but '"', CR, LF; a sniffed or given delimiter outside that set,
- * and encodings other than UTF-8, are refused.
+ * and encodings other than UTF-8, are refused.  --encoding utf-8 keeps a BOM
+ * as data (U+FEFF in the first header name, as the script's DictReader sees
+ * it); utf-8-sig, the default, drops it.
  */
 #define _POSIX_C_SOURCE 200809L
 #include <errno.h>
@@ -125,16 +127,13 @@ int main(int argc, char **argv) {
         fprintf(stderr, "cannot read %s\n", csv);
         return 1;
     }
-    if (!strcmp(enc, "utf-8") && n >= 3 && (unsigned char)data[0] == 0xEF && (unsigned char)data[1] == 0xBB &&
-        (unsigned char)data[2] == 0xBF) {
-        /* plain utf-8 would keep the BOM as U+FEFF in the first header name */
-        fprintf(stderr, "--encoding utf-8 with a BOM is not implemented on the GPU path (use utf-8-sig)\n");
-        return 2;
-    }
+    /* "utf-8" (not "utf-8-sig") keeps a BOM: U+FEFF is the sample's first
+     * character and the first header name's first character (main 111-115) */
+    const int utf8_sig = strcmp(enc, "utf-8-sig") == 0;
     uint32_t dch = delim ? (unsigned char)delim[0] : ',';
     if (!delim) {  /* detect_delimiter(fh.read(65536)) */
         uint32_t *cps = malloc(65536 * sizeof *cps);
-        const long k = msa_sniff_sample((const unsigned char *)data, n, cps, 65536);
+        const long k = msa_sniff_sample((const unsigned char *)data, n, utf8_sig, cps, 65536);
         if (k < 0) {
             fprintf(stderr, "UnicodeDecodeError: 'utf-8' codec can't decode the first 65536 characters of %s\n", csv);
             free(cps);
@@ -157,6 +156,7 @@ int main(int argc, char **argv) {
         return 1;
     }
     rc = msa_wcs_set_delimiter(w, (int)dch);
+    if (!rc) rc = msa_wcs_set_encoding(w, utf8_sig);
     if (!rc) rc = msa_wcs_load_csv(w, data, n);
     free(data);
     if (!rc) rc = msa_wcs_run(w);

@@ -44,7 +44,7 @@ EXPORTS = [
     "msa_set_shard", "msa_piece_size", "msa_shard_function", "msa_shard_head", "msa_segment_copy",
     "msa_segment_set", "msa_artist_reader_needed", "msa_set_artist_reader", "msa_export_partitions", "msa_export_ranked", "msa_export_copy", "msa_import_partitions",
     "msa_wcs_create", "msa_wcs_destroy", "msa_wcs_last_error", "msa_wcs_stream", "msa_wcs_load_csv",
-    "msa_wcs_set_table_bits", "msa_wcs_set_delimiter", "msa_wcs_run", "msa_wcs_get_summary", "msa_wcs_get_csv", "msa_wcs_write_outputs",
+    "msa_wcs_set_table_bits", "msa_wcs_set_delimiter", "msa_wcs_set_quoting", "msa_wcs_set_encoding", "msa_wcs_run", "msa_wcs_get_summary", "msa_wcs_get_csv", "msa_wcs_write_outputs",
     "msa_csvcol_run", "msa_csvcol_header", "msa_csvcol_get",
 ]
 MSA_WCS_GLOBAL = 0
@@ -162,6 +162,8 @@ def load(path: str = LIB_PATH):
     lib.msa_wcs_load_csv.argtypes = [vp, vp, sz]
     lib.msa_wcs_set_table_bits.argtypes = [vp, i]
     lib.msa_wcs_set_delimiter.argtypes = [vp, i]
+    lib.msa_wcs_set_quoting.argtypes = [vp, i, i]
+    lib.msa_wcs_set_encoding.argtypes = [vp, i]
     lib.msa_wcs_run.argtypes = [vp]
     lib.msa_wcs_get_summary.argtypes = [vp, C.POINTER(_WcsSummary)]
     lib.msa_wcs_get_csv.argtypes = [vp, i, C.POINTER(C.c_void_p), C.POINTER(sz)]
@@ -423,10 +425,23 @@ class WordCountPerSong:
         self._check(self.lib.msa_wcs_set_table_bits(self.h, bits))
 
     def set_delimiter(self, delimiter: str):
-        """The reader's field delimiter (one ASCII character, not '"', CR, LF or NUL)."""
+        """The reader's field delimiter (one ASCII character, not the quotechar, CR, LF or NUL)."""
         if len(delimiter) != 1:
             raise MsaError(-1, f"delimiter must be one character, got {delimiter!r}")
         self._check(self.lib.msa_wcs_set_delimiter(self.h, ord(delimiter)))
+
+    def set_quoting(self, quotechar: str = '"', skipinitialspace: bool = False):
+        """The column splitter's quotechar and skipinitialspace (split_csv_columns.py)."""
+        if len(quotechar) != 1:
+            raise MsaError(-1, f"quotechar must be one character, got {quotechar!r}")
+        self._check(self.lib.msa_wcs_set_quoting(self.h, ord(quotechar), 1 if skipinitialspace else 0))
+
+    def set_encoding(self, encoding: str = "utf-8-sig"):
+        """--encoding: "utf-8-sig" drops a leading BOM, "utf-8" keeps it as data."""
+        e = encoding.lower().replace("_", "-")
+        if e not in ("utf-8-sig", "utf-8", "utf8"):
+            raise MsaError(-1, f"only UTF-8 input is implemented on the GPU path, not {encoding!r}")
+        self._check(self.lib.msa_wcs_set_encoding(self.h, 1 if e == "utf-8-sig" else 0))
 
     def count(self):
         self._check(self.lib.msa_wcs_run(self.h))

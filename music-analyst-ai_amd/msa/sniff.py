@@ -33,6 +33,6 @@ def detect_csv_params(sample: str) -> Tuple[str, bool]:
         return ",", False
 
 
-def gpu_supported(delimiter: str) -> bool:
-    """What the GPU reader implements: one ASCII byte other than '"', CR, LF, NUL."""
-    return len(delimiter) == 1 and 0 < ord(delimiter) < 128 and delimiter not in '"\r\n'
+def gpu_supported(delimiter: str, quotechar: str = '"') -> bool:
+    """What the GPU reader implements: one ASCII byte other than the quotechar, CR, LF, NUL."""
+    return len(delimiter) == 1 and 0 < ord(delimiter) < 128 and delimiter not in quotechar + "\r\n"

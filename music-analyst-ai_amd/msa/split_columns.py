@@ -9,10 +9,13 @@ the script (sanitize_filename 24-28, the name loop 159-174).
            [--quotechar '"'] [--encoding utf-8-sig] [--no-header] [--force]
 
 Without --delimiter the dialect is detect_csv_params' (46-66): the stdlib's
-csv.Sniffer on the first 65536 characters (msa/sniff.py), ',' when it fails.
-The GPU reader takes any one-byte ASCII delimiter but '"', CR, LF, with
-quotechar '"'; a sniffed skipinitialspace dialect is refused (not implemented
-on the GPU path), as are other delimiters and quotechars.
+csv.Sniffer on the first 65536 characters (msa/sniff.py), ',' when it fails,
+with its skipinitialspace; --quotechar is the reader's and the writer's quote
+character either way.  --encoding utf-8-sig (default) drops a leading BOM and
+writes one at the start of every output file; utf-8 keeps it as the first
+header name's first character and writes none.  The GPU reader takes one-byte
+ASCII delimiters and quotechars other than CR, LF, NUL (and each other);
+other encodings and characters are refused.
 """
 from __future__ import annotations
 
@@ -34,10 +37,10 @@ def sanitize_filename(name: str, max_len: int = 80) -> str:
     return (s or "col")[:max_len]
 
 
-def _header_line(h: str, delimiter: str = ",") -> str:
-    """csv.writer(QUOTE_MINIMAL, lineterminator "\n").writerow([h])"""
-    if h == "" or any(c in h for c in (delimiter, '"', "\n")):
-        return '"' + h.replace('"', '""') + '"\n'
+def _header_line(h: str, delimiter: str = ",", quotechar: str = '"') -> str:
+    """csv.writer(QUOTE_MINIMAL, lineterminator "\n", the dialect's quotechar).writerow([h])"""
+    if h == "" or any(c in h for c in (delimiter, quotechar, "\n")):
+        return quotechar + h.replace(quotechar, quotechar * 2) + quotechar + "\n"
     return h + "\n"
 
 
@@ -47,19 +50,23 @@ def split_csv_columns(csv_path: str, output_dir: Optional[str] = None, delimiter
     in_path = Path(csv_path)
     if not in_path.exists():
         raise SystemExit(f"Erro: arquivo não encontrado: {in_path}")
-    if encoding.lower().replace("_", "-") not in ("utf-8-sig", "utf-8", "utf8"):
+    enc = encoding.lower().replace("_", "-")
+    if enc not in ("utf-8-sig", "utf-8", "utf8"):
         raise SystemExit("only UTF-8 input is implemented on the GPU path")
     skipinitialspace = False
     if not delimiter:  # detect_csv_params: csv.Sniffer on the script's sample
         delimiter, skipinitialspace = detect_csv_params(read_sample(str(in_path), encoding))
-    if quotechar != '"' or not gpu_supported(delimiter) or skipinitialspace:
+    quotechar = quotechar or '"'  # detect_csv_params: (quotechar or '"')
+    if not (gpu_supported(delimiter, quotechar) and gpu_supported(quotechar, delimiter)):
         raise SystemExit(f"dialect delimiter={delimiter!r} quotechar={quotechar!r} "
-                         f"skipinitialspace={skipinitialspace} is not implemented on the GPU path")
+                         f"is not implemented on the GPU path")
     base_out = Path(output_dir) if output_dir else in_path.with_suffix("").parent / f"{in_path.stem}_columns"
     base_out.mkdir(parents=True, exist_ok=True)
     data = in_path.read_bytes()
     with WordCountPerSong(device) as w:
+        w.set_quoting(quotechar, skipinitialspace)
         w.set_delimiter(delimiter)
+        w.set_encoding(encoding)
         w.load_csv(data)
         try:
             ncols, _ = w.split_columns(has_header=not no_header)
@@ -81,12 +88,12 @@ def split_csv_columns(csv_path: str, output_dir: Optional[str] = None, delimiter
                 k += 1
             seen.add(cand.lower())
             names.append(cand)
-        bom = "﻿".encode("utf-8") if encoding.lower().replace("_", "-") == "utf-8-sig" else b""
+        bom = "\ufeff".encode("utf-8") if enc == "utf-8-sig" else b""
         for i in range(ncols):
             with open(base_out / names[i], "wb") as fh:
                 fh.write(bom)
                 if not no_header:
-                    fh.write(_header_line(headers[i], delimiter).encode("utf-8"))
+                    fh.write(_header_line(headers[i], delimiter, quotechar).encode("utf-8"))
                 fh.write(w.column_body(i))
     print(f"Concluído. {ncols} arquivo(s) gerado(s) em: {base_out}")
     for name in names:

@@ -130,9 +130,14 @@ def golden_delimiter(case_dir):
     from msa.sniff import detect_delimiter, read_sample
 
     try:
-        return detect_delimiter(read_sample(os.path.join(case_dir, "input.csv")))
+        return detect_delimiter(read_sample(os.path.join(case_dir, "input.csv"), golden_encoding(args)))
     except UnicodeDecodeError:
         return ","
+
+
+def golden_encoding(args):
+    """The --encoding a golden case ran with (the scripts' default utf-8-sig)."""
+    return args[args.index("--encoding") + 1] if "--encoding" in args else "utf-8-sig"
 
 
 def golden_dialect(case_dir):
@@ -143,7 +148,7 @@ def golden_dialect(case_dir):
     from msa.sniff import detect_csv_params, read_sample
 
     try:
-        return detect_csv_params(read_sample(os.path.join(case_dir, "input.csv")))
+        return detect_csv_params(read_sample(os.path.join(case_dir, "input.csv"), golden_encoding(args)))
     except UnicodeDecodeError:
         return ",", False
 

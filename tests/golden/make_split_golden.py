@@ -46,9 +46,28 @@ def cases():
 
     for k, (text, _) in sniffed_cases().items():
         c[k] = (text, [])
-    # a sniffed skipinitialspace dialect (", " after every delimiter): the GPU
-    # path refuses it (not implemented); the golden records what the script does
+    # sniffed skipinitialspace dialects (", " after every delimiter): spaces at
+    # a field's start are dropped, a quote after them opens a quoted field
     c["sniff_skipinitialspace"] = ('a, b, c\n"x", "y", "z"\n"1", "2", "3"\n', [])
+    c["sniff_skip_quoted_delims"] = ('h1, h2, h3\n1, "a, b", c\n2,   "x\ny", "q""q"\n3, , " lead"\n', [])
+    c["sniff_skip_semicolon"] = ('name; value; note\nab; "c; d"; e\n  f;g ;  "h"\n', [])
+    rows = ["artist, song, text"]
+    for i in range(60):
+        rows.append('A%d, S%d, "w%d, x %s"' % (i % 7, i, i, "y" * (i % 5)))
+    c["sniff_skip_lyrics"] = ("\n".join(rows) + "\n", [])
+    # --quotechar: the reader's and the writer's quote character
+    q1 = ("artist,song,text\n'Art, ist',S1,'line one\nline \"two\"'\n"
+          "B,'S''2',plain \"dq\" text\nC,it's,'a,b'\n'',x,'y'\n")
+    c["quotechar_single"] = (q1, ["--delimiter", ",", "--quotechar", "'"])
+    c["quotechar_single_sniffed"] = (q1.replace(",", ";"), ["--quotechar", "'"])
+    c["quotechar_pipe"] = ("a,b\n|x,y|,|p||q|\n|multi\nline|,z\n", ["--delimiter", ",", "--quotechar", "|"])
+    c["quotechar_dq_literal"] = ('a,b\n"x",y "z"\n', ["--delimiter", ",", "--quotechar", "'"])
+    # --encoding utf-8: a BOM is the first header's first character (output
+    # files without a BOM); utf-8-sig drops it and writes one per file
+    bom = "\ufeff"
+    c["utf8_bom"] = (bom + "artist,song\nA,\"x,y\"\n", ["--delimiter", ",", "--encoding", "utf-8"])
+    c["utf8_no_bom"] = ("artist,song\nA,\"x,y\"\n", ["--delimiter", ",", "--encoding", "utf-8"])
+    c["utf8_bom_sniffed"] = (bom + "a;b;c\n1;2;3\n4;\"5;6\";7\n", ["--encoding", "utf-8"])
     return c
 
 

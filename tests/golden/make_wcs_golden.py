@@ -120,6 +120,17 @@ def main():
     cases.update(sniffed_cases())
     for s in range(6):
         cases[f"torture_{s}"] = (torture(100 + s, 150), ["--delimiter", ","])
+    # --encoding utf-8: a BOM is not stripped -- it becomes the first header
+    # name's first character (the required "artist" column is then missing
+    # when it is the first column) and is part of the Sniffer's sample
+    bom = "\ufeff"
+    cases["utf8_bom_artist_first"] = (bom + HDR + 'A,S,/l,"hello there world"\n', ["--encoding", "utf-8"])
+    cases["utf8_bom_id_first"] = (bom + "id,artist,song,text\n1,A,S,\"hello there world\"\n2,B,T,\"more words here\"\n",
+                                  ["--encoding", "utf-8"])
+    cases["utf8_bom_sniffed"] = (bom + "id;artist;song;text\n1;A;S;\"hello; there world\"\n2;B;T;more words here\n",
+                                 ["--encoding", "utf-8"])
+    cases["utf8_no_bom"] = (HDR + 'A,S,/l,"hello there, world"\nB,T,/m,words words words\n', ["--encoding", "utf-8"])
+    cases["utf8_sig_explicit"] = (bom + HDR + 'A,S,/l,"hello there, world"\n', ["--encoding", "utf-8-sig"])
     cases["zipf_300"] = (zipf(300, 3), [])
     cases["zipf_crlf_200"] = (zipf(200, 7, crlf=True), [])
     if os.path.isdir(OUT):

@@ -11,8 +11,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(HERE, "..", "oracle"))
 sys.path.insert(0, os.path.join(HERE, "golden"))
 import split_oracle  # noqa: E402
-from conftest import golden_dialect  # noqa: E402
-from test_split_oracle import CASES, GOLD, load_case  # noqa: E402
+from test_split_oracle import CASES, GOLD, case_dialect, load_case  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
@@ -25,14 +24,16 @@ def test_split_golden(msa_mod, name, tmp_path):
     inp = tmp_path / "in.csv"
     inp.write_bytes(data)
     od = tmp_path / "cols"
-    # the script's own invocation: --delimiter as recorded, else the host sniffs
+    # the script's own invocation: --delimiter as recorded, else the host
+    # sniffs (delimiter + skipinitialspace); --quotechar and --encoding as recorded
     delim = args[args.index("--delimiter") + 1] if "--delimiter" in args else None
-    _, skip = golden_dialect(os.path.join(GOLD, name))
-    if exp is None or skip:  # skipinitialspace dialects are refused (not implemented on the GPU path)
+    _, quote, _, enc = case_dialect(name, args)
+    kw = dict(quotechar=quote, encoding=enc, no_header="--no-header" in args)
+    if exp is None:
         with pytest.raises((SystemExit, msa_mod.MsaError)):
-            split_csv_columns(str(inp), str(od), delim, no_header="--no-header" in args)
+            split_csv_columns(str(inp), str(od), delim, **kw)
         return
-    split_csv_columns(str(inp), str(od), delim, no_header="--no-header" in args)
+    split_csv_columns(str(inp), str(od), delim, **kw)
     got = {p.name: p.read_bytes() for p in od.iterdir()}
     assert got == exp
 
@@ -92,3 +93,53 @@ def test_split_cli(msa_mod, tmp_path):
     assert r.returncode == 0, r.stderr
     assert "Concluído. 4 arquivo(s) gerado(s) em:".encode() in r.stdout
     assert {p.name: p.read_bytes() for p in od.iterdir()} == exp
+
+
+def dialect_corpus(seed: int, rows: int, delim: str, quote: str, space_after: bool) -> bytes:
+    """Random rows of a dialect: fields holding the delimiter, the quotechar,
+    '"', CR/LF, spaces and UTF-8 letters, quoted (quotechar doubled) when they
+    need it or at random; with space_after, ' ' after delimiters (sometimes
+    before a quoted field) -- skipinitialspace input."""
+    import random
+
+    rnd = random.Random(seed)
+    alpha = ["a", "b", "Zé", " ", delim, quote, '"', "\n", "\r\n", "x y", "ü"]
+    out = []
+    for _ in range(rows):
+        fields = []
+        for _ in range(rnd.randint(1, 5)):
+            v = "".join(rnd.choice(alpha) for _ in range(rnd.randint(0, 6)))
+            if any(c in v for c in (delim, quote, "\n", "\r")) or rnd.random() < 0.3:
+                v = quote + v.replace(quote, quote * 2) + quote
+            elif v.startswith(" ") and space_after:
+                v = v.lstrip(" ")  # would be skipped: not an interesting difference
+            fields.append(v)
+        sep = delim + (" " * rnd.randint(0, 2) if space_after else "")
+        out.append(sep.join(fields))
+    return ("\n".join(out) + "\n").encode("utf-8")
+
+
+@pytest.mark.parametrize("delim,quote,skip", [(",", "'", False), (";", "|", False), (",", '"', True), (",", "'", True),
+                                              ("\t", "'", True), (" ", '"', True)])
+def test_split_dialects_vs_oracle(msa_mod, delim, quote, skip):
+    """--quotechar and skipinitialspace dialects (split_csv_columns.py:58,
+    90-95): the GPU reader and writer against the oracle on random rows."""
+    for seed in range(3):
+        data = dialect_corpus(300 + seed, 400, delim, quote, skip)
+        first, bodies = split_oracle.split_columns(data, True, delim, quote, skip)
+        with msa_mod.WordCountPerSong(0) as w:
+            w.set_quoting(quote, skip)
+            w.set_delimiter(delim)
+            w.load_csv(data)
+            nc, _ = w.split_columns(True)
+            assert [w.column_header(i) for i in range(nc)] == first
+            assert [w.column_body(i) for i in range(nc)] == bodies
+
+
+def test_per_song_counter_refuses_other_quoting(msa_mod):
+    """csv.DictReader(fh, delimiter=...) (word_count_per_song.py:115) reads the
+    default dialect: msa_wcs_run refuses a quotechar / skipinitialspace."""
+    with msa_mod.WordCountPerSong(0) as w:
+        w.set_quoting("'", False)
+        with pytest.raises(msa_mod.MsaError):
+            w.run(b"artist,song,text\nA,S,hello world\n")

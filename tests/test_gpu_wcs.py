@@ -22,7 +22,7 @@ sys.path.insert(0, os.path.join(HERE, "..", "oracle"))
 sys.path.insert(0, os.path.join(HERE, "golden"))
 import wcs_oracle  # noqa: E402
 from conftest import golden_delimiter  # noqa: E402
-from test_wcs_oracle import CASES, GOLD, load_case  # noqa: E402
+from test_wcs_oracle import CASES, GOLD, case_encoding, load_case  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
@@ -38,6 +38,7 @@ def wcs(msa_mod):
 def test_wcs_golden(msa_mod, wcs, name):
     data, exp = load_case(name)
     wcs.set_delimiter(golden_delimiter(os.path.join(GOLD, name)))
+    wcs.set_encoding(case_encoding(name))
     try:
         if exp is None:
             with pytest.raises(msa_mod.MsaError):
@@ -46,6 +47,7 @@ def test_wcs_golden(msa_mod, wcs, name):
         assert wcs.run(data) == exp
     finally:
         wcs.set_delimiter(",")
+        wcs.set_encoding("utf-8-sig")
 
 
 def _torture(seed, n):
@@ -155,11 +157,13 @@ def test_wcs_full_size_properties(msa_mod, wcs):
 
 
 @pytest.mark.parametrize("name", [c for c in CASES if c in ("basic", "crlf_cr_blank", "zipf_300", "err_missing_col",
-                                                          "err_short_row", "torture_2") or c.startswith("sniff_")])
+                                                          "err_short_row", "torture_2") or c.startswith("sniff_")
+                                  or c.startswith("utf8")])
 def test_wcs_cli_golden(msa_mod, name, tmp_path):
     """bin/word_count_per_song writes the script's two files and prints its row
     count -- invoked like the golden run: with its --delimiter, or without one
-    (the CLI's own csv.Sniffer restatement then picks it, as the script did)."""
+    (the CLI's own csv.Sniffer restatement then picks it, as the script did),
+    and its --encoding (utf-8 keeps a BOM in the first header name)."""
     cli = os.path.join(msa_mod.PKG_DIR, "bin", "word_count_per_song")
     data, exp = load_case(name)
     args = open(os.path.join(GOLD, name, "args.txt")).read().split()

@@ -33,20 +33,27 @@ def test_cases_present():
     assert len(CASES) >= 20
 
 
+def case_dialect(name, args):
+    """(delimiter, quotechar, skipinitialspace, encoding) the script ran a golden case with."""
+    delim, skip = golden_dialect(os.path.join(GOLD, name))
+    quote = args[args.index("--quotechar") + 1] if "--quotechar" in args else '"'
+    enc = args[args.index("--encoding") + 1] if "--encoding" in args else "utf-8-sig"
+    return delim, quote, skip, enc
+
+
 @pytest.mark.parametrize("name", CASES)
 def test_split_oracle_matches_reference(name):
     from msa.split_columns import _header_line, sanitize_filename  # host naming logic (no GPU)
 
     data, args, exp = load_case(name)
     no_header = "--no-header" in args
-    delim, skip = golden_dialect(os.path.join(GOLD, name))
-    if skip:
-        pytest.skip("skipinitialspace dialect: not restated (the GPU path refuses it, tests/test_gpu_split.py)")
+    delim, quote, skip, enc = case_dialect(name, args)
+    strip = enc != "utf-8"
     if exp is None:
         with pytest.raises((ValueError, split_oracle.WcsError)):
-            split_oracle.split_columns(data, not no_header, delim)
+            split_oracle.split_columns(data, not no_header, delim, quote, skip, strip)
         return
-    first, bodies = split_oracle.split_columns(data, not no_header, delim)
+    first, bodies = split_oracle.split_columns(data, not no_header, delim, quote, skip, strip)
     assert len(bodies) == len(exp)
     # file contents in column order, matched to the reference's file names
     names = []
@@ -60,6 +67,6 @@ def test_split_oracle_matches_reference(name):
         seen.add(cand.lower())
         names.append(cand)
         want = exp[cand]
-        hdr = b"" if no_header else _header_line(h, delim).encode()
-        assert want == BOM + hdr + bodies[i - 1], cand
+        hdr = b"" if no_header else _header_line(h, delim, quote).encode()
+        assert want == (BOM if strip else b"") + hdr + bodies[i - 1], cand
     assert sorted(names) == sorted(exp)

@@ -23,15 +23,22 @@ def load_case(name):
     return rd("input.csv"), exp
 
 
+def case_encoding(name):
+    from conftest import golden_encoding
+
+    return golden_encoding(open(os.path.join(GOLD, name, "args.txt")).read().split())
+
+
 @pytest.mark.parametrize("name", CASES)
 def test_oracle_matches_reference(name):
     data, exp = load_case(name)
     d = golden_delimiter(os.path.join(GOLD, name))
+    enc = case_encoding(name)
     if exp is None:
         with pytest.raises(wcs_oracle.WcsError):
-            wcs_oracle.word_count_per_song(data, d)
+            wcs_oracle.word_count_per_song(data, d, enc)
         return
-    assert wcs_oracle.word_count_per_song(data, d) == exp
+    assert wcs_oracle.word_count_per_song(data, d, enc) == exp
 
 
 def test_oracle_refuses_bad_bytes():
