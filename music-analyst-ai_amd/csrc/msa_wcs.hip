@@ -1407,6 +1407,8 @@ struct msa_wcs {
     msa_wcs_summary sum{};
     u64 gbits = 0;  // global table size of the next run (log2), 0 = auto
     u32 delim = ',';  // field delimiter (msa_wcs_set_delimiter: the script's --delimiter or csv.Sniffer's guess)
+    hipEvent_t ev_a = nullptr, ev_b = nullptr;  // k_wcs_wrows of the last run (msa_wcs_kernel_ms)
+    float wrows_ms = 0;
     u32 quote = '"';  // quotechar and skipinitialspace (msa_wcs_set_quoting): the column splitter's dialect
     u32 skipsp = 0;
     bool keep_bom = false;  // msa_wcs_set_encoding: "utf-8" keeps a leading BOM as data ("utf-8-sig" drops it)
@@ -1479,13 +1481,18 @@ extern "C" int msa_wcs_create(int device, msa_wcs **out) {
     w->device = device;
     if (hipDeviceGetAttribute(&w->cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || w->cus < 1)
         w->cus = 1;
-    if (hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&w->ev_a) != hipSuccess || hipEventCreate(&w->ev_b) != hipSuccess) {
         delete w;
         return MSA_ERR_HIP;
     }
     *out = w;
     return MSA_OK;
 }
+
+// Not part of include/msa_hip.h: the last run's k_wcs_wrows time (HIP events
+// on the context's stream), for tools/bench_wcs.py's roofline.
+extern "C" double msa_wcs_kernel_ms(msa_wcs *w) { return w ? (double)w->wrows_ms : 0.0; }
 
 extern "C" void msa_wcs_destroy(msa_wcs *w) {
     if (!w) return;
@@ -1494,6 +1501,8 @@ extern "C" void msa_wcs_destroy(msa_wcs *w) {
     for (auto &p : w->scr) wfree(p);
     wfree((void *&)w->d_buf);
     wfree((void *&)w->d_rend);
+    if (w->ev_a) (void)hipEventDestroy(w->ev_a);
+    if (w->ev_b) (void)hipEventDestroy(w->ev_b);
     (void)hipStreamDestroy(w->stream);
     delete w;
 }
@@ -1767,10 +1776,13 @@ extern "C" int msa_wcs_run(msa_wcs *w) {
             // happens a few hundred times, not once per 256 rows
             const u64 per = (u64)WR_W * WR_ROWS, blocks = (R - 2 + per - 1) / per;
             const u64 g = (u64)w->cus * WR_GPC;
+            WCHECK(hipEventRecord(w->ev_a, st));
             hipLaunchKernelGGL(k_wcs_wrows, dim3((u32)(blocks < g ? blocks : g)), dim3(WR_W * 64), 0, st, a);
             WCHECK(hipGetLastError());
+            WCHECK(hipEventRecord(w->ev_b, st));
             WCHECK(hipMemcpyAsync(&hc, ctr, sizeof hc, hipMemcpyDeviceToHost, st));
             WCHECK(hipStreamSynchronize(st));
+            WCHECK(hipEventElapsedTime(&w->wrows_ms, w->ev_a, w->ev_b));
             if (getenv("MSA_WCS_DEBUG")) fprintf(stderr, "k_wcs_wrows: %llu of %llu rows left to k_wcs_rows\n",
                                                  (unsigned long long)hc.fallback, (unsigned long long)(R - 2));
             w->fallback_rows = hc.fallback;

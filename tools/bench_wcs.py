@@ -9,6 +9,13 @@ tokenise + count, ranking, by-song lines; results left in HBM) -- it syncs
 with the host between phases, so wall-clock around it is the step time.
 cpu_baseline: oracle/wcs_oracle.py (pure-Python restatement of the script,
 kind "port", 1 core) on a bounded sample of the same corpus.
+
+roofline: the dominant kernel k_wcs_wrows (wave per window of whole rows),
+timed with HIP events on the library's stream (msa_wcs_kernel_ms); its
+algorithmic bytes per launch = every input byte read once + 48 B per row
+(row end 8 B read; distinct-word count 8 B and artist/song spans 32 B
+written) + 8 B per (song, word) line written (n_pairs); `traffic` from the
+PMC file of tools/pmc_rowf.sh when it is stamped with this build, else null.
 """
 import argparse
 import json
@@ -34,6 +41,12 @@ def main():
         return bench_split(a)
     data = msa.gen_corpus(a.songs, mode="zipf", seed=1)
     n = len(data)
+    lib = msa.load()
+    import ctypes as C
+
+    lib.msa_wcs_kernel_ms.argtypes = [C.c_void_p]
+    lib.msa_wcs_kernel_ms.restype = C.c_double
+    kms = []
     with msa.WordCountPerSong(0) as w:
         w.load_csv(data)
         for _ in range(a.warmup):
@@ -41,14 +54,31 @@ def main():
         t0 = time.perf_counter()
         for _ in range(a.steps):
             w.count()
+            kms.append(lib.msa_wcs_kernel_ms(w.h))
         dt = (time.perf_counter() - t0) / a.steps
         s = w.summary()
+    k_ms = sum(kms) / len(kms)
+    alg = n + 48 * s["total_rows"] + 8 * s["n_pairs"]
+    achieved = alg / (k_ms * 1e-3) / 1e9
+    roof = {"kernel": "k_wcs_wrows", "bound": "hbm", "achieved": round(achieved, 1), "peak": 8000.0, "unit": "GB/s",
+            "frac": round(achieved / 8000.0, 4), "traffic": None, "avg_launch_ms": round(k_ms, 4),
+            "alg_bytes_per_launch": alg}
+    pmc = os.path.join(REPO, "profiles", "pmc_wcs_main.json")
+    if os.path.exists(pmc):
+        p = json.load(open(pmc))
+        k = p.get("kernels", {}).get("k_wcs_wrows")
+        if p.get("build_id") == msa.build_id() and p.get("input_bytes") == n and k:
+            roof["traffic"] = k["hbm_bytes_per_launch"]
+            roof["traffic_over_alg"] = round(k["hbm_bytes_per_launch"] / alg, 3)
+        else:
+            roof["counters"] = {"note": "PMC file not taken on this build / corpus"}
     out = {
         "metric": "CSV->per-song word counts GB/s (word_count_per_song.py path)",
         "value": round(n / dt / 1e9, 3), "unit": "GB/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,
         "ms_per_step": round(dt * 1e3, 3), "higher_is_better": True, "dtype": "u8",
         "data": "synthetic (csrc/msa_gen.c Zipfian lyric CSV, seed 1)",
-        "config": {"workload": f"{a.songs} songs, {n} bytes, resident in HBM", "summary": s},
+        "config": {"workload": f"{a.songs} songs, {n} bytes, resident in HBM", "bytes_per_gpu": n, "summary": s},
+        "roofline": roof,
     }
     if not a.no_cpu_baseline:
         sys.path.insert(0, os.path.join(REPO, "oracle"))

@@ -24,7 +24,9 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "music-analyst-ai_amd"))
 KERNELS = ["k_scan_csv", "k_miss_agg", "k_chunk_summary", "k_rec_spans", "k_rec_fast", "k_rec_fix", "k_col_gather", "k_col_lines",
-           "k_artist_count", "k_tile_sort", "k_merge_pass"]
+           "k_artist_count", "k_tile_sort", "k_merge_pass",
+           # the per-song counter (tools/pmc_wcs.sh, --wcs)
+           "k_wcs_wrows", "k_wcs_rows", "k_wcs_map", "k_wcs_emit", "k_wcs_validate", "k_wcs_pairs"]
 PASSES = ["fetch", "write", "sq", "atomic"]
 
 
@@ -35,6 +37,7 @@ def build_id():
 
 
 def short(name):
+    name = name.replace("(anonymous namespace)::", "")
     for k in KERNELS:
         if name.startswith(k + "(") or name.startswith(k + "<") or name == k:
             return k
@@ -67,7 +70,9 @@ def bench_line(log):
 
 
 def main():
-    out = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
+    args = [x for x in sys.argv[1:] if not x.startswith("--")]
+    wcs = "--wcs" in sys.argv  # passes over tools/bench_wcs.py: the roofline kernel is k_wcs_wrows
+    out = args[0] if args else "gpurun_out/pmc"
     per = collect(out)
     kernels = {}
     for k, c in per.items():
@@ -78,16 +83,19 @@ def main():
             e["write_bytes_per_launch"] = int(c["WRITE_SIZE"] * 1024)
         kernels[k] = e
     b = bench_line(os.path.join(out, "fetch.log"))
+    rk = "k_wcs_wrows" if wcs else "k_scan_csv"
     res = {
         "build_id": build_id(),
         "input_bytes": b["config"]["bytes_per_gpu"] if b else None,
-        "roofline_kernel": "k_scan_csv",
+        "roofline_kernel": rk,
         "alg_bytes_per_launch": b["roofline"]["alg_bytes_per_launch"] if b else None,
         "correction": "hbm = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE halves 16B/lane streams)",
-        "command": "tools/pmc.sh: rocprofv3 --pmc <group> -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline",
+        "command": ("tools/pmc_wcs.sh: rocprofv3 --pmc <group> -- python3 tools/bench_wcs.py --steps 1 --warmup 1 "
+                    "--no-cpu-baseline" if wcs else
+                    "tools/pmc.sh: rocprofv3 --pmc <group> -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline"),
         "kernels": kernels,
     }
-    k3 = kernels.get("k_scan_csv", {})
+    k3 = kernels.get(rk, {})
     if res["alg_bytes_per_launch"] and k3.get("hbm_bytes_per_launch"):
         res["traffic_over_alg"] = round(k3["hbm_bytes_per_launch"] / res["alg_bytes_per_launch"], 3)
     with open(os.path.join(out, "pmc.json"), "w") as f:
