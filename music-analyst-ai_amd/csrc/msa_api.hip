@@ -213,6 +213,11 @@ struct msa_ctx {
     // the library stream by the first entry point that needs it
     bool text_deferred = false;
     std::string text_hdr;
+    // artist.csv likewise waits until the artist pass of msa_count is
+    // enqueued (that pass reads k_rec_fast's keys, not the column), so that
+    // text.csv starts earlier; entry points that read acol launch it first
+    bool artist_deferred = false;
+    std::string artist_hdr;
     // pinned read-back area: the counters, states and header bytes a run reads
     // back are copied here asynchronously and waited for with one sync
     // (pageable destinations made every copy a round trip of its own)
@@ -280,9 +285,23 @@ static hipError_t start_text_side(msa_ctx *c) {
     if (e == hipSuccess) c->side_pending = true;
     return e;
 }
-// Everything the library owes on its stream: a text.csv pass not launched
-// yet runs there, one on the side stream is waited for (enqueued, no host wait).
+// The deferred artist.csv pass on the library stream.
+static hipError_t launch_artist_col(msa_ctx *c) {
+    if (!c->artist_deferred) return hipSuccess;
+    c->artist_deferred = false;
+    prof_begin(c, ST_ARTIST_COLUMN);
+    if (materialise_column(c, false, c->artist_hdr, c->acol, c->alen, c->aoff, c->asrc, c->apairs, c->stream))
+        return hipErrorUnknown;
+    prof_end(c, ST_ARTIST_COLUMN, c->nrec * 16 * 2);  // ~16-byte artist lines read + written
+    return hipGetLastError();
+}
+// Everything the library owes on its stream: column passes not launched yet
+// run there, one on the side stream is waited for (enqueued, no host wait).
 static hipError_t join_side(msa_ctx *c) {
+    if (c->artist_deferred) {
+        const hipError_t e = launch_artist_col(c);
+        if (e != hipSuccess) return e;
+    }
     if (c->text_deferred) {
         const hipError_t e = launch_text(c, c->stream);
         if (e != hipSuccess) return e;
@@ -669,11 +688,9 @@ static int launch_spans(msa_ctx *c, bool want_text) {
 }
 
 static int split_columns_rest(msa_ctx *c, bool want_text, const std::string &ah, const std::string &th) {
-    int rc;
-    prof_begin(c, ST_ARTIST_COLUMN);
     HIPC(c, ensure(c->acol, ah.size() + c->n + 1 + MSA_INPUT_PAD));
-    if ((rc = materialise_column(c, false, ah, c->acol, c->alen, c->aoff, c->asrc, c->apairs, c->stream))) return rc;
-    prof_end(c, ST_ARTIST_COLUMN, c->nrec * 16 * 2);  // ~16-byte artist lines read + written
+    c->artist_hdr = ah;  // deferred (see msa_ctx::artist_deferred)
+    c->artist_deferred = true;
     // compute_header_length (parallel_spotify.c:444-459): getline's end
     c->a_hdr_getline = ah.empty() ? 0 : ah.find('\n') + 1;
     c->a_hdr_len = ah.size();
@@ -710,7 +727,7 @@ static int check_split_overflow(msa_ctx *c, bool read_back = true) {
 
 static int split_once(msa_ctx *c, int flags) {
     int rc;
-    c->text_deferred = false;  // superseded by this split
+    c->text_deferred = c->artist_deferred = false;  // superseded by this split
     HIPC(c, join_side(c));     // a text column pass in flight reads buffers this one rewrites
     if (!c->in) return fail(c, MSA_ERR_ARG, "no input bound (msa_load_csv / msa_bind_csv)");
     if (c->n == 0 && !c->cont) return fail(c, MSA_ERR_NOHEADER, "Dataset does not contain a header row");
@@ -963,6 +980,7 @@ static int do_count(msa_ctx *c) {
                 launch_long_words(c, nl);
                 long_ran = true;
                 HIPC(c, start_text_side(c));  // text.csv beside this read-back and the ranking
+                HIPC(c, launch_artist_col(c));  // artist.csv beside text.csv
             }
             if ((rc = sync_counters(c))) return rc;
             long_ok = attempt == 0;
@@ -980,6 +998,7 @@ static int do_count(msa_ctx *c) {
         }
     }
     if (exact) {
+        HIPC(c, launch_artist_col(c));  // read below; the arena it copies keys from is rewritten below
         if ((rc = resolve_col_lens(c))) return rc;
         // the artist pass over artist.csv records from its getline header end (or
         // the segment msa_segment_set chose for a shard)
@@ -1336,6 +1355,7 @@ int msa_create(int device, msa_ctx **out) {
 void msa_destroy(msa_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
+    c->text_deferred = c->artist_deferred = false;  // nothing reads them any more
     (void)join_side(c);
     (void)hipStreamSynchronize(c->stream);
     DevBuf *all[] = {&c->in_own, &c->sums, &c->carry, &c->btot, &c->bstate, &c->small, &c->rec_start, &c->extra, &c->exp_buf, &c->exp_meta, &c->imp_w, &c->imp_a, &c->imp_meta,
