@@ -19,7 +19,7 @@
 // ---- launchers (msa_scan.hip / msa_post.hip)
 hipError_t msa_launch_summary(const u8 *, u64, u64, u32, ChunkSum *, hipStream_t);
 u32 msa_fn_blocks(u32 nchunks);
-hipError_t msa_launch_fn(const ChunkSum *, u64, u32, Fn *, State *, Fn *, const State *, State *, State *, hipStream_t);
+hipError_t msa_launch_fn(const ChunkSum *, u64, u32, Fn *, State *, Fn *, State, State *, State *, hipStream_t);
 hipError_t msa_launch_scan(const ScanArgs &, int, hipStream_t);
 hipError_t msa_launch_scan_csv(const ScanArgs &, hipStream_t);
 hipError_t msa_launch_miss_agg(const ScanArgs &, hipStream_t);
@@ -62,12 +62,21 @@ hipError_t msa_launch_tie_apply(const u32 *, const u32 *, const u64 *, u64, u32 
 hipError_t msa_launch_sort(u64 *const[3], u64 *const[3], u64 *const[3], u32 *const[3], u64, int *, hipStream_t);
 hipError_t msa_launch_fixup(const u64 *, const u64 *, const u64 *, const u32 *, u64, const u64 *, const u8 *,
                             const u8 *, const u64 *, const u32 *, const u8 *, const u64 *, const u32 *, u32 *, hipStream_t);
+u64 msa_rank_small_max();
+hipError_t msa_launch_rank_small(u64 *const[3], u64 *const[3], u64 *const[3], u32 *const[3], u64, const u64 *,
+                                 const u8 *, const u8 *, const u64 *, const u32 *, const u8 *, const u64 *,
+                                 const u32 *, u32 *, u64 *, u64 *, u64 *, hipStream_t);
 hipError_t msa_launch_blob(const u32 *, u64, const u64 *, const u64 *, const u64 *, const u64 *, const u8 *,
                            const u8 *, const u64 *, const u32 *, const u8 *, const u64 *, const u32 *, u64 *, u64 *, u64 *, u64 *,
                            u8 *, u64 *, u64, hipStream_t, int);
 
 // ---------------------------------------------------------------------------
 namespace {
+
+// Room before a text column's body for its header line (a label of at most
+// 127 bytes + '\n', msa_summary's text_label): the body can be written
+// before the header is known.
+static const u64 kColHdrRoom = 256;
 
 struct DevBuf {
     void *p = nullptr;
@@ -207,15 +216,23 @@ struct msa_ctx {
     // (both small-table sorts are launch/latency-bound chains)
     hipStream_t rank2 = nullptr;
     hipEvent_t ev_r2_fork = nullptr, ev_r2_join = nullptr;
+    // K3's word-miss aggregation runs on rank2 beside the record spans
+    hipEvent_t ev_ma_fork = nullptr, ev_ma_join = nullptr;
+    // the K2 final-state read-back (launch_scan_fn / wait_scan_fn)
+    hipEvent_t ev_fin = nullptr;
+    State fin_init{};
+    bool fin_pending = false;
+    // text.csv is written on the side stream from the moment its record
+    // spans exist (right after the split's scans): beside the split's
+    // read-back, the artist pass and the ranking; every entry point that
+    // could touch its buffers joins it first (join_side)
     bool side_pending = false;
-    // text.csv is launched after the counting (it shares the CUs badly with
-    // the per-CU artist tables): on the side stream during the ranking, or on
-    // the library stream by the first entry point that needs it
-    bool text_deferred = false;
-    std::string text_hdr;
-    // artist.csv likewise waits until the artist pass of msa_count is
-    // enqueued (that pass reads k_rec_fast's keys, not the column), so that
-    // text.csv starts earlier; entry points that read acol launch it first
+    // the text column's body starts at kColHdrRoom, its header line right
+    // before it (written once the header is read back): tcol + tcol_off
+    u64 tcol_off = 0;
+    // artist.csv waits until the artist pass of msa_count is enqueued (that
+    // pass reads k_rec_fast's keys, not the column); entry points that read
+    // acol launch it first
     bool artist_deferred = false;
     std::string artist_hdr;
     // pinned read-back area: the counters, states and header bytes a run reads
@@ -263,47 +280,26 @@ static hipError_t fork_side(msa_ctx *c) {
     if (e == hipSuccess) e = hipStreamWaitEvent(c->side, c->ev_fork, 0);
     return e;
 }
-static int materialise_column(msa_ctx *c, bool text, const std::string &hdr_line, DevBuf &col, DevBuf &lenb,
-                              DevBuf &offb, DevBuf &srcb, DevBuf &pairsb, hipStream_t st);
-// The deferred text.csv pass on stream st.
-static hipError_t launch_text(msa_ctx *c, hipStream_t st) {
-    c->text_deferred = false;
-    prof_begin(c, ST_TEXT_COLUMN, st);
-    if (materialise_column(c, true, c->text_hdr, c->tcol, c->tlen, c->toff, c->tsrc, c->tpairs, st))
-        return hipErrorUnknown;
-    prof_end(c, ST_TEXT_COLUMN, c->n * 2 + c->nrec * 40, st);  // ~ the text column read + written
-    return hipGetLastError();
-}
-// The deferred text.csv pass on the side stream, after what is enqueued on
-// the library stream so far (its artist-table kernels need whole CUs' LDS:
-// the pass starts behind them).
-static hipError_t start_text_side(msa_ctx *c) {
-    if (!c->text_deferred) return hipSuccess;
-    hipError_t e = fork_side(c);
-    if (e == hipSuccess) e = launch_text(c, c->side);
-    if (e == hipSuccess) e = hipEventRecord(c->ev_join, c->side);
-    if (e == hipSuccess) c->side_pending = true;
-    return e;
-}
+static int materialise_column(msa_ctx *c, bool text, u64 hdr, DevBuf &col, DevBuf &lenb, DevBuf &offb,
+                              DevBuf &srcb, DevBuf &pairsb, hipStream_t st);
+static int put_bytes(msa_ctx *c, u8 *dst, const std::string &b, hipStream_t st);
+static int start_text_side(msa_ctx *c);
 // The deferred artist.csv pass on the library stream.
 static hipError_t launch_artist_col(msa_ctx *c) {
     if (!c->artist_deferred) return hipSuccess;
     c->artist_deferred = false;
     prof_begin(c, ST_ARTIST_COLUMN);
-    if (materialise_column(c, false, c->artist_hdr, c->acol, c->alen, c->aoff, c->asrc, c->apairs, c->stream))
+    if (put_bytes(c, c->acol.as<u8>(), c->artist_hdr, c->stream) ||
+        materialise_column(c, false, c->artist_hdr.size(), c->acol, c->alen, c->aoff, c->asrc, c->apairs, c->stream))
         return hipErrorUnknown;
     prof_end(c, ST_ARTIST_COLUMN, c->nrec * 16 * 2);  // ~16-byte artist lines read + written
     return hipGetLastError();
 }
-// Everything the library owes on its stream: column passes not launched yet
-// run there, one on the side stream is waited for (enqueued, no host wait).
+// Everything the library owes on its stream: a column pass not launched yet
+// runs there, one on the side stream is waited for (enqueued, no host wait).
 static hipError_t join_side(msa_ctx *c) {
     if (c->artist_deferred) {
         const hipError_t e = launch_artist_col(c);
-        if (e != hipSuccess) return e;
-    }
-    if (c->text_deferred) {
-        const hipError_t e = launch_text(c, c->stream);
         if (e != hipSuccess) return e;
     }
     if (!c->side_pending) return hipSuccess;
@@ -414,31 +410,45 @@ static void h_sanitize(const std::string &in, char *out) {
 static const u64 kPinSmall = 512, kPinHead = 4096, kPinBytes = 1024 + kPinHead;
 static_assert(sizeof(Counters) <= 512 && sizeof(State) <= 512, "pinned read-back layout");
 
-static int run_scan_fn(msa_ctx *c, const u8 *buf, u64 b, u64 e, State init, State *fin, int stage_id) {
+// launch_scan_fn enqueues K1 + K2 and the read-back of the final state;
+// wait_scan_fn waits for that read-back alone (work enqueued in between, such
+// as a speculative K3, keeps running).
+static int launch_scan_fn(msa_ctx *c, const u8 *buf, u64 b, u64 e, State init, int stage_id) {
     const u64 len = e > b ? e - b : 0;
     const u32 nch = (u32)((len + MSA_CHUNK - 1) / MSA_CHUNK);
+    c->fin_init = init;
+    c->fin_pending = nch != 0;
+    if (!nch) return MSA_OK;
     HIPC(c, ensure(c->sums, sizeof(ChunkSum) * (size_t)(nch + 1)));
     HIPC(c, ensure(c->carry, sizeof(State) * (size_t)(nch + 1)));
     HIPC(c, ensure(c->btot, sizeof(Fn) * (size_t)(msa_fn_blocks(nch) + 1)));
     HIPC(c, ensure(c->bstate, sizeof(State) * (size_t)(msa_fn_blocks(nch) + 1)));
     HIPC(c, ensure(c->small, 4096));
     Fn *total = c->small.as<Fn>();
-    State *d_init = reinterpret_cast<State *>(c->small.as<char>() + 1024);
-    State *d_fin = d_init + 1;
-    HIPC(c, hipMemcpyAsync(d_init, &init, sizeof(State), hipMemcpyHostToDevice, c->stream));
-    if (nch) {
-        prof_begin(c, stage_id);
-        HIPC(c, msa_launch_summary(buf, b, e, nch, c->sums.as<ChunkSum>(), c->stream));
-        HIPC(c, msa_launch_fn(c->sums.as<ChunkSum>(), b, nch, c->btot.as<Fn>(), c->bstate.as<State>(), total, d_init,
-                              c->carry.as<State>(), d_fin, c->stream));
-        prof_end(c, stage_id, len);
-        HIPC(c, hipMemcpyAsync(c->pin + kPinSmall, d_fin, sizeof(State), hipMemcpyDeviceToHost, c->stream));
-        HIPC(c, hipStreamSynchronize(c->stream));
-        memcpy(fin, c->pin + kPinSmall, sizeof(State));
-    } else {
-        *fin = init;
-    }
+    State *d_fin = reinterpret_cast<State *>(c->small.as<char>() + 1024);
+    prof_begin(c, stage_id);
+    HIPC(c, msa_launch_summary(buf, b, e, nch, c->sums.as<ChunkSum>(), c->stream));
+    HIPC(c, msa_launch_fn(c->sums.as<ChunkSum>(), b, nch, c->btot.as<Fn>(), c->bstate.as<State>(), total, init,
+                          c->carry.as<State>(), d_fin, c->stream));
+    prof_end(c, stage_id, len);
+    HIPC(c, hipMemcpyAsync(c->pin + kPinSmall, d_fin, sizeof(State), hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipEventRecord(c->ev_fin, c->stream));
     return MSA_OK;
+}
+static int wait_scan_fn(msa_ctx *c, State *fin) {
+    if (!c->fin_pending) {
+        *fin = c->fin_init;
+        return MSA_OK;
+    }
+    c->fin_pending = false;
+    HIPC(c, hipEventSynchronize(c->ev_fin));
+    memcpy(fin, c->pin + kPinSmall, sizeof(State));
+    return MSA_OK;
+}
+static int run_scan_fn(msa_ctx *c, const u8 *buf, u64 b, u64 e, State init, State *fin, int stage_id) {
+    int rc;
+    if ((rc = launch_scan_fn(c, buf, b, e, init, stage_id))) return rc;
+    return wait_scan_fn(c, fin);
 }
 
 static u32 log2_ceil(u64 v) {
@@ -525,26 +535,6 @@ __global__ void k_clear_slots(u64 *tab, const u32 *list, u64 n, u32 words_per_sl
     for (u32 k = 0; k < words_per_slot; ++k) s[k] = 0;
 }
 
-static int clear_tables(msa_ctx *c) {
-    struct {
-        DevBuf *tab, *list;
-        u64 *used;
-        u32 w;
-    } t[4] = {{&c->s_tab, &c->s_list, &c->s_used_prev, 2},
-              {&c->m_tab, &c->m_list, &c->m_used_prev, 4},
-              {&c->l_tab, &c->l_list, &c->lt_used_prev, 4},
-              {&c->a_tab, &c->a_list, &c->a_used_prev, 4}};
-    for (auto &x : t) {
-        if (*x.used && x.tab->p) {
-            hipLaunchKernelGGL(k_clear_slots, dim3((u32)((*x.used + 255) / 256)), dim3(256), 0, c->stream,
-                               x.tab->as<u64>(), x.list->as<u32>(), *x.used, x.w);
-            HIPC(c, hipGetLastError());
-        }
-        *x.used = 0;
-    }
-    return MSA_OK;
-}
-
 // Every read-back of the run counters also settles the column lengths the
 // split left on the device.
 static void take_col_lens(msa_ctx *c) {
@@ -625,17 +615,52 @@ static int scan_columns(msa_ctx *c, bool text) {
     return MSA_OK;
 }
 
-static int materialise_column(msa_ctx *c, bool text, const std::string &hdr_line, DevBuf &col, DevBuf &lenb,
-                              DevBuf &offb, DevBuf &srcb, DevBuf &pairsb, hipStream_t st) {
+// A column's body at col + hdr (its header line is written by put_bytes).
+static int materialise_column(msa_ctx *c, bool text, u64 hdr, DevBuf &col, DevBuf &lenb, DevBuf &offb,
+                              DevBuf &srcb, DevBuf &pairsb, hipStream_t st) {
     const u64 nrec = c->nrec;
     u64 *body_p = &c->ctr.as<Counters>()->col_body[text ? 1 : 0];  // from scan_columns
-    HIPC(c, hipMemcpyAsync(col.p, hdr_line.data(), hdr_line.size(), hipMemcpyHostToDevice, st));
     // the artist column reads lines equal to their keys from the arena k_rec_fast filled
     const bool keys = !text && c->spans;
     HIPC(c, msa_launch_col_write(text ? 1 : 0, c->in, lenb.as<u64>(), offb.as<u64>(), srcb.as<u64>(), pairsb.as<u32>(),
-                                 nrec, hdr_line.size(), body_p, col.as<u8>(), keys ? c->arena.as<u8>() : nullptr,
+                                 nrec, hdr, body_p, col.as<u8>(), keys ? c->arena.as<u8>() : nullptr,
                                  c->key_off.as<u64>(), c->key_len.as<u32>(), st));
     return MSA_OK;
+}
+
+// Small host values written by a kernel (a pageable hipMemcpyAsync source
+// makes the call wait for the stream to drain up to the copy).
+struct Bytes256 {
+    unsigned char b[256];
+};
+__global__ void k_put_bytes(u8 *dst, Bytes256 v, u32 n) {
+    if (threadIdx.x < n) dst[threadIdx.x] = v.b[threadIdx.x];
+}
+// text.csv's body on the side stream, after what is enqueued on the library
+// stream so far (the record spans and their offset scans)
+static int start_text_side(msa_ctx *c) {
+    int rc;
+    HIPC(c, fork_side(c));
+    prof_begin(c, ST_TEXT_COLUMN, c->side);
+    if ((rc = materialise_column(c, true, kColHdrRoom, c->tcol, c->tlen, c->toff, c->tsrc, c->tpairs, c->side)))
+        return rc;
+    prof_end(c, ST_TEXT_COLUMN, c->n * 2 + c->nrec * 40, c->side);  // ~ the text column read + written
+    HIPC(c, hipEventRecord(c->ev_join, c->side));
+    c->side_pending = true;
+    return MSA_OK;
+}
+static int put_bytes(msa_ctx *c, u8 *dst, const std::string &b, hipStream_t st) {
+    if (b.empty()) return MSA_OK;
+    if (b.size() > sizeof(Bytes256)) return fail(c, MSA_ERR_ARG, "header line longer than %zu bytes", sizeof(Bytes256));
+    Bytes256 v;
+    memcpy(v.b, b.data(), b.size());
+    hipLaunchKernelGGL(k_put_bytes, dim3(1), dim3(256), 0, st, dst, v, (u32)b.size());
+    HIPC(c, hipGetLastError());
+    return MSA_OK;
+}
+__global__ void k_put_u64(u64 *p0, u64 v0, u64 *p1, u64 v1) {
+    if (threadIdx.x == 0 && p0) *p0 = v0;
+    if (threadIdx.x == 1 && p1) *p1 = v1;
 }
 
 // The main scan inserts into the HBM word tables without appending to their
@@ -699,10 +724,12 @@ static int split_columns_rest(msa_ctx *c, bool want_text, const std::string &ah,
     c->col_hdr[1] = th.size();
     c->col_lens_pending = true;  // acol_len / tcol_len / a_end: from the next counter read-back
     c->have_tcol = false;
-    if (want_text) {  // deferred (see msa_ctx::text_deferred)
-        HIPC(c, ensure(c->tcol, th.size() + c->n + 1 + MSA_INPUT_PAD));
-        c->text_hdr = th;
-        c->text_deferred = true;
+    if (want_text) {  // the body is on its way (start_text_side): the header line goes right before it
+        if (th.size() > kColHdrRoom) return fail(c, MSA_ERR_ARG, "text header line longer than %llu bytes",
+                                                 (unsigned long long)kColHdrRoom);
+        c->tcol_off = kColHdrRoom - th.size();
+        int rc;
+        if ((rc = put_bytes(c, c->tcol.as<u8>() + c->tcol_off, th, c->stream))) return rc;
         c->have_tcol = true;
     }
     c->stage = 1;
@@ -725,10 +752,80 @@ static int check_split_overflow(msa_ctx *c, bool read_back = true) {
     return MSA_OK;
 }
 
+// Before the split's K1, in one launch: the claimed slots of the four tables
+// cleared, the run counters zeroed, nulrel[0, nul_n) zeroed, rec_start[0] = 0
+// (four clear launches, a memset and two copies before: ~60 us of launch gaps).
+struct ClearJob {
+    u64 *tab;
+    const u32 *list;
+    u64 n;
+    u32 w, blocks;
+};
+struct Prologue {
+    ClearJob job[4];
+    u64 *ctr;
+    u32 ctr_words, fill_blocks;
+    u32 *nul;
+    u64 nul_n;
+    u64 *rs0;
+};
+#define PRO_T 256
+__global__ __launch_bounds__(PRO_T) void k_prologue(Prologue p) {
+    u32 b = blockIdx.x;
+    const u32 t = threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        if (b < p.job[j].blocks) {
+            const u64 i = (u64)b * PRO_T + t;
+            if (i < p.job[j].n) {
+                u64 *s = p.job[j].tab + (u64)p.job[j].list[i] * p.job[j].w;
+                for (u32 k = 0; k < p.job[j].w; ++k) s[k] = 0;
+            }
+            return;
+        }
+        b -= p.job[j].blocks;
+    }
+    if (b == 0) {
+        if (t < p.ctr_words) p.ctr[t] = 0;
+        if (t == 0 && p.rs0) *p.rs0 = 0;
+        for (u64 i = (p.nul_n & ~3ull) + t; i < p.nul_n; i += PRO_T) p.nul[i] = 0;
+    }
+    uint4 *q = reinterpret_cast<uint4 *>(p.nul);
+    for (u64 i = (u64)b * PRO_T + t; i < p.nul_n / 4; i += (u64)p.fill_blocks * PRO_T) q[i] = make_uint4(0, 0, 0, 0);
+}
+static int split_prologue(msa_ctx *c, u64 nul_n, bool rs0) {
+    Prologue p{};
+    struct {
+        DevBuf *tab, *list;
+        u64 *used;
+        u32 w;
+    } t[4] = {{&c->s_tab, &c->s_list, &c->s_used_prev, 2},
+              {&c->m_tab, &c->m_list, &c->m_used_prev, 4},
+              {&c->l_tab, &c->l_list, &c->lt_used_prev, 4},
+              {&c->a_tab, &c->a_list, &c->a_used_prev, 4}};
+    u32 blocks = 0;
+    for (int j = 0; j < 4; ++j) {
+        const u64 n = t[j].tab->p ? *t[j].used : 0;
+        p.job[j] = ClearJob{t[j].tab->as<u64>(), t[j].list->as<u32>(), n, t[j].w, (u32)((n + PRO_T - 1) / PRO_T)};
+        blocks += p.job[j].blocks;
+        *t[j].used = 0;
+    }
+    static_assert(sizeof(Counters) % 8 == 0 && sizeof(Counters) / 8 <= PRO_T, "k_prologue zeroes Counters in one block");
+    p.ctr = c->ctr.as<u64>();
+    p.ctr_words = sizeof(Counters) / 8;
+    p.nul = c->nulrel.as<u32>();
+    p.nul_n = nul_n;
+    p.rs0 = rs0 ? c->rec_start.as<u64>() : nullptr;
+    p.fill_blocks = (u32)std::min<u64>(1024, std::max<u64>(1, (nul_n / 4 + PRO_T - 1) / PRO_T));
+    hipLaunchKernelGGL(k_prologue, dim3(blocks + p.fill_blocks), dim3(PRO_T), 0, c->stream, p);
+    HIPC(c, hipGetLastError());
+    return MSA_OK;
+}
+
 static int split_once(msa_ctx *c, int flags) {
     int rc;
-    c->text_deferred = c->artist_deferred = false;  // superseded by this split
-    HIPC(c, join_side(c));     // a text column pass in flight reads buffers this one rewrites
+    c->artist_deferred = false;  // superseded by this split
+    HIPC(c, join_side(c));       // a text column pass in flight reads buffers this one rewrites
     if (!c->in) return fail(c, MSA_ERR_ARG, "no input bound (msa_load_csv / msa_bind_csv)");
     if (c->n == 0 && !c->cont) return fail(c, MSA_ERR_NOHEADER, "Dataset does not contain a header row");
     const bool want_text = (flags & MSA_SPLIT_TEXT_COLUMN) != 0;
@@ -737,82 +834,108 @@ static int split_once(msa_ctx *c, int flags) {
     c->col_lens_pending = false;
     c->extra_len = 0;
     HIPC(c, ensure(c->ctr, sizeof(Counters)));
-    if ((rc = clear_tables(c))) return rc;
-    HIPC(c, hipMemsetAsync(c->ctr.p, 0, sizeof(Counters), c->stream));
-
+    // K3 is launched right behind K2 on the record arrays an earlier split
+    // sized (cap0 records), and checked against K2's record count when the
+    // host reads it back -- K3 runs meanwhile.  Too small (the first split, or
+    // a larger input): the arrays grow and K3 runs again.
+    const u64 cap0 = c->rec_cap;
+    if ((rc = split_prologue(c, want_text ? cap0 : 0, cap0 != 0))) return rc;
     State init{0, 0, 0, 0, 0, 0}, fin;
-    if ((rc = run_scan_fn(c, c->in, 0, c->n, init, &fin, ST_CSV_SUMMARY))) return rc;
+    if ((rc = launch_scan_fn(c, c->in, 0, c->n, init, ST_CSV_SUMMARY))) return rc;
+
+    ScanArgs a{};
+    auto launch_k3 = [&](u64 cap) -> int {
+        if ((rc = ensure_tables(c))) return rc;
+        a = ScanArgs{};
+        a.buf = c->in;
+        a.seg_begin = 0;
+        a.seg_end = c->n;
+        a.nchunks = (u32)((c->n + MSA_CHUNK - 1) / MSA_CHUNK);
+        a.carry = c->carry.as<State>();
+        a.sums = c->sums.as<ChunkSum>();  // from launch_scan_fn over the same [0, n)
+        a.rec_start = c->rec_start.as<u64>();
+        a.nulrel = c->nulrel.as<u32>();
+        a.rec_cap = cap;
+        a.f0 = c->f0.as<u64>();
+        a.tss = c->tss.as<u64>();
+        a.tse = c->tse.as<u64>();
+        c->spans = !(c->ablate & 64);  // the round-1 kernel records no spans
+        a.s_tab = c->s_tab.as<u64>();
+        a.s_mask = c->s_slots - 1;
+        a.s_list = c->s_list.as<u32>();
+        a.s_list_cap = c->s_slots / 2;
+        a.m_tab = c->m_tab.as<u64>();
+        a.m_mask = c->m_slots - 1;
+        a.m_list = c->m_list.as<u32>();
+        a.m_list_cap = c->m_slots / 2;
+        a.l_pos = c->l_pos.as<u64>();
+        a.l_cap = c->l_occ_cap;
+        a.ctr = c->ctr.as<Counters>();
+        a.want_nul = want_text ? 1 : 0;
+        a.ablate = c->ablate;
+        a.first_rec = c->cont ? 0 : 1;
+        {  // miss logs: room for about a quarter of the tokens (a full partition falls back to HBM inserts)
+            const u64 parts = (u64)c->cus * MSA_MLOG_PARTS;
+            const u64 entries = std::max<u64>(parts * 1024, c->n / 16);
+            a.mlog_cap = (u32)std::min<u64>(entries / parts, 1u << 30);
+            HIPC(c, ensure(c->mlog, parts * a.mlog_cap * 16));
+            HIPC(c, ensure(c->mlog_n, parts * 4));
+            a.mlog = c->mlog.as<ulonglong2>();
+            a.mlog_n = c->mlog_n.as<u32>();
+        }
+        prof_begin(c, ST_CSV_SCAN);
+        // k_scan_csv (msa_k3.hip); MSA_ABLATE bit 64 selects the round-1 kernel (A/B runs)
+        if (c->ablate & 64) HIPC(c, msa_launch_scan(a, 0, c->stream));
+        else HIPC(c, msa_launch_scan_csv(a, c->stream));
+        // algorithmic bytes: every CSV byte once + the per-record SoA it writes
+        // (rec_start 8, nulrel 4 with the text column, the span events f0 / tss / tse 24)
+        prof_end(c, ST_CSV_SCAN, c->n + c->nrec * ((want_text ? 12ull : 8ull) + (c->spans ? 24ull : 0ull)));
+        return MSA_OK;
+    };
+    if (cap0 && (rc = launch_k3(cap0))) return rc;
+    if ((rc = wait_scan_fn(c, &fin))) return rc;
     const u64 nterm = fin.rec;
     c->nrec = nterm + (fin.rs < c->n ? 1 : 0);
     const u64 cap = nterm + 2;
-    HIPC(c, ensure(c->rec_start, cap * 8));
-    HIPC(c, ensure(c->nulrel, cap * 4));
-    HIPC(c, ensure(c->f0, cap * 8));
-    HIPC(c, ensure(c->tss, cap * 8));
-    HIPC(c, ensure(c->tse, cap * 8));
-    c->rec_cap = cap;
-    if (want_text) HIPC(c, hipMemsetAsync(c->nulrel.p, 0, cap * 4, c->stream));
-    u64 zero = 0;
-    HIPC(c, hipMemcpyAsync(c->rec_start.p, &zero, 8, hipMemcpyHostToDevice, c->stream));
-    if ((rc = ensure_tables(c))) return rc;
-
-    ScanArgs a{};
-    a.buf = c->in;
-    a.seg_begin = 0;
-    a.seg_end = c->n;
-    a.nchunks = (u32)((c->n + MSA_CHUNK - 1) / MSA_CHUNK);
-    a.carry = c->carry.as<State>();
-    a.sums = c->sums.as<ChunkSum>();  // from run_scan_fn over the same [0, n)
-    a.rec_start = c->rec_start.as<u64>();
-    a.nulrel = c->nulrel.as<u32>();
-    a.rec_cap = cap;
-    a.f0 = c->f0.as<u64>();
-    a.tss = c->tss.as<u64>();
-    a.tse = c->tse.as<u64>();
-    c->spans = !(c->ablate & 64);  // the round-1 kernel records no spans
-    a.s_tab = c->s_tab.as<u64>();
-    a.s_mask = c->s_slots - 1;
-    a.s_list = c->s_list.as<u32>();
-    a.s_list_cap = c->s_slots / 2;
-    a.m_tab = c->m_tab.as<u64>();
-    a.m_mask = c->m_slots - 1;
-    a.m_list = c->m_list.as<u32>();
-    a.m_list_cap = c->m_slots / 2;
-    a.l_pos = c->l_pos.as<u64>();
-    a.l_cap = c->l_occ_cap;
-    a.ctr = c->ctr.as<Counters>();
-    a.want_nul = want_text ? 1 : 0;
-    a.ablate = c->ablate;
-    a.first_rec = c->cont ? 0 : 1;
-    {  // miss logs: room for about a quarter of the tokens (a full partition falls back to HBM inserts)
-        const u64 parts = (u64)c->cus * MSA_MLOG_PARTS;
-        const u64 entries = std::max<u64>(parts * 1024, c->n / 16);
-        a.mlog_cap = (u32)std::min<u64>(entries / parts, 1u << 30);
-        HIPC(c, ensure(c->mlog, parts * a.mlog_cap * 16));
-        HIPC(c, ensure(c->mlog_n, parts * 4));
-        a.mlog = c->mlog.as<ulonglong2>();
-        a.mlog_n = c->mlog_n.as<u32>();
+    if (cap > cap0) {
+        if (cap0) {  // K3 ran out of record room: its counts are undone, it runs again
+            HIPC(c, hipStreamSynchronize(c->stream));
+            if ((rc = wipe_tables(c))) return rc;
+            HIPC(c, hipMemsetAsync(c->ctr.p, 0, sizeof(Counters), c->stream));
+        }
+        HIPC(c, ensure(c->rec_start, cap * 8));
+        HIPC(c, ensure(c->nulrel, cap * 4));
+        HIPC(c, ensure(c->f0, cap * 8));
+        HIPC(c, ensure(c->tss, cap * 8));
+        HIPC(c, ensure(c->tse, cap * 8));
+        c->rec_cap = cap;
+        if (want_text) HIPC(c, hipMemsetAsync(c->nulrel.p, 0, cap * 4, c->stream));
+        HIPC(c, hipMemsetAsync(c->rec_start.p, 0, 8, c->stream));
+        if ((rc = launch_k3(cap))) return rc;
     }
-    prof_begin(c, ST_CSV_SCAN);
-    // k_scan_csv (msa_k3.hip); MSA_ABLATE bit 64 selects the round-1 kernel (A/B runs)
-    if (c->ablate & 64) HIPC(c, msa_launch_scan(a, 0, c->stream));
-    else HIPC(c, msa_launch_scan_csv(a, c->stream));
-    // algorithmic bytes: every CSV byte once + the per-record SoA it writes
-    // (rec_start 8, nulrel 4 with the text column, the span events f0 / tss / tse 24)
-    prof_end(c, ST_CSV_SCAN, c->n + c->nrec * ((want_text ? 12ull : 8ull) + (c->spans ? 24ull : 0ull)));
+    // the word-miss aggregation beside the record spans (rank2 is idle until
+    // do_rank); the library stream waits for it before the word lists
     if (!(c->ablate & 64)) {
-        prof_begin(c, ST_MISS_AGG);
-        HIPC(c, msa_launch_miss_agg(a, c->stream));
-        prof_end(c, ST_MISS_AGG, 0);
+        HIPC(c, hipEventRecord(c->ev_ma_fork, c->stream));
+        HIPC(c, hipStreamWaitEvent(c->rank2, c->ev_ma_fork, 0));
+        prof_begin(c, ST_MISS_AGG, c->rank2);
+        HIPC(c, msa_launch_miss_agg(a, c->rank2));
+        prof_end(c, ST_MISS_AGG, 0, c->rank2);
+        HIPC(c, hipEventRecord(c->ev_ma_join, c->rank2));
     }
-    // rec_start[nrec] = end of the last record (EOF when it has no terminator)
+    // rec_start[nrec] = end of the last record (EOF when it has no terminator);
+    // no terminator: k_rec_fast leaves the last record to the exact path
     if (fin.rs < c->n) {
-        u64 v = c->n;
-        HIPC(c, hipMemcpyAsync(c->rec_start.as<u64>() + c->nrec, &v, 8, hipMemcpyHostToDevice, c->stream));
-        u64 fx = SPAN_FIX;  // no terminator: k_rec_fast leaves the last record to the exact path
-        HIPC(c, hipMemcpyAsync(c->tse.as<u64>() + c->nrec - 1, &fx, 8, hipMemcpyHostToDevice, c->stream));
+        hipLaunchKernelGGL(k_put_u64, dim3(1), dim3(64), 0, c->stream, c->rec_start.as<u64>() + c->nrec, (u64)c->n,
+                           c->tse.as<u64>() + c->nrec - 1, (u64)SPAN_FIX);
+        HIPC(c, hipGetLastError());
     }
     if ((rc = launch_spans(c, want_text))) return rc;
+    if (want_text) {  // text.csv's body from here on, on the side stream
+        HIPC(c, ensure(c->tcol, kColHdrRoom + c->n + 1 + MSA_INPUT_PAD));
+        if ((rc = start_text_side(c))) return rc;
+    }
+    if (!(c->ablate & 64)) HIPC(c, hipStreamWaitEvent(c->stream, c->ev_ma_join, 0));
     // one read-back after the scan: the counters (table overflow, long-word
     // occurrences) and -- for the first shard -- the header record's end plus
     // the input's first bytes (the header, almost always)
@@ -979,7 +1102,6 @@ static int do_count(msa_ctx *c) {
             if (attempt == 0) {
                 launch_long_words(c, nl);
                 long_ran = true;
-                HIPC(c, start_text_side(c));  // text.csv beside this read-back and the ranking
                 HIPC(c, launch_artist_col(c));  // artist.csv beside text.csv
             }
             if ((rc = sync_counters(c))) return rc;
@@ -1164,9 +1286,24 @@ static int sort_and_blob(msa_ctx *c, Ranked &R, const u8 *wbuf, const u8 *wextra
     }
     int cur = 1;
     // large tables: LSD radix sort (msa_sort.hip); small ones: LDS bitonic
-    // tiles + merge passes (launch-bound sizes).  MSA_SORT=radix|merge forces one.
+    // tiles, then one ranking launch (<= 64 Ki keys) or merge passes
+    // (launch-bound sizes).  MSA_SORT=radix|merge forces one.
     HIPC(c, ensure(R.order, n * 4));
-    if (!small_sort(c, n)) {
+    HIPC(c, ensure(R.len, n * 8));
+    HIPC(c, ensure(R.off, (n + 1) * 8));
+    HIPC(c, ensure(c->blob_tot, 64));
+    // the blob length stays on the device until do_rank's one sync (the scan
+    // leaves it in blob_tot[slot]): the blob is sized from what the host knows
+    // (the last run's length, or an estimate) and k_blob_write skips keys past
+    // that capacity (do_rank redoes them)
+    bool lens_done = false;
+    if (small_sort(c, n) && n <= msa_rank_small_max()) {
+        // up to 64 Ki keys: tile sort + one ranking launch + one scan launch
+        HIPC(c, msa_launch_rank_small(k2, k1, k0, vv, n, R.ref.as<u64>(), wbuf, wextra, c->l_pos.as<u64>(),
+                                      c->l_len.as<u32>(), arena, key_off, key_len, R.order.as<u32>(),
+                                      R.len.as<u64>(), R.off.as<u64>(), c->blob_tot.as<u64>() + slot, st));
+        lens_done = true;
+    } else if (!small_sort(c, n)) {
         if (st != c->stream) return fail(c, MSA_ERR_ARG, "radix ranking runs on the library stream");
         HIPC(c, ensure(c->sort_scratch, msa_radix_scratch_bytes(n)));
         HIPC(c, msa_radix_sort(k2, k1, k0, vv, n, &cur, c->sort_scratch.as<u8>(), c->stream));
@@ -1179,20 +1316,14 @@ static int sort_and_blob(msa_ctx *c, Ranked &R, const u8 *wbuf, const u8 *wextra
                                  c->l_len.as<u32>(), arena, key_off, key_len, R.order.as<u32>(), st));
     }
     // key blob in rank order
-    HIPC(c, ensure(R.len, n * 8));
-    HIPC(c, ensure(R.off, (n + 1) * 8));
     HIPC(c, ensure(R.counts, n * 8));
     HIPC(c, ensure(R.scan_total, 64));
     HIPC(c, ensure(R.scan_bsum, ((n + 1023) / 1024 + 1) * 8));
-    HIPC(c, msa_launch_blob(R.order.as<u32>(), n, R.ref.as<u64>(), R.K[0][1].as<u64>(), R.K[0][2].as<u64>(),
-                            R.cnt.as<u64>(), wbuf, wextra, c->l_pos.as<u64>(), c->l_len.as<u32>(), arena, key_off, key_len,
-                            R.len.as<u64>(), R.off.as<u64>(), R.scan_bsum.as<u64>(), R.scan_total.as<u64>(), nullptr,
-                            nullptr, 0, st, 0));
-    // the blob length stays on the device until do_rank's one sync: the blob is
-    // sized from what the host knows (the last run's length, or an estimate)
-    // and k_blob_write skips keys past that capacity (do_rank redoes them)
-    HIPC(c, ensure(c->blob_tot, 64));
-    HIPC(c, hipMemcpyAsync(c->blob_tot.as<u64>() + slot, R.scan_total.p, 8, hipMemcpyDeviceToDevice, st));
+    if (!lens_done)
+        HIPC(c, msa_launch_blob(R.order.as<u32>(), n, R.ref.as<u64>(), R.K[0][1].as<u64>(), R.K[0][2].as<u64>(),
+                                R.cnt.as<u64>(), wbuf, wextra, c->l_pos.as<u64>(), c->l_len.as<u32>(), arena, key_off,
+                                key_len, R.len.as<u64>(), R.off.as<u64>(), R.scan_bsum.as<u64>(),
+                                c->blob_tot.as<u64>() + slot, nullptr, nullptr, 0, st, 0));
     HIPC(c, ensure(R.blob, std::max<u64>(est, R.blob_len) + 16));
     R.blob_cap = R.blob.cap - 16;
     HIPC(c, msa_launch_blob(R.order.as<u32>(), n, R.ref.as<u64>(), R.K[0][1].as<u64>(), R.K[0][2].as<u64>(),
@@ -1206,7 +1337,6 @@ static int sort_and_blob(msa_ctx *c, Ranked &R, const u8 *wbuf, const u8 *wextra
 static int do_rank(msa_ctx *c) {
     int rc;
     if (c->stage < 2) return fail(c, MSA_ERR_ARG, "msa_rank before msa_count");
-    HIPC(c, start_text_side(c));
     // words
     Ranked &W = c->rw;
     W.n = c->sum.n_words;
@@ -1342,6 +1472,9 @@ int msa_create(int device, msa_ctx **out) {
         hipStreamCreateWithFlags(&c->rank2, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_r2_fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_r2_join, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_ma_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_ma_join, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_fin, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
         hipHostMalloc((void **)&c->pin, kPinBytes, hipHostMallocDefault) != hipSuccess) {
@@ -1355,7 +1488,7 @@ int msa_create(int device, msa_ctx **out) {
 void msa_destroy(msa_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    c->text_deferred = c->artist_deferred = false;  // nothing reads them any more
+    c->artist_deferred = false;  // nothing reads it any more
     (void)join_side(c);
     (void)hipStreamSynchronize(c->stream);
     DevBuf *all[] = {&c->in_own, &c->sums, &c->carry, &c->btot, &c->bstate, &c->small, &c->rec_start, &c->extra, &c->exp_buf, &c->exp_meta, &c->imp_w, &c->imp_a, &c->imp_meta,
@@ -1385,6 +1518,9 @@ void msa_destroy(msa_ctx *c) {
     (void)hipEventDestroy(c->ev_fork);
     (void)hipEventDestroy(c->ev_join);
     (void)hipEventDestroy(c->ev_r2_fork);
+    (void)hipEventDestroy(c->ev_ma_fork);
+    (void)hipEventDestroy(c->ev_ma_join);
+    (void)hipEventDestroy(c->ev_fin);
     (void)hipEventDestroy(c->ev_r2_join);
     (void)hipStreamDestroy(c->side);
     (void)hipStreamDestroy(c->rank2);
@@ -1533,12 +1669,12 @@ int msa_get_split_column(msa_ctx *c, int which, char **out, size_t *len) {
     HIPC(c, hipSetDevice(c->device));
     int rc;
     if ((rc = resolve_col_lens(c))) return rc;
-    const DevBuf &b = which ? c->tcol : c->acol;
+    const u8 *b = which ? c->tcol.as<u8>() + c->tcol_off : c->acol.as<u8>();
     const u64 n = which ? c->tcol_len : c->acol_len;
     char *p = (char *)malloc(n + 1);
     if (!p) return fail(c, MSA_ERR_ARG, "out of host memory");
     HIPC(c, hipStreamSynchronize(c->stream));
-    if (n) HIPC(c, hipMemcpy(p, b.p, n, hipMemcpyDeviceToHost));
+    if (n) HIPC(c, hipMemcpy(p, b, n, hipMemcpyDeviceToHost));
     p[n] = 0;
     *out = p;
     *len = n;

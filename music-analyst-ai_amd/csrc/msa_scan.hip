@@ -248,7 +248,7 @@ __global__ __launch_bounds__(FN_T) void k_fn_reduce(const ChunkSum *__restrict__
 }
 
 __global__ __launch_bounds__(FN_T) void k_fn_top(const Fn *__restrict__ btot, u32 nb, u64 seg_begin,
-                                                 const State *__restrict__ init, State *__restrict__ bstate,
+                                                 const State init, State *__restrict__ bstate,
                                                  Fn *__restrict__ total) {
     // tiles of FN_T block totals: an inclusive scan in LDS per tile (as
     // k_fn_down), the state carried from tile to tile -- one element per
@@ -258,7 +258,7 @@ __global__ __launch_bounds__(FN_T) void k_fn_top(const Fn *__restrict__ btot, u3
     __shared__ Fn tot_s;
     const u32 t = threadIdx.x;
     if (t == 0) {
-        carry_s = *init;
+        carry_s = init;
         tot_s = fn_identity(seg_begin);
     }
     for (u32 base = 0; base < nb; base += FN_T) {
@@ -776,7 +776,7 @@ hipError_t msa_launch_summary(const u8 *buf, u64 seg_begin, u64 seg_end, u32 nch
 u32 msa_fn_blocks(u32 nchunks) { return (nchunks + FN_T - 1) / FN_T; }
 
 hipError_t msa_launch_fn(const ChunkSum *sums, u64 seg_begin, u32 nchunks, Fn *btot, State *bstate, Fn *total,
-                         const State *init, State *carry, State *final_state, hipStream_t s) {
+                         State init, State *carry, State *final_state, hipStream_t s) {
     if (!nchunks) return hipSuccess;
     const u32 nb = msa_fn_blocks(nchunks);
     hipLaunchKernelGGL(k_fn_reduce, dim3(nb), dim3(FN_T), 0, s, sums, seg_begin, nchunks, btot);
