@@ -63,9 +63,10 @@ hipError_t msa_launch_sort(u64 *const[3], u64 *const[3], u64 *const[3], u32 *con
 hipError_t msa_launch_fixup(const u64 *, const u64 *, const u64 *, const u32 *, u64, const u64 *, const u8 *,
                             const u8 *, const u64 *, const u32 *, const u8 *, const u64 *, const u32 *, u32 *, hipStream_t);
 u64 msa_rank_small_max();
+u64 msa_rank_small_scratch(u64 n);
 hipError_t msa_launch_rank_small(u64 *const[3], u64 *const[3], u64 *const[3], u32 *const[3], u64, const u64 *,
                                  const u8 *, const u8 *, const u64 *, const u32 *, const u8 *, const u64 *,
-                                 const u32 *, u32 *, u64 *, u64 *, u64 *, hipStream_t);
+                                 const u32 *, u32 *, u64 *, u64 *, u64 *, u64 *, u32 *, hipStream_t);
 hipError_t msa_launch_blob(const u32 *, u64, const u64 *, const u64 *, const u64 *, const u64 *, const u8 *,
                            const u8 *, const u64 *, const u32 *, const u8 *, const u64 *, const u32 *, u64 *, u64 *, u64 *, u64 *,
                            u8 *, u64 *, u64, hipStream_t, int);
@@ -94,6 +95,7 @@ struct Ranked {
     DevBuf V[3];
     DevBuf ref, cnt, order, len, off, blob, counts;
     DevBuf scan_bsum, scan_total;  // the blob offsets' scan scratch (the two tables rank concurrently)
+    DevBuf rank_cnt;               // the small-table ranking's per-tile counts
     u64 n = 0, blob_len = 0, blob_cap = 0;
     bool blob_pending = false;  // blob_len not read back yet (do_rank's sync)
     BlobArgs pending{};
@@ -216,8 +218,6 @@ struct msa_ctx {
     // (both small-table sorts are launch/latency-bound chains)
     hipStream_t rank2 = nullptr;
     hipEvent_t ev_r2_fork = nullptr, ev_r2_join = nullptr;
-    // K3's word-miss aggregation runs on rank2 beside the record spans
-    hipEvent_t ev_ma_fork = nullptr, ev_ma_join = nullptr;
     // the K2 final-state read-back (launch_scan_fn / wait_scan_fn)
     hipEvent_t ev_fin = nullptr;
     State fin_init{};
@@ -230,6 +230,14 @@ struct msa_ctx {
     // the text column's body starts at kColHdrRoom, its header line right
     // before it (written once the header is read back): tcol + tcol_off
     u64 tcol_off = 0;
+    // the body is launched after the artist pass of msa_count: on the side
+    // stream beside the count read-back and the ranking, or on the library
+    // stream by the first entry point that needs it.  Measured: launched right
+    // after the split's span scans, the gather's full grid held every CU and
+    // the read-back copies waited ~440 us for it; with a persistent grid of 2
+    // workgroups per CU (room for the artist tables beside it) the gather
+    // itself took 1.5-1.9 ms instead of 0.55
+    bool text_deferred = false;
     // artist.csv waits until the artist pass of msa_count is enqueued (that
     // pass reads k_rec_fast's keys, not the column); entry points that read
     // acol launch it first
@@ -284,6 +292,7 @@ static int materialise_column(msa_ctx *c, bool text, u64 hdr, DevBuf &col, DevBu
                               DevBuf &srcb, DevBuf &pairsb, hipStream_t st);
 static int put_bytes(msa_ctx *c, u8 *dst, const std::string &b, hipStream_t st);
 static int start_text_side(msa_ctx *c);
+static int launch_text(msa_ctx *c, hipStream_t st);
 // The deferred artist.csv pass on the library stream.
 static hipError_t launch_artist_col(msa_ctx *c) {
     if (!c->artist_deferred) return hipSuccess;
@@ -302,6 +311,7 @@ static hipError_t join_side(msa_ctx *c) {
         const hipError_t e = launch_artist_col(c);
         if (e != hipSuccess) return e;
     }
+    if (c->text_deferred && launch_text(c, c->stream)) return hipErrorUnknown;
     if (!c->side_pending) return hipSuccess;
     c->side_pending = false;
     return hipStreamWaitEvent(c->stream, c->ev_join, 0);
@@ -636,15 +646,21 @@ struct Bytes256 {
 __global__ void k_put_bytes(u8 *dst, Bytes256 v, u32 n) {
     if (threadIdx.x < n) dst[threadIdx.x] = v.b[threadIdx.x];
 }
-// text.csv's body on the side stream, after what is enqueued on the library
-// stream so far (the record spans and their offset scans)
+// The deferred body of text.csv on stream st (the side stream: after what is
+// enqueued on the library stream so far).
+static int launch_text(msa_ctx *c, hipStream_t st) {
+    int rc;
+    c->text_deferred = false;
+    prof_begin(c, ST_TEXT_COLUMN, st);
+    if ((rc = materialise_column(c, true, kColHdrRoom, c->tcol, c->tlen, c->toff, c->tsrc, c->tpairs, st))) return rc;
+    prof_end(c, ST_TEXT_COLUMN, c->n * 2 + c->nrec * 40, st);  // ~ the text column read + written
+    return MSA_OK;
+}
 static int start_text_side(msa_ctx *c) {
+    if (!c->text_deferred) return MSA_OK;
     int rc;
     HIPC(c, fork_side(c));
-    prof_begin(c, ST_TEXT_COLUMN, c->side);
-    if ((rc = materialise_column(c, true, kColHdrRoom, c->tcol, c->tlen, c->toff, c->tsrc, c->tpairs, c->side)))
-        return rc;
-    prof_end(c, ST_TEXT_COLUMN, c->n * 2 + c->nrec * 40, c->side);  // ~ the text column read + written
+    if ((rc = launch_text(c, c->side))) return rc;
     HIPC(c, hipEventRecord(c->ev_join, c->side));
     c->side_pending = true;
     return MSA_OK;
@@ -824,8 +840,8 @@ static int split_prologue(msa_ctx *c, u64 nul_n, bool rs0) {
 
 static int split_once(msa_ctx *c, int flags) {
     int rc;
-    c->artist_deferred = false;  // superseded by this split
-    HIPC(c, join_side(c));       // a text column pass in flight reads buffers this one rewrites
+    c->artist_deferred = c->text_deferred = false;  // superseded by this split
+    HIPC(c, join_side(c));  // a text column pass in flight reads buffers this one rewrites
     if (!c->in) return fail(c, MSA_ERR_ARG, "no input bound (msa_load_csv / msa_bind_csv)");
     if (c->n == 0 && !c->cont) return fail(c, MSA_ERR_NOHEADER, "Dataset does not contain a header row");
     const bool want_text = (flags & MSA_SPLIT_TEXT_COLUMN) != 0;
@@ -913,15 +929,12 @@ static int split_once(msa_ctx *c, int flags) {
         HIPC(c, hipMemsetAsync(c->rec_start.p, 0, 8, c->stream));
         if ((rc = launch_k3(cap))) return rc;
     }
-    // the word-miss aggregation beside the record spans (rank2 is idle until
-    // do_rank); the library stream waits for it before the word lists
+    // the word-miss aggregation (measured beside k_rec_fast on rank2: both
+    // kernels took twice as long, no gain)
     if (!(c->ablate & 64)) {
-        HIPC(c, hipEventRecord(c->ev_ma_fork, c->stream));
-        HIPC(c, hipStreamWaitEvent(c->rank2, c->ev_ma_fork, 0));
-        prof_begin(c, ST_MISS_AGG, c->rank2);
-        HIPC(c, msa_launch_miss_agg(a, c->rank2));
-        prof_end(c, ST_MISS_AGG, 0, c->rank2);
-        HIPC(c, hipEventRecord(c->ev_ma_join, c->rank2));
+        prof_begin(c, ST_MISS_AGG);
+        HIPC(c, msa_launch_miss_agg(a, c->stream));
+        prof_end(c, ST_MISS_AGG, 0);
     }
     // rec_start[nrec] = end of the last record (EOF when it has no terminator);
     // no terminator: k_rec_fast leaves the last record to the exact path
@@ -931,11 +944,10 @@ static int split_once(msa_ctx *c, int flags) {
         HIPC(c, hipGetLastError());
     }
     if ((rc = launch_spans(c, want_text))) return rc;
-    if (want_text) {  // text.csv's body from here on, on the side stream
+    if (want_text) {  // text.csv's body: deferred (msa_ctx::text_deferred)
         HIPC(c, ensure(c->tcol, kColHdrRoom + c->n + 1 + MSA_INPUT_PAD));
-        if ((rc = start_text_side(c))) return rc;
+        c->text_deferred = true;
     }
-    if (!(c->ablate & 64)) HIPC(c, hipStreamWaitEvent(c->stream, c->ev_ma_join, 0));
     // one read-back after the scan: the counters (table overflow, long-word
     // occurrences) and -- for the first shard -- the header record's end plus
     // the input's first bytes (the header, almost always)
@@ -1102,7 +1114,8 @@ static int do_count(msa_ctx *c) {
             if (attempt == 0) {
                 launch_long_words(c, nl);
                 long_ran = true;
-                HIPC(c, launch_artist_col(c));  // artist.csv beside text.csv
+                if ((rc = start_text_side(c))) return rc;  // text.csv beside this read-back and the ranking
+                HIPC(c, launch_artist_col(c));               // artist.csv beside text.csv
             }
             if ((rc = sync_counters(c))) return rc;
             long_ok = attempt == 0;
@@ -1292,16 +1305,19 @@ static int sort_and_blob(msa_ctx *c, Ranked &R, const u8 *wbuf, const u8 *wextra
     HIPC(c, ensure(R.len, n * 8));
     HIPC(c, ensure(R.off, (n + 1) * 8));
     HIPC(c, ensure(c->blob_tot, 64));
+    HIPC(c, ensure(R.scan_bsum, ((n + 1023) / 1024 + 1) * 8));
     // the blob length stays on the device until do_rank's one sync (the scan
     // leaves it in blob_tot[slot]): the blob is sized from what the host knows
     // (the last run's length, or an estimate) and k_blob_write skips keys past
     // that capacity (do_rank redoes them)
     bool lens_done = false;
     if (small_sort(c, n) && n <= msa_rank_small_max()) {
-        // up to 64 Ki keys: tile sort + one ranking launch + one scan launch
+        // up to 64 Ki keys: tile sort + two ranking launches + the offsets' scan
+        HIPC(c, ensure(R.rank_cnt, msa_rank_small_scratch(n)));
         HIPC(c, msa_launch_rank_small(k2, k1, k0, vv, n, R.ref.as<u64>(), wbuf, wextra, c->l_pos.as<u64>(),
                                       c->l_len.as<u32>(), arena, key_off, key_len, R.order.as<u32>(),
-                                      R.len.as<u64>(), R.off.as<u64>(), c->blob_tot.as<u64>() + slot, st));
+                                      R.len.as<u64>(), R.off.as<u64>(), R.scan_bsum.as<u64>(),
+                                      c->blob_tot.as<u64>() + slot, R.rank_cnt.as<u32>(), st));
         lens_done = true;
     } else if (!small_sort(c, n)) {
         if (st != c->stream) return fail(c, MSA_ERR_ARG, "radix ranking runs on the library stream");
@@ -1337,6 +1353,7 @@ static int sort_and_blob(msa_ctx *c, Ranked &R, const u8 *wbuf, const u8 *wextra
 static int do_rank(msa_ctx *c) {
     int rc;
     if (c->stage < 2) return fail(c, MSA_ERR_ARG, "msa_rank before msa_count");
+    if ((rc = start_text_side(c))) return rc;
     // words
     Ranked &W = c->rw;
     W.n = c->sum.n_words;
@@ -1472,8 +1489,6 @@ int msa_create(int device, msa_ctx **out) {
         hipStreamCreateWithFlags(&c->rank2, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_r2_fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_r2_join, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_ma_fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_ma_join, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fin, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
@@ -1488,7 +1503,7 @@ int msa_create(int device, msa_ctx **out) {
 void msa_destroy(msa_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    c->artist_deferred = false;  // nothing reads it any more
+    c->artist_deferred = c->text_deferred = false;  // nothing reads them any more
     (void)join_side(c);
     (void)hipStreamSynchronize(c->stream);
     DevBuf *all[] = {&c->in_own, &c->sums, &c->carry, &c->btot, &c->bstate, &c->small, &c->rec_start, &c->extra, &c->exp_buf, &c->exp_meta, &c->imp_w, &c->imp_a, &c->imp_meta,
@@ -1504,7 +1519,7 @@ void msa_destroy(msa_ctx *c) {
             for (auto &k : s) release(k);
         for (auto &v : R->V) release(v);
         DevBuf *rb[] = {&R->ref, &R->cnt, &R->order, &R->len, &R->off, &R->blob, &R->counts, &R->scan_bsum,
-                        &R->scan_total};
+                        &R->scan_total, &R->rank_cnt};
         for (DevBuf *b : rb) release(*b);
     }
     for (auto &s : c->t_K)
@@ -1518,8 +1533,6 @@ void msa_destroy(msa_ctx *c) {
     (void)hipEventDestroy(c->ev_fork);
     (void)hipEventDestroy(c->ev_join);
     (void)hipEventDestroy(c->ev_r2_fork);
-    (void)hipEventDestroy(c->ev_ma_fork);
-    (void)hipEventDestroy(c->ev_ma_join);
     (void)hipEventDestroy(c->ev_fin);
     (void)hipEventDestroy(c->ev_r2_join);
     (void)hipStreamDestroy(c->side);

@@ -1863,99 +1863,77 @@ __global__ void k_blob_write(const u32 *__restrict__ order, u64 n, const u64 *__
 }
 
 // ---------------------------------------------------------------------------
-// Small tables (<= MR_MAXN keys) in one more launch after k_tile_sort: every
-// element finds its final rank directly -- the count of smaller keys in each
-// sorted tile (a lower bound: 32 samples per tile in LDS, then 5 steps in the
-// tile, four tiles' searches interleaved), plus, for keys tied on all 24 bytes
-// (long words sharing 16 bytes and a count), the tied entries that full_cmp
-// orders first -- and writes its entry id and key length at that rank (the
-// merge passes, the tie fix-up and k_blob_len in one launch).
-#define MR_T 256
-#define MR_SPT 32  // samples per tile (stride TS_N / MR_SPT)
+// Small tables (<= MR_MAXN keys) in two launches after k_tile_sort, with no
+// dependent global loads (the ranking runs beside the text column's gather,
+// which makes every L2 miss slow):
+//   k_rank_count  workgroup u: tile u's keys in LDS; every key counts the
+//                 keys of tile u smaller than it (binary search in LDS) and
+//                 flags an equal one (keys tied on all 24 bytes: long words
+//                 sharing 16 bytes and a count) -> cnt[u][i].  One workgroup
+//                 per tile: few, long workgroups (beside the gather, a grid
+//                 of tile pairs waited for CU slots: 320 us)
+//   k_rank_place  rank = sum over u; tied keys ordered by full_cmp (rare);
+//                 writes the entry id and its key length at that rank
+// (the merge passes, the tie fix-up and k_blob_len in two launches).
 #define MR_MAXT 64
 #define MR_MAXN ((u64)MR_MAXT * TS_N)
-__global__ __launch_bounds__(MR_T) void k_merge_rank(const u64 *__restrict__ K2, const u64 *__restrict__ K1,
-                                                     const u64 *__restrict__ K0, const u32 *__restrict__ V, u64 n,
-                                                     const u64 *__restrict__ ref, const u8 *buf, const u8 *extra,
-                                                     const u64 *l_pos, const u32 *l_len, const u8 *arena,
-                                                     const u64 *key_off, const u32 *key_len, u32 *__restrict__ order,
-                                                     u64 *__restrict__ len) {
-    __shared__ u64 s2[MR_MAXT * MR_SPT], s1[MR_MAXT * MR_SPT], s0[MR_MAXT * MR_SPT];
-    constexpr u32 STRIDE = TS_N / MR_SPT;
-    const u32 T = (u32)((n + TS_N - 1) / TS_N);
-    for (u32 j = threadIdx.x; j < T * MR_SPT; j += MR_T) {
-        const u64 g = (u64)(j / MR_SPT) * TS_N + (u64)(j % MR_SPT) * STRIDE;
-        const bool ok = g < n && (j % MR_SPT) * STRIDE < TS_N;
-        s2[j] = ok ? K2[g] : ~0ull;
-        s1[j] = ok ? K1[g] : ~0ull;
-        s0[j] = ok ? K0[g] : ~0ull;
+#define RC_T 1024
+__global__ __launch_bounds__(RC_T) void k_rank_count(const u64 *__restrict__ K2, const u64 *__restrict__ K1,
+                                                     const u64 *__restrict__ K0, u64 n, u32 *__restrict__ cnt) {
+    __shared__ u64 s2[TS_N], s1[TS_N], s0[TS_N];
+    const u32 u = blockIdx.x;
+    const u64 ub = (u64)u * TS_N;
+    const u32 un = (u32)min((u64)TS_N, n - ub);
+    for (u32 j = threadIdx.x; j < un; j += RC_T) {
+        s2[j] = K2[ub + j];
+        s1[j] = K1[ub + j];
+        s0[j] = K0[ub + j];
     }
     __syncthreads();
-    const u64 i = (u64)blockIdx.x * MR_T + threadIdx.x;
-    if (i >= n) return;
-    const u64 a2 = K2[i], a1 = K1[i], a0 = K0[i];
-    const u32 me_t = (u32)(i / TS_N);
-    u64 less = 0;
-    bool tied = false;
-    for (u32 u0 = 0; u0 < T; u0 += 4) {
-        u32 p[4], R[4];
-        u64 base[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const u32 u = min(u0 + q, T - 1);
-            base[q] = (u64)u * TS_N;
-            const u32 tn = (u32)min((u64)TS_N, n - base[q]);
-            // samples < a: the lower bound lies in (STRIDE (kk - 1), STRIDE kk]
-            u32 kk = 0;
-#pragma unroll
-            for (u32 st = MR_SPT / 2; st; st >>= 1) {
-                const u32 j = u * MR_SPT + kk + st - 1;
-                if (key_lt(s2[j], s1[j], s0[j], a2, a1, a0)) kk += st;
-            }
-            if (kk == MR_SPT - 1 && key_lt(s2[u * MR_SPT + kk], s1[u * MR_SPT + kk], s0[u * MR_SPT + kk], a2, a1, a0))
-                kk = MR_SPT;
-            p[q] = kk ? STRIDE * (kk - 1) + 1 : 0;
-            R[q] = kk ? min(STRIDE * kk, tn) : 0;
+    for (u64 i = threadIdx.x; i < n; i += RC_T) {
+        const u64 a2 = K2[i], a1 = K1[i], a0 = K0[i];
+        const u32 j = (u32)(i - ub);  // own tile: its index in the tile
+        u32 lo = 0, hi = un;  // first key of tile u not smaller than a
+        while (lo < hi) {
+            const u32 m = (lo + hi) >> 1;
+            if (key_lt(s2[m], s1[m], s0[m], a2, a1, a0)) lo = m + 1;
+            else hi = m;
         }
-#pragma unroll
-        for (u32 st = STRIDE / 2; st; st >>= 1) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const u32 x = p[q] + st - 1;
-                if (x < R[q]) {
-                    const u64 g = base[q] + x;
-                    if (key_lt(K2[g], K1[g], K0[g], a2, a1, a0)) p[q] += st;
-                }
-            }
+        bool tie;
+        if (i >= ub && i < ub + un) {
+            tie = (j > 0 && s2[j - 1] == a2 && s1[j - 1] == a1 && s0[j - 1] == a0) ||
+                  (j + 1 < un && s2[j + 1] == a2 && s1[j + 1] == a1 && s0[j + 1] == a0);
+        } else {
+            tie = lo < un && s2[lo] == a2 && s1[lo] == a1 && s0[lo] == a0;
         }
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const u32 u = u0 + q;
-            if (u >= T) break;
-            less += p[q];
-            const u64 g = base[q] + p[q];
-            const u64 tn = min((u64)TS_N, n - base[q]);
-            // another entry with the same 24 key bytes in this tile?
-            if (u == me_t) {
-                if ((i > base[q] && K2[i - 1] == a2 && K1[i - 1] == a1 && K0[i - 1] == a0) ||
-                    (i + 1 < base[q] + tn && K2[i + 1] == a2 && K1[i + 1] == a1 && K0[i + 1] == a0))
-                    tied = true;
-            } else if (p[q] < tn && K2[g] == a2 && K1[g] == a1 && K0[g] == a0) {
-                tied = true;
-            }
-        }
+        cnt[(u64)u * n + i] = lo | (tie ? 0x80000000u : 0u);
     }
+}
+
+__global__ __launch_bounds__(256) void k_rank_place(const u64 *__restrict__ K2, const u64 *__restrict__ K1,
+                                                    const u64 *__restrict__ K0, const u32 *__restrict__ V, u64 n,
+                                                    const u32 *__restrict__ cnt, const u64 *__restrict__ ref,
+                                                    const u8 *buf, const u8 *extra, const u64 *l_pos,
+                                                    const u32 *l_len, const u8 *arena, const u64 *key_off,
+                                                    const u32 *key_len, u32 *__restrict__ order,
+                                                    u64 *__restrict__ len) {
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const u32 T = (u32)((n + TS_N - 1) / TS_N);
+    u64 less = 0;
+    u32 tie = 0;
+    for (u32 u = 0; u < T; ++u) {
+        const u32 c = cnt[(u64)u * n + i];
+        less += c & 0x7FFFFFFFu;
+        tie |= c;
+    }
+    const u64 a2 = K2[i], a1 = K1[i], a0 = K0[i];
     const u32 v = V[i];
     const u64 me = ref[v];
-    if (tied) {  // rare: rank among the tied entries of every tile by full key
+    if (tie & 0x80000000u) {  // rare: rank among the tied entries of every tile by full key
         for (u32 u = 0; u < T; ++u) {
             const u64 b = (u64)u * TS_N, e = min(b + TS_N, n);
-            u64 lo = b, hi = e;  // first element >= a in the tile
-            while (lo < hi) {
-                const u64 m = (lo + hi) >> 1;
-                if (key_lt(K2[m], K1[m], K0[m], a2, a1, a0)) lo = m + 1;
-                else hi = m;
-            }
+            u64 lo = b + (cnt[(u64)u * n + i] & 0x7FFFFFFFu);
             for (u64 j = lo; j < e && K2[j] == a2 && K1[j] == a1 && K0[j] == a0; ++j)
                 if (j != i && full_cmp(ref[V[j]], me, a1, a0, buf, extra, l_pos, l_len, arena, key_off, key_len) < 0)
                     ++less;
@@ -1963,35 +1941,6 @@ __global__ __launch_bounds__(MR_T) void k_merge_rank(const u64 *__restrict__ K2,
     }
     order[less] = v;
     len[less] = entry_key_len(me, a1, a0, l_len, key_len);
-}
-
-// Exclusive scan of up to SS_T * SS_PER u64 in one workgroup (the small
-// tables' key lengths -> blob offsets), total to *total.
-#define SS_T 1024
-#define SS_PER 64
-__global__ __launch_bounds__(SS_T) void k_scan_small(const u64 *__restrict__ in, u64 n, u64 *__restrict__ out,
-                                                     u64 *__restrict__ total) {
-    __shared__ u64 wtot[SS_T / 64];
-    const u32 t = threadIdx.x, lane = lane_id(), w = t >> 6;
-    const u64 per = (n + SS_T - 1) / SS_T;
-    const u64 a = min(n, (u64)t * per), b = min(n, a + per);
-    u64 s = 0;
-    for (u64 k = a; k < b; ++k) s += in[k];
-    u64 x = s;  // inclusive wave scan
-    for (int o = 1; o < 64; o <<= 1) {
-        const u64 y = __shfl_up(x, o);
-        if (lane >= (u32)o) x += y;
-    }
-    if (lane == 63) wtot[w] = x;
-    __syncthreads();
-    u64 acc = x - s;
-    for (u32 k = 0; k < w; ++k) acc += wtot[k];
-    if (t == SS_T - 1) *total = acc + s;
-    for (u64 k = a; k < b; ++k) {
-        const u64 v = in[k];
-        out[k] = acc;
-        acc += v;
-    }
 }
 
 // ---------------------------------------------------------------------------
@@ -2135,20 +2084,22 @@ hipError_t msa_launch_sort(u64 *const K2[3], u64 *const K1[3], u64 *const K0[3],
     return hipGetLastError();
 }
 u64 msa_rank_small_max() { return MR_MAXN; }
-// Small-table ranking: k_tile_sort + k_merge_rank (entry ids and key lengths
-// in rank order) + k_scan_small (blob offsets, total to *total).  Set 1 of
-// K2/K1/K0/V holds the sorted tiles.
+u64 msa_rank_small_scratch(u64 n) { return ((n + TS_N - 1) / TS_N) * n * 4; }
+// Small-table ranking: k_tile_sort + k_rank_count + k_rank_place (entry ids
+// and key lengths in rank order) + the blob offsets' scan (total to *total).
+// Set 1 of K2/K1/K0/V holds the sorted tiles; cnt: msa_rank_small_scratch(n)
+// bytes.
 hipError_t msa_launch_rank_small(u64 *const K2[3], u64 *const K1[3], u64 *const K0[3], u32 *const V[3], u64 n,
                                  const u64 *ref, const u8 *buf, const u8 *extra, const u64 *l_pos, const u32 *l_len,
                                  const u8 *arena, const u64 *key_off, const u32 *key_len, u32 *order, u64 *len,
-                                 u64 *off, u64 *total, hipStream_t s) {
+                                 u64 *off, u64 *bsum, u64 *total, u32 *cnt, hipStream_t s) {
     if (!n || n > MR_MAXN) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_tile_sort, dim3((u32)((n + TS_N - 1) / TS_N)), dim3(TS_T), 0, s, K2[0], K1[0], K0[0], V[0],
-                       n, K2[1], K1[1], K0[1], V[1]);
-    hipLaunchKernelGGL(k_merge_rank, grid1(n, MR_T), dim3(MR_T), 0, s, K2[1], K1[1], K0[1], V[1], n, ref, buf, extra,
-                       l_pos, l_len, arena, key_off, key_len, order, len);
-    hipLaunchKernelGGL(k_scan_small, dim3(1), dim3(SS_T), 0, s, (const u64 *)len, n, off, total);
-    return hipGetLastError();
+    const u32 T = (u32)((n + TS_N - 1) / TS_N);
+    hipLaunchKernelGGL(k_tile_sort, dim3(T), dim3(TS_T), 0, s, K2[0], K1[0], K0[0], V[0], n, K2[1], K1[1], K0[1], V[1]);
+    hipLaunchKernelGGL(k_rank_count, dim3(T), dim3(RC_T), 0, s, K2[1], K1[1], K0[1], n, cnt);
+    hipLaunchKernelGGL(k_rank_place, grid1(n), dim3(256), 0, s, K2[1], K1[1], K0[1], V[1], n, (const u32 *)cnt, ref,
+                       buf, extra, l_pos, l_len, arena, key_off, key_len, order, len);
+    return msa_exclusive_scan(len, n, off, bsum, total, s);
 }
 hipError_t msa_launch_fixup(const u64 *K2, const u64 *K1, const u64 *K0, const u32 *V, u64 n, const u64 *ref,
                             const u8 *buf, const u8 *extra, const u64 *l_pos, const u32 *l_len, const u8 *arena, const u64 *key_off,
