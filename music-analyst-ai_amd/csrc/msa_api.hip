@@ -1696,7 +1696,6 @@ int msa_get_split_column(msa_ctx *c, int which, char **out, size_t *len) {
 
 int msa_set_artist_reader(msa_ctx *c, int exact) {
     if (!c) return MSA_ERR_ARG;
-    HIPC(c, join_side(c));  // text.csv (side stream) may still read the buffers this touches
     c->artist_exact = exact != 0;
     return MSA_OK;
 }
@@ -1740,7 +1739,6 @@ static_assert(sizeof(msa_shard_fn) == sizeof(Fn), "msa_shard_fn mirrors Fn");
 
 int msa_set_shard(msa_ctx *c, int first) {
     if (!c) return MSA_ERR_ARG;
-    HIPC(c, join_side(c));  // text.csv (side stream) may still read the buffers this touches
     c->cont = first == 0;
     return MSA_OK;
 }
@@ -1766,7 +1764,7 @@ static int piece_of(msa_ctx *c, int piece, const u8 **base, u64 *len) {
 
 int msa_piece_size(msa_ctx *c, int piece, uint64_t *len) {
     if (!c || !len) return MSA_ERR_ARG;
-    HIPC(c, join_side(c));  // text.csv (side stream) may still read the buffers this touches
+    if (piece == MSA_PIECE_ARTISTS) HIPC(c, launch_artist_col(c));  // artist.csv read below; text.csv may keep running
     const u8 *base;
     u64 n;
     int rc;
@@ -1777,7 +1775,7 @@ int msa_piece_size(msa_ctx *c, int piece, uint64_t *len) {
 
 int msa_shard_function(msa_ctx *c, int piece, msa_shard_fn *out) {
     if (!c || !out) return MSA_ERR_ARG;
-    HIPC(c, join_side(c));  // text.csv (side stream) may still read the buffers this touches
+    if (piece == MSA_PIECE_ARTISTS) HIPC(c, launch_artist_col(c));  // artist.csv read below; text.csv may keep running
     HIPC(c, hipSetDevice(c->device));
     const u8 *base;
     u64 len;
@@ -1796,7 +1794,7 @@ int msa_shard_function(msa_ctx *c, int piece, msa_shard_fn *out) {
 int msa_shard_head(msa_ctx *c, int piece, const msa_shard_fn *before, int nbefore, const uint64_t *sizes,
                    uint64_t *head) {
     if (!c || !head || nbefore < 0 || (nbefore && (!before || !sizes))) return MSA_ERR_ARG;
-    HIPC(c, join_side(c));  // text.csv (side stream) may still read the buffers this touches
+    if (piece == MSA_PIECE_ARTISTS) HIPC(c, launch_artist_col(c));  // artist.csv read below; text.csv may keep running
     HIPC(c, hipSetDevice(c->device));
     const u8 *base;
     u64 len;
@@ -1835,7 +1833,7 @@ int msa_shard_head(msa_ctx *c, int piece, const msa_shard_fn *before, int nbefor
 
 int msa_segment_copy(msa_ctx *c, int piece, uint64_t off, uint64_t len, void *dst) {
     if (!c || (len && !dst)) return MSA_ERR_ARG;
-    HIPC(c, join_side(c));  // text.csv (side stream) may still read the buffers this touches
+    if (piece == MSA_PIECE_ARTISTS) HIPC(c, launch_artist_col(c));  // artist.csv read below; text.csv may keep running
     HIPC(c, hipSetDevice(c->device));
     const u8 *base;
     u64 plen;
@@ -1865,7 +1863,8 @@ static hipError_t grow_keep(DevBuf &b, size_t bytes, size_t keep, hipStream_t s)
 
 int msa_segment_set(msa_ctx *c, int piece, uint64_t skip, const void *tail, uint64_t tail_len) {
     if (!c || (tail_len && !tail)) return MSA_ERR_ARG;
-    HIPC(c, join_side(c));  // text.csv (side stream) may still read the buffers this touches
+    // the input is rewritten: text.csv (side stream) must be done with it
+    HIPC(c, piece == MSA_PIECE_ARTISTS ? launch_artist_col(c) : join_side(c));
     HIPC(c, hipSetDevice(c->device));
     const u8 *base;
     u64 len;
@@ -1932,7 +1931,6 @@ static void fill_exp_src(msa_ctx *c, int table, ExpSrc &x, u64 *n) {
 
 int msa_export_partitions(msa_ctx *c, int table, int nparts, uint64_t *part_bytes) {
     if (!c || nparts < 1 || nparts > 4096 || !part_bytes) return MSA_ERR_ARG;
-    HIPC(c, join_side(c));  // text.csv (side stream) may still read the buffers this touches
     if (table != MSA_TABLE_WORDS && table != MSA_TABLE_ARTISTS) return MSA_ERR_ARG;
     if (c->stage < 2) return fail(c, MSA_ERR_ARG, "msa_export_partitions before msa_count");
     HIPC(c, hipSetDevice(c->device));
@@ -1963,7 +1961,6 @@ int msa_export_partitions(msa_ctx *c, int table, int nparts, uint64_t *part_byte
 
 int msa_export_ranked(msa_ctx *c, int table, uint64_t limit, uint64_t *bytes) {
     if (!c || !bytes) return MSA_ERR_ARG;
-    HIPC(c, join_side(c));  // text.csv (side stream) may still read the buffers this touches
     if (table != MSA_TABLE_WORDS && table != MSA_TABLE_ARTISTS) return MSA_ERR_ARG;
     if (c->stage < 3) return fail(c, MSA_ERR_ARG, "msa_export_ranked before msa_rank");
     HIPC(c, hipSetDevice(c->device));
@@ -1984,7 +1981,6 @@ int msa_export_ranked(msa_ctx *c, int table, uint64_t limit, uint64_t *bytes) {
 
 int msa_export_copy(msa_ctx *c, void *dst) {
     if (!c || (c->exp_bytes && !dst)) return MSA_ERR_ARG;
-    HIPC(c, join_side(c));  // text.csv (side stream) may still read the buffers this touches
     HIPC(c, hipSetDevice(c->device));
     if (c->exp_bytes) HIPC(c, hipMemcpyAsync(dst, c->exp_buf.p, c->exp_bytes, hipMemcpyDefault, c->stream));
     HIPC(c, hipStreamSynchronize(c->stream));
@@ -2003,7 +1999,7 @@ static int clear_one(msa_ctx *c, DevBuf &tab, DevBuf &list, u64 &used, u32 w) {
 
 int msa_import_partitions(msa_ctx *c, int table, const void *src, const uint64_t *blk_off, int nblk) {
     if (!c || !blk_off || nblk < 1) return MSA_ERR_ARG;
-    HIPC(c, join_side(c));  // text.csv (side stream) may still read the buffers this touches
+    HIPC(c, launch_artist_col(c));  // it reads key_off / key_len, which an artist import rewrites
     if (table != MSA_TABLE_WORDS && table != MSA_TABLE_ARTISTS) return MSA_ERR_ARG;
     if (c->stage < 2) return fail(c, MSA_ERR_ARG, "msa_import_partitions before msa_count");
     HIPC(c, hipSetDevice(c->device));

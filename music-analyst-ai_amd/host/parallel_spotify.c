@@ -47,6 +47,13 @@ typedef struct {
     int word_limit, artist_limit, device, processes;
     char outdir[PATH_MAX];
     char split_dir[PATH_MAX];
+    /* bench mode (no reference counterpart; bench.py --driver chost): each
+     * rank generates its song range of one synthetic corpus in memory
+     * (msa_gen_corpus_range, bench.py's corpus) and times bench_steps runs of
+     * the whole pipeline -- boundary exchange, split, count, merge, rank, full
+     * ranked gather -- after bench_warmup untimed ones; no files are written */
+    uint64_t synth_songs;
+    int bench_steps, bench_warmup;
 } Opts;
 
 static double now_s(void) {
@@ -353,6 +360,68 @@ static int gather_ranked(Rank *R, const uint64_t *limit) {
     return 0;
 }
 
+/* One pipeline run of a rank (the timed unit of the bench mode): exact shard
+ * boundaries, split, count, key-hash merge, ranking, full ranked gather. */
+static int pipeline_step(Rank *R) {
+    msa_tr *t = R->t;
+    int rc;
+    if ((rc = resolve_piece(R, MSA_PIECE_CSV))) return rc;
+    if ((rc = msa_split_columns(R->ctx, MSA_SPLIT_TEXT_COLUMN))) return fail_rc(R->ctx, rc, "split");
+    int need = 0;
+    uint64_t need_any = 0;
+    TRY(msa_artist_reader_needed(R->ctx, &need), "artist reader");
+    TRY_T(msa_allreduce_sum_u64(t, (uint64_t)need, &need_any), "all-reduce");
+    TRY(msa_set_artist_reader(R->ctx, need_any ? 1 : 0), "artist reader");
+    if (need_any && (rc = resolve_piece(R, MSA_PIECE_ARTISTS))) return rc;
+    TRY(msa_count(R->ctx), "count");
+    if ((rc = merge_table(R, MSA_TABLE_WORDS)) || (rc = merge_table(R, MSA_TABLE_ARTISTS))) return rc;
+    TRY(msa_rank(R->ctx), "rank");
+    const uint64_t all[2] = {0, 0};
+    return gather_ranked(R, all);
+}
+
+/* Bench mode: warmup + timed runs between barriers and device syncs; rank 0
+ * prints one JSON line with the slowest rank's time and the corpus bytes. */
+static int bench_ranks(Rank *R, const Opts *o, uint64_t nbytes) {
+    msa_tr *t = R->t;
+    int rc;
+    for (int i = 0; i < o->bench_warmup; ++i)
+        if ((rc = pipeline_step(R))) return rc;
+    TRY(msa_set_profiling(R->ctx, 1), "profiling");
+    msa_profile pr;
+    TRY(msa_get_profile(R->ctx, &pr, 1), "profile");
+    TRY(msa_sync(R->ctx), "sync");
+    TRY_T(msa_barrier(t), "barrier");
+    const double t0 = now_s();
+    for (int i = 0; i < o->bench_steps; ++i)
+        if ((rc = pipeline_step(R))) return rc;
+    TRY(msa_sync(R->ctx), "sync");
+    TRY_T(msa_barrier(t), "barrier");
+    const double dt = now_s() - t0;
+    TRY(msa_get_profile(R->ctx, &pr, 1), "profile");
+    double all_dt[MSA_MAX_RANKS];
+    uint64_t total = 0;
+    TRY_T(t->allgather(t, &dt, sizeof dt, all_dt), "all-gather of timings");
+    TRY_T(msa_allreduce_sum_u64(t, nbytes, &total), "all-reduce");
+    if (t->rank == 0) {
+        double mx = 0;
+        for (int r = 0; r < t->world; ++r) mx = all_dt[r] > mx ? all_dt[r] : mx;
+        printf("{\"driver\": \"chost\", \"ranks\": %d, \"steps\": %d, \"warmup\": %d, \"seconds\": %.6f, "
+               "\"bytes_total\": %llu, \"bytes_rank0\": %llu, \"stages\": {",
+               t->world, o->bench_steps, o->bench_warmup, mx, (unsigned long long)total,
+               (unsigned long long)nbytes);
+        for (int k = 0; k < pr.n; ++k)
+            printf("%s\"%s\": [%.6f, %llu, %llu]", k ? ", " : "", pr.name[k], pr.ms[k],
+                   (unsigned long long)pr.launches[k], (unsigned long long)pr.bytes[k]);
+        printf("}}\n");
+        fflush(stdout);
+    }
+    if (t->set_stream) t->set_stream(t, NULL);
+    msa_destroy(R->ctx);
+    t->destroy(t);
+    return EXIT_SUCCESS;
+}
+
 static int rank_main(int rank, int world, msa_shared *sh, void *arg) {
     const Opts *o = (const Opts *)arg;
     int ndev = 0;
@@ -368,17 +437,28 @@ static int rank_main(int rank, int world, msa_shared *sh, void *arg) {
     if (!R->t) return 2;
     msa_tr *t = R->t;
 
-    int ok = 0;
-    const size_t n = file_size(o->dataset, &ok);
-    if (!ok) {
-        if (rank == 0) fprintf(stderr, "Failed to open dataset %s\n", o->dataset);
-        return EXIT_FAILURE;
-    }
     size_t len = 0;
-    const size_t lo = (size_t)((uint64_t)n * (uint64_t)rank / (uint64_t)world);
-    const size_t hi = (size_t)((uint64_t)n * (uint64_t)(rank + 1) / (uint64_t)world);
-    char *part = read_range(o->dataset, lo, hi, &len);
-    if (!part) { fprintf(stderr, "rank %d: cannot read %s\n", rank, o->dataset); return EXIT_FAILURE; }
+    char *part = NULL;
+    if (o->synth_songs) {  /* bench mode: this rank's songs of the synthetic corpus */
+        const msa_gen_params gp = {1, o->synth_songs, 50000, 5000, 30, MSA_GEN_ZIPF, 0};
+        const uint64_t s0 = o->synth_songs * (uint64_t)rank / (uint64_t)world;
+        const uint64_t s1 = o->synth_songs * (uint64_t)(rank + 1) / (uint64_t)world;
+        if (msa_gen_corpus_range(&gp, s0, s1 - s0, &part, &len)) {
+            fprintf(stderr, "rank %d: corpus generation failed\n", rank);
+            return EXIT_FAILURE;
+        }
+    } else {
+        int ok = 0;
+        const size_t n = file_size(o->dataset, &ok);
+        if (!ok) {
+            if (rank == 0) fprintf(stderr, "Failed to open dataset %s\n", o->dataset);
+            return EXIT_FAILURE;
+        }
+        const size_t lo = (size_t)((uint64_t)n * (uint64_t)rank / (uint64_t)world);
+        const size_t hi = (size_t)((uint64_t)n * (uint64_t)(rank + 1) / (uint64_t)world);
+        part = read_range(o->dataset, lo, hi, &len);
+        if (!part) { fprintf(stderr, "rank %d: cannot read %s\n", rank, o->dataset); return EXIT_FAILURE; }
+    }
     int rc = msa_create(device, &R->ctx);
     if (rc) { fprintf(stderr, "rank %d: libmsa_hip: cannot open GPU %d (code %d)\n", rank, device, rc); return 2; }
     /* RCCL exchanges on the library's stream: stream-ordered with the export /
@@ -386,8 +466,10 @@ static int rank_main(int rank, int world, msa_shared *sh, void *arg) {
     if (t->set_stream) t->set_stream(t, msa_stream(R->ctx));
     TRY(msa_set_shard(R->ctx, rank == 0), "set shard");
     TRY(msa_load_csv(R->ctx, part, len), "load");
-    free(part);
+    if (o->synth_songs) msa_free(part);
+    else free(part);
     TRY_T(msa_barrier(t), "barrier");
+    if (o->bench_steps > 0) return bench_ranks(R, o, (uint64_t)len);
 
     /* timed region as in run_single; compute = this rank's split + count */
     const double t0 = now_s();
@@ -479,6 +561,9 @@ int main(int argc, char **argv) {
         } else if (!strcmp(argv[i], "--device") && i + 1 < argc) o.device = atoi(argv[++i]);
         else if ((!strcmp(argv[i], "--processes") || !strcmp(argv[i], "-np")) && i + 1 < argc)
             o.processes = atoi(argv[++i]);
+        else if (!strcmp(argv[i], "--synthetic-songs") && i + 1 < argc) o.synth_songs = strtoull(argv[++i], NULL, 10);
+        else if (!strcmp(argv[i], "--bench-steps") && i + 1 < argc) o.bench_steps = atoi(argv[++i]);
+        else if (!strcmp(argv[i], "--bench-warmup") && i + 1 < argc) o.bench_warmup = atoi(argv[++i]);
         else fprintf(stderr, "Ignoring unknown argument: %s\n", argv[i]);
     }
     if (o.processes < 1 || o.processes > MSA_MAX_RANKS) {
@@ -498,7 +583,11 @@ int main(int argc, char **argv) {
     /* MSA_RANK_PATH=1 runs even one process through the rank layer (tests
      * the RCCL transport on a one-GPU box: a world of one) */
     const char *rp = getenv("MSA_RANK_PATH");
-    if (o.processes == 1 && !(rp && rp[0] == '1')) return run_single(&o);
+    if (o.bench_steps > 0 && !o.synth_songs) {
+        fprintf(stderr, "--bench-steps needs --synthetic-songs\n");
+        return EXIT_FAILURE;
+    }
+    if (o.processes == 1 && !(rp && rp[0] == '1') && o.bench_steps <= 0) return run_single(&o);
     /* fork the ranks before anything initialises the GPU in this process */
     return msa_spawn_ranks(o.processes, rank_main, &o);
 }

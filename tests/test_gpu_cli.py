@@ -115,3 +115,22 @@ def test_cli_processes_errors(case, msg, tmp_path):
                         "--processes", "2"], capture_output=True, timeout=120)
     assert p.returncode != 0
     assert msg in p.stderr
+
+
+@pytest.mark.parametrize("procs,transport", [(1, None), (2, "shm"), (4, "shm"), (1, "rccl")])
+def test_cli_bench_mode(msa_mod, procs, transport, tmp_path):
+    """bench.py --driver chost: the C host's bench mode (each rank generates its
+    song range of the synthetic corpus, times the whole pipeline) reports the
+    corpus bytes of all ranks and rank 0's stage profile."""
+    env = dict(os.environ)
+    if transport:
+        env["MSA_TRANSPORT"] = transport
+    songs = 20000
+    p = subprocess.run([CLI, "-", "--synthetic-songs", str(songs), "--processes", str(procs), "--bench-steps", "2",
+                        "--bench-warmup", "1", "--output-dir", str(tmp_path / "o")],
+                       capture_output=True, timeout=180, env=env)
+    assert p.returncode == 0, p.stderr
+    res = json.loads(p.stdout.decode().strip().splitlines()[-1])
+    assert res["driver"] == "chost" and res["ranks"] == procs and res["steps"] == 2
+    assert res["bytes_total"] == len(msa_mod.gen_corpus(songs, mode="zipf", seed=1))
+    assert res["stages"]["csv_scan"][1] == 2 and res["seconds"] > 0

@@ -29,7 +29,8 @@ for r in rows(os.path.join(d, "**", "*memory_copy_trace.csv")):
     ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), "copy/" + r.get("Stream_Id", "?"),
                f"copy {r.get('Direction', '')} {n}B"))
 ev.sort()
-starts = [i for i, e in enumerate(ev) if e[3] == "k_chunk_summary"]
+mark = os.environ.get("STEP_MARK", "k_chunk_summary")
+starts = [i for i, e in enumerate(ev) if e[3] == mark]
 if len(starts) < back + 1:
     sys.exit("not enough steps in the trace")
 a, b = starts[-back - 1], starts[-back]
