@@ -242,6 +242,12 @@ int msa_export_copy(msa_ctx *ctx, void *dst);
 /* Replace the table by the union of the received blocks (counts summed);
  * blk_off[0..nblk] are the blocks' byte offsets in src (last = total).     */
 int msa_import_partitions(msa_ctx *ctx, int table, const void *src, const uint64_t *blk_off, int nblk);
+/* Root GPU of the final gather: the blocks are every GPU's msa_export_ranked
+ * block (ranked, disjoint key partitions); the table's ranking becomes their
+ * k-way merge (no re-insertion, no sort; large tables fall back to
+ * msa_import_partitions + a ranking of this table).  Replaces, with
+ * msa_import_partitions + msa_rank, rank 0's merge + qsort (main 1011-1039). */
+int msa_import_ranked(msa_ctx *ctx, int table, const void *src, const uint64_t *blk_off, int nblk);
 
 /* ------------------------------------------- per-song word counter (row f)
  * The GPU path of /root/reference/scripts/word_count_per_song.py:

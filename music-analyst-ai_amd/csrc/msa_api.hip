@@ -63,6 +63,10 @@ hipError_t msa_launch_sort(u64 *const[3], u64 *const[3], u64 *const[3], u32 *con
 hipError_t msa_launch_fixup(const u64 *, const u64 *, const u64 *, const u32 *, u64, const u64 *, const u8 *,
                             const u8 *, const u64 *, const u32 *, const u8 *, const u64 *, const u32 *, u32 *, hipStream_t);
 u64 msa_rank_small_max();
+hipError_t msa_launch_merge_ranked(const u8 *, const u64 *, const u64 *, u32, u64, const u64 *, u32, u64 *, u64 *,
+                                   u64 *, u64 *, u64 *, u32 *, u32 *, u64 *, u64 *, u64 *, u64 *, hipStream_t);
+hipError_t msa_launch_merge_blob(const u32 *, u64, const u8 *, const u64 *, const u64 *, const u64 *, u8 *, u64 *,
+                                 hipStream_t);
 u64 msa_rank_small_scratch(u64 n);
 hipError_t msa_launch_rank_small(u64 *const[3], u64 *const[3], u64 *const[3], u32 *const[3], u64, const u64 *,
                                  const u8 *, const u8 *, const u64 *, const u32 *, const u8 *, const u64 *,
@@ -1350,15 +1354,17 @@ static int sort_and_blob(msa_ctx *c, Ranked &R, const u8 *wbuf, const u8 *wextra
     return MSA_OK;
 }
 
-static int do_rank(msa_ctx *c) {
+// tables: bit 0 words, bit 1 artists (a table left out keeps its ranking)
+static int do_rank(msa_ctx *c, int tables = 3) {
     int rc;
     if (c->stage < 2) return fail(c, MSA_ERR_ARG, "msa_rank before msa_count");
     if ((rc = start_text_side(c))) return rc;
     // words
     Ranked &W = c->rw;
-    W.n = c->sum.n_words;
+    const bool dw = (tables & 1) != 0, da = (tables & 2) != 0;
+    if (dw) W.n = c->sum.n_words;
     prof_begin(c, ST_RANK_WORDS);
-    if (W.n) {
+    if (dw && W.n) {
         for (int k = 0; k < 3; ++k) HIPC(c, ensure(W.K[0][k], W.n * 8));
         HIPC(c, ensure(W.V[0], W.n * 4));
         HIPC(c, ensure(W.ref, W.n * 8));
@@ -1391,17 +1397,17 @@ static int do_rank(msa_ctx *c) {
     // artists: on their own stream beside the words when both tables take the
     // small-table sort (a chain of short latency-bound launches each)
     Ranked &A = c->ra;
-    A.n = c->sum.n_artists;
-    const bool conc = small_sort(c, W.n) && small_sort(c, A.n) && A.n;
+    if (da) A.n = c->sum.n_artists;
+    const bool conc = dw && da && small_sort(c, W.n) && small_sort(c, A.n) && A.n;
     hipStream_t ast = conc ? c->rank2 : c->stream;
     if (conc) {
         HIPC(c, hipEventRecord(c->ev_r2_fork, c->stream));
         HIPC(c, hipStreamWaitEvent(c->rank2, c->ev_r2_fork, 0));
     }
-    if ((rc = sort_and_blob(c, W, wbuf, wextra, nullptr, nullptr, nullptr, 0, west, c->stream))) return rc;
+    if (dw && (rc = sort_and_blob(c, W, wbuf, wextra, nullptr, nullptr, nullptr, 0, west, c->stream))) return rc;
     prof_end(c, ST_RANK_WORDS, W.n * 64 + W.blob_len);
     prof_begin(c, ST_RANK_ARTISTS, ast);
-    if (A.n) {
+    if (da && A.n) {
         for (int k = 0; k < 3; ++k) HIPC(c, ensure(A.K[0][k], A.n * 8));
         HIPC(c, ensure(A.V[0], A.n * 4));
         HIPC(c, ensure(A.ref, A.n * 8));
@@ -1413,8 +1419,8 @@ static int do_rank(msa_ctx *c) {
                                           A.cnt.as<u64>(), ast));
     }
     const u8 *aarena = c->merged_a ? c->imp_a.as<u8>() : c->arena.as<u8>();
-    if ((rc = sort_and_blob(c, A, wbuf, wextra, aarena, c->key_off.as<u64>(), c->key_len.as<u32>(), 1, A.n * 32,
-                            ast)))
+    if (da && (rc = sort_and_blob(c, A, wbuf, wextra, aarena, c->key_off.as<u64>(), c->key_len.as<u32>(), 1,
+                                  A.n * 32, ast)))
         return rc;
     prof_end(c, ST_RANK_ARTISTS, A.n * 64 + A.blob_len, ast);
     if (conc) {
@@ -2110,6 +2116,83 @@ extern "C" int msa_debug_stat(msa_ctx *c, const char *name, uint64_t *v) {
 
 // Not part of include/msa_hip.h: the per-record arrays of the last split
 // (tools/k3_debug.py compares kernel variants with it).
+// Root GPU of the final gather: the received blocks are the GPUs' ranked,
+// disjoint key partitions (msa_export_ranked), merged into this context's
+// ranking of the table (k-way merge by per-tile counts, csrc/msa_post.hip:
+// k_mr_keys / k_rank_count / k_mr_place / k_mr_blob).  Above kMergeMaxKeys
+// keys the per-tile counts would outgrow the scratch: the blocks are imported
+// as partitions and this table is ranked again.
+static const u64 kMergeMaxKeys = 1ull << 18;  // MSA_MERGE_MAX_KEYS overrides (tests)
+int msa_import_ranked(msa_ctx *c, int table, const void *src, const uint64_t *blk_off, int nblk) {
+    if (!c || !blk_off || nblk < 1) return MSA_ERR_ARG;
+    if (table != MSA_TABLE_WORDS && table != MSA_TABLE_ARTISTS) return MSA_ERR_ARG;
+    if (c->stage < 2) return fail(c, MSA_ERR_ARG, "msa_import_ranked before msa_count");
+    HIPC(c, hipSetDevice(c->device));
+    const bool art = table == MSA_TABLE_ARTISTS;
+    Ranked &R = art ? c->ra : c->rw;
+    const u64 total = blk_off[nblk];
+    DevBuf &imp = art ? c->imp_a : c->imp_w;
+    HIPC(c, ensure(imp, total + 64));
+    if (total) HIPC(c, hipMemcpyAsync(imp.p, src, total, hipMemcpyDefault, c->stream));
+    HIPC(c, ensure(c->imp_meta, (2 * (size_t)nblk + 2) * 8));
+    u64 *d_off = c->imp_meta.as<u64>(), *d_base = d_off + nblk + 1;
+    HIPC(c, hipMemcpyAsync(d_off, blk_off, ((size_t)nblk + 1) * 8, hipMemcpyHostToDevice, c->stream));
+    ImpDst none;
+    memset(&none, 0, sizeof none);
+    HIPC(c, msa_launch_imp(imp.as<u8>(), d_off, (u32)nblk, d_base, 0, none, c->stream));  // record bases only
+    std::vector<u64> base((size_t)nblk + 1);
+    HIPC(c, hipMemcpyAsync(base.data(), d_base, base.size() * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    const u64 n = base[nblk];
+    u64 merge_max = kMergeMaxKeys;
+    if (const char *mm = getenv("MSA_MERGE_MAX_KEYS")) merge_max = strtoull(mm, nullptr, 10);
+    if (n > merge_max) {
+        int rc;
+        if ((rc = msa_import_partitions(c, table, src, blk_off, nblk))) return rc;
+        return do_rank(c, art ? 2 : 1);
+    }
+    // tiles: every block cut into runs of <= 1024 records (sorted, as the block is)
+    std::vector<u64> ts;
+    for (int p = 0; p < nblk; ++p)
+        for (u64 s0 = base[p]; s0 < base[p + 1]; s0 += 1024) ts.push_back(s0);
+    ts.push_back(n);
+    const u32 T = (u32)(ts.size() - 1);
+    for (int k = 0; k < 3; ++k) HIPC(c, ensure(R.K[1][k], std::max<u64>(n, 1) * 8));
+    HIPC(c, ensure(R.K[2][0], ts.size() * 8));
+    HIPC(c, ensure(R.ref, std::max<u64>(n, 1) * 8));
+    HIPC(c, ensure(R.cnt, std::max<u64>(n, 1) * 8));
+    HIPC(c, ensure(R.rank_cnt, std::max<u64>((u64)T * n, 1) * 4));
+    HIPC(c, ensure(R.order, std::max<u64>(n, 1) * 4));
+    HIPC(c, ensure(R.len, std::max<u64>(n, 1) * 8));
+    HIPC(c, ensure(R.off, (n + 1) * 8));
+    HIPC(c, ensure(R.counts, std::max<u64>(n, 1) * 8));
+    HIPC(c, ensure(R.scan_bsum, ((n + 1023) / 1024 + 1) * 8));
+    HIPC(c, ensure(c->blob_tot, 64));
+    u64 *tot = c->blob_tot.as<u64>() + (art ? 1 : 0);
+    HIPC(c, hipMemsetAsync(tot, 0, 8, c->stream));
+    HIPC(c, hipMemcpyAsync(R.K[2][0].p, ts.data(), ts.size() * 8, hipMemcpyHostToDevice, c->stream));
+    HIPC(c, msa_launch_merge_ranked(imp.as<u8>(), d_off, d_base, (u32)nblk, n, R.K[2][0].as<u64>(), T,
+                                    R.K[1][0].as<u64>(), R.K[1][1].as<u64>(), R.K[1][2].as<u64>(), R.ref.as<u64>(),
+                                    R.cnt.as<u64>(), R.rank_cnt.as<u32>(), R.order.as<u32>(), R.len.as<u64>(),
+                                    R.off.as<u64>(), R.scan_bsum.as<u64>(), tot, c->stream));
+    u64 blob = 0;
+    HIPC(c, hipMemcpyAsync(c->pin + kPinSmall, tot, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    memcpy(&blob, c->pin + kPinSmall, 8);
+    HIPC(c, ensure(R.blob, blob + 16));
+    HIPC(c, msa_launch_merge_blob(R.order.as<u32>(), n, imp.as<u8>(), R.ref.as<u64>(), R.cnt.as<u64>(),
+                                  R.off.as<u64>(), R.blob.as<u8>(), R.counts.as<u64>(), c->stream));
+    R.n = n;
+    R.blob_len = blob;
+    R.blob_cap = R.blob.cap - 16;
+    R.blob_pending = false;
+    R.host_valid = false;
+    if (art) c->sum.n_artists = n;
+    else c->sum.n_words = n;
+    c->stage = 3;
+    return MSA_OK;
+}
+
 extern "C" int msa_debug_records(msa_ctx *c, uint64_t *rec_start, uint32_t *nulrel, uint64_t cap, uint64_t *n) {
     if (!c || !n) return MSA_ERR_ARG;
     HIPC(c, join_side(c));  // text.csv (side stream) may still read the buffers this touches

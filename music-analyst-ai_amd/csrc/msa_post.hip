@@ -1878,12 +1878,14 @@ __global__ void k_blob_write(const u32 *__restrict__ order, u64 n, const u64 *__
 #define MR_MAXT 64
 #define MR_MAXN ((u64)MR_MAXT * TS_N)
 #define RC_T 1024
+// tiles: [u TS_N, (u + 1) TS_N), or [ts[u], ts[u + 1]) (<= TS_N keys each)
 __global__ __launch_bounds__(RC_T) void k_rank_count(const u64 *__restrict__ K2, const u64 *__restrict__ K1,
-                                                     const u64 *__restrict__ K0, u64 n, u32 *__restrict__ cnt) {
+                                                     const u64 *__restrict__ K0, u64 n, u32 *__restrict__ cnt,
+                                                     const u64 *__restrict__ ts) {
     __shared__ u64 s2[TS_N], s1[TS_N], s0[TS_N];
     const u32 u = blockIdx.x;
-    const u64 ub = (u64)u * TS_N;
-    const u32 un = (u32)min((u64)TS_N, n - ub);
+    const u64 ub = ts ? ts[u] : (u64)u * TS_N;
+    const u32 un = (u32)(ts ? ts[u + 1] - ub : min((u64)TS_N, n - ub));
     for (u32 j = threadIdx.x; j < un; j += RC_T) {
         s2[j] = K2[ub + j];
         s1[j] = K1[ub + j];
@@ -1941,6 +1943,82 @@ __global__ __launch_bounds__(256) void k_rank_place(const u64 *__restrict__ K2, 
     }
     order[less] = v;
     len[less] = entry_key_len(me, a1, a0, l_len, key_len);
+}
+
+// ---------------------------------------------------------------------------
+// Root-GPU merge of ranked partitions (msa_import_ranked): every received
+// block is one GPU's ranked key partition (msa_export_ranked), the blocks'
+// keys are disjoint, so the global ranking is their k-way merge -- no
+// re-insertion and no sort.  Each block is cut into tiles of <= TS_N records
+// (sorted, as the block is), k_rank_count counts per tile, k_mr_place ranks
+// every record (ties on 24 key bytes by the key bytes), k_mr_blob writes the
+// counts and the key blob in rank order.
+//   block: u64 n, u64 blob_bytes, u64 0, u64 0 | n x {u64 count, u32 len,
+//          u32 blob_off, u8 key[16]} | blob (keys in rank order)
+__global__ void k_mr_keys(const u8 *__restrict__ in, const u64 *__restrict__ blk_off, const u64 *__restrict__ rec_base,
+                          u32 nblk, u64 n, u64 *__restrict__ K2, u64 *__restrict__ K1, u64 *__restrict__ K0,
+                          u64 *__restrict__ kptr, u64 *__restrict__ cntv) {
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    u32 lo = 0, hi = nblk;  // block p: rec_base[p] <= i < rec_base[p + 1]
+    while (hi - lo > 1) {
+        const u32 m = (lo + hi) >> 1;
+        if (rec_base[m] <= i) lo = m;
+        else hi = m;
+    }
+    const u64 p0 = blk_off[lo], j = i - rec_base[lo];
+    const u64 nb = rec_base[lo + 1] - rec_base[lo];
+    const u64 *rec = reinterpret_cast<const u64 *>(in + p0 + 32 + 32 * j);
+    const u64 c = rec[0], w = rec[1];
+    const u32 len = (u32)w;
+    const u64 kp = p0 + 32 + 32 * nb + (w >> 32);
+    u64 h, l;
+    be16(in + kp, len, 0, &h, &l);
+    K2[i] = ~c;
+    K1[i] = h;
+    K0[i] = l;
+    kptr[i] = kp | ((u64)len << 40);
+    cntv[i] = c;
+}
+__device__ __forceinline__ int mr_cmp(const u8 *in, u64 a, u64 b) {  // strcmp of two keys (a, b: kptr)
+    const u8 *pa = in + (a & ((1ull << 40) - 1)), *pb = in + (b & ((1ull << 40) - 1));
+    const u64 na = a >> 40, nb = b >> 40, m = na < nb ? na : nb;
+    for (u64 k = 16 < m ? 16 : m; k < m; ++k)
+        if (pa[k] != pb[k]) return pa[k] < pb[k] ? -1 : 1;
+    return na < nb ? -1 : (na > nb ? 1 : 0);
+}
+__global__ void k_mr_place(const u64 *__restrict__ K2, const u64 *__restrict__ K1, const u64 *__restrict__ K0, u64 n,
+                           const u32 *__restrict__ cnt, const u64 *__restrict__ ts, u32 T, const u8 *__restrict__ in,
+                           const u64 *__restrict__ kptr, u32 *__restrict__ order, u64 *__restrict__ len) {
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    u64 less = 0;
+    u32 tie = 0;
+    for (u32 u = 0; u < T; ++u) {
+        const u32 c = cnt[(u64)u * n + i];
+        less += c & 0x7FFFFFFFu;
+        tie |= c;
+    }
+    const u64 a2 = K2[i], a1 = K1[i], a0 = K0[i], me = kptr[i];
+    if (tie & 0x80000000u)  // rare: keys sharing a count and 16 bytes, ordered by their bytes
+        for (u32 u = 0; u < T; ++u)
+            for (u64 j = ts[u] + (cnt[(u64)u * n + i] & 0x7FFFFFFFu);
+                 j < ts[u + 1] && K2[j] == a2 && K1[j] == a1 && K0[j] == a0; ++j)
+                if (j != i && mr_cmp(in, kptr[j], me) < 0) ++less;
+    order[less] = (u32)i;
+    len[less] = me >> 40;
+}
+__global__ void k_mr_blob(const u32 *__restrict__ order, u64 n, const u8 *__restrict__ in, const u64 *__restrict__ kptr,
+                          const u64 *__restrict__ cntv, const u64 *__restrict__ off, u8 *__restrict__ blob,
+                          u64 *__restrict__ counts) {
+    const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const u32 i = order[r];
+    const u64 kp = kptr[i];
+    const u8 *src = in + (kp & ((1ull << 40) - 1));
+    u8 *dst = blob + off[r];
+    for (u64 k = 0; k < (kp >> 40); ++k) dst[k] = src[k];
+    counts[r] = cntv[i];
 }
 
 // ---------------------------------------------------------------------------
@@ -2083,6 +2161,25 @@ hipError_t msa_launch_sort(u64 *const K2[3], u64 *const K1[3], u64 *const K0[3],
     *which = cur;
     return hipGetLastError();
 }
+// Root-GPU merge of ranked blocks (see k_mr_keys).  Scratch: K2/K1/K0,
+// kptr, cntv (n each), cnt (T x n u32), ts (T + 1).  Ends with len / off /
+// total (blob offsets) in rank order; k_mr_blob then writes counts + blob.
+hipError_t msa_launch_merge_ranked(const u8 *in, const u64 *blk_off, const u64 *rec_base, u32 nblk, u64 n,
+                                   const u64 *ts, u32 T, u64 *K2, u64 *K1, u64 *K0, u64 *kptr, u64 *cntv, u32 *cnt,
+                                   u32 *order, u64 *len, u64 *off, u64 *bsum, u64 *total, hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_mr_keys, grid1(n), dim3(256), 0, s, in, blk_off, rec_base, nblk, n, K2, K1, K0, kptr, cntv);
+    hipLaunchKernelGGL(k_rank_count, dim3(T), dim3(RC_T), 0, s, (const u64 *)K2, (const u64 *)K1, (const u64 *)K0, n,
+                       cnt, ts);
+    hipLaunchKernelGGL(k_mr_place, grid1(n), dim3(256), 0, s, (const u64 *)K2, (const u64 *)K1, (const u64 *)K0, n,
+                       (const u32 *)cnt, ts, T, in, (const u64 *)kptr, order, len);
+    return msa_exclusive_scan(len, n, off, bsum, total, s);
+}
+hipError_t msa_launch_merge_blob(const u32 *order, u64 n, const u8 *in, const u64 *kptr, const u64 *cntv,
+                                 const u64 *off, u8 *blob, u64 *counts, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_mr_blob, grid1(n), dim3(256), 0, s, order, n, in, kptr, cntv, off, blob, counts);
+    return hipGetLastError();
+}
 u64 msa_rank_small_max() { return MR_MAXN; }
 u64 msa_rank_small_scratch(u64 n) { return ((n + TS_N - 1) / TS_N) * n * 4; }
 // Small-table ranking: k_tile_sort + k_rank_count + k_rank_place (entry ids
@@ -2096,7 +2193,7 @@ hipError_t msa_launch_rank_small(u64 *const K2[3], u64 *const K1[3], u64 *const 
     if (!n || n > MR_MAXN) return hipErrorInvalidValue;
     const u32 T = (u32)((n + TS_N - 1) / TS_N);
     hipLaunchKernelGGL(k_tile_sort, dim3(T), dim3(TS_T), 0, s, K2[0], K1[0], K0[0], V[0], n, K2[1], K1[1], K0[1], V[1]);
-    hipLaunchKernelGGL(k_rank_count, dim3(T), dim3(RC_T), 0, s, K2[1], K1[1], K0[1], n, cnt);
+    hipLaunchKernelGGL(k_rank_count, dim3(T), dim3(RC_T), 0, s, K2[1], K1[1], K0[1], n, cnt, (const u64 *)nullptr);
     hipLaunchKernelGGL(k_rank_place, grid1(n), dim3(256), 0, s, K2[1], K1[1], K0[1], V[1], n, (const u32 *)cnt, ref,
                        buf, extra, l_pos, l_len, arena, key_off, key_len, order, len);
     return msa_exclusive_scan(len, n, off, bsum, total, s);

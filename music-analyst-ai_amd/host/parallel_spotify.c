@@ -350,11 +350,9 @@ static int gather_ranked(Rank *R, const uint64_t *limit) {
         TRY_T(t->alltoallv(t, sb, send, rb[table], recv), "ranked gather");
         t->release(t, sb);
     }
-    if (t->rank == 0) {
+    if (t->rank == 0)  /* the k-way merge of the ranked, disjoint key partitions */
         for (int table = 0; table < 2; ++table)
-            TRY(msa_import_partitions(R->ctx, table, rb[table], off[table], world), "import ranked");
-        TRY(msa_rank(R->ctx), "rank");
-    }
+            TRY(msa_import_ranked(R->ctx, table, rb[table], off[table], world), "import ranked");
     t->release(t, rb[0]);
     t->release(t, rb[1]);
     return 0;

@@ -42,7 +42,7 @@ EXPORTS = [
     "msa_count", "msa_rank", "msa_run", "msa_get_summary", "msa_get_ranked",
     "msa_write_table_csv", "msa_get_split_column", "msa_set_profiling", "msa_get_profile",
     "msa_set_shard", "msa_piece_size", "msa_shard_function", "msa_shard_head", "msa_segment_copy",
-    "msa_segment_set", "msa_artist_reader_needed", "msa_set_artist_reader", "msa_export_partitions", "msa_export_ranked", "msa_export_copy", "msa_import_partitions",
+    "msa_segment_set", "msa_artist_reader_needed", "msa_set_artist_reader", "msa_export_partitions", "msa_export_ranked", "msa_export_copy", "msa_import_partitions", "msa_import_ranked",
     "msa_wcs_create", "msa_wcs_destroy", "msa_wcs_last_error", "msa_wcs_stream", "msa_wcs_load_csv",
     "msa_wcs_set_table_bits", "msa_wcs_set_delimiter", "msa_wcs_set_quoting", "msa_wcs_set_encoding", "msa_wcs_run", "msa_wcs_get_summary", "msa_wcs_get_csv", "msa_wcs_write_outputs",
     "msa_csvcol_run", "msa_csvcol_header", "msa_csvcol_get",
@@ -150,6 +150,7 @@ def load(path: str = LIB_PATH):
     lib.msa_export_copy.argtypes = [vp, vp]
     lib.msa_export_ranked.argtypes = [vp, i, u64, C.POINTER(u64)]
     lib.msa_import_partitions.argtypes = [vp, i, vp, C.POINTER(u64), i]
+    lib.msa_import_ranked.argtypes = [vp, i, vp, C.POINTER(u64), i]
     lib.msa_set_profiling.argtypes = [vp, i]
     lib.msa_get_profile.argtypes = [vp, C.POINTER(_Profile), i]
     lib.msa_wcs_create.argtypes = [i, C.POINTER(vp)]
@@ -339,6 +340,11 @@ class Context:
     def import_partitions(self, table: int, src_ptr: int, blk_off: List[int]):
         arr = (C.c_uint64 * len(blk_off))(*blk_off)
         self._check(self.lib.msa_import_partitions(self.h, table, C.c_void_p(src_ptr or None), arr, len(blk_off) - 1))
+
+    def import_ranked(self, table: int, src_ptr: int, blk_off: List[int]):
+        """Root of the final gather: merge the GPUs' ranked blocks (msa_import_ranked)."""
+        arr = (C.c_uint64 * len(blk_off))(*blk_off)
+        self._check(self.lib.msa_import_ranked(self.h, table, C.c_void_p(src_ptr or None), arr, len(blk_off) - 1))
 
     def summary(self) -> Summary:
         s = _Summary()

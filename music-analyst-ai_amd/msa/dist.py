@@ -165,9 +165,9 @@ def gather_ranked(ctx, comm: Comm, topk: Optional[int] = None,
                   tables: Sequence[int] = (MSA_TABLE_WORDS, MSA_TABLE_ARTISTS)) -> bool:
     """Device-side final gather: every rank serialises its ranked partition
     (or its top-k) with msa_export_ranked, one all-to-all moves the blocks to
-    rank 0 (RCCL: GPU to GPU), and rank 0 imports their union and ranks it --
-    the key partitions are disjoint, so that is the global ranking (its top-k
-    when each rank sent its own top-k).  Returns True on rank 0, whose context
+    rank 0 (RCCL: GPU to GPU), and rank 0 merges them (msa_import_ranked: a
+    k-way merge of the ranked blocks) -- the key partitions are disjoint, so
+    that is the global ranking (its top-k when each rank sent its own top-k).  Returns True on rank 0, whose context
     then holds the global ranked tables (ctx.ranked / msa_write_table_csv).
     Replaces rank 0's receive + merge of every rank's table
     (parallel_spotify.c:1011-1025) and the final qsort (325-344)."""
@@ -186,6 +186,5 @@ def gather_ranked(ctx, comm: Comm, topk: Optional[int] = None,
         offs = [0]
         for c in recv_counts:
             offs.append(offs[-1] + c)
-        ctx.import_partitions(t, recv.data_ptr(), offs)
-    ctx.rank()
+        ctx.import_ranked(t, recv.data_ptr(), offs)
     return True

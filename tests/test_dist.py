@@ -123,6 +123,10 @@ class FakeCtx:
     def rank(self):
         pass
 
+    def import_ranked(self, table, src, offs):
+        # like msa_import_ranked: the table becomes the merge of the ranked blocks
+        self.import_partitions(table, src, offs)
+
     def ranked(self, table, first=0, count=None):
         r = sorted(self.merged.items(), key=lambda kv: (-kv[1], kv[0]))
         return r[first:first + count] if count else r[first:]

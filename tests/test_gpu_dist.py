@@ -54,7 +54,7 @@ def free_port():
     return p
 
 
-def run_world(tmp_path, data, cuts, csv=None, timeout=240):
+def run_world(tmp_path, data, cuts, csv=None, timeout=240, env_extra=None):
     if csv is None:
         csv = tmp_path / "in.csv"
         csv.write_bytes(data)
@@ -66,7 +66,7 @@ def run_world(tmp_path, data, cuts, csv=None, timeout=240):
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
-                   MSA_PKG=PKG, MSA_CSV=str(csv), MSA_CUTS=json.dumps(cuts), MSA_OUT=out)
+                   MSA_PKG=PKG, MSA_CSV=str(csv), MSA_CUTS=json.dumps(cuts), MSA_OUT=out, **(env_extra or {}))
         procs.append(subprocess.Popen([sys.executable, str(script)], env=env, stdout=subprocess.PIPE,
                                       stderr=subprocess.STDOUT))
     logs = []
@@ -131,6 +131,19 @@ def test_sharded_equals_single_process(msa_mod, tmp_path, world, mode, gen):
     words, artists, tot = run_world(tmp_path, data, cuts)
     exp = expected(tmp_path, data)
     assert tot == {k: exp["metrics"][k] for k in ("total_songs", "total_words")}
+    assert words == exp["word_counts.csv"]
+    assert artists == exp["top_artists.csv"]
+
+
+@pytest.mark.parametrize("merge_max", ["0", "64"])
+def test_sharded_gather_merge_fallback(msa_mod, tmp_path, merge_max):
+    """msa_import_ranked: above its key limit the root imports the ranked blocks
+    as partitions and ranks the table again (0: always; 64: the artists merge,
+    the words do not) -- same bytes as the k-way merge."""
+    data = msa_mod.gen_corpus(4000, mode="highcard", seed=5, vocab=8000)
+    cuts = cuts_for(data, 3, "in_quotes")
+    words, artists, tot = run_world(tmp_path, data, cuts, env_extra={"MSA_MERGE_MAX_KEYS": merge_max})
+    exp = expected(tmp_path, data)
     assert words == exp["word_counts.csv"]
     assert artists == exp["top_artists.csv"]
 
