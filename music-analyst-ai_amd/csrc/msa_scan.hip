@@ -122,7 +122,10 @@ __device__ __forceinline__ u64 pxor_excl64(u64 q) {  // bit j = xor of bits < j
     return x;
 }
 
-__global__ __launch_bounds__(256) void k_chunk_summary(const u8 *__restrict__ buf, u64 seg_begin,
+#ifndef K1_MINW
+#define K1_MINW 5  // min waves per SIMD: 96 VGPRs, 5 waves (4 at 111 VGPRs: 0.362 -> 0.338 ms; 6 and 8 spill: 0.43, 0.89)
+#endif
+__global__ __launch_bounds__(256, K1_MINW) void k_chunk_summary(const u8 *__restrict__ buf, u64 seg_begin,
                                                        u64 seg_end, u32 nchunks,
                                                        ChunkSum *__restrict__ out) {
     const u32 lane = lane_id();
