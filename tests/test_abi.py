@@ -66,3 +66,15 @@ def test_table_csv_format(msa_mod):
     got = msa_mod.table_csv_bytes([(b'a"b', 3), (b"c", 1)], "word")
     assert got == b'word,count\n"a""b",3\n"c",1\n'
     assert msa_mod.table_csv_bytes([(b"x", 2), (b"y", 1)], "artist", limit=1) == b'artist,count\n"x",2\n'
+
+
+def test_cli_bench_mode_arguments(tmp_path):
+    """The C host's bench mode (bench.py --driver chost) refuses a run without
+    a synthetic corpus, before any rank or GPU starts (no GPU needed)."""
+    import subprocess
+
+    cli = os.path.join(PKG, "bin", "parallel_spotify")
+    p = subprocess.run([cli, "-", "--bench-steps", "2", "--output-dir", str(tmp_path / "o")], capture_output=True,
+                       timeout=60)
+    assert p.returncode != 0
+    assert b"--bench-steps needs --synthetic-songs" in p.stderr
