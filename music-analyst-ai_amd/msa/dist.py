@@ -85,8 +85,12 @@ class Comm:
         dist.all_gather(out, t, group=self.group)
         return [bytes(o.cpu().numpy().tobytes()) for o in out]
 
-    def alltoallv(self, send: torch.Tensor, send_counts: List[int]) -> Tuple[torch.Tensor, List[int]]:
-        recv_counts = [row[self.rank] for row in self.all_gather_u64(send_counts)]
+    def alltoallv(self, send: torch.Tensor, send_counts: List[int],
+                  recv_counts: Optional[List[int]] = None) -> Tuple[torch.Tensor, List[int]]:
+        """One all-to-all-v; recv_counts when every rank already knows them
+        (else one all-gather of the send counts first)."""
+        if recv_counts is None:
+            recv_counts = [row[self.rank] for row in self.all_gather_u64(send_counts)]
         recv = torch.empty(max(1, sum(recv_counts)), dtype=torch.uint8, device=self.device)
         if self.world == 1:
             recv[: sum(recv_counts)].copy_(send[: sum(send_counts)])
@@ -113,29 +117,76 @@ def resolve_piece(ctx, comm: Comm, piece: int) -> int:
     """Make this rank's piece start at a record boundary and end with the
     records that began here: returns the number of bytes appended."""
     size = ctx.piece_size(piece)
-    fns = comm.all_gather_bytes(ctx.shard_function(piece))
-    sizes = [row[0] for row in comm.all_gather_u64([size])]
+    # the functions and the sizes in one all-gather
+    got = comm.all_gather_bytes(ctx.shard_function(piece) + size.to_bytes(8, "little"))
+    fns = [g[:-8] for g in got]
+    sizes = [int.from_bytes(g[-8:], "little") for g in got]
     head = ctx.shard_head(piece, fns[:comm.rank], sizes[:comm.rank]) if comm.rank > 0 else 0
     heads = [row[0] for row in comm.all_gather_u64([head])]
-    send_counts, _ = tail_plan(comm.rank, heads, sizes)
+    send_counts, recv_plan = tail_plan(comm.rank, heads, sizes)
     send = torch.empty(max(1, head), dtype=torch.uint8, device=comm.device)
     if sum(send_counts):
         ctx.segment_copy(piece, 0, head, send.data_ptr())
-    recv, recv_counts = comm.alltoallv(send, send_counts)
+    recv, recv_counts = comm.alltoallv(send, send_counts, recv_plan)
     tail = sum(recv_counts)
     ctx.segment_set(piece, head, recv.data_ptr() if tail else 0, tail)
     return tail
 
 
+def _prefix(v: Sequence[int]) -> List[int]:
+    out = [0]
+    for x in v:
+        out.append(out[-1] + x)
+    return out
+
+
+def _split_tables(comm: Comm, recv: torch.Tensor, mine: List[List[int]]) -> List[Tuple[torch.Tensor, List[int]]]:
+    """recv holds, per source rank, its blocks of every table in table order
+    (mine[src][t] bytes each): per table, the sources' blocks made contiguous
+    and their offsets."""
+    src_off = _prefix([sum(m) for m in mine])
+    out = []
+    for t in range(len(mine[0]) if mine else 0):
+        segs, offs = [], [0]
+        for src, m in enumerate(mine):
+            start, n = src_off[src] + sum(m[:t]), m[t]
+            if n:
+                segs.append(recv[start:start + n])
+            offs.append(offs[-1] + n)
+        buf = torch.cat(segs) if len(segs) > 1 else (segs[0] if segs else recv[:1])
+        out.append((buf, offs))
+    comm.sync()  # the library reads these buffers on its own stream
+    return out
+
+
+def merge_tables(ctx, comm: Comm, tables: Sequence[int] = (MSA_TABLE_WORDS, MSA_TABLE_ARTISTS)):
+    """The key-hash partitioned merge of several tables in ONE all-gather (the
+    partition sizes) + ONE all-to-all (every table's partition p to rank p)."""
+    W, me, T = comm.world, comm.rank, len(tables)
+    bufs, parts = [], []
+    for t in tables:
+        pt = ctx.export_partitions(t, W)
+        b = torch.empty(max(1, sum(pt)), dtype=torch.uint8, device=comm.device)
+        ctx.export_copy(b.data_ptr())  # the export buffer is per context: copy before the next table's
+        bufs.append(b)
+        parts.append(pt)
+    offs = [_prefix(pt) for pt in parts]
+    pieces, send_counts = [], []
+    for p in range(W):
+        for ti in range(T):
+            if parts[ti][p]:
+                pieces.append(bufs[ti][offs[ti][p]:offs[ti][p + 1]])
+        send_counts.append(sum(parts[ti][p] for ti in range(T)))
+    send = torch.cat(pieces) if len(pieces) > 1 else (pieces[0] if pieces else bufs[0])
+    sizes = comm.all_gather_u64([parts[ti][p] for ti in range(T) for p in range(W)])
+    mine = [[sizes[src][ti * W + me] for ti in range(T)] for src in range(W)]
+    recv, _ = comm.alltoallv(send, send_counts, [sum(m) for m in mine])
+    for t, (buf, o) in zip(tables, _split_tables(comm, recv, mine)):
+        ctx.import_partitions(t, buf.data_ptr(), o)
+
+
 def merge_table(ctx, comm: Comm, table: int):
-    parts = ctx.export_partitions(table, comm.world)
-    send = torch.empty(max(1, sum(parts)), dtype=torch.uint8, device=comm.device)
-    ctx.export_copy(send.data_ptr())
-    recv, recv_counts = comm.alltoallv(send, parts)
-    offs = [0]
-    for c in recv_counts:
-        offs.append(offs[-1] + c)
-    ctx.import_partitions(table, recv.data_ptr(), offs)
+    merge_tables(ctx, comm, (table,))
 
 
 def run_sharded(ctx, comm: Comm, text_column: bool = True) -> Tuple[int, int]:
@@ -154,8 +205,7 @@ def run_sharded(ctx, comm: Comm, text_column: bool = True) -> Tuple[int, int]:
         ctx.set_artist_reader(False)
     ctx.count()
     s = ctx.summary()
-    merge_table(ctx, comm, MSA_TABLE_WORDS)
-    merge_table(ctx, comm, MSA_TABLE_ARTISTS)
+    merge_tables(ctx, comm, (MSA_TABLE_WORDS, MSA_TABLE_ARTISTS))
     ctx.rank()
     songs, words = comm.all_reduce_sum([s.total_songs, s.total_words])
     return songs, words
@@ -171,20 +221,23 @@ def gather_ranked(ctx, comm: Comm, topk: Optional[int] = None,
     then holds the global ranked tables (ctx.ranked / msa_write_table_csv).
     Replaces rank 0's receive + merge of every rank's table
     (parallel_spotify.c:1011-1025) and the final qsort (325-344)."""
-    got = []
-    for t in tables:
-        nbytes = ctx.export_ranked(t, topk or 0)
-        send = torch.empty(max(1, nbytes), dtype=torch.uint8, device=comm.device)
-        ctx.export_copy(send.data_ptr())
-        counts = [0] * comm.world
-        counts[0] = nbytes
-        recv, recv_counts = comm.alltoallv(send, counts)
-        got.append((t, recv, recv_counts))
+    bufs, nbs = [], []
+    for t in tables:  # every table's block in one all-gather (sizes) + one all-to-all
+        nb = ctx.export_ranked(t, topk or 0)
+        b = torch.empty(max(1, nb), dtype=torch.uint8, device=comm.device)
+        ctx.export_copy(b.data_ptr())
+        bufs.append(b[:nb])
+        nbs.append(nb)
+    pieces = [b for b in bufs if b.numel()]
+    send = torch.cat(pieces) if len(pieces) > 1 else (pieces[0] if pieces else torch.empty(
+        1, dtype=torch.uint8, device=comm.device))
+    sizes = comm.all_gather_u64(nbs)
+    counts = [0] * comm.world
+    counts[0] = sum(nbs)
+    mine = [list(row) for row in sizes] if comm.rank == 0 else [[0] * len(tables) for _ in range(comm.world)]
+    recv, _ = comm.alltoallv(send, counts, [sum(m) for m in mine])
     if comm.rank != 0:
         return False
-    for t, recv, recv_counts in got:
-        offs = [0]
-        for c in recv_counts:
-            offs.append(offs[-1] + c)
-        ctx.import_ranked(t, recv.data_ptr(), offs)
+    for t, (buf, o) in zip(tables, _split_tables(comm, recv, mine)):
+        ctx.import_ranked(t, buf.data_ptr(), o)
     return True

@@ -64,7 +64,7 @@ class FakeCtx:
         self.shard = full[lo:hi]
         self.skip, self.tail = 0, b""
         self.exported = b""
-        self.merged = {}
+        self.counts, self.merged = {}, {}
 
     def piece_size(self, piece):
         return len(self.shard)
@@ -88,12 +88,12 @@ class FakeCtx:
         return self.shard[self.skip:] + self.tail
 
     # merge: a "table" is a dict key -> count, exported as key-hash partitions
-    def set_counts(self, counts):
-        self.counts = counts
+    def set_counts(self, table, counts):
+        self.counts[table] = counts
 
     def export_partitions(self, table, nparts):
         parts = [[] for _ in range(nparts)]
-        for k, c in self.counts.items():
+        for k, c in self.counts[table].items():
             parts[int(hashlib.md5(k).hexdigest(), 16) % nparts].append(
                 len(k).to_bytes(4, "little") + c.to_bytes(8, "little") + k)
         blobs = [b"".join(p) for p in parts]
@@ -111,13 +111,13 @@ class FakeCtx:
     def import_partitions(self, table, src, offs):
         # like msa_import_partitions: the table becomes the union of the blocks
         raw = ctypes.string_at(src, offs[-1]) if offs[-1] else b""
-        self.merged = {}
+        m = self.merged[table] = {}
         i = 0
         while i < len(raw):
             kl = int.from_bytes(raw[i:i + 4], "little")
             c = int.from_bytes(raw[i + 4:i + 12], "little")
             k = raw[i + 12:i + 12 + kl]
-            self.merged[k] = self.merged.get(k, 0) + c
+            m[k] = m.get(k, 0) + c
             i += 12 + kl
 
     def rank(self):
@@ -128,8 +128,15 @@ class FakeCtx:
         self.import_partitions(table, src, offs)
 
     def ranked(self, table, first=0, count=None):
-        r = sorted(self.merged.items(), key=lambda kv: (-kv[1], kv[0]))
+        r = sorted(self.merged[table].items(), key=lambda kv: (-kv[1], kv[0]))
         return r[first:first + count] if count else r[first:]
+
+
+def _count(keys):
+    out = {}
+    for k in keys:
+        out[k] = out.get(k, 0) + 1
+    return out
 
 
 def _worker(rank, world, port, data, cuts, q):
@@ -142,19 +149,17 @@ def _worker(rank, world, port, data, cuts, q):
         seg = ctx.segment()
         # count "records" of this rank's segment and merge them by key
         recs = [seg[a:b] for a, b in zip(record_starts(seg), record_starts(seg)[1:] + [len(seg)])] if seg else []
-        counts = {}
-        for r in recs:
-            counts[r] = counts.get(r, 0) + 1
-        ctx.set_counts(counts)
-        mdist.merge_table(ctx, comm, 0)
-        top = ctx.ranked(0, 0, 3)  # this rank's partition
-        root = mdist.gather_ranked(ctx, comm, tables=(0,))
-        ranked = ctx.ranked(0) if root else None
+        ctx.set_counts(0, _count(recs))
+        ctx.set_counts(1, _count(r.split(b",")[0] for r in recs))  # a second table: first fields
+        mdist.merge_tables(ctx, comm, (0, 1))  # both tables in one exchange
+        top = {t: ctx.ranked(t, 0, 3) for t in (0, 1)}  # this rank's partitions
+        root = mdist.gather_ranked(ctx, comm, tables=(0, 1))
+        ranked = [ctx.ranked(t) for t in (0, 1)] if root else None
         tot = comm.all_reduce_sum([len(recs)])
         # top-k gather: each rank sends its top 3, the root ranks the union
-        ctx.merged = dict(top)
-        mdist.gather_ranked(ctx, comm, topk=3, tables=(0,))
-        top3 = ctx.ranked(0, 0, 3) if root else None
+        ctx.merged = {t: dict(top[t]) for t in (0, 1)}
+        mdist.gather_ranked(ctx, comm, topk=3, tables=(0, 1))
+        top3 = [ctx.ranked(t, 0, 3) for t in (0, 1)] if root else None
         q.put((rank, seg, ranked, tot, top3))
     finally:
         dist.destroy_process_group()
@@ -197,10 +202,8 @@ def test_gloo_world_resolves_and_merges(cuts_kind):
     assert b"".join(res[r][0] for r in range(world)) == data
     whole = [data[a:b] for a, b in zip(record_starts(data), record_starts(data)[1:] + [n])]
     assert res[0][2] == [len(whole)]
-    expect = {}
-    for r in whole:
-        expect[r] = expect.get(r, 0) + 1
-    full = sorted(expect.items(), key=lambda kv: (-kv[1], kv[0]))
-    assert res[0][1] == full
-    assert res[0][3] == full[:3]
+    for t, keys in enumerate((whole, [r.split(b",")[0] for r in whole])):
+        full = sorted(_count(keys).items(), key=lambda kv: (-kv[1], kv[0]))
+        assert res[0][1][t] == full
+        assert res[0][3][t] == full[:3]
     assert all(res[r][1] is None for r in range(1, world))
