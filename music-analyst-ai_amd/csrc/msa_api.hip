@@ -32,6 +32,7 @@ hipError_t msa_launch_rec_spans(const u8 *, const u64 *, const u32 *, u64, u64, 
 hipError_t msa_launch_artist_count(const u64 *, const u32 *, const u64 *, const u64 *, u64, u64 *, u64, u32 *, u64,
                                    Counters *, int, int, ulonglong2 *, u32 *, u32, hipStream_t);
 hipError_t msa_launch_first_end(const u8 *, u64, u32, u32, u64 *, hipStream_t);
+hipError_t msa_launch_quote_parity(const u8 *, u64, u32 *, hipStream_t);
 hipError_t msa_launch_artist_verify(const u8 *, const u64 *, const u32 *, const u64 *, u64, const u64 *, Counters *,
                                     hipStream_t);
 hipError_t msa_launch_long_verify(const u8 *, const u8 *, const u64 *, const u32 *, const u64 *, u64, const u64 *,
@@ -1787,11 +1788,44 @@ int msa_shard_function(msa_ctx *c, int piece, msa_shard_fn *out) {
     u64 len;
     int rc;
     if ((rc = piece_of(c, piece, &base, &len))) return rc;
+    // msa_shard_head reads the earlier pieces' functions for the state at its
+    // first byte: the quote parity p, the carried '\r' cr, and whether a record
+    // starts exactly there (rs == the piece start).  Those depend only on the
+    // piece's quote parity and its last bytes, so the function is built from
+    // one parity reduction (a streaming read) instead of K1 + K2: for input
+    // (p, cr), p' = p ^ q; the last byte b is read with parity p ^ q (b is no
+    // '"' when it matters); cr' = b is an unquoted '\r'; a record starts at
+    // the piece end iff b is an unquoted '\r' or '\n' -- unless the piece is
+    // the single '\n' a carried '\r' swallows.  Record counts, c and z are
+    // left 0 (unused by msa_shard_head).
     Fn f = fn_identity(0);
     if (len) {
-        State init{0, 0, 0, 0, 0, 0}, fin;
-        if ((rc = run_scan_fn(c, base, 0, len, init, &fin, piece ? ST_ARTIST_SUMMARY : ST_CSV_SUMMARY))) return rc;
-        HIPC(c, hipMemcpy(&f, c->small.p, sizeof(Fn), hipMemcpyDeviceToHost));  // k_fn_top's total
+        HIPC(c, ensure(c->small, 4096));
+        u32 *d_q = reinterpret_cast<u32 *>(c->small.as<char>() + 3584);
+        HIPC(c, msa_launch_quote_parity(base, len, d_q, c->stream));
+        u32 q = 0;
+        u8 last = 0;
+        HIPC(c, hipMemcpyAsync(c->pin + kPinSmall, d_q, 4, hipMemcpyDeviceToHost, c->stream));
+        HIPC(c, hipMemcpyAsync(c->pin + kPinSmall + 8, base + len - 1, 1, hipMemcpyDeviceToHost, c->stream));
+        HIPC(c, hipStreamSynchronize(c->stream));
+        memcpy(&q, c->pin + kPinSmall, 4);
+        last = c->pin[kPinSmall + 8];
+        q &= 1u;
+        const bool term_byte = last == '\n' || last == '\r';
+        for (u32 i = 0; i < 3; ++i) {
+            const u32 p_in = i == 1, cr_in = i == 2;
+            FnEnt &e = f.e[i];
+            e.p = p_in ^ q;
+            const bool unquoted = e.p == 0;
+            e.cr = last == '\r' && unquoted;
+            const bool ends = term_byte && unquoted && !(cr_in && len == 1 && last == '\n');
+            e.has = ends;
+            e.nterm = ends;
+            e.rs = ends ? len : 0;
+            e.c = 0;
+            e.z = 0;
+            e.pad = 0;
+        }
     }
     memcpy(out, &f, sizeof f);
     return MSA_OK;

@@ -747,6 +747,40 @@ __global__ __launch_bounds__(64) void k_first_end(const u8 *__restrict__ buf, u6
     if (lane == 0) *out = n;
 }
 
+// Quote parity of a byte range (the boundary resolution of the multi-GPU
+// path needs only the reader state at each shard's end: the parity of its
+// '"' bytes and its last byte, see msa_shard_function).  A streaming read,
+// 16 bytes per lane per step; the unaligned head and tail by byte; one
+// atomic XOR per wave.
+__global__ __launch_bounds__(256) void k_quote_parity(const u8 *__restrict__ buf, u64 n, u32 *__restrict__ out) {
+    const u64 a0 = (16 - ((size_t)buf & 15)) & 15;  // bytes before the first 16-byte boundary
+    const u64 head = a0 < n ? a0 : n;
+    const u64 nv = (n - head) / 16;
+    const uint4 *v = reinterpret_cast<const uint4 *>(buf + head);
+    const u64 tid = (u64)blockIdx.x * blockDim.x + threadIdx.x, nt = (u64)gridDim.x * blockDim.x;
+    u32 par = 0;
+    for (u64 i = tid; i < nv; i += nt) {
+        const uint4 x = v[i];
+        par ^= __popc(k1_eq80(x.x, '"') ^ k1_eq80(x.y, '"') ^ k1_eq80(x.z, '"') ^ k1_eq80(x.w, '"'));
+    }
+    if (tid < head) par ^= buf[tid] == '"';
+    const u64 t0 = head + nv * 16;
+    if (tid < n - t0) par ^= buf[t0 + tid] == '"';
+    par &= 1u;
+    const u64 b = __ballot(par);
+    if (lane_id() == 0 && (__popcll(b) & 1)) atomicXor(out, 1u);
+}
+hipError_t msa_launch_quote_parity(const u8 *buf, u64 n, u32 *out, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(out, 0, 4, s);
+    if (e != hipSuccess || !n) return e;
+    u64 blocks = (n / 16 + 255) / 256;
+    const u64 cap = 2048;  // 8 workgroups per CU of a 256-CU MI355X
+    if (blocks > cap) blocks = cap;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(k_quote_parity, dim3((u32)blocks), dim3(256), 0, s, buf, n, out);
+    return hipGetLastError();
+}
+
 hipError_t msa_launch_first_end(const u8 *buf, u64 n, u32 p, u32 cr, u64 *out, hipStream_t s) {
     hipLaunchKernelGGL(k_first_end, dim3(1), dim3(64), 0, s, buf, n, p, cr, out);
     return hipGetLastError();

@@ -57,98 +57,177 @@ __global__ __launch_bounds__(256) void k_rx_vary(const u64 *__restrict__ K2, con
     }
 }
 
-// th[d * ntiles + tile] = entries of the tile whose digit is d
-__global__ __launch_bounds__(RX_T) void k_rx_hist(const u64 *__restrict__ W, u64 n, u32 shift, u32 ntiles,
-                                                  u64 *__restrict__ th) {
-    __shared__ u32 h[256];
+// ---- one-sweep passes: the digit histograms of every varying byte position
+// are counted once up front (they do not depend on the order), so a pass is
+// ONE kernel: tiles take tickets in order, rank their entries by digit within
+// each wave (ballot multi-split + per-wave running counts in LDS), publish
+// their per-digit counts and look back over earlier tiles' published counts
+// (decoupled look-back, one digit per thread) for their global offsets.
+#define OS_T 512
+#define OS_PER 16
+#define OS_TILE (OS_T * OS_PER)
+#define OS_W (OS_T / 64)
+#define OS_POS 24               // byte positions: K0 bytes 0..7, K1, K2
+#define OS_SPIN_LIMIT (1u << 24)  // polls before a look-back gives up (error, never a hang)
+
+// part[block][pos][digit] = entries of the block's stride with that digit at pos
+__global__ __launch_bounds__(256) void k_os_ghist(const u64 *__restrict__ K0, const u64 *__restrict__ K1,
+                                                  const u64 *__restrict__ K2, u64 n, u32 pmask,
+                                                  u32 *__restrict__ part) {
+    __shared__ u32 h[OS_POS * 256];
     const u32 t = threadIdx.x;
-    h[t] = 0;
+    for (u32 k = t; k < OS_POS * 256; k += 256) h[k] = 0;
     __syncthreads();
-    const u64 base = (u64)blockIdx.x * RX_TILE;
-#pragma unroll 4
-    for (u32 j = 0; j < RX_PER; ++j) {
-        const u64 e = base + (u64)j * RX_T + t;
-        if (e < n) atomicAdd(&h[(u32)(W[e] >> shift) & 0xFFu], 1u);
+    for (u64 i = (u64)blockIdx.x * 256 + t; i < n; i += (u64)gridDim.x * 256) {
+        const u64 w[3] = {(pmask & 0xFFu) ? K0[i] : 0, (pmask & 0xFF00u) ? K1[i] : 0,
+                          (pmask & 0xFF0000u) ? K2[i] : 0};
+#pragma unroll
+        for (u32 p = 0; p < OS_POS; ++p)
+            if ((pmask >> p) & 1u) atomicAdd(&h[p * 256 + ((u32)(w[p >> 3] >> (8 * (p & 7))) & 0xFFu)], 1u);
     }
     __syncthreads();
-    th[(u64)t * ntiles + blockIdx.x] = h[t];
+    for (u32 k = t; k < OS_POS * 256; k += 256) part[(u64)blockIdx.x * (OS_POS * 256) + k] = h[k];
 }
 
-// Stable scatter of one tile by the digit at `shift`; toff = the scanned th.
-__global__ __launch_bounds__(RX_T) void k_rx_scatter(const u64 *__restrict__ W, const u32 *__restrict__ V, u64 n,
-                                                     u32 shift, u32 ntiles, const u64 *__restrict__ toff,
-                                                     u64 *__restrict__ Wo, u32 *__restrict__ Vo) {
-    __shared__ u64 sW[RX_TILE];
-    __shared__ u32 sV[RX_TILE];
-    __shared__ u32 h[256], lstart[256], run[256], wsum[RX_W];
-    __shared__ u32 wcnt[RX_W][256], wpre[RX_W][256];
-    const u32 t = threadIdx.x, lane = lane_id(), w = t >> 6;
-    const u64 lt = (1ull << lane) - 1ull;
-    const u64 base = (u64)blockIdx.x * RX_TILE;
-    h[t] = 0;
-    run[t] = 0;
-    for (u32 k = 0; k < RX_W; ++k) wcnt[k][t] = 0;
+// gstart[pos][d] = entries whose digit at pos is below d (one block per position)
+__global__ __launch_bounds__(256) void k_os_gscan(const u32 *__restrict__ part, u32 nparts,
+                                                  u64 *__restrict__ gstart) {
+    __shared__ u64 c[256];
+    const u32 t = threadIdx.x, p = blockIdx.x;
+    u64 s = 0;
+    for (u32 b = 0; b < nparts; ++b) s += part[(u64)b * (OS_POS * 256) + p * 256 + t];
+    c[t] = s;
     __syncthreads();
-    u64 kw[RX_PER];
-    u32 kv[RX_PER];
+    u64 e = 0;
+    for (u32 k = 0; k < t; ++k) e += c[k];
+    gstart[p * 256 + t] = e;
+}
+
+__device__ __forceinline__ u64 os_pack(u32 epoch, u32 incl, u32 v) {
+    return ((u64)(epoch * 2u + incl) << 32) | v;
+}
+
+// One stable pass by the digit at `shift`.  status: [tile][digit] words
+// (epoch, inclusive?, count), zeroed once per sort; epoch = pass number + 1.
+__global__ __launch_bounds__(OS_T) void k_os_pass(const u64 *__restrict__ W, const u32 *__restrict__ V, u64 n,
+                                                  u32 shift, const u64 *__restrict__ gstart,
+                                                  u64 *__restrict__ status, u32 *__restrict__ ticket, u32 epoch,
+                                                  u32 *__restrict__ err, u64 *__restrict__ Wo,
+                                                  u32 *__restrict__ Vo) {
+    __shared__ u64 sbuf[OS_TILE];
+    __shared__ u32 wcnt[OS_W][256];
+    __shared__ u32 lstart[256], wsum[4], stile;
+    __shared__ u64 gbase[256];
+    const u32 t = threadIdx.x, lane = lane_id(), w = t >> 6;
+    for (u32 k = t; k < OS_W * 256; k += OS_T) (&wcnt[0][0])[k] = 0;
+    if (t == 0) stile = atomicAdd(ticket, 1u);
+    __syncthreads();
+    const u32 tile = stile;
+    const u64 tbase = (u64)tile * OS_TILE;
+    const u64 base = tbase + (u64)w * (OS_PER * 64);
+    u64 kw[OS_PER];
+    u32 kv[OS_PER], lr[OS_PER];
 #pragma unroll
-    for (u32 j = 0; j < RX_PER; ++j) {
-        const u64 e = base + (u64)j * RX_T + t;
+    for (u32 j = 0; j < OS_PER; ++j) {
+        const u64 e = base + (u64)j * 64 + lane;
         kw[j] = e < n ? W[e] : 0;
         kv[j] = e < n ? V[e] : 0;
-        if (e < n) atomicAdd(&h[(u32)(kw[j] >> shift) & 0xFFu], 1u);
     }
-    __syncthreads();
-    {  // lstart = exclusive scan of h (256 digits: 4 waves of 64)
-        const u32 x = h[t];
-        u32 tot;
-        const u32 pre = wave_prefix<13>(x, tot);
-        if (lane == 0) wsum[w] = tot;
-        __syncthreads();
-        u32 add = 0;
-        for (u32 k = 0; k < w; ++k) add += wsum[k];
-        lstart[t] = pre + add;
-    }
-    __syncthreads();
+    // rank within the wave: lanes of a round with the same digit (8 ballots),
+    // after the wave's earlier rounds (running count per digit in LDS; a wave's
+    // LDS reads and writes execute in order)
 #pragma unroll
-    for (u32 j = 0; j < RX_PER; ++j) {
-        const u64 e = base + (u64)j * RX_T + t;
-        const bool ok = e < n;
+    for (u32 j = 0; j < OS_PER; ++j) {
+        const bool ok = base + (u64)j * 64 + lane < n;
         const u32 d = (u32)(kw[j] >> shift) & 0xFFu;
-        // lanes holding the same digit (multi-split by ballots)
         u64 M = __ballot(ok);
 #pragma unroll
         for (u32 b = 0; b < 8; ++b) {
             const u64 B = __ballot((d >> b) & 1u);
             M &= ((d >> b) & 1u) ? B : ~B;
         }
-        const u32 rank = (u32)__popcll(M & lt);
-        if (ok && rank == 0) wcnt[w][d] = (u32)__popcll(M);
-        __syncthreads();
-        {  // per digit: earlier waves of this round, after earlier rounds
-            u32 b0 = run[t];
-            for (u32 k = 0; k < RX_W; ++k) {
-                wpre[k][t] = b0;
-                b0 += wcnt[k][t];
-                wcnt[k][t] = 0;
-            }
-            run[t] = b0;
+        const u32 r = mbcnt(M);
+        const u32 pre = ok ? wcnt[w][d] : 0u;
+        lr[j] = pre + r;
+        if (ok && r == 0) wcnt[w][d] = pre + (u32)__popcll(M);
+    }
+    __syncthreads();
+    u32 h = 0, pre = 0;
+    if (t < 256) {
+        for (u32 k = 0; k < OS_W; ++k) {  // per digit: wave offsets within the tile
+            const u32 c = wcnt[k][t];
+            wcnt[k][t] = h;
+            h += c;
         }
-        __syncthreads();
-        if (ok) {
-            const u32 pos = lstart[d] + wpre[w][d] + rank;
-            sW[pos] = kw[j];
-            sV[pos] = kv[j];
+        u64 *st = status + (u64)tile * 256 + t;
+        u64 excl = 0;
+        if (tile == 0) {
+            __hip_atomic_store(st, os_pack(epoch, 1, h), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            __hip_atomic_store(st, os_pack(epoch, 0, h), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            u64 q = tile - 1;
+            u32 spins = 0;
+            for (;;) {
+                const u64 sv =
+                    __hip_atomic_load(status + q * 256 + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const u32 hi = (u32)(sv >> 32);
+                if ((hi >> 1) != epoch) {  // not published yet in this pass
+                    if (++spins > OS_SPIN_LIMIT) {
+                        atomicOr(err, 1u);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                excl += (u32)sv;
+                if ((hi & 1u) || q == 0) break;
+                --q;
+            }
+            __hip_atomic_store(st, os_pack(epoch, 1, (u32)(excl + h)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        gbase[t] = gstart[t] + excl;
+        u32 tot;
+        pre = wave_prefix<14>(h, tot);
+        if (lane == 0) wsum[w] = tot;
+    }
+    __syncthreads();
+    if (t < 256) {
+        u32 add = 0;
+        for (u32 k = 0; k < w; ++k) add += wsum[k];
+        lstart[t] = pre + add;
+    }
+    __syncthreads();
+#pragma unroll
+    for (u32 j = 0; j < OS_PER; ++j) {
+        if (base + (u64)j * 64 + lane < n) {
+            const u32 d = (u32)(kw[j] >> shift) & 0xFFu;
+            lr[j] += lstart[d] + wcnt[w][d];
+            sbuf[lr[j]] = kw[j];
         }
     }
     __syncthreads();
-    const u32 cnt = (u32)min((u64)RX_TILE, n - base);
-    for (u32 i = t; i < cnt; i += RX_T) {
-        const u64 x = sW[i];
-        const u32 d = (u32)(x >> shift) & 0xFFu;
-        const u64 g = toff[(u64)d * ntiles + blockIdx.x] + (i - lstart[d]);
-        Wo[g] = x;
-        Vo[g] = sV[i];
+    const u32 cnt = (u32)min((u64)OS_TILE, n - tbase);
+    u32 g[OS_PER];
+#pragma unroll
+    for (u32 k = 0; k < OS_PER; ++k) {
+        const u32 i = t + k * OS_T;
+        if (i < cnt) {
+            const u64 x = sbuf[i];
+            const u32 d = (u32)(x >> shift) & 0xFFu;
+            g[k] = (u32)(gbase[d] + (i - lstart[d]));
+            Wo[g[k]] = x;
+        }
+    }
+    __syncthreads();
+    u32 *sv = reinterpret_cast<u32 *>(sbuf);
+#pragma unroll
+    for (u32 j = 0; j < OS_PER; ++j)
+        if (base + (u64)j * 64 + lane < n) sv[lr[j]] = kv[j];
+    __syncthreads();
+#pragma unroll
+    for (u32 k = 0; k < OS_PER; ++k) {
+        const u32 i = t + k * OS_T;
+        if (i < cnt) Vo[g[k]] = sv[i];
     }
 }
 
@@ -171,13 +250,14 @@ __global__ void k_rx_final(const u64 *__restrict__ K2, const u64 *__restrict__ K
 }
 
 inline dim3 g1(u64 n, u32 t = 256) { return dim3((u32)((n + t - 1) / t)); }
-inline u64 rx_tiles(u64 n) { return (n + RX_TILE - 1) / RX_TILE; }
+inline u64 os_tiles(u64 n) { return (n + OS_TILE - 1) / OS_TILE; }
+inline u32 os_parts(u64 n) { return (u32)std::max<u64>(1, std::min<u64>(512, (n + 4095) / 4096)); }
 
 }  // namespace
 
+// vary (64 B) | tickets + error word (256 B) | gstart | part | status
 u64 msa_radix_scratch_bytes(u64 n) {
-    const u64 m = 256 * rx_tiles(n);
-    return 64 + 2 * m * 8 + ((m + 1023) / 1024 + 1) * 8 + 64;
+    return 64 + 256 + (u64)OS_POS * 256 * 8 + (u64)os_parts(n) * OS_POS * 256 * 4 + os_tiles(n) * 256 * 8 + 64;
 }
 
 // Sorts set 0 (K2, K1, K0, V: the entries, V[0][i] = i) ascending; the result
@@ -187,22 +267,37 @@ hipError_t msa_radix_sort(u64 *const K2[3], u64 *const K1[3], u64 *const K0[3], 
                           u8 *scratch, hipStream_t s) {
     *which = 1;
     if (!n) return hipSuccess;
-    const u64 ntiles = rx_tiles(n), m = 256 * ntiles;
+    if (n >= (1ull << 32)) return hipErrorInvalidValue;  // u32 indices and counts
+    const u64 ntiles = os_tiles(n);
+    const u32 nparts = os_parts(n);
     u64 *vary = reinterpret_cast<u64 *>(scratch);
-    u64 *th = vary + 8, *toff = th + m, *bsum = toff + m, *total = bsum + (m + 1023) / 1024 + 1;
+    u32 *tickets = reinterpret_cast<u32 *>(scratch + 64), *err = tickets + 63;
+    u64 *gstart = reinterpret_cast<u64 *>(scratch + 64 + 256);
+    u32 *part = reinterpret_cast<u32 *>(gstart + OS_POS * 256);
+    u64 *status = reinterpret_cast<u64 *>(part + (u64)nparts * OS_POS * 256);
     hipError_t e;
-    if ((e = hipMemsetAsync(vary, 0, 64, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(scratch, 0, 64 + 256, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(status, 0, ntiles * 256 * 8, s)) != hipSuccess) return e;
     hipLaunchKernelGGL(k_rx_vary, dim3((u32)std::min<u64>(1024, (n + 255) / 256)), dim3(256), 0, s, K2[0], K1[0],
                        K0[0], n, vary);
     u64 hv[3];
     if ((e = hipMemcpyAsync(hv, vary, sizeof hv, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
     if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+    u32 pmask = 0;
+    for (int wi = 0; wi < 3; ++wi)
+        for (u32 b = 0; b < 8; ++b)
+            if ((hv[wi] >> (8 * b)) & 0xFFull) pmask |= 1u << (wi * 8 + b);
+    if (pmask) {
+        hipLaunchKernelGGL(k_os_ghist, dim3(nparts), dim3(256), 0, s, K0[0], K1[0], K2[0], n, pmask, part);
+        hipLaunchKernelGGL(k_os_gscan, dim3(OS_POS), dim3(256), 0, s, (const u32 *)part, nparts, gstart);
+    }
 
     const u64 *orig[3] = {K0[0], K1[0], K2[0]};  // least significant word first
     u64 *Wb[3] = {nullptr, K0[1], K0[2]};
     const u64 *Wp = nullptr;
     int vloc = 0;
     bool any = false;
+    u32 pass = 0;
     for (int wi = 0; wi < 3; ++wi) {
         if (!hv[wi]) continue;
         if (!any) {
@@ -216,10 +311,10 @@ hipError_t msa_radix_sort(u64 *const K2[3], u64 *const K1[3], u64 *const K0[3], 
         for (u32 b = 0; b < 8; ++b) {
             if (!((hv[wi] >> (8 * b)) & 0xFFull)) continue;  // the same byte in every entry
             const int dst = (vloc == 1 || Wp == Wb[1]) ? 2 : 1;
-            hipLaunchKernelGGL(k_rx_hist, dim3((u32)ntiles), dim3(RX_T), 0, s, Wp, n, 8 * b, (u32)ntiles, th);
-            if ((e = msa_exclusive_scan(th, m, toff, bsum, total, s)) != hipSuccess) return e;
-            hipLaunchKernelGGL(k_rx_scatter, dim3((u32)ntiles), dim3(RX_T), 0, s, Wp, (const u32 *)V[vloc], n, 8 * b,
-                               (u32)ntiles, (const u64 *)toff, Wb[dst], V[dst]);
+            hipLaunchKernelGGL(k_os_pass, dim3((u32)ntiles), dim3(OS_T), 0, s, Wp, (const u32 *)V[vloc], n, 8 * b,
+                               (const u64 *)(gstart + (wi * 8 + b) * 256), status, tickets + pass, pass + 1, err,
+                               Wb[dst], V[dst]);
+            ++pass;
             vloc = dst;
             Wp = Wb[dst];
         }
@@ -228,5 +323,9 @@ hipError_t msa_radix_sort(u64 *const K2[3], u64 *const K1[3], u64 *const K0[3], 
     hipLaunchKernelGGL(k_rx_final, g1(n), dim3(256), 0, s, K2[0], K1[0], K0[0], (const u32 *)V[vloc], n, K2[o], K1[o],
                        K0[o], V[o]);
     *which = o;
-    return hipGetLastError();
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    u32 herr = 0;  // a look-back that gave up (never expected: tiles take tickets in order)
+    if ((e = hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+    return herr ? hipErrorLaunchFailure : hipSuccess;
 }
