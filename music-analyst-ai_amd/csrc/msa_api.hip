@@ -74,7 +74,7 @@ hipError_t msa_launch_rank_small(u64 *const[3], u64 *const[3], u64 *const[3], u3
                                  const u32 *, u32 *, u64 *, u64 *, u64 *, u64 *, u32 *, hipStream_t);
 hipError_t msa_launch_blob(const u32 *, u64, const u64 *, const u64 *, const u64 *, const u64 *, const u8 *,
                            const u8 *, const u64 *, const u32 *, const u8 *, const u64 *, const u32 *, u64 *, u64 *, u64 *, u64 *,
-                           u8 *, u64 *, u64, hipStream_t, int);
+                           u8 *, u64 *, u64, hipStream_t, int, const u64 *, const u64 *, const u64 *, u64);
 
 // ---------------------------------------------------------------------------
 namespace {
@@ -94,6 +94,8 @@ struct BlobArgs {  // key sources of the last blob pass (for a rewrite after gro
     const u8 *wbuf, *wextra, *arena;
     const u64 *key_off;
     const u32 *key_len;
+    const u64 *ks2, *ks1, *ks0;  // the sorted key planes (null: read the keys through order)
+    u64 lthr;                    // entries below: S/M words (the key is K1/K0)
 };
 struct Ranked {
     DevBuf K[3][3];  // [set][k2,k1,k0]: set 0 = input, 1/2 = ping-pong
@@ -102,6 +104,7 @@ struct Ranked {
     DevBuf scan_bsum, scan_total;  // the blob offsets' scan scratch (the two tables rank concurrently)
     DevBuf rank_cnt;               // the small-table ranking's per-tile counts
     u64 n = 0, blob_len = 0, blob_cap = 0;
+    u64 lthr = 0;  // words: entries [0, lthr) are S/M keys (k_word_entries' order)
     bool blob_pending = false;  // blob_len not read back yet (do_rank's sync)
     BlobArgs pending{};
     std::vector<u64> h_counts, h_off;
@@ -1340,18 +1343,22 @@ static int sort_and_blob(msa_ctx *c, Ranked &R, const u8 *wbuf, const u8 *wextra
     HIPC(c, ensure(R.counts, n * 8));
     HIPC(c, ensure(R.scan_total, 64));
     HIPC(c, ensure(R.scan_bsum, ((n + 1023) / 1024 + 1) * 8));
+    // after a full sort, rank i's key planes are R.K[cur][*][i] (read in order)
+    const u64 *ks2 = lens_done ? nullptr : R.K[cur][0].as<u64>();
+    const u64 *ks1 = lens_done ? nullptr : R.K[cur][1].as<u64>();
+    const u64 *ks0 = lens_done ? nullptr : R.K[cur][2].as<u64>();
     if (!lens_done)
         HIPC(c, msa_launch_blob(R.order.as<u32>(), n, R.ref.as<u64>(), R.K[0][1].as<u64>(), R.K[0][2].as<u64>(),
                                 R.cnt.as<u64>(), wbuf, wextra, c->l_pos.as<u64>(), c->l_len.as<u32>(), arena, key_off,
                                 key_len, R.len.as<u64>(), R.off.as<u64>(), R.scan_bsum.as<u64>(),
-                                c->blob_tot.as<u64>() + slot, nullptr, nullptr, 0, st, 0));
+                                c->blob_tot.as<u64>() + slot, nullptr, nullptr, 0, st, 0, ks2, ks1, ks0, R.lthr));
     HIPC(c, ensure(R.blob, std::max<u64>(est, R.blob_len) + 16));
     R.blob_cap = R.blob.cap - 16;
     HIPC(c, msa_launch_blob(R.order.as<u32>(), n, R.ref.as<u64>(), R.K[0][1].as<u64>(), R.K[0][2].as<u64>(),
                             R.cnt.as<u64>(), wbuf, wextra, c->l_pos.as<u64>(), c->l_len.as<u32>(), arena, key_off, key_len,
                             R.len.as<u64>(), R.off.as<u64>(), R.scan_bsum.as<u64>(), R.scan_total.as<u64>(),
-                            R.blob.as<u8>(), R.counts.as<u64>(), R.blob_cap, st, 1));
-    R.pending = BlobArgs{wbuf, wextra, arena, key_off, key_len};
+                            R.blob.as<u8>(), R.counts.as<u64>(), R.blob_cap, st, 1, ks2, ks1, ks0, R.lthr));
+    R.pending = BlobArgs{wbuf, wextra, arena, key_off, key_len, ks2, ks1, ks0, R.lthr};
     return MSA_OK;
 }
 
@@ -1363,7 +1370,10 @@ static int do_rank(msa_ctx *c, int tables = 3) {
     // words
     Ranked &W = c->rw;
     const bool dw = (tables & 1) != 0, da = (tables & 2) != 0;
-    if (dw) W.n = c->sum.n_words;
+    if (dw) {
+        W.n = c->sum.n_words;
+        W.lthr = c->h_ctr.s_claimed + c->h_ctr.m_claimed;
+    }
     prof_begin(c, ST_RANK_WORDS);
     if (dw && W.n) {
         for (int k = 0; k < 3; ++k) HIPC(c, ensure(W.K[0][k], W.n * 8));
@@ -1449,7 +1459,7 @@ static int do_rank(msa_ctx *c, int tables = 3) {
                                 R.cnt.as<u64>(), b.wbuf, b.wextra, c->l_pos.as<u64>(), c->l_len.as<u32>(), b.arena,
                                 b.key_off, b.key_len, R.len.as<u64>(), R.off.as<u64>(), R.scan_bsum.as<u64>(),
                                 R.scan_total.as<u64>(), R.blob.as<u8>(), R.counts.as<u64>(), R.blob_cap, c->stream,
-                                1));
+                                1, b.ks2, b.ks1, b.ks0, b.lthr));
         again = true;
     }
     if (again) HIPC(c, hipStreamSynchronize(c->stream));

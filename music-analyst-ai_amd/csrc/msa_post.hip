@@ -1820,28 +1820,49 @@ __device__ __forceinline__ u64 entry_key_len(u64 ref, u64 k1, u64 k0, const u32 
     return n;
 }
 
+// SortedKeys: the sorted (K2, K1, K0) planes, position i = rank i (entries tied
+// on all 24 bytes share them, so the tie order does not matter); entries below
+// `lthr` are S/M words whose K1/K0 are the whole key.  Those need no random
+// reads of ref/K/cnt: only the long words' and artists' keys do.
+struct SortedKeys {
+    const u64 *K2, *K1, *K0;
+    u64 lthr;
+};
+
 __global__ void k_blob_len(const u32 *__restrict__ order, u64 n, const u64 *__restrict__ ref,
                            const u64 *__restrict__ K1u, const u64 *__restrict__ K0u, const u32 *l_len,
-                           const u32 *key_len, u64 *__restrict__ len) {
+                           const u32 *key_len, SortedKeys sk, u64 *__restrict__ len) {
     const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const u32 e = order[i];
-    len[i] = entry_key_len(ref[e], K1u[e], K0u[e], l_len, key_len);
+    len[i] = e < sk.lthr ? entry_key_len((u64)KIND_S << 60, sk.K1[i], sk.K0[i], l_len, key_len)
+                         : entry_key_len(ref[e], K1u[e], K0u[e], l_len, key_len);
 }
 
 __global__ void k_blob_write(const u32 *__restrict__ order, u64 n, const u64 *__restrict__ ref,
                              const u64 *__restrict__ K1u, const u64 *__restrict__ K0u, const u64 *__restrict__ cnt,
                              const u8 *buf, const u8 *extra, const u64 *l_pos, const u32 *l_len, const u8 *arena,
                              const u64 *key_off, const u32 *key_len, const u64 *__restrict__ off,
-                             const u64 *__restrict__ len, u8 *__restrict__ blob, u64 *__restrict__ counts_out,
-                             u64 blob_cap) {
+                             const u64 *__restrict__ len, SortedKeys sk, u8 *__restrict__ blob,
+                             u64 *__restrict__ counts_out, u64 blob_cap) {
     const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const u32 e = order[i];
+    counts_out[i] = sk.K2 ? ~sk.K2[i] : cnt[e];
+    if (off[i] + len[i] > blob_cap) return;
+    if (e < sk.lthr) {  // S/M word: the key is the sorted K1/K0
+        u8 *dst = blob + off[i];
+        const u64 k1 = sk.K1[i], k0 = sk.K0[i];
+        for (int k = 0; k < 16; ++k) {
+            const u8 b = (u8)((k < 8 ? k1 : k0) >> (56 - 8 * (k & 7)));
+            if (!b) break;
+            dst[k] = b;
+        }
+        return;
+    }
     const u64 r = ref[e];
     const u32 kind = (u32)(r >> 60);
     const u64 idx = r & ((1ull << 60) - 1);
-    counts_out[i] = cnt[e];
     // the blob was sized before its length came back to the host: a key that
     // does not fit is skipped (the host sees the total, grows the blob and
     // writes it again)
@@ -2209,14 +2230,16 @@ hipError_t msa_launch_fixup(const u64 *K2, const u64 *K1, const u64 *K0, const u
 hipError_t msa_launch_blob(const u32 *order, u64 n, const u64 *ref, const u64 *K1u, const u64 *K0u, const u64 *cnt,
                            const u8 *buf, const u8 *extra, const u64 *l_pos, const u32 *l_len, const u8 *arena, const u64 *key_off,
                            const u32 *key_len, u64 *len, u64 *off, u64 *bsum, u64 *total, u8 *blob, u64 *counts_out,
-                           u64 blob_cap, hipStream_t s, int phase) {
+                           u64 blob_cap, hipStream_t s, int phase, const u64 *Ks2, const u64 *Ks1, const u64 *Ks0,
+                           u64 lthr) {
     if (!n) return hipSuccess;
+    const SortedKeys sk{Ks2, Ks1, Ks0, Ks1 ? lthr : 0};
     if (phase == 0) {
-        hipLaunchKernelGGL(k_blob_len, grid1(n), dim3(256), 0, s, order, n, ref, K1u, K0u, l_len, key_len, len);
+        hipLaunchKernelGGL(k_blob_len, grid1(n), dim3(256), 0, s, order, n, ref, K1u, K0u, l_len, key_len, sk, len);
         return msa_exclusive_scan(len, n, off, bsum, total, s);
     }
     hipLaunchKernelGGL(k_blob_write, grid1(n), dim3(256), 0, s, order, n, ref, K1u, K0u, cnt, buf, extra, l_pos, l_len, arena,
-                       key_off, key_len, (const u64 *)off, (const u64 *)len, blob, counts_out, blob_cap);
+                       key_off, key_len, (const u64 *)off, (const u64 *)len, sk, blob, counts_out, blob_cap);
     return hipGetLastError();
 }
 

@@ -81,9 +81,20 @@ __global__ __launch_bounds__(256) void k_os_ghist(const u64 *__restrict__ K0, co
     for (u64 i = (u64)blockIdx.x * 256 + t; i < n; i += (u64)gridDim.x * 256) {
         const u64 w[3] = {(pmask & 0xFFu) ? K0[i] : 0, (pmask & 0xFF00u) ? K1[i] : 0,
                           (pmask & 0xFF0000u) ? K2[i] : 0};
+        const u64 act = __ballot(1);
 #pragma unroll
-        for (u32 p = 0; p < OS_POS; ++p)
-            if ((pmask >> p) & 1u) atomicAdd(&h[p * 256 + ((u32)(w[p >> 3] >> (8 * (p & 7))) & 0xFFu)], 1u);
+        for (u32 p = 0; p < OS_POS; ++p) {
+            if (!((pmask >> p) & 1u)) continue;
+            const u32 d = (u32)(w[p >> 3] >> (8 * (p & 7))) & 0xFFu;
+            // a digit the whole wave shares (zero padding of short keys, the
+            // high bytes of small counts): one add instead of a 64-way conflict
+            const u32 d0 = __builtin_amdgcn_readfirstlane(d);
+            if (__ballot(d == d0) == act) {
+                if (mbcnt(act) == 0) atomicAdd(&h[p * 256 + d0], (u32)__popcll(act));
+            } else {
+                atomicAdd(&h[p * 256 + d], 1u);
+            }
+        }
     }
     __syncthreads();
     for (u32 k = t; k < OS_POS * 256; k += 256) part[(u64)blockIdx.x * (OS_POS * 256) + k] = h[k];
@@ -237,15 +248,17 @@ __global__ void k_rx_gather(const u64 *__restrict__ src, const u32 *__restrict__
     if (i < n) out[i] = src[V[i]];
 }
 
+// the sorted entries; word `wsel` (0 = K0 .. 2 = K2; 3 = none) is already in
+// order in Ws (the last sorted word), the others are gathered through V
 __global__ void k_rx_final(const u64 *__restrict__ K2, const u64 *__restrict__ K1, const u64 *__restrict__ K0,
-                           const u32 *__restrict__ V, u64 n, u64 *__restrict__ O2, u64 *__restrict__ O1,
-                           u64 *__restrict__ O0, u32 *__restrict__ OV) {
+                           const u32 *__restrict__ V, u64 n, const u64 *__restrict__ Ws, u32 wsel,
+                           u64 *__restrict__ O2, u64 *__restrict__ O1, u64 *__restrict__ O0, u32 *__restrict__ OV) {
     const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const u32 v = V[i];
-    O2[i] = K2[v];
-    O1[i] = K1[v];
-    O0[i] = K0[v];
+    O2[i] = wsel == 2 ? Ws[i] : K2[v];
+    O1[i] = wsel == 1 ? Ws[i] : K1[v];
+    O0[i] = wsel == 0 ? Ws[i] : K0[v];
     OV[i] = v;
 }
 
@@ -297,7 +310,7 @@ hipError_t msa_radix_sort(u64 *const K2[3], u64 *const K1[3], u64 *const K0[3], 
     const u64 *Wp = nullptr;
     int vloc = 0;
     bool any = false;
-    u32 pass = 0;
+    u32 pass = 0, wsel = 3;
     for (int wi = 0; wi < 3; ++wi) {
         if (!hv[wi]) continue;
         if (!any) {
@@ -308,6 +321,7 @@ hipError_t msa_radix_sort(u64 *const K2[3], u64 *const K1[3], u64 *const K0[3], 
             Wp = dst;
         }
         any = true;
+        wsel = (u32)wi;
         for (u32 b = 0; b < 8; ++b) {
             if (!((hv[wi] >> (8 * b)) & 0xFFull)) continue;  // the same byte in every entry
             const int dst = (vloc == 1 || Wp == Wb[1]) ? 2 : 1;
@@ -320,8 +334,10 @@ hipError_t msa_radix_sort(u64 *const K2[3], u64 *const K1[3], u64 *const K0[3], 
         }
     }
     const int o = vloc == 1 ? 2 : 1;
-    hipLaunchKernelGGL(k_rx_final, g1(n), dim3(256), 0, s, K2[0], K1[0], K0[0], (const u32 *)V[vloc], n, K2[o], K1[o],
-                       K0[o], V[o]);
+    // Wp: the last sorted word in order (unless it was gathered into set o's K0 buffer)
+    if (wsel < 3 && Wp == K0[o]) wsel = 3;
+    hipLaunchKernelGGL(k_rx_final, g1(n), dim3(256), 0, s, K2[0], K1[0], K0[0], (const u32 *)V[vloc], n, Wp, wsel,
+                       K2[o], K1[o], K0[o], V[o]);
     *which = o;
     if ((e = hipGetLastError()) != hipSuccess) return e;
     u32 herr = 0;  // a look-back that gave up (never expected: tiles take tickets in order)
