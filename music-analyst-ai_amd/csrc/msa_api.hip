@@ -1501,8 +1501,21 @@ int msa_create(int device, msa_ctx **out) {
         if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
             c->cus = prop.multiProcessorCount;
     }
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
+    // MSA_SIDE_FREE=N (experiment): the side stream (text.csv's gather) is kept
+    // off every CU i with i % N == N - 1, so the ranking chain beside it finds
+    // free CUs instead of waiting for the gather's workgroups to drain
+    int side_free = 0;
+    if (const char *sf = getenv("MSA_SIDE_FREE")) side_free = atoi(sf);
+    hipError_t side_e;
+    if (side_free > 1 && c->cus > 0) {
+        std::vector<uint32_t> mask((c->cus + 31) / 32, 0u);
+        for (int i = 0; i < c->cus; ++i)
+            if (i % side_free != side_free - 1) mask[i / 32] |= 1u << (i % 32);
+        side_e = hipExtStreamCreateWithCUMask(&c->side, (uint32_t)mask.size(), mask.data());
+    } else {
+        side_e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
+    }
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess || side_e != hipSuccess ||
         hipStreamCreateWithFlags(&c->rank2, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_r2_fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_r2_join, hipEventDisableTiming) != hipSuccess ||

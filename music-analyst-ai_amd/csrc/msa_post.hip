@@ -1966,6 +1966,115 @@ __global__ __launch_bounds__(256) void k_rank_place(const u64 *__restrict__ K2, 
     len[less] = entry_key_len(me, a1, a0, l_len, key_len);
 }
 
+// The small-table path's count in one sum per key (k_rank_total + k_rank_put):
+// workgroup u keeps tile u's keys in registers (thread = key) and streams every
+// tile v through LDS -- double-buffered, the next tile's coalesced loads in
+// flight while the current one is searched -- counting the smaller keys of all
+// tiles in a register.  Beside the text column's gather every dependent L2 miss
+// of k_rank_count's per-key loads waited behind the gather's traffic (386 us
+// for 33 K words against ~0.1 ms alone); here each workgroup issues T bulk
+// tile loads, each one tile ahead.  cnt[i] = smaller keys | 1 << 31 when an
+// equal key (all 24 bytes) exists elsewhere.
+// Small workgroups (RT_T threads, RT_T keys, one 24 KiB tile buffer in LDS,
+// the next tile held in registers): the gather's workgroups fill every CU, and
+// a workgroup of this size fits in what one finished gather workgroup frees.
+#ifndef RC_TOT
+#define RC_TOT 1
+#endif
+#ifndef RT_T
+#define RT_T 256
+#endif
+#define RT_K (TS_N / RT_T)  // tile elements per thread
+__global__ __launch_bounds__(RT_T) void k_rank_total(const u64 *__restrict__ K2, const u64 *__restrict__ K1,
+                                                     const u64 *__restrict__ K0, u64 n, u32 *__restrict__ cnt) {
+    __shared__ u64 s2[TS_N], s1[TS_N], s0[TS_N];
+    const u32 T = (u32)((n + TS_N - 1) / TS_N);
+    const u32 t = threadIdx.x;
+    const u32 u = blockIdx.x / RT_K;                     // the keys' tile
+    const u32 j = (blockIdx.x % RT_K) * RT_T + t;        // the key's place in it
+    const u64 i = (u64)u * TS_N + j;
+    const bool mine = i < n;
+    u64 a2 = 0, a1 = 0, a0 = 0;
+    if (mine) { a2 = K2[i]; a1 = K1[i]; a0 = K0[i]; }
+    u64 p2[RT_K], p1[RT_K], p0[RT_K];
+#pragma unroll
+    for (int k = 0; k < RT_K; ++k) {
+        const u64 e = (u64)k * RT_T + t;
+        p2[k] = p1[k] = p0[k] = 0;
+        if (e < n) { p2[k] = K2[e]; p1[k] = K1[e]; p0[k] = K0[e]; }
+    }
+    u32 less = 0;
+    bool tie = false;
+    for (u32 v = 0; v < T; ++v) {
+#pragma unroll
+        for (int k = 0; k < RT_K; ++k) {
+            s2[k * RT_T + t] = p2[k];
+            s1[k * RT_T + t] = p1[k];
+            s0[k * RT_T + t] = p0[k];
+        }
+        __syncthreads();
+        if (v + 1 < T) {  // the next tile's loads in flight during the search
+#pragma unroll
+            for (int k = 0; k < RT_K; ++k) {
+                const u64 e = (u64)(v + 1) * TS_N + (u64)k * RT_T + t;
+                if (e < n) { p2[k] = K2[e]; p1[k] = K1[e]; p0[k] = K0[e]; }
+            }
+        }
+        const u32 un = (u32)min((u64)TS_N, n - (u64)v * TS_N);
+        if (mine) {
+            u32 lo = 0, hi = un;  // first key of tile v not smaller than a
+            while (lo < hi) {
+                const u32 m = (lo + hi) >> 1;
+                if (key_lt(s2[m], s1[m], s0[m], a2, a1, a0)) lo = m + 1;
+                else hi = m;
+            }
+            less += lo;
+            if (v == u) {
+                tie |= (j > 0 && s2[j - 1] == a2 && s1[j - 1] == a1 && s0[j - 1] == a0) ||
+                       (j + 1 < un && s2[j + 1] == a2 && s1[j + 1] == a1 && s0[j + 1] == a0);
+            } else {
+                tie |= lo < un && s2[lo] == a2 && s1[lo] == a1 && s0[lo] == a0;
+            }
+        }
+        __syncthreads();  // tile v read by every thread before the next one is stored
+    }
+    if (mine) cnt[i] = less | (tie ? 0x80000000u : 0u);
+}
+
+// rank = cnt[i]; tied keys (rare) ordered by full_cmp among the equal keys of
+// every tile (found by a binary search of the tile in global memory)
+__global__ __launch_bounds__(256) void k_rank_put(const u64 *__restrict__ K2, const u64 *__restrict__ K1,
+                                                  const u64 *__restrict__ K0, const u32 *__restrict__ V, u64 n,
+                                                  const u32 *__restrict__ cnt, const u64 *__restrict__ ref,
+                                                  const u8 *buf, const u8 *extra, const u64 *l_pos, const u32 *l_len,
+                                                  const u8 *arena, const u64 *key_off, const u32 *key_len,
+                                                  u32 *__restrict__ order, u64 *__restrict__ len) {
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const u32 c = cnt[i];
+    u64 less = c & 0x7FFFFFFFu;
+    const u64 a2 = K2[i], a1 = K1[i], a0 = K0[i];
+    const u32 v = V[i];
+    const u64 me = ref[v];
+    if (c & 0x80000000u) {
+        const u32 T = (u32)((n + TS_N - 1) / TS_N);
+        for (u32 u = 0; u < T; ++u) {
+            const u64 b = (u64)u * TS_N, e = min(b + TS_N, n);
+            u64 lo = b, hi = e;
+            while (lo < hi) {
+                const u64 m = (lo + hi) >> 1;
+                if (key_lt(K2[m], K1[m], K0[m], a2, a1, a0)) lo = m + 1;
+                else hi = m;
+            }
+            for (u64 j = lo; j < e && K2[j] == a2 && K1[j] == a1 && K0[j] == a0; ++j)
+                if (j != i && full_cmp(ref[V[j]], me, a1, a0, buf, extra, l_pos, l_len, arena, key_off, key_len) < 0)
+                    ++less;
+        }
+    }
+    order[less] = v;
+    len[less] = entry_key_len(me, a1, a0, l_len, key_len);
+}
+
 // ---------------------------------------------------------------------------
 // Root-GPU merge of ranked partitions (msa_import_ranked): every received
 // block is one GPU's ranked key partition (msa_export_ranked), the blocks'
@@ -2214,9 +2323,15 @@ hipError_t msa_launch_rank_small(u64 *const K2[3], u64 *const K1[3], u64 *const 
     if (!n || n > MR_MAXN) return hipErrorInvalidValue;
     const u32 T = (u32)((n + TS_N - 1) / TS_N);
     hipLaunchKernelGGL(k_tile_sort, dim3(T), dim3(TS_T), 0, s, K2[0], K1[0], K0[0], V[0], n, K2[1], K1[1], K0[1], V[1]);
+#if RC_TOT
+    hipLaunchKernelGGL(k_rank_total, dim3(T * RT_K), dim3(RT_T), 0, s, K2[1], K1[1], K0[1], n, cnt);
+    hipLaunchKernelGGL(k_rank_put, grid1(n), dim3(256), 0, s, K2[1], K1[1], K0[1], V[1], n, (const u32 *)cnt, ref,
+                       buf, extra, l_pos, l_len, arena, key_off, key_len, order, len);
+#else
     hipLaunchKernelGGL(k_rank_count, dim3(T), dim3(RC_T), 0, s, K2[1], K1[1], K0[1], n, cnt, (const u64 *)nullptr);
     hipLaunchKernelGGL(k_rank_place, grid1(n), dim3(256), 0, s, K2[1], K1[1], K0[1], V[1], n, (const u32 *)cnt, ref,
                        buf, extra, l_pos, l_len, arena, key_off, key_len, order, len);
+#endif
     return msa_exclusive_scan(len, n, off, bsum, total, s);
 }
 hipError_t msa_launch_fixup(const u64 *K2, const u64 *K1, const u64 *K0, const u32 *V, u64 n, const u64 *ref,
