@@ -2,7 +2,8 @@
 #   bash tools/gpu_final.sh TAG
 # GPU tests, smoke, PMC passes (stamped with this build's msa_build_id and
 # installed as the PMC file the bench attaches), bench (with the CPU baseline),
-# kernel-trace profile, per-song counter bench.  The PMC passes run BEFORE the
+# kernel-trace profile, PMC passes of the per-song counter (stamped the same
+# way), per-song counter bench.  The PMC passes run BEFORE the
 # bench so that its `traffic` comes from the build it times.  Every GPU step has
 # its own time limit; a failing step ends the script.
 set -eo pipefail
@@ -21,5 +22,7 @@ bash tools/pmc.sh $D/pmc
 cp $D/pmc/pmc.json profiles/pmc_scan_main.json
 timeout -k 10 300 python -u bench.py > $D/bench.json 2> $D/bench.err
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $D/prof -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline > $D/prof.log 2>&1
+bash tools/pmc_wcs.sh $D/pmc_wcs
+cp $D/pmc_wcs/pmc.json profiles/pmc_wcs_main.json
 timeout -k 10 300 python -u tools/bench_wcs.py > $D/bench_wcs.json 2> $D/bench_wcs.err
 echo done; exit $rc
