@@ -246,7 +246,9 @@ int msa_import_partitions(msa_ctx *ctx, int table, const void *src, const uint64
  * block (ranked, disjoint key partitions); the table's ranking becomes their
  * k-way merge (no re-insertion, no sort; large tables fall back to
  * msa_import_partitions + a ranking of this table).  Replaces, with
- * msa_import_partitions + msa_rank, rank 0's merge + qsort (main 1011-1039). */
+ * msa_import_partitions + msa_rank, rank 0's merge + qsort (main 1011-1039).
+ * A table merged this way is ranked-only until the next split or partition
+ * import: msa_rank keeps its ranking, msa_export_partitions refuses it.     */
 int msa_import_ranked(msa_ctx *ctx, int table, const void *src, const uint64_t *blk_off, int nblk);
 
 /* ------------------------------------------- per-song word counter (row f)
@@ -289,6 +291,11 @@ int msa_wcs_set_delimiter(msa_wcs *w, int delimiter);
  * per-song counter, whose csv.DictReader reads the default dialect) refuses
  * anything but the default.                                                 */
 int msa_wcs_set_quoting(msa_wcs *w, int quotechar, int skipinitialspace);
+/* Delimiter, quotechar and skipinitialspace in one call, the pair validated
+ * together (split_csv_columns.py's reader/writer dialect, 48-66, 90-95): a
+ * quotechar equal to the OLD delimiter is fine here (e.g. --quotechar ','
+ * with a sniffed ';'), which two separate calls would refuse.              */
+int msa_wcs_set_dialect(msa_wcs *w, int delimiter, int quotechar, int skipinitialspace);
 /* The scripts' --encoding (word_count_per_song.py:63-66,111;
  * split_csv_columns.py:97-101,130): utf8_sig = 1, "utf-8-sig" (default),
  * drops a leading BOM; 0, "utf-8", keeps it as the first field's first

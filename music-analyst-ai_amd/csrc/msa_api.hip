@@ -22,6 +22,7 @@ u32 msa_fn_blocks(u32 nchunks);
 hipError_t msa_launch_fn(const ChunkSum *, u64, u32, Fn *, State *, Fn *, State, State *, State *, hipStream_t);
 hipError_t msa_launch_scan(const ScanArgs &, int, hipStream_t);
 hipError_t msa_launch_scan_csv(const ScanArgs &, hipStream_t);
+hipError_t msa_launch_scan_tokens(const ScanArgs &, hipStream_t);
 hipError_t msa_launch_miss_agg(const ScanArgs &, hipStream_t);
 hipError_t msa_exclusive_scan(const u64 *, u64, u64 *, u64 *, u64 *, hipStream_t);
 hipError_t msa_exclusive_scan2(const u64 *, u64, u64 *, u64 *, u64 *, const u64 *, u64, u64 *, u64 *, u64 *,
@@ -65,7 +66,7 @@ hipError_t msa_launch_fixup(const u64 *, const u64 *, const u64 *, const u32 *, 
                             const u8 *, const u64 *, const u32 *, const u8 *, const u64 *, const u32 *, u32 *, hipStream_t);
 u64 msa_rank_small_max();
 hipError_t msa_launch_merge_ranked(const u8 *, const u64 *, const u64 *, u32, u64, const u64 *, u32, u64 *, u64 *,
-                                   u64 *, u64 *, u64 *, u32 *, u32 *, u64 *, u64 *, u64 *, u64 *, hipStream_t);
+                                   u64 *, u64 *, u64 *, u32 *, u64 *, u64 *, u64 *, u64 *, hipStream_t);
 hipError_t msa_launch_merge_blob(const u32 *, u64, const u8 *, const u64 *, const u64 *, const u64 *, u8 *, u64 *,
                                  hipStream_t);
 u64 msa_rank_small_scratch(u64 n);
@@ -132,11 +133,13 @@ enum {
     ST_RANK_ARTISTS,     // the same, artists
     ST_MISS_AGG,         // K3's logged LDS-table misses -> word tables (k_miss_agg)
     ST_REC_SPANS,        // both columns' line spans + artist keys (k_rec_fast / k_rec_fix) + offset scans
+    ST_CSV_TOKENS,       // split scan, second kernel: lyric tokens -> word tables (k_scan_tokens)
     ST_COUNT_
 };
 const char *const kStageName[ST_COUNT_] = {"csv_summary", "csv_scan",    "artist_column", "text_column",
                                            "artist_summary", "artist_scan", "artist_keys",  "long_words",
-                                           "rank_words",  "rank_artists", "csv_miss_agg", "rec_spans"};
+                                           "rank_words",  "rank_artists", "csv_miss_agg", "rec_spans",
+                                           "csv_tokens"};
 
 struct ProfStage {
     hipEvent_t a = nullptr, b = nullptr;
@@ -163,6 +166,10 @@ struct msa_ctx {
     DevBuf exp_buf, exp_meta, imp_w, imp_a, imp_meta;
     u64 exp_bytes = 0;
     bool merged_w = false, merged_a = false;
+    // tables (bit 0 words, bit 1 artists) whose ranking is msa_import_ranked's
+    // merge of received blocks: the count tables still hold this GPU's own
+    // keys, so the table is ranked-only until the next split / partition import
+    int ranked_only = 0;
     // scan scratch
     DevBuf sums, carry, btot, bstate, small;  // small: Fn total + 2 States + ...
     // CSV records
@@ -202,6 +209,8 @@ struct msa_ctx {
     // tables
     DevBuf s_tab, s_list, m_tab, m_list, l_pos, l_len, l_slot, l_tab, l_list, a_tab, a_list;
     DevBuf mlog, mlog_n;  // K3's logged LDS-table misses (k_miss_agg)
+    DevBuf lmask;         // the split scan's lyric token-byte mask (k_scan_struct -> k_scan_tokens)
+    int k3split = 1;      // MSA_K3SPLIT=0: the fused k_scan_csv instead (A/B runs)
     u64 s_slots = 0, m_slots = 0, l_occ_cap = 0, lt_slots = 0, a_slots = 0;
     u64 s_used_prev = 0, m_used_prev = 0, lt_used_prev = 0, a_used_prev = 0;
     // Table capacities (log2 slots / occurrence capacity).  They start small --
@@ -226,6 +235,8 @@ struct msa_ctx {
     // (both small-table sorts are launch/latency-bound chains)
     hipStream_t rank2 = nullptr;
     hipEvent_t ev_r2_fork = nullptr, ev_r2_join = nullptr;
+    // split scan: k_scan_struct done (the spans may start) / the spans done
+    hipEvent_t ev_scan_a = nullptr, ev_spans = nullptr;
     // the K2 final-state read-back (launch_scan_fn / wait_scan_fn)
     hipEvent_t ev_fin = nullptr;
     State fin_init{};
@@ -619,7 +630,7 @@ static int reset_artist_table(msa_ctx *c) {
 // next counter read-back (col_lens_pending).
 // Line offsets of both columns: one scan launch sequence over both length
 // arrays (the bodies' totals stay on the device, Counters::col_body).
-static int scan_columns(msa_ctx *c, bool text) {
+static int scan_columns(msa_ctx *c, bool text, hipStream_t st) {
     const u64 nrec = c->nrec;
     const u64 nbb = (nrec + 1023) / 1024 + 1;
     HIPC(c, ensure(c->aoff, nrec * 8));
@@ -629,7 +640,7 @@ static int scan_columns(msa_ctx *c, bool text) {
     u64 *bs = c->scan_bsum.as<u64>();
     HIPC(c, msa_exclusive_scan2(c->alen.as<u64>(), nrec, c->aoff.as<u64>(), bs, &body[0],
                                 text ? c->tlen.as<u64>() : nullptr, nrec, c->toff.as<u64>(), bs + nbb, &body[1],
-                                c->stream));
+                                st));
     return MSA_OK;
 }
 
@@ -703,9 +714,9 @@ static int build_word_lists(msa_ctx *c) {
 // Line spans of both columns and the artist keys, then the offset scans: they
 // depend on the scan alone, so they are enqueued before its read-back (the
 // host's header work overlaps them).
-static int launch_spans(msa_ctx *c, bool want_text) {
+static int launch_spans(msa_ctx *c, bool want_text, hipStream_t st) {
     int rc;
-    prof_begin(c, ST_REC_SPANS);
+    prof_begin(c, ST_REC_SPANS, st);
     const u64 nrec = c->nrec;
     HIPC(c, ensure(c->alen, nrec * 8));
     HIPC(c, ensure(c->asrc, nrec * 8));
@@ -730,9 +741,9 @@ static int launch_spans(msa_ctx *c, bool want_text) {
                                  want_text ? 1 : 0, c->alen.as<u64>(), c->asrc.as<u64>(), c->apairs.as<u32>(),
                                  c->tlen.as<u64>(), c->tsrc.as<u64>(), c->tpairs.as<u32>(), c->ctr.as<Counters>(), ak,
                                  c->spans ? c->f0.as<u64>() : nullptr, c->tss.as<u64>(), c->tse.as<u64>(),
-                                 c->span_fix.as<u64>(), c->ablate, c->stream));
-    if ((rc = scan_columns(c, want_text))) return rc;
-    prof_end(c, ST_REC_SPANS, nrec * 136);  // ~36 B read + 100 B written per record
+                                 c->span_fix.as<u64>(), c->ablate, st));
+    if ((rc = scan_columns(c, want_text, st))) return rc;
+    prof_end(c, ST_REC_SPANS, nrec * 136, st);  // ~36 B read + 100 B written per record
     return MSA_OK;
 }
 
@@ -854,6 +865,7 @@ static int split_once(msa_ctx *c, int flags) {
     if (c->n == 0 && !c->cont) return fail(c, MSA_ERR_NOHEADER, "Dataset does not contain a header row");
     const bool want_text = (flags & MSA_SPLIT_TEXT_COLUMN) != 0;
     c->merged_w = c->merged_a = false;
+    c->ranked_only = 0;
     c->artist_piece_set = false;
     c->col_lens_pending = false;
     c->extra_len = 0;
@@ -907,13 +919,31 @@ static int split_once(msa_ctx *c, int flags) {
             a.mlog = c->mlog.as<ulonglong2>();
             a.mlog_n = c->mlog_n.as<u32>();
         }
+        a.split = c->k3split;
+        if (a.split) {  // a word per 64 bytes of every 4 KiB block, behind one zero word
+            const u64 words = (c->n + 4095) / 4096 * 64 + 2;
+            if (c->lmask.cap < words * 8) {
+                HIPC(c, ensure(c->lmask, words * 8));
+                HIPC(c, hipMemsetAsync(c->lmask.p, 0, 8, c->stream));
+            }
+            a.lmask = c->lmask.as<u64>();
+        }
         prof_begin(c, ST_CSV_SCAN);
-        // k_scan_csv (msa_k3.hip); MSA_ABLATE bit 64 selects the round-1 kernel (A/B runs)
+        // k_scan_csv / k_scan_struct (msa_k3.hip); MSA_ABLATE bit 64 selects the round-1 kernel (A/B runs)
         if (c->ablate & 64) HIPC(c, msa_launch_scan(a, 0, c->stream));
         else HIPC(c, msa_launch_scan_csv(a, c->stream));
         // algorithmic bytes: every CSV byte once + the per-record SoA it writes
         // (rec_start 8, nulrel 4 with the text column, the span events f0 / tss / tse 24)
-        prof_end(c, ST_CSV_SCAN, c->n + c->nrec * ((want_text ? 12ull : 8ull) + (c->spans ? 24ull : 0ull)));
+        // + the split scan's token-byte mask (1 bit per byte)
+        prof_end(c, ST_CSV_SCAN, c->n + c->nrec * ((want_text ? 12ull : 8ull) + (c->spans ? 24ull : 0ull)) +
+                                     (a.split ? c->n / 8 : 0));
+        if (a.split && !(c->ablate & 64)) {
+            HIPC(c, hipEventRecord(c->ev_scan_a, c->stream));  // the record arrays are final
+            prof_begin(c, ST_CSV_TOKENS);
+            HIPC(c, msa_launch_scan_tokens(a, c->stream));
+            // the mask (1 bit per byte) + the token bytes re-read (at most every byte once)
+            prof_end(c, ST_CSV_TOKENS, c->n + c->n / 8);
+        }
         return MSA_OK;
     };
     if (cap0 && (rc = launch_k3(cap0))) return rc;
@@ -937,8 +967,17 @@ static int split_once(msa_ctx *c, int flags) {
         HIPC(c, hipMemsetAsync(c->rec_start.p, 0, 8, c->stream));
         if ((rc = launch_k3(cap))) return rc;
     }
-    // the word-miss aggregation (measured beside k_rec_fast on rank2: both
-    // kernels took twice as long, no gain)
+    // The column spans depend on the record arrays alone: with the split scan
+    // they run on the rank2 stream from the end of k_scan_struct, beside
+    // k_scan_tokens (whose one workgroup per CU leaves wave slots free) and
+    // k_miss_agg.  (The fused scan: k_miss_agg measured beside k_rec_fast on
+    // rank2 -- both kernels took twice as long, no gain.)
+    const bool spans_beside = a.split && !(c->ablate & 64) && !(c->ablate & 8192);
+    hipStream_t sst = c->stream;
+    if (spans_beside) {
+        sst = c->rank2;
+        HIPC(c, hipStreamWaitEvent(c->rank2, c->ev_scan_a, 0));
+    }
     if (!(c->ablate & 64)) {
         prof_begin(c, ST_MISS_AGG);
         HIPC(c, msa_launch_miss_agg(a, c->stream));
@@ -947,11 +986,15 @@ static int split_once(msa_ctx *c, int flags) {
     // rec_start[nrec] = end of the last record (EOF when it has no terminator);
     // no terminator: k_rec_fast leaves the last record to the exact path
     if (fin.rs < c->n) {
-        hipLaunchKernelGGL(k_put_u64, dim3(1), dim3(64), 0, c->stream, c->rec_start.as<u64>() + c->nrec, (u64)c->n,
+        hipLaunchKernelGGL(k_put_u64, dim3(1), dim3(64), 0, sst, c->rec_start.as<u64>() + c->nrec, (u64)c->n,
                            c->tse.as<u64>() + c->nrec - 1, (u64)SPAN_FIX);
         HIPC(c, hipGetLastError());
     }
-    if ((rc = launch_spans(c, want_text))) return rc;
+    if ((rc = launch_spans(c, want_text, sst))) return rc;
+    if (spans_beside) {
+        HIPC(c, hipEventRecord(c->ev_spans, c->rank2));
+        HIPC(c, hipStreamWaitEvent(c->stream, c->ev_spans, 0));
+    }
     if (want_text) {  // text.csv's body: deferred (msa_ctx::text_deferred)
         HIPC(c, ensure(c->tcol, kColHdrRoom + c->n + 1 + MSA_INPUT_PAD));
         c->text_deferred = true;
@@ -1366,6 +1409,11 @@ static int sort_and_blob(msa_ctx *c, Ranked &R, const u8 *wbuf, const u8 *wextra
 static int do_rank(msa_ctx *c, int tables = 3) {
     int rc;
     if (c->stage < 2) return fail(c, MSA_ERR_ARG, "msa_rank before msa_count");
+    // a table merged by msa_import_ranked is ranked already (its count tables
+    // are not the merged table: ranking them again would write entries for keys
+    // the ranked arrays were not sized for)
+    tables &= ~c->ranked_only;
+    if (!tables) return MSA_OK;
     if ((rc = start_text_side(c))) return rc;
     // words
     Ranked &W = c->rw;
@@ -1415,6 +1463,18 @@ static int do_rank(msa_ctx *c, int tables = 3) {
         HIPC(c, hipEventRecord(c->ev_r2_fork, c->stream));
         HIPC(c, hipStreamWaitEvent(c->rank2, c->ev_r2_fork, 0));
     }
+    // every exit after the fork joins rank2 back into the library stream (an
+    // error return too: later work there must stay ordered after the artist
+    // kernels still running on rank2)
+    struct R2Join {
+        msa_ctx *c;
+        bool on;
+        ~R2Join() {
+            if (!on) return;
+            (void)hipEventRecord(c->ev_r2_join, c->rank2);
+            (void)hipStreamWaitEvent(c->stream, c->ev_r2_join, 0);
+        }
+    } r2_join{c, conc};
     if (dw && (rc = sort_and_blob(c, W, wbuf, wextra, nullptr, nullptr, nullptr, 0, west, c->stream))) return rc;
     prof_end(c, ST_RANK_WORDS, W.n * 64 + W.blob_len);
     prof_begin(c, ST_RANK_ARTISTS, ast);
@@ -1435,6 +1495,7 @@ static int do_rank(msa_ctx *c, int tables = 3) {
         return rc;
     prof_end(c, ST_RANK_ARTISTS, A.n * 64 + A.blob_len, ast);
     if (conc) {
+        r2_join.on = false;
         HIPC(c, hipEventRecord(c->ev_r2_join, c->rank2));
         HIPC(c, hipStreamWaitEvent(c->stream, c->ev_r2_join, 0));
     }
@@ -1495,30 +1556,22 @@ int msa_create(int device, msa_ctx **out) {
     msa_ctx *c = new msa_ctx();
     c->device = device;
     if (const char *ab = getenv("MSA_ABLATE")) c->ablate = atoi(ab);
+    if (const char *ks = getenv("MSA_K3SPLIT")) c->k3split = atoi(ks) != 0;
     if (const char *so = getenv("MSA_SORT")) c->sort_mode = !strcmp(so, "merge") ? 1 : (!strcmp(so, "radix") ? 2 : 0);
     {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
             c->cus = prop.multiProcessorCount;
     }
-    // MSA_SIDE_FREE=N (experiment): the side stream (text.csv's gather) is kept
-    // off every CU i with i % N == N - 1, so the ranking chain beside it finds
-    // free CUs instead of waiting for the gather's workgroups to drain
-    int side_free = 0;
-    if (const char *sf = getenv("MSA_SIDE_FREE")) side_free = atoi(sf);
-    hipError_t side_e;
-    if (side_free > 1 && c->cus > 0) {
-        std::vector<uint32_t> mask((c->cus + 31) / 32, 0u);
-        for (int i = 0; i < c->cus; ++i)
-            if (i % side_free != side_free - 1) mask[i / 32] |= 1u << (i % 32);
-        side_e = hipExtStreamCreateWithCUMask(&c->side, (uint32_t)mask.size(), mask.data());
-    } else {
-        side_e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
-    }
+    // (round 3 measured and removed: the side stream masked off every 8th /
+    // 16th CU with hipExtStreamCreateWithCUMask -- no gain)
+    const hipError_t side_e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess || side_e != hipSuccess ||
         hipStreamCreateWithFlags(&c->rank2, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_r2_fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_r2_join, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_scan_a, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_spans, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fin, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
@@ -1540,7 +1593,7 @@ void msa_destroy(msa_ctx *c) {
                      &c->nulrel, &c->f0, &c->tss, &c->tse, &c->span_fix, &c->alog, &c->alog_n, &c->acol, &c->alen, &c->aoff, &c->asrc, &c->apairs, &c->tcol, &c->tlen, &c->toff, &c->tsrc, &c->tpairs,
                      &c->scan_bsum, &c->scan_total, &c->ar_start, &c->arena, &c->key_off,
                      &c->key_len, &c->key_slot, &c->s_tab, &c->s_list, &c->m_tab, &c->m_list, &c->l_pos, &c->l_len,
-                     &c->l_slot, &c->l_tab, &c->l_list, &c->a_tab, &c->a_list, &c->ctr, &c->kh1, &c->kh2, &c->mlog, &c->mlog_n, &c->sort_scratch, &c->blob_tot,
+                     &c->l_slot, &c->l_tab, &c->l_list, &c->a_tab, &c->a_list, &c->ctr, &c->kh1, &c->kh2, &c->mlog, &c->mlog_n, &c->lmask, &c->sort_scratch, &c->blob_tot,
                      &c->t_head, &c->t_tie, &c->t_runid, &c->t_tpos, &c->t_bsum, &c->t_total, &c->t_Vn, &c->t_Pn,
                      &c->t_Vc, &c->t_Pc};
     for (DevBuf *b : all) release(*b);
@@ -1565,6 +1618,8 @@ void msa_destroy(msa_ctx *c) {
     (void)hipEventDestroy(c->ev_r2_fork);
     (void)hipEventDestroy(c->ev_fin);
     (void)hipEventDestroy(c->ev_r2_join);
+    (void)hipEventDestroy(c->ev_scan_a);
+    (void)hipEventDestroy(c->ev_spans);
     (void)hipStreamDestroy(c->side);
     (void)hipStreamDestroy(c->rank2);
     (void)hipStreamDestroy(c->stream);
@@ -1996,6 +2051,8 @@ int msa_export_partitions(msa_ctx *c, int table, int nparts, uint64_t *part_byte
     if (!c || nparts < 1 || nparts > 4096 || !part_bytes) return MSA_ERR_ARG;
     if (table != MSA_TABLE_WORDS && table != MSA_TABLE_ARTISTS) return MSA_ERR_ARG;
     if (c->stage < 2) return fail(c, MSA_ERR_ARG, "msa_export_partitions before msa_count");
+    if (c->ranked_only & (table == MSA_TABLE_WORDS ? 1 : 2))
+        return fail(c, MSA_ERR_ARG, "msa_export_partitions of a table merged by msa_import_ranked");
     HIPC(c, hipSetDevice(c->device));
     ExpSrc x;
     u64 n;
@@ -2140,6 +2197,7 @@ int msa_import_partitions(msa_ctx *c, int table, const void *src, const uint64_t
     if ((rc = sync_counters(c))) return rc;
     if (c->h_ctr.collision)
         return fail(c, MSA_ERR_COLLISION, "64-bit key hash collision detected while merging");
+    c->ranked_only &= art ? ~2 : ~1;
     if (art) {
         c->merged_a = true;
         c->sum.n_artists = c->h_ctr.a_claimed;
@@ -2175,11 +2233,8 @@ extern "C" int msa_debug_stat(msa_ctx *c, const char *name, uint64_t *v) {
 // (tools/k3_debug.py compares kernel variants with it).
 // Root GPU of the final gather: the received blocks are the GPUs' ranked,
 // disjoint key partitions (msa_export_ranked), merged into this context's
-// ranking of the table (k-way merge by per-tile counts, csrc/msa_post.hip:
-// k_mr_keys / k_rank_count / k_mr_place / k_mr_blob).  Above kMergeMaxKeys
-// keys the per-tile counts would outgrow the scratch: the blocks are imported
-// as partitions and this table is ranked again.
-static const u64 kMergeMaxKeys = 1ull << 18;  // MSA_MERGE_MAX_KEYS overrides (tests)
+// ranking of the table by co-rank (csrc/msa_post.hip: k_mr_keys /
+// k_mr_corank / k_mr_blob): O(n) scratch and no size limit.
 int msa_import_ranked(msa_ctx *c, int table, const void *src, const uint64_t *blk_off, int nblk) {
     if (!c || !blk_off || nblk < 1) return MSA_ERR_ARG;
     if (table != MSA_TABLE_WORDS && table != MSA_TABLE_ARTISTS) return MSA_ERR_ARG;
@@ -2201,13 +2256,7 @@ int msa_import_ranked(msa_ctx *c, int table, const void *src, const uint64_t *bl
     HIPC(c, hipMemcpyAsync(base.data(), d_base, base.size() * 8, hipMemcpyDeviceToHost, c->stream));
     HIPC(c, hipStreamSynchronize(c->stream));
     const u64 n = base[nblk];
-    u64 merge_max = kMergeMaxKeys;
-    if (const char *mm = getenv("MSA_MERGE_MAX_KEYS")) merge_max = strtoull(mm, nullptr, 10);
-    if (n > merge_max) {
-        int rc;
-        if ((rc = msa_import_partitions(c, table, src, blk_off, nblk))) return rc;
-        return do_rank(c, art ? 2 : 1);
-    }
+    if (n >> 32) return fail(c, MSA_ERR_CAPACITY, "merged table over 2^32 keys");
     // tiles: every block cut into runs of <= 1024 records (sorted, as the block is)
     std::vector<u64> ts;
     for (int p = 0; p < nblk; ++p)
@@ -2218,7 +2267,6 @@ int msa_import_ranked(msa_ctx *c, int table, const void *src, const uint64_t *bl
     HIPC(c, ensure(R.K[2][0], ts.size() * 8));
     HIPC(c, ensure(R.ref, std::max<u64>(n, 1) * 8));
     HIPC(c, ensure(R.cnt, std::max<u64>(n, 1) * 8));
-    HIPC(c, ensure(R.rank_cnt, std::max<u64>((u64)T * n, 1) * 4));
     HIPC(c, ensure(R.order, std::max<u64>(n, 1) * 4));
     HIPC(c, ensure(R.len, std::max<u64>(n, 1) * 8));
     HIPC(c, ensure(R.off, (n + 1) * 8));
@@ -2230,7 +2278,7 @@ int msa_import_ranked(msa_ctx *c, int table, const void *src, const uint64_t *bl
     HIPC(c, hipMemcpyAsync(R.K[2][0].p, ts.data(), ts.size() * 8, hipMemcpyHostToDevice, c->stream));
     HIPC(c, msa_launch_merge_ranked(imp.as<u8>(), d_off, d_base, (u32)nblk, n, R.K[2][0].as<u64>(), T,
                                     R.K[1][0].as<u64>(), R.K[1][1].as<u64>(), R.K[1][2].as<u64>(), R.ref.as<u64>(),
-                                    R.cnt.as<u64>(), R.rank_cnt.as<u32>(), R.order.as<u32>(), R.len.as<u64>(),
+                                    R.cnt.as<u64>(), R.order.as<u32>(), R.len.as<u64>(),
                                     R.off.as<u64>(), R.scan_bsum.as<u64>(), tot, c->stream));
     u64 blob = 0;
     HIPC(c, hipMemcpyAsync(c->pin + kPinSmall, tot, 8, hipMemcpyDeviceToHost, c->stream));
@@ -2246,6 +2294,7 @@ int msa_import_ranked(msa_ctx *c, int table, const void *src, const uint64_t *bl
     R.host_valid = false;
     if (art) c->sum.n_artists = n;
     else c->sum.n_words = n;
+    c->ranked_only |= art ? 2 : 1;
     c->stage = 3;
     return MSA_OK;
 }

@@ -338,6 +338,11 @@ struct ScanArgs {
     ulonglong2 *mlog;
     u32 *mlog_n;
     u32 mlog_cap;
+    // split scan (k_scan_struct -> k_scan_tokens): bit i of lmask[1 + i / 64]
+    // = byte seg_begin + i is a token byte of a counted lyric field
+    // (process_lyrics input, parallel_spotify.c:350-394); lmask[0] = 0 pad
+    u64 *lmask;
+    int split;       // 1: k_scan_struct + k_scan_tokens, 0: the fused k_scan_csv
 };
 
 #define MSA_MLOG_PARTS 16

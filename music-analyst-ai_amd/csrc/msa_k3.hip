@@ -290,9 +290,179 @@ __device__ __forceinline__ void flush_miss(const ScanArgs &a, const ulonglong2 *
     wsync();
 }
 
+// The token phase of one 4 KiB block (process_lyrics, parallel_spotify.c:
+// 350-394): w = the lane's 64 token-byte bits, Tn = the 64 after them, S0 =
+// the counted token starts.  Shared by k_scan_csv and k_scan_tokens.
+__device__ __forceinline__ void tok_phase(const ScanArgs &a, u64 ib, u64 lpos, u64 w, u64 Tn, u64 S0, u64 *skeys,
+                                          u32 *scnts, u16 *list, ulonglong2 *miss, u32 &nmiss, u32 *lcur,
+                                          u64 &words) {
+    const u32 lane = lane_id();
+    // runs: rK bit b = bytes b .. b+K-1 are token bytes (w = Tn:T)
+    const u64 r2 = w & shr128(w, Tn, 1), r2h = Tn & (Tn >> 1);
+    const u64 r3 = r2 & shr128(w, Tn, 2);
+    const u64 r4 = r2 & shr128(r2, r2h, 2), r4h = r2h & (r2h >> 2);
+    const u64 r8 = r4 & shr128(r4, r4h, 4), r8h = r4h & (r4h >> 4);
+    const u64 r16 = r8 & shr128(r8, r8h, 8);
+    const u64 r17 = r16 & shr128(w, Tn, 16);
+    const u64 r9 = r8 & shr128(w, Tn, 8);
+    const u64 sS = S0 & r3 & ~r9, sM = S0 & r9 & ~r17, sL = S0 & r17;
+    words += (u64)__popcll(S0 & r3);
+
+    // long words (> 16 bytes): positions for k_long_insert
+    const u64 BL = __ballot(sL != 0);
+    if (BL) {
+        const u32 nl = (u32)__popcll(sL);
+        u32 tot;
+        const u32 pre = wave_prefix<6>(nl, tot);
+        u64 base = 0;
+        if (lane == 0) base = atomicAdd((unsigned long long *)&a.ctr->l_occ, (unsigned long long)tot);
+        base = readlane64(base, 0) + pre;
+        for (u64 m = sL; m; m &= m - 1) {
+            const u32 b = (u32)__ffsll((long long)m) - 1;
+            if (base < a.l_cap) a.l_pos[base] = (lpos + b) | a.lpos_tag;
+            else atomicOr((unsigned long long *)&a.ctr->overflow, (unsigned long long)OVF_L);
+            ++base;
+        }
+    }
+
+    // 3..16-byte words.  The wave's token starts go to its LDS list
+    // (block offset | (length - 3) << 12); then the lanes take them 64
+    // at a time: 3..8-byte words probe the LDS table, 9..16-byte words
+    // go to the miss logs.  Diagnostic ablations (K3_ABLATE builds,
+    // MSA_ABLATE; results invalid): 1 no tokens at all, 2 no counting,
+    // 32 keys without the LDS table, 4 LDS misses dropped, 128 keys not
+    // re-read from memory
+    u64 m = (K3_ABLATE && (a.ablate & 3)) ? 0ull : (sS | sM);
+    u32 nS;
+    u32 li = wave_prefix<5>((u32)__popcll(m), nS);
+    while (__ballot(m != 0)) {
+        if (m) {
+            const u32 b = (u32)__ffsll((long long)m) - 1;
+            m &= m - 1;
+            // token length (<= 16 here): first non-token bit at or after b,
+            // from the 32 bits [b, b + 32) of (Tn:T)
+            const u32 d0 = (u32)w, d1 = (u32)(w >> 32), d2 = (u32)Tn;
+            const u32 run = __builtin_amdgcn_alignbit(b >= 32 ? d2 : d1, b >= 32 ? d1 : d0, b & 31u);
+            const u32 len = (u32)__ffs(~run) - 1;  // 3..16
+            list[li++] = (u16)((lane * 64 + b) | ((len - 3) << 12));
+        }
+    }
+    wsync();
+    // Keys are re-read from the block (L2) as dwords from the token's
+    // dword; the next 64 tokens' loads are issued before this batch is
+    // probed, so their latency hides behind the LDS work.
+    const u32 nb = (nS + 63) >> 6;
+    u32 en = 0;
+    uint4 kv = make_uint4(0, 0, 0, 0);
+    u32 k4 = 0;
+    if (lane < nS) {
+        en = list[lane];
+        const u32 *gp = reinterpret_cast<const u32 *>(a.buf + ((ib + (en & 4095u)) & ~3ull));
+        kv = *reinterpret_cast<const uint4 *>(gp);
+        k4 = gp[4];
+    }
+    for (u32 bt = 0; bt < nb; ++bt) {
+        bool mis = false;
+        u64 k0 = 0, k1 = KMARK;
+        const u32 e = en;
+        const uint4 v = kv;
+        const u32 v4 = k4;
+        const bool have = bt * 64 + lane < nS;
+        if ((bt + 1) * 64 + lane < nS) {
+            en = list[(bt + 1) * 64 + lane];
+            const u32 *gp = reinterpret_cast<const u32 *>(a.buf + ((ib + (en & 4095u)) & ~3ull));
+            kv = *reinterpret_cast<const uint4 *>(gp);
+            k4 = gp[4];
+        }
+        if (have) {
+            const u32 len = (e >> 12) + 3;
+            const u32 sh = (u32)(ib + (e & 4095u)) & 3u;
+            u64 x0 = mk64(__builtin_amdgcn_alignbyte(v.y, v.x, sh), __builtin_amdgcn_alignbyte(v.z, v.y, sh));
+            u64 x1 = mk64(__builtin_amdgcn_alignbyte(v.w, v.z, sh), __builtin_amdgcn_alignbyte(v4, v.w, sh));
+            if (K3_ABLATE && (a.ablate & 128)) {  // diagnostic: keys made up from the list entry (no re-read)
+                x0 = (u64)e * 0x9E3779B97F4A7C15ull & 0x7F7F7F7F7F7F7F7Full;
+                x1 = x0 >> 3;
+            }
+            // the token's bytes only (selects, no branches), lower-cased
+            const u32 nbits = 8 * len;  // 24..128
+            x0 &= bits_lo(nbits);
+            x1 = nbits <= 64 ? 0ull : (x1 & bits_lo(nbits - 64));
+            k0 = lower_tok8(x0);
+            k1 = lower_tok8(x1) | KMARK;
+            if (K3_ABLATE && (a.ablate & 32)) {
+                words += (k0 ^ k1) == 1;  // keep the key build alive
+            } else if (len <= 8) {
+                const u32 slot = lds_find8(skeys, k0);
+                if (slot != ~0u) atomicAdd(&scnts[slot], 1u);
+                else mis = !(K3_ABLATE && (a.ablate & 4));
+            } else {
+                mis = !(K3_ABLATE && (a.ablate & 4));
+            }
+        }
+        const u64 MB = __ballot(mis);
+        if (MB) {
+            const u32 nm = (u32)__popcll(MB);
+            if (nmiss + nm > Q_MISS) {
+                flush_miss(a, miss, nmiss, lcur);
+                nmiss = 0;
+            }
+            if (mis) {
+                const u32 at = nmiss + mbcnt(MB);
+                if (at < Q_MISS) miss[at] = make_ulonglong2(k0, k1);
+                else hbm_insert16(a, k0, k1, 1);  // more misses than the buffer holds (> 32 in one pass)
+            }
+            nmiss = min(nmiss + nm, (u32)Q_MISS);
+        }
+    }
+    wsync();
+}
+
+// End of a counting workgroup: the wave's pending misses, total_words, the
+// LDS table flushed into the logs (counts encoded; full partitions: HBM
+// inserts) and the log lengths.
+__device__ __forceinline__ void tok_epilogue(const ScanArgs &a, u64 *skeys, u32 *scnts, ulonglong2 *miss, u32 nmiss,
+                                             u32 *lcur, u64 words) {
+    const u32 lane = lane_id();
+    if (nmiss) flush_miss(a, miss, nmiss, lcur);
+    words = wave_sum64(words);
+    if (lane == 0 && words) atomicAdd((unsigned long long *)&a.ctr->total_words, (unsigned long long)words);
+    __syncthreads();
+    // the LDS table into the logs, counts encoded (full partitions: HBM inserts)
+    for (u32 i = threadIdx.x; i < Q_SSLOTS && !(K3_ABLATE && (a.ablate & 32768)); i += Q_T) {  // 32768: no flush
+        u32 n = scnts[i];
+        if (!n) continue;
+        const ulonglong2 kk = make_ulonglong2(skeys[i], KMARK);
+        const u32 part = mlog_part(kk.x, kk.y);
+        const u64 base = ((u64)blockIdx.x * MSA_MLOG_PARTS + part) * a.mlog_cap;
+        while (n) {
+            const u32 c = min(n, MLOG_CMAX);
+            const u32 at = atomicAdd(&lcur[part], 1u);
+            if (at < a.mlog_cap) a.mlog[base + at] = make_ulonglong2(kk.x | spread8(c), kk.y | spread8(c >> 8));
+            else hbm_insert16(a, kk.x, kk.y, c);
+            n -= c;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < MSA_MLOG_PARTS)
+        a.mlog_n[blockIdx.x * MSA_MLOG_PARTS + threadIdx.x] = min(lcur[threadIdx.x], a.mlog_cap);
+}
+
 }  // namespace
 
-__global__ __launch_bounds__(Q_T, 1) void k_scan_csv(ScanArgs a) {
+// SPLIT = 0: k_scan_csv, the fused pass (structure + tokens + LDS counting,
+// one 1024-thread workgroup per CU).  SPLIT = 1: k_scan_struct, the structure
+// alone: no LDS, 256-thread workgroups at SA_MINW waves per SIMD; instead of
+// counting it writes the lyric token-byte mask (ScanArgs::lmask) that
+// k_scan_tokens counts.
+#ifndef SA_T
+#define SA_T 256
+#endif
+#ifndef SA_MINW
+#define SA_MINW 5
+#endif
+template <int SPLIT>
+__device__ __forceinline__ void scan_body(const ScanArgs &a) {
+    constexpr u32 NT = SPLIT ? SA_T : Q_T;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     u64 *skeys = reinterpret_cast<u64 *>(smem);
     u32 *scnts = reinterpret_cast<u32 *>(smem + Q_SSLOTS * 8);
@@ -305,17 +475,19 @@ __global__ __launch_bounds__(Q_T, 1) void k_scan_csv(ScanArgs a) {
     const u64 lt = (1ull << lane) - 1ull;
 
     u32 *lcur = reinterpret_cast<u32 *>(smem + Q_TAB + Q_W * Q_WLDS);  // log cursors per key partition
-    for (u32 i = threadIdx.x; i < Q_SSLOTS; i += Q_T) {
-        skeys[i] = 0;
-        scnts[i] = 0;
+    if (!SPLIT) {
+        for (u32 i = threadIdx.x; i < Q_SSLOTS; i += Q_T) {
+            skeys[i] = 0;
+            scnts[i] = 0;
+        }
+        if (threadIdx.x < MSA_MLOG_PARTS) lcur[threadIdx.x] = 0;
+        __syncthreads();
     }
-    if (threadIdx.x < MSA_MLOG_PARTS) lcur[threadIdx.x] = 0;
-    __syncthreads();
 
     // wave-uniform chunk walk (scalar registers; the chunk-start values below
     // come through scalar loads, which do not wait behind the vector prefetch)
-    const u32 gw = __builtin_amdgcn_readfirstlane(blockIdx.x * Q_W + wib);
-    const u32 nw = gridDim.x * Q_W;
+    const u32 gw = __builtin_amdgcn_readfirstlane(blockIdx.x * (NT / 64) + wib);
+    const u32 nw = gridDim.x * (NT / 64);
     u64 words = 0;
 
     // Software pipeline: the next block (the wave's next chunk's first block
@@ -363,11 +535,13 @@ __global__ __launch_bounds__(Q_T, 1) void k_scan_csv(ScanArgs a) {
             const u64 tpos = ib + Q_BLK;
             const uint4 tail = tl;
             const u32 tvm = tpos < a.seg_end ? (a.seg_end - tpos >= 16 ? 0xFFFFu : (1u << (a.seg_end - tpos)) - 1u) : 0u;
-            u32 tw[4] = {tail.x, tail.y, tail.z, tail.w};
             u32 ttok = 0;
+            if (!SPLIT) {
+                u32 tw[4] = {tail.x, tail.y, tail.z, tail.w};
 #pragma unroll
-            for (int d = 0; d < 4; ++d) ttok |= pk4(lower_tok(tw[d])) << (4 * d);
-            ttok &= tvm;
+                for (int d = 0; d < 4; ++d) ttok |= pk4(lower_tok(tw[d])) << (4 * d);
+                ttok &= tvm;
+            }
             const u64 rem = cend > lpos ? cend - lpos : 0;
             const Masks k = classify64x(cur, (u32)min(rem, (u64)64), rare_chunk);
             // the block's bytes now live in the masks: load the next block (and
@@ -517,157 +691,80 @@ __global__ __launch_bounds__(Q_T, 1) void k_scan_csv(ScanArgs a) {
                 if (Bh) st.rs = readlane64(endp, 63 - __clzll(Bh));
             }
 
+            prevQ = readlane((u32)(k.Q >> 63), 63);
+            if (SPLIT) {
+                // the lyric token bytes for k_scan_tokens (every lane of the
+                // block writes its word, past the segment end too: zero)
+                a.lmask[1 + ((ib - a.seg_begin) >> 6) + lane] = k.T & live;
+                continue;
+            }
             // ---- tokens of the lyric field (process_lyrics, 350-394) ----
             const u64 Tp = from_prev(k.T) >> 63;
             const u64 tp = lane ? Tp : (u64)prevT;
             const u64 S0 = k.T & live & ~((k.T << 1) | tp);
             prevT = readlane((u32)(k.T >> 63), 63);
-            prevQ = readlane((u32)(k.Q >> 63), 63);
             const u64 Tnx = from_next(k.T);
             const u64 Tn = lane == 63 ? (u64)ttok : Tnx;
-            // runs: rK bit b = bytes b .. b+K-1 are token bytes (w = Tn:T)
-            const u64 w = k.T;
-            const u64 r2 = w & shr128(w, Tn, 1), r2h = Tn & (Tn >> 1);
-            const u64 r3 = r2 & shr128(w, Tn, 2);
-            const u64 r4 = r2 & shr128(r2, r2h, 2), r4h = r2h & (r2h >> 2);
-            const u64 r8 = r4 & shr128(r4, r4h, 4), r8h = r4h & (r4h >> 4);
-            const u64 r16 = r8 & shr128(r8, r8h, 8);
-            const u64 r17 = r16 & shr128(w, Tn, 16);
-            const u64 r9 = r8 & shr128(w, Tn, 8);
-            const u64 sS = S0 & r3 & ~r9, sM = S0 & r9 & ~r17, sL = S0 & r17;
-            words += (u64)__popcll(S0 & r3);
-
-            // long words (> 16 bytes): positions for k_long_insert
-            const u64 BL = __ballot(sL != 0);
-            if (BL) {
-                const u32 nl = (u32)__popcll(sL);
-                u32 tot;
-                const u32 pre = wave_prefix<6>(nl, tot);
-                u64 base = 0;
-                if (lane == 0) base = atomicAdd((unsigned long long *)&a.ctr->l_occ, (unsigned long long)tot);
-                base = readlane64(base, 0) + pre;
-                for (u64 m = sL; m; m &= m - 1) {
-                    const u32 b = (u32)__ffsll((long long)m) - 1;
-                    if (base < a.l_cap) a.l_pos[base] = (lpos + b) | a.lpos_tag;
-                    else atomicOr((unsigned long long *)&a.ctr->overflow, (unsigned long long)OVF_L);
-                    ++base;
-                }
-            }
-
-            // 3..16-byte words.  The wave's token starts go to its LDS list
-            // (block offset | (length - 3) << 12); then the lanes take them 64
-            // at a time: 3..8-byte words probe the LDS table, 9..16-byte words
-            // go to the miss logs.  Diagnostic ablations (K3_ABLATE builds,
-            // MSA_ABLATE; results invalid): 1 no tokens at all, 2 no counting,
-            // 32 keys without the LDS table, 4 LDS misses dropped, 128 keys not
-            // re-read from memory
-            u64 m = (K3_ABLATE && (a.ablate & 3)) ? 0ull : (sS | sM);
-            u32 nS;
-            u32 li = wave_prefix<5>((u32)__popcll(m), nS);
-            while (__ballot(m != 0)) {
-                if (m) {
-                    const u32 b = (u32)__ffsll((long long)m) - 1;
-                    m &= m - 1;
-                    // token length (<= 16 here): first non-token bit at or after b,
-                    // from the 32 bits [b, b + 32) of (Tn:T)
-                    const u32 d0 = (u32)w, d1 = (u32)(w >> 32), d2 = (u32)Tn;
-                    const u32 run = __builtin_amdgcn_alignbit(b >= 32 ? d2 : d1, b >= 32 ? d1 : d0, b & 31u);
-                    const u32 len = (u32)__ffs(~run) - 1;  // 3..16
-                    list[li++] = (u16)((lane * 64 + b) | ((len - 3) << 12));
-                }
-            }
-            wsync();
-            // Keys are re-read from the block (L2) as dwords from the token's
-            // dword; the next 64 tokens' loads are issued before this batch is
-            // probed, so their latency hides behind the LDS work.
-            const u32 nb = (nS + 63) >> 6;
-            u32 en = 0;
-            uint4 kv = make_uint4(0, 0, 0, 0);
-            u32 k4 = 0;
-            if (lane < nS) {
-                en = list[lane];
-                const u32 *gp = reinterpret_cast<const u32 *>(a.buf + ((ib + (en & 4095u)) & ~3ull));
-                kv = *reinterpret_cast<const uint4 *>(gp);
-                k4 = gp[4];
-            }
-            for (u32 bt = 0; bt < nb; ++bt) {
-                bool mis = false;
-                u64 k0 = 0, k1 = KMARK;
-                const u32 e = en;
-                const uint4 v = kv;
-                const u32 v4 = k4;
-                const bool have = bt * 64 + lane < nS;
-                if ((bt + 1) * 64 + lane < nS) {
-                    en = list[(bt + 1) * 64 + lane];
-                    const u32 *gp = reinterpret_cast<const u32 *>(a.buf + ((ib + (en & 4095u)) & ~3ull));
-                    kv = *reinterpret_cast<const uint4 *>(gp);
-                    k4 = gp[4];
-                }
-                if (have) {
-                    const u32 len = (e >> 12) + 3;
-                    const u32 sh = (u32)(ib + (e & 4095u)) & 3u;
-                    u64 x0 = mk64(__builtin_amdgcn_alignbyte(v.y, v.x, sh), __builtin_amdgcn_alignbyte(v.z, v.y, sh));
-                    u64 x1 = mk64(__builtin_amdgcn_alignbyte(v.w, v.z, sh), __builtin_amdgcn_alignbyte(v4, v.w, sh));
-                    if (K3_ABLATE && (a.ablate & 128)) {  // diagnostic: keys made up from the list entry (no re-read)
-                        x0 = (u64)e * 0x9E3779B97F4A7C15ull & 0x7F7F7F7F7F7F7F7Full;
-                        x1 = x0 >> 3;
-                    }
-                    // the token's bytes only (selects, no branches), lower-cased
-                    const u32 nbits = 8 * len;  // 24..128
-                    x0 &= bits_lo(nbits);
-                    x1 = nbits <= 64 ? 0ull : (x1 & bits_lo(nbits - 64));
-                    k0 = lower_tok8(x0);
-                    k1 = lower_tok8(x1) | KMARK;
-                    if (K3_ABLATE && (a.ablate & 32)) {
-                        words += (k0 ^ k1) == 1;  // keep the key build alive
-                    } else if (len <= 8) {
-                        const u32 slot = lds_find8(skeys, k0);
-                        if (slot != ~0u) atomicAdd(&scnts[slot], 1u);
-                        else mis = !(K3_ABLATE && (a.ablate & 4));
-                    } else {
-                        mis = !(K3_ABLATE && (a.ablate & 4));
-                    }
-                }
-                const u64 MB = __ballot(mis);
-                if (MB) {
-                    const u32 nm = (u32)__popcll(MB);
-                    if (nmiss + nm > Q_MISS) {
-                        flush_miss(a, miss, nmiss, lcur);
-                        nmiss = 0;
-                    }
-                    if (mis) {
-                        const u32 at = nmiss + mbcnt(MB);
-                        if (at < Q_MISS) miss[at] = make_ulonglong2(k0, k1);
-                        else hbm_insert16(a, k0, k1, 1);  // more misses than the buffer holds (> 32 in one pass)
-                    }
-                    nmiss = min(nmiss + nm, (u32)Q_MISS);
-                }
-            }
-            wsync();
+            tok_phase(a, ib, lpos, k.T, Tn, S0, skeys, scnts, list, miss, nmiss, lcur, words);
         }
     }
-    if (nmiss) flush_miss(a, miss, nmiss, lcur);
-    words = wave_sum64(words);
-    if (lane == 0 && words) atomicAdd((unsigned long long *)&a.ctr->total_words, (unsigned long long)words);
-    __syncthreads();
-    // the LDS table into the logs, counts encoded (full partitions: HBM inserts)
-    for (u32 i = threadIdx.x; i < Q_SSLOTS && !(K3_ABLATE && (a.ablate & 32768)); i += Q_T) {  // 32768: no flush
-        u32 n = scnts[i];
-        if (!n) continue;
-        const ulonglong2 kk = make_ulonglong2(skeys[i], KMARK);
-        const u32 part = mlog_part(kk.x, kk.y);
-        const u64 base = ((u64)blockIdx.x * MSA_MLOG_PARTS + part) * a.mlog_cap;
-        while (n) {
-            const u32 c = min(n, MLOG_CMAX);
-            const u32 at = atomicAdd(&lcur[part], 1u);
-            if (at < a.mlog_cap) a.mlog[base + at] = make_ulonglong2(kk.x | spread8(c), kk.y | spread8(c >> 8));
-            else hbm_insert16(a, kk.x, kk.y, c);
-            n -= c;
-        }
+    if (!SPLIT) tok_epilogue(a, skeys, scnts, miss, nmiss, lcur, words);
+}
+
+__global__ __launch_bounds__(Q_T, 1) void k_scan_csv(ScanArgs a) { scan_body<0>(a); }
+__global__ __launch_bounds__(SA_T, SA_MINW) void k_scan_struct(ScanArgs a) { scan_body<1>(a); }
+
+// k_scan_tokens: the token phase of the split scan over k_scan_struct's
+// lmask -- no reader state, no byte classes: a wave per 4 KiB block (grid
+// stride), token starts and lengths from the mask, keys re-read from the
+// input, counted in the workgroup's LDS table as in k_scan_csv.  The next
+// block's mask words and one 16-byte load per lane of its bytes (the keys'
+// cache lines) are in flight while a block is counted.
+__global__ __launch_bounds__(Q_T, 1) void k_scan_tokens(ScanArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    u64 *skeys = reinterpret_cast<u64 *>(smem);
+    u32 *scnts = reinterpret_cast<u32 *>(smem + Q_SSLOTS * 8);
+    const u32 lane = lane_id();
+    const u32 wib = threadIdx.x >> 6;
+    unsigned char *wl = smem + Q_TAB + wib * Q_WLDS;
+    u16 *list = reinterpret_cast<u16 *>(wl);
+    ulonglong2 *miss = reinterpret_cast<ulonglong2 *>(wl + Q_LIST * 2);
+    u32 nmiss = 0;  // wave-uniform
+    u32 *lcur = reinterpret_cast<u32 *>(smem + Q_TAB + Q_W * Q_WLDS);
+    for (u32 i = threadIdx.x; i < Q_SSLOTS; i += Q_T) {
+        skeys[i] = 0;
+        scnts[i] = 0;
     }
+    if (threadIdx.x < MSA_MLOG_PARTS) lcur[threadIdx.x] = 0;
     __syncthreads();
-    if (threadIdx.x < MSA_MLOG_PARTS)
-        a.mlog_n[blockIdx.x * MSA_MLOG_PARTS + threadIdx.x] = min(lcur[threadIdx.x], a.mlog_cap);
+
+    const u64 nblk = (a.seg_end - a.seg_begin + Q_BLK - 1) / Q_BLK;
+    const u64 nwords = nblk * 64;  // k_scan_struct writes every lane's word of every block
+    const u32 gw = __builtin_amdgcn_readfirstlane(blockIdx.x * Q_W + wib);
+    const u32 nw = gridDim.x * Q_W;
+    u64 words = 0;
+    // mask words of the block: this lane's, the one after it and the one before
+    u64 Lc = 0, Ln = 0, Lp = 0;
+    uint4 warm = make_uint4(0, 0, 0, 0);
+    auto fetch = [&](u64 blk) {
+        u64 wi = blk * 64 + lane;
+        pin64(wi);
+        Lc = a.lmask[1 + wi];
+        Ln = wi + 1 < nwords ? a.lmask[2 + wi] : 0ull;
+        Lp = a.lmask[wi];  // lmask[0] is the zero pad
+        warm = ldg16(a.buf + a.seg_begin + blk * Q_BLK + lane * 64);
+    };
+    if (gw < nblk) fetch(gw);
+    for (u64 blk = gw; blk < nblk; blk += nw) {
+        const u64 L = Lc, Lnext = Ln, Lprev = Lp;
+        asm volatile("" ::"v"(warm.x));  // the block's lines are in cache
+        if (blk + nw < nblk) fetch(blk + nw);
+        const u64 ib = a.seg_begin + blk * Q_BLK;
+        const u64 lpos = ib + lane * 64;
+        const u64 S0 = L & ~((L << 1) | (Lprev >> 63));
+        tok_phase(a, ib, lpos, L, Lnext, S0, skeys, scnts, list, miss, nmiss, lcur, words);
+    }
+    tok_epilogue(a, skeys, scnts, miss, nmiss, lcur, words);
 }
 
 // k_miss_agg: workgroup (partition p, group g) counts partition p of the
@@ -763,6 +860,8 @@ __global__ __launch_bounds__(MA_T) void k_miss_agg(ScanArgs a, u32 nsrc, u32 gro
 }
 
 static int g_q_cus = 0;
+// Counting workgroups: one per CU (k_scan_csv: a wave per 16 KiB chunk;
+// k_scan_tokens: a wave per 4 KiB block).  k_miss_agg reads their logs.
 static u32 scan_blocks(const ScanArgs &a) {
     if (!g_q_cus) {
         int dev = 0;
@@ -771,14 +870,30 @@ static u32 scan_blocks(const ScanArgs &a) {
         g_q_cus = (hipGetDeviceProperties(&p, dev) == hipSuccess && p.multiProcessorCount > 0) ? p.multiProcessorCount
                                                                                                  : 256;
         (void)hipFuncSetAttribute((const void *)k_scan_csv, hipFuncAttributeMaxDynamicSharedMemorySize, Q_LDS);
+        (void)hipFuncSetAttribute((const void *)k_scan_tokens, hipFuncAttributeMaxDynamicSharedMemorySize, Q_LDS);
         (void)hipFuncSetAttribute((const void *)k_miss_agg, hipFuncAttributeMaxDynamicSharedMemorySize, MA_SLOTS * 20);
     }
-    const u32 blocks = (a.nchunks + Q_W - 1) / Q_W;
-    return blocks > (u32)g_q_cus ? (u32)g_q_cus : blocks;
+    const u64 units = a.split ? (a.seg_end - a.seg_begin + Q_BLK - 1) / Q_BLK : a.nchunks;
+    const u64 blocks = (units + Q_W - 1) / Q_W;
+    return blocks > (u64)g_q_cus ? (u32)g_q_cus : (u32)blocks;
 }
+// The fused k_scan_csv, or the split scan's first kernel k_scan_struct
+// (msa_launch_scan_tokens then runs the second on the same stream).
 hipError_t msa_launch_scan_csv(const ScanArgs &a, hipStream_t s) {
     if (!a.nchunks) return hipSuccess;
-    hipLaunchKernelGGL(k_scan_csv, dim3(scan_blocks(a)), dim3(Q_T), Q_LDS, s, a);
+    const u32 blocks = scan_blocks(a);
+    if (a.split) {
+        // a wave per chunk, SA_MINW waves per SIMD while chunks last
+        const u32 waves = std::min<u32>(a.nchunks, (u32)g_q_cus * 4 * SA_MINW);
+        hipLaunchKernelGGL(k_scan_struct, dim3((waves + SA_T / 64 - 1) / (SA_T / 64)), dim3(SA_T), 0, s, a);
+    } else {
+        hipLaunchKernelGGL(k_scan_csv, dim3(blocks), dim3(Q_T), Q_LDS, s, a);
+    }
+    return hipGetLastError();
+}
+hipError_t msa_launch_scan_tokens(const ScanArgs &a, hipStream_t s) {
+    if (!a.nchunks || !a.split) return hipSuccess;
+    hipLaunchKernelGGL(k_scan_tokens, dim3(scan_blocks(a)), dim3(Q_T), Q_LDS, s, a);
     return hipGetLastError();
 }
 // after k_scan_csv on the same stream: fold the logged misses, 16 partitions x

@@ -2079,10 +2079,13 @@ __global__ __launch_bounds__(256) void k_rank_put(const u64 *__restrict__ K2, co
 // Root-GPU merge of ranked partitions (msa_import_ranked): every received
 // block is one GPU's ranked key partition (msa_export_ranked), the blocks'
 // keys are disjoint, so the global ranking is their k-way merge -- no
-// re-insertion and no sort.  Each block is cut into tiles of <= TS_N records
-// (sorted, as the block is), k_rank_count counts per tile, k_mr_place ranks
-// every record (ties on 24 key bytes by the key bytes), k_mr_blob writes the
-// counts and the key blob in rank order.
+// re-insertion and no sort.  Co-rank: a record's global rank is its index in
+// its own block plus, for every other block, the number of that block's keys
+// smaller than it (k_mr_corank: one workgroup per tile of <= TS_N records,
+// each other block's window of keys between the tile's first and last key
+// streamed through LDS; ties on 24 key bytes ordered by the key bytes);
+// k_mr_blob writes the counts and the key blob in rank order.  O(n x blocks)
+// coalesced loads and O(n) scratch at any table size.
 //   block: u64 n, u64 blob_bytes, u64 0, u64 0 | n x {u64 count, u32 len,
 //          u32 blob_off, u8 key[16]} | blob (keys in rank order)
 __global__ void k_mr_keys(const u8 *__restrict__ in, const u64 *__restrict__ blk_off, const u64 *__restrict__ rec_base,
@@ -2117,24 +2120,78 @@ __device__ __forceinline__ int mr_cmp(const u8 *in, u64 a, u64 b) {  // strcmp o
         if (pa[k] != pb[k]) return pa[k] < pb[k] ? -1 : 1;
     return na < nb ? -1 : (na > nb ? 1 : 0);
 }
-__global__ void k_mr_place(const u64 *__restrict__ K2, const u64 *__restrict__ K1, const u64 *__restrict__ K0, u64 n,
-                           const u32 *__restrict__ cnt, const u64 *__restrict__ ts, u32 T, const u8 *__restrict__ in,
-                           const u64 *__restrict__ kptr, u32 *__restrict__ order, u64 *__restrict__ len) {
-    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    u64 less = 0;
-    u32 tie = 0;
-    for (u32 u = 0; u < T; ++u) {
-        const u32 c = cnt[(u64)u * n + i];
-        less += c & 0x7FFFFFFFu;
-        tie |= c;
+#define CR_T TS_N
+__global__ __launch_bounds__(CR_T) void k_mr_corank(const u64 *__restrict__ K2, const u64 *__restrict__ K1,
+                                                   const u64 *__restrict__ K0, const u64 *__restrict__ ts,
+                                                   const u64 *__restrict__ rec_base, u32 nblk,
+                                                   const u8 *__restrict__ in, const u64 *__restrict__ kptr,
+                                                   u32 *__restrict__ order, u64 *__restrict__ len) {
+    __shared__ u64 s2[CR_T], s1[CR_T], s0[CR_T];
+    __shared__ u64 win[2][2];
+    const u32 t = threadIdx.x;
+    const u64 tb = ts[blockIdx.x], te = ts[blockIdx.x + 1];
+    u32 p = 0, ph = nblk;  // the tile's block: rec_base[p] <= tb < rec_base[p + 1]
+    while (ph - p > 1) {
+        const u32 m = (p + ph) >> 1;
+        if (rec_base[m] <= tb) p = m;
+        else ph = m;
     }
-    const u64 a2 = K2[i], a1 = K1[i], a0 = K0[i], me = kptr[i];
-    if (tie & 0x80000000u)  // rare: keys sharing a count and 16 bytes, ordered by their bytes
-        for (u32 u = 0; u < T; ++u)
-            for (u64 j = ts[u] + (cnt[(u64)u * n + i] & 0x7FFFFFFFu);
-                 j < ts[u + 1] && K2[j] == a2 && K1[j] == a1 && K0[j] == a0; ++j)
-                if (j != i && mr_cmp(in, kptr[j], me) < 0) ++less;
+    const u64 i = tb + t;
+    const bool mine = i < te;
+    u64 a2 = 0, a1 = 0, a0 = 0;
+    if (mine) { a2 = K2[i]; a1 = K1[i]; a0 = K0[i]; }
+    u64 less = mine ? i - rec_base[p] : 0;  // its own block is ranked: the index is its rank there
+    bool tie = false;
+    const u64 f2 = K2[tb], f1 = K1[tb], f0 = K0[tb], l2 = K2[te - 1], l1 = K1[te - 1], l0 = K0[te - 1];
+    for (u32 q = 0; q < nblk; ++q) {
+        const u64 qb = rec_base[q], qe = rec_base[q + 1];
+        if (q == p || qb == qe) continue;
+        // block q's window: [first key >= the tile's first, first key > the tile's last)
+        if (t < 2) {
+            u64 lo = qb, hi = qe;
+            while (lo < hi) {
+                const u64 m = (lo + hi) >> 1;
+                const bool go = t == 0 ? key_lt(K2[m], K1[m], K0[m], f2, f1, f0) : !key_lt(l2, l1, l0, K2[m], K1[m], K0[m]);
+                if (go) lo = m + 1;
+                else hi = m;
+            }
+            win[q & 1][t] = lo;
+        }
+        __syncthreads();
+        const u64 L = win[q & 1][0], H = win[q & 1][1];
+        less += L - qb;
+        for (u64 c0 = L; c0 < H; c0 += CR_T) {
+            const u32 cn = (u32)min((u64)CR_T, H - c0);
+            if (t < cn) { s2[t] = K2[c0 + t]; s1[t] = K1[c0 + t]; s0[t] = K0[c0 + t]; }
+            __syncthreads();
+            if (mine) {
+                u32 lo = 0, hi = cn;  // first key of the chunk not smaller than this one
+                while (lo < hi) {
+                    const u32 m = (lo + hi) >> 1;
+                    if (key_lt(s2[m], s1[m], s0[m], a2, a1, a0)) lo = m + 1;
+                    else hi = m;
+                }
+                less += lo;
+                tie |= lo < cn && s2[lo] == a2 && s1[lo] == a1 && s0[lo] == a0;
+            }
+            __syncthreads();
+        }
+    }
+    if (!mine) return;
+    const u64 me = kptr[i];
+    if (tie)  // rare: a key of another block shares the count and 16 bytes; order by the key bytes
+        for (u32 q = 0; q < nblk; ++q) {
+            if (q == p) continue;
+            u64 lo = rec_base[q], hi = rec_base[q + 1];
+            const u64 qe = hi;
+            while (lo < hi) {
+                const u64 m = (lo + hi) >> 1;
+                if (key_lt(K2[m], K1[m], K0[m], a2, a1, a0)) lo = m + 1;
+                else hi = m;
+            }
+            for (u64 j = lo; j < qe && K2[j] == a2 && K1[j] == a1 && K0[j] == a0; ++j)
+                if (mr_cmp(in, kptr[j], me) < 0) ++less;
+        }
     order[less] = (u32)i;
     len[less] = me >> 40;
 }
@@ -2295,14 +2352,12 @@ hipError_t msa_launch_sort(u64 *const K2[3], u64 *const K1[3], u64 *const K0[3],
 // kptr, cntv (n each), cnt (T x n u32), ts (T + 1).  Ends with len / off /
 // total (blob offsets) in rank order; k_mr_blob then writes counts + blob.
 hipError_t msa_launch_merge_ranked(const u8 *in, const u64 *blk_off, const u64 *rec_base, u32 nblk, u64 n,
-                                   const u64 *ts, u32 T, u64 *K2, u64 *K1, u64 *K0, u64 *kptr, u64 *cntv, u32 *cnt,
+                                   const u64 *ts, u32 T, u64 *K2, u64 *K1, u64 *K0, u64 *kptr, u64 *cntv,
                                    u32 *order, u64 *len, u64 *off, u64 *bsum, u64 *total, hipStream_t s) {
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(k_mr_keys, grid1(n), dim3(256), 0, s, in, blk_off, rec_base, nblk, n, K2, K1, K0, kptr, cntv);
-    hipLaunchKernelGGL(k_rank_count, dim3(T), dim3(RC_T), 0, s, (const u64 *)K2, (const u64 *)K1, (const u64 *)K0, n,
-                       cnt, ts);
-    hipLaunchKernelGGL(k_mr_place, grid1(n), dim3(256), 0, s, (const u64 *)K2, (const u64 *)K1, (const u64 *)K0, n,
-                       (const u32 *)cnt, ts, T, in, (const u64 *)kptr, order, len);
+    hipLaunchKernelGGL(k_mr_corank, dim3(T), dim3(CR_T), 0, s, (const u64 *)K2, (const u64 *)K1, (const u64 *)K0, ts,
+                       rec_base, nblk, in, (const u64 *)kptr, order, len);
     return msa_exclusive_scan(len, n, off, bsum, total, s);
 }
 hipError_t msa_launch_merge_blob(const u32 *order, u64 n, const u8 *in, const u64 *kptr, const u64 *cntv,
@@ -2311,7 +2366,8 @@ hipError_t msa_launch_merge_blob(const u32 *order, u64 n, const u8 *in, const u6
     return hipGetLastError();
 }
 u64 msa_rank_small_max() { return MR_MAXN; }
-u64 msa_rank_small_scratch(u64 n) { return ((n + TS_N - 1) / TS_N) * n * 4; }
+// k_rank_total writes one count per key; the per-tile k_rank_count path T x n
+u64 msa_rank_small_scratch(u64 n) { return RC_TOT ? n * 4 : ((n + TS_N - 1) / TS_N) * n * 4; }
 // Small-table ranking: k_tile_sort + k_rank_count + k_rank_place (entry ids
 // and key lengths in rank order) + the blob offsets' scan (total to *total).
 // Set 1 of K2/K1/K0/V holds the sorted tiles; cnt: msa_rank_small_scratch(n)

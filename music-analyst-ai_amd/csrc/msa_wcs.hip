@@ -1549,6 +1549,19 @@ extern "C" int msa_wcs_set_quoting(msa_wcs *w, int quotechar, int skipinitialspa
     return MSA_OK;
 }
 
+// Both at once, the pair validated together (the column splitter: a new
+// quotechar may equal the current delimiter and vice versa).
+extern "C" int msa_wcs_set_dialect(msa_wcs *w, int delim, int quotechar, int skipinitialspace) {
+    auto bad = [](int b) { return b <= 0 || b > 127 || b == '\r' || b == '\n'; };
+    if (!w || bad(delim) || bad(quotechar) || delim == quotechar) return MSA_ERR_ARG;
+    if ((u32)delim != w->delim || (u32)quotechar != w->quote || (u32)(skipinitialspace != 0) != w->skipsp)
+        wcs_release_results(w);
+    w->delim = (u32)delim;
+    w->quote = (u32)quotechar;
+    w->skipsp = skipinitialspace != 0;
+    return MSA_OK;
+}
+
 // The scripts' --encoding: utf8_sig = 1 ("utf-8-sig", their default) drops a
 // leading BOM; 0 ("utf-8") keeps it as the first field's first character.
 // Invalidates results.

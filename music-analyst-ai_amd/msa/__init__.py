@@ -44,7 +44,7 @@ EXPORTS = [
     "msa_set_shard", "msa_piece_size", "msa_shard_function", "msa_shard_head", "msa_segment_copy",
     "msa_segment_set", "msa_artist_reader_needed", "msa_set_artist_reader", "msa_export_partitions", "msa_export_ranked", "msa_export_copy", "msa_import_partitions", "msa_import_ranked",
     "msa_wcs_create", "msa_wcs_destroy", "msa_wcs_last_error", "msa_wcs_stream", "msa_wcs_load_csv",
-    "msa_wcs_set_table_bits", "msa_wcs_set_delimiter", "msa_wcs_set_quoting", "msa_wcs_set_encoding", "msa_wcs_run", "msa_wcs_get_summary", "msa_wcs_get_csv", "msa_wcs_write_outputs",
+    "msa_wcs_set_table_bits", "msa_wcs_set_delimiter", "msa_wcs_set_quoting", "msa_wcs_set_dialect", "msa_wcs_set_encoding", "msa_wcs_run", "msa_wcs_get_summary", "msa_wcs_get_csv", "msa_wcs_write_outputs",
     "msa_csvcol_run", "msa_csvcol_header", "msa_csvcol_get",
 ]
 MSA_WCS_GLOBAL = 0
@@ -164,6 +164,7 @@ def load(path: str = LIB_PATH):
     lib.msa_wcs_set_table_bits.argtypes = [vp, i]
     lib.msa_wcs_set_delimiter.argtypes = [vp, i]
     lib.msa_wcs_set_quoting.argtypes = [vp, i, i]
+    lib.msa_wcs_set_dialect.argtypes = [vp, i, i, i]
     lib.msa_wcs_set_encoding.argtypes = [vp, i]
     lib.msa_wcs_run.argtypes = [vp]
     lib.msa_wcs_get_summary.argtypes = [vp, C.POINTER(_WcsSummary)]
@@ -441,6 +442,12 @@ class WordCountPerSong:
         if len(quotechar) != 1:
             raise MsaError(-1, f"quotechar must be one character, got {quotechar!r}")
         self._check(self.lib.msa_wcs_set_quoting(self.h, ord(quotechar), 1 if skipinitialspace else 0))
+
+    def set_dialect(self, delimiter: str, quotechar: str = '"', skipinitialspace: bool = False):
+        """Delimiter + quotechar + skipinitialspace at once, validated as a pair (msa_wcs_set_dialect)."""
+        if len(delimiter) != 1 or len(quotechar) != 1:
+            raise MsaError(-1, f"delimiter/quotechar must be one character, got {delimiter!r}/{quotechar!r}")
+        self._check(self.lib.msa_wcs_set_dialect(self.h, ord(delimiter), ord(quotechar), 1 if skipinitialspace else 0))
 
     def set_encoding(self, encoding: str = "utf-8-sig"):
         """--encoding: "utf-8-sig" drops a leading BOM, "utf-8" keeps it as data."""

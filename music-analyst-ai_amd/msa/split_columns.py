@@ -64,8 +64,7 @@ def split_csv_columns(csv_path: str, output_dir: Optional[str] = None, delimiter
     base_out.mkdir(parents=True, exist_ok=True)
     data = in_path.read_bytes()
     with WordCountPerSong(device) as w:
-        w.set_quoting(quotechar, skipinitialspace)
-        w.set_delimiter(delimiter)
+        w.set_dialect(delimiter, quotechar, skipinitialspace)
         w.set_encoding(encoding)
         w.load_csv(data)
         try:

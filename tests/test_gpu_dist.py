@@ -135,14 +135,14 @@ def test_sharded_equals_single_process(msa_mod, tmp_path, world, mode, gen):
     assert artists == exp["top_artists.csv"]
 
 
-@pytest.mark.parametrize("merge_max", ["0", "64"])
-def test_sharded_gather_merge_fallback(msa_mod, tmp_path, merge_max):
-    """msa_import_ranked: above its key limit the root imports the ranked blocks
-    as partitions and ranks the table again (0: always; 64: the artists merge,
-    the words do not) -- same bytes as the k-way merge."""
-    data = msa_mod.gen_corpus(4000, mode="highcard", seed=5, vocab=8000)
-    cuts = cuts_for(data, 3, "in_quotes")
-    words, artists, tot = run_world(tmp_path, data, cuts, env_extra={"MSA_MERGE_MAX_KEYS": merge_max})
+@pytest.mark.parametrize("world,kind", [(5, "highcard"), (4, "torture")])
+def test_sharded_gather_corank(msa_mod, tmp_path, world, kind):
+    """msa_import_ranked's co-rank merge (k_mr_corank) with more blocks: many
+    tiles per block, blocks of very different sizes, and (highcard) long keys
+    sharing their first 16 bytes and a count across blocks (the tie path)."""
+    data = msa_mod.gen_corpus(6000, mode=kind, seed=5, vocab=8000)
+    cuts = cuts_for(data, world, "in_quotes")
+    words, artists, tot = run_world(tmp_path, data, cuts)
     exp = expected(tmp_path, data)
     assert words == exp["word_counts.csv"]
     assert artists == exp["top_artists.csv"]
@@ -165,11 +165,14 @@ def test_sharded_tiny_shards(msa_mod, tmp_path):
 def test_sharded_highcard_every_table_overflows(msa_mod, tmp_path):
     """2 ranks on the corpus of test_gpu_scale.py whose cardinalities exceed
     every initial table: each rank's split/count and the merged partitions
-    grow their tables and the result is still the single-process one."""
+    grow their tables and the result is still the single-process one.  The
+    root's co-rank merge takes the whole union (no size limit, no re-rank:
+    the round-3 count matrix fell back above 2^18 keys)."""
     data = msa_mod.gen_corpus(150_000, mode="highcard", seed=31)
     cuts = cuts_for(data, 2, "in_quotes")
     words, artists, tot = run_world(tmp_path, data, cuts)
     exp = expected(tmp_path, data)
+    assert words.count(b"\n") > 4 * (1 << 18)
     assert tot == {k: exp["metrics"][k] for k in ("total_songs", "total_words")}
     assert words == exp["word_counts.csv"]
     assert artists == exp["top_artists.csv"]
@@ -235,3 +238,31 @@ def test_configs3_c_host_four_ranks_shm(configs3_corpus, tmp_path):
         m = json.load(f)
     e = read_outputs_tables(od)["metrics"]
     assert m["processes"] == 4 and (m["total_songs"], m["total_words"]) == (e["total_songs"], e["total_words"])
+
+
+def test_rank_after_import_ranked_topk(msa_mod):
+    """A table merged by msa_import_ranked (here one GPU's own top-k block) is
+    ranked-only: a later msa_rank keeps the merged ranking (it must not rank
+    the local count tables, which hold more keys than the merged arrays were
+    sized for) and msa_export_partitions refuses it."""
+    import ctypes
+    msa = msa_mod
+    data = msa.gen_corpus(3000, mode="zipf", seed=11)
+    with msa.Context(0) as ctx:
+        ctx.load_csv(data)
+        ctx.run(text_column=False)
+        full_w = ctx.ranked(msa.MSA_TABLE_WORDS)
+        full_a = ctx.ranked(msa.MSA_TABLE_ARTISTS)
+        k = 25
+        assert len(full_w) > 10 * k
+        for t, full in ((msa.MSA_TABLE_WORDS, full_w), (msa.MSA_TABLE_ARTISTS, full_a)):
+            nb = ctx.export_ranked(t, k)
+            buf = ctypes.create_string_buffer(nb)
+            ctx.export_copy(ctypes.addressof(buf))
+            ctx.import_ranked(t, ctypes.addressof(buf), [0, nb])
+            assert ctx.ranked(t) == full[:k]
+        ctx.rank()  # must leave both merged rankings as they are
+        assert ctx.ranked(msa.MSA_TABLE_WORDS) == full_w[:k]
+        assert ctx.ranked(msa.MSA_TABLE_ARTISTS) == full_a[:k]
+        with pytest.raises(msa.MsaError):
+            ctx.export_partitions(msa.MSA_TABLE_WORDS, 2)

@@ -120,7 +120,7 @@ def dialect_corpus(seed: int, rows: int, delim: str, quote: str, space_after: bo
 
 
 @pytest.mark.parametrize("delim,quote,skip", [(",", "'", False), (";", "|", False), (",", '"', True), (",", "'", True),
-                                              ("\t", "'", True), (" ", '"', True)])
+                                              ("\t", "'", True), (" ", '"', True), (";", ",", False)])
 def test_split_dialects_vs_oracle(msa_mod, delim, quote, skip):
     """--quotechar and skipinitialspace dialects (split_csv_columns.py:58,
     90-95): the GPU reader and writer against the oracle on random rows."""
@@ -128,12 +128,27 @@ def test_split_dialects_vs_oracle(msa_mod, delim, quote, skip):
         data = dialect_corpus(300 + seed, 400, delim, quote, skip)
         first, bodies = split_oracle.split_columns(data, True, delim, quote, skip)
         with msa_mod.WordCountPerSong(0) as w:
-            w.set_quoting(quote, skip)
-            w.set_delimiter(delim)
+            w.set_dialect(delim, quote, skip)
             w.load_csv(data)
             nc, _ = w.split_columns(True)
             assert [w.column_header(i) for i in range(nc)] == first
             assert [w.column_body(i) for i in range(nc)] == bodies
+
+
+def test_split_quotechar_equal_to_default_delimiter(msa_mod, tmp_path):
+    """--quotechar ',' with a ';' delimiter (Python's csv accepts it): the host
+    mirror sets the pair in one call, so the old ',' delimiter does not make
+    the new quotechar look invalid."""
+    from msa.split_columns import split_csv_columns
+
+    data = dialect_corpus(7, 200, ";", ",", False)
+    first, bodies = split_oracle.split_columns(data, True, ";", ",", False)
+    inp = tmp_path / "in.csv"
+    inp.write_bytes(data)
+    files = split_csv_columns(str(inp), str(tmp_path / "cols"), delimiter=";", quotechar=",", encoding="utf-8")
+    assert len(files) == len(bodies)
+    for f, b in zip(files, bodies):
+        assert f.read_bytes().endswith(b)
 
 
 def test_per_song_counter_refuses_other_quoting(msa_mod):

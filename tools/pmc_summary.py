@@ -23,7 +23,7 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "music-analyst-ai_amd"))
-KERNELS = ["k_scan_csv", "k_miss_agg", "k_chunk_summary", "k_rec_spans", "k_rec_fast", "k_rec_fix", "k_col_gather", "k_col_lines",
+KERNELS = ["k_scan_csv", "k_scan_struct", "k_scan_tokens", "k_miss_agg", "k_chunk_summary", "k_rec_spans", "k_rec_fast", "k_rec_fix", "k_col_gather", "k_col_lines",
            "k_artist_count", "k_tile_sort", "k_merge_pass",
            # the per-song counter (tools/pmc_wcs.sh, --wcs)
            "k_wcs_wrows", "k_wcs_rows", "k_wcs_map", "k_wcs_emit", "k_wcs_validate", "k_wcs_pairs"]
@@ -83,7 +83,8 @@ def main():
             e["write_bytes_per_launch"] = int(c["WRITE_SIZE"] * 1024)
         kernels[k] = e
     b = bench_line(os.path.join(out, "fetch.log"))
-    rk = "k_wcs_wrows" if wcs else "k_scan_csv"
+    # the bench line names the roofline kernel ("k_scan_tokens (csv_tokens)", ...)
+    rk = "k_wcs_wrows" if wcs else ((b or {}).get("roofline", {}).get("kernel", "k_scan_csv").split(" ")[0])
     res = {
         "build_id": build_id(),
         "input_bytes": b["config"]["bytes_per_gpu"] if b else None,
