@@ -353,10 +353,20 @@ static int fail(msa_ctx *c, int code, const char *fmt, ...) {
                                           __FILE__, __LINE__);                                          \
     } while (0)
 
+// A buffer is freed only once no kernel can still touch it: work on the
+// library's other streams (text.csv on the side stream, the spans / artist
+// ranking on rank2) may be in flight when a host call grows a buffer, and
+// memory hipFree returns can be handed out again at once.
+static void free_quiet(void *p) {
+    if (!p) return;
+    (void)hipDeviceSynchronize();
+    (void)hipFree(p);
+}
+
 static hipError_t ensure(DevBuf &b, size_t bytes, bool zero = false) {
     if (bytes == 0) bytes = 16;
     if (b.cap >= bytes) return hipSuccess;
-    if (b.p) (void)hipFree(b.p);
+    free_quiet(b.p);
     b.p = nullptr;
     b.cap = 0;
     size_t want = bytes + bytes / 4;
@@ -368,7 +378,7 @@ static hipError_t ensure(DevBuf &b, size_t bytes, bool zero = false) {
 }
 
 static void release(DevBuf &b) {
-    if (b.p) (void)hipFree(b.p);
+    free_quiet(b.p);
     b.p = nullptr;
     b.cap = 0;
 }
@@ -1973,7 +1983,7 @@ static hipError_t grow_keep(DevBuf &b, size_t bytes, size_t keep, hipStream_t s)
     if (keep) e = hipMemcpyAsync(np, b.p, keep, hipMemcpyDeviceToDevice, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) { (void)hipFree(np); return e; }
-    if (b.p) (void)hipFree(b.p);
+    free_quiet(b.p);
     b.p = np;
     b.cap = want;
     return hipSuccess;
@@ -2225,6 +2235,9 @@ extern "C" int msa_debug_stat(msa_ctx *c, const char *name, uint64_t *v) {
     else if (n == "a_long") *v = k.a_long;
     else if (n == "overflow") *v = k.overflow;
     else if (n == "span_fix") *v = k.span_fix;
+    else if (n == "s_claimed") *v = k.s_claimed;
+    else if (n == "m_claimed") *v = k.m_claimed;
+    else if (n == "l_claimed") *v = k.l_claimed;
     else return MSA_ERR_ARG;
     return MSA_OK;
 }

@@ -290,6 +290,149 @@ __device__ __forceinline__ void flush_miss(const ScanArgs &a, const ulonglong2 *
     wsync();
 }
 
+// Record structure of one 4 KiB block (read_csv_record 549-633 + parse_csv_line
+// 258-304): from the reader state st at the block start (updated to the state
+// after it) and the block's byte classes, the per-record arrays (rec_start,
+// f0, tss, tse, nulrel) and the lane's live lyric bytes (returned).  tail /
+// tvm: the 16 bytes after the block and their validity; prevQ: the byte
+// before the block is a '"'.
+__device__ __forceinline__ u64 struct_block(const ScanArgs &a, State &st, const Masks &k, uint4 tail, u32 tvm,
+                                            u64 lpos, u32 prevQ) {
+    const u32 lane = lane_id();
+    const u64 lt = (1ull << lane) - 1ull;
+    // ---- record structure (read_csv_record + parse_csv_line) ----
+    const u64 B = __ballot(__popcll(k.Q) & 1u);
+    const u32 pin = st.p ^ (mbcnt(B) & 1u);
+    const u64 inq = pxor_ex64(k.Q) ^ (pin ? ~0ull : 0ull);
+    const u64 CRu = k.CR & ~inq, NLu = k.NL & ~inq, Cu = k.C & ~inq;
+    // DPP and bpermute read the source lane's register only when that
+    // lane is active: every cross-lane move below runs on all 64 lanes,
+    // the per-lane choice is a select afterwards
+    const u64 CRp = from_prev(CRu) >> 63;
+    const u64 NLn = from_next(k.NL) & 1ull;
+    const u64 pCR = lane ? CRp : (u64)st.cr;
+    const u64 TERM = CRu | (NLu & ~((CRu << 1) | pCR));
+    const u32 tail_nl = ((tail.x & 0xFFu) == '\n' && (tvm & 1u)) ? 1u : 0u;
+    const u64 nNL = lane == 63 ? (u64)tail_nl : NLn;
+    // '"' at the byte after the lane (text start after a comma at byte
+    // 63) and at the byte before it (text end before a terminator at byte 0)
+    const u32 tail_q = ((tail.x & 0xFFu) == '"' && (tvm & 1u)) ? 1u : 0u;
+    const u64 Qnx = from_next(k.Q) & 1ull, Qpv = from_prev(k.Q) >> 63;
+    const u32 qnext = lane == 63 ? tail_q : (u32)Qnx;
+    const u32 qprev = lane ? (u32)Qpv : prevQ;
+    const u64 SW = CRu & ((k.NL >> 1) | (nNL << 63));  // '\r' terminators that swallow a '\n'
+
+    const u32 nt = (u32)__popcll(TERM);
+    const u32 lastT = nt ? 63u - (u32)__clzll(TERM) : 0u;
+    const u64 above = nt ? bits_hi(lastT + 1) : ~0ull;
+    const u32 cq = min((u32)__popcll(Cu & above), 3u);
+    const bool zq = (k.Z & above) != 0;
+    const u64 C1 = __ballot(cq >= 1), C2 = __ballot(cq >= 2), C3 = __ballot(cq >= 3);
+    const u64 Zb = __ballot(zq), Bh = __ballot(nt != 0);
+    const u64 J = Bh & lt;
+    u64 M;
+    u32 cin;
+    bool zin;
+    if (J) {
+        const u32 jl = 63u - (u32)__clzll(J);
+        M = lt & ~bits_lo(jl);
+        cin = 0;
+        zin = (Zb & M) != 0;
+    } else {
+        M = lt;
+        cin = st.c;
+        zin = st.z || ((Zb & M) != 0);
+    }
+    cin = min(cin + (u32)__popcll(C1 & M) + (u32)__popcll(C2 & M) + (u32)__popcll(C3 & M), 3u);
+    // record index at the lane's first byte: prefix of terminator counts
+    const u64 T1 = __ballot(nt >= 1), T2 = __ballot(nt >= 2), T3 = __ballot(nt >= 3);
+    u64 rin = st.rec + (u64)__popcll(T1 & lt) + (u64)__popcll(T2 & lt);
+    if (T3) {  // records shorter than 32 bytes (rare): full prefix of nt
+        u32 tot;
+        rin = st.rec + wave_prefix<7>(nt, tot);
+    }
+    // record start at the lane's first byte (for NUL offsets; only
+    // when a NUL is anywhere in this block's wave)
+    const u64 endp = nt ? lpos + lastT + 1 + ((SW >> lastT) & 1ull) : 0;
+    const u64 Zany = __ballot(k.Z != 0);
+    u64 rsin = st.rs;
+    if (Zany) {  // wave-uniform branch: the shuffle runs on every lane
+        const u64 rsj = __shfl(endp, J ? 63 - __clzll(J) : (int)lane);
+        if (J) rsin = rsj;
+    }
+
+    // per segment of the lane (between terminators): live lyric bytes,
+    // record starts, first NUL
+    u64 live = 0;
+    {
+        u64 E = TERM;
+        u32 lo = 0, cc = cin;
+        bool zz = zin;
+        u64 r = rin, rs = rsin;
+        for (;;) {
+            const u32 hi = E ? (u32)__ffsll((long long)E) - 1 : 64u;
+            const u64 seg = bits_hi(lo) & bits_lo(hi);
+            const u64 zs = k.Z & seg;
+            if (zs && !zz && a.want_nul && r < a.rec_cap) {
+                const u32 zp = (u32)__ffsll((long long)zs) - 1;
+                a.nulrel[r] = (u32)(lpos + zp - rs) + 1u;
+            }
+            bool ok = false;  // the record's third comma is at or before this segment's end
+            if (r >= a.first_rec && !zz) {
+                // commas after a NUL do not count (the C string ends there)
+                u64 x = Cu & seg & (zs ? bits_lo((u32)__ffsll((long long)zs) - 1) : ~0ull);
+                u32 from = lo;
+                ok = true;
+                for (u32 n = cc; n < 3; ++n) {
+                    if (!x) { ok = false; break; }
+                    from = (u32)__ffsll((long long)x);  // one past that comma
+                    x &= x - 1;
+                    // field 0 ends here (artist span for k_rec_fast)
+                    if (n == 0 && r < a.rec_cap) a.f0[r] = lpos + from - 1;
+                }
+                if (ok) {
+                    u64 lv = bits_hi(from) & bits_lo(hi);
+                    if (zs) lv &= bits_lo((u32)__ffsll((long long)zs) - 1);
+                    live |= lv;
+                    if (cc < 3 && r < a.rec_cap) {  // field 3 starts here; '"' there?
+                        const u32 q = from < 64 ? (u32)(k.Q >> from) & 1u : qnext;
+                        a.tss[r] = (lpos + from) | (q ? SPAN_Q : 0ull);
+                    }
+                }
+            }
+            if (!E) break;
+            if (r < a.rec_cap) {  // the record ends at this terminator
+                const u32 q = hi ? (u32)(k.Q >> (hi - 1)) & 1u : qprev;
+                u64 fl = q ? SPAN_Q : 0ull;
+                if (zz || zs) fl |= SPAN_NUL;  // the C string ends before: exact path
+                else if (!ok) fl |= SPAN_NOLINE;  // header, or < 3 commas (parse_csv_line fails)
+                a.tse[r] = (lpos + hi) | fl;
+            }
+            const u64 ns = lpos + hi + 1 + ((SW >> hi) & 1ull);
+            ++r;
+            if (r < a.rec_cap) a.rec_start[r] = ns;
+            rs = ns;
+            cc = 0;
+            zz = false;
+            lo = hi + 1;
+            E &= E - 1;
+        }
+    }
+    // carry the reader state to the next block (lane 63 has seen every byte)
+    {
+        const u32 cout = nt ? cq : min(cin + cq, 3u);
+        const bool zout = nt ? zq : (zin || zq);
+        st.p ^= (u32)__popcll(B) & 1u;
+        st.cr = readlane((u32)(CRu >> 63), 63);
+        st.c = readlane(cout, 63);
+        st.z = readlane((u32)zout, 63);
+        st.rec = rin + nt;
+        st.rec = readlane64(st.rec, 63);
+        if (Bh) st.rs = readlane64(endp, 63 - __clzll(Bh));
+    }
+    return live;
+}
+
 // The token phase of one 4 KiB block (process_lyrics, parallel_spotify.c:
 // 350-394): w = the lane's 64 token-byte bits, Tn = the 64 after them, S0 =
 // the counted token starts.  Shared by k_scan_csv and k_scan_tokens.
@@ -417,6 +560,107 @@ __device__ __forceinline__ void tok_phase(const ScanArgs &a, u64 ib, u64 lpos, u
     wsync();
 }
 
+// The split token pass, software-pipelined across blocks (k_scan_tokens):
+// tok_prep builds a block's token list (starts and lengths from the mask,
+// long words listed for k_long_insert) and issues the key loads of its first
+// batch; tok_probe counts one batch.  The next block's list is built while
+// the current block's last batch is still to be probed, so its first key
+// loads are in flight during that probe instead of stalling the next block.
+__device__ __forceinline__ u32 tok_prep(const ScanArgs &a, u64 ib, u64 L, u64 Lnext, u64 Lprev, u16 *list,
+                                        u64 &words, u32 &en, uint4 &kv, u32 &k4) {
+    const u32 lane = lane_id();
+    const u64 lpos = ib + lane * 64;
+    const u64 S0 = L & ~((L << 1) | (Lprev >> 63));
+    const u64 w = L, Tn = Lnext;
+    // runs: rK bit b = bytes b .. b+K-1 are token bytes (w = Tn:L)
+    const u64 r2 = w & shr128(w, Tn, 1), r2h = Tn & (Tn >> 1);
+    const u64 r3 = r2 & shr128(w, Tn, 2);
+    const u64 r4 = r2 & shr128(r2, r2h, 2), r4h = r2h & (r2h >> 2);
+    const u64 r8 = r4 & shr128(r4, r4h, 4), r8h = r4h & (r4h >> 4);
+    const u64 r16 = r8 & shr128(r8, r8h, 8);
+    const u64 r17 = r16 & shr128(w, Tn, 16);
+    const u64 r9 = r8 & shr128(w, Tn, 8);
+    const u64 sS = S0 & r3 & ~r9, sM = S0 & r9 & ~r17, sL = S0 & r17;
+    words += (u64)__popcll(S0 & r3);
+    if (__ballot(sL != 0)) {  // long words (> 16 bytes): positions for k_long_insert
+        const u32 nl = (u32)__popcll(sL);
+        u32 tot;
+        const u32 pre = wave_prefix<6>(nl, tot);
+        u64 base = 0;
+        if (lane == 0) base = atomicAdd((unsigned long long *)&a.ctr->l_occ, (unsigned long long)tot);
+        base = readlane64(base, 0) + pre;
+        for (u64 m = sL; m; m &= m - 1) {
+            const u32 b = (u32)__ffsll((long long)m) - 1;
+            if (base < a.l_cap) a.l_pos[base] = (lpos + b) | a.lpos_tag;
+            else atomicOr((unsigned long long *)&a.ctr->overflow, (unsigned long long)OVF_L);
+            ++base;
+        }
+    }
+    // 3..16-byte words into the wave's list: block offset | (length - 3) << 12
+    u64 m = sS | sM;
+    u32 nS;
+    u32 li = wave_prefix<5>((u32)__popcll(m), nS);
+    while (__ballot(m != 0)) {
+        if (m) {
+            const u32 b = (u32)__ffsll((long long)m) - 1;
+            m &= m - 1;
+            const u32 d0 = (u32)w, d1 = (u32)(w >> 32), d2 = (u32)Tn;
+            const u32 run = __builtin_amdgcn_alignbit(b >= 32 ? d2 : d1, b >= 32 ? d1 : d0, b & 31u);
+            const u32 len = (u32)__ffs(~run) - 1;  // 3..16
+            list[li++] = (u16)((lane * 64 + b) | ((len - 3) << 12));
+        }
+    }
+    wsync();
+    en = 0;
+    kv = make_uint4(0, 0, 0, 0);
+    k4 = 0;
+    if (lane < nS) {
+        en = list[lane];
+        const u32 *gp = reinterpret_cast<const u32 *>(a.buf + ((ib + (en & 4095u)) & ~3ull));
+        kv = *reinterpret_cast<const uint4 *>(gp);
+        k4 = gp[4];
+    }
+    return nS;
+}
+
+__device__ __forceinline__ void tok_probe(const ScanArgs &a, u64 ib, bool have, u32 e, uint4 v, u32 v4, u64 *skeys,
+                                          u32 *scnts, ulonglong2 *miss, u32 &nmiss, u32 *lcur) {
+    bool mis = false;
+    u64 k0 = 0, k1 = KMARK;
+    if (have) {
+        const u32 len = (e >> 12) + 3;
+        const u32 sh = (u32)(ib + (e & 4095u)) & 3u;
+        u64 x0 = mk64(__builtin_amdgcn_alignbyte(v.y, v.x, sh), __builtin_amdgcn_alignbyte(v.z, v.y, sh));
+        u64 x1 = mk64(__builtin_amdgcn_alignbyte(v.w, v.z, sh), __builtin_amdgcn_alignbyte(v4, v.w, sh));
+        const u32 nbits = 8 * len;  // 24..128
+        x0 &= bits_lo(nbits);
+        x1 = nbits <= 64 ? 0ull : (x1 & bits_lo(nbits - 64));
+        k0 = lower_tok8(x0);
+        k1 = lower_tok8(x1) | KMARK;
+        if (len <= 8) {
+            const u32 slot = lds_find8(skeys, k0);
+            if (slot != ~0u) atomicAdd(&scnts[slot], 1u);
+            else mis = true;
+        } else {
+            mis = true;
+        }
+    }
+    const u64 MB = __ballot(mis);
+    if (MB) {
+        const u32 nm = (u32)__popcll(MB);
+        if (nmiss + nm > Q_MISS) {
+            flush_miss(a, miss, nmiss, lcur);
+            nmiss = 0;
+        }
+        if (mis) {
+            const u32 at = nmiss + mbcnt(MB);
+            if (at < Q_MISS) miss[at] = make_ulonglong2(k0, k1);
+            else hbm_insert16(a, k0, k1, 1);
+        }
+        nmiss = min(nmiss + nm, (u32)Q_MISS);
+    }
+}
+
 // End of a counting workgroup: the wave's pending misses, total_words, the
 // LDS table flushed into the logs (counts encoded; full partitions: HBM
 // inserts) and the log lengths.
@@ -472,7 +716,6 @@ __device__ __forceinline__ void scan_body(const ScanArgs &a) {
     u16 *list = reinterpret_cast<u16 *>(wl);
     ulonglong2 *miss = reinterpret_cast<ulonglong2 *>(wl + Q_LIST * 2);
     u32 nmiss = 0;  // wave-uniform
-    const u64 lt = (1ull << lane) - 1ull;
 
     u32 *lcur = reinterpret_cast<u32 *>(smem + Q_TAB + Q_W * Q_WLDS);  // log cursors per key partition
     if (!SPLIT) {
@@ -560,137 +803,7 @@ __device__ __forceinline__ void scan_body(const ScanArgs &a) {
                 tl = ldg16(a.buf + ta);
             }
 
-            // ---- record structure (read_csv_record + parse_csv_line) ----
-            const u64 B = __ballot(__popcll(k.Q) & 1u);
-            const u32 pin = st.p ^ (mbcnt(B) & 1u);
-            const u64 inq = pxor_ex64(k.Q) ^ (pin ? ~0ull : 0ull);
-            const u64 CRu = k.CR & ~inq, NLu = k.NL & ~inq, Cu = k.C & ~inq;
-            // DPP and bpermute read the source lane's register only when that
-            // lane is active: every cross-lane move below runs on all 64 lanes,
-            // the per-lane choice is a select afterwards
-            const u64 CRp = from_prev(CRu) >> 63;
-            const u64 NLn = from_next(k.NL) & 1ull;
-            const u64 pCR = lane ? CRp : (u64)st.cr;
-            const u64 TERM = CRu | (NLu & ~((CRu << 1) | pCR));
-            const u32 tail_nl = ((tail.x & 0xFFu) == '\n' && (tvm & 1u)) ? 1u : 0u;
-            const u64 nNL = lane == 63 ? (u64)tail_nl : NLn;
-            // '"' at the byte after the lane (text start after a comma at byte
-            // 63) and at the byte before it (text end before a terminator at byte 0)
-            const u32 tail_q = ((tail.x & 0xFFu) == '"' && (tvm & 1u)) ? 1u : 0u;
-            const u64 Qnx = from_next(k.Q) & 1ull, Qpv = from_prev(k.Q) >> 63;
-            const u32 qnext = lane == 63 ? tail_q : (u32)Qnx;
-            const u32 qprev = lane ? (u32)Qpv : prevQ;
-            const u64 SW = CRu & ((k.NL >> 1) | (nNL << 63));  // '\r' terminators that swallow a '\n'
-
-            const u32 nt = (u32)__popcll(TERM);
-            const u32 lastT = nt ? 63u - (u32)__clzll(TERM) : 0u;
-            const u64 above = nt ? bits_hi(lastT + 1) : ~0ull;
-            const u32 cq = min((u32)__popcll(Cu & above), 3u);
-            const bool zq = (k.Z & above) != 0;
-            const u64 C1 = __ballot(cq >= 1), C2 = __ballot(cq >= 2), C3 = __ballot(cq >= 3);
-            const u64 Zb = __ballot(zq), Bh = __ballot(nt != 0);
-            const u64 J = Bh & lt;
-            u64 M;
-            u32 cin;
-            bool zin;
-            if (J) {
-                const u32 jl = 63u - (u32)__clzll(J);
-                M = lt & ~bits_lo(jl);
-                cin = 0;
-                zin = (Zb & M) != 0;
-            } else {
-                M = lt;
-                cin = st.c;
-                zin = st.z || ((Zb & M) != 0);
-            }
-            cin = min(cin + (u32)__popcll(C1 & M) + (u32)__popcll(C2 & M) + (u32)__popcll(C3 & M), 3u);
-            // record index at the lane's first byte: prefix of terminator counts
-            const u64 T1 = __ballot(nt >= 1), T2 = __ballot(nt >= 2), T3 = __ballot(nt >= 3);
-            u64 rin = st.rec + (u64)__popcll(T1 & lt) + (u64)__popcll(T2 & lt);
-            if (T3) {  // records shorter than 32 bytes (rare): full prefix of nt
-                u32 tot;
-                rin = st.rec + wave_prefix<7>(nt, tot);
-            }
-            // record start at the lane's first byte (for NUL offsets; only
-            // when a NUL is anywhere in this block's wave)
-            const u64 endp = nt ? lpos + lastT + 1 + ((SW >> lastT) & 1ull) : 0;
-            const u64 Zany = __ballot(k.Z != 0);
-            u64 rsin = st.rs;
-            if (Zany) {  // wave-uniform branch: the shuffle runs on every lane
-                const u64 rsj = __shfl(endp, J ? 63 - __clzll(J) : (int)lane);
-                if (J) rsin = rsj;
-            }
-
-            // per segment of the lane (between terminators): live lyric bytes,
-            // record starts, first NUL
-            u64 live = 0;
-            {
-                u64 E = TERM;
-                u32 lo = 0, cc = cin;
-                bool zz = zin;
-                u64 r = rin, rs = rsin;
-                for (;;) {
-                    const u32 hi = E ? (u32)__ffsll((long long)E) - 1 : 64u;
-                    const u64 seg = bits_hi(lo) & bits_lo(hi);
-                    const u64 zs = k.Z & seg;
-                    if (zs && !zz && a.want_nul && r < a.rec_cap) {
-                        const u32 zp = (u32)__ffsll((long long)zs) - 1;
-                        a.nulrel[r] = (u32)(lpos + zp - rs) + 1u;
-                    }
-                    bool ok = false;  // the record's third comma is at or before this segment's end
-                    if (r >= a.first_rec && !zz) {
-                        // commas after a NUL do not count (the C string ends there)
-                        u64 x = Cu & seg & (zs ? bits_lo((u32)__ffsll((long long)zs) - 1) : ~0ull);
-                        u32 from = lo;
-                        ok = true;
-                        for (u32 n = cc; n < 3; ++n) {
-                            if (!x) { ok = false; break; }
-                            from = (u32)__ffsll((long long)x);  // one past that comma
-                            x &= x - 1;
-                            // field 0 ends here (artist span for k_rec_fast)
-                            if (n == 0 && r < a.rec_cap) a.f0[r] = lpos + from - 1;
-                        }
-                        if (ok) {
-                            u64 lv = bits_hi(from) & bits_lo(hi);
-                            if (zs) lv &= bits_lo((u32)__ffsll((long long)zs) - 1);
-                            live |= lv;
-                            if (cc < 3 && r < a.rec_cap) {  // field 3 starts here; '"' there?
-                                const u32 q = from < 64 ? (u32)(k.Q >> from) & 1u : qnext;
-                                a.tss[r] = (lpos + from) | (q ? SPAN_Q : 0ull);
-                            }
-                        }
-                    }
-                    if (!E) break;
-                    if (r < a.rec_cap) {  // the record ends at this terminator
-                        const u32 q = hi ? (u32)(k.Q >> (hi - 1)) & 1u : qprev;
-                        u64 fl = q ? SPAN_Q : 0ull;
-                        if (zz || zs) fl |= SPAN_NUL;  // the C string ends before: exact path
-                        else if (!ok) fl |= SPAN_NOLINE;  // header, or < 3 commas (parse_csv_line fails)
-                        a.tse[r] = (lpos + hi) | fl;
-                    }
-                    const u64 ns = lpos + hi + 1 + ((SW >> hi) & 1ull);
-                    ++r;
-                    if (r < a.rec_cap) a.rec_start[r] = ns;
-                    rs = ns;
-                    cc = 0;
-                    zz = false;
-                    lo = hi + 1;
-                    E &= E - 1;
-                }
-            }
-            // carry the reader state to the next block (lane 63 has seen every byte)
-            {
-                const u32 cout = nt ? cq : min(cin + cq, 3u);
-                const bool zout = nt ? zq : (zin || zq);
-                st.p ^= (u32)__popcll(B) & 1u;
-                st.cr = readlane((u32)(CRu >> 63), 63);
-                st.c = readlane(cout, 63);
-                st.z = readlane((u32)zout, 63);
-                st.rec = rin + nt;
-                st.rec = readlane64(st.rec, 63);
-                if (Bh) st.rs = readlane64(endp, 63 - __clzll(Bh));
-            }
-
+            const u64 live = struct_block(a, st, k, tail, tvm, lpos, prevQ);
             prevQ = readlane((u32)(k.Q >> 63), 63);
             if (SPLIT) {
                 // the lyric token bytes for k_scan_tokens (every lane of the
@@ -712,7 +825,88 @@ __device__ __forceinline__ void scan_body(const ScanArgs &a) {
 }
 
 __global__ __launch_bounds__(Q_T, 1) void k_scan_csv(ScanArgs a) { scan_body<0>(a); }
-__global__ __launch_bounds__(SA_T, SA_MINW) void k_scan_struct(ScanArgs a) { scan_body<1>(a); }
+
+// k_scan_struct: the split scan's structure pass.  Each wave walks its
+// blocks (the 4 KiB blocks of chunks gw, gw + nw, ...) with the input loaded
+// SA_PF blocks ahead (1: as k_scan_csv; 2: two blocks in flight -- one
+// block's structure work alone did not cover the HBM latency at these wave
+// counts).  Per block: byte classes, record structure (struct_block), and the
+// lyric token-byte mask for k_scan_tokens.
+#ifndef SA_PF
+#define SA_PF 2
+#endif
+__global__ __launch_bounds__(SA_T, SA_MINW) void k_scan_struct(ScanArgs a) {
+    const u32 lane = lane_id();
+    const u32 wib = threadIdx.x >> 6;
+    const u32 gw = __builtin_amdgcn_readfirstlane(blockIdx.x * (SA_T / 64) + wib);
+    const u32 nw = gridDim.x * (SA_T / 64);
+    if (gw >= a.nchunks) return;
+    // block s of this wave: chunk gw + (s / 4) nw, block s % 4 of it (past the
+    // segment end: no block -- its loads re-read the wave's first block)
+    auto blk_at = [&](u32 s, u64 &ib) -> bool {
+        const u32 c = gw + (s >> 2) * nw;
+        ib = a.seg_begin + (u64)c * MSA_CHUNK + (u64)(s & 3u) * Q_BLK;
+        return c < a.nchunks && ib < a.seg_end;
+    };
+    auto load_blk = [&](u32 s, uint4 (&v)[4], uint4 &t) {
+        u64 ib;
+        if (!blk_at(s, ib)) ib = a.seg_begin + (u64)gw * MSA_CHUNK;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = ldg16(a.buf + ib + lane * 64 + 16 * q);
+        // a vector load (a uniform address would become a scalar load, which
+        // drops the low address bits -- a.buf is a view at any alignment)
+        u64 ta = ib + Q_BLK < a.seg_end ? ib + Q_BLK : ib;
+        pin64(ta);
+        t = ldg16(a.buf + ta);
+    };
+    uint4 cur[4], tl;
+    load_blk(0, cur, tl);
+#if SA_PF > 1
+    uint4 nx[4], ntl;
+    load_blk(1, nx, ntl);
+#endif
+    State st{};
+    bool rare_chunk = true;
+    u32 prevQ = 0;
+    for (u32 s = 0;; ++s) {
+        u64 ib;
+        const bool valid = blk_at(s, ib);
+        const u32 c = gw + (s >> 2) * nw;
+        if (c >= a.nchunks) break;
+        if ((s & 3u) == 0) {  // a chunk starts: its reader state and '"' before it
+            st = sload_state(a.carry + c);
+            rare_chunk = !a.sums || ((*sload(&a.sums[c].h[0]) >> 22) & 1u);
+            prevQ = 0;
+            if (ib > a.seg_begin) {
+                const size_t pa = (size_t)(a.buf + ib - 1);
+                const u32 b = (*sload(reinterpret_cast<const u32 *>(pa & ~(size_t)3)) >> (8 * (pa & 3))) & 0xFFu;
+                prevQ = (u32)(b == '"');
+            }
+        }
+        const uint4 tail = tl;
+        const u64 cend = min(a.seg_begin + (u64)c * MSA_CHUNK + (u64)MSA_CHUNK, a.seg_end);
+        const u64 lpos = ib + lane * 64;
+        const u64 rem = valid && cend > lpos ? cend - lpos : 0;
+        const Masks k = classify64x(cur, (u32)min(rem, (u64)64), rare_chunk);
+        // the block's bytes now live in the masks: rotate the prefetch
+#if SA_PF > 1
+#pragma unroll
+        for (int q = 0; q < 4; ++q) cur[q] = nx[q];
+        tl = ntl;
+        load_blk(s + 2, nx, ntl);
+#else
+        load_blk(s + 1, cur, tl);
+#endif
+        if (!valid) continue;
+        const u64 tpos = ib + Q_BLK;
+        const u32 tvm = tpos < a.seg_end ? (a.seg_end - tpos >= 16 ? 0xFFFFu : (1u << (a.seg_end - tpos)) - 1u) : 0u;
+        const u64 live = struct_block(a, st, k, tail, tvm, lpos, prevQ);
+        prevQ = readlane((u32)(k.Q >> 63), 63);
+        // the lyric token bytes (every lane of the block writes its word, past
+        // the segment end too: zero)
+        a.lmask[1 + ((ib - a.seg_begin) >> 6) + lane] = k.T & live;
+    }
+}
 
 // k_scan_tokens: the token phase of the split scan over k_scan_struct's
 // lmask -- no reader state, no byte classes: a wave per 4 KiB block (grid
@@ -720,6 +914,9 @@ __global__ __launch_bounds__(SA_T, SA_MINW) void k_scan_struct(ScanArgs a) { sca
 // input, counted in the workgroup's LDS table as in k_scan_csv.  The next
 // block's mask words and one 16-byte load per lane of its bytes (the keys'
 // cache lines) are in flight while a block is counted.
+#ifndef TOK_PIPE
+#define TOK_PIPE 1
+#endif
 __global__ __launch_bounds__(Q_T, 1) void k_scan_tokens(ScanArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     u64 *skeys = reinterpret_cast<u64 *>(smem);
@@ -754,6 +951,51 @@ __global__ __launch_bounds__(Q_T, 1) void k_scan_tokens(ScanArgs a) {
         Lp = a.lmask[wi];  // lmask[0] is the zero pad
         warm = ldg16(a.buf + a.seg_begin + blk * Q_BLK + lane * 64);
     };
+#if TOK_PIPE
+    u64 blk = gw;
+    u32 nS = 0, en = 0, k4 = 0;
+    uint4 kv = make_uint4(0, 0, 0, 0);
+    u64 ib = 0;
+    if (blk < nblk) {
+        fetch(blk);
+        ib = a.seg_begin + blk * Q_BLK;
+        nS = tok_prep(a, ib, Lc, Ln, Lp, list, words, en, kv, k4);
+    }
+    while (blk < nblk) {
+        const u64 next = blk + nw;
+        if (next < nblk) fetch(next);  // the next block's mask words and key lines, in flight during this block
+        const u64 ibc = ib;
+        const u32 nSc = nS, nb = (nS + 63) >> 6;
+        if (nb == 0 && next < nblk) {
+            asm volatile("" ::"v"(warm.x));
+            ib = a.seg_begin + next * Q_BLK;
+            nS = tok_prep(a, ib, Lc, Ln, Lp, list, words, en, kv, k4);
+        }
+        for (u32 bt = 0; bt < nb; ++bt) {
+            const u32 e = en;
+            const uint4 v = kv;
+            const u32 v4 = k4;
+            const bool have = bt * 64 + lane < nSc;
+            if (bt + 1 < nb) {
+                if ((bt + 1) * 64 + lane < nSc) {
+                    en = list[(bt + 1) * 64 + lane];
+                    const u32 *gp = reinterpret_cast<const u32 *>(a.buf + ((ibc + (en & 4095u)) & ~3ull));
+                    kv = *reinterpret_cast<const uint4 *>(gp);
+                    k4 = gp[4];
+                }
+            } else if (next < nblk) {
+                // every entry of this block's list is read: the next block's list
+                // goes into the same buffer, its first keys are loaded before this
+                // last batch is probed
+                asm volatile("" ::"v"(warm.x));
+                ib = a.seg_begin + next * Q_BLK;
+                nS = tok_prep(a, ib, Lc, Ln, Lp, list, words, en, kv, k4);
+            }
+            tok_probe(a, ibc, have, e, v, v4, skeys, scnts, miss, nmiss, lcur);
+        }
+        blk = next;
+    }
+#else
     if (gw < nblk) fetch(gw);
     for (u64 blk = gw; blk < nblk; blk += nw) {
         const u64 L = Lc, Lnext = Ln, Lprev = Lp;
@@ -764,6 +1006,7 @@ __global__ __launch_bounds__(Q_T, 1) void k_scan_tokens(ScanArgs a) {
         const u64 S0 = L & ~((L << 1) | (Lprev >> 63));
         tok_phase(a, ib, lpos, L, Lnext, S0, skeys, scnts, list, miss, nmiss, lcur, words);
     }
+#endif
     tok_epilogue(a, skeys, scnts, miss, nmiss, lcur, words);
 }
 

@@ -60,9 +60,17 @@ __global__ __launch_bounds__(SCAN_T) void k_scan_reduce(ScanJobs js) {
 
 // exclusive scan of the block sums in place: per-thread runs, then a block
 // scan of the run totals (wave shuffles + wave totals)
+__global__ void k_scan_zero_totals(ScanJobs js) {
+    if (threadIdx.x < 2 && js.j[threadIdx.x].total)
+        __hip_atomic_store(js.j[threadIdx.x].total, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __global__ __launch_bounds__(SCAN_T) void k_scan_top(ScanJobs js) {
     const ScanJob &J = js.j[blockIdx.y];
-    if (!J.n) return;
+    if (!J.n) {
+        if (threadIdx.x == 0 && J.total) __hip_atomic_store(J.total, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
     __shared__ u64 wtot[SCAN_T / 64];
     const u64 nb = (J.n + SCAN_TILE - 1) / SCAN_TILE;
     const u64 per = (nb + SCAN_T - 1) / SCAN_T;
@@ -79,7 +87,11 @@ __global__ __launch_bounds__(SCAN_T) void k_scan_top(ScanJobs js) {
     __syncthreads();
     u64 acc = x - s;
     for (u32 i = 0; i < w; ++i) acc += wtot[i];
-    if (threadIdx.x == SCAN_T - 1 && J.total) *J.total = acc + s;
+    // the total may live in the run's Counters, whose other fields kernels on
+    // other streams update meanwhile (e.g. the column spans beside the token
+    // pass): a write-through store, so no dirty copy of that line stays in
+    // this XCD's L2 to be written back over their updates later
+    if (threadIdx.x == SCAN_T - 1 && J.total) __hip_atomic_store(J.total, acc + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (u64 i = a; i < b; ++i) { const u64 v = J.bsum[i]; J.bsum[i] = acc; acc += v; }
 }
 
@@ -122,13 +134,11 @@ hipError_t msa_exclusive_scan2(const u64 *in, u64 n, u64 *out, u64 *bsum, u64 *t
     js.j[0] = ScanJob{in, out, bsum, total, n};
     js.j[1] = ScanJob{in2, out2, bsum2, total2, in2 ? n2 : 0};
     const u32 ny = in2 ? 2 : 1;
-    for (u32 k = 0; k < ny; ++k)
-        if (js.j[k].n == 0 && js.j[k].total) {
-            hipError_t e = hipMemsetAsync(js.j[k].total, 0, sizeof(u64), s);
-            if (e != hipSuccess) return e;
-        }
     const u64 nmax = std::max(js.j[0].n, js.j[1].n);
-    if (nmax == 0) return hipSuccess;
+    if (nmax == 0) {  // empty: the totals are 0 (write-through, as k_scan_top stores them)
+        hipLaunchKernelGGL(k_scan_zero_totals, dim3(1), dim3(64), 0, s, js);
+        return hipGetLastError();
+    }
     const u64 nb = (nmax + SCAN_TILE - 1) / SCAN_TILE;
     hipLaunchKernelGGL(k_scan_reduce, dim3((u32)nb, ny), dim3(SCAN_T), 0, s, js);
     hipLaunchKernelGGL(k_scan_top, dim3(1, ny), dim3(SCAN_T), 0, s, js);
@@ -2127,7 +2137,7 @@ __global__ __launch_bounds__(CR_T) void k_mr_corank(const u64 *__restrict__ K2, 
                                                    const u8 *__restrict__ in, const u64 *__restrict__ kptr,
                                                    u32 *__restrict__ order, u64 *__restrict__ len) {
     __shared__ u64 s2[CR_T], s1[CR_T], s0[CR_T];
-    __shared__ u64 win[2][2];
+    __shared__ u64 win[2];
     const u32 t = threadIdx.x;
     const u64 tb = ts[blockIdx.x], te = ts[blockIdx.x + 1];
     u32 p = 0, ph = nblk;  // the tile's block: rec_base[p] <= tb < rec_base[p + 1]
@@ -2155,10 +2165,11 @@ __global__ __launch_bounds__(CR_T) void k_mr_corank(const u64 *__restrict__ K2, 
                 if (go) lo = m + 1;
                 else hi = m;
             }
-            win[q & 1][t] = lo;
+            win[t] = lo;
         }
         __syncthreads();
-        const u64 L = win[q & 1][0], H = win[q & 1][1];
+        const u64 L = win[0], H = win[1];
+        __syncthreads();  // read by every thread before the next block's window is stored
         less += L - qb;
         for (u64 c0 = L; c0 < H; c0 += CR_T) {
             const u32 cn = (u32)min((u64)CR_T, H - c0);

@@ -1440,7 +1440,10 @@ static int wfail(msa_wcs *w, int code, const char *fmt, ...) {
     } while (0)
 
 static void wfree(void *&p) {
-    if (p) (void)hipFree(p);
+    if (p) {  // nothing in flight may still touch it (its memory can be handed out again at once)
+        (void)hipDeviceSynchronize();
+        (void)hipFree(p);
+    }
     p = nullptr;
 }
 template <typename T>

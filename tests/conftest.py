@@ -99,6 +99,36 @@ def files_equal(a, b, chunk=1 << 24):
                 return True
 
 
+def table_counts(path):
+    """{key: count} of a word_counts.csv / top_artists.csv (write_csv_entry lines,
+    parallel_spotify.c:307-319)."""
+    out = {}
+    with open(path, "rb") as f:
+        f.readline()
+        for line in f:
+            j = line.rindex(b'",')
+            out[line[1:j].replace(b'""', b'"')] = int(line[j + 2:])
+    return out
+
+
+def table_bytes(header, counts):
+    """The table as write_table_csv writes it: entry_compare_desc order (count
+    desc, then strcmp; parallel_spotify.c:176-188), write_csv_entry lines."""
+    rows = sorted(counts.items(), key=lambda kv: (-kv[1], kv[0]))
+    return header + b"".join(b'"' + k.replace(b'"', b'""') + b'",' + str(v).encode() + b"\n" for k, v in rows)
+
+
+def hash_file(path, skip_first_line, h):
+    with open(path, "rb") as f:
+        if skip_first_line:
+            f.readline()
+        while True:
+            b = f.read(1 << 24)
+            if not b:
+                return
+            h.update(b)
+
+
 def run_oracle(csv_path, outdir, ranks=1, word_limit=0, artist_limit=0, timeout=300):
     """The CPU oracle (C restatement of parallel_spotify.c, virtual np)."""
     if not os.path.exists(ORACLE):

@@ -12,7 +12,8 @@ import sys
 
 import pytest
 
-from conftest import PKG, REPO, files_equal, read_outputs, run_oracle, run_with_heartbeat
+from conftest import (PKG, REPO, files_equal, hash_file, read_outputs, run_oracle, run_with_heartbeat, say,
+                      table_bytes, table_counts)
 
 pytestmark = pytest.mark.gpu
 
@@ -266,3 +267,100 @@ def test_rank_after_import_ranked_topk(msa_mod):
         assert ctx.ranked(msa.MSA_TABLE_ARTISTS) == full_a[:k]
         with pytest.raises(msa.MsaError):
             ctx.export_partitions(msa.MSA_TABLE_WORDS, 2)
+
+
+# ---- BASELINE configs[3] at its stated size: the 100M-song corpus (~23.7 GB)
+# through the C host as a 4-rank world on the one GPU (shm transport).  The
+# generator's songs are independent draws, so the corpus is the concatenation
+# of its song ranges and the np = 1 answer is the sum of the ranges' answers:
+# the oracle runs on 5 ranges of 20M songs in parallel (each with the header
+# line), their tables are summed and ranked by entry_compare_desc
+# (parallel_spotify.c:176-188: count desc, then strcmp) and written as
+# write_csv_entry does (307-319); the split files are the header line plus
+# the ranges' bodies in order.  Everything lives in /dev/shm (host memory).
+C3_FULL_SONGS = 100_000_000
+C3_FULL_RANGES = 5
+
+
+@pytest.mark.timeout(1500)
+def test_configs3_full_size_c_host_four_ranks(msa_mod, tmp_path):
+    """configs[3] at full size (100M songs, ~23.7 GB, one logical CSV):
+    bin/parallel_spotify --processes 4 (four ranks on the one GPU, shm
+    exchanges) -- word_counts.csv, top_artists.csv, both split files and the
+    totals identical to the oracle's np = 1 answer."""
+    import shutil
+    import tempfile
+    import xxhash
+
+    base = "/dev/shm" if os.path.isdir("/dev/shm") else str(tmp_path)
+    d = tempfile.mkdtemp(dir=base, prefix="msa_c3full_")
+    try:
+        big = os.path.join(d, "c3full.csv")
+        header = None
+        procs = []
+        with open(big, "wb") as f:
+            for k in range(C3_FULL_RANGES):
+                lo, hi = C3_FULL_SONGS * k // C3_FULL_RANGES, C3_FULL_SONGS * (k + 1) // C3_FULL_RANGES
+                data = msa_mod.gen_corpus(C3_FULL_SONGS, mode="zipf", seed=1, vocab=50000, n_artists=5000,
+                                          words_per_song=30, first_song=lo, count=hi - lo)
+                f.write(data)
+                if k == 0:
+                    header = data[:data.index(b"\n") + 1]
+                rp = os.path.join(d, f"r{k}.csv")
+                with open(rp, "wb") as g:
+                    if k:
+                        g.write(header)
+                    g.write(data)
+                del data
+                od = os.path.join(d, f"o{k}")
+                procs.append((rp, od, subprocess.Popen([os.path.join(REPO, "oracle", "msa_oracle"), rp, "--output-dir", od],
+                                                       stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)))
+                say(f"  [configs3 full: range {k} generated, oracle started]")
+        assert os.path.getsize(big) > 20 * (1 << 30)
+        words, artists, songs, total_words = {}, {}, 0, 0
+        hashes, hdrs, names = {}, {}, None
+        for k, (rp, od, p) in enumerate(procs):
+            while True:
+                try:
+                    _, err = p.communicate(timeout=30)
+                    break
+                except subprocess.TimeoutExpired:
+                    say(f"  [configs3 full: oracle range {k} running]")
+            assert p.returncode == 0, err[-2000:]
+            for key, v in table_counts(os.path.join(od, "word_counts.csv")).items():
+                words[key] = words.get(key, 0) + v
+            for key, v in table_counts(os.path.join(od, "top_artists.csv")).items():
+                artists[key] = artists.get(key, 0) + v
+            with open(os.path.join(od, "performance_metrics.json")) as f:
+                m = json.load(f)
+            songs += m["total_songs"]
+            total_words += m["total_words"]
+            sd = os.path.join(od, "split_columns")
+            names = sorted(os.listdir(sd))
+            for n in names:
+                if k == 0:
+                    with open(os.path.join(sd, n), "rb") as f:
+                        hdrs[n] = f.readline()
+                    hashes[n] = xxhash.xxh3_128(hdrs[n])
+                hash_file(os.path.join(sd, n), True, hashes[n])
+            shutil.rmtree(od)
+            os.remove(rp)
+        out = os.path.join(d, "out")
+        cli = os.path.join(PKG, "bin", "parallel_spotify")
+        env = dict(os.environ, MSA_TRANSPORT="shm")
+        p = run_with_heartbeat([cli, big, "--output-dir", out, "--processes", "4"], 900, "parallel_spotify -np 4 (23.7 GB)",
+                               env=env)
+        assert p.returncode == 0, p.stderr[-3000:]
+        assert open(os.path.join(out, "word_counts.csv"), "rb").read() == table_bytes(b"word,count\n", words)
+        assert open(os.path.join(out, "top_artists.csv"), "rb").read() == table_bytes(b"artist,count\n", artists)
+        with open(os.path.join(out, "performance_metrics.json")) as f:
+            m = json.load(f)
+        assert (m["processes"], m["total_songs"], m["total_words"]) == (4, songs, total_words)
+        sd = os.path.join(out, "split_columns")
+        assert sorted(os.listdir(sd)) == names
+        for n in names:
+            h = xxhash.xxh3_128()
+            hash_file(os.path.join(sd, n), False, h)
+            assert h.digest() == hashes[n].digest(), n
+    finally:
+        shutil.rmtree(d, ignore_errors=True)

@@ -89,3 +89,51 @@ def test_reference_is_np_dependent():
                                       r1["total_songs"] != r4["total_songs"]):
             diffs += 1
     assert diffs >= 1
+
+
+def test_song_ranges_sum_to_the_whole(msa_mod, tmp_path):
+    """The checker of test_gpu_dist.py's full-size configs[3] test: the oracle
+    over a corpus's song ranges (each with the header line), tables summed and
+    ranked again (conftest.table_counts / table_bytes), split bodies
+    concatenated -- byte-identical to the oracle over the whole corpus."""
+    import xxhash
+
+    from conftest import hash_file, table_bytes, table_counts
+
+    total, parts = 20000, 4
+    whole = b""
+    header = None
+    words, artists, songs, twords, hashes = {}, {}, 0, 0, {}
+    for k in range(parts):
+        lo, hi = total * k // parts, total * (k + 1) // parts
+        data = msa_mod.gen_corpus(total, mode="zipf", seed=1, vocab=50000, n_artists=5000, words_per_song=30,
+                                  first_song=lo, count=hi - lo)
+        whole += data
+        if k == 0:
+            header = data[:data.index(b"\n") + 1]
+        rp = tmp_path / f"r{k}.csv"
+        rp.write_bytes((header if k else b"") + data)
+        od = tmp_path / f"o{k}"
+        assert run_oracle(str(rp), str(od)).returncode == 0
+        for key, v in table_counts(str(od / "word_counts.csv")).items():
+            words[key] = words.get(key, 0) + v
+        for key, v in table_counts(str(od / "top_artists.csv")).items():
+            artists[key] = artists.get(key, 0) + v
+        m = json.loads((od / "performance_metrics.json").read_text())
+        songs += m["total_songs"]
+        twords += m["total_words"]
+        for n in sorted(os.listdir(od / "split_columns")):
+            p = str(od / "split_columns" / n)
+            if k == 0:
+                hashes[n] = xxhash.xxh3_128(open(p, "rb").readline())
+            hash_file(p, True, hashes[n])
+    wp = tmp_path / "whole.csv"
+    wp.write_bytes(whole)
+    assert run_oracle(str(wp), str(tmp_path / "ow")).returncode == 0
+    exp = read_outputs(str(tmp_path / "ow"))
+    assert table_bytes(b"word,count\n", words) == exp["word_counts.csv"]
+    assert table_bytes(b"artist,count\n", artists) == exp["top_artists.csv"]
+    m = json.loads((tmp_path / "ow" / "performance_metrics.json").read_text())
+    assert (songs, twords) == (m["total_songs"], m["total_words"])
+    for n, h in hashes.items():
+        assert h.digest() == xxhash.xxh3_128(exp["split"][n]).digest(), n
