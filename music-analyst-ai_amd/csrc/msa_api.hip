@@ -170,6 +170,7 @@ struct msa_ctx {
     // merge of received blocks: the count tables still hold this GPU's own
     // keys, so the table is ranked-only until the next split / partition import
     int ranked_only = 0;
+    u64 split_attempts = 0;  // diagnostic (msa_debug_stat "split_attempts")
     // scan scratch
     DevBuf sums, carry, btot, bstate, small;  // small: Fn total + 2 States + ...
     // CSV records
@@ -373,7 +374,10 @@ static hipError_t ensure(DevBuf &b, size_t bytes, bool zero = false) {
     hipError_t e = hipMalloc(&b.p, want);
     if (e != hipSuccess) return e;
     b.cap = want;
-    if (zero) e = hipMemset(b.p, 0, want);
+    // zeroed before any library stream can use it: the library's streams are
+    // non-blocking, so nothing orders them after a null-stream memset -- wait
+    // for it here
+    if (zero && (e = hipMemset(b.p, 0, want)) == hipSuccess) e = hipDeviceSynchronize();
     return e;
 }
 
@@ -1095,6 +1099,7 @@ static int split_once(msa_ctx *c, int flags) {
 static int do_split(msa_ctx *c, int flags) {
     int rc = MSA_OK;
     for (int attempt = 0; attempt < 12; ++attempt) {
+        ++c->split_attempts;
         rc = split_once(c, flags);
         if (rc != MSA_ERR_CAPACITY || !(c->h_ctr.overflow & kSplitOvf)) return rc;
         grow_tables(c, kSplitOvf);
@@ -1654,6 +1659,7 @@ int msa_load_csv(msa_ctx *c, const void *host, size_t n) {
     HIPC(c, ensure(c->in_own, n + MSA_INPUT_PAD));
     if (n) HIPC(c, hipMemcpy(c->in_own.p, host, n, hipMemcpyHostToDevice));
     HIPC(c, hipMemset(c->in_own.as<char>() + n, 0, MSA_INPUT_PAD));
+    HIPC(c, hipDeviceSynchronize());  // null-stream work: not ordered with the library's non-blocking streams
     c->in = c->in_own.as<u8>();
     c->n = n;
     c->in_base = c->in;
@@ -2238,6 +2244,16 @@ extern "C" int msa_debug_stat(msa_ctx *c, const char *name, uint64_t *v) {
     else if (n == "s_claimed") *v = k.s_claimed;
     else if (n == "m_claimed") *v = k.m_claimed;
     else if (n == "l_claimed") *v = k.l_claimed;
+    else if (n == "split_attempts") *v = c->split_attempts;
+    else if (n == "s_table_used" || n == "m_table_used") {  // occupied slots, counted on the host
+        const bool sm = n == "s_table_used";
+        const u64 slots = sm ? c->s_slots : c->m_slots, w = sm ? 2 : 4;
+        std::vector<u64> t(slots * w);
+        if (slots) HIPC(c, hipMemcpy(t.data(), sm ? c->s_tab.p : c->m_tab.p, slots * w * 8, hipMemcpyDeviceToHost));
+        u64 used = 0;
+        for (u64 i = 0; i < slots; ++i) used += t[i * w] != 0;
+        *v = used;
+    }
     else return MSA_ERR_ARG;
     return MSA_OK;
 }

@@ -833,7 +833,7 @@ __global__ __launch_bounds__(Q_T, 1) void k_scan_csv(ScanArgs a) { scan_body<0>(
 // counts).  Per block: byte classes, record structure (struct_block), and the
 // lyric token-byte mask for k_scan_tokens.
 #ifndef SA_PF
-#define SA_PF 2
+#define SA_PF 1
 #endif
 __global__ __launch_bounds__(SA_T, SA_MINW) void k_scan_struct(ScanArgs a) {
     const u32 lane = lane_id();
@@ -915,7 +915,7 @@ __global__ __launch_bounds__(SA_T, SA_MINW) void k_scan_struct(ScanArgs a) {
 // block's mask words and one 16-byte load per lane of its bytes (the keys'
 // cache lines) are in flight while a block is counted.
 #ifndef TOK_PIPE
-#define TOK_PIPE 1
+#define TOK_PIPE 0
 #endif
 __global__ __launch_bounds__(Q_T, 1) void k_scan_tokens(ScanArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];

@@ -30,7 +30,7 @@ ctx.split_columns(False)
 import ctypes
 ctx.lib.msa_debug_stat.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint64)]
 dbg = {}
-for nm in ("k3_misses", "total_words", "overflow", "s_claimed", "m_claimed"):
+for nm in ("k3_misses", "total_words", "overflow", "s_claimed", "m_claimed", "s_table_used", "m_table_used", "split_attempts"):
     v = ctypes.c_uint64(0)
     ctx.lib.msa_debug_stat(ctx.h, nm.encode(), ctypes.byref(v))
     dbg[nm] = v.value

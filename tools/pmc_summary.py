@@ -27,7 +27,7 @@ KERNELS = ["k_scan_csv", "k_scan_struct", "k_scan_tokens", "k_miss_agg", "k_chun
            "k_artist_count", "k_tile_sort", "k_merge_pass",
            # the per-song counter (tools/pmc_wcs.sh, --wcs)
            "k_wcs_wrows", "k_wcs_rows", "k_wcs_map", "k_wcs_emit", "k_wcs_validate", "k_wcs_pairs"]
-PASSES = ["fetch", "write", "sq", "atomic"]
+PASSES = ["fetch", "write", "sq", "atomic", "sq2"]
 
 
 def build_id():
