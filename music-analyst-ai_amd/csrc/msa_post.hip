@@ -1983,8 +1983,11 @@ __global__ __launch_bounds__(256) void k_rank_place(const u64 *__restrict__ K2, 
 // tiles in a register.  Beside the text column's gather every dependent L2 miss
 // of k_rank_count's per-key loads waited behind the gather's traffic (386 us
 // for 33 K words against ~0.1 ms alone); here each workgroup issues T bulk
-// tile loads, each one tile ahead.  cnt[i] = smaller keys | 1 << 31 when an
-// equal key (all 24 bytes) exists elsewhere.
+// tile loads, each one tile ahead.  Keys equal in all 24 bytes (long words
+// sharing 16 bytes and a count) are ordered here too, by full_cmp against the
+// equal run the search lands on in each tile (rare; it had been a global
+// binary search per tile in k_rank_put: 0.11 ms of the words' chain).
+// cnt[i] = the key's rank.
 // Small workgroups (RT_T threads, RT_T keys, one 24 KiB tile buffer in LDS,
 // the next tile held in registers): the gather's workgroups fill every CU, and
 // a workgroup of this size fits in what one finished gather workgroup frees.
@@ -1996,7 +1999,10 @@ __global__ __launch_bounds__(256) void k_rank_place(const u64 *__restrict__ K2, 
 #endif
 #define RT_K (TS_N / RT_T)  // tile elements per thread
 __global__ __launch_bounds__(RT_T) void k_rank_total(const u64 *__restrict__ K2, const u64 *__restrict__ K1,
-                                                     const u64 *__restrict__ K0, u64 n, u32 *__restrict__ cnt) {
+                                                     const u64 *__restrict__ K0, const u32 *__restrict__ V, u64 n,
+                                                     const u64 *__restrict__ ref, const u8 *buf, const u8 *extra,
+                                                     const u64 *l_pos, const u32 *l_len, const u8 *arena,
+                                                     const u64 *key_off, const u32 *key_len, u32 *__restrict__ cnt) {
     __shared__ u64 s2[TS_N], s1[TS_N], s0[TS_N];
     const u32 T = (u32)((n + TS_N - 1) / TS_N);
     const u32 t = threadIdx.x;
@@ -2014,7 +2020,7 @@ __global__ __launch_bounds__(RT_T) void k_rank_total(const u64 *__restrict__ K2,
         if (e < n) { p2[k] = K2[e]; p1[k] = K1[e]; p0[k] = K0[e]; }
     }
     u32 less = 0;
-    bool tie = false;
+    u64 me = ~0ull;  // this entry's ref, loaded at its first tie
     for (u32 v = 0; v < T; ++v) {
 #pragma unroll
         for (int k = 0; k < RT_K; ++k) {
@@ -2039,50 +2045,30 @@ __global__ __launch_bounds__(RT_T) void k_rank_total(const u64 *__restrict__ K2,
                 else hi = m;
             }
             less += lo;
-            if (v == u) {
-                tie |= (j > 0 && s2[j - 1] == a2 && s1[j - 1] == a1 && s0[j - 1] == a0) ||
-                       (j + 1 < un && s2[j + 1] == a2 && s1[j + 1] == a1 && s0[j + 1] == a0);
-            } else {
-                tie |= lo < un && s2[lo] == a2 && s1[lo] == a1 && s0[lo] == a0;
+            // the run of keys equal to this one in tile v (itself excluded):
+            // the ones whose full key is smaller come first
+            for (u32 q = lo; q < un && s2[q] == a2 && s1[q] == a1 && s0[q] == a0; ++q) {
+                if (v == u && q == j) continue;
+                if (me == ~0ull) me = ref[V[i]];
+                const u64 vb = (u64)v * TS_N;
+                if (full_cmp(ref[V[vb + q]], me, a1, a0, buf, extra, l_pos, l_len, arena, key_off, key_len) < 0) ++less;
             }
         }
         __syncthreads();  // tile v read by every thread before the next one is stored
     }
-    if (mine) cnt[i] = less | (tie ? 0x80000000u : 0u);
+    if (mine) cnt[i] = less;
 }
 
-// rank = cnt[i]; tied keys (rare) ordered by full_cmp among the equal keys of
-// every tile (found by a binary search of the tile in global memory)
-__global__ __launch_bounds__(256) void k_rank_put(const u64 *__restrict__ K2, const u64 *__restrict__ K1,
-                                                  const u64 *__restrict__ K0, const u32 *__restrict__ V, u64 n,
-                                                  const u32 *__restrict__ cnt, const u64 *__restrict__ ref,
-                                                  const u8 *buf, const u8 *extra, const u64 *l_pos, const u32 *l_len,
-                                                  const u8 *arena, const u64 *key_off, const u32 *key_len,
+// order[rank] = entry id, len[rank] = its key length
+__global__ __launch_bounds__(256) void k_rank_put(const u64 *__restrict__ K1, const u64 *__restrict__ K0,
+                                                  const u32 *__restrict__ V, u64 n, const u32 *__restrict__ cnt,
+                                                  const u64 *__restrict__ ref, const u32 *l_len, const u32 *key_len,
                                                   u32 *__restrict__ order, u64 *__restrict__ len) {
     const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const u32 c = cnt[i];
-    u64 less = c & 0x7FFFFFFFu;
-    const u64 a2 = K2[i], a1 = K1[i], a0 = K0[i];
-    const u32 v = V[i];
-    const u64 me = ref[v];
-    if (c & 0x80000000u) {
-        const u32 T = (u32)((n + TS_N - 1) / TS_N);
-        for (u32 u = 0; u < T; ++u) {
-            const u64 b = (u64)u * TS_N, e = min(b + TS_N, n);
-            u64 lo = b, hi = e;
-            while (lo < hi) {
-                const u64 m = (lo + hi) >> 1;
-                if (key_lt(K2[m], K1[m], K0[m], a2, a1, a0)) lo = m + 1;
-                else hi = m;
-            }
-            for (u64 j = lo; j < e && K2[j] == a2 && K1[j] == a1 && K0[j] == a0; ++j)
-                if (j != i && full_cmp(ref[V[j]], me, a1, a0, buf, extra, l_pos, l_len, arena, key_off, key_len) < 0)
-                    ++less;
-        }
-    }
-    order[less] = v;
-    len[less] = entry_key_len(me, a1, a0, l_len, key_len);
+    const u32 r = cnt[i], v = V[i];
+    order[r] = v;
+    len[r] = entry_key_len(ref[v], K1[i], K0[i], l_len, key_len);
 }
 
 // ---------------------------------------------------------------------------
@@ -2391,9 +2377,10 @@ hipError_t msa_launch_rank_small(u64 *const K2[3], u64 *const K1[3], u64 *const 
     const u32 T = (u32)((n + TS_N - 1) / TS_N);
     hipLaunchKernelGGL(k_tile_sort, dim3(T), dim3(TS_T), 0, s, K2[0], K1[0], K0[0], V[0], n, K2[1], K1[1], K0[1], V[1]);
 #if RC_TOT
-    hipLaunchKernelGGL(k_rank_total, dim3(T * RT_K), dim3(RT_T), 0, s, K2[1], K1[1], K0[1], n, cnt);
-    hipLaunchKernelGGL(k_rank_put, grid1(n), dim3(256), 0, s, K2[1], K1[1], K0[1], V[1], n, (const u32 *)cnt, ref,
-                       buf, extra, l_pos, l_len, arena, key_off, key_len, order, len);
+    hipLaunchKernelGGL(k_rank_total, dim3(T * RT_K), dim3(RT_T), 0, s, K2[1], K1[1], K0[1], (const u32 *)V[1], n, ref,
+                       buf, extra, l_pos, l_len, arena, key_off, key_len, cnt);
+    hipLaunchKernelGGL(k_rank_put, grid1(n), dim3(256), 0, s, K1[1], K0[1], V[1], n, (const u32 *)cnt, ref, l_len,
+                       key_len, order, len);
 #else
     hipLaunchKernelGGL(k_rank_count, dim3(T), dim3(RC_T), 0, s, K2[1], K1[1], K0[1], n, cnt, (const u64 *)nullptr);
     hipLaunchKernelGGL(k_rank_place, grid1(n), dim3(256), 0, s, K2[1], K1[1], K0[1], V[1], n, (const u32 *)cnt, ref,

@@ -17,8 +17,40 @@
 
 #define MSA_MAX_PROBE 4096u
 
+// Probe by CAS straight away (the CAS returns the slot's key: one L2 atomic
+// per probe) instead of an atomic load first and a CAS only on an empty slot
+// (two for every new key: the high-cardinality inserts).  TAB_CAS_FIRST=0
+// builds the load-first probe.
+#ifndef TAB_CAS_FIRST
+#define TAB_CAS_FIRST 1
+#endif
+__device__ __forceinline__ u64 probe_word(u64 *p, u64 key) {
+    if (TAB_CAS_FIRST) return atomicCAS((unsigned long long *)p, 0ull, (unsigned long long)key);
+    const u64 cur = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return cur ? cur : atomicCAS((unsigned long long *)p, 0ull, (unsigned long long)key);
+}
+
 __device__ __forceinline__ u64 ld_relaxed(const u64 *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Append the slots the calling lanes claimed to a table's dense slot list:
+// one claim-counter atomic per wave, not per key (a same-address atomic per
+// new key serialised at the L2: 5 M new long words took 3.8 ms).  Called by
+// every lane that ran the insert, after its probe loop (reconverged).
+__device__ __forceinline__ void list_append_wave(bool isnew, u64 slot, u32 *list, u64 list_cap, u64 *claimed,
+                                                 Counters *ctr, u64 ovf_bit) {
+    const u64 B = __ballot(isnew);
+    if (!B) return;
+    const int leader = __ffsll((long long)B) - 1;
+    u64 base = 0;
+    if ((int)lane_id() == leader) base = atomicAdd((unsigned long long *)claimed, (unsigned long long)__popcll(B));
+    base = readlane64(base, leader);
+    if (isnew) {
+        const u64 i = base + mbcnt(B);
+        if (i < list_cap) list[i] = (u32)slot;
+        else atomicOr((unsigned long long *)&ctr->overflow, (unsigned long long)ovf_bit);
+    }
 }
 
 // S-table insert; claimed slots are appended to `list` (dense, for ranking)
@@ -28,29 +60,24 @@ template <bool LIST = true>
 __device__ __forceinline__ void s_insert(u64 *tab, u64 mask, u64 key, u64 cnt, u32 *list,
                                          u64 list_cap, Counters *ctr) {
     u64 h = fmix64(key) & mask;
+    bool isnew = false, found = false;
     for (u32 probe = 0; probe < MSA_MAX_PROBE; ++probe) {
         u64 *slot = tab + 2 * h;
-        u64 cur = ld_relaxed(slot);
+        const u64 cur = probe_word(slot, key);
         if (cur == 0) {
-            u64 old = atomicCAS((unsigned long long *)slot, 0ull, (unsigned long long)key);
-            if (old == 0) {
-                atomicAdd((unsigned long long *)(slot + 1), (unsigned long long)cnt);
-                if (LIST) {
-                    u64 i = atomicAdd((unsigned long long *)&ctr->s_claimed, 1ull);
-                    if (i < list_cap) list[i] = (u32)h;
-                    else atomicOr((unsigned long long *)&ctr->overflow, (unsigned long long)OVF_S);
-                }
-                return;
-            }
-            cur = old;
+            atomicAdd((unsigned long long *)(slot + 1), (unsigned long long)cnt);
+            isnew = found = true;
+            break;
         }
         if (cur == key) {
             atomicAdd((unsigned long long *)(slot + 1), (unsigned long long)cnt);
-            return;
+            found = true;
+            break;
         }
         h = (h + 1) & mask;
     }
-    atomicOr((unsigned long long *)&ctr->overflow, (unsigned long long)OVF_S);
+    if (!found) atomicOr((unsigned long long *)&ctr->overflow, (unsigned long long)OVF_S);
+    if (LIST) list_append_wave(isnew, h, list, list_cap, &ctr->s_claimed, ctr, OVF_S);
 }
 
 // M-table insert (two-word key).  The slot is claimed by CAS on k0 and the
@@ -62,22 +89,15 @@ __device__ __forceinline__ void m_insert(u64 *tab, u64 mask, u64 k0, u64 k1, u64
                                          u64 list_cap, Counters *ctr) {
     u64 h = fmix64(k0 ^ fmix64(k1)) & mask;
     u32 probe = 0, spins = 0;
+    bool isnew = false, found = false;
     while (probe < MSA_MAX_PROBE) {
         u64 *slot = tab + 4 * h;
-        u64 c0 = ld_relaxed(slot);
+        const u64 c0 = probe_word(slot, k0);
         if (c0 == 0) {
-            u64 old = atomicCAS((unsigned long long *)slot, 0ull, (unsigned long long)k0);
-            if (old == 0) {
-                __hip_atomic_store(slot + 1, k1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                atomicAdd((unsigned long long *)(slot + 2), (unsigned long long)cnt);
-                if (LIST) {
-                    u64 i = atomicAdd((unsigned long long *)&ctr->m_claimed, 1ull);
-                    if (i < list_cap) list[i] = (u32)h;
-                    else atomicOr((unsigned long long *)&ctr->overflow, (unsigned long long)OVF_M);
-                }
-                return;
-            }
-            c0 = old;
+            __hip_atomic_store(slot + 1, k1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            atomicAdd((unsigned long long *)(slot + 2), (unsigned long long)cnt);
+            isnew = found = true;
+            break;
         }
         if (c0 == k0) {
             u64 c1 = ld_relaxed(slot + 1);
@@ -88,13 +108,15 @@ __device__ __forceinline__ void m_insert(u64 *tab, u64 mask, u64 k0, u64 k1, u64
             }
             if (c1 == k1) {
                 atomicAdd((unsigned long long *)(slot + 2), (unsigned long long)cnt);
-                return;
+                found = true;
+                break;
             }
         }
         h = (h + 1) & mask;
         ++probe;
     }
-    atomicOr((unsigned long long *)&ctr->overflow, (unsigned long long)OVF_M);
+    if (!found) atomicOr((unsigned long long *)&ctr->overflow, (unsigned long long)OVF_M);
+    if (LIST) list_append_wave(isnew, h, list, list_cap, &ctr->m_claimed, ctr, OVF_M);
 }
 
 // H-table insert by 64-bit hash; returns the slot index (or ~0 on overflow).
@@ -102,30 +124,28 @@ __device__ __forceinline__ void m_insert(u64 *tab, u64 mask, u64 k0, u64 k1, u64
 __device__ __forceinline__ u64 h_insert(u64 *tab, u64 mask, u64 hash, u64 cnt, u64 rep, u32 *list,
                                         u64 list_cap, u64 *claimed, Counters *ctr, u64 ovf_bit) {
     if (hash == 0) hash = 0x8000000000000000ULL;
-    u64 h = hash & mask;
+    u64 h = hash & mask, res = ~0ull;
+    bool isnew = false;
     for (u32 probe = 0; probe < MSA_MAX_PROBE; ++probe) {
         u64 *slot = tab + 4 * h;
-        u64 cur = ld_relaxed(slot);
+        const u64 cur = probe_word(slot, hash);
         if (cur == 0) {
-            u64 old = atomicCAS((unsigned long long *)slot, 0ull, (unsigned long long)hash);
-            if (old == 0) {
-                __hip_atomic_store(slot + 2, rep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                atomicAdd((unsigned long long *)(slot + 1), (unsigned long long)cnt);
-                u64 i = atomicAdd((unsigned long long *)claimed, 1ull);
-                if (i < list_cap) list[i] = (u32)h;
-                else atomicOr((unsigned long long *)&ctr->overflow, (unsigned long long)ovf_bit);
-                return h;
-            }
-            cur = old;
+            __hip_atomic_store(slot + 2, rep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            atomicAdd((unsigned long long *)(slot + 1), (unsigned long long)cnt);
+            isnew = true;
+            res = h;
+            break;
         }
         if (cur == hash) {
             atomicAdd((unsigned long long *)(slot + 1), (unsigned long long)cnt);
-            return h;
+            res = h;
+            break;
         }
         h = (h + 1) & mask;
     }
-    atomicOr((unsigned long long *)&ctr->overflow, (unsigned long long)ovf_bit);
-    return ~0ull;
+    if (res == ~0ull) atomicOr((unsigned long long *)&ctr->overflow, (unsigned long long)ovf_bit);
+    list_append_wave(isnew, res, list, list_cap, claimed, ctr, ovf_bit);
+    return res;
 }
 
 // Artist-key hashes of the lines shortcut (k_rec_spans -> k_artist_count):
@@ -160,32 +180,30 @@ __device__ __forceinline__ u64 akey_hash_bytes(const u8 *p, u64 n, int second) {
 __device__ __forceinline__ u64 h_insert2(u64 *tab, u64 mask, u64 hash, u64 cnt, u64 rep, u64 sum2, u32 *list,
                                          u64 list_cap, u64 *claimed, Counters *ctr, u64 ovf_bit) {
     if (hash == 0) hash = 0x8000000000000000ULL;
-    u64 h = hash & mask;
+    u64 h = hash & mask, res = ~0ull;
+    bool isnew = false;
     for (u32 probe = 0; probe < MSA_MAX_PROBE; ++probe) {
         u64 *slot = tab + 4 * h;
-        u64 cur = ld_relaxed(slot);
+        const u64 cur = probe_word(slot, hash);
         if (cur == 0) {
-            u64 old = atomicCAS((unsigned long long *)slot, 0ull, (unsigned long long)hash);
-            if (old == 0) {
-                __hip_atomic_store(slot + 2, rep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                atomicAdd((unsigned long long *)(slot + 1), (unsigned long long)cnt);
-                atomicAdd((unsigned long long *)(slot + 3), (unsigned long long)sum2);
-                u64 i = atomicAdd((unsigned long long *)claimed, 1ull);
-                if (i < list_cap) list[i] = (u32)h;
-                else atomicOr((unsigned long long *)&ctr->overflow, (unsigned long long)ovf_bit);
-                return h;
-            }
-            cur = old;
+            __hip_atomic_store(slot + 2, rep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            atomicAdd((unsigned long long *)(slot + 1), (unsigned long long)cnt);
+            atomicAdd((unsigned long long *)(slot + 3), (unsigned long long)sum2);
+            isnew = true;
+            res = h;
+            break;
         }
         if (cur == hash) {
             atomicAdd((unsigned long long *)(slot + 1), (unsigned long long)cnt);
             atomicAdd((unsigned long long *)(slot + 3), (unsigned long long)sum2);
-            return h;
+            res = h;
+            break;
         }
         h = (h + 1) & mask;
     }
-    atomicOr((unsigned long long *)&ctr->overflow, (unsigned long long)ovf_bit);
-    return ~0ull;
+    if (res == ~0ull) atomicOr((unsigned long long *)&ctr->overflow, (unsigned long long)ovf_bit);
+    list_append_wave(isnew, res, list, list_cap, claimed, ctr, ovf_bit);
+    return res;
 }
 
 // 64-bit hash of a byte string (lower-cased when `lower`), for the H-table.

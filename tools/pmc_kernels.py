@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
 """Per-kernel mean of every PMC counter found under a rocprofv3 output
-directory (one or more --pmc passes): python tools/pmc_kernels.py DIR [filter]"""
+directory (one or more --pmc passes): python tools/pmc_kernels.py DIR [filter]
+LAST=k in the environment: only each kernel's last k dispatches per pass (the
+steady state of a run whose first call grows its tables)."""
 import csv
 import glob
 import os
@@ -19,7 +21,14 @@ for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=T
             key = (f, r.get("Dispatch_Id") or r.get("Correlation_Id"))
             c = acc[k][r["Counter_Name"]]
             c[key] = c.get(key, 0.0) + float(r["Counter_Value"])
+last = int(os.environ.get("LAST", "0"))
 for k, cs in sorted(acc.items()):
     print(k[:90])
     for c, v in sorted(cs.items()):
+        if last:
+            keep = {}
+            for f in {key[0] for key in v}:
+                ids = sorted((key for key in v if key[0] == f), key=lambda key: int(key[1]))[-last:]
+                keep.update({key: v[key] for key in ids})
+            v = keep
         print(f"   {c:28s} {sum(v.values()) / len(v):16.1f}   (n={len(v)})")
