@@ -27,6 +27,10 @@ hipError_t msa_launch_miss_agg(const ScanArgs &, hipStream_t);
 hipError_t msa_exclusive_scan(const u64 *, u64, u64 *, u64 *, u64 *, hipStream_t);
 hipError_t msa_exclusive_scan2(const u64 *, u64, u64 *, u64 *, u64 *, const u64 *, u64, u64 *, u64 *, u64 *,
                                hipStream_t);
+hipError_t msa_launch_rec_text(const u8 *, const u64 *, const u32 *, const u64 *, const u64 *, u64, u64, u64 *, u64 *,
+                               u32 *, Counters *, hipStream_t);
+hipError_t msa_launch_text_gather_w(const u8 *, const u64 *, const u64 *, const u64 *, const u32 *, u64, u64,
+                                    const u64 *, u8 *, hipStream_t);
 hipError_t msa_launch_rec_spans(const u8 *, const u64 *, const u32 *, u64, u64, int, u64 *, u64 *, u32 *, u64 *, u64 *,
                                 u32 *, Counters *, const AKeys &, const u64 *, const u64 *, const u64 *, u64 *, int,
                                 hipStream_t);
@@ -54,7 +58,8 @@ hipError_t msa_launch_list_build(const u64 *, u64, u32, u32 *, u64, u64 *, Count
 hipError_t msa_launch_artist_entries(const u64 *, const u32 *, u64, const u8 *, const u64 *, const u32 *, u64 *, u64 *,
                                      u64 *, u32 *, u64 *, u64 *, hipStream_t);
 u64 msa_radix_scratch_bytes(u64 n);
-hipError_t msa_radix_sort(u64 *const[3], u64 *const[3], u64 *const[3], u32 *const[3], u64, int *, u8 *, hipStream_t);
+hipError_t msa_radix_sort(u64 *const[3], u64 *const[3], u64 *const[3], u32 *const[3], u64, int *, u8 *, hipStream_t,
+                          const u64 * = nullptr);
 hipError_t msa_launch_tie_mark(const u64 *, const u64 *, const u64 *, u64, u64 *, u64 *, hipStream_t);
 hipError_t msa_launch_tie_build(const u64 *, const u64 *, const u64 *, const u64 *, u64, const u32 *, const u64 *, u32,
                                 const u64 *,
@@ -106,6 +111,8 @@ struct Ranked {
     DevBuf rank_cnt;               // the small-table ranking's per-tile counts
     u64 n = 0, blob_len = 0, blob_cap = 0;
     u64 lthr = 0;  // words: entries [0, lthr) are S/M keys (k_word_entries' order)
+    DevBuf vary;   // the key planes' OR / AND over the entries (k_word_entries), for the radix sort
+    bool vary_ok = false;
     bool blob_pending = false;  // blob_len not read back yet (do_rank's sync)
     BlobArgs pending{};
     std::vector<u64> h_counts, h_off;
@@ -184,7 +191,7 @@ struct msa_ctx {
     DevBuf extra;
     u64 extra_len = 0;
     // columns
-    DevBuf acol, alen, aoff, asrc, apairs, tcol, tlen, toff, tsrc, tpairs, scan_bsum, scan_total;
+    DevBuf acol, alen, aoff, asrc, apairs, tcol, tlen, toff, tsrc, tpairs, scan_bsum, scan_total, tscan_bsum;
     int cus = 256;
     int ablate = 0;  // MSA_ABLATE: diagnostic kernel ablations (results invalid)
     int sort_mode = 0;  // MSA_SORT: 0 by size, 1 merge sort, 2 radix sort
@@ -220,6 +227,7 @@ struct msa_ctx {
     // table (msa_run retries); the grown size is kept for later runs.
     u32 s_log2 = 0, m_log2 = 0, lt_log2 = 0, a_log2 = 0;
     u64 l_occ_want = 0;
+    u64 mlog_want = 0;  // K3 log entries the last split needed (grown when a log partition filled)
     // counters
     DevBuf ctr;
     Counters h_ctr{};
@@ -238,6 +246,13 @@ struct msa_ctx {
     hipEvent_t ev_r2_fork = nullptr, ev_r2_join = nullptr;
     // split scan: k_scan_struct done (the spans may start) / the spans done
     hipEvent_t ev_scan_a = nullptr, ev_spans = nullptr;
+    // text.csv early (beside the token pass): the side stream starts at ev_put
+    // (rank2, after the record arrays are final), ev_tscan = its offsets' scan done
+    hipEvent_t ev_put = nullptr, ev_tscan = nullptr;
+    // env MSA_EARLY_TEXT=1: text.csv gathered beside the token pass (measured
+    // and rejected: the token pass's neighbours and k_miss_agg slowed down more
+    // than the deferred gather costs, 3.55 vs 3.05 ms/step)
+    int early_text = 0;
     // the K2 final-state read-back (launch_scan_fn / wait_scan_fn)
     hipEvent_t ev_fin = nullptr;
     State fin_init{};
@@ -761,6 +776,37 @@ static int launch_spans(msa_ctx *c, bool want_text, hipStream_t st) {
     return MSA_OK;
 }
 
+// text.csv's body on the side stream as soon as the record arrays are final:
+// its line spans (k_rec_text), their offsets' scan (the body length into
+// Counters::col_body[1]; the library stream waits for it at ev_tscan before
+// the split's counter read-back) and the LDS-free gather, which fits beside
+// the token pass and the miss aggregation (both hold every CU's LDS) -- the
+// deferred gather had been the step's tail, after the artist pass.
+static int launch_text_early(msa_ctx *c) {
+    const u64 nrec = c->nrec;
+    HIPC(c, ensure(c->tcol, kColHdrRoom + c->n + 1 + MSA_INPUT_PAD));
+    HIPC(c, ensure(c->tlen, nrec * 8));
+    HIPC(c, ensure(c->tsrc, nrec * 8));
+    HIPC(c, ensure(c->tpairs, nrec * 4));
+    HIPC(c, ensure(c->toff, nrec * 8));
+    HIPC(c, ensure(c->tscan_bsum, ((nrec + 1023) / 1024 + 1) * 8));
+    HIPC(c, hipStreamWaitEvent(c->side, c->ev_put, 0));
+    prof_begin(c, ST_TEXT_COLUMN, c->side);
+    u64 *body = &c->ctr.as<Counters>()->col_body[1];
+    HIPC(c, msa_launch_rec_text(c->in, c->rec_start.as<u64>(), c->nulrel.as<u32>(), c->tss.as<u64>(),
+                                c->tse.as<u64>(), nrec, c->cont ? 0 : 1, c->tlen.as<u64>(), c->tsrc.as<u64>(),
+                                c->tpairs.as<u32>(), c->ctr.as<Counters>(), c->side));
+    HIPC(c, msa_exclusive_scan(c->tlen.as<u64>(), nrec, c->toff.as<u64>(), c->tscan_bsum.as<u64>(), body, c->side));
+    HIPC(c, hipEventRecord(c->ev_tscan, c->side));
+    HIPC(c, msa_launch_text_gather_w(c->in, c->tlen.as<u64>(), c->toff.as<u64>(), c->tsrc.as<u64>(),
+                                     c->tpairs.as<u32>(), nrec, kColHdrRoom, body, c->tcol.as<u8>(), c->side));
+    prof_end(c, ST_TEXT_COLUMN, c->n * 2 + c->nrec * 40, c->side);
+    HIPC(c, hipEventRecord(c->ev_join, c->side));
+    c->side_pending = true;
+    c->text_deferred = false;
+    return MSA_OK;
+}
+
 static int split_columns_rest(msa_ctx *c, bool want_text, const std::string &ah, const std::string &th) {
     HIPC(c, ensure(c->acol, ah.size() + c->n + 1 + MSA_INPUT_PAD));
     c->artist_hdr = ah;  // deferred (see msa_ctx::artist_deferred)
@@ -924,9 +970,10 @@ static int split_once(msa_ctx *c, int flags) {
         a.want_nul = want_text ? 1 : 0;
         a.ablate = c->ablate;
         a.first_rec = c->cont ? 0 : 1;
-        {  // miss logs: room for about a quarter of the tokens (a full partition falls back to HBM inserts)
+        {  // miss logs: room for about a quarter of the tokens, or for what the last
+           // split logged (a full partition falls back to an HBM insert per entry)
             const u64 parts = (u64)c->cus * MSA_MLOG_PARTS;
-            const u64 entries = std::max<u64>(parts * 1024, c->n / 16);
+            const u64 entries = std::max<u64>(std::max<u64>(parts * 1024, c->n / 16), c->mlog_want);
             a.mlog_cap = (u32)std::min<u64>(entries / parts, 1u << 30);
             HIPC(c, ensure(c->mlog, parts * a.mlog_cap * 16));
             HIPC(c, ensure(c->mlog_n, parts * 4));
@@ -1004,12 +1051,18 @@ static int split_once(msa_ctx *c, int flags) {
                            c->tse.as<u64>() + c->nrec - 1, (u64)SPAN_FIX);
         HIPC(c, hipGetLastError());
     }
-    if ((rc = launch_spans(c, want_text, sst))) return rc;
+    const bool early = want_text && spans_beside && c->early_text;
+    if (early) {
+        HIPC(c, hipEventRecord(c->ev_put, c->rank2));  // the record arrays (and the put above) are final
+        if ((rc = launch_text_early(c))) return rc;
+    }
+    if ((rc = launch_spans(c, want_text && !early, sst))) return rc;
     if (spans_beside) {
         HIPC(c, hipEventRecord(c->ev_spans, c->rank2));
         HIPC(c, hipStreamWaitEvent(c->stream, c->ev_spans, 0));
     }
-    if (want_text) {  // text.csv's body: deferred (msa_ctx::text_deferred)
+    if (early) HIPC(c, hipStreamWaitEvent(c->stream, c->ev_tscan, 0));  // col_body[1] before the read-back
+    if (want_text && !early) {  // text.csv's body: deferred (msa_ctx::text_deferred)
         HIPC(c, ensure(c->tcol, kColHdrRoom + c->n + 1 + MSA_INPUT_PAD));
         c->text_deferred = true;
     }
@@ -1029,6 +1082,8 @@ static int split_once(msa_ctx *c, int flags) {
     }
     HIPC(c, hipStreamSynchronize(c->stream));
     memcpy(&c->h_ctr, c->pin, sizeof(Counters));
+    if (c->h_ctr.mlog_full)  // the logs were too small for this input's misses: 25 % more than all of them
+        c->mlog_want = std::max<u64>(c->mlog_want, (c->h_ctr.k3_misses + c->h_ctr.mlog_full) / 4 * 5);
     if (!c->cont) {
         if (nterm > 0) memcpy(&hend, c->pin + kPinSmall, 8);
         if (c->n) memcpy(hdr.data(), c->pin + 1024, std::min<u64>(c->n, kHead));
@@ -1388,7 +1443,8 @@ static int sort_and_blob(msa_ctx *c, Ranked &R, const u8 *wbuf, const u8 *wextra
     } else if (!small_sort(c, n)) {
         if (st != c->stream) return fail(c, MSA_ERR_ARG, "radix ranking runs on the library stream");
         HIPC(c, ensure(c->sort_scratch, msa_radix_scratch_bytes(n)));
-        HIPC(c, msa_radix_sort(k2, k1, k0, vv, n, &cur, c->sort_scratch.as<u8>(), c->stream));
+        HIPC(c, msa_radix_sort(k2, k1, k0, vv, n, &cur, c->sort_scratch.as<u8>(), c->stream,
+                               R.vary_ok ? R.vary.as<u64>() : nullptr));
         int rc;
         if ((rc = refine_ties(c, R, cur, wbuf, wextra, arena, key_off, key_len))) return rc;
     } else {
@@ -1463,6 +1519,13 @@ static int do_rank(msa_ctx *c, int tables = 3) {
         ea.val = W.V[0].as<u32>();
         ea.ref = W.ref.as<u64>();
         ea.cnt = W.cnt.as<u64>();
+        W.vary_ok = !small_sort(c, W.n);  // the radix sort's varying bytes, reduced while the entries are written
+        if (W.vary_ok) {
+            HIPC(c, ensure(W.vary, 64));
+            HIPC(c, hipMemsetAsync(W.vary.p, 0, 24, c->stream));
+            HIPC(c, hipMemsetAsync(W.vary.as<u64>() + 3, 0xFF, 24, c->stream));
+            ea.vary = W.vary.as<u64>();
+        }
         HIPC(c, msa_launch_word_entries(ea, c->stream));
     }
     const u8 *wbuf = c->merged_w ? c->imp_w.as<u8>() : c->in;
@@ -1572,6 +1635,7 @@ int msa_create(int device, msa_ctx **out) {
     c->device = device;
     if (const char *ab = getenv("MSA_ABLATE")) c->ablate = atoi(ab);
     if (const char *ks = getenv("MSA_K3SPLIT")) c->k3split = atoi(ks) != 0;
+    if (const char *et = getenv("MSA_EARLY_TEXT")) c->early_text = atoi(et) != 0;
     if (const char *so = getenv("MSA_SORT")) c->sort_mode = !strcmp(so, "merge") ? 1 : (!strcmp(so, "radix") ? 2 : 0);
     {
         hipDeviceProp_t prop;
@@ -1587,6 +1651,8 @@ int msa_create(int device, msa_ctx **out) {
         hipEventCreateWithFlags(&c->ev_r2_join, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_scan_a, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_spans, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_put, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_tscan, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fin, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
@@ -1606,7 +1672,7 @@ void msa_destroy(msa_ctx *c) {
     (void)hipStreamSynchronize(c->stream);
     DevBuf *all[] = {&c->in_own, &c->sums, &c->carry, &c->btot, &c->bstate, &c->small, &c->rec_start, &c->extra, &c->exp_buf, &c->exp_meta, &c->imp_w, &c->imp_a, &c->imp_meta,
                      &c->nulrel, &c->f0, &c->tss, &c->tse, &c->span_fix, &c->alog, &c->alog_n, &c->acol, &c->alen, &c->aoff, &c->asrc, &c->apairs, &c->tcol, &c->tlen, &c->toff, &c->tsrc, &c->tpairs,
-                     &c->scan_bsum, &c->scan_total, &c->ar_start, &c->arena, &c->key_off,
+                     &c->tscan_bsum, &c->scan_bsum, &c->scan_total, &c->ar_start, &c->arena, &c->key_off,
                      &c->key_len, &c->key_slot, &c->s_tab, &c->s_list, &c->m_tab, &c->m_list, &c->l_pos, &c->l_len,
                      &c->l_slot, &c->l_tab, &c->l_list, &c->a_tab, &c->a_list, &c->ctr, &c->kh1, &c->kh2, &c->mlog, &c->mlog_n, &c->lmask, &c->sort_scratch, &c->blob_tot,
                      &c->t_head, &c->t_tie, &c->t_runid, &c->t_tpos, &c->t_bsum, &c->t_total, &c->t_Vn, &c->t_Pn,
@@ -1617,7 +1683,7 @@ void msa_destroy(msa_ctx *c) {
             for (auto &k : s) release(k);
         for (auto &v : R->V) release(v);
         DevBuf *rb[] = {&R->ref, &R->cnt, &R->order, &R->len, &R->off, &R->blob, &R->counts, &R->scan_bsum,
-                        &R->scan_total, &R->rank_cnt};
+                        &R->scan_total, &R->rank_cnt, &R->vary};
         for (DevBuf *b : rb) release(*b);
     }
     for (auto &s : c->t_K)
@@ -1635,6 +1701,8 @@ void msa_destroy(msa_ctx *c) {
     (void)hipEventDestroy(c->ev_r2_join);
     (void)hipEventDestroy(c->ev_scan_a);
     (void)hipEventDestroy(c->ev_spans);
+    (void)hipEventDestroy(c->ev_put);
+    (void)hipEventDestroy(c->ev_tscan);
     (void)hipStreamDestroy(c->side);
     (void)hipStreamDestroy(c->rank2);
     (void)hipStreamDestroy(c->stream);
@@ -2245,6 +2313,7 @@ extern "C" int msa_debug_stat(msa_ctx *c, const char *name, uint64_t *v) {
     else if (n == "m_claimed") *v = k.m_claimed;
     else if (n == "l_claimed") *v = k.l_claimed;
     else if (n == "split_attempts") *v = c->split_attempts;
+    else if (n == "mlog_full") *v = k.mlog_full;
     else if (n == "s_table_used" || n == "m_table_used") {  // occupied slots, counted on the host
         const bool sm = n == "s_table_used";
         const u64 slots = sm ? c->s_slots : c->m_slots, w = sm ? 2 : 4;

@@ -284,7 +284,7 @@ struct Counters {
     u64 k3_misses;   // K3 log entries folded by k_miss_agg: LDS-table misses + flushed table entries (diagnostic)
     u64 col_body[2]; // artist.csv / text.csv body bytes (the line-offset scans' totals)
     u64 span_fix;    // records k_rec_fast hands to k_rec_fix (the exact per-record path)
-    u64 pad;
+    u64 mlog_full;   // K3 misses that found their log partition full (inserted straight into HBM)
 };
 
 enum { OVF_S = 1, OVF_M = 2, OVF_L = 4, OVF_LT = 8, OVF_A = 16, OVF_REC = 32 };
@@ -377,6 +377,10 @@ struct EntryArgs {
     u32 *val;
     u64 *ref;
     u64 *cnt;
+    // optional: OR of each key plane over all entries ([0..2] = K0, K1, K2)
+    // and their AND ([3..5]), for the radix sort's varying-byte mask (the
+    // caller zeroes the ORs and sets the ANDs to all ones)
+    u64 *vary;
 };
 
 // Export source: the counted table (words or artists) of one GPU.

@@ -241,9 +241,10 @@ __device__ __forceinline__ u32 lds_find8(u64 *skeys, u64 k0) {
     return ~0u;
 }
 
+template <bool CASF = (TAB_CAS_FIRST != 0)>
 __device__ __forceinline__ void hbm_insert16(const ScanArgs &a, u64 k0, u64 k1m, u64 cnt) {
-    if (k1m == KMARK) s_insert<false>(a.s_tab, a.s_mask, k0, cnt, a.s_list, a.s_list_cap, a.ctr);
-    else m_insert<false>(a.m_tab, a.m_mask, k0, k1m & ~KMARK, cnt, a.m_list, a.m_list_cap, a.ctr);
+    if (k1m == KMARK) s_insert<false, CASF>(a.s_tab, a.s_mask, k0, cnt, a.s_list, a.s_list_cap, a.ctr);
+    else m_insert<false, CASF>(a.m_tab, a.m_mask, k0, k1m & ~KMARK, cnt, a.m_list, a.m_list_cap, a.ctr);
 }
 
 // Keys the LDS table cannot hold are not counted in HBM one atomic at a
@@ -285,7 +286,7 @@ __device__ __forceinline__ void flush_miss(const ScanArgs &a, const ulonglong2 *
         const u32 part = mlog_part(x.x, x.y);
         const u32 at = atomicAdd(&lcur[part], 1u);
         if (at < a.mlog_cap) a.mlog[((u64)blockIdx.x * MSA_MLOG_PARTS + part) * a.mlog_cap + at] = x;
-        else hbm_insert16(a, x.x, x.y, 1);
+        else hbm_insert16<false>(a, x.x, x.y, 1);
     }
     wsync();
 }
@@ -552,7 +553,7 @@ __device__ __forceinline__ void tok_phase(const ScanArgs &a, u64 ib, u64 lpos, u
             if (mis) {
                 const u32 at = nmiss + mbcnt(MB);
                 if (at < Q_MISS) miss[at] = make_ulonglong2(k0, k1);
-                else hbm_insert16(a, k0, k1, 1);  // more misses than the buffer holds (> 32 in one pass)
+                else hbm_insert16<false>(a, k0, k1, 1);  // more misses than the buffer holds (> 32 in one pass)
             }
             nmiss = min(nmiss + nm, (u32)Q_MISS);
         }
@@ -655,7 +656,7 @@ __device__ __forceinline__ void tok_probe(const ScanArgs &a, u64 ib, bool have, 
         if (mis) {
             const u32 at = nmiss + mbcnt(MB);
             if (at < Q_MISS) miss[at] = make_ulonglong2(k0, k1);
-            else hbm_insert16(a, k0, k1, 1);
+            else hbm_insert16<false>(a, k0, k1, 1);
         }
         nmiss = min(nmiss + nm, (u32)Q_MISS);
     }
@@ -687,8 +688,12 @@ __device__ __forceinline__ void tok_epilogue(const ScanArgs &a, u64 *skeys, u32 
         }
     }
     __syncthreads();
-    if (threadIdx.x < MSA_MLOG_PARTS)
-        a.mlog_n[blockIdx.x * MSA_MLOG_PARTS + threadIdx.x] = min(lcur[threadIdx.x], a.mlog_cap);
+    if (threadIdx.x < MSA_MLOG_PARTS) {
+        const u32 n = lcur[threadIdx.x];
+        a.mlog_n[blockIdx.x * MSA_MLOG_PARTS + threadIdx.x] = min(n, a.mlog_cap);
+        // the next split sizes the logs from this (full partitions cost an HBM insert per entry)
+        if (n > a.mlog_cap) atomicAdd((unsigned long long *)&a.ctr->mlog_full, (unsigned long long)(n - a.mlog_cap));
+    }
 }
 
 }  // namespace
@@ -1088,7 +1093,7 @@ __global__ __launch_bounds__(MA_T) void k_miss_agg(ScanArgs a, u32 nsrc, u32 gro
                 const u64 k0 = x.x & MLOG_KEYBITS, k1 = x.y & (MLOG_KEYBITS | KMARK);
                 const u32 slot = ma_find(keys, k0, k1);
                 if (slot != ~0u) atomicAdd(&cnts[slot], c ? c : 1u);
-                else hbm_insert16(a, k0, k1, c ? c : 1u);
+                else hbm_insert16<false>(a, k0, k1, c ? c : 1u);  // table full: one insert per entry
             }
         }
     }

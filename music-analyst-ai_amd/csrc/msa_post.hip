@@ -632,7 +632,7 @@ __device__ __forceinline__ void rec_noline(u64 r, int want_text, const SpanOut &
 // (<= 48 bytes) is trimmed and its pairs counted in the first window.
 __device__ void rec_full(const u8 *__restrict__ buf, const u64 *__restrict__ rec_start,
                          const u32 *__restrict__ nulrel, u64 r, u64 first_rec, int want_text, const SpanOut &o,
-                         Counters *ctr, const AKeys &ak) {
+                         Counters *ctr, const AKeys &ak, bool want_artist = true) {
     const u64 s = rec_start[r], e = rec_start[r + 1];
     const u64 b0 = s & ~15ull;
     const Win64 w0 = load_win64(buf, s);
@@ -663,10 +663,11 @@ __device__ void rec_full(const u8 *__restrict__ buf, const u64 *__restrict__ rec
         if (nc >= 3 || Z) break;
     }
     if (r < first_rec || nc < 3) {
-        rec_noline(r, want_text, o, ak);
+        if (want_artist) rec_noline(r, want_text, o, ak);
+        else o.tlen[r] = 0;
         return;
     }
-    rec_artist(buf, w0, s, f0, r, o, ctr, ak);
+    if (want_artist) rec_artist(buf, w0, s, f0, r, o, ctr, ak);
     if (want_text) {  // field 3: after the third comma up to the first NUL; the
                       // terminator is part of the record and trimmed as whitespace
         u64 ts = s + f3, te = e;
@@ -758,6 +759,146 @@ __global__ __launch_bounds__(256) void k_rec_fix(const u8 *__restrict__ buf, con
     const u64 n = *(volatile const u64 *)&ctr->span_fix;
     for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x)
         rec_full(buf, rec_start, nulrel, fix[i], first_rec, want_text, o, ctr, ak);
+}
+
+// The text column's line spans alone, on the side stream right after the
+// record structure pass (k_scan_struct), so that text.csv is gathered beside
+// the token pass instead of after the artist pass: thread per record, the
+// quoted common record from its span events (as k_rec_fast), every other one
+// on the exact path (rec_full without the artist part).  k_rec_fast then runs
+// without the text (its fix list holds only the records its artist span needs).
+__global__ __launch_bounds__(256) void k_rec_text(const u8 *__restrict__ buf, const u64 *__restrict__ rec_start,
+                                                  const u32 *__restrict__ nulrel, const u64 *__restrict__ tss,
+                                                  const u64 *__restrict__ tse, u64 nrec, u64 first_rec, SpanOut o,
+                                                  Counters *ctr, AKeys ak) {
+    const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nrec) return;
+    const u64 E = tse[r];
+    if (r < first_rec || (E & (SPAN_NOLINE | SPAN_NUL | SPAN_FIX)) == SPAN_NOLINE) {
+        o.tlen[r] = 0;
+        return;
+    }
+    const u64 S = tss[r];
+    const u64 ts = S & SPAN_POS, te = E & SPAN_POS;
+    const bool quoted = (S & SPAN_Q) && (E & SPAN_Q) && te >= ts + 2;
+    if ((E & (SPAN_NUL | SPAN_FIX)) || !quoted) {
+        rec_full(buf, rec_start, nulrel, r, first_rec, 1, o, ctr, ak, false);
+        return;
+    }
+    o.tlen[r] = te - ts + 1;
+    o.tsrc[r] = ts;
+    o.tpairs[r] = 0;
+}
+
+// Segmented gather without LDS (so that it fits beside the token pass, whose
+// workgroups hold every CU's LDS): a wave owns 64 consecutive lines -- lane j
+// holds line j's offset and source -- and so the output range [off[r0],
+// off[r0 + 64]).  Its lanes walk the range's aligned 16-byte slots, two per
+// lane per round, each slot's line found by a binary search over the lanes'
+// offsets (cross-lane reads, all lanes active); a slot inside one line is
+// five dword loads + v_alignbyte and one 16-byte store, a slot that meets a
+// line end is composed from the lines it meets (their offsets re-read from
+// memory, L1), the range's ragged first / last slot stored byte by byte.
+#define CW_T 256
+__global__ __launch_bounds__(CW_T) void k_col_gather_w(const u8 *__restrict__ buf, const u64 *__restrict__ line_len,
+                                                       const u64 *__restrict__ line_off,
+                                                       const u64 *__restrict__ span_src, u64 nrec, u64 hdr,
+                                                       const u64 *__restrict__ body_p, u8 *__restrict__ col) {
+    const u32 lane = lane_id();
+    const u64 r0 = ((u64)blockIdx.x * CW_T + threadIdx.x) & ~63ull;  // the wave's first line
+    if (r0 >= nrec) return;  // wave-uniform
+    const u64 body = *body_p;
+    const u32 wn = (u32)min((u64)64, nrec - r0);
+    // lane j: start of line j (absolute column byte); lanes >= wn: the range end
+    const u64 O1 = hdr + ((r0 + wn < nrec) ? line_off[r0 + wn] : body);
+    const u64 myoff = lane < wn ? hdr + line_off[r0 + lane] : O1;
+    const u64 mysrc = lane < wn ? span_src[r0 + lane] : 0;
+    const u64 O0 = readlane64(myoff, 0);
+    if (O1 <= O0) return;
+    const u64 S0 = O0 & ~15ull;
+    const u64 nslots = (O1 - S0 + 15) / 16;
+    auto lstart = [&](u32 j) -> u64 { return j < wn ? hdr + line_off[r0 + j] : O1; };
+    for (u64 base = 0; base < nslots; base += 128) {
+        u64 A[2];
+        u32 jj[2];
+        uint4 va[2];
+        u32 d4[2], sh[2];
+        bool fast[2], ok[2];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const u64 si = base + (u64)k * 64 + lane;
+            ok[k] = si < nslots;
+            A[k] = S0 + (ok[k] ? si : nslots - 1) * 16;
+            const u64 lo = max(A[k], O0);
+            // last line j with start <= lo (every lane takes part: cross-lane reads)
+            u32 j = 0;
+#pragma unroll
+            for (u32 step = 32; step > 0; step >>= 1) {
+                const u32 c = j + step;
+                const u32 cl = c < 64 ? c : 63;
+                const u64 oc = ((u64)__shfl((int)(u32)(myoff >> 32), (int)cl) << 32) |
+                               (u32)__shfl((int)(u32)myoff, (int)cl);
+                if (c < wn && oc <= lo) j = c;
+            }
+            jj[k] = j;
+            const u64 ls = ((u64)__shfl((int)(u32)(myoff >> 32), (int)j) << 32) | (u32)__shfl((int)(u32)myoff, (int)j);
+            const u32 jn = j + 1 < 64 ? j + 1 : 63;
+            u64 le = ((u64)__shfl((int)(u32)(myoff >> 32), (int)jn) << 32) | (u32)__shfl((int)(u32)myoff, (int)jn);
+            if (j + 1 >= wn) le = O1;
+            const u64 sj = ((u64)__shfl((int)(u32)(mysrc >> 32), (int)j) << 32) | (u32)__shfl((int)(u32)mysrc, (int)j);
+            fast[k] = ok[k] && A[k] >= O0 && A[k] + 16 <= O1 && A[k] >= ls && A[k] + 16 < le;
+            va[k] = make_uint4(0, 0, 0, 0);
+            d4[k] = 0;
+            sh[k] = 0;
+            if (fast[k]) {
+                const u64 src = sj + (A[k] - ls);
+                const u32 *p = reinterpret_cast<const u32 *>(buf + (src & ~3ull));
+                va[k] = make_uint4(p[0], p[1], p[2], p[3]);
+                d4[k] = p[4];
+                sh[k] = (u32)(src & 3);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            if (!ok[k]) continue;
+            const u64 a0 = A[k];
+            if (fast[k]) {
+                *reinterpret_cast<uint4 *>(col + a0) = align16(va[k], d4[k], sh[k]);
+                continue;
+            }
+            // a line end in the slot (or the range's ragged edge): compose it
+            const u64 lo = max(a0, O0), hi = min(a0 + 16, O1);
+            uint4 out = make_uint4(0, 0, 0, 0);
+            bool good = true;
+            for (u32 j = jj[k]; j < wn; ++j) {
+                const u64 ls = lstart(j), le = lstart(j + 1);
+                if (ls >= hi) break;
+                if (le > ls) {
+                    const u64 src = span_src[r0 + j];
+                    const u64 a = max(a0, ls), b = min(a0 + 16, le - 1);
+                    if (b > a) {
+                        if (src + a0 < ls) { good = false; break; }  // window would start before the buffer
+                        out = bytes_blend(out, load16u(buf, src + a0 - ls), (u32)(a - a0), (u32)(b - a0));
+                    }
+                    if (le - 1 >= a0 && le - 1 < a0 + 16) out = byte_put(out, (u32)(le - 1 - a0), '\n');
+                }
+                if (le >= hi) break;
+            }
+            if (good && lo == a0 && hi == a0 + 16) {
+                *reinterpret_cast<uint4 *>(col + a0) = out;
+            } else if (good) {  // owned bytes only
+                const u32 d[4] = {out.x, out.y, out.z, out.w};
+                for (u64 q = lo; q < hi; ++q) col[q] = (u8)(d[(q - a0) >> 2] >> (8 * ((q - a0) & 3)));
+            } else {
+                u32 j = jj[k];
+                for (u64 q = lo; q < hi; ++q) {
+                    while (q >= lstart(j + 1)) ++j;
+                    const u64 ls = lstart(j), le = lstart(j + 1);
+                    col[q] = (q + 1 == le) ? (u8)'\n' : buf[span_src[r0 + j] + (q - ls)];
+                }
+            }
+        }
+    }
 }
 
 // Segmented gather.  A workgroup owns 256 consecutive lines (their metadata
@@ -1471,10 +1612,43 @@ __global__ void k_long_insert(const u8 *__restrict__ buf, u64 seg_end, const u8 
     const u64 p = l_pos[i];
     const u8 *src = tok_at(buf, extra, p);
     const u64 lim = (p & MSA_POS_EXTRA) ? extra_len - (p & ~MSA_POS_EXTRA) : seg_end - p;
-    u64 len = 0;
-    while (len < lim && c_tok(src[len])) ++len;
-    l_len[i] = (u32)len;
-    const u64 h = bytes_hash(src, len, 1);
+    // the token's first 48 bytes from 13 dword loads (the buffers are padded
+    // past their end), aligned in registers: its length and its hash
+    // (bytes_hash's 8-byte groups) without a byte loop through memory
+    const u32 *wp = reinterpret_cast<const u32 *>(reinterpret_cast<uintptr_t>(src) & ~(uintptr_t)3);
+    const u32 sh = (u32)(reinterpret_cast<uintptr_t>(src) & 3);
+    u32 w[13], a[12];
+#pragma unroll
+    for (int k = 0; k < 13; ++k) w[k] = wp[k];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) a[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
+    u32 len = 48;
+#pragma unroll
+    for (int k = 47; k >= 0; --k)
+        if (!c_tok((a[k >> 2] >> (8 * (k & 3))) & 0xFFu)) len = (u32)k;
+    if ((u64)len > lim) len = (u32)lim;
+    u64 h;
+    if (len < 48) {
+        h = 0x243F6A8885A308D3ULL ^ ((u64)len * 0x9E3779B97F4A7C15ULL);
+        u64 acc = 0;
+#pragma unroll
+        for (u32 g = 0; g < 6; ++g) {
+            u64 x = ((u64)a[2 * g + 1] << 32) | a[2 * g];
+            x |= (x >> 1) & 0x2020202020202020ull;  // lower-case (token bytes: letters, digits, ')
+            if (8 * g + 8 <= len) {
+                h = fmix64(h ^ x) * 0x9E3779B97F4A7C15ULL;
+            } else if (8 * g < len) {
+                acc = x & ((1ull << (8 * (len - 8 * g))) - 1ull);
+            }
+        }
+        h = fmix64(h ^ acc ^ ((u64)(len & 7u) << 59));
+    } else {  // a longer token: the byte loops
+        u64 L = 48;
+        while (L < lim && c_tok(src[L])) ++L;
+        len = (u32)L;
+        h = bytes_hash(src, L, 1);
+    }
+    l_len[i] = len;
     l_slot[i] = h_insert(ltab, lmask, h, 1, i, llist, llist_cap, &ctr->l_claimed, ctr, OVF_LT);
 }
 
@@ -1549,37 +1723,63 @@ __global__ __launch_bounds__(256) void k_list_build(const u64 *__restrict__ tab,
     }
 }
 
-__global__ void k_word_entries(EntryArgs a) {
-    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(256) void k_word_entries(EntryArgs a) {
     const u64 n = a.ns + a.nm + a.nl;
-    if (i >= n) return;
-    u64 c, hi, lo, ref;
-    if (i < a.ns) {
-        const u64 slot = a.s_list[i];
-        const u64 key = a.s_tab[2 * slot];
-        c = a.s_tab[2 * slot + 1];
-        hi = __builtin_bswap64(key);
-        lo = 0;
-        ref = ((u64)KIND_S << 60) | slot;
-    } else if (i < a.ns + a.nm) {
-        const u64 slot = a.m_list[i - a.ns];
-        hi = __builtin_bswap64(a.m_tab[4 * slot]);
-        lo = __builtin_bswap64(a.m_tab[4 * slot + 1]);
-        c = a.m_tab[4 * slot + 2];
-        ref = ((u64)KIND_M << 60) | slot;
-    } else {
-        const u64 slot = a.l_list[i - a.ns - a.nm];
-        c = a.l_tab[4 * slot + 1];
-        const u64 rep = a.l_tab[4 * slot + 2];
-        be16(tok_at(a.buf, a.extra, a.l_pos[rep]), a.l_len[rep], 1, &hi, &lo);
-        ref = ((u64)KIND_L << 60) | rep;
+    // the key planes' OR / AND (a.vary): per thread over its grid-stride
+    // entries, then per workgroup, one atomic per plane and workgroup (one per
+    // wave on the same six words serialised at the L2: 47 ms at 50 M entries)
+    u64 vo[3] = {0, 0, 0}, va[3] = {~0ull, ~0ull, ~0ull};
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
+        u64 c, hi, lo, ref;
+        if (i < a.ns) {
+            const u64 slot = a.s_list[i];
+            const u64 key = a.s_tab[2 * slot];
+            c = a.s_tab[2 * slot + 1];
+            hi = __builtin_bswap64(key);
+            lo = 0;
+            ref = ((u64)KIND_S << 60) | slot;
+        } else if (i < a.ns + a.nm) {
+            const u64 slot = a.m_list[i - a.ns];
+            hi = __builtin_bswap64(a.m_tab[4 * slot]);
+            lo = __builtin_bswap64(a.m_tab[4 * slot + 1]);
+            c = a.m_tab[4 * slot + 2];
+            ref = ((u64)KIND_M << 60) | slot;
+        } else {
+            const u64 slot = a.l_list[i - a.ns - a.nm];
+            c = a.l_tab[4 * slot + 1];
+            const u64 rep = a.l_tab[4 * slot + 2];
+            be16(tok_at(a.buf, a.extra, a.l_pos[rep]), a.l_len[rep], 1, &hi, &lo);
+            ref = ((u64)KIND_L << 60) | rep;
+        }
+        a.K2[i] = ~c;
+        a.K1[i] = hi;
+        a.K0[i] = lo;
+        a.val[i] = (u32)i;
+        a.ref[i] = ref;
+        a.cnt[i] = c;
+        vo[0] |= lo; vo[1] |= hi; vo[2] |= ~c;
+        va[0] &= lo; va[1] &= hi; va[2] &= ~c;
     }
-    a.K2[i] = ~c;
-    a.K1[i] = hi;
-    a.K0[i] = lo;
-    a.val[i] = (u32)i;
-    a.ref[i] = ref;
-    a.cnt[i] = c;
+    if (!a.vary) return;
+    __shared__ u64 r[4][6];
+#pragma unroll
+    for (int w = 0; w < 3; ++w) {
+        for (int o = 32; o > 0; o >>= 1) {
+            vo[w] |= __shfl_xor(vo[w], o);
+            va[w] &= __shfl_xor(va[w], o);
+        }
+    }
+    const u32 wv = threadIdx.x >> 6;
+    if (lane_id() == 0)
+        for (int w = 0; w < 3; ++w) { r[wv][w] = vo[w]; r[wv][3 + w] = va[w]; }
+    __syncthreads();
+    if (threadIdx.x < 6) {
+        const u32 k = threadIdx.x;
+        u64 x = r[0][k];
+        for (u32 q = 1; q < blockDim.x / 64; ++q) x = k < 3 ? (x | r[q][k]) : (x & r[q][k]);
+        if (k < 3) atomicOr((unsigned long long *)&a.vary[k], (unsigned long long)x);
+        else atomicAnd((unsigned long long *)&a.vary[k], (unsigned long long)x);
+    }
 }
 
 __global__ void k_artist_entries(const u64 *__restrict__ atab, const u32 *__restrict__ alist, u64 n,
@@ -2248,6 +2448,24 @@ hipError_t msa_launch_col_write(int text, const u8 *buf, const u64 *len, const u
     hipLaunchKernelGGL(k_col_collapse, grid1(nrec), dim3(256), 0, s, buf, len, off, src, pairs, nrec, hdr, col);
     return hipGetLastError();
 }
+hipError_t msa_launch_rec_text(const u8 *buf, const u64 *rs, const u32 *nul, const u64 *tss, const u64 *tse, u64 nrec,
+                               u64 first_rec, u64 *tlen, u64 *tsrc, u32 *tpairs, Counters *ctr, hipStream_t s) {
+    if (!nrec) return hipSuccess;
+    const SpanOut o{nullptr, nullptr, nullptr, tlen, tsrc, tpairs};
+    const AKeys ak{};
+    hipLaunchKernelGGL(k_rec_text, grid1(nrec), dim3(256), 0, s, buf, rs, nul, tss, tse, nrec, first_rec, o, ctr, ak);
+    return hipGetLastError();
+}
+// text.csv's body with the LDS-free gather (beside the token pass)
+hipError_t msa_launch_text_gather_w(const u8 *buf, const u64 *len, const u64 *off, const u64 *src, const u32 *pairs,
+                                    u64 nrec, u64 hdr, const u64 *body_p, u8 *col, hipStream_t s) {
+    hipLaunchKernelGGL(k_zero_tail, dim3(1), dim3(256), 0, s, col, hdr, body_p, (u32)MSA_INPUT_PAD);
+    if (!nrec) return hipGetLastError();
+    hipLaunchKernelGGL(k_col_gather_w, dim3((u32)((nrec + CW_T - 1) / CW_T)), dim3(CW_T), 0, s, buf, len, off, src,
+                       nrec, hdr, body_p, col);
+    hipLaunchKernelGGL(k_col_collapse, grid1(nrec), dim3(256), 0, s, buf, len, off, src, pairs, nrec, hdr, col);
+    return hipGetLastError();
+}
 hipError_t msa_launch_artist_key(const u8 *col, const u64 *ar_start, const u64 *line_off, const u64 *line_len, u64 hdr,
                                  u64 nrec, u8 *arena, u64 *key_off, u32 *key_len, u64 *key_slot, u64 *atab, u64 amask,
                                  u32 *alist, u64 alist_cap, Counters *ctr, u64 short_base, int cus, int abl,
@@ -2316,7 +2534,8 @@ hipError_t msa_launch_list_build(const u64 *tab, u64 nslots, u32 stride, u32 *li
 }
 hipError_t msa_launch_word_entries(const EntryArgs &a, hipStream_t s) {
     const u64 n = a.ns + a.nm + a.nl;
-    if (n) hipLaunchKernelGGL(k_word_entries, grid1(n), dim3(256), 0, s, a);
+    // a grid-stride launch (its key-plane reduction ends in one atomic per workgroup)
+    if (n) hipLaunchKernelGGL(k_word_entries, dim3((u32)std::min<u64>(4096, (n + 255) / 256)), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 hipError_t msa_launch_artist_entries(const u64 *atab, const u32 *alist, u64 n, const u8 *arena, const u64 *key_off,

@@ -100,18 +100,31 @@ __global__ __launch_bounds__(256) void k_os_ghist(const u64 *__restrict__ K0, co
     for (u32 k = t; k < OS_POS * 256; k += 256) part[(u64)blockIdx.x * (OS_POS * 256) + k] = h[k];
 }
 
-// gstart[pos][d] = entries whose digit at pos is below d (one block per position)
-__global__ __launch_bounds__(256) void k_os_gscan(const u32 *__restrict__ part, u32 nparts,
-                                                  u64 *__restrict__ gstart) {
+// gstart[pos][d] = entries whose digit at pos is below d (one block per
+// varying position; four threads per digit sum the workgroup histograms)
+#define GS_T 1024
+__global__ __launch_bounds__(GS_T) void k_os_gscan(const u32 *__restrict__ part, u32 nparts, u32 pmask,
+                                                   u64 *__restrict__ gstart) {
+    __shared__ u32 c4[GS_T / 256][256];
     __shared__ u64 c[256];
-    const u32 t = threadIdx.x, p = blockIdx.x;
-    u64 s = 0;
-    for (u32 b = 0; b < nparts; ++b) s += part[(u64)b * (OS_POS * 256) + p * 256 + t];
-    c[t] = s;
+    const u32 t = threadIdx.x, d = t & 255u, q = t >> 8, p = blockIdx.x;
+    if (!((pmask >> p) & 1u)) return;  // a byte no pass sorts by
+    u32 s = 0;
+#pragma unroll 8
+    for (u32 b = q; b < nparts; b += GS_T / 256) s += part[(u64)b * (OS_POS * 256) + p * 256 + d];
+    c4[q][d] = s;
     __syncthreads();
-    u64 e = 0;
-    for (u32 k = 0; k < t; ++k) e += c[k];
-    gstart[p * 256 + t] = e;
+    if (t < 256) {
+        u64 tot = 0;
+        for (u32 k = 0; k < GS_T / 256; ++k) tot += c4[k][t];
+        c[t] = tot;
+    }
+    __syncthreads();
+    if (t < 256) {
+        u64 e = 0;
+        for (u32 k = 0; k < t; ++k) e += c[k];
+        gstart[p * 256 + t] = e;
+    }
 }
 
 __device__ __forceinline__ u64 os_pack(u32 epoch, u32 incl, u32 v) {
@@ -277,7 +290,7 @@ u64 msa_radix_scratch_bytes(u64 n) {
 // lands in set 1 or 2 (*which).  Sets 1 and 2 are scratch, as for
 // msa_launch_sort.  `scratch` holds msa_radix_scratch_bytes(n) bytes.
 hipError_t msa_radix_sort(u64 *const K2[3], u64 *const K1[3], u64 *const K0[3], u32 *const V[3], u64 n, int *which,
-                          u8 *scratch, hipStream_t s) {
+                          u8 *scratch, hipStream_t s, const u64 *vary_pre) {
     *which = 1;
     if (!n) return hipSuccess;
     if (n >= (1ull << 32)) return hipErrorInvalidValue;  // u32 indices and counts
@@ -291,18 +304,24 @@ hipError_t msa_radix_sort(u64 *const K2[3], u64 *const K1[3], u64 *const K0[3], 
     hipError_t e;
     if ((e = hipMemsetAsync(scratch, 0, 64 + 256, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(status, 0, ntiles * 256 * 8, s)) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_rx_vary, dim3((u32)std::min<u64>(1024, (n + 255) / 256)), dim3(256), 0, s, K2[0], K1[0],
-                       K0[0], n, vary);
-    u64 hv[3];
-    if ((e = hipMemcpyAsync(hv, vary, sizeof hv, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
-    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+    u64 hv[6];
+    if (vary_pre) {  // the planes' OR / AND from the entries' builder
+        if ((e = hipMemcpyAsync(hv, vary_pre, sizeof hv, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+        for (int w = 0; w < 3; ++w) hv[w] &= ~hv[3 + w];
+    } else {
+        hipLaunchKernelGGL(k_rx_vary, dim3((u32)std::min<u64>(1024, (n + 255) / 256)), dim3(256), 0, s, K2[0], K1[0],
+                           K0[0], n, vary);
+        if ((e = hipMemcpyAsync(hv, vary, 3 * sizeof(u64), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+    }
     u32 pmask = 0;
     for (int wi = 0; wi < 3; ++wi)
         for (u32 b = 0; b < 8; ++b)
             if ((hv[wi] >> (8 * b)) & 0xFFull) pmask |= 1u << (wi * 8 + b);
     if (pmask) {
         hipLaunchKernelGGL(k_os_ghist, dim3(nparts), dim3(256), 0, s, K0[0], K1[0], K2[0], n, pmask, part);
-        hipLaunchKernelGGL(k_os_gscan, dim3(OS_POS), dim3(256), 0, s, (const u32 *)part, nparts, gstart);
+        hipLaunchKernelGGL(k_os_gscan, dim3(OS_POS), dim3(GS_T), 0, s, (const u32 *)part, nparts, pmask, gstart);
     }
 
     const u64 *orig[3] = {K0[0], K1[0], K2[0]};  // least significant word first

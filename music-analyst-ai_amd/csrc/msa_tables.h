@@ -20,12 +20,15 @@
 // Probe by CAS straight away (the CAS returns the slot's key: one L2 atomic
 // per probe) instead of an atomic load first and a CAS only on an empty slot
 // (two for every new key: the high-cardinality inserts).  TAB_CAS_FIRST=0
-// builds the load-first probe.
+// builds the load-first probe.  A key inserted once per occurrence (an
+// aggregation table that is full) probes load-first: on a hot key a CAS
+// that fails is still a serialised read-modify-write at the L2.
 #ifndef TAB_CAS_FIRST
 #define TAB_CAS_FIRST 1
 #endif
+template <bool CASF = (TAB_CAS_FIRST != 0)>
 __device__ __forceinline__ u64 probe_word(u64 *p, u64 key) {
-    if (TAB_CAS_FIRST) return atomicCAS((unsigned long long *)p, 0ull, (unsigned long long)key);
+    if (CASF) return atomicCAS((unsigned long long *)p, 0ull, (unsigned long long)key);
     const u64 cur = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return cur ? cur : atomicCAS((unsigned long long *)p, 0ull, (unsigned long long)key);
 }
@@ -56,14 +59,14 @@ __device__ __forceinline__ void list_append_wave(bool isnew, u64 slot, u32 *list
 // S-table insert; claimed slots are appended to `list` (dense, for ranking)
 // unless LIST is false (the main scan: its lists are built afterwards by
 // k_list_build, so new keys do not serialise on one claim counter).
-template <bool LIST = true>
+template <bool LIST = true, bool CASF = (TAB_CAS_FIRST != 0)>
 __device__ __forceinline__ void s_insert(u64 *tab, u64 mask, u64 key, u64 cnt, u32 *list,
                                          u64 list_cap, Counters *ctr) {
     u64 h = fmix64(key) & mask;
     bool isnew = false, found = false;
     for (u32 probe = 0; probe < MSA_MAX_PROBE; ++probe) {
         u64 *slot = tab + 2 * h;
-        const u64 cur = probe_word(slot, key);
+        const u64 cur = probe_word<CASF>(slot, key);
         if (cur == 0) {
             atomicAdd((unsigned long long *)(slot + 1), (unsigned long long)cnt);
             isnew = found = true;
@@ -84,7 +87,7 @@ __device__ __forceinline__ void s_insert(u64 *tab, u64 mask, u64 key, u64 cnt, u
 // winner then publishes k1; a prober that finds k0 equal but k1 still 0 simply
 // retries that slot on its next loop trip (no spin inside a divergent branch,
 // so a same-wave winner always gets to publish).  LIST as for s_insert.
-template <bool LIST = true>
+template <bool LIST = true, bool CASF = (TAB_CAS_FIRST != 0)>
 __device__ __forceinline__ void m_insert(u64 *tab, u64 mask, u64 k0, u64 k1, u64 cnt, u32 *list,
                                          u64 list_cap, Counters *ctr) {
     u64 h = fmix64(k0 ^ fmix64(k1)) & mask;
@@ -92,7 +95,7 @@ __device__ __forceinline__ void m_insert(u64 *tab, u64 mask, u64 k0, u64 k1, u64
     bool isnew = false, found = false;
     while (probe < MSA_MAX_PROBE) {
         u64 *slot = tab + 4 * h;
-        const u64 c0 = probe_word(slot, k0);
+        const u64 c0 = probe_word<CASF>(slot, k0);
         if (c0 == 0) {
             __hip_atomic_store(slot + 1, k1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             atomicAdd((unsigned long long *)(slot + 2), (unsigned long long)cnt);

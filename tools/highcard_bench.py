@@ -40,6 +40,14 @@ with msa.Context(0) as c:
     print(f"ms/step {dt * 1e3:.2f}  GB/s {len(data) / dt / 1e9:.1f}  distinct words {s.n_words}  "
           f"artists {s.n_artists}  words {s.total_words}", flush=True)
     print("stages", st, flush=True)
+    import ctypes
+    c.lib.msa_debug_stat.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint64)]
+    dbg = {}
+    for nm in ("k3_misses", "mlog_full", "s_claimed", "m_claimed", "l_claimed", "split_attempts"):
+        v = ctypes.c_uint64(0)
+        if c.lib.msa_debug_stat(c.h, nm.encode(), ctypes.byref(v)) == 0:
+            dbg[nm] = v.value
+    print("counters", dbg, flush=True)
     if a.oracle:
         d = tempfile.mkdtemp()
         p_ = os.path.join(d, "hc.csv")
