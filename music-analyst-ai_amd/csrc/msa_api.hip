@@ -228,6 +228,10 @@ struct msa_ctx {
     u32 s_log2 = 0, m_log2 = 0, lt_log2 = 0, a_log2 = 0;
     u64 l_occ_want = 0;
     u64 mlog_want = 0;  // K3 log entries the last split needed (grown when a log partition filled)
+    u64 mlog_test = 0;  // env MSA_MLOG_ENTRIES (tests): the logs' first size, so that they overflow
+    u64 mlog_cap_last = 0;  // entries per partition of the last split's logs
+    State fin_cache{};     // the last split's final reader state (MSA_ABLATE 16384)
+    u64 fin_cache_n = 0;   // its input length + 1 (0: none)
     // counters
     DevBuf ctr;
     Counters h_ctr{};
@@ -253,6 +257,7 @@ struct msa_ctx {
     // and rejected: the token pass's neighbours and k_miss_agg slowed down more
     // than the deferred gather costs, 3.55 vs 3.05 ms/step)
     int early_text = 0;
+    int gather_w = 0;  // env MSA_GATHER_W=1: the deferred text.csv with the LDS-free gather (A/B)
     // the K2 final-state read-back (launch_scan_fn / wait_scan_fn)
     hipEvent_t ev_fin = nullptr;
     State fin_init{};
@@ -700,7 +705,13 @@ static int launch_text(msa_ctx *c, hipStream_t st) {
     int rc;
     c->text_deferred = false;
     prof_begin(c, ST_TEXT_COLUMN, st);
-    if ((rc = materialise_column(c, true, kColHdrRoom, c->tcol, c->tlen, c->toff, c->tsrc, c->tpairs, st))) return rc;
+    if (c->gather_w) {  // A/B: the LDS-free gather (k_col_gather_w)
+        HIPC(c, msa_launch_text_gather_w(c->in, c->tlen.as<u64>(), c->toff.as<u64>(), c->tsrc.as<u64>(),
+                                         c->tpairs.as<u32>(), c->nrec, kColHdrRoom,
+                                         &c->ctr.as<Counters>()->col_body[1], c->tcol.as<u8>(), st));
+    } else if ((rc = materialise_column(c, true, kColHdrRoom, c->tcol, c->tlen, c->toff, c->tsrc, c->tpairs, st))) {
+        return rc;
+    }
     prof_end(c, ST_TEXT_COLUMN, c->n * 2 + c->nrec * 40, st);  // ~ the text column read + written
     return MSA_OK;
 }
@@ -833,7 +844,7 @@ static int split_columns_rest(msa_ctx *c, bool want_text, const std::string &ah,
 
 // Word-table overflows of the scan (S/M tables, long-word occurrence list):
 // the split is repeated with grown tables (msa_split_columns' retry loop).
-static const u64 kSplitOvf = OVF_S | OVF_M | OVF_L;
+static const u64 kSplitOvf = OVF_S | OVF_M | OVF_L | OVF_MLOG;  // OVF_MLOG: K3 dropped misses (logs grown)
 static int check_split_overflow(msa_ctx *c, bool read_back = true) {
     int rc;
     if (read_back && (rc = sync_counters(c))) return rc;
@@ -937,7 +948,15 @@ static int split_once(msa_ctx *c, int flags) {
     const u64 cap0 = c->rec_cap;
     if ((rc = split_prologue(c, want_text ? cap0 : 0, cap0 != 0))) return rc;
     State init{0, 0, 0, 0, 0, 0}, fin;
-    if ((rc = launch_scan_fn(c, c->in, 0, c->n, init, ST_CSV_SUMMARY))) return rc;
+    if ((c->ablate & 16384) && c->fin_cache_n == c->n + 1) {
+        // diagnostic (MSA_ABLATE bit 16384, valid only for an unchanged input):
+        // K1 + K2 skipped, the chunk states of the previous split reused -- the
+        // ceiling of what folding K1 into the record pass could save
+        c->fin_init = c->fin_cache;
+        c->fin_pending = false;
+    } else if ((rc = launch_scan_fn(c, c->in, 0, c->n, init, ST_CSV_SUMMARY))) {
+        return rc;
+    }
 
     ScanArgs a{};
     auto launch_k3 = [&](u64 cap) -> int {
@@ -973,8 +992,11 @@ static int split_once(msa_ctx *c, int flags) {
         {  // miss logs: room for about a quarter of the tokens, or for what the last
            // split logged (a full partition falls back to an HBM insert per entry)
             const u64 parts = (u64)c->cus * MSA_MLOG_PARTS;
-            const u64 entries = std::max<u64>(std::max<u64>(parts * 1024, c->n / 16), c->mlog_want);
-            a.mlog_cap = (u32)std::min<u64>(entries / parts, 1u << 30);
+            u64 entries = std::max<u64>(std::max<u64>(parts * 1024, c->n / 16), c->mlog_want);
+            if (c->mlog_test) entries = std::max<u64>(c->mlog_test, c->mlog_want);  // tests: small first logs
+            // (a workgroup's 16 partitions are addressed with 32-bit byte offsets)
+            a.mlog_cap = (u32)std::min<u64>(entries / parts, (1u << 24) - 1);
+            c->mlog_cap_last = a.mlog_cap;
             HIPC(c, ensure(c->mlog, parts * a.mlog_cap * 16));
             HIPC(c, ensure(c->mlog_n, parts * 4));
             a.mlog = c->mlog.as<ulonglong2>();
@@ -1009,6 +1031,8 @@ static int split_once(msa_ctx *c, int flags) {
     };
     if (cap0 && (rc = launch_k3(cap0))) return rc;
     if ((rc = wait_scan_fn(c, &fin))) return rc;
+    c->fin_cache = fin;
+    c->fin_cache_n = c->n + 1;
     const u64 nterm = fin.rec;
     c->nrec = nterm + (fin.rs < c->n ? 1 : 0);
     const u64 cap = nterm + 2;
@@ -1082,8 +1106,14 @@ static int split_once(msa_ctx *c, int flags) {
     }
     HIPC(c, hipStreamSynchronize(c->stream));
     memcpy(&c->h_ctr, c->pin, sizeof(Counters));
-    if (c->h_ctr.mlog_full)  // the logs were too small for this input's misses: 25 % more than all of them
-        c->mlog_want = std::max<u64>(c->mlog_want, (c->h_ctr.k3_misses + c->h_ctr.mlog_full) / 4 * 5);
+    if (c->h_ctr.mlog_full) {  // the logs were too small for this input's misses: 25 % more than all of
+                               // them -- doubled when misses were dropped (OVF_MLOG: this split runs
+                               // again) and that would not be more (a partition fuller than the rest)
+        u64 want = (c->h_ctr.k3_misses + c->h_ctr.mlog_full) / 4 * 5;
+        if (c->h_ctr.overflow & OVF_MLOG)
+            want = std::max<u64>(want, 2 * std::max<u64>(c->mlog_want, c->mlog_cap_last * (u64)c->cus * MSA_MLOG_PARTS));
+        c->mlog_want = std::max<u64>(c->mlog_want, want);
+    }
     if (!c->cont) {
         if (nterm > 0) memcpy(&hend, c->pin + kPinSmall, 8);
         if (c->n) memcpy(hdr.data(), c->pin + 1024, std::min<u64>(c->n, kHead));
@@ -1636,6 +1666,8 @@ int msa_create(int device, msa_ctx **out) {
     if (const char *ab = getenv("MSA_ABLATE")) c->ablate = atoi(ab);
     if (const char *ks = getenv("MSA_K3SPLIT")) c->k3split = atoi(ks) != 0;
     if (const char *et = getenv("MSA_EARLY_TEXT")) c->early_text = atoi(et) != 0;
+    if (const char *gw = getenv("MSA_GATHER_W")) c->gather_w = atoi(gw) != 0;
+    if (const char *me = getenv("MSA_MLOG_ENTRIES")) c->mlog_test = strtoull(me, nullptr, 10);
     if (const char *so = getenv("MSA_SORT")) c->sort_mode = !strcmp(so, "merge") ? 1 : (!strcmp(so, "radix") ? 2 : 0);
     {
         hipDeviceProp_t prop;
@@ -1720,6 +1752,7 @@ int msa_sync(msa_ctx *c) {
 }
 
 int msa_load_csv(msa_ctx *c, const void *host, size_t n) {
+    if (c) c->fin_cache_n = 0;  // a new input
     if (!c || (!host && n)) return MSA_ERR_ARG;
     HIPC(c, hipSetDevice(c->device));
     HIPC(c, join_side(c));
@@ -1738,6 +1771,7 @@ int msa_load_csv(msa_ctx *c, const void *host, size_t n) {
 
 int msa_bind_csv(msa_ctx *c, const void *dev, size_t n) {
     if (!c || (!dev && n)) return MSA_ERR_ARG;
+    c->fin_cache_n = 0;  // a new input
     HIPC(c, join_side(c));
     c->in = reinterpret_cast<const u8 *>(dev);
     c->n = n;

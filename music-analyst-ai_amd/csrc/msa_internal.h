@@ -287,7 +287,7 @@ struct Counters {
     u64 mlog_full;   // K3 misses that found their log partition full (inserted straight into HBM)
 };
 
-enum { OVF_S = 1, OVF_M = 2, OVF_L = 4, OVF_LT = 8, OVF_A = 16, OVF_REC = 32 };
+enum { OVF_S = 1, OVF_M = 2, OVF_L = 4, OVF_LT = 8, OVF_A = 16, OVF_REC = 32, OVF_MLOG = 64 };
 
 // Artist keys built by k_rec_spans for the lines shortcut of the artist pass:
 // per record the key bytes (duplicate_field(duplicate_field(field0, 1), 0))

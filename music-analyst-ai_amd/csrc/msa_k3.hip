@@ -35,8 +35,19 @@ namespace {
 // to a per-wave list of the block's token starts: the lanes share the tokens
 // evenly (compaction) instead of each walking its own.
 #define Q_LIST 1024              // token entries per wave-iteration (>= 4 bytes per token)
+// TOK_DIRECT: each probe batch's misses go straight to the logs in one buffer
+// store per wave (no LDS miss buffer); 0: buffered per wave and flushed when
+// full (round 3)
+#ifndef TOK_DIRECT
+#define TOK_DIRECT 1
+#endif
+#if TOK_DIRECT
+#define Q_MISS 0
+#else
 #define Q_MISS 32                // deferred HBM inserts per wave (16 B each)
+#endif
 #define Q_WLDS (Q_LIST * 2 + Q_MISS * 16)
+#define Q_CUR ((MSA_MLOG_PARTS + 4) * 4)  // log cursors per partition + the dropped-entry count
 // LDS word table: 3..8-byte words (92 % of the tokens of lyric text) as
 // single u64 keys (12 bytes a slot, 4-slot buckets read as two ds_read_b128);
 // 9..16-byte words are logged for k_miss_agg.  Measured on configs[2]
@@ -44,11 +55,11 @@ namespace {
 // M table 1.95 ms, mixed with an M table 1.99, mixed without an M table (the S
 // table takes the whole LDS) 1.82 -- the design kept.
 #ifndef Q_SSLOTS                 // the rest of the CU's LDS
-#define Q_SSLOTS (((163840 - Q_W * (Q_LIST * 2 + Q_MISS * 16) - MSA_MLOG_PARTS * 4) / 12) & ~31)
+#define Q_SSLOTS (((163840 - Q_W * (Q_LIST * 2 + Q_MISS * 16) - Q_CUR) / 12) & ~31)
 #endif
 #define Q_SNB (Q_SSLOTS / 4)
 #define Q_TAB (Q_SSLOTS * 12)
-#define Q_LDS (Q_TAB + Q_W * Q_WLDS + MSA_MLOG_PARTS * 4)
+#define Q_LDS (Q_TAB + Q_W * Q_WLDS + Q_CUR)
 static_assert(Q_LDS <= 163840, "K3 LDS exceeds the CU's 160 KiB");
 static_assert(Q_SNB < 4096, "lds_find8 scales 20 hash bits by Q_SNB in 32 bits");
 static_assert(Q_SSLOTS % 32 == 0 && Q_TAB % 16 == 0 && Q_WLDS % 16 == 0,
@@ -437,9 +448,17 @@ __device__ __forceinline__ u64 struct_block(const ScanArgs &a, State &st, const 
 // The token phase of one 4 KiB block (process_lyrics, parallel_spotify.c:
 // 350-394): w = the lane's 64 token-byte bits, Tn = the 64 after them, S0 =
 // the counted token starts.  Shared by k_scan_csv and k_scan_tokens.
+// the workgroup's miss logs as a buffer resource: a store out of its range
+// (lanes without a miss) is dropped by the bounds check
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t mlog_rsrc(const ScanArgs &a) {
+    ulonglong2 *base = a.mlog + (u64)blockIdx.x * MSA_MLOG_PARTS * a.mlog_cap;
+    return __builtin_amdgcn_make_buffer_rsrc(base, (short)0, (int)(MSA_MLOG_PARTS * a.mlog_cap * 16u), 0x00020000);
+}
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+
 __device__ __forceinline__ void tok_phase(const ScanArgs &a, u64 ib, u64 lpos, u64 w, u64 Tn, u64 S0, u64 *skeys,
                                           u32 *scnts, u16 *list, ulonglong2 *miss, u32 &nmiss, u32 *lcur,
-                                          u64 &words) {
+                                          u64 &words, __amdgpu_buffer_rsrc_t rsrc) {
     const u32 lane = lane_id();
     // runs: rK bit b = bytes b .. b+K-1 are token bytes (w = Tn:T)
     const u64 r2 = w & shr128(w, Tn, 1), r2h = Tn & (Tn >> 1);
@@ -512,12 +531,22 @@ __device__ __forceinline__ void tok_phase(const ScanArgs &a, u64 ib, u64 lpos, u
         const uint4 v = kv;
         const u32 v4 = k4;
         const bool have = bt * 64 + lane < nS;
+#if TOK_DIRECT
+        {  // unconditional (a stale list entry: an address inside the block), so
+           // that the loop's vector memory sequence is the same every trip
+            en = list[min((bt + 1) * 64 + lane, (u32)Q_LIST - 1u)];
+            const u32 *gp = reinterpret_cast<const u32 *>(a.buf + ((ib + (en & 4095u)) & ~3ull));
+            kv = *reinterpret_cast<const uint4 *>(gp);
+            k4 = gp[4];
+        }
+#else
         if ((bt + 1) * 64 + lane < nS) {
             en = list[(bt + 1) * 64 + lane];
             const u32 *gp = reinterpret_cast<const u32 *>(a.buf + ((ib + (en & 4095u)) & ~3ull));
             kv = *reinterpret_cast<const uint4 *>(gp);
             k4 = gp[4];
         }
+#endif
         if (have) {
             const u32 len = (e >> 12) + 3;
             const u32 sh = (u32)(ib + (e & 4095u)) & 3u;
@@ -543,6 +572,23 @@ __device__ __forceinline__ void tok_phase(const ScanArgs &a, u64 ib, u64 lpos, u
                 mis = !(K3_ABLATE && (a.ablate & 4));
             }
         }
+#if TOK_DIRECT
+        // the batch's misses straight to their log partitions: a slot from the
+        // partition's LDS cursor, then one store for the whole wave -- every
+        // trip, lanes without a miss out of the buffer's range -- so waiting for
+        // the next batch's key loads never waits for this store.  A full
+        // partition drops the entry and counts it: the split runs again with
+        // larger logs (Counters::mlog_full, OVF_MLOG)
+        u32 off = 0xFFFFFFF0u;
+        if (mis) {
+            const u32 part = mlog_part(k0, k1);
+            const u32 at = atomicAdd(&lcur[part], 1u);
+            if (at < a.mlog_cap) off = (part * a.mlog_cap + at) * 16u;
+            else atomicAdd(&lcur[MSA_MLOG_PARTS], 1u);
+        }
+        const u32x4_t ent = {(u32)k0, (u32)(k0 >> 32), (u32)k1, (u32)(k1 >> 32)};
+        __builtin_amdgcn_raw_buffer_store_b128(ent, rsrc, (int)off, 0, 0);
+#else
         const u64 MB = __ballot(mis);
         if (MB) {
             const u32 nm = (u32)__popcll(MB);
@@ -557,109 +603,9 @@ __device__ __forceinline__ void tok_phase(const ScanArgs &a, u64 ib, u64 lpos, u
             }
             nmiss = min(nmiss + nm, (u32)Q_MISS);
         }
+#endif
     }
     wsync();
-}
-
-// The split token pass, software-pipelined across blocks (k_scan_tokens):
-// tok_prep builds a block's token list (starts and lengths from the mask,
-// long words listed for k_long_insert) and issues the key loads of its first
-// batch; tok_probe counts one batch.  The next block's list is built while
-// the current block's last batch is still to be probed, so its first key
-// loads are in flight during that probe instead of stalling the next block.
-__device__ __forceinline__ u32 tok_prep(const ScanArgs &a, u64 ib, u64 L, u64 Lnext, u64 Lprev, u16 *list,
-                                        u64 &words, u32 &en, uint4 &kv, u32 &k4) {
-    const u32 lane = lane_id();
-    const u64 lpos = ib + lane * 64;
-    const u64 S0 = L & ~((L << 1) | (Lprev >> 63));
-    const u64 w = L, Tn = Lnext;
-    // runs: rK bit b = bytes b .. b+K-1 are token bytes (w = Tn:L)
-    const u64 r2 = w & shr128(w, Tn, 1), r2h = Tn & (Tn >> 1);
-    const u64 r3 = r2 & shr128(w, Tn, 2);
-    const u64 r4 = r2 & shr128(r2, r2h, 2), r4h = r2h & (r2h >> 2);
-    const u64 r8 = r4 & shr128(r4, r4h, 4), r8h = r4h & (r4h >> 4);
-    const u64 r16 = r8 & shr128(r8, r8h, 8);
-    const u64 r17 = r16 & shr128(w, Tn, 16);
-    const u64 r9 = r8 & shr128(w, Tn, 8);
-    const u64 sS = S0 & r3 & ~r9, sM = S0 & r9 & ~r17, sL = S0 & r17;
-    words += (u64)__popcll(S0 & r3);
-    if (__ballot(sL != 0)) {  // long words (> 16 bytes): positions for k_long_insert
-        const u32 nl = (u32)__popcll(sL);
-        u32 tot;
-        const u32 pre = wave_prefix<6>(nl, tot);
-        u64 base = 0;
-        if (lane == 0) base = atomicAdd((unsigned long long *)&a.ctr->l_occ, (unsigned long long)tot);
-        base = readlane64(base, 0) + pre;
-        for (u64 m = sL; m; m &= m - 1) {
-            const u32 b = (u32)__ffsll((long long)m) - 1;
-            if (base < a.l_cap) a.l_pos[base] = (lpos + b) | a.lpos_tag;
-            else atomicOr((unsigned long long *)&a.ctr->overflow, (unsigned long long)OVF_L);
-            ++base;
-        }
-    }
-    // 3..16-byte words into the wave's list: block offset | (length - 3) << 12
-    u64 m = sS | sM;
-    u32 nS;
-    u32 li = wave_prefix<5>((u32)__popcll(m), nS);
-    while (__ballot(m != 0)) {
-        if (m) {
-            const u32 b = (u32)__ffsll((long long)m) - 1;
-            m &= m - 1;
-            const u32 d0 = (u32)w, d1 = (u32)(w >> 32), d2 = (u32)Tn;
-            const u32 run = __builtin_amdgcn_alignbit(b >= 32 ? d2 : d1, b >= 32 ? d1 : d0, b & 31u);
-            const u32 len = (u32)__ffs(~run) - 1;  // 3..16
-            list[li++] = (u16)((lane * 64 + b) | ((len - 3) << 12));
-        }
-    }
-    wsync();
-    en = 0;
-    kv = make_uint4(0, 0, 0, 0);
-    k4 = 0;
-    if (lane < nS) {
-        en = list[lane];
-        const u32 *gp = reinterpret_cast<const u32 *>(a.buf + ((ib + (en & 4095u)) & ~3ull));
-        kv = *reinterpret_cast<const uint4 *>(gp);
-        k4 = gp[4];
-    }
-    return nS;
-}
-
-__device__ __forceinline__ void tok_probe(const ScanArgs &a, u64 ib, bool have, u32 e, uint4 v, u32 v4, u64 *skeys,
-                                          u32 *scnts, ulonglong2 *miss, u32 &nmiss, u32 *lcur) {
-    bool mis = false;
-    u64 k0 = 0, k1 = KMARK;
-    if (have) {
-        const u32 len = (e >> 12) + 3;
-        const u32 sh = (u32)(ib + (e & 4095u)) & 3u;
-        u64 x0 = mk64(__builtin_amdgcn_alignbyte(v.y, v.x, sh), __builtin_amdgcn_alignbyte(v.z, v.y, sh));
-        u64 x1 = mk64(__builtin_amdgcn_alignbyte(v.w, v.z, sh), __builtin_amdgcn_alignbyte(v4, v.w, sh));
-        const u32 nbits = 8 * len;  // 24..128
-        x0 &= bits_lo(nbits);
-        x1 = nbits <= 64 ? 0ull : (x1 & bits_lo(nbits - 64));
-        k0 = lower_tok8(x0);
-        k1 = lower_tok8(x1) | KMARK;
-        if (len <= 8) {
-            const u32 slot = lds_find8(skeys, k0);
-            if (slot != ~0u) atomicAdd(&scnts[slot], 1u);
-            else mis = true;
-        } else {
-            mis = true;
-        }
-    }
-    const u64 MB = __ballot(mis);
-    if (MB) {
-        const u32 nm = (u32)__popcll(MB);
-        if (nmiss + nm > Q_MISS) {
-            flush_miss(a, miss, nmiss, lcur);
-            nmiss = 0;
-        }
-        if (mis) {
-            const u32 at = nmiss + mbcnt(MB);
-            if (at < Q_MISS) miss[at] = make_ulonglong2(k0, k1);
-            else hbm_insert16<false>(a, k0, k1, 1);
-        }
-        nmiss = min(nmiss + nm, (u32)Q_MISS);
-    }
 }
 
 // End of a counting workgroup: the wave's pending misses, total_words, the
@@ -694,6 +640,8 @@ __device__ __forceinline__ void tok_epilogue(const ScanArgs &a, u64 *skeys, u32 
         // the next split sizes the logs from this (full partitions cost an HBM insert per entry)
         if (n > a.mlog_cap) atomicAdd((unsigned long long *)&a.ctr->mlog_full, (unsigned long long)(n - a.mlog_cap));
     }
+    if (TOK_DIRECT && threadIdx.x == 0 && lcur[MSA_MLOG_PARTS])  // misses dropped: this split is repeated
+        atomicOr((unsigned long long *)&a.ctr->overflow, (unsigned long long)OVF_MLOG);
 }
 
 }  // namespace
@@ -728,9 +676,10 @@ __device__ __forceinline__ void scan_body(const ScanArgs &a) {
             skeys[i] = 0;
             scnts[i] = 0;
         }
-        if (threadIdx.x < MSA_MLOG_PARTS) lcur[threadIdx.x] = 0;
+        if (threadIdx.x < MSA_MLOG_PARTS + 1) lcur[threadIdx.x] = 0;
         __syncthreads();
     }
+    const __amdgpu_buffer_rsrc_t rsrc = mlog_rsrc(a);
 
     // wave-uniform chunk walk (scalar registers; the chunk-start values below
     // come through scalar loads, which do not wait behind the vector prefetch)
@@ -823,7 +772,7 @@ __device__ __forceinline__ void scan_body(const ScanArgs &a) {
             prevT = readlane((u32)(k.T >> 63), 63);
             const u64 Tnx = from_next(k.T);
             const u64 Tn = lane == 63 ? (u64)ttok : Tnx;
-            tok_phase(a, ib, lpos, k.T, Tn, S0, skeys, scnts, list, miss, nmiss, lcur, words);
+            tok_phase(a, ib, lpos, k.T, Tn, S0, skeys, scnts, list, miss, nmiss, lcur, words, rsrc);
         }
     }
     if (!SPLIT) tok_epilogue(a, skeys, scnts, miss, nmiss, lcur, words);
@@ -918,10 +867,10 @@ __global__ __launch_bounds__(SA_T, SA_MINW) void k_scan_struct(ScanArgs a) {
 // stride), token starts and lengths from the mask, keys re-read from the
 // input, counted in the workgroup's LDS table as in k_scan_csv.  The next
 // block's mask words and one 16-byte load per lane of its bytes (the keys'
-// cache lines) are in flight while a block is counted.
-#ifndef TOK_PIPE
-#define TOK_PIPE 0
-#endif
+// cache lines) are in flight while a block is counted.  (Measured and
+// removed: the token lists software-pipelined across blocks, the next
+// block's list built before the current block's last batch is probed --
+// 1.02 vs 0.81 ms.)
 __global__ __launch_bounds__(Q_T, 1) void k_scan_tokens(ScanArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     u64 *skeys = reinterpret_cast<u64 *>(smem);
@@ -937,8 +886,9 @@ __global__ __launch_bounds__(Q_T, 1) void k_scan_tokens(ScanArgs a) {
         skeys[i] = 0;
         scnts[i] = 0;
     }
-    if (threadIdx.x < MSA_MLOG_PARTS) lcur[threadIdx.x] = 0;
+    if (threadIdx.x < MSA_MLOG_PARTS + 1) lcur[threadIdx.x] = 0;
     __syncthreads();
+    const __amdgpu_buffer_rsrc_t rsrc = mlog_rsrc(a);
 
     const u64 nblk = (a.seg_end - a.seg_begin + Q_BLK - 1) / Q_BLK;
     const u64 nwords = nblk * 64;  // k_scan_struct writes every lane's word of every block
@@ -956,51 +906,6 @@ __global__ __launch_bounds__(Q_T, 1) void k_scan_tokens(ScanArgs a) {
         Lp = a.lmask[wi];  // lmask[0] is the zero pad
         warm = ldg16(a.buf + a.seg_begin + blk * Q_BLK + lane * 64);
     };
-#if TOK_PIPE
-    u64 blk = gw;
-    u32 nS = 0, en = 0, k4 = 0;
-    uint4 kv = make_uint4(0, 0, 0, 0);
-    u64 ib = 0;
-    if (blk < nblk) {
-        fetch(blk);
-        ib = a.seg_begin + blk * Q_BLK;
-        nS = tok_prep(a, ib, Lc, Ln, Lp, list, words, en, kv, k4);
-    }
-    while (blk < nblk) {
-        const u64 next = blk + nw;
-        if (next < nblk) fetch(next);  // the next block's mask words and key lines, in flight during this block
-        const u64 ibc = ib;
-        const u32 nSc = nS, nb = (nS + 63) >> 6;
-        if (nb == 0 && next < nblk) {
-            asm volatile("" ::"v"(warm.x));
-            ib = a.seg_begin + next * Q_BLK;
-            nS = tok_prep(a, ib, Lc, Ln, Lp, list, words, en, kv, k4);
-        }
-        for (u32 bt = 0; bt < nb; ++bt) {
-            const u32 e = en;
-            const uint4 v = kv;
-            const u32 v4 = k4;
-            const bool have = bt * 64 + lane < nSc;
-            if (bt + 1 < nb) {
-                if ((bt + 1) * 64 + lane < nSc) {
-                    en = list[(bt + 1) * 64 + lane];
-                    const u32 *gp = reinterpret_cast<const u32 *>(a.buf + ((ibc + (en & 4095u)) & ~3ull));
-                    kv = *reinterpret_cast<const uint4 *>(gp);
-                    k4 = gp[4];
-                }
-            } else if (next < nblk) {
-                // every entry of this block's list is read: the next block's list
-                // goes into the same buffer, its first keys are loaded before this
-                // last batch is probed
-                asm volatile("" ::"v"(warm.x));
-                ib = a.seg_begin + next * Q_BLK;
-                nS = tok_prep(a, ib, Lc, Ln, Lp, list, words, en, kv, k4);
-            }
-            tok_probe(a, ibc, have, e, v, v4, skeys, scnts, miss, nmiss, lcur);
-        }
-        blk = next;
-    }
-#else
     if (gw < nblk) fetch(gw);
     for (u64 blk = gw; blk < nblk; blk += nw) {
         const u64 L = Lc, Lnext = Ln, Lprev = Lp;
@@ -1009,9 +914,8 @@ __global__ __launch_bounds__(Q_T, 1) void k_scan_tokens(ScanArgs a) {
         const u64 ib = a.seg_begin + blk * Q_BLK;
         const u64 lpos = ib + lane * 64;
         const u64 S0 = L & ~((L << 1) | (Lprev >> 63));
-        tok_phase(a, ib, lpos, L, Lnext, S0, skeys, scnts, list, miss, nmiss, lcur, words);
+        tok_phase(a, ib, lpos, L, Lnext, S0, skeys, scnts, list, miss, nmiss, lcur, words, rsrc);
     }
-#endif
     tok_epilogue(a, skeys, scnts, miss, nmiss, lcur, words);
 }
 

@@ -71,6 +71,33 @@ def test_medium_corpora(msa_mod, ctx, tmp_path, mode):
     check_against_oracle(msa_mod, ctx, data, tmp_path, f"{mode}_medium")
 
 
+@pytest.mark.parametrize("mode", ["zipf", "highcard"])
+def test_miss_logs_overflow_and_grow(msa_mod, tmp_path, monkeypatch, mode):
+    """K3's miss logs sized far too small (MSA_MLOG_ENTRIES): the token pass
+    drops what does not fit and flags OVF_MLOG, the split runs again with logs
+    sized from what it counted -- same bytes as the oracle, and a second run on
+    the same context needs no retry."""
+    import ctypes
+    monkeypatch.setenv("MSA_MLOG_ENTRIES", "4096")
+    c = msa_mod.Context(0)
+    try:
+        data = msa_mod.gen_corpus(20_000, mode=mode, seed=31)
+        c.lib.msa_debug_stat.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint64)]
+
+        def stat(name):
+            v = ctypes.c_uint64(0)
+            assert c.lib.msa_debug_stat(c.h, name.encode(), ctypes.byref(v)) == 0
+            return v.value
+
+        check_against_oracle(msa_mod, c, data, tmp_path, f"mlog_{mode}")
+        first = stat("split_attempts")
+        assert first >= 2, "the tiny logs should have overflowed once"
+        check_against_oracle(msa_mod, c, data, tmp_path, f"mlog2_{mode}")
+        assert stat("split_attempts") == first + 1, "grown logs: one attempt"
+    finally:
+        c.close()
+
+
 EDGE = {
     "header_only": b"artist,song,link,text\n",
     "header_no_newline": b"artist,song,link,text",
