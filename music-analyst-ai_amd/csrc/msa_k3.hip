@@ -266,7 +266,14 @@ __device__ __forceinline__ void hbm_insert16(const ScanArgs &a, u64 k0, u64 k1m,
 // the HBM table once per aggregating workgroup.  A full log partition falls
 // back to the direct insert.
 __device__ __forceinline__ u32 mlog_part(u64 k0, u64 k1m) {
-    return (u32)((k0 * 0xD6E8FEB86659FD93ull ^ k1m * 0x9E3779B97F4A7C15ull) >> 60);
+    // full-rate operations only: two 64-bit multiplies had cost six
+    // quarter-rate v_mul_lo/hi_u32 per probe batch of the token pass
+    u32 t = (u32)k0 ^ __builtin_amdgcn_alignbit((u32)(k0 >> 32), (u32)(k0 >> 32), 11) ^ (u32)k1m ^
+            __builtin_amdgcn_alignbit((u32)(k1m >> 32), (u32)(k1m >> 32), 23);
+    t ^= t >> 15;
+    u32 h;  // v_mul_u32_u24 (full rate) by hand: the compiler turns the masked __umul24 into v_mul_lo_u32
+    asm("v_mul_u32_u24 %0, 0x9e3779, %1" : "=v"(h) : "v"(t ^ (t >> 16)));
+    return (h >> 20) & 15u;
 }
 
 // The workgroup's LDS table is flushed into the same logs at the end of the
@@ -583,7 +590,7 @@ __device__ __forceinline__ void tok_phase(const ScanArgs &a, u64 ib, u64 lpos, u
         if (mis) {
             const u32 part = mlog_part(k0, k1);
             const u32 at = atomicAdd(&lcur[part], 1u);
-            if (at < a.mlog_cap) off = (part * a.mlog_cap + at) * 16u;
+            if (at < a.mlog_cap) off = ((u32)__umul24(part, a.mlog_cap) + at) * 16u;  // cap < 2^24
             else atomicAdd(&lcur[MSA_MLOG_PARTS], 1u);
         }
         const u32x4_t ent = {(u32)k0, (u32)(k0 >> 32), (u32)k1, (u32)(k1 >> 32)};

@@ -140,7 +140,8 @@ __global__ __launch_bounds__(256, K1_MINW) void k_chunk_summary(const u8 *__rest
         const u64 cbase = seg_begin + (u64)c * MSA_CHUNK;
         const u64 cend = min(cbase + (u64)MSA_CHUNK, seg_end);
         u32 par = 0, first_nl = 0, anyrare = 0;
-        u32 cr[2] = {0, 0}, nterm[2] = {0, 0}, cc[2] = {0, 0}, zz[2] = {0, 0}, lend[2] = {0, 0};
+        // terminators per lane, summed over the wave once per chunk (not per block)
+        u32 cr[2] = {0, 0}, ntl[2] = {0, 0}, cc[2] = {0, 0}, zz[2] = {0, 0}, lend[2] = {0, 0};
         for (u64 ibase = cbase; ibase < cend; ibase += K1_ITER) {
             const u64 lpos = ibase + lane * 64;
             // one iteration ahead: the chunk's next block, else the wave's next
@@ -178,9 +179,7 @@ __global__ __launch_bounds__(256, K1_MINW) void k_chunk_summary(const u8 *__rest
                 const u64 pc0 = lane ? ((up >> 63) & 1u) : (u64)cr[h];
                 const u64 TERM = CRu | (NLu & ~((CRu << 1) | pc0));
                 const u32 nt = (u32)__popcll(TERM);
-                u32 totT = 0;
-#pragma unroll
-                for (int b = 0; b < 7; ++b) totT += (u32)__popcll(__ballot((nt >> b) & 1u)) << b;
+                ntl[h] += nt;
                 const u32 cq = min((u32)__popcll(Cu), 3u);
                 const u64 C1 = __ballot(cq >= 1u), C2 = __ballot(cq >= 2u), C3 = __ballot(cq >= 3u);
                 const u64 Bh = __ballot(nt != 0);
@@ -200,11 +199,18 @@ __global__ __launch_bounds__(256, K1_MINW) void k_chunk_summary(const u8 *__rest
                     cc[h] = min(cc[h] + (u32)__popcll(C1) + (u32)__popcll(C2) + (u32)__popcll(C3), 3u);
                     zz[h] |= (Bz != 0);
                 }
-                nterm[h] += totT;
                 cr[h] = (u32)((readlane64(CRu, Lz) >> bz) & 1u);
             }
 #pragma unroll
             for (int q = 0; q < 4; ++q) cur[q] = nxt[q];
+        }
+        u32 nterm[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {  // <= 16384 terminators per chunk: 15 bits
+            u32 tot = 0;
+#pragma unroll
+            for (int b = 0; b < 15; ++b) tot += (u32)__popcll(__ballot((ntl[h] >> b) & 1u)) << b;
+            nterm[h] = tot;
         }
         if (lane == 0) {
             ChunkSum s;
