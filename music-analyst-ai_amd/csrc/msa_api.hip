@@ -59,13 +59,15 @@ hipError_t msa_launch_artist_entries(const u64 *, const u32 *, u64, const u8 *, 
                                      u64 *, u32 *, u64 *, u64 *, hipStream_t);
 u64 msa_radix_scratch_bytes(u64 n);
 hipError_t msa_radix_sort(u64 *const[3], u64 *const[3], u64 *const[3], u32 *const[3], u64, int *, u8 *, hipStream_t,
-                          const u64 * = nullptr);
+                          const u64 * = nullptr, bool = true);
 hipError_t msa_launch_tie_mark(const u64 *, const u64 *, const u64 *, u64, u64 *, u64 *, hipStream_t);
 hipError_t msa_launch_tie_build(const u64 *, const u64 *, const u64 *, const u64 *, u64, const u32 *, const u64 *, u32,
                                 const u64 *,
+                                const u64 *,
                                 const u8 *, const u8 *, const u64 *, const u32 *, const u8 *, const u64 *, const u32 *,
                                 u64 *, u64 *, u64 *, u32 *, u32 *, u64 *, hipStream_t);
-hipError_t msa_launch_tie_apply(const u32 *, const u32 *, const u64 *, u64, u32 *, u32 *, u64 *, hipStream_t);
+hipError_t msa_launch_tie_apply(const u32 *, const u32 *, const u64 *, u64, u32 *, u32 *, u64 *, const u64 *, u64 *,
+                                hipStream_t);
 hipError_t msa_launch_sort(u64 *const[3], u64 *const[3], u64 *const[3], u32 *const[3], u64, int *, hipStream_t);
 hipError_t msa_launch_fixup(const u64 *, const u64 *, const u64 *, const u32 *, u64, const u64 *, const u8 *,
                             const u8 *, const u64 *, const u32 *, const u8 *, const u64 *, const u32 *, u32 *, hipStream_t);
@@ -258,6 +260,7 @@ struct msa_ctx {
     // than the deferred gather costs, 3.55 vs 3.05 ms/step)
     int early_text = 0;
     int gather_w = 0;  // env MSA_GATHER_W=1: the deferred text.csv with the LDS-free gather (A/B)
+    int sort_k0 = 0;   // env MSA_SORT_K0=1: the words' radix sort covers key bytes 8..15 too
     // the K2 final-state read-back (launch_scan_fn / wait_scan_fn)
     hipEvent_t ev_fin = nullptr;
     State fin_init{};
@@ -1365,14 +1368,17 @@ static const u64 kRadixMin = 1ull << 18;
 // Order of entries equal in (count, first 16 key bytes), radix path: round r
 // re-sorts the tied entries by (their run, key bytes [16 r, 16 r + 16)) with
 // the radix sort, until no two adjacent keys are equal (keys are distinct).
+// covered: key bytes the main sort ordered by (16, or 8 when it left K0 out:
+// the first round then also orders runs equal in count and first 8 bytes)
 static int refine_ties(msa_ctx *c, Ranked &R, int cur, const u8 *wbuf, const u8 *wextra, const u8 *arena,
-                       const u64 *key_off, const u32 *key_len) {
+                       const u64 *key_off, const u32 *key_len, u32 covered) {
     const u64 n = R.n;
     HIPC(c, hipMemcpyAsync(R.order.p, R.V[cur].p, n * 4, hipMemcpyDeviceToDevice, c->stream));
     for (DevBuf *b : {&c->t_head, &c->t_tie, &c->t_runid, &c->t_tpos}) HIPC(c, ensure(*b, n * 8));
     HIPC(c, ensure(c->t_bsum, ((n + 1023) / 1024 + 1) * 8));
     HIPC(c, ensure(c->t_total, 64));
-    const u64 *K2 = R.K[cur][0].as<u64>(), *K1 = R.K[cur][1].as<u64>(), *K0 = R.K[cur][2].as<u64>();
+    const u64 *K2 = R.K[cur][0].as<u64>(), *K1 = R.K[cur][1].as<u64>();
+    const u64 *K0 = covered == 16 ? R.K[cur][2].as<u64>() : nullptr;
     const u32 *Vc = R.V[cur].as<u32>();
     const u64 *Pc = nullptr;
     u64 mc = n;
@@ -1405,14 +1411,15 @@ static int refine_ties(msa_ctx *c, Ranked &R, int cur, const u8 *wbuf, const u8 
             vv[s] = c->t_V[s].as<u32>();
         }
         HIPC(c, msa_launch_tie_build(c->t_runid.as<u64>(), c->t_head.as<u64>(), c->t_tie.as<u64>(), c->t_tpos.as<u64>(),
-                                     mc, Vc, Pc, r,
+                                     mc, Vc, Pc, covered + 16 * (r - 1), R.K[0][2].as<u64>(),
                                      R.ref.as<u64>(), wbuf, wextra, c->l_pos.as<u64>(), c->l_len.as<u32>(), arena,
                                      key_off, key_len, k2[0], k1[0], k0[0], vv[0], c->t_Vn.as<u32>(),
                                      c->t_Pn.as<u64>(), c->stream));
         int o = 1;
         HIPC(c, msa_radix_sort(k2, k1, k0, vv, m, &o, c->sort_scratch.as<u8>(), c->stream));
         HIPC(c, msa_launch_tie_apply(vv[o], c->t_Vn.as<u32>(), c->t_Pn.as<u64>(), m, R.order.as<u32>(),
-                                     c->t_Vc.as<u32>(), c->t_Pc.as<u64>(), c->stream));
+                                     c->t_Vc.as<u32>(), c->t_Pc.as<u64>(), R.K[0][2].as<u64>(),
+                                     covered == 16 ? nullptr : R.K[cur][2].as<u64>(), c->stream));
         K2 = k2[o];
         K1 = k1[o];
         K0 = k0[o];
@@ -1473,10 +1480,15 @@ static int sort_and_blob(msa_ctx *c, Ranked &R, const u8 *wbuf, const u8 *wextra
     } else if (!small_sort(c, n)) {
         if (st != c->stream) return fail(c, MSA_ERR_ARG, "radix ranking runs on the library stream");
         HIPC(c, ensure(c->sort_scratch, msa_radix_scratch_bytes(n)));
+        // words: the passes over K0 (key bytes 8..15) are left to the tie
+        // refinement -- equal (count, first 8 bytes) runs are rare in a word
+        // table, so a round over them is cheaper than 8 passes over all entries
+        // (artists: prefixes shared by many names; MSA_SORT_K0=1 sorts K0 for words too)
+        const bool sk0 = slot != 0 || c->sort_k0;
         HIPC(c, msa_radix_sort(k2, k1, k0, vv, n, &cur, c->sort_scratch.as<u8>(), c->stream,
-                               R.vary_ok ? R.vary.as<u64>() : nullptr));
+                               R.vary_ok ? R.vary.as<u64>() : nullptr, sk0));
         int rc;
-        if ((rc = refine_ties(c, R, cur, wbuf, wextra, arena, key_off, key_len))) return rc;
+        if ((rc = refine_ties(c, R, cur, wbuf, wextra, arena, key_off, key_len, sk0 ? 16 : 8))) return rc;
     } else {
         HIPC(c, msa_launch_sort(k2, k1, k0, vv, n, &cur, st));
         HIPC(c, msa_launch_fixup(R.K[cur][0].as<u64>(), R.K[cur][1].as<u64>(), R.K[cur][2].as<u64>(),
@@ -1667,6 +1679,7 @@ int msa_create(int device, msa_ctx **out) {
     if (const char *ks = getenv("MSA_K3SPLIT")) c->k3split = atoi(ks) != 0;
     if (const char *et = getenv("MSA_EARLY_TEXT")) c->early_text = atoi(et) != 0;
     if (const char *gw = getenv("MSA_GATHER_W")) c->gather_w = atoi(gw) != 0;
+    if (const char *k0 = getenv("MSA_SORT_K0")) c->sort_k0 = atoi(k0) != 0;
     if (const char *me = getenv("MSA_MLOG_ENTRIES")) c->mlog_test = strtoull(me, nullptr, 10);
     if (const char *so = getenv("MSA_SORT")) c->sort_mode = !strcmp(so, "merge") ? 1 : (!strcmp(so, "radix") ? 2 : 0);
     {

@@ -1928,9 +1928,10 @@ __global__ void k_tie_fixup(const u64 *__restrict__ K2, const u64 *__restrict__ 
                             const u32 *key_len, u32 *__restrict__ out) {
     const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const u64 a2 = K2[i], a1 = K1[i], a0 = K0[i];
-    const bool eq_prev = i > 0 && K2[i - 1] == a2 && K1[i - 1] == a1 && K0[i - 1] == a0;
-    const bool eq_next = i + 1 < n && K2[i + 1] == a2 && K1[i + 1] == a1 && K0[i + 1] == a0;
+    // K0 null: the sort covered K2 and K1 only (K0's bytes are the first refinement round's)
+    const u64 a2 = K2[i], a1 = K1[i], a0 = K0 ? K0[i] : 0;
+    const bool eq_prev = i > 0 && K2[i - 1] == a2 && K1[i - 1] == a1 && (!K0 || K0[i - 1] == a0);
+    const bool eq_next = i + 1 < n && K2[i + 1] == a2 && K1[i + 1] == a1 && (!K0 || K0[i + 1] == a0);
     if (!eq_prev && !eq_next) { out[i] = V[i]; return; }
     u64 s = i, e = i + 1;
     while (s > 0 && K2[s - 1] == a2 && K1[s - 1] == a1 && K0[s - 1] == a0) --s;
@@ -1955,23 +1956,23 @@ __global__ void k_tie_mark(const u64 *__restrict__ K2, const u64 *__restrict__ K
                            u64 *__restrict__ head, u64 *__restrict__ tie) {
     const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const u64 a2 = K2[i], a1 = K1[i], a0 = K0[i];
-    const bool eq_prev = i > 0 && K2[i - 1] == a2 && K1[i - 1] == a1 && K0[i - 1] == a0;
-    const bool eq_next = i + 1 < n && K2[i + 1] == a2 && K1[i + 1] == a1 && K0[i + 1] == a0;
+    // K0 null: the sort covered K2 and K1 only (K0's bytes are the first refinement round's)
+    const u64 a2 = K2[i], a1 = K1[i], a0 = K0 ? K0[i] : 0;
+    const bool eq_prev = i > 0 && K2[i - 1] == a2 && K1[i - 1] == a1 && (!K0 || K0[i - 1] == a0);
+    const bool eq_next = i + 1 < n && K2[i + 1] == a2 && K1[i + 1] == a1 && (!K0 || K0[i + 1] == a0);
     head[i] = eq_prev ? 0 : 1;
     tie[i] = (eq_prev || eq_next) ? 1 : 0;
 }
 
-// key bytes [16 r, 16 r + 16) of an entry as two big-endian words (zero past its end)
-__device__ __forceinline__ void key16_round(u64 refv, u32 r, const u8 *buf, const u8 *extra, const u64 *l_pos,
+// key bytes [skip, skip + 16) of an entry as two big-endian words (zero past its end)
+__device__ __forceinline__ void key16_round(u64 refv, u32 skip, const u8 *buf, const u8 *extra, const u64 *l_pos,
                                             const u32 *l_len, const u8 *arena, const u64 *key_off,
                                             const u32 *key_len, u64 *hi, u64 *lo) {
     const u8 *p;
     u64 n;
     int lower;
     key_bytes(refv, 0, 0, buf, extra, l_pos, l_len, arena, key_off, key_len, &p, &n, &lower);
-    const u64 skip = 16ull * r;
-    if (!p || n <= skip) {  // S/M keys end within their first 16 bytes
+    if (!p || n <= skip) {  // the key ends before (S/M keys: within their first 16 bytes)
         *hi = 0;
         *lo = 0;
         return;
@@ -1984,7 +1985,8 @@ __device__ __forceinline__ void key16_round(u64 refv, u32 r, const u8 *buf, cons
 // Pc ? Pc[i] : i) goes to slot tpos[i] of the next level's subset
 __global__ void k_tie_build(const u64 *__restrict__ runid, const u64 *__restrict__ head, const u64 *__restrict__ tie,
                             const u64 *__restrict__ tpos,
-                            u64 mc, const u32 *__restrict__ Vc, const u64 *__restrict__ Pc, u32 r,
+                            u64 mc, const u32 *__restrict__ Vc, const u64 *__restrict__ Pc, u32 skip,
+                            const u64 *__restrict__ K0u,
                             const u64 *__restrict__ ref, const u8 *buf, const u8 *extra, const u64 *l_pos,
                             const u32 *l_len, const u8 *arena, const u64 *key_off, const u32 *key_len,
                             u64 *__restrict__ K2n, u64 *__restrict__ K1n, u64 *__restrict__ K0n,
@@ -1994,7 +1996,14 @@ __global__ void k_tie_build(const u64 *__restrict__ runid, const u64 *__restrict
     const u64 j = tpos[i];
     const u32 e = Vc[i];
     u64 hi, lo;
-    key16_round(ref[e], r, buf, extra, l_pos, l_len, arena, key_off, key_len, &hi, &lo);
+    if (skip == 8) {  // after a K2/K1-only sort: bytes 8..15 are K0 (S/M keys have no byte source)
+        u64 h2, l2;
+        key16_round(ref[e], 16, buf, extra, l_pos, l_len, arena, key_off, key_len, &h2, &l2);
+        hi = K0u[e];
+        lo = h2;
+    } else {
+        key16_round(ref[e], skip, buf, extra, l_pos, l_len, arena, key_off, key_len, &hi, &lo);
+    }
     K2n[j] = runid[i] + head[i];  // inclusive count of run heads: the same for every entry of a run
     K1n[j] = hi;
     K0n[j] = lo;
@@ -2004,12 +2013,16 @@ __global__ void k_tie_build(const u64 *__restrict__ runid, const u64 *__restrict
 }
 
 // the subset sorted (perm): its entries take the same order positions, in order
+// (and the sorted K0 plane at those positions: after a K2/K1-only sort the
+// tied entries' K0 differ, and the key blob reads K0 in rank order)
 __global__ void k_tie_apply(const u32 *__restrict__ perm, const u32 *__restrict__ Vn, const u64 *__restrict__ Pn,
-                            u64 m, u32 *__restrict__ order, u32 *__restrict__ Vc, u64 *__restrict__ Pc) {
+                            u64 m, u32 *__restrict__ order, u32 *__restrict__ Vc, u64 *__restrict__ Pc,
+                            const u64 *__restrict__ K0u, u64 *__restrict__ ks0) {
     const u64 j = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= m) return;
     const u32 e = Vn[perm[j]];
     order[Pn[j]] = e;
+    if (ks0) ks0[Pn[j]] = K0u[e];
     Vc[j] = e;
     Pc[j] = Pn[j];
 }
@@ -2637,16 +2650,18 @@ hipError_t msa_launch_tie_mark(const u64 *K2, const u64 *K1, const u64 *K0, u64 
 }
 hipError_t msa_launch_tie_build(const u64 *runid, const u64 *head, const u64 *tie, const u64 *tpos, u64 mc, const u32 *Vc,
                                 const u64 *Pc,
-                                u32 r, const u64 *ref, const u8 *buf, const u8 *extra, const u64 *l_pos,
-                                const u32 *l_len, const u8 *arena, const u64 *key_off, const u32 *key_len, u64 *K2n,
-                                u64 *K1n, u64 *K0n, u32 *Vid, u32 *Vn, u64 *Pn, hipStream_t s) {
+                                u32 skip, const u64 *K0u, const u64 *ref, const u8 *buf, const u8 *extra,
+                                const u64 *l_pos, const u32 *l_len, const u8 *arena, const u64 *key_off,
+                                const u32 *key_len, u64 *K2n, u64 *K1n, u64 *K0n, u32 *Vid, u32 *Vn, u64 *Pn,
+                                hipStream_t s) {
     if (mc)
-        hipLaunchKernelGGL(k_tie_build, grid1(mc), dim3(256), 0, s, runid, head, tie, tpos, mc, Vc, Pc, r, ref, buf, extra,
+        hipLaunchKernelGGL(k_tie_build, grid1(mc), dim3(256), 0, s, runid, head, tie, tpos, mc, Vc, Pc, skip, K0u, ref,
+                           buf, extra,
                            l_pos, l_len, arena, key_off, key_len, K2n, K1n, K0n, Vid, Vn, Pn);
     return hipGetLastError();
 }
 hipError_t msa_launch_tie_apply(const u32 *perm, const u32 *Vn, const u64 *Pn, u64 m, u32 *order, u32 *Vc, u64 *Pc,
-                                hipStream_t s) {
-    if (m) hipLaunchKernelGGL(k_tie_apply, grid1(m), dim3(256), 0, s, perm, Vn, Pn, m, order, Vc, Pc);
+                                const u64 *K0u, u64 *ks0, hipStream_t s) {
+    if (m) hipLaunchKernelGGL(k_tie_apply, grid1(m), dim3(256), 0, s, perm, Vn, Pn, m, order, Vc, Pc, K0u, ks0);
     return hipGetLastError();
 }

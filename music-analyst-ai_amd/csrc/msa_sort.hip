@@ -290,7 +290,7 @@ u64 msa_radix_scratch_bytes(u64 n) {
 // lands in set 1 or 2 (*which).  Sets 1 and 2 are scratch, as for
 // msa_launch_sort.  `scratch` holds msa_radix_scratch_bytes(n) bytes.
 hipError_t msa_radix_sort(u64 *const K2[3], u64 *const K1[3], u64 *const K0[3], u32 *const V[3], u64 n, int *which,
-                          u8 *scratch, hipStream_t s, const u64 *vary_pre) {
+                          u8 *scratch, hipStream_t s, const u64 *vary_pre, bool sort_k0) {
     *which = 1;
     if (!n) return hipSuccess;
     if (n >= (1ull << 32)) return hipErrorInvalidValue;  // u32 indices and counts
@@ -315,6 +315,7 @@ hipError_t msa_radix_sort(u64 *const K2[3], u64 *const K1[3], u64 *const K0[3], 
         if ((e = hipMemcpyAsync(hv, vary, 3 * sizeof(u64), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
         if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
     }
+    if (!sort_k0) hv[0] = 0;  // K0's bytes are left to the tie refinement (refine_ties)
     u32 pmask = 0;
     for (int wi = 0; wi < 3; ++wi)
         for (u32 b = 0; b < 8; ++b)
