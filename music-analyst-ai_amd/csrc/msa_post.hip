@@ -1030,6 +1030,28 @@ __global__ __launch_bounds__(CG_T) void k_col_gather(const u8 *__restrict__ buf,
             // the slot holds a line end: compose it from the (usually two) lines
             // it meets, in registers
             const u64 lo = max(A, O0), hi = min(A + CG_SLOT, O1);
+            {  // the common case: line j's tail, its '\n', line j+1's head to the
+               // slot's end -- two unaligned loads and a byte-mask select (the
+               // line loop below costs ~3x the instructions, and every wave has
+               // a few such slots per batch)
+                const u32 j = jj[k];
+                const u64 ls = hdr + w_off[j], le = hdr + w_off[j + 1];  // '\n' at le - 1
+                if (lo == A && hi == A + CG_SLOT && j + 1 < wn && ls <= A && le - 1 >= A && le - 1 < A + CG_SLOT &&
+                    hdr + w_off[j + 2] > A + CG_SLOT && w_src[j + 1] + A >= le) {
+                    const u32 e = (u32)(le - 1 - A);  // 0..15
+                    const uint4 X = load16u(buf, w_src[j] + (A - ls));
+                    const uint4 Y = load16u(buf, w_src[j + 1] + A - le);
+                    const u64 xl = e >= 8 ? ~0ull : bits_below(8 * e), xh = e >= 8 ? bits_below(8 * e - 64) : 0ull;
+                    const u64 nl = e >= 8 ? 0ull : (0x0Aull << (8 * e)), nh = e >= 8 ? (0x0Aull << (8 * e - 64)) : 0ull;
+                    const u64 yl = ~(xl | (0xFFull << (8 * (e & 7))) * (e < 8));
+                    const u64 yh = ~(xh | (e >= 8 ? (0xFFull << (8 * (e - 8))) : 0ull));
+                    const u64 Xl = ((u64)X.y << 32) | X.x, Xh = ((u64)X.w << 32) | X.z;
+                    const u64 Yl = ((u64)Y.y << 32) | Y.x, Yh = ((u64)Y.w << 32) | Y.z;
+                    const u64 ol = (Xl & xl) | (Yl & yl) | nl, oh = (Xh & xh) | (Yh & yh) | nh;
+                    *reinterpret_cast<uint4 *>(col + A) = make_uint4((u32)ol, (u32)(ol >> 32), (u32)oh, (u32)(oh >> 32));
+                    continue;
+                }
+            }
             uint4 out = make_uint4(0, 0, 0, 0);
             bool ok = true;
             for (u32 j = jj[k]; j < wn; ++j) {
