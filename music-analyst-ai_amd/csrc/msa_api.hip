@@ -10,7 +10,9 @@
 #include <stdarg.h>
 #include <algorithm>
 
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "msa_hip.h"
@@ -105,6 +107,11 @@ struct BlobArgs {  // key sources of the last blob pass (for a rewrite after gro
     const u64 *ks2, *ks1, *ks0;  // the sorted key planes (null: read the keys through order)
     u64 lthr;                    // entries below: S/M words (the key is K1/K0)
 };
+struct RefineBufs {
+    DevBuf sort_scratch;
+    DevBuf t_head, t_tie, t_runid, t_tpos, t_bsum, t_total, t_K[3][3], t_V[3], t_Vn, t_Pn, t_Vc, t_Pc;
+};
+
 struct Ranked {
     DevBuf K[3][3];  // [set][k2,k1,k0]: set 0 = input, 1/2 = ping-pong
     DevBuf V[3];
@@ -163,6 +170,7 @@ struct msa_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     std::string err;
+    std::mutex err_mu;
     // input
     DevBuf in_own;
     const u8 *in = nullptr;  // the segment processed (a view of the input)
@@ -197,11 +205,13 @@ struct msa_ctx {
     int cus = 256;
     int ablate = 0;  // MSA_ABLATE: diagnostic kernel ablations (results invalid)
     int sort_mode = 0;  // MSA_SORT: 0 by size, 1 merge sort, 2 radix sort
-    DevBuf sort_scratch;
+    // radix sort + tie refinement scratch, one set per concurrently ranked
+    // table (rb[1]: the artists on their own host thread and stream)
+    RefineBufs rb[2];
     DevBuf blob_tot;  // the two tables' key-blob lengths (device), read back once per msa_rank
     // tie refinement of the radix path: per-level marks/scans, the subset's
     // three key sets + values, and its order positions
-    DevBuf t_head, t_tie, t_runid, t_tpos, t_bsum, t_total, t_K[3][3], t_V[3], t_Vn, t_Pn, t_Vc, t_Pc;
+
     u64 acol_len = 0, a_hdr_getline = 0, a_hdr_len = 0, tcol_len = 0;
     u64 col_hdr[2] = {0, 0};        // header-line bytes of artist.csv / text.csv
     bool col_lens_pending = false;  // acol_len, tcol_len, a_end not read back yet
@@ -211,6 +221,8 @@ struct msa_ctx {
     // holding a '"' (Counters::a_quoted) or the label holds a '\n'
     bool artist_exact = false;       // msa_set_artist_reader
     bool artist_piece_set = false;   // msa_segment_set(MSA_PIECE_ARTISTS) since the split
+    bool artist_spec = false;        // the split ran the artist pass's first count (msa_count uses it)
+    bool a_dirty = false;            // the artist table holds slots no list names (wiped before the next split)
     bool have_tcol = false;
     // artist.csv records + keys
     DevBuf ar_start, arena, key_off, key_len, key_slot, kh1, kh2;
@@ -261,6 +273,7 @@ struct msa_ctx {
     int early_text = 0;
     int gather_w = 0;  // env MSA_GATHER_W=1: the deferred text.csv with the LDS-free gather (A/B)
     int sort_k0 = 0;   // env MSA_SORT_K0=1: the words' radix sort covers key bytes 8..15 too
+X
     // the K2 final-state read-back (launch_scan_fn / wait_scan_fn)
     hipEvent_t ev_fin = nullptr;
     State fin_init{};
@@ -366,7 +379,10 @@ static int fail(msa_ctx *c, int code, const char *fmt, ...) {
     va_start(ap, fmt);
     vsnprintf(b, sizeof b, fmt, ap);
     va_end(ap);
-    if (c) c->err = b;
+    if (c) {
+        std::lock_guard<std::mutex> g(c->err_mu);  // the artists' ranking may fail on its own thread
+        c->err = b;
+    }
     return code;
 }
 
@@ -654,6 +670,7 @@ static int reset_artist_table(msa_ctx *c) {
     int rc;
     if ((rc = ensure_tables(c))) return rc;
     if ((rc = wipe_one(c, c->a_tab, c->a_slots, 4, c->a_used_prev))) return rc;
+    c->a_dirty = false;
     if ((rc = reset_ctr(c, &Counters::a_claimed))) return rc;
     if ((rc = reset_ctr(c, &Counters::overflow))) return rc;
     if ((rc = reset_ctr(c, &Counters::songs))) return rc;  // the lines kernel counts them again
@@ -931,6 +948,7 @@ static int split_prologue(msa_ctx *c, u64 nul_n, bool rs0) {
     return MSA_OK;
 }
 
+static int launch_artist_count(msa_ctx *c);
 static int split_once(msa_ctx *c, int flags) {
     int rc;
     c->artist_deferred = c->text_deferred = false;  // superseded by this split
@@ -941,6 +959,7 @@ static int split_once(msa_ctx *c, int flags) {
     c->merged_w = c->merged_a = false;
     c->ranked_only = 0;
     c->artist_piece_set = false;
+    c->artist_spec = false;
     c->col_lens_pending = false;
     c->extra_len = 0;
     HIPC(c, ensure(c->ctr, sizeof(Counters)));
@@ -949,6 +968,10 @@ static int split_once(msa_ctx *c, int flags) {
     // host reads it back -- K3 runs meanwhile.  Too small (the first split, or
     // a larger input): the arrays grow and K3 runs again.
     const u64 cap0 = c->rec_cap;
+    if (c->a_dirty) {  // an earlier split's artist count overflowed and no msa_count wiped the table
+        if ((rc = ensure_tables(c)) || (rc = wipe_one(c, c->a_tab, c->a_slots, 4, c->a_used_prev))) return rc;
+        c->a_dirty = false;
+    }
     if ((rc = split_prologue(c, want_text ? cap0 : 0, cap0 != 0))) return rc;
     State init{0, 0, 0, 0, 0, 0}, fin;
     if ((c->ablate & 16384) && c->fin_cache_n == c->n + 1) {
@@ -1097,6 +1120,15 @@ static int split_once(msa_ctx *c, int flags) {
     // occurrences) and -- for the first shard -- the header record's end plus
     // the input's first bytes (the header, almost always)
     if ((rc = build_word_lists(c))) return rc;
+    // the artist pass of msa_count (lines shortcut) right here, before the
+    // read-back: it needs only the split's keys, and its counters come back
+    // with the split's -- the text column's gather (launched by msa_count)
+    // then no longer waits behind a second round trip and the artist kernels
+    // (an exact-reader input resets the table in msa_count)
+    if (!c->artist_exact && c->nrec && !(c->ablate & 32768)) {
+        if ((rc = launch_artist_count(c))) return rc;
+        c->artist_spec = true;
+    }
     HIPC(c, hipMemcpyAsync(c->pin, c->ctr.p, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
     u64 hend = c->n;
     static const u64 kHead = kPinHead;
@@ -1107,8 +1139,25 @@ static int split_once(msa_ctx *c, int flags) {
         if (c->n)
             HIPC(c, hipMemcpyAsync(c->pin + 1024, c->in, std::min<u64>(c->n, kHead), hipMemcpyDeviceToHost, c->stream));
     }
+    // text.csv's gather forked here, behind the read-back's copies (it needs
+    // nothing the host reads back): it runs during the host's header work and
+    // msa_count's launches instead of after them (MSA_TEXT_AT_SPLIT=0: forked
+    // by msa_count)
+    if (c->text_deferred && c->text_at_split) {
+        int trc;
+        if ((trc = start_text_side(c))) return trc;
+    }
     HIPC(c, hipStreamSynchronize(c->stream));
     memcpy(&c->h_ctr, c->pin, sizeof(Counters));
+    // the slots this split claimed are cleared by the next one's prologue even
+    // when this split fails below (a bad header) or no msa_count follows; an
+    // artist table that overflowed its list is wiped whole next time
+    c->s_used_prev = std::min<u64>(c->h_ctr.s_claimed, c->s_slots / 2);
+    c->m_used_prev = std::min<u64>(c->h_ctr.m_claimed, c->m_slots / 2);
+    if (c->artist_spec) {
+        c->a_used_prev = std::min<u64>(c->h_ctr.a_claimed, c->a_slots / 2);
+        if (c->h_ctr.overflow & OVF_A) c->a_dirty = true;
+    }
     if (c->h_ctr.mlog_full) {  // the logs were too small for this input's misses: 25 % more than all of
                                // them -- doubled when misses were dropped (OVF_MLOG: this split runs
                                // again) and that would not be more (a partition fuller than the rest)
@@ -1234,6 +1283,26 @@ static int wipe_long_table(msa_ctx *c) {
     return reset_ctr(c, &Counters::l_claimed);
 }
 
+// The artist pass of the lines shortcut (k_artist_count + merge + h2 check)
+// over the split's keys, on the library stream.
+static int launch_artist_count(msa_ctx *c) {
+    const u64 nrec = c->nrec;
+    // flush logs of the per-CU tables: (workgroup, 16 partitions) x cap
+    // entries of 32 B; a workgroup holds <= min(6144, its records) keys
+    const u64 wgs = std::max<u64>(1, std::min<u64>((nrec + 1023) / 1024, (u64)c->cus));  // k_artist_count's grid
+    const u64 per_wg = (nrec + wgs - 1) / wgs;
+    const u32 alog_cap = (u32)std::min<u64>(1024, std::max<u64>(64, per_wg / 8));
+    HIPC(c, ensure(c->alog, (size_t)c->cus * 16 * alog_cap * 32));
+    HIPC(c, ensure(c->alog_n, (size_t)c->cus * 16 * 4));
+    prof_begin(c, ST_ARTIST_KEYS);
+    HIPC(c, msa_launch_artist_count(c->alen.as<u64>(), c->key_len.as<u32>(), c->kh1.as<u64>(), c->kh2.as<u64>(), nrec,
+                                    c->a_tab.as<u64>(), c->a_slots - 1, c->a_list.as<u32>(), c->a_slots / 2,
+                                    c->ctr.as<Counters>(), c->cus, c->ablate, c->alog.as<ulonglong2>(),
+                                    c->alog_n.as<u32>(), alog_cap, c->stream));
+    prof_end(c, ST_ARTIST_KEYS, nrec * 28);
+    return MSA_OK;
+}
+
 static int do_count(msa_ctx *c) {
     int rc;
     if (c->stage < 1) return fail(c, MSA_ERR_ARG, "msa_count before msa_split_columns");
@@ -1249,26 +1318,16 @@ static int do_count(msa_ctx *c) {
         // the same launch sequence, and ONE counter read-back settles both (and
         // the column lengths).  The split's a_quoted flag says whether the
         // shortcut held -- if not, start over with the exact reader.
-        const u64 nrec = c->nrec;
-        // flush logs of the per-CU tables: (workgroup, 16 partitions) x cap
-        // entries of 32 B; a workgroup holds <= min(6144, its records) keys
-        const u64 wgs = std::max<u64>(1, std::min<u64>((nrec + 1023) / 1024, (u64)c->cus));  // k_artist_count's grid
-        const u64 per_wg = (nrec + wgs - 1) / wgs;
-        const u32 alog_cap = (u32)std::min<u64>(1024, std::max<u64>(64, per_wg / 8));
-        HIPC(c, ensure(c->alog, (size_t)c->cus * 16 * alog_cap * 32));
-        HIPC(c, ensure(c->alog_n, (size_t)c->cus * 16 * 4));
         for (int attempt = 0;; ++attempt) {
-            prof_begin(c, ST_ARTIST_KEYS);
-            HIPC(c, msa_launch_artist_count(c->alen.as<u64>(), c->key_len.as<u32>(), c->kh1.as<u64>(),
-                                            c->kh2.as<u64>(), nrec, c->a_tab.as<u64>(), c->a_slots - 1,
-                                            c->a_list.as<u32>(), c->a_slots / 2, c->ctr.as<Counters>(), c->cus,
-                                            c->ablate, c->alog.as<ulonglong2>(), c->alog_n.as<u32>(), alog_cap,
-                                            c->stream));
-            prof_end(c, ST_ARTIST_KEYS, nrec * 28);
+            // the first attempt may have run already, at the end of the split
+            // (its counters came back with the split's read-back)
+            if (attempt > 0 || !c->artist_spec) {
+                if ((rc = launch_artist_count(c))) return rc;
+            }
             if (attempt == 0) {
+                if ((rc = start_text_side(c))) return rc;  // text.csv beside this read-back and the ranking
                 launch_long_words(c, nl);
                 long_ran = true;
-                if ((rc = start_text_side(c))) return rc;  // text.csv beside this read-back and the ranking
                 HIPC(c, launch_artist_col(c));               // artist.csv beside text.csv
             }
             if ((rc = sync_counters(c))) return rc;
@@ -1282,10 +1341,16 @@ static int do_count(msa_ctx *c) {
             exact = true;
             long_ok = false;
             if ((rc = reset_artist_table(c))) return rc;
+            c->artist_spec = false;  // its counts are gone with the table
         } else {
             c->nrec_a = c->h_ctr.songs;
         }
     }
+    if (exact && c->artist_spec) {
+        // the split ran the lines shortcut's count, but this input takes the exact reader
+        if ((rc = reset_artist_table(c))) return rc;
+    }
+    c->artist_spec = false;
     if (exact) {
         HIPC(c, launch_artist_col(c));  // read below; the arena it copies keys from is rewritten below
         if ((rc = resolve_col_lens(c))) return rc;
@@ -1371,60 +1436,60 @@ static const u64 kRadixMin = 1ull << 18;
 // covered: key bytes the main sort ordered by (16, or 8 when it left K0 out:
 // the first round then also orders runs equal in count and first 8 bytes)
 static int refine_ties(msa_ctx *c, Ranked &R, int cur, const u8 *wbuf, const u8 *wextra, const u8 *arena,
-                       const u64 *key_off, const u32 *key_len, u32 covered) {
+                       const u64 *key_off, const u32 *key_len, u32 covered, RefineBufs &rb, hipStream_t st) {
     const u64 n = R.n;
-    HIPC(c, hipMemcpyAsync(R.order.p, R.V[cur].p, n * 4, hipMemcpyDeviceToDevice, c->stream));
-    for (DevBuf *b : {&c->t_head, &c->t_tie, &c->t_runid, &c->t_tpos}) HIPC(c, ensure(*b, n * 8));
-    HIPC(c, ensure(c->t_bsum, ((n + 1023) / 1024 + 1) * 8));
-    HIPC(c, ensure(c->t_total, 64));
+    HIPC(c, hipMemcpyAsync(R.order.p, R.V[cur].p, n * 4, hipMemcpyDeviceToDevice, st));
+    for (DevBuf *b : {&rb.t_head, &rb.t_tie, &rb.t_runid, &rb.t_tpos}) HIPC(c, ensure(*b, n * 8));
+    HIPC(c, ensure(rb.t_bsum, ((n + 1023) / 1024 + 1) * 8));
+    HIPC(c, ensure(rb.t_total, 64));
     const u64 *K2 = R.K[cur][0].as<u64>(), *K1 = R.K[cur][1].as<u64>();
     const u64 *K0 = covered == 16 ? R.K[cur][2].as<u64>() : nullptr;
     const u32 *Vc = R.V[cur].as<u32>();
     const u64 *Pc = nullptr;
     u64 mc = n;
     for (u32 r = 1; r < 4096; ++r) {
-        HIPC(c, msa_launch_tie_mark(K2, K1, K0, mc, c->t_head.as<u64>(), c->t_tie.as<u64>(), c->stream));
-        HIPC(c, msa_exclusive_scan(c->t_head.as<u64>(), mc, c->t_runid.as<u64>(), c->t_bsum.as<u64>(),
-                                   c->t_total.as<u64>(), c->stream));
-        HIPC(c, msa_exclusive_scan(c->t_tie.as<u64>(), mc, c->t_tpos.as<u64>(), c->t_bsum.as<u64>(),
-                                   c->t_total.as<u64>(), c->stream));
+        HIPC(c, msa_launch_tie_mark(K2, K1, K0, mc, rb.t_head.as<u64>(), rb.t_tie.as<u64>(), st));
+        HIPC(c, msa_exclusive_scan(rb.t_head.as<u64>(), mc, rb.t_runid.as<u64>(), rb.t_bsum.as<u64>(),
+                                   rb.t_total.as<u64>(), st));
+        HIPC(c, msa_exclusive_scan(rb.t_tie.as<u64>(), mc, rb.t_tpos.as<u64>(), rb.t_bsum.as<u64>(),
+                                   rb.t_total.as<u64>(), st));
         u64 m = 0;
-        HIPC(c, hipMemcpyAsync(&m, c->t_total.p, 8, hipMemcpyDeviceToHost, c->stream));
-        HIPC(c, hipStreamSynchronize(c->stream));
+        HIPC(c, hipMemcpyAsync(&m, rb.t_total.p, 8, hipMemcpyDeviceToHost, st));
+        HIPC(c, hipStreamSynchronize(st));
         if (c->ablate & 4096) fprintf(stderr, "refine_ties: n %llu round %u ties %llu\n", (unsigned long long)n, r,
                                       (unsigned long long)m);
         if (!m) return MSA_OK;
         for (int s = 0; s < 3; ++s) {
-            for (int k = 0; k < 3; ++k) HIPC(c, ensure(c->t_K[s][k], m * 8));
-            HIPC(c, ensure(c->t_V[s], m * 4));
+            for (int k = 0; k < 3; ++k) HIPC(c, ensure(rb.t_K[s][k], m * 8));
+            HIPC(c, ensure(rb.t_V[s], m * 4));
         }
-        HIPC(c, ensure(c->t_Vn, m * 4));
-        HIPC(c, ensure(c->t_Pn, m * 8));
-        HIPC(c, ensure(c->t_Vc, m * 4));
-        HIPC(c, ensure(c->t_Pc, m * 8));
+        HIPC(c, ensure(rb.t_Vn, m * 4));
+        HIPC(c, ensure(rb.t_Pn, m * 8));
+        HIPC(c, ensure(rb.t_Vc, m * 4));
+        HIPC(c, ensure(rb.t_Pc, m * 8));
         u64 *k2[3], *k1[3], *k0[3];
         u32 *vv[3];
         for (int s = 0; s < 3; ++s) {
-            k2[s] = c->t_K[s][0].as<u64>();
-            k1[s] = c->t_K[s][1].as<u64>();
-            k0[s] = c->t_K[s][2].as<u64>();
-            vv[s] = c->t_V[s].as<u32>();
+            k2[s] = rb.t_K[s][0].as<u64>();
+            k1[s] = rb.t_K[s][1].as<u64>();
+            k0[s] = rb.t_K[s][2].as<u64>();
+            vv[s] = rb.t_V[s].as<u32>();
         }
-        HIPC(c, msa_launch_tie_build(c->t_runid.as<u64>(), c->t_head.as<u64>(), c->t_tie.as<u64>(), c->t_tpos.as<u64>(),
+        HIPC(c, msa_launch_tie_build(rb.t_runid.as<u64>(), rb.t_head.as<u64>(), rb.t_tie.as<u64>(), rb.t_tpos.as<u64>(),
                                      mc, Vc, Pc, covered + 16 * (r - 1), R.K[0][2].as<u64>(),
                                      R.ref.as<u64>(), wbuf, wextra, c->l_pos.as<u64>(), c->l_len.as<u32>(), arena,
-                                     key_off, key_len, k2[0], k1[0], k0[0], vv[0], c->t_Vn.as<u32>(),
-                                     c->t_Pn.as<u64>(), c->stream));
+                                     key_off, key_len, k2[0], k1[0], k0[0], vv[0], rb.t_Vn.as<u32>(),
+                                     rb.t_Pn.as<u64>(), st));
         int o = 1;
-        HIPC(c, msa_radix_sort(k2, k1, k0, vv, m, &o, c->sort_scratch.as<u8>(), c->stream));
-        HIPC(c, msa_launch_tie_apply(vv[o], c->t_Vn.as<u32>(), c->t_Pn.as<u64>(), m, R.order.as<u32>(),
-                                     c->t_Vc.as<u32>(), c->t_Pc.as<u64>(), R.K[0][2].as<u64>(),
-                                     covered == 16 ? nullptr : R.K[cur][2].as<u64>(), c->stream));
+        HIPC(c, msa_radix_sort(k2, k1, k0, vv, m, &o, rb.sort_scratch.as<u8>(), st));
+        HIPC(c, msa_launch_tie_apply(vv[o], rb.t_Vn.as<u32>(), rb.t_Pn.as<u64>(), m, R.order.as<u32>(),
+                                     rb.t_Vc.as<u32>(), rb.t_Pc.as<u64>(), R.K[0][2].as<u64>(),
+                                     covered == 16 ? nullptr : R.K[cur][2].as<u64>(), st));
         K2 = k2[o];
         K1 = k1[o];
         K0 = k0[o];
-        Vc = c->t_Vc.as<u32>();
-        Pc = c->t_Pc.as<u64>();
+        Vc = rb.t_Vc.as<u32>();
+        Pc = rb.t_Pc.as<u64>();
         mc = m;
     }
     return fail(c, MSA_ERR_COLLISION, "tie refinement did not converge (equal keys in one table)");
@@ -1435,7 +1500,7 @@ static bool small_sort(const msa_ctx *c, u64 n) { return c->sort_mode == 1 || (c
 // Sort + key blob of one table on stream st (the radix path -- large tables --
 // reads back tie counts and runs on the library stream only).
 static int sort_and_blob(msa_ctx *c, Ranked &R, const u8 *wbuf, const u8 *wextra, const u8 *arena, const u64 *key_off,
-                         const u32 *key_len, int slot, u64 est, hipStream_t st) {
+                         const u32 *key_len, int slot, u64 est, hipStream_t st, RefineBufs &rb) {
     const u64 n = R.n;
     R.host_valid = false;
     R.blob_pending = n != 0;
@@ -1478,17 +1543,16 @@ static int sort_and_blob(msa_ctx *c, Ranked &R, const u8 *wbuf, const u8 *wextra
                                       c->blob_tot.as<u64>() + slot, R.rank_cnt.as<u32>(), st));
         lens_done = true;
     } else if (!small_sort(c, n)) {
-        if (st != c->stream) return fail(c, MSA_ERR_ARG, "radix ranking runs on the library stream");
-        HIPC(c, ensure(c->sort_scratch, msa_radix_scratch_bytes(n)));
+        HIPC(c, ensure(rb.sort_scratch, msa_radix_scratch_bytes(n)));
         // words: the passes over K0 (key bytes 8..15) are left to the tie
         // refinement -- equal (count, first 8 bytes) runs are rare in a word
         // table, so a round over them is cheaper than 8 passes over all entries
         // (artists: prefixes shared by many names; MSA_SORT_K0=1 sorts K0 for words too)
         const bool sk0 = slot != 0 || c->sort_k0;
-        HIPC(c, msa_radix_sort(k2, k1, k0, vv, n, &cur, c->sort_scratch.as<u8>(), c->stream,
+        HIPC(c, msa_radix_sort(k2, k1, k0, vv, n, &cur, rb.sort_scratch.as<u8>(), st,
                                R.vary_ok ? R.vary.as<u64>() : nullptr, sk0));
         int rc;
-        if ((rc = refine_ties(c, R, cur, wbuf, wextra, arena, key_off, key_len, sk0 ? 16 : 8))) return rc;
+        if ((rc = refine_ties(c, R, cur, wbuf, wextra, arena, key_off, key_len, sk0 ? 16 : 8, rb, st))) return rc;
     } else {
         HIPC(c, msa_launch_sort(k2, k1, k0, vv, n, &cur, st));
         HIPC(c, msa_launch_fixup(R.K[cur][0].as<u64>(), R.K[cur][1].as<u64>(), R.K[cur][2].as<u64>(),
@@ -1574,10 +1638,15 @@ static int do_rank(msa_ctx *c, int tables = 3) {
     const u8 *wextra = c->merged_w ? c->imp_w.as<u8>() : c->extra.as<u8>();
     const u64 west = c->h_ctr.s_claimed * 8 + c->h_ctr.m_claimed * 16 + c->h_ctr.l_claimed * 48;
     // artists: on their own stream beside the words when both tables take the
-    // small-table sort (a chain of short latency-bound launches each)
+    // small-table sort (a chain of short latency-bound launches each); a
+    // radix-sorted artist table (configs[4]: millions of artists, its tie
+    // refinement reading counts back round after round) is ranked on a host
+    // thread of its own, with its own scratch, beside the words'
     Ranked &A = c->ra;
     if (da) A.n = c->sum.n_artists;
-    const bool conc = dw && da && small_sort(c, W.n) && small_sort(c, A.n) && A.n;
+    const bool conc_small = dw && da && small_sort(c, W.n) && small_sort(c, A.n) && A.n;
+    const bool conc_thread = dw && da && W.n && A.n && !small_sort(c, A.n);
+    const bool conc = conc_small || conc_thread;
     hipStream_t ast = conc ? c->rank2 : c->stream;
     if (conc) {
         HIPC(c, hipEventRecord(c->ev_r2_fork, c->stream));
@@ -1595,25 +1664,52 @@ static int do_rank(msa_ctx *c, int tables = 3) {
             (void)hipStreamWaitEvent(c->stream, c->ev_r2_join, 0);
         }
     } r2_join{c, conc};
-    if (dw && (rc = sort_and_blob(c, W, wbuf, wextra, nullptr, nullptr, nullptr, 0, west, c->stream))) return rc;
-    prof_end(c, ST_RANK_WORDS, W.n * 64 + W.blob_len);
-    prof_begin(c, ST_RANK_ARTISTS, ast);
-    if (da && A.n) {
-        for (int k = 0; k < 3; ++k) HIPC(c, ensure(A.K[0][k], A.n * 8));
-        HIPC(c, ensure(A.V[0], A.n * 4));
-        HIPC(c, ensure(A.ref, A.n * 8));
-        HIPC(c, ensure(A.cnt, A.n * 8));
-        HIPC(c, msa_launch_artist_entries(c->a_tab.as<u64>(), c->a_list.as<u32>(), A.n,
-                                          c->merged_a ? c->imp_a.as<u8>() : c->arena.as<u8>(),
-                                          c->key_off.as<u64>(), c->key_len.as<u32>(), A.K[0][0].as<u64>(),
-                                          A.K[0][1].as<u64>(), A.K[0][2].as<u64>(), A.V[0].as<u32>(), A.ref.as<u64>(),
-                                          A.cnt.as<u64>(), ast));
-    }
     const u8 *aarena = c->merged_a ? c->imp_a.as<u8>() : c->arena.as<u8>();
-    if (da && (rc = sort_and_blob(c, A, wbuf, wextra, aarena, c->key_off.as<u64>(), c->key_len.as<u32>(), 1,
-                                  A.n * 32, ast)))
+    auto rank_artists = [&]() -> int {
+        int arc;
+        prof_begin(c, ST_RANK_ARTISTS, ast);
+        if (da && A.n) {
+            for (int k = 0; k < 3; ++k) HIPC(c, ensure(A.K[0][k], A.n * 8));
+            HIPC(c, ensure(A.V[0], A.n * 4));
+            HIPC(c, ensure(A.ref, A.n * 8));
+            HIPC(c, ensure(A.cnt, A.n * 8));
+            HIPC(c, msa_launch_artist_entries(c->a_tab.as<u64>(), c->a_list.as<u32>(), A.n, aarena,
+                                              c->key_off.as<u64>(), c->key_len.as<u32>(), A.K[0][0].as<u64>(),
+                                              A.K[0][1].as<u64>(), A.K[0][2].as<u64>(), A.V[0].as<u32>(),
+                                              A.ref.as<u64>(), A.cnt.as<u64>(), ast));
+        }
+        if (da && (arc = sort_and_blob(c, A, wbuf, wextra, aarena, c->key_off.as<u64>(), c->key_len.as<u32>(), 1,
+                                       A.n * 32, ast, conc_thread ? c->rb[1] : c->rb[0])))
+            return arc;
+        prof_end(c, ST_RANK_ARTISTS, A.n * 64 + A.blob_len, ast);
+        return MSA_OK;
+    };
+    int arc = MSA_OK;
+    HIPC(c, ensure(c->blob_tot, 64));  // shared by both tables' blob scans: allocated before the thread
+    std::thread ath;
+    struct TJoin {
+        std::thread &t;
+        ~TJoin() {
+            if (t.joinable()) t.join();
+        }
+    } ath_join{ath};  // joined before r2_join records (declared after it)
+    if (conc_thread)
+        ath = std::thread([&] {
+            if (hipSetDevice(c->device) != hipSuccess) {
+                arc = fail(c, MSA_ERR_HIP, "hipSetDevice on the ranking thread");
+                return;
+            }
+            arc = rank_artists();
+        });
+    if (dw && (rc = sort_and_blob(c, W, wbuf, wextra, nullptr, nullptr, nullptr, 0, west, c->stream, c->rb[0])))
         return rc;
-    prof_end(c, ST_RANK_ARTISTS, A.n * 64 + A.blob_len, ast);
+    prof_end(c, ST_RANK_WORDS, W.n * 64 + W.blob_len);
+    if (conc_thread) {
+        ath.join();
+        if (arc) return arc;
+    } else if ((rc = rank_artists())) {
+        return rc;
+    }
     if (conc) {
         r2_join.on = false;
         HIPC(c, hipEventRecord(c->ev_r2_join, c->rank2));
@@ -1680,6 +1776,7 @@ int msa_create(int device, msa_ctx **out) {
     if (const char *et = getenv("MSA_EARLY_TEXT")) c->early_text = atoi(et) != 0;
     if (const char *gw = getenv("MSA_GATHER_W")) c->gather_w = atoi(gw) != 0;
     if (const char *k0 = getenv("MSA_SORT_K0")) c->sort_k0 = atoi(k0) != 0;
+    if (const char *ts = getenv("MSA_TEXT_AT_SPLIT")) c->text_at_split = atoi(ts) != 0;
     if (const char *me = getenv("MSA_MLOG_ENTRIES")) c->mlog_test = strtoull(me, nullptr, 10);
     if (const char *so = getenv("MSA_SORT")) c->sort_mode = !strcmp(so, "merge") ? 1 : (!strcmp(so, "radix") ? 2 : 0);
     {
@@ -1719,9 +1816,7 @@ void msa_destroy(msa_ctx *c) {
                      &c->nulrel, &c->f0, &c->tss, &c->tse, &c->span_fix, &c->alog, &c->alog_n, &c->acol, &c->alen, &c->aoff, &c->asrc, &c->apairs, &c->tcol, &c->tlen, &c->toff, &c->tsrc, &c->tpairs,
                      &c->tscan_bsum, &c->scan_bsum, &c->scan_total, &c->ar_start, &c->arena, &c->key_off,
                      &c->key_len, &c->key_slot, &c->s_tab, &c->s_list, &c->m_tab, &c->m_list, &c->l_pos, &c->l_len,
-                     &c->l_slot, &c->l_tab, &c->l_list, &c->a_tab, &c->a_list, &c->ctr, &c->kh1, &c->kh2, &c->mlog, &c->mlog_n, &c->lmask, &c->sort_scratch, &c->blob_tot,
-                     &c->t_head, &c->t_tie, &c->t_runid, &c->t_tpos, &c->t_bsum, &c->t_total, &c->t_Vn, &c->t_Pn,
-                     &c->t_Vc, &c->t_Pc};
+                     &c->l_slot, &c->l_tab, &c->l_list, &c->a_tab, &c->a_list, &c->ctr, &c->kh1, &c->kh2, &c->mlog, &c->mlog_n, &c->lmask, &c->blob_tot};
     for (DevBuf *b : all) release(*b);
     for (Ranked *R : {&c->rw, &c->ra}) {
         for (auto &s : R->K)
@@ -1731,9 +1826,14 @@ void msa_destroy(msa_ctx *c) {
                         &R->scan_total, &R->rank_cnt, &R->vary};
         for (DevBuf *b : rb) release(*b);
     }
-    for (auto &s : c->t_K)
-        for (auto &k : s) release(k);
-    for (auto &v : c->t_V) release(v);
+    for (RefineBufs &rb : c->rb) {
+        for (DevBuf *b : {&rb.sort_scratch, &rb.t_head, &rb.t_tie, &rb.t_runid, &rb.t_tpos, &rb.t_bsum, &rb.t_total,
+                          &rb.t_Vn, &rb.t_Pn, &rb.t_Vc, &rb.t_Pc})
+            release(*b);
+        for (auto &s : rb.t_K)
+            for (auto &k : s) release(k);
+        for (auto &v : rb.t_V) release(v);
+    }
     for (ProfStage &s : c->ps) {
         if (s.a) (void)hipEventDestroy(s.a);
         if (s.b) (void)hipEventDestroy(s.b);

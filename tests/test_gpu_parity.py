@@ -229,6 +229,16 @@ def test_bad_header_fails_loudly(msa_mod, ctx):
     assert e.value.code == -4  # MSA_ERR_BADHEADER
 
 
+def test_failed_split_leaves_no_stale_slots(msa_mod, ctx, tmp_path):
+    """A split that fails after its scan (bad header: the artist count and the
+    word tables ran) must not leave claimed table slots behind for the next run."""
+    ctx.load_csv(b"a,b\nSame,s,l,\"repeated words repeated words\"\nOther,s,l,\"more words here\"\n")
+    with pytest.raises(msa_mod.MsaError):
+        ctx.run()
+    data = b"artist,song,link,text\nSame,s,l,\"repeated words again\"\nNew,s,l,\"fresh words\"\n"
+    check_against_oracle(msa_mod, ctx, data, tmp_path, "after_failed_split")
+
+
 # ---------------------------------------------------------------- golden vectors
 from test_oracle import CASES as GOLDEN_CASES, golden  # noqa: E402
 
