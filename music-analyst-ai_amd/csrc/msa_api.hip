@@ -273,7 +273,7 @@ struct msa_ctx {
     int early_text = 0;
     int gather_w = 0;  // env MSA_GATHER_W=1: the deferred text.csv with the LDS-free gather (A/B)
     int sort_k0 = 0;   // env MSA_SORT_K0=1: the words' radix sort covers key bytes 8..15 too
-X
+    int text_at_split = 0;  // env MSA_TEXT_AT_SPLIT=1: text.csv's gather forked at the split's read-back
     // the K2 final-state read-back (launch_scan_fn / wait_scan_fn)
     hipEvent_t ev_fin = nullptr;
     State fin_init{};
@@ -1141,8 +1141,8 @@ static int split_once(msa_ctx *c, int flags) {
     }
     // text.csv's gather forked here, behind the read-back's copies (it needs
     // nothing the host reads back): it runs during the host's header work and
-    // msa_count's launches instead of after them (MSA_TEXT_AT_SPLIT=0: forked
-    // by msa_count)
+    // msa_count's launches instead of after them (MSA_TEXT_AT_SPLIT; otherwise
+    // forked by msa_count)
     if (c->text_deferred && c->text_at_split) {
         int trc;
         if ((trc = start_text_side(c))) return trc;
