@@ -261,6 +261,11 @@ struct msa_ctx {
     // the artist table is ranked on a stream of its own beside the word table
     // (both small-table sorts are launch/latency-bound chains)
     hipStream_t rank2 = nullptr;
+    // artist.csv beside the ranking (env MSA_AUX_COL=0: on the library stream)
+    hipStream_t aux = nullptr;
+    hipEvent_t ev_aux_fork = nullptr, ev_aux_join = nullptr;
+    bool aux_pending = false;
+    int aux_col = 1;
     hipEvent_t ev_r2_fork = nullptr, ev_r2_join = nullptr;
     // split scan: k_scan_struct done (the spans may start) / the spans done
     hipEvent_t ev_scan_a = nullptr, ev_spans = nullptr;
@@ -273,7 +278,7 @@ struct msa_ctx {
     int early_text = 0;
     int gather_w = 0;  // env MSA_GATHER_W=1: the deferred text.csv with the LDS-free gather (A/B)
     int sort_k0 = 0;   // env MSA_SORT_K0=1: the words' radix sort covers key bytes 8..15 too
-    int text_at_split = 0;  // env MSA_TEXT_AT_SPLIT=1: text.csv's gather forked at the split's read-back
+    int text_at_split = 1;  // env MSA_TEXT_AT_SPLIT=0: text.csv's gather forked by msa_count
     // the K2 final-state read-back (launch_scan_fn / wait_scan_fn)
     hipEvent_t ev_fin = nullptr;
     State fin_init{};
@@ -350,14 +355,34 @@ static int put_bytes(msa_ctx *c, u8 *dst, const std::string &b, hipStream_t st);
 static int start_text_side(msa_ctx *c);
 static int launch_text(msa_ctx *c, hipStream_t st);
 // The deferred artist.csv pass on the library stream.
-static hipError_t launch_artist_col(msa_ctx *c) {
-    if (!c->artist_deferred) return hipSuccess;
+// beside: on the aux stream (forked from the library stream here), so that the
+// ranking does not queue behind it; every later call (and join_side) orders
+// the library stream after it again.
+static hipError_t launch_artist_col(msa_ctx *c, bool beside = false) {
+    if (!c->artist_deferred) {
+        if (!beside && c->aux_pending) {
+            c->aux_pending = false;
+            return hipStreamWaitEvent(c->stream, c->ev_aux_join, 0);
+        }
+        return hipSuccess;
+    }
     c->artist_deferred = false;
-    prof_begin(c, ST_ARTIST_COLUMN);
-    if (put_bytes(c, c->acol.as<u8>(), c->artist_hdr, c->stream) ||
-        materialise_column(c, false, c->artist_hdr.size(), c->acol, c->alen, c->aoff, c->asrc, c->apairs, c->stream))
+    hipStream_t st = c->stream;
+    hipError_t e;
+    if (beside) {
+        if ((e = hipEventRecord(c->ev_aux_fork, c->stream)) != hipSuccess) return e;
+        if ((e = hipStreamWaitEvent(c->aux, c->ev_aux_fork, 0)) != hipSuccess) return e;
+        st = c->aux;
+    }
+    prof_begin(c, ST_ARTIST_COLUMN, st);
+    if (put_bytes(c, c->acol.as<u8>(), c->artist_hdr, st) ||
+        materialise_column(c, false, c->artist_hdr.size(), c->acol, c->alen, c->aoff, c->asrc, c->apairs, st))
         return hipErrorUnknown;
-    prof_end(c, ST_ARTIST_COLUMN, c->nrec * 16 * 2);  // ~16-byte artist lines read + written
+    prof_end(c, ST_ARTIST_COLUMN, c->nrec * 16 * 2, st);  // ~16-byte artist lines read + written
+    if (beside) {
+        if ((e = hipEventRecord(c->ev_aux_join, c->aux)) != hipSuccess) return e;
+        c->aux_pending = true;
+    }
     return hipGetLastError();
 }
 // Everything the library owes on its stream: a column pass not launched yet
@@ -368,6 +393,11 @@ static hipError_t join_side(msa_ctx *c) {
         if (e != hipSuccess) return e;
     }
     if (c->text_deferred && launch_text(c, c->stream)) return hipErrorUnknown;
+    if (c->aux_pending) {  // artist.csv beside the ranking
+        c->aux_pending = false;
+        const hipError_t e = hipStreamWaitEvent(c->stream, c->ev_aux_join, 0);
+        if (e != hipSuccess) return e;
+    }
     if (!c->side_pending) return hipSuccess;
     c->side_pending = false;
     return hipStreamWaitEvent(c->stream, c->ev_join, 0);
@@ -1328,7 +1358,7 @@ static int do_count(msa_ctx *c) {
                 if ((rc = start_text_side(c))) return rc;  // text.csv beside this read-back and the ranking
                 launch_long_words(c, nl);
                 long_ran = true;
-                HIPC(c, launch_artist_col(c));               // artist.csv beside text.csv
+                HIPC(c, launch_artist_col(c, c->aux_col));   // artist.csv beside text.csv and the ranking
             }
             if ((rc = sync_counters(c))) return rc;
             long_ok = attempt == 0;
@@ -1777,6 +1807,7 @@ int msa_create(int device, msa_ctx **out) {
     if (const char *gw = getenv("MSA_GATHER_W")) c->gather_w = atoi(gw) != 0;
     if (const char *k0 = getenv("MSA_SORT_K0")) c->sort_k0 = atoi(k0) != 0;
     if (const char *ts = getenv("MSA_TEXT_AT_SPLIT")) c->text_at_split = atoi(ts) != 0;
+    if (const char *ac = getenv("MSA_AUX_COL")) c->aux_col = atoi(ac) != 0;
     if (const char *me = getenv("MSA_MLOG_ENTRIES")) c->mlog_test = strtoull(me, nullptr, 10);
     if (const char *so = getenv("MSA_SORT")) c->sort_mode = !strcmp(so, "merge") ? 1 : (!strcmp(so, "radix") ? 2 : 0);
     {
@@ -1789,6 +1820,9 @@ int msa_create(int device, msa_ctx **out) {
     const hipError_t side_e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess || side_e != hipSuccess ||
         hipStreamCreateWithFlags(&c->rank2, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_aux_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_aux_join, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_r2_fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_r2_join, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_scan_a, hipEventDisableTiming) != hipSuccess ||
@@ -1850,6 +1884,9 @@ void msa_destroy(msa_ctx *c) {
     (void)hipEventDestroy(c->ev_tscan);
     (void)hipStreamDestroy(c->side);
     (void)hipStreamDestroy(c->rank2);
+    (void)hipStreamDestroy(c->aux);
+    (void)hipEventDestroy(c->ev_aux_fork);
+    (void)hipEventDestroy(c->ev_aux_join);
     (void)hipStreamDestroy(c->stream);
     delete c;
 }

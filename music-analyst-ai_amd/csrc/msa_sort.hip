@@ -63,8 +63,12 @@ __global__ __launch_bounds__(256) void k_rx_vary(const u64 *__restrict__ K2, con
 // each wave (ballot multi-split + per-wave running counts in LDS), publish
 // their per-digit counts and look back over earlier tiles' published counts
 // (decoupled look-back, one digit per thread) for their global offsets.
+#ifndef OS_T
 #define OS_T 512
+#endif
+#ifndef OS_PER
 #define OS_PER 16
+#endif
 #define OS_TILE (OS_T * OS_PER)
 #define OS_W (OS_T / 64)
 #define OS_POS 24               // byte positions: K0 bytes 0..7, K1, K2
