@@ -61,15 +61,19 @@ hipError_t msa_launch_artist_entries(const u64 *, const u32 *, u64, const u8 *, 
                                      u64 *, u32 *, u64 *, u64 *, hipStream_t);
 u64 msa_radix_scratch_bytes(u64 n);
 hipError_t msa_radix_sort(u64 *const[3], u64 *const[3], u64 *const[3], u32 *const[3], u64, int *, u8 *, hipStream_t,
-                          const u64 * = nullptr, bool = true);
+                          const u64 * = nullptr, bool = true, const u64 * = nullptr, bool = false);
+u64 msa_comp_scratch_bytes();
+hipError_t msa_radix_sort_comp(u64 *const[3], u64 *const[3], u64 *const[3], u32 *const[3], u64, int *, u8 *,
+                               hipStream_t, const u64 *, u64 *, u8 *, u32 *);
+hipError_t msa_comp_finish(u64 *, u64, const u8 *, u32, hipStream_t);
 hipError_t msa_launch_tie_mark(const u64 *, const u64 *, const u64 *, u64, u64 *, u64 *, hipStream_t);
 hipError_t msa_launch_tie_build(const u64 *, const u64 *, const u64 *, const u64 *, u64, const u32 *, const u64 *, u32,
-                                const u64 *,
+                                const u64 *, const u64 *,
                                 const u64 *,
                                 const u8 *, const u8 *, const u64 *, const u32 *, const u8 *, const u64 *, const u32 *,
                                 u64 *, u64 *, u64 *, u32 *, u32 *, u64 *, hipStream_t);
-hipError_t msa_launch_tie_apply(const u32 *, const u32 *, const u64 *, u64, u32 *, u32 *, u64 *, const u64 *, u64 *,
-                                hipStream_t);
+hipError_t msa_launch_tie_apply(const u32 *, const u32 *, const u64 *, u64, u32 *, u32 *, u64 *, const u64 *,
+                                const u64 *, u64 *, u64 *, hipStream_t);
 hipError_t msa_launch_sort(u64 *const[3], u64 *const[3], u64 *const[3], u32 *const[3], u64, int *, hipStream_t);
 hipError_t msa_launch_fixup(const u64 *, const u64 *, const u64 *, const u32 *, u64, const u64 *, const u8 *,
                             const u8 *, const u64 *, const u32 *, const u8 *, const u64 *, const u32 *, u32 *, hipStream_t);
@@ -121,6 +125,7 @@ struct Ranked {
     u64 n = 0, blob_len = 0, blob_cap = 0;
     u64 lthr = 0;  // words: entries [0, lthr) are S/M keys (k_word_entries' order)
     DevBuf vary;   // the key planes' OR / AND over the entries (k_word_entries), for the radix sort
+    DevBuf comp, cset;  // words: the composite sort keys and the distinct-count set (msa_radix_sort_comp)
     bool vary_ok = false;
     bool blob_pending = false;  // blob_len not read back yet (do_rank's sync)
     BlobArgs pending{};
@@ -279,6 +284,11 @@ struct msa_ctx {
     int gather_w = 0;  // env MSA_GATHER_W=1: the deferred text.csv with the LDS-free gather (A/B)
     int sort_k0 = 0;   // env MSA_SORT_K0=1: the words' radix sort covers key bytes 8..15 too
     int text_at_split = 1;  // env MSA_TEXT_AT_SPLIT=0: text.csv's gather forked by msa_count
+    int comp_sort = 1;      // env MSA_COMP_SORT=0: the words' radix sort by K2 and K1 (no composite key)
+    // env MSA_TEXT_AT_SPANS=1: text.csv's gather forked from the spans' stream
+    // (measured and rejected: it slowed the artist pass beside it, 0.13 -> 0.51
+    // ms, 2.97-3.00 vs 2.92-2.95 ms/step; profiles/r04_t28_ab_text_at_spans.txt)
+    int text_at_spans = 0;
     // the K2 final-state read-back (launch_scan_fn / wait_scan_fn)
     hipEvent_t ev_fin = nullptr;
     State fin_init{};
@@ -953,15 +963,22 @@ static int split_prologue(msa_ctx *c, u64 nul_n, bool rs0) {
     Prologue p{};
     struct {
         DevBuf *tab, *list;
-        u64 *used;
+        u64 *used, slots;
         u32 w;
-    } t[4] = {{&c->s_tab, &c->s_list, &c->s_used_prev, 2},
-              {&c->m_tab, &c->m_list, &c->m_used_prev, 4},
-              {&c->l_tab, &c->l_list, &c->lt_used_prev, 4},
-              {&c->a_tab, &c->a_list, &c->a_used_prev, 4}};
+    } t[4] = {{&c->s_tab, &c->s_list, &c->s_used_prev, c->s_slots, 2},
+              {&c->m_tab, &c->m_list, &c->m_used_prev, c->m_slots, 4},
+              {&c->l_tab, &c->l_list, &c->lt_used_prev, c->lt_slots, 4},
+              {&c->a_tab, &c->a_list, &c->a_used_prev, c->a_slots, 4}};
     u32 blocks = 0;
     for (int j = 0; j < 4; ++j) {
-        const u64 n = t[j].tab->p ? *t[j].used : 0;
+        u64 n = t[j].tab->p ? *t[j].used : 0;
+        // a slot cleared by itself costs about as much as zeroing 128 bytes
+        // of a whole table (configs[4]: 45 M claimed word slots took 1.4 ms
+        // of scattered clears): past that, the table is zeroed whole
+        if (n && n * 128 > t[j].slots * t[j].w * 8 && !(c->ablate & 1048576)) {
+            HIPC(c, hipMemsetAsync(t[j].tab->p, 0, t[j].slots * t[j].w * 8, c->stream));
+            n = 0;
+        }
         p.job[j] = ClearJob{t[j].tab->as<u64>(), t[j].list->as<u32>(), n, t[j].w, (u32)((n + PRO_T - 1) / PRO_T)};
         blocks += p.job[j].blocks;
         *t[j].used = 0;
@@ -1145,6 +1162,16 @@ static int split_once(msa_ctx *c, int flags) {
     if (want_text && !early) {  // text.csv's body: deferred (msa_ctx::text_deferred)
         HIPC(c, ensure(c->tcol, kColHdrRoom + c->n + 1 + MSA_INPUT_PAD));
         c->text_deferred = true;
+        // forked from the spans' stream as soon as they are final (rank2 was
+        // ordered after this split's prologue; the gather reads only the input,
+        // the spans and the body length the spans' scan wrote), not behind the
+        // miss aggregation, the artist pass and the read-back's copies
+        if (spans_beside && c->text_at_spans) {
+            HIPC(c, hipStreamWaitEvent(c->side, c->ev_spans, 0));
+            if ((rc = launch_text(c, c->side))) return rc;
+            HIPC(c, hipEventRecord(c->ev_join, c->side));
+            c->side_pending = true;
+        }
     }
     // one read-back after the scan: the counters (table overflow, long-word
     // occurrences) and -- for the first shard -- the header record's end plus
@@ -1464,15 +1491,18 @@ static const u64 kRadixMin = 1ull << 18;
 // re-sorts the tied entries by (their run, key bytes [16 r, 16 r + 16)) with
 // the radix sort, until no two adjacent keys are equal (keys are distinct).
 // covered: key bytes the main sort ordered by (16, or 8 when it left K0 out:
-// the first round then also orders runs equal in count and first 8 bytes)
+// the first round then also orders runs equal in count and first 8 bytes; 6
+// or 7 after the composite key's sort, whose sorted keys -- the set's K2
+// plane -- mark the first round's runs)
 static int refine_ties(msa_ctx *c, Ranked &R, int cur, const u8 *wbuf, const u8 *wextra, const u8 *arena,
-                       const u64 *key_off, const u32 *key_len, u32 covered, RefineBufs &rb, hipStream_t st) {
+                       const u64 *key_off, const u32 *key_len, u32 covered, RefineBufs &rb, hipStream_t st,
+                       bool comp = false) {
     const u64 n = R.n;
     HIPC(c, hipMemcpyAsync(R.order.p, R.V[cur].p, n * 4, hipMemcpyDeviceToDevice, st));
     for (DevBuf *b : {&rb.t_head, &rb.t_tie, &rb.t_runid, &rb.t_tpos}) HIPC(c, ensure(*b, n * 8));
     HIPC(c, ensure(rb.t_bsum, ((n + 1023) / 1024 + 1) * 8));
     HIPC(c, ensure(rb.t_total, 64));
-    const u64 *K2 = R.K[cur][0].as<u64>(), *K1 = R.K[cur][1].as<u64>();
+    const u64 *K2 = R.K[cur][0].as<u64>(), *K1 = comp ? K2 : R.K[cur][1].as<u64>();
     const u64 *K0 = covered == 16 ? R.K[cur][2].as<u64>() : nullptr;
     const u32 *Vc = R.V[cur].as<u32>();
     const u64 *Pc = nullptr;
@@ -1506,14 +1536,15 @@ static int refine_ties(msa_ctx *c, Ranked &R, int cur, const u8 *wbuf, const u8 
             vv[s] = rb.t_V[s].as<u32>();
         }
         HIPC(c, msa_launch_tie_build(rb.t_runid.as<u64>(), rb.t_head.as<u64>(), rb.t_tie.as<u64>(), rb.t_tpos.as<u64>(),
-                                     mc, Vc, Pc, covered + 16 * (r - 1), R.K[0][2].as<u64>(),
+                                     mc, Vc, Pc, covered + 16 * (r - 1), R.K[0][1].as<u64>(), R.K[0][2].as<u64>(),
                                      R.ref.as<u64>(), wbuf, wextra, c->l_pos.as<u64>(), c->l_len.as<u32>(), arena,
                                      key_off, key_len, k2[0], k1[0], k0[0], vv[0], rb.t_Vn.as<u32>(),
                                      rb.t_Pn.as<u64>(), st));
         int o = 1;
         HIPC(c, msa_radix_sort(k2, k1, k0, vv, m, &o, rb.sort_scratch.as<u8>(), st));
         HIPC(c, msa_launch_tie_apply(vv[o], rb.t_Vn.as<u32>(), rb.t_Pn.as<u64>(), m, R.order.as<u32>(),
-                                     rb.t_Vc.as<u32>(), rb.t_Pc.as<u64>(), R.K[0][2].as<u64>(),
+                                     rb.t_Vc.as<u32>(), rb.t_Pc.as<u64>(), R.K[0][1].as<u64>(), R.K[0][2].as<u64>(),
+                                     covered < 8 ? R.K[cur][1].as<u64>() : nullptr,
                                      covered == 16 ? nullptr : R.K[cur][2].as<u64>(), st));
         K2 = k2[o];
         K1 = k1[o];
@@ -1579,10 +1610,24 @@ static int sort_and_blob(msa_ctx *c, Ranked &R, const u8 *wbuf, const u8 *wextra
         // table, so a round over them is cheaper than 8 passes over all entries
         // (artists: prefixes shared by many names; MSA_SORT_K0=1 sorts K0 for words too)
         const bool sk0 = slot != 0 || c->sort_k0;
-        HIPC(c, msa_radix_sort(k2, k1, k0, vv, n, &cur, rb.sort_scratch.as<u8>(), st,
-                               R.vary_ok ? R.vary.as<u64>() : nullptr, sk0));
+        // words: the composite key (dense count rank + first key bytes, one
+        // word; msa_sort.hip) when the counts take few enough distinct values
+        u32 gB = ~0u;
+        if (!sk0 && c->comp_sort && R.vary_ok) {
+            HIPC(c, ensure(R.comp, n * 8));
+            HIPC(c, ensure(R.cset, msa_comp_scratch_bytes()));
+            HIPC(c, msa_radix_sort_comp(k2, k1, k0, vv, n, &cur, rb.sort_scratch.as<u8>(), st, R.vary.as<u64>(),
+                                        R.comp.as<u64>(), R.cset.as<u8>(), &gB));
+        }
         int rc;
-        if ((rc = refine_ties(c, R, cur, wbuf, wextra, arena, key_off, key_len, sk0 ? 16 : 8, rb, st))) return rc;
+        if (gB != ~0u) {
+            if ((rc = refine_ties(c, R, cur, wbuf, wextra, arena, key_off, key_len, 8 - gB, rb, st, true))) return rc;
+            HIPC(c, msa_comp_finish(R.K[cur][0].as<u64>(), n, R.cset.as<u8>(), gB, st));
+        } else {
+            HIPC(c, msa_radix_sort(k2, k1, k0, vv, n, &cur, rb.sort_scratch.as<u8>(), st,
+                                   R.vary_ok ? R.vary.as<u64>() : nullptr, sk0));
+            if ((rc = refine_ties(c, R, cur, wbuf, wextra, arena, key_off, key_len, sk0 ? 16 : 8, rb, st))) return rc;
+        }
     } else {
         HIPC(c, msa_launch_sort(k2, k1, k0, vv, n, &cur, st));
         HIPC(c, msa_launch_fixup(R.K[cur][0].as<u64>(), R.K[cur][1].as<u64>(), R.K[cur][2].as<u64>(),
@@ -1807,6 +1852,8 @@ int msa_create(int device, msa_ctx **out) {
     if (const char *gw = getenv("MSA_GATHER_W")) c->gather_w = atoi(gw) != 0;
     if (const char *k0 = getenv("MSA_SORT_K0")) c->sort_k0 = atoi(k0) != 0;
     if (const char *ts = getenv("MSA_TEXT_AT_SPLIT")) c->text_at_split = atoi(ts) != 0;
+    if (const char *tp = getenv("MSA_TEXT_AT_SPANS")) c->text_at_spans = atoi(tp) != 0;
+    if (const char *cs = getenv("MSA_COMP_SORT")) c->comp_sort = atoi(cs) != 0;
     if (const char *ac = getenv("MSA_AUX_COL")) c->aux_col = atoi(ac) != 0;
     if (const char *me = getenv("MSA_MLOG_ENTRIES")) c->mlog_test = strtoull(me, nullptr, 10);
     if (const char *so = getenv("MSA_SORT")) c->sort_mode = !strcmp(so, "merge") ? 1 : (!strcmp(so, "radix") ? 2 : 0);

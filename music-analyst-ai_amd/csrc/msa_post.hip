@@ -2008,7 +2008,7 @@ __device__ __forceinline__ void key16_round(u64 refv, u32 skip, const u8 *buf, c
 __global__ void k_tie_build(const u64 *__restrict__ runid, const u64 *__restrict__ head, const u64 *__restrict__ tie,
                             const u64 *__restrict__ tpos,
                             u64 mc, const u32 *__restrict__ Vc, const u64 *__restrict__ Pc, u32 skip,
-                            const u64 *__restrict__ K0u,
+                            const u64 *__restrict__ K1u, const u64 *__restrict__ K0u,
                             const u64 *__restrict__ ref, const u8 *buf, const u8 *extra, const u64 *l_pos,
                             const u32 *l_len, const u8 *arena, const u64 *key_off, const u32 *key_len,
                             u64 *__restrict__ K2n, u64 *__restrict__ K1n, u64 *__restrict__ K0n,
@@ -2018,11 +2018,20 @@ __global__ void k_tie_build(const u64 *__restrict__ runid, const u64 *__restrict
     const u64 j = tpos[i];
     const u32 e = Vc[i];
     u64 hi, lo;
-    if (skip == 8) {  // after a K2/K1-only sort: bytes 8..15 are K0 (S/M keys have no byte source)
+    if (skip <= 8) {  // after a sort of fewer than 16 key bytes: bytes skip .. 15 are in K1/K0 (S/M keys have
+                      // no byte source), bytes 16 .. from the key's bytes
         u64 h2, l2;
         key16_round(ref[e], 16, buf, extra, l_pos, l_len, arena, key_off, key_len, &h2, &l2);
-        hi = K0u[e];
-        lo = h2;
+        const u64 k0 = K0u[e];
+        if (skip == 8) {
+            hi = k0;
+            lo = h2;
+        } else {  // the composite key's sort (skip 6 or 7: msa_radix_sort_comp)
+            const u32 sb = 8 * skip;
+            const u64 k1 = K1u[e];
+            hi = (k1 << sb) | (k0 >> (64 - sb));
+            lo = (k0 << sb) | (h2 >> (64 - sb));
+        }
     } else {
         key16_round(ref[e], skip, buf, extra, l_pos, l_len, arena, key_off, key_len, &hi, &lo);
     }
@@ -2039,12 +2048,14 @@ __global__ void k_tie_build(const u64 *__restrict__ runid, const u64 *__restrict
 // tied entries' K0 differ, and the key blob reads K0 in rank order)
 __global__ void k_tie_apply(const u32 *__restrict__ perm, const u32 *__restrict__ Vn, const u64 *__restrict__ Pn,
                             u64 m, u32 *__restrict__ order, u32 *__restrict__ Vc, u64 *__restrict__ Pc,
-                            const u64 *__restrict__ K0u, u64 *__restrict__ ks0) {
+                            const u64 *__restrict__ K1u, const u64 *__restrict__ K0u, u64 *__restrict__ ks1,
+                            u64 *__restrict__ ks0) {
     const u64 j = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= m) return;
     const u32 e = Vn[perm[j]];
     order[Pn[j]] = e;
     if (ks0) ks0[Pn[j]] = K0u[e];
+    if (ks1) ks1[Pn[j]] = K1u[e];  // the composite key's sort: tied entries share only bytes 0 .. skip-1
     Vc[j] = e;
     Pc[j] = Pn[j];
 }
@@ -2084,19 +2095,12 @@ __global__ void k_blob_len(const u32 *__restrict__ order, u64 n, const u64 *__re
                          : entry_key_len(ref[e], K1u[e], K0u[e], l_len, key_len);
 }
 
-__global__ void k_blob_write(const u32 *__restrict__ order, u64 n, const u64 *__restrict__ ref,
-                             const u64 *__restrict__ K1u, const u64 *__restrict__ K0u, const u64 *__restrict__ cnt,
-                             const u8 *buf, const u8 *extra, const u64 *l_pos, const u32 *l_len, const u8 *arena,
-                             const u64 *key_off, const u32 *key_len, const u64 *__restrict__ off,
-                             const u64 *__restrict__ len, SortedKeys sk, u8 *__restrict__ blob,
-                             u64 *__restrict__ counts_out, u64 blob_cap) {
-    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const u32 e = order[i];
-    counts_out[i] = sk.K2 ? ~sk.K2[i] : cnt[e];
-    if (off[i] + len[i] > blob_cap) return;
+// one entry's key bytes to dst (rank i, entry e = order[i])
+__device__ __forceinline__ void blob_key_bytes(u64 i, u32 e, const u64 *__restrict__ ref, const u64 *__restrict__ K1u,
+                                               const u64 *__restrict__ K0u, const u8 *buf, const u8 *extra,
+                                               const u64 *l_pos, const u32 *l_len, const u8 *arena,
+                                               const u64 *key_off, const u32 *key_len, const SortedKeys &sk, u8 *dst) {
     if (e < sk.lthr) {  // S/M word: the key is the sorted K1/K0
-        u8 *dst = blob + off[i];
         const u64 k1 = sk.K1[i], k0 = sk.K0[i];
         for (int k = 0; k < 16; ++k) {
             const u8 b = (u8)((k < 8 ? k1 : k0) >> (56 - 8 * (k & 7)));
@@ -2108,11 +2112,6 @@ __global__ void k_blob_write(const u32 *__restrict__ order, u64 n, const u64 *__
     const u64 r = ref[e];
     const u32 kind = (u32)(r >> 60);
     const u64 idx = r & ((1ull << 60) - 1);
-    // the blob was sized before its length came back to the host: a key that
-    // does not fit is skipped (the host sees the total, grows the blob and
-    // writes it again)
-    if (off[i] + len[i] > blob_cap) return;
-    u8 *dst = blob + off[i];
     if (kind == KIND_L) {
         const u8 *p = tok_at(buf, extra, l_pos[idx]);
         for (u32 k = 0; k < l_len[idx]; ++k) dst[k] = (u8)lower1(p[k]);
@@ -2120,10 +2119,66 @@ __global__ void k_blob_write(const u32 *__restrict__ order, u64 n, const u64 *__
         const u8 *p = arena + key_off[idx];
         for (u32 k = 0; k < key_len[idx]; ++k) dst[k] = p[k];
     } else {
+        const u64 k1 = K1u[e], k0 = K0u[e];
         for (int k = 0; k < 16; ++k) {
-            const u8 b = (u8)((k < 8 ? K1u[e] : K0u[e]) >> (56 - 8 * (k & 7)));
+            const u8 b = (u8)((k < 8 ? k1 : k0) >> (56 - 8 * (k & 7)));
             if (!b) break;
             dst[k] = b;
+        }
+    }
+}
+
+// A workgroup writes the keys of BW_T consecutive ranks: their bytes are one
+// contiguous range of the blob, composed in LDS at the blob's 16-byte phase
+// and written as whole 16-byte chunks (the range's first and last chunk byte
+// by byte: they share bytes with the neighbouring workgroups).  Byte stores
+// of every key straight to the blob (one lane per key, 1-16 byte stores at
+// scattered offsets) had cost 1.6 ms for configs[4]'s 50 M words.  A range
+// longer than the staging buffer (long keys), or past the blob's capacity,
+// is written key by key.
+#define BW_T 256
+#define BW_LDS 16384
+__global__ __launch_bounds__(BW_T) void k_blob_write(const u32 *__restrict__ order, u64 n, const u64 *__restrict__ ref,
+                                                     const u64 *__restrict__ K1u, const u64 *__restrict__ K0u,
+                                                     const u64 *__restrict__ cnt, const u8 *buf, const u8 *extra,
+                                                     const u64 *l_pos, const u32 *l_len, const u8 *arena,
+                                                     const u64 *key_off, const u32 *key_len,
+                                                     const u64 *__restrict__ off, const u64 *__restrict__ len,
+                                                     SortedKeys sk, u8 *__restrict__ blob,
+                                                     u64 *__restrict__ counts_out, u64 blob_cap) {
+    __shared__ __attribute__((aligned(16))) u8 stage[BW_LDS + 32];
+    const u32 t = threadIdx.x;
+    const u64 i0 = (u64)blockIdx.x * BW_T, i = i0 + t;
+    const u64 last = min(n, i0 + BW_T) - 1;
+    const bool live = i < n;
+    const u32 e = live ? order[i] : 0u;
+    if (live) counts_out[i] = sk.K2 ? ~sk.K2[i] : cnt[e];
+    const u64 base = off[i0], end = off[last] + len[last];
+    const u32 ph = (u32)(base & 15u);
+    if (end - base > BW_LDS || end > blob_cap) {  // key by key (uniform per workgroup)
+        // the blob was sized before its length came back to the host: a key
+        // that does not fit is skipped (the host sees the total, grows the
+        // blob and writes it again)
+        if (live && off[i] + len[i] <= blob_cap)
+            blob_key_bytes(i, e, ref, K1u, K0u, buf, extra, l_pos, l_len, arena, key_off, key_len, sk, blob + off[i]);
+        return;
+    }
+    if (live)
+        blob_key_bytes(i, e, ref, K1u, K0u, buf, extra, l_pos, l_len, arena, key_off, key_len, sk,
+                       stage + ph + (off[i] - base));
+    __syncthreads();
+    // chunks c = 0 .. nc-1 cover blob bytes [base - ph + 16 c, + 16)
+    const u64 L = end - base;
+    if (!L) return;
+    const u32 nc = (u32)((ph + L + 15) >> 4);
+    u8 *gb = blob + (base - ph);
+    for (u32 c = t; c < nc; c += BW_T) {
+        const u32 lo = c * 16u, hi = lo + 16u;
+        if (lo >= ph && hi <= ph + L) {
+            *reinterpret_cast<uint4 *>(gb + lo) = *reinterpret_cast<const uint4 *>(stage + lo);
+        } else {
+            const u32 a = max(lo, ph), b = min(hi, (u32)(ph + L));
+            for (u32 k = a; k < b; ++k) gb[k] = stage[k];
         }
     }
 }
@@ -2661,7 +2716,7 @@ hipError_t msa_launch_blob(const u32 *order, u64 n, const u64 *ref, const u64 *K
         hipLaunchKernelGGL(k_blob_len, grid1(n), dim3(256), 0, s, order, n, ref, K1u, K0u, l_len, key_len, sk, len);
         return msa_exclusive_scan(len, n, off, bsum, total, s);
     }
-    hipLaunchKernelGGL(k_blob_write, grid1(n), dim3(256), 0, s, order, n, ref, K1u, K0u, cnt, buf, extra, l_pos, l_len, arena,
+    hipLaunchKernelGGL(k_blob_write, grid1(n, BW_T), dim3(BW_T), 0, s, order, n, ref, K1u, K0u, cnt, buf, extra, l_pos, l_len, arena,
                        key_off, key_len, (const u64 *)off, (const u64 *)len, sk, blob, counts_out, blob_cap);
     return hipGetLastError();
 }
@@ -2672,18 +2727,18 @@ hipError_t msa_launch_tie_mark(const u64 *K2, const u64 *K1, const u64 *K0, u64 
 }
 hipError_t msa_launch_tie_build(const u64 *runid, const u64 *head, const u64 *tie, const u64 *tpos, u64 mc, const u32 *Vc,
                                 const u64 *Pc,
-                                u32 skip, const u64 *K0u, const u64 *ref, const u8 *buf, const u8 *extra,
+                                u32 skip, const u64 *K1u, const u64 *K0u, const u64 *ref, const u8 *buf, const u8 *extra,
                                 const u64 *l_pos, const u32 *l_len, const u8 *arena, const u64 *key_off,
                                 const u32 *key_len, u64 *K2n, u64 *K1n, u64 *K0n, u32 *Vid, u32 *Vn, u64 *Pn,
                                 hipStream_t s) {
     if (mc)
-        hipLaunchKernelGGL(k_tie_build, grid1(mc), dim3(256), 0, s, runid, head, tie, tpos, mc, Vc, Pc, skip, K0u, ref,
+        hipLaunchKernelGGL(k_tie_build, grid1(mc), dim3(256), 0, s, runid, head, tie, tpos, mc, Vc, Pc, skip, K1u, K0u, ref,
                            buf, extra,
                            l_pos, l_len, arena, key_off, key_len, K2n, K1n, K0n, Vid, Vn, Pn);
     return hipGetLastError();
 }
 hipError_t msa_launch_tie_apply(const u32 *perm, const u32 *Vn, const u64 *Pn, u64 m, u32 *order, u32 *Vc, u64 *Pc,
-                                const u64 *K0u, u64 *ks0, hipStream_t s) {
-    if (m) hipLaunchKernelGGL(k_tie_apply, grid1(m), dim3(256), 0, s, perm, Vn, Pn, m, order, Vc, Pc, K0u, ks0);
+                                const u64 *K1u, const u64 *K0u, u64 *ks1, u64 *ks0, hipStream_t s) {
+    if (m) hipLaunchKernelGGL(k_tie_apply, grid1(m), dim3(256), 0, s, perm, Vn, Pn, m, order, Vc, Pc, K1u, K0u, ks1, ks0);
     return hipGetLastError();
 }

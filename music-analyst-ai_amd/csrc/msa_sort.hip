@@ -71,6 +71,9 @@ __global__ __launch_bounds__(256) void k_rx_vary(const u64 *__restrict__ K2, con
 #endif
 #define OS_TILE (OS_T * OS_PER)
 #define OS_W (OS_T / 64)
+#ifndef GH_FLY
+#define GH_FLY 4
+#endif
 #define OS_POS 24               // byte positions: K0 bytes 0..7, K1, K2
 #define OS_SPIN_LIMIT (1u << 24)  // polls before a look-back gives up (error, never a hang)
 
@@ -82,21 +85,36 @@ __global__ __launch_bounds__(256) void k_os_ghist(const u64 *__restrict__ K0, co
     const u32 t = threadIdx.x;
     for (u32 k = t; k < OS_POS * 256; k += 256) h[k] = 0;
     __syncthreads();
-    for (u64 i = (u64)blockIdx.x * 256 + t; i < n; i += (u64)gridDim.x * 256) {
-        const u64 w[3] = {(pmask & 0xFFu) ? K0[i] : 0, (pmask & 0xFF00u) ? K1[i] : 0,
-                          (pmask & 0xFF0000u) ? K2[i] : 0};
-        const u64 act = __ballot(1);
+    // GH_FLY entries per thread per round, their loads issued first: one
+    // entry per round left every wave waiting on its loads (8 waves per CU,
+    // ~100 rounds each: 1.1 ms for configs[4]'s 50 M word entries)
+    const u64 stride = (u64)gridDim.x * 256;
+    for (u64 i0 = (u64)blockIdx.x * 256 + t; i0 < n; i0 += GH_FLY * stride) {
+        u64 w[GH_FLY][3];
 #pragma unroll
-        for (u32 p = 0; p < OS_POS; ++p) {
-            if (!((pmask >> p) & 1u)) continue;
-            const u32 d = (u32)(w[p >> 3] >> (8 * (p & 7))) & 0xFFu;
-            // a digit the whole wave shares (zero padding of short keys, the
-            // high bytes of small counts): one add instead of a 64-way conflict
-            const u32 d0 = __builtin_amdgcn_readfirstlane(d);
-            if (__ballot(d == d0) == act) {
-                if (mbcnt(act) == 0) atomicAdd(&h[p * 256 + d0], (u32)__popcll(act));
-            } else {
-                atomicAdd(&h[p * 256 + d], 1u);
+        for (u32 q = 0; q < GH_FLY; ++q) {
+            const u64 i = i0 + q * stride;
+            const bool ok = i < n;
+            w[q][0] = ok && (pmask & 0xFFu) ? K0[i] : 0;
+            w[q][1] = ok && (pmask & 0xFF00u) ? K1[i] : 0;
+            w[q][2] = ok && (pmask & 0xFF0000u) ? K2[i] : 0;
+        }
+#pragma unroll
+        for (u32 q = 0; q < GH_FLY; ++q) {
+            if (i0 + q * stride >= n) break;
+            const u64 act = __ballot(1);
+#pragma unroll
+            for (u32 p = 0; p < OS_POS; ++p) {
+                if (!((pmask >> p) & 1u)) continue;
+                const u32 d = (u32)(w[q][p >> 3] >> (8 * (p & 7))) & 0xFFu;
+                // a digit the whole wave shares (zero padding of short keys, the
+                // high bytes of small counts): one add instead of a 64-way conflict
+                const u32 d0 = __builtin_amdgcn_readfirstlane(d);
+                if (__ballot(d == d0) == act) {
+                    if (mbcnt(act) == 0) atomicAdd(&h[p * 256 + d0], (u32)__popcll(act));
+                } else {
+                    atomicAdd(&h[p * 256 + d], 1u);
+                }
             }
         }
     }
@@ -267,15 +285,18 @@ __global__ void k_rx_gather(const u64 *__restrict__ src, const u32 *__restrict__
 
 // the sorted entries; word `wsel` (0 = K0 .. 2 = K2; 3 = none) is already in
 // order in Ws (the last sorted word), the others are gathered through V
+// k0z: keys hold no zero byte (words), so a key whose byte 7 is zero ended
+// before byte 8 and its K0 is zero -- not gathered (most words are short)
 __global__ void k_rx_final(const u64 *__restrict__ K2, const u64 *__restrict__ K1, const u64 *__restrict__ K0,
-                           const u32 *__restrict__ V, u64 n, const u64 *__restrict__ Ws, u32 wsel,
+                           const u32 *__restrict__ V, u64 n, const u64 *__restrict__ Ws, u32 wsel, u32 k0z,
                            u64 *__restrict__ O2, u64 *__restrict__ O1, u64 *__restrict__ O0, u32 *__restrict__ OV) {
     const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const u32 v = V[i];
     O2[i] = wsel == 2 ? Ws[i] : K2[v];
-    O1[i] = wsel == 1 ? Ws[i] : K1[v];
-    O0[i] = wsel == 0 ? Ws[i] : K0[v];
+    const u64 k1 = wsel == 1 ? Ws[i] : K1[v];
+    O1[i] = k1;
+    O0[i] = wsel == 0 ? Ws[i] : ((k0z && !(k1 & 0xFFu)) ? 0ull : K0[v]);
     OV[i] = v;
 }
 
@@ -294,7 +315,8 @@ u64 msa_radix_scratch_bytes(u64 n) {
 // lands in set 1 or 2 (*which).  Sets 1 and 2 are scratch, as for
 // msa_launch_sort.  `scratch` holds msa_radix_scratch_bytes(n) bytes.
 hipError_t msa_radix_sort(u64 *const K2[3], u64 *const K1[3], u64 *const K0[3], u32 *const V[3], u64 n, int *which,
-                          u8 *scratch, hipStream_t s, const u64 *vary_pre, bool sort_k0) {
+                          u8 *scratch, hipStream_t s, const u64 *vary_pre, bool sort_k0, const u64 *hv_host,
+                          bool k0z) {
     *which = 1;
     if (!n) return hipSuccess;
     if (n >= (1ull << 32)) return hipErrorInvalidValue;  // u32 indices and counts
@@ -309,7 +331,9 @@ hipError_t msa_radix_sort(u64 *const K2[3], u64 *const K1[3], u64 *const K0[3], 
     if ((e = hipMemsetAsync(scratch, 0, 64 + 256, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(status, 0, ntiles * 256 * 8, s)) != hipSuccess) return e;
     u64 hv[6];
-    if (vary_pre) {  // the planes' OR / AND from the entries' builder
+    if (hv_host) {  // the varying bits of each word, known to the caller
+        for (int w = 0; w < 3; ++w) hv[w] = hv_host[w];
+    } else if (vary_pre) {  // the planes' OR / AND from the entries' builder
         if ((e = hipMemcpyAsync(hv, vary_pre, sizeof hv, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
         if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
         for (int w = 0; w < 3; ++w) hv[w] &= ~hv[3 + w];
@@ -361,11 +385,225 @@ hipError_t msa_radix_sort(u64 *const K2[3], u64 *const K1[3], u64 *const K0[3], 
     // Wp: the last sorted word in order (unless it was gathered into set o's K0 buffer)
     if (wsel < 3 && Wp == K0[o]) wsel = 3;
     hipLaunchKernelGGL(k_rx_final, g1(n), dim3(256), 0, s, K2[0], K1[0], K0[0], (const u32 *)V[vloc], n, Wp, wsel,
-                       K2[o], K1[o], K0[o], V[o]);
+                       (u32)k0z, K2[o], K1[o], K0[o], V[o]);
     *which = o;
     if ((e = hipGetLastError()) != hipSuccess) return e;
     u32 herr = 0;  // a look-back that gave up (never expected: tiles take tickets in order)
     if ((e = hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
     if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
     return herr ? hipErrorLaunchFailure : hipSuccess;
+}
+
+// ---------------------------------------------------------------------------
+// Words' composite sort key.  The ranking order is (count descending, key
+// ascending); counts take few distinct values (at most ~sqrt(2 * total
+// words): ~15 K for configs[4]'s 107 M words), so each count is replaced by
+// its dense rank among the distinct counts (gid, 0 = the largest count) in
+// the top 1-2 bytes of ONE 64-bit word whose other bytes are the key's first
+// bytes: C = gid << (64 - 8 gB) | K1 >> 8 gB.  Sorting C alone (8 passes at
+// most) replaces the passes over the count's varying bytes (3 for configs[4])
+// and the gather of the second word between the two words' passes; entries
+// equal in C are ordered by the tie refinement from key byte 8 - gB on.
+#define CS_SLOTS (1u << 18)  // distinct-count set (open addressing, <= 25 % full)
+#define CS_MAXD 65536u       // distinct counts the composite key takes (2-byte gid)
+#define CS_PROBE 256u        // probes before the set counts as full
+namespace {
+__device__ __forceinline__ u32 cs_hash(u64 v) {
+    v ^= v >> 33;
+    v *= 0xff51afd7ed558ccdull;
+    v ^= v >> 29;
+    return (u32)v & (CS_SLOTS - 1);
+}
+struct CsBufs {
+    u32 *meta;  // [0] distinct counts inserted, [1] listed, [2] a probe run gave up
+    u64 *set;   // count + 1 per used slot
+    u32 *gidv;  // slot -> gid
+    u32 *list;  // used slots
+    u64 *gcnt;  // gid -> count
+};
+inline CsBufs cs_bufs(u8 *p) {
+    CsBufs b;
+    b.meta = reinterpret_cast<u32 *>(p);
+    b.set = reinterpret_cast<u64 *>(p + 64);
+    b.gidv = reinterpret_cast<u32 *>(b.set + CS_SLOTS);
+    b.list = b.gidv + CS_SLOTS;
+    b.gcnt = reinterpret_cast<u64 *>(b.list + CS_MAXD);
+    return b;
+}
+#define CS_FLY 4
+#define CS_LSLOTS 2048u  // per-workgroup set in LDS
+// v into the device set: compare-and-swap first (its returned value is the
+// slot's word at the memory side; a plain load may read a stale zero from
+// this CU's L1 for the whole kernel -- every later lane then CASes the same
+// hot slot: 4.3 ms for 50 M entries)
+__device__ __forceinline__ void cs_put(const CsBufs &b, u64 v) {
+    u32 h = cs_hash(v);
+    for (u32 p = 0; p < CS_PROBE; ++p) {
+        const u64 old = atomicCAS((unsigned long long *)&b.set[h], 0ull, (unsigned long long)v);
+        if (old == 0) {
+            atomicAdd(&b.meta[0], 1u);
+            return;
+        }
+        if (old == v) return;
+        h = (h + 1) & (CS_SLOTS - 1);
+    }
+    atomicOr(&b.meta[2], 1u);  // far too many distinct counts: the caller falls back
+}
+// Each workgroup collects its entries' distinct counts in LDS, then puts each
+// into the device set once.
+__global__ __launch_bounds__(256) void k_cset_insert(const u64 *__restrict__ K2, u64 n, CsBufs b) {
+    __shared__ u64 ls[CS_LSLOTS];
+    for (u32 k = threadIdx.x; k < CS_LSLOTS; k += 256) ls[k] = 0;
+    __syncthreads();
+    const u64 stride = (u64)gridDim.x * 256;
+    for (u64 i0 = (u64)blockIdx.x * 256 + threadIdx.x; i0 < n; i0 += CS_FLY * stride) {
+        u64 v[CS_FLY];
+#pragma unroll
+        for (u32 q = 0; q < CS_FLY; ++q) {
+            const u64 i = i0 + q * stride;
+            v[q] = i < n ? ~K2[i] + 1 : 0;  // count + 1: never 0
+        }
+#pragma unroll
+        for (u32 q = 0; q < CS_FLY; ++q) {
+            if (!v[q]) continue;
+            // a count the whole wave shares (count 1 of a high-cardinality
+            // table): one lane inserts it
+            const u64 v0 = __builtin_amdgcn_readfirstlane(v[q]);
+            if (__ballot(v[q] == v0) == __ballot(1) && mbcnt(__ballot(1)) != 0) continue;
+            u32 h = cs_hash(v[q]) & (CS_LSLOTS - 1);
+            u32 p = 0;
+            for (; p < 32; ++p) {
+                const u64 old = atomicCAS((unsigned long long *)&ls[h], 0ull, (unsigned long long)v[q]);
+                if (old == 0 || old == v[q]) break;
+                h = (h + 1) & (CS_LSLOTS - 1);
+            }
+            if (p == 32) cs_put(b, v[q]);  // the workgroup's set is crowded
+        }
+    }
+    __syncthreads();
+    for (u32 k = threadIdx.x; k < CS_LSLOTS; k += 256)
+        if (ls[k]) cs_put(b, ls[k]);
+}
+__global__ __launch_bounds__(256) void k_cset_list(CsBufs b) {
+    const u32 sl = blockIdx.x * 256 + threadIdx.x;
+    const bool used = b.set[sl] != 0;
+    const u64 m = __ballot(used);
+    if (!m) return;
+    u32 base = 0;
+    if (mbcnt(m) == 0 && used) base = atomicAdd(&b.meta[1], (u32)__popcll(m));
+    // the wave's first used lane took the wave's places
+    const u32 first = (u32)__builtin_ctzll(m);
+    base = __shfl(base, first);
+    const u32 at = base + mbcnt(m);
+    if (used && at < CS_MAXD) b.list[at] = sl;
+}
+// gid of listed count i = listed counts larger than it
+#define CR_TILE 2048
+__global__ __launch_bounds__(256) void k_cset_rank(CsBufs b) {
+    __shared__ u64 tile[CR_TILE];
+    const u32 m = min(__hip_atomic_load(&b.meta[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), CS_MAXD);
+    if (b.meta[0] > CS_MAXD || b.meta[2]) return;
+    const u32 i = blockIdx.x * 256 + threadIdx.x;
+    if (blockIdx.x * 256 >= m) return;  // whole workgroup
+    const u64 v = i < m ? b.set[b.list[i]] : 0;
+    u32 r = 0;
+    for (u32 t0 = 0; t0 < m; t0 += CR_TILE) {
+        const u32 tn = min(CR_TILE, m - t0);
+        __syncthreads();
+        for (u32 k = threadIdx.x; k < tn; k += 256) tile[k] = b.set[b.list[t0 + k]];
+        __syncthreads();
+        for (u32 k = 0; k < tn; ++k) r += tile[k] > v;
+    }
+    if (i < m) {
+        b.gidv[b.list[i]] = r;
+        b.gcnt[r] = v - 1;
+    }
+}
+__device__ __forceinline__ u32 cs_gid(const CsBufs &b, u64 v) {
+    u32 h = cs_hash(v);
+    for (u32 p = 0; p < CS_PROBE; ++p) {
+        if (b.set[h] == v) return b.gidv[h];
+        h = (h + 1) & (CS_SLOTS - 1);
+    }
+    return 0;  // never: every count was inserted
+}
+__global__ __launch_bounds__(256) void k_comp_build(const u64 *__restrict__ K2, const u64 *__restrict__ K1, u64 n,
+                                                    CsBufs b, u32 gB, u64 *__restrict__ C) {
+    const u64 stride = (u64)gridDim.x * 256;
+    for (u64 i0 = (u64)blockIdx.x * 256 + threadIdx.x; i0 < n; i0 += CS_FLY * stride) {
+        u64 v[CS_FLY], k1[CS_FLY];
+#pragma unroll
+        for (u32 q = 0; q < CS_FLY; ++q) {
+            const u64 i = i0 + q * stride;
+            v[q] = i < n ? ~K2[i] + 1 : 0;
+            k1[q] = i < n ? K1[i] : 0;
+        }
+#pragma unroll
+        for (u32 q = 0; q < CS_FLY; ++q) {
+            const u64 i = i0 + q * stride;
+            if (i >= n) break;
+            if (!gB) {
+                C[i] = k1[q];
+                continue;
+            }
+            const u32 g = cs_gid(b, v[q]);
+            C[i] = ((u64)g << (64 - 8 * gB)) | (k1[q] >> (8 * gB));
+        }
+    }
+}
+// sorted C -> ~count, in place
+__global__ void k_comp_k2(u64 *__restrict__ P, u64 n, const u64 *__restrict__ gcnt, u32 gB) {
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    P[i] = ~gcnt[gB ? (u32)(P[i] >> (64 - 8 * gB)) : 0u];
+}
+}  // namespace
+
+u64 msa_comp_scratch_bytes() { return 64 + (u64)CS_SLOTS * 12 + (u64)CS_MAXD * 12 + 64; }
+
+// The words' sort by the composite key (above).  *gB_out = gid bytes (key
+// bytes 0 .. 7 - gB are sorted), or ~0u when the table's counts take more
+// than CS_MAXD distinct values (nothing sorted: the caller sorts K2/K1).
+// vary_pre: the planes' OR / AND from k_word_entries (device, 6 words).
+// C: n words of scratch; after the sort set *which's K2 plane holds the sorted
+// composite keys (msa_comp_finish turns them into ~count).
+hipError_t msa_radix_sort_comp(u64 *const K2[3], u64 *const K1[3], u64 *const K0[3], u32 *const V[3], u64 n,
+                               int *which, u8 *scratch, hipStream_t s, const u64 *vary_pre, u64 *C, u8 *cs,
+                               u32 *gB_out) {
+    *gB_out = ~0u;
+    if (!n || n >= (1ull << 32)) return hipSuccess;
+    const CsBufs b = cs_bufs(cs);
+    hipError_t e;
+    if ((e = hipMemsetAsync(cs, 0, 64 + (u64)CS_SLOTS * 8, s)) != hipSuccess) return e;
+    const u32 g = (u32)std::min<u64>(2048, (n + 1023) / 1024);
+    hipLaunchKernelGGL(k_cset_insert, dim3(g), dim3(256), 0, s, (const u64 *)K2[0], n, b);
+    hipLaunchKernelGGL(k_cset_list, dim3(CS_SLOTS / 256), dim3(256), 0, s, b);
+    hipLaunchKernelGGL(k_cset_rank, dim3(CS_MAXD / 256), dim3(256), 0, s, b);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    u64 hv[8];
+    u32 meta[3];
+    if ((e = hipMemcpyAsync(hv, vary_pre, 6 * 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+    if ((e = hipMemcpyAsync(meta, b.meta, 12, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+    const u32 m = meta[0];
+    if (m == 0 || m > CS_MAXD || meta[1] != m || meta[2]) return hipSuccess;
+    const u32 gB = m == 1 ? 0 : (m <= 256 ? 1 : 2);
+    u64 vk1 = hv[1] & ~hv[4];  // K1's varying bits
+    u64 vc = gB ? vk1 >> (8 * gB) : vk1;
+    if (gB) {
+        u64 gm = m - 1;  // gids 0 .. m-1: the bits below m-1's top bit may vary
+        gm |= gm >> 1; gm |= gm >> 2; gm |= gm >> 4; gm |= gm >> 8; gm |= gm >> 16;
+        vc |= gm << (64 - 8 * gB);
+    }
+    hipLaunchKernelGGL(k_comp_build, dim3(g), dim3(256), 0, s, (const u64 *)K2[0], (const u64 *)K1[0], n, b, gB, C);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    u64 *const Kc[3] = {C, K2[1], K2[2]};
+    const u64 hvc[3] = {0, 0, vc};
+    if ((e = msa_radix_sort(Kc, K1, K0, V, n, which, scratch, s, nullptr, false, hvc, true)) != hipSuccess) return e;
+    *gB_out = gB;
+    return hipSuccess;
+}
+hipError_t msa_comp_finish(u64 *P, u64 n, const u8 *cs, u32 gB, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_comp_k2, g1(n), dim3(256), 0, s, P, n, (const u64 *)cs_bufs(const_cast<u8 *>(cs)).gcnt, gB);
+    return hipGetLastError();
 }

@@ -23,7 +23,7 @@ back = int(sys.argv[2]) if len(sys.argv) > 2 else 1
 ev = []
 for r in rows(os.path.join(d, "**", "*kernel_trace.csv")):
     ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r.get("Queue_Id", "?") + "/" + r.get("Stream_Id", "?"),
-               r["Kernel_Name"].split("(")[0]))
+               r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0]))
 for r in rows(os.path.join(d, "**", "*memory_copy_trace.csv")):
     n = int(r.get("Size", 0) or 0) if "Size" in r else 0
     ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), "copy/" + r.get("Stream_Id", "?"),
