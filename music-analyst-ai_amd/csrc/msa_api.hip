@@ -61,17 +61,18 @@ hipError_t msa_launch_artist_entries(const u64 *, const u32 *, u64, const u8 *, 
                                      u64 *, u32 *, u64 *, u64 *, hipStream_t);
 u64 msa_radix_scratch_bytes(u64 n);
 hipError_t msa_radix_sort(u64 *const[3], u64 *const[3], u64 *const[3], u32 *const[3], u64, int *, u8 *, hipStream_t,
-                          const u64 * = nullptr, bool = true, const u64 * = nullptr, bool = false);
+                          const u64 * = nullptr, bool = true, const u64 * = nullptr, bool = false, u64 ** = nullptr,
+                          u32 ** = nullptr);
 u64 msa_comp_scratch_bytes();
 hipError_t msa_radix_sort_comp(u64 *const[3], u64 *const[3], u64 *const[3], u32 *const[3], u64, int *, u8 *,
-                               hipStream_t, const u64 *, u64 *, u8 *, u32 *);
+                               hipStream_t, const u64 *, u64 *, u8 *, u32 *, u64 **, u32 **);
 hipError_t msa_comp_finish(u64 *, u64, const u8 *, u32, hipStream_t);
-hipError_t msa_launch_tie_mark(const u64 *, const u64 *, const u64 *, u64, u64 *, u64 *, hipStream_t);
-hipError_t msa_launch_tie_build(const u64 *, const u64 *, const u64 *, const u64 *, u64, const u32 *, const u64 *, u32,
-                                const u64 *, const u64 *,
-                                const u64 *,
-                                const u8 *, const u8 *, const u64 *, const u32 *, const u8 *, const u64 *, const u32 *,
-                                u64 *, u64 *, u64 *, u32 *, u32 *, u64 *, hipStream_t);
+u64 msa_tie_blocks(u64);
+hipError_t msa_launch_tie_count(const u64 *, const u64 *, const u64 *, u64, u64 *, u64 *, hipStream_t);
+hipError_t msa_launch_tie_build(const u64 *, const u64 *, const u64 *, u64, const u64 *, const u64 *, const u32 *,
+                                const u64 *, u32, const u64 *, const u64 *, const u64 *, const u8 *, const u8 *,
+                                const u64 *, const u32 *, const u8 *, const u64 *, const u32 *, u64 *, u64 *, u64 *,
+                                u32 *, u32 *, u64 *, hipStream_t);
 hipError_t msa_launch_tie_apply(const u32 *, const u32 *, const u64 *, u64, u32 *, u32 *, u64 *, const u64 *,
                                 const u64 *, u64 *, u64 *, hipStream_t);
 hipError_t msa_launch_sort(u64 *const[3], u64 *const[3], u64 *const[3], u32 *const[3], u64, int *, hipStream_t);
@@ -829,7 +830,7 @@ static int launch_spans(msa_ctx *c, bool want_text, hipStream_t st) {
     // artist keys for the lines shortcut of the artist pass (msa_count)
     if (!c->a_long_cap) c->a_long_cap = std::max<u64>(1ull << 20, c->n / 32);
     const u64 long_base = 32 * (nrec + 2);
-    HIPC(c, ensure(c->arena, long_base + c->a_long_cap));
+    HIPC(c, ensure(c->arena, long_base + c->a_long_cap + 64));  // + 64: 16-byte loads past a key's end
     HIPC(c, ensure(c->key_off, (nrec + 2) * 8));
     HIPC(c, ensure(c->key_len, (nrec + 2) * 4));
     HIPC(c, ensure(c->kh1, (nrec + 2) * 8));
@@ -972,10 +973,11 @@ static int split_prologue(msa_ctx *c, u64 nul_n, bool rs0) {
     u32 blocks = 0;
     for (int j = 0; j < 4; ++j) {
         u64 n = t[j].tab->p ? *t[j].used : 0;
-        // a slot cleared by itself costs about as much as zeroing 128 bytes
-        // of a whole table (configs[4]: 45 M claimed word slots took 1.4 ms
-        // of scattered clears): past that, the table is zeroed whole
-        if (n && n * 128 > t[j].slots * t[j].w * 8 && !(c->ablate & 1048576)) {
+        // a slot cleared by itself costs about as much as zeroing 256 bytes
+        // of a whole table (configs[4]: 18.5 M claimed 9..16-byte word slots
+        // took 0.9 ms of scattered clears, a 4 GiB table 0.6 ms of memset):
+        // past that, the table is zeroed whole
+        if (n && n * 256 > t[j].slots * t[j].w * 8 && !(c->ablate & 1048576)) {
             HIPC(c, hipMemsetAsync(t[j].tab->p, 0, t[j].slots * t[j].w * 8, c->stream));
             n = 0;
         }
@@ -1423,7 +1425,7 @@ static int do_count(msa_ctx *c) {
         // arena: keys rewritten by duplicate_field at their artist.csv offsets, then
         // one aligned 32-byte slot per record for keys built in registers
         const u64 short_base = (e + 64 + 255) & ~255ull;
-        HIPC(c, ensure(c->arena, short_base + 32 * cap));
+        HIPC(c, ensure(c->arena, short_base + 32 * cap + 64));
         HIPC(c, ensure(c->key_off, cap * 8));
         HIPC(c, ensure(c->key_len, cap * 4));
         HIPC(c, ensure(c->key_slot, cap * 8));
@@ -1499,8 +1501,11 @@ static int refine_ties(msa_ctx *c, Ranked &R, int cur, const u8 *wbuf, const u8 
                        bool comp = false) {
     const u64 n = R.n;
     HIPC(c, hipMemcpyAsync(R.order.p, R.V[cur].p, n * 4, hipMemcpyDeviceToDevice, st));
-    for (DevBuf *b : {&rb.t_head, &rb.t_tie, &rb.t_runid, &rb.t_tpos}) HIPC(c, ensure(*b, n * 8));
-    HIPC(c, ensure(rb.t_bsum, ((n + 1023) / 1024 + 1) * 8));
+    // per block of entries: head / tie counts (t_head / t_tie) and their scans (t_runid / t_tpos)
+    const u64 nb0 = msa_tie_blocks(n);
+    for (DevBuf *b : {&rb.t_head, &rb.t_tie, &rb.t_runid, &rb.t_tpos}) HIPC(c, ensure(*b, nb0 * 8));
+    const u64 nbb = (nb0 + 1023) / 1024 + 1;
+    HIPC(c, ensure(rb.t_bsum, 2 * nbb * 8));
     HIPC(c, ensure(rb.t_total, 64));
     const u64 *K2 = R.K[cur][0].as<u64>(), *K1 = comp ? K2 : R.K[cur][1].as<u64>();
     const u64 *K0 = covered == 16 ? R.K[cur][2].as<u64>() : nullptr;
@@ -1508,13 +1513,13 @@ static int refine_ties(msa_ctx *c, Ranked &R, int cur, const u8 *wbuf, const u8 
     const u64 *Pc = nullptr;
     u64 mc = n;
     for (u32 r = 1; r < 4096; ++r) {
-        HIPC(c, msa_launch_tie_mark(K2, K1, K0, mc, rb.t_head.as<u64>(), rb.t_tie.as<u64>(), st));
-        HIPC(c, msa_exclusive_scan(rb.t_head.as<u64>(), mc, rb.t_runid.as<u64>(), rb.t_bsum.as<u64>(),
-                                   rb.t_total.as<u64>(), st));
-        HIPC(c, msa_exclusive_scan(rb.t_tie.as<u64>(), mc, rb.t_tpos.as<u64>(), rb.t_bsum.as<u64>(),
-                                   rb.t_total.as<u64>(), st));
+        const u64 nb = msa_tie_blocks(mc);
+        HIPC(c, msa_launch_tie_count(K2, K1, K0, mc, rb.t_head.as<u64>(), rb.t_tie.as<u64>(), st));
+        HIPC(c, msa_exclusive_scan2(rb.t_head.as<u64>(), nb, rb.t_runid.as<u64>(), rb.t_bsum.as<u64>(),
+                                    rb.t_total.as<u64>(), rb.t_tie.as<u64>(), nb, rb.t_tpos.as<u64>(),
+                                    rb.t_bsum.as<u64>() + nbb, rb.t_total.as<u64>() + 1, st));
         u64 m = 0;
-        HIPC(c, hipMemcpyAsync(&m, rb.t_total.p, 8, hipMemcpyDeviceToHost, st));
+        HIPC(c, hipMemcpyAsync(&m, rb.t_total.as<u64>() + 1, 8, hipMemcpyDeviceToHost, st));
         HIPC(c, hipStreamSynchronize(st));
         if (c->ablate & 4096) fprintf(stderr, "refine_ties: n %llu round %u ties %llu\n", (unsigned long long)n, r,
                                       (unsigned long long)m);
@@ -1535,9 +1540,8 @@ static int refine_ties(msa_ctx *c, Ranked &R, int cur, const u8 *wbuf, const u8 
             k0[s] = rb.t_K[s][2].as<u64>();
             vv[s] = rb.t_V[s].as<u32>();
         }
-        HIPC(c, msa_launch_tie_build(rb.t_runid.as<u64>(), rb.t_head.as<u64>(), rb.t_tie.as<u64>(), rb.t_tpos.as<u64>(),
-                                     mc, Vc, Pc, covered + 16 * (r - 1), R.K[0][1].as<u64>(), R.K[0][2].as<u64>(),
-                                     R.ref.as<u64>(), wbuf, wextra, c->l_pos.as<u64>(), c->l_len.as<u32>(), arena,
+        HIPC(c, msa_launch_tie_build(K2, K1, K0, mc, rb.t_runid.as<u64>(), rb.t_tpos.as<u64>(), Vc, Pc,
+                                     covered + 16 * (r - 1), R.K[0][1].as<u64>(), R.K[0][2].as<u64>(), R.ref.as<u64>(), wbuf, wextra, c->l_pos.as<u64>(), c->l_len.as<u32>(), arena,
                                      key_off, key_len, k2[0], k1[0], k0[0], vv[0], rb.t_Vn.as<u32>(),
                                      rb.t_Pn.as<u64>(), st));
         int o = 1;
@@ -1616,8 +1620,24 @@ static int sort_and_blob(msa_ctx *c, Ranked &R, const u8 *wbuf, const u8 *wextra
         if (!sk0 && c->comp_sort && R.vary_ok) {
             HIPC(c, ensure(R.comp, n * 8));
             HIPC(c, ensure(R.cset, msa_comp_scratch_bytes()));
+            u64 *wsk = nullptr;
+            u32 *vk = nullptr;
             HIPC(c, msa_radix_sort_comp(k2, k1, k0, vv, n, &cur, rb.sort_scratch.as<u8>(), st, R.vary.as<u64>(),
-                                        R.comp.as<u64>(), R.cset.as<u8>(), &gB));
+                                        R.comp.as<u64>(), R.cset.as<u8>(), &gB, &wsk, &vk));
+            if (vk) {  // the sorted values stayed in the last pass's buffer (set 1 or 2): set cur's V
+                if (R.V[1].p == vk) std::swap(R.V[cur], R.V[1]);
+                else if (R.V[2].p == vk) std::swap(R.V[cur], R.V[2]);
+                else return fail(c, MSA_ERR_HIP, "radix sort: sorted values in an unknown buffer");
+            }
+            if (wsk) {  // the sorted keys stayed in a pass buffer (a K0 plane of sets 1/2): it becomes set cur's K2
+                bool swapped = false;
+                for (int s2 = 1; s2 < 3 && !swapped; ++s2)
+                    if (R.K[s2][2].p == wsk) {
+                        std::swap(R.K[cur][0], R.K[s2][2]);
+                        swapped = true;
+                    }
+                if (!swapped) return fail(c, MSA_ERR_HIP, "radix sort: sorted keys in an unknown buffer");
+            }
         }
         int rc;
         if (gB != ~0u) {

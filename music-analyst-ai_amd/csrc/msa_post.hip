@@ -1674,6 +1674,12 @@ __global__ void k_long_insert(const u8 *__restrict__ buf, u64 seg_end, const u8 
     l_slot[i] = h_insert(ltab, lmask, h, 1, i, llist, llist_cap, &ctr->l_claimed, ctr, OVF_LT);
 }
 
+__device__ __forceinline__ u64 lower8x(u64 x) {  // 'A'..'Z' -> 'a'..'z' in each byte (bytes >= 0x80 kept)
+    const u64 h = 0x8080808080808080ull, o = 0x0101010101010101ull;
+    const u64 t = x & ~h;
+    const u64 ge = (t + (0x80 - 0x41) * o) & h, gt = (t + (0x80 - 0x5B) * o) & h;
+    return x | ((ge & ~gt & ~x) >> 2);
+}
 __device__ __forceinline__ u32 lower1(u32 c) { return (c >= 'A' && c <= 'Z') ? c + 32 : c; }
 
 __global__ void k_long_verify(const u8 *__restrict__ buf, const u8 *__restrict__ extra, const u64 *__restrict__ l_pos,
@@ -1685,8 +1691,18 @@ __global__ void k_long_verify(const u8 *__restrict__ buf, const u8 *__restrict__
     if (rep == i) return;
     const u32 len = l_len[i];
     bool same = l_len[rep] == len;
-    const u8 *a = tok_at(buf, extra, l_pos[i]), *b = tok_at(buf, extra, l_pos[rep]);
-    for (u32 k = 0; same && k < len; ++k) same = lower1(a[k]) == lower1(b[k]);
+    // 16 bytes of each at a time (dword-aligned bases, padded inputs), lower-cased in registers
+    const u64 pa = l_pos[i], pb = l_pos[rep];
+    const u8 *ba = (pa & MSA_POS_EXTRA) ? extra : buf, *bb = (pb & MSA_POS_EXTRA) ? extra : buf;
+    const u64 oa = pa & ~MSA_POS_EXTRA, ob = pb & ~MSA_POS_EXTRA;
+    for (u32 k = 0; same && k < len; k += 16) {
+        const uint4 x = load16u(ba, oa + k), y = load16u(bb, ob + k);
+        u64 x0 = ((u64)x.y << 32) | x.x, x1 = ((u64)x.w << 32) | x.z;
+        u64 y0 = ((u64)y.y << 32) | y.x, y1 = ((u64)y.w << 32) | y.z;
+        const u32 r = len - k;  // bytes of this piece that belong to the words
+        const u64 m0 = r >= 8 ? ~0ull : bits_below(8 * r), m1 = r >= 16 ? ~0ull : (r > 8 ? bits_below(8 * (r - 8)) : 0ull);
+        same = ((lower8x(x0) ^ lower8x(y0)) & m0) == 0 && ((lower8x(x1) ^ lower8x(y1)) & m1) == 0;
+    }
     if (!same) atomicAdd((unsigned long long *)&ctr->collision, 1ull);
 }
 
@@ -1707,6 +1723,28 @@ __device__ __forceinline__ void be16(const u8 *p, u64 n, int lower, u64 *hi, u64
     }
     *hi = h;
     *lo = l;
+}
+
+// be16 from one unaligned 16-byte load (base dword-aligned, padded past the
+// key): a byte load per key byte left each long word's lane waiting on 16
+// loads in turn
+__device__ __forceinline__ void be16w(const u8 *base, u64 off, u64 n, int lower, u64 *hi, u64 *lo) {
+    const uint4 v = load16u(base, off);
+    u64 a = ((u64)v.y << 32) | v.x, b = ((u64)v.w << 32) | v.z;  // bytes 0..7, 8..15 (little-endian)
+    if (n < 16) {
+        if (n <= 8) {
+            a &= bits_below(8 * (u32)n);
+            b = 0;
+        } else {
+            b &= bits_below(8 * (u32)(n - 8));
+        }
+    }
+    if (lower) {
+        a = lower8x(a);
+        b = lower8x(b);
+    }
+    *hi = __builtin_bswap64(a);
+    *lo = __builtin_bswap64(b);
 }
 
 // Dense list of the claimed slots of an S or M word table.  The main scan
@@ -1770,7 +1808,8 @@ __global__ __launch_bounds__(256) void k_word_entries(EntryArgs a) {
             const u64 slot = a.l_list[i - a.ns - a.nm];
             c = a.l_tab[4 * slot + 1];
             const u64 rep = a.l_tab[4 * slot + 2];
-            be16(tok_at(a.buf, a.extra, a.l_pos[rep]), a.l_len[rep], 1, &hi, &lo);
+            const u64 lp = a.l_pos[rep];
+            be16w((lp & MSA_POS_EXTRA) ? a.extra : a.buf, lp & ~MSA_POS_EXTRA, a.l_len[rep], 1, &hi, &lo);
             ref = ((u64)KIND_L << 60) | rep;
         }
         a.K2[i] = ~c;
@@ -1814,7 +1853,7 @@ __global__ void k_artist_entries(const u64 *__restrict__ atab, const u32 *__rest
     const u64 c = atab[4 * slot + 1];
     const u64 rep = atab[4 * slot + 2];
     u64 hi, lo;
-    be16(arena + key_off[rep], key_len[rep], 0, &hi, &lo);
+    be16w(arena, key_off[rep], key_len[rep], 0, &hi, &lo);
     K2[i] = ~c;
     K1[i] = hi;
     K0[i] = lo;
@@ -1974,16 +2013,60 @@ __global__ void k_tie_fixup(const u64 *__restrict__ K2, const u64 *__restrict__ 
 // round, until no two adjacent keys are equal.  A run of thousands of artists
 // sharing 16 bytes and a count (configs[4]) costs one small radix sort, not
 // run^2 string compares.
-__global__ void k_tie_mark(const u64 *__restrict__ K2, const u64 *__restrict__ K1, const u64 *__restrict__ K0, u64 n,
-                           u64 *__restrict__ head, u64 *__restrict__ tie) {
-    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    // K0 null: the sort covered K2 and K1 only (K0's bytes are the first refinement round's)
+// Tie runs by stream compaction: a block of TB_N consecutive entries counts
+// its run heads and tied entries (k_tie_count), the block counts are scanned,
+// and k_tie_build recomputes the flags, ranks them within the block (wave
+// ballots) and writes only the tied entries.  (Per-entry head / tie / run-id /
+// position arrays and their two full scans had cost ~1.3 ms for configs[4]'s
+// 50 M words, to find a few hundred thousand tied entries.)
+#define TB_T 256
+#define TB_PER 4
+#define TB_N (TB_T * TB_PER)
+struct TieFlags {
+    bool head, tie;
+};
+// K0 null: the sort covered K2 and K1 only (K0's bytes are the first refinement round's)
+__device__ __forceinline__ TieFlags tie_flags(const u64 *__restrict__ K2, const u64 *__restrict__ K1,
+                                              const u64 *__restrict__ K0, u64 n, u64 i) {
     const u64 a2 = K2[i], a1 = K1[i], a0 = K0 ? K0[i] : 0;
     const bool eq_prev = i > 0 && K2[i - 1] == a2 && K1[i - 1] == a1 && (!K0 || K0[i - 1] == a0);
     const bool eq_next = i + 1 < n && K2[i + 1] == a2 && K1[i + 1] == a1 && (!K0 || K0[i + 1] == a0);
-    head[i] = eq_prev ? 0 : 1;
-    tie[i] = (eq_prev || eq_next) ? 1 : 0;
+    return TieFlags{!eq_prev, eq_prev || eq_next};
+}
+// entry (row k, thread t) of block b is entry b * TB_N + k * TB_T + t
+__global__ __launch_bounds__(TB_T) void k_tie_count(const u64 *__restrict__ K2, const u64 *__restrict__ K1,
+                                                    const u64 *__restrict__ K0, u64 n, u64 *__restrict__ bh,
+                                                    u64 *__restrict__ bt) {
+    __shared__ u32 ws[2][TB_T / 64];
+    const u32 t = threadIdx.x;
+    u32 h = 0, q = 0;
+#pragma unroll
+    for (u32 k = 0; k < TB_PER; ++k) {
+        const u64 i = (u64)blockIdx.x * TB_N + k * TB_T + t;
+        if (i < n) {
+            const TieFlags f = tie_flags(K2, K1, K0, n, i);
+            h += f.head;
+            q += f.tie;
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        h += __shfl_xor(h, o);
+        q += __shfl_xor(q, o);
+    }
+    if (lane_id() == 0) {
+        ws[0][t >> 6] = h;
+        ws[1][t >> 6] = q;
+    }
+    __syncthreads();
+    if (t == 0) {
+        u32 H = 0, Q = 0;
+        for (u32 w = 0; w < TB_T / 64; ++w) {
+            H += ws[0][w];
+            Q += ws[1][w];
+        }
+        bh[blockIdx.x] = H;
+        bt[blockIdx.x] = Q;
+    }
 }
 
 // key bytes [skip, skip + 16) of an entry as two big-endian words (zero past its end)
@@ -2002,45 +2085,84 @@ __device__ __forceinline__ void key16_round(u64 refv, u32 skip, const u8 *buf, c
     be16(p + skip, n - skip, lower, hi, lo);
 }
 
-// runid = exclusive scan of head (+ head: run index of each entry), tpos = exclusive
-// scan of tie; entry i of the current level (value Vc[i], order position
-// Pc ? Pc[i] : i) goes to slot tpos[i] of the next level's subset
-__global__ void k_tie_build(const u64 *__restrict__ runid, const u64 *__restrict__ head, const u64 *__restrict__ tie,
-                            const u64 *__restrict__ tpos,
-                            u64 mc, const u32 *__restrict__ Vc, const u64 *__restrict__ Pc, u32 skip,
-                            const u64 *__restrict__ K1u, const u64 *__restrict__ K0u,
-                            const u64 *__restrict__ ref, const u8 *buf, const u8 *extra, const u64 *l_pos,
-                            const u32 *l_len, const u8 *arena, const u64 *key_off, const u32 *key_len,
-                            u64 *__restrict__ K2n, u64 *__restrict__ K1n, u64 *__restrict__ K0n,
-                            u32 *__restrict__ Vid, u32 *__restrict__ Vn, u64 *__restrict__ Pn) {
-    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= mc || !tie[i]) return;
-    const u64 j = tpos[i];
-    const u32 e = Vc[i];
-    u64 hi, lo;
-    if (skip <= 8) {  // after a sort of fewer than 16 key bytes: bytes skip .. 15 are in K1/K0 (S/M keys have
-                      // no byte source), bytes 16 .. from the key's bytes
-        u64 h2, l2;
-        key16_round(ref[e], 16, buf, extra, l_pos, l_len, arena, key_off, key_len, &h2, &l2);
-        const u64 k0 = K0u[e];
-        if (skip == 8) {
-            hi = k0;
-            lo = h2;
-        } else {  // the composite key's sort (skip 6 or 7: msa_radix_sort_comp)
-            const u32 sb = 8 * skip;
-            const u64 k1 = K1u[e];
-            hi = (k1 << sb) | (k0 >> (64 - sb));
-            lo = (k0 << sb) | (h2 >> (64 - sb));
+// hoff / toff: exclusive scans of the blocks' head / tie counts.  Tied entry
+// i of the current level (value Vc[i], order position Pc ? Pc[i] : i) goes to
+// slot j of the next level's subset, keyed by (its run's inclusive head count,
+// key bytes [skip, skip + 16)).
+__global__ __launch_bounds__(TB_T) void k_tie_build(const u64 *__restrict__ K2, const u64 *__restrict__ K1,
+                                                    const u64 *__restrict__ K0, u64 mc, const u64 *__restrict__ hoff,
+                                                    const u64 *__restrict__ toff, const u32 *__restrict__ Vc,
+                                                    const u64 *__restrict__ Pc, u32 skip,
+                                                    const u64 *__restrict__ K1u, const u64 *__restrict__ K0u,
+                                                    const u64 *__restrict__ ref, const u8 *buf, const u8 *extra,
+                                                    const u64 *l_pos, const u32 *l_len, const u8 *arena,
+                                                    const u64 *key_off, const u32 *key_len, u64 *__restrict__ K2n,
+                                                    u64 *__restrict__ K1n, u64 *__restrict__ K0n, u32 *__restrict__ Vid,
+                                                    u32 *__restrict__ Vn, u64 *__restrict__ Pn) {
+    __shared__ u32 ws[2][TB_PER][TB_T / 64];
+    const u32 t = threadIdx.x, lane = lane_id(), w = t >> 6;
+    TieFlags f[TB_PER];
+    u32 hp[TB_PER], tp[TB_PER];
+#pragma unroll
+    for (u32 k = 0; k < TB_PER; ++k) {
+        const u64 i = (u64)blockIdx.x * TB_N + k * TB_T + t;
+        f[k] = i < mc ? tie_flags(K2, K1, K0, mc, i) : TieFlags{false, false};
+        const u64 H = __ballot(f[k].head), Q = __ballot(f[k].tie);
+        hp[k] = mbcnt(H);
+        tp[k] = mbcnt(Q);
+        if (lane == 0) {
+            ws[0][k][w] = (u32)__popcll(H);
+            ws[1][k][w] = (u32)__popcll(Q);
         }
-    } else {
-        key16_round(ref[e], skip, buf, extra, l_pos, l_len, arena, key_off, key_len, &hi, &lo);
     }
-    K2n[j] = runid[i] + head[i];  // inclusive count of run heads: the same for every entry of a run
-    K1n[j] = hi;
-    K0n[j] = lo;
-    Vid[j] = (u32)j;
-    Vn[j] = e;
-    Pn[j] = Pc ? Pc[i] : i;
+    __syncthreads();
+    bool any = false;
+#pragma unroll
+    for (u32 k = 0; k < TB_PER; ++k) any |= f[k].tie;
+    if (!any) return;
+    // exclusive offsets of (row k, wave w) within the block: earlier rows, then earlier waves of row k
+    u32 hb = 0, tb = 0;
+#pragma unroll
+    for (u32 k = 0; k < TB_PER; ++k) {
+        u32 hw = hb, tw = tb;
+        for (u32 v = 0; v < w; ++v) {
+            hw += ws[0][k][v];
+            tw += ws[1][k][v];
+        }
+        if (f[k].tie) {
+            const u64 i = (u64)blockIdx.x * TB_N + k * TB_T + t;
+            const u64 j = toff[blockIdx.x] + tw + tp[k];
+            const u32 e = Vc[i];
+            u64 hi, lo;
+            if (skip <= 8) {  // after a sort of fewer than 16 key bytes: bytes skip .. 15 are in K1/K0 (S/M keys
+                              // have no byte source), bytes 16 .. from the key's bytes
+                u64 h2, l2;
+                key16_round(ref[e], 16, buf, extra, l_pos, l_len, arena, key_off, key_len, &h2, &l2);
+                const u64 k0 = K0u[e];
+                if (skip == 8) {
+                    hi = k0;
+                    lo = h2;
+                } else {  // the composite key's sort (skip 6 or 7: msa_radix_sort_comp)
+                    const u32 sb = 8 * skip;
+                    const u64 k1 = K1u[e];
+                    hi = (k1 << sb) | (k0 >> (64 - sb));
+                    lo = (k0 << sb) | (h2 >> (64 - sb));
+                }
+            } else {
+                key16_round(ref[e], skip, buf, extra, l_pos, l_len, arena, key_off, key_len, &hi, &lo);
+            }
+            K2n[j] = hoff[blockIdx.x] + hw + hp[k] + (f[k].head ? 1 : 0);  // the same for every entry of a run
+            K1n[j] = hi;
+            K0n[j] = lo;
+            Vid[j] = (u32)j;
+            Vn[j] = e;
+            Pn[j] = Pc ? Pc[i] : i;
+        }
+        for (u32 v = 0; v < TB_T / 64; ++v) {
+            hb += ws[0][k][v];
+            tb += ws[1][k][v];
+        }
+    }
 }
 
 // the subset sorted (perm): its entries take the same order positions, in order
@@ -2112,12 +2234,27 @@ __device__ __forceinline__ void blob_key_bytes(u64 i, u32 e, const u64 *__restri
     const u64 r = ref[e];
     const u32 kind = (u32)(r >> 60);
     const u64 idx = r & ((1ull << 60) - 1);
-    if (kind == KIND_L) {
-        const u8 *p = tok_at(buf, extra, l_pos[idx]);
-        for (u32 k = 0; k < l_len[idx]; ++k) dst[k] = (u8)lower1(p[k]);
-    } else if (kind == KIND_A) {
-        const u8 *p = arena + key_off[idx];
-        for (u32 k = 0; k < key_len[idx]; ++k) dst[k] = p[k];
+    if (kind == KIND_L || kind == KIND_A) {
+        // 16-byte unaligned loads, two in flight (a byte load per key byte
+        // left each long word's lane waiting on ~20 loads in turn); the input,
+        // the side buffer and the key arena are padded past their last key
+        const bool low = kind == KIND_L;
+        const u64 lp = low ? l_pos[idx] : 0;
+        // an aligned base and a byte offset (load16u's dword loads stay aligned)
+        const u8 *base = low ? ((lp & MSA_POS_EXTRA) ? extra : buf) : arena;
+        const u64 o = low ? (lp & ~MSA_POS_EXTRA) : key_off[idx];
+        const u32 L = low ? l_len[idx] : key_len[idx];
+        for (u32 k = 0; k < L; k += 32) {
+            const uint4 a = load16u(base, o + k), b = load16u(base, o + k + 16);
+            const u32 w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+            const u32 m = min(32u, L - k);
+#pragma unroll
+            for (u32 q = 0; q < 32; ++q) {
+                if (q >= m) break;
+                const u32 ch = (w[q >> 2] >> (8 * (q & 3))) & 0xFFu;
+                dst[k + q] = (u8)(low ? lower1(ch) : ch);
+            }
+        }
     } else {
         const u64 k1 = K1u[e], k0 = K0u[e];
         for (int k = 0; k < 16; ++k) {
@@ -2721,20 +2858,20 @@ hipError_t msa_launch_blob(const u32 *order, u64 n, const u64 *ref, const u64 *K
     return hipGetLastError();
 }
 
-hipError_t msa_launch_tie_mark(const u64 *K2, const u64 *K1, const u64 *K0, u64 n, u64 *head, u64 *tie, hipStream_t s) {
-    if (n) hipLaunchKernelGGL(k_tie_mark, grid1(n), dim3(256), 0, s, K2, K1, K0, n, head, tie);
+u64 msa_tie_blocks(u64 n) { return (n + TB_N - 1) / TB_N; }
+hipError_t msa_launch_tie_count(const u64 *K2, const u64 *K1, const u64 *K0, u64 n, u64 *bh, u64 *bt, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_tie_count, dim3((u32)msa_tie_blocks(n)), dim3(TB_T), 0, s, K2, K1, K0, n, bh, bt);
     return hipGetLastError();
 }
-hipError_t msa_launch_tie_build(const u64 *runid, const u64 *head, const u64 *tie, const u64 *tpos, u64 mc, const u32 *Vc,
-                                const u64 *Pc,
-                                u32 skip, const u64 *K1u, const u64 *K0u, const u64 *ref, const u8 *buf, const u8 *extra,
-                                const u64 *l_pos, const u32 *l_len, const u8 *arena, const u64 *key_off,
-                                const u32 *key_len, u64 *K2n, u64 *K1n, u64 *K0n, u32 *Vid, u32 *Vn, u64 *Pn,
-                                hipStream_t s) {
+hipError_t msa_launch_tie_build(const u64 *K2, const u64 *K1, const u64 *K0, u64 mc, const u64 *hoff, const u64 *toff,
+                                const u32 *Vc, const u64 *Pc, u32 skip, const u64 *K1u, const u64 *K0u, const u64 *ref,
+                                const u8 *buf, const u8 *extra, const u64 *l_pos, const u32 *l_len, const u8 *arena,
+                                const u64 *key_off, const u32 *key_len, u64 *K2n, u64 *K1n, u64 *K0n, u32 *Vid,
+                                u32 *Vn, u64 *Pn, hipStream_t s) {
     if (mc)
-        hipLaunchKernelGGL(k_tie_build, grid1(mc), dim3(256), 0, s, runid, head, tie, tpos, mc, Vc, Pc, skip, K1u, K0u, ref,
-                           buf, extra,
-                           l_pos, l_len, arena, key_off, key_len, K2n, K1n, K0n, Vid, Vn, Pn);
+        hipLaunchKernelGGL(k_tie_build, dim3((u32)msa_tie_blocks(mc)), dim3(TB_T), 0, s, K2, K1, K0, mc, hoff, toff, Vc,
+                           Pc, skip, K1u, K0u, ref, buf, extra, l_pos, l_len, arena, key_off, key_len, K2n, K1n, K0n,
+                           Vid, Vn, Pn);
     return hipGetLastError();
 }
 hipError_t msa_launch_tie_apply(const u32 *perm, const u32 *Vn, const u64 *Pn, u64 m, u32 *order, u32 *Vc, u64 *Pc,

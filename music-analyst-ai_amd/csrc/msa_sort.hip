@@ -293,11 +293,11 @@ __global__ void k_rx_final(const u64 *__restrict__ K2, const u64 *__restrict__ K
     const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const u32 v = V[i];
-    O2[i] = wsel == 2 ? Ws[i] : K2[v];
+    if (O2) O2[i] = wsel == 2 ? Ws[i] : K2[v];  // null: the caller keeps Ws as the sorted K2 plane
     const u64 k1 = wsel == 1 ? Ws[i] : K1[v];
     O1[i] = k1;
     O0[i] = wsel == 0 ? Ws[i] : ((k0z && !(k1 & 0xFFu)) ? 0ull : K0[v]);
-    OV[i] = v;
+    if (OV) OV[i] = v;  // null: the caller keeps V as the sorted values
 }
 
 inline dim3 g1(u64 n, u32 t = 256) { return dim3((u32)((n + t - 1) / t)); }
@@ -316,7 +316,9 @@ u64 msa_radix_scratch_bytes(u64 n) {
 // msa_launch_sort.  `scratch` holds msa_radix_scratch_bytes(n) bytes.
 hipError_t msa_radix_sort(u64 *const K2[3], u64 *const K1[3], u64 *const K0[3], u32 *const V[3], u64 n, int *which,
                           u8 *scratch, hipStream_t s, const u64 *vary_pre, bool sort_k0, const u64 *hv_host,
-                          bool k0z) {
+                          bool k0z, u64 **ws_keep, u32 **v_keep) {
+    if (ws_keep) *ws_keep = nullptr;
+    if (v_keep) *v_keep = nullptr;
     *which = 1;
     if (!n) return hipSuccess;
     if (n >= (1ull << 32)) return hipErrorInvalidValue;  // u32 indices and counts
@@ -384,8 +386,15 @@ hipError_t msa_radix_sort(u64 *const K2[3], u64 *const K1[3], u64 *const K0[3], 
     const int o = vloc == 1 ? 2 : 1;
     // Wp: the last sorted word in order (unless it was gathered into set o's K0 buffer)
     if (wsel < 3 && Wp == K0[o]) wsel = 3;
+    // ws_keep: the sorted K2 words stay where the last pass left them (the
+    // caller takes that buffer as set o's K2 plane) instead of being copied
+    // (v_keep: likewise the sorted values, when a pass wrote them)
+    const bool keep = ws_keep && wsel == 2;
+    if (keep) *ws_keep = const_cast<u64 *>(Wp);
+    const bool vk = v_keep && vloc != 0;
+    if (vk) *v_keep = V[vloc];
     hipLaunchKernelGGL(k_rx_final, g1(n), dim3(256), 0, s, K2[0], K1[0], K0[0], (const u32 *)V[vloc], n, Wp, wsel,
-                       (u32)k0z, K2[o], K1[o], K0[o], V[o]);
+                       (u32)k0z, keep ? nullptr : K2[o], K1[o], K0[o], vk ? nullptr : V[o]);
     *which = o;
     if ((e = hipGetLastError()) != hipSuccess) return e;
     u32 herr = 0;  // a look-back that gave up (never expected: tiles take tickets in order)
@@ -417,6 +426,7 @@ __device__ __forceinline__ u32 cs_hash(u64 v) {
 struct CsBufs {
     u32 *meta;  // [0] distinct counts inserted, [1] listed, [2] a probe run gave up
     u64 *set;   // count + 1 per used slot
+    u32 *rk;    // listed count -> gid (summed over k_cset_rank's tiles)
     u32 *gidv;  // slot -> gid
     u32 *list;  // used slots
     u64 *gcnt;  // gid -> count
@@ -425,7 +435,8 @@ inline CsBufs cs_bufs(u8 *p) {
     CsBufs b;
     b.meta = reinterpret_cast<u32 *>(p);
     b.set = reinterpret_cast<u64 *>(p + 64);
-    b.gidv = reinterpret_cast<u32 *>(b.set + CS_SLOTS);
+    b.rk = reinterpret_cast<u32 *>(b.set + CS_SLOTS);
+    b.gidv = b.rk + CS_MAXD;
     b.list = b.gidv + CS_SLOTS;
     b.gcnt = reinterpret_cast<u64 *>(b.list + CS_MAXD);
     return b;
@@ -484,40 +495,55 @@ __global__ __launch_bounds__(256) void k_cset_insert(const u64 *__restrict__ K2,
     for (u32 k = threadIdx.x; k < CS_LSLOTS; k += 256)
         if (ls[k]) cs_put(b, ls[k]);
 }
-__global__ __launch_bounds__(256) void k_cset_list(CsBufs b) {
-    const u32 sl = blockIdx.x * 256 + threadIdx.x;
+// the used slots, listed (one claim per workgroup: a claim per wave on the
+// one counter serialised, 150 us)
+__global__ __launch_bounds__(1024) void k_cset_list(CsBufs b) {
+    __shared__ u32 wc[16], wb[16], gb;
+    const u32 t = threadIdx.x, w = t >> 6, sl = blockIdx.x * 1024 + t;
     const bool used = b.set[sl] != 0;
-    const u64 m = __ballot(used);
-    if (!m) return;
-    u32 base = 0;
-    if (mbcnt(m) == 0 && used) base = atomicAdd(&b.meta[1], (u32)__popcll(m));
-    // the wave's first used lane took the wave's places
-    const u32 first = (u32)__builtin_ctzll(m);
-    base = __shfl(base, first);
-    const u32 at = base + mbcnt(m);
+    const u64 M = __ballot(used);
+    if (lane_id() == 0) wc[w] = (u32)__popcll(M);
+    __syncthreads();
+    if (t == 0) {
+        u32 tot = 0;
+        for (u32 k = 0; k < 16; ++k) {
+            wb[k] = tot;
+            tot += wc[k];
+        }
+        gb = tot ? atomicAdd(&b.meta[1], tot) : 0u;
+    }
+    __syncthreads();
+    const u32 at = gb + wb[w] + mbcnt(M);
     if (used && at < CS_MAXD) b.list[at] = sl;
 }
-// gid of listed count i = listed counts larger than it
+// gid of listed count i = listed counts larger than it: workgroup (x, y)
+// counts, for its 256 listed counts, the larger ones among listed counts
+// [y CR_TILE, (y + 1) CR_TILE) (a grid over both, not one thread looping over
+// all of them: 330 us for ~25 K distinct counts); k_cset_fin stores the gids
 #define CR_TILE 2048
 __global__ __launch_bounds__(256) void k_cset_rank(CsBufs b) {
     __shared__ u64 tile[CR_TILE];
-    const u32 m = min(__hip_atomic_load(&b.meta[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), CS_MAXD);
+    const u32 m = min(b.meta[1], CS_MAXD);
+    if (b.meta[0] > CS_MAXD || b.meta[2]) return;
+    const u32 j0 = blockIdx.y * CR_TILE;
+    if (blockIdx.x * 256 >= m || j0 >= m) return;  // whole workgroup
+    const u32 i = blockIdx.x * 256 + threadIdx.x;
+    const u32 tn = min(CR_TILE, m - j0);
+    for (u32 k = threadIdx.x; k < tn; k += 256) tile[k] = b.set[b.list[j0 + k]];
+    const u64 v = i < m ? b.set[b.list[i]] : ~0ull;
+    __syncthreads();
+    u32 r = 0;
+    for (u32 k = 0; k < tn; ++k) r += tile[k] > v;
+    if (i < m && r) atomicAdd(&b.rk[i], r);
+}
+__global__ __launch_bounds__(256) void k_cset_fin(CsBufs b) {
+    const u32 m = min(b.meta[1], CS_MAXD);
     if (b.meta[0] > CS_MAXD || b.meta[2]) return;
     const u32 i = blockIdx.x * 256 + threadIdx.x;
-    if (blockIdx.x * 256 >= m) return;  // whole workgroup
-    const u64 v = i < m ? b.set[b.list[i]] : 0;
-    u32 r = 0;
-    for (u32 t0 = 0; t0 < m; t0 += CR_TILE) {
-        const u32 tn = min(CR_TILE, m - t0);
-        __syncthreads();
-        for (u32 k = threadIdx.x; k < tn; k += 256) tile[k] = b.set[b.list[t0 + k]];
-        __syncthreads();
-        for (u32 k = 0; k < tn; ++k) r += tile[k] > v;
-    }
-    if (i < m) {
-        b.gidv[b.list[i]] = r;
-        b.gcnt[r] = v - 1;
-    }
+    if (i >= m) return;
+    const u32 sl = b.list[i], r = b.rk[i];
+    b.gidv[sl] = r;
+    b.gcnt[r] = b.set[sl] - 1;
 }
 __device__ __forceinline__ u32 cs_gid(const CsBufs &b, u64 v) {
     u32 h = cs_hash(v);
@@ -559,7 +585,7 @@ __global__ void k_comp_k2(u64 *__restrict__ P, u64 n, const u64 *__restrict__ gc
 }
 }  // namespace
 
-u64 msa_comp_scratch_bytes() { return 64 + (u64)CS_SLOTS * 12 + (u64)CS_MAXD * 12 + 64; }
+u64 msa_comp_scratch_bytes() { return 64 + (u64)CS_SLOTS * 12 + (u64)CS_MAXD * 16 + 64; }
 
 // The words' sort by the composite key (above).  *gB_out = gid bytes (key
 // bytes 0 .. 7 - gB are sorted), or ~0u when the table's counts take more
@@ -569,16 +595,19 @@ u64 msa_comp_scratch_bytes() { return 64 + (u64)CS_SLOTS * 12 + (u64)CS_MAXD * 1
 // composite keys (msa_comp_finish turns them into ~count).
 hipError_t msa_radix_sort_comp(u64 *const K2[3], u64 *const K1[3], u64 *const K0[3], u32 *const V[3], u64 n,
                                int *which, u8 *scratch, hipStream_t s, const u64 *vary_pre, u64 *C, u8 *cs,
-                               u32 *gB_out) {
+                               u32 *gB_out, u64 **ws_keep, u32 **v_keep) {
     *gB_out = ~0u;
+    *ws_keep = nullptr;
+    *v_keep = nullptr;
     if (!n || n >= (1ull << 32)) return hipSuccess;
     const CsBufs b = cs_bufs(cs);
     hipError_t e;
-    if ((e = hipMemsetAsync(cs, 0, 64 + (u64)CS_SLOTS * 8, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(cs, 0, 64 + (u64)CS_SLOTS * 8 + (u64)CS_MAXD * 4, s)) != hipSuccess) return e;  // meta, set, rk
     const u32 g = (u32)std::min<u64>(2048, (n + 1023) / 1024);
     hipLaunchKernelGGL(k_cset_insert, dim3(g), dim3(256), 0, s, (const u64 *)K2[0], n, b);
-    hipLaunchKernelGGL(k_cset_list, dim3(CS_SLOTS / 256), dim3(256), 0, s, b);
-    hipLaunchKernelGGL(k_cset_rank, dim3(CS_MAXD / 256), dim3(256), 0, s, b);
+    hipLaunchKernelGGL(k_cset_list, dim3(CS_SLOTS / 1024), dim3(1024), 0, s, b);
+    hipLaunchKernelGGL(k_cset_rank, dim3(CS_MAXD / 256, CS_MAXD / CR_TILE), dim3(256), 0, s, b);
+    hipLaunchKernelGGL(k_cset_fin, dim3(CS_MAXD / 256), dim3(256), 0, s, b);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     u64 hv[8];
     u32 meta[3];
@@ -599,7 +628,8 @@ hipError_t msa_radix_sort_comp(u64 *const K2[3], u64 *const K1[3], u64 *const K0
     if ((e = hipGetLastError()) != hipSuccess) return e;
     u64 *const Kc[3] = {C, K2[1], K2[2]};
     const u64 hvc[3] = {0, 0, vc};
-    if ((e = msa_radix_sort(Kc, K1, K0, V, n, which, scratch, s, nullptr, false, hvc, true)) != hipSuccess) return e;
+    if ((e = msa_radix_sort(Kc, K1, K0, V, n, which, scratch, s, nullptr, false, hvc, true, ws_keep, v_keep)) != hipSuccess)
+        return e;
     *gB_out = gB;
     return hipSuccess;
 }
