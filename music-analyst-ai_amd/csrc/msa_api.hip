@@ -286,6 +286,7 @@ struct msa_ctx {
     int sort_k0 = 0;   // env MSA_SORT_K0=1: the words' radix sort covers key bytes 8..15 too
     int text_at_split = 1;  // env MSA_TEXT_AT_SPLIT=0: text.csv's gather forked by msa_count
     int comp_sort = 1;      // env MSA_COMP_SORT=0: the words' radix sort by K2 and K1 (no composite key)
+    u64 grow_mul = 4;       // env MSA_GROW_MUL: a grown table has >= this many slots per key the failed run claimed
     // env MSA_TEXT_AT_SPANS=1: text.csv's gather forked from the spans' stream
     // (measured and rejected: it slowed the artist pass beside it, 0.13 -> 0.51
     // ms, 2.97-3.00 vs 2.92-2.95 ms/step; profiles/r04_t28_ab_text_at_spans.txt)
@@ -638,8 +639,9 @@ static int ensure_tables(msa_ctx *c) {
 // stage that is retried.
 static void grow_tables(msa_ctx *c, u64 mask = ~0ull) {
     const u64 f = c->h_ctr.overflow & mask;
-    auto grow = [](u32 &lg, u64 claimed) {
-        const u32 want = log2_ceil(std::max<u64>(claimed * 4, 1));
+    const u64 mul = c->grow_mul;
+    auto grow = [mul](u32 &lg, u64 claimed) {
+        const u32 want = log2_ceil(std::max<u64>(claimed * mul, 1));
         lg = std::max<u32>(lg + 3, want);
         if (lg > 31) lg = 31;  // slot lists hold u32 indices
     };
@@ -1874,6 +1876,7 @@ int msa_create(int device, msa_ctx **out) {
     if (const char *ts = getenv("MSA_TEXT_AT_SPLIT")) c->text_at_split = atoi(ts) != 0;
     if (const char *tp = getenv("MSA_TEXT_AT_SPANS")) c->text_at_spans = atoi(tp) != 0;
     if (const char *cs = getenv("MSA_COMP_SORT")) c->comp_sort = atoi(cs) != 0;
+    if (const char *gm = getenv("MSA_GROW_MUL")) c->grow_mul = std::max(2, std::min(16, atoi(gm)));
     if (const char *ac = getenv("MSA_AUX_COL")) c->aux_col = atoi(ac) != 0;
     if (const char *me = getenv("MSA_MLOG_ENTRIES")) c->mlog_test = strtoull(me, nullptr, 10);
     if (const char *so = getenv("MSA_SORT")) c->sort_mode = !strcmp(so, "merge") ? 1 : (!strcmp(so, "radix") ? 2 : 0);
