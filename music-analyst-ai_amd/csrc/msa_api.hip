@@ -26,6 +26,9 @@ hipError_t msa_launch_scan(const ScanArgs &, int, hipStream_t);
 hipError_t msa_launch_scan_csv(const ScanArgs &, hipStream_t);
 hipError_t msa_launch_scan_tokens(const ScanArgs &, hipStream_t);
 hipError_t msa_launch_miss_agg(const ScanArgs &, hipStream_t);
+u64 msa_mb_hist_words(const ScanArgs &, u32);
+u32 msa_scan_blocks(const ScanArgs &);
+hipError_t msa_launch_miss_buckets(const ScanArgs &, u64 *, u64 *, u64 *, u64 *, ulonglong2 *, hipStream_t);
 hipError_t msa_exclusive_scan(const u64 *, u64, u64 *, u64 *, u64 *, hipStream_t);
 hipError_t msa_exclusive_scan2(const u64 *, u64, u64 *, u64 *, u64 *, const u64 *, u64, u64 *, u64 *, u64 *,
                                hipStream_t);
@@ -61,7 +64,7 @@ hipError_t msa_launch_artist_entries(const u64 *, const u32 *, u64, const u8 *, 
                                      u64 *, u32 *, u64 *, u64 *, hipStream_t);
 u64 msa_radix_scratch_bytes(u64 n);
 hipError_t msa_radix_sort(u64 *const[3], u64 *const[3], u64 *const[3], u32 *const[3], u64, int *, u8 *, hipStream_t,
-                          const u64 * = nullptr, bool = true, const u64 * = nullptr, bool = false, u64 ** = nullptr,
+                          const u64 * = nullptr, bool = true, const u64 * = nullptr, u32 = 0, u64 ** = nullptr,
                           u32 ** = nullptr);
 u64 msa_comp_scratch_bytes();
 hipError_t msa_radix_sort_comp(u64 *const[3], u64 *const[3], u64 *const[3], u32 *const[3], u64, int *, u8 *,
@@ -237,6 +240,17 @@ struct msa_ctx {
     // tables
     DevBuf s_tab, s_list, m_tab, m_list, l_pos, l_len, l_slot, l_tab, l_list, a_tab, a_list;
     DevBuf mlog, mlog_n;  // K3's logged LDS-table misses (k_miss_agg)
+    // the bucketed aggregation of the logs (msa_launch_miss_buckets): tile
+    // histograms, their scan, the bucketed entries
+    DevBuf mb_hist, mb_off, mb_bsum, mb_tot, mb_out;
+    // env MSA_MISS_BUCKETS: 0 never (default), 1 always, 2 when the last split
+    // logged > mb_min misses.  Measured and not taken: configs[4] 32.5 vs 28.6
+    // ms/step (the bucket scatter 2.0 ms, the bucket aggregation 8.0: one claim
+    // and one add per distinct key, far fewer in flight than k_miss_agg's
+    // per-entry inserts); configs[2] 4.38 vs 2.90 (profiles/r04_t36_*)
+    int mb_mode = 0;
+    u64 mb_min = 24000000;
+    u64 mb_prev = 0;     // the last split's logged misses
     DevBuf lmask;         // the split scan's lyric token-byte mask (k_scan_struct -> k_scan_tokens)
     int k3split = 1;      // MSA_K3SPLIT=0: the fused k_scan_csv instead (A/B runs)
     u64 s_slots = 0, m_slots = 0, l_occ_cap = 0, lt_slots = 0, a_slots = 0;
@@ -287,6 +301,7 @@ struct msa_ctx {
     int text_at_split = 1;  // env MSA_TEXT_AT_SPLIT=0: text.csv's gather forked by msa_count
     int comp_sort = 1;      // env MSA_COMP_SORT=0: the words' radix sort by K2 and K1 (no composite key)
     u64 grow_mul = 4;       // env MSA_GROW_MUL: a grown table has >= this many slots per key the failed run claimed
+    u32 grow_step = 3;      // env MSA_GROW_STEP: ... and at least 2^step times the slots it had
     // env MSA_TEXT_AT_SPANS=1: text.csv's gather forked from the spans' stream
     // (measured and rejected: it slowed the artist pass beside it, 0.13 -> 0.51
     // ms, 2.97-3.00 vs 2.92-2.95 ms/step; profiles/r04_t28_ab_text_at_spans.txt)
@@ -640,9 +655,10 @@ static int ensure_tables(msa_ctx *c) {
 static void grow_tables(msa_ctx *c, u64 mask = ~0ull) {
     const u64 f = c->h_ctr.overflow & mask;
     const u64 mul = c->grow_mul;
-    auto grow = [mul](u32 &lg, u64 claimed) {
+    const u32 step = c->grow_step;
+    auto grow = [mul, step](u32 &lg, u64 claimed) {
         const u32 want = log2_ceil(std::max<u64>(claimed * mul, 1));
-        lg = std::max<u32>(lg + 3, want);
+        lg = std::max<u32>(lg + step, want);
         if (lg > 31) lg = 31;  // slot lists hold u32 indices
     };
     if (f & OVF_S) grow(c->s_log2, c->h_ctr.s_claimed);
@@ -1142,7 +1158,21 @@ static int split_once(msa_ctx *c, int flags) {
     }
     if (!(c->ablate & 64)) {
         prof_begin(c, ST_MISS_AGG);
-        HIPC(c, msa_launch_miss_agg(a, c->stream));
+        // high cardinality (the last split's logs held far more distinct keys
+        // than the aggregating workgroups' LDS tables): bucketed first
+        const bool mb = c->mb_mode == 1 || (c->mb_mode == 2 && c->mb_prev > c->mb_min);
+        if (mb) {
+            const u64 hw = msa_mb_hist_words(a, msa_scan_blocks(a));
+            HIPC(c, ensure(c->mb_hist, hw * 8));
+            HIPC(c, ensure(c->mb_off, hw * 8));
+            HIPC(c, ensure(c->mb_bsum, ((hw + 1023) / 1024 + 1) * 8));
+            HIPC(c, ensure(c->mb_tot, 64));
+            HIPC(c, ensure(c->mb_out, (u64)msa_scan_blocks(a) * MSA_MLOG_PARTS * a.mlog_cap * 16));
+            HIPC(c, msa_launch_miss_buckets(a, c->mb_hist.as<u64>(), c->mb_off.as<u64>(), c->mb_bsum.as<u64>(),
+                                            c->mb_tot.as<u64>(), c->mb_out.as<ulonglong2>(), c->stream));
+        } else {
+            HIPC(c, msa_launch_miss_agg(a, c->stream));
+        }
         prof_end(c, ST_MISS_AGG, 0);
     }
     // rec_start[nrec] = end of the last record (EOF when it has no terminator);
@@ -1219,6 +1249,7 @@ static int split_once(msa_ctx *c, int flags) {
         c->a_used_prev = std::min<u64>(c->h_ctr.a_claimed, c->a_slots / 2);
         if (c->h_ctr.overflow & OVF_A) c->a_dirty = true;
     }
+    c->mb_prev = c->h_ctr.k3_misses;
     if (c->h_ctr.mlog_full) {  // the logs were too small for this input's misses: 25 % more than all of
                                // them -- doubled when misses were dropped (OVF_MLOG: this split runs
                                // again) and that would not be more (a partition fuller than the rest)
@@ -1721,8 +1752,10 @@ static int do_rank(msa_ctx *c, int tables = 3) {
         ea.K0 = W.K[0][2].as<u64>();
         ea.val = W.V[0].as<u32>();
         ea.ref = W.ref.as<u64>();
-        ea.cnt = W.cnt.as<u64>();
         W.vary_ok = !small_sort(c, W.n);  // the radix sort's varying bytes, reduced while the entries are written
+        // the count plane: read only by the small-table ranking's key blob (the
+        // radix path's blob reads the sorted ~count plane)
+        ea.cnt = W.vary_ok ? nullptr : W.cnt.as<u64>();
         if (W.vary_ok) {
             HIPC(c, ensure(W.vary, 64));
             HIPC(c, hipMemsetAsync(W.vary.p, 0, 24, c->stream));
@@ -1877,6 +1910,9 @@ int msa_create(int device, msa_ctx **out) {
     if (const char *tp = getenv("MSA_TEXT_AT_SPANS")) c->text_at_spans = atoi(tp) != 0;
     if (const char *cs = getenv("MSA_COMP_SORT")) c->comp_sort = atoi(cs) != 0;
     if (const char *gm = getenv("MSA_GROW_MUL")) c->grow_mul = std::max(2, std::min(16, atoi(gm)));
+    if (const char *gs = getenv("MSA_GROW_STEP")) c->grow_step = (u32)std::max(1, std::min(4, atoi(gs)));
+    if (const char *mb = getenv("MSA_MISS_BUCKETS")) c->mb_mode = atoi(mb);
+    if (const char *mm = getenv("MSA_MISS_BUCKETS_MIN")) c->mb_min = strtoull(mm, nullptr, 10);
     if (const char *ac = getenv("MSA_AUX_COL")) c->aux_col = atoi(ac) != 0;
     if (const char *me = getenv("MSA_MLOG_ENTRIES")) c->mlog_test = strtoull(me, nullptr, 10);
     if (const char *so = getenv("MSA_SORT")) c->sort_mode = !strcmp(so, "merge") ? 1 : (!strcmp(so, "radix") ? 2 : 0);

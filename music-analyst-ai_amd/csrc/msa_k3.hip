@@ -1018,6 +1018,152 @@ __global__ __launch_bounds__(MA_T) void k_miss_agg(ScanArgs a, u32 nsrc, u32 gro
     }
 }
 
+// ---------------------------------------------------------------------------
+// High-cardinality aggregation (configs[4]: 70 M logged misses, 50 M distinct
+// keys).  k_miss_agg's LDS table fills after ~8 K keys per workgroup and then
+// every further entry is one HBM insert (probe + claim + count: ~2 memory-side
+// atomics per entry, 6.5 ms).  Here the logs are first bucketed by a second
+// key hash -- MB_B buckets per partition, small enough that a bucket's
+// distinct keys fit one workgroup's LDS table -- with a counting sort
+// (k_mb_hist: per-tile bucket counts, bucket-major; one exclusive scan;
+// k_mb_scatter).  k_mb_agg then counts each bucket in LDS and inserts each
+// distinct key once, claim first (CAS) and count (no-return add), with no
+// load-first probe.  The count stays an atomic add: the LDS table can hold a
+// key twice (a prober that meets a slot claimed but not yet keyed moves on)
+// and an entry that finds the LDS table full takes the atomic insert -- a
+// plain count store lost those adds (caught by test_gpu_miss_buckets).
+// Opt-in (MSA_MISS_BUCKETS=1): slower than k_miss_agg at both configs[2] and
+// configs[4] (msa_ctx::mb_mode).
+#define MB_B 1024u       // buckets per partition
+#define MB_TT 512u       // threads per tile
+#define MB_TILE 8192u    // log entries per tile
+__device__ __forceinline__ u32 mb_bucket(u64 k0, u64 k1m) {
+    u64 h = (k0 & MLOG_KEYBITS) * 0x9E3779B97F4A7C15ull ^ (k1m & (MLOG_KEYBITS | KMARK)) * 0xC2B2AE3D27D4EB4Full;
+    h ^= h >> 29;
+    return (u32)(h >> 40) & (MB_B - 1);  // independent of mlog_part's bits (low 32 of a different mix)
+}
+// tile (part p, source s, chunk c) = entries [c MB_TILE, (c + 1) MB_TILE) of log (s, p);
+// t = s * chunks + c; hist[(p * MB_B + b) * T + t]
+__global__ __launch_bounds__(MB_TT) void k_mb_hist(ScanArgs a, u32 chunks, u32 T, u64 *__restrict__ hist) {
+    __shared__ u32 h[MB_B];
+    const u32 p = blockIdx.y, t = blockIdx.x, src = t / chunks, c = t % chunks;
+    for (u32 k = threadIdx.x; k < MB_B; k += MB_TT) h[k] = 0;
+    __syncthreads();
+    const u32 n = a.mlog_n[src * MSA_MLOG_PARTS + p];
+    if (c == 0 && threadIdx.x == 0 && n) atomicAdd((unsigned long long *)&a.ctr->k3_misses, (unsigned long long)n);
+    const u32 lo = c * MB_TILE, hi = min(n, lo + MB_TILE);
+    const u64 base = ((u64)src * MSA_MLOG_PARTS + p) * a.mlog_cap;
+    for (u32 i = lo + threadIdx.x; i < hi; i += MB_TT) {
+        const ulonglong2 x = a.mlog[base + i];
+        atomicAdd(&h[mb_bucket(x.x, x.y)], 1u);
+    }
+    __syncthreads();
+    for (u32 k = threadIdx.x; k < MB_B; k += MB_TT) hist[((u64)p * MB_B + k) * T + t] = h[k];
+}
+__global__ __launch_bounds__(MB_TT) void k_mb_scatter(ScanArgs a, u32 chunks, u32 T, const u64 *__restrict__ off,
+                                                      ulonglong2 *__restrict__ out) {
+    __shared__ u32 cur[MB_B];
+    const u32 p = blockIdx.y, t = blockIdx.x, src = t / chunks, c = t % chunks;
+    const u32 n = a.mlog_n[src * MSA_MLOG_PARTS + p];
+    const u32 lo = c * MB_TILE, hi = min(n, lo + MB_TILE);
+    if (lo >= hi) return;  // whole workgroup
+    for (u32 k = threadIdx.x; k < MB_B; k += MB_TT) cur[k] = 0;
+    __syncthreads();
+    const u64 base = ((u64)src * MSA_MLOG_PARTS + p) * a.mlog_cap;
+    for (u32 i = lo + threadIdx.x; i < hi; i += MB_TT) {
+        const ulonglong2 x = a.mlog[base + i];
+        const u32 b = mb_bucket(x.x, x.y);
+        const u32 r = atomicAdd(&cur[b], 1u);  // order within a bucket does not matter
+        out[off[((u64)p * MB_B + b) * T + t] + r] = x;
+    }
+}
+// one claim per distinct key of a bucket (CAS first: most keys are new)
+__device__ __forceinline__ void mb_insert_once(const ScanArgs &a, u64 k0, u64 k1m, u64 cnt) {
+    if (k1m == KMARK) {
+        u64 h = fmix64(k0) & a.s_mask;
+        for (u32 probe = 0; probe < MSA_MAX_PROBE; ++probe) {
+            u64 *slot = a.s_tab + 2 * h;
+            const u64 old = atomicCAS((unsigned long long *)slot, 0ull, (unsigned long long)k0);
+            if (old == 0 || old == k0) {
+                atomicAdd((unsigned long long *)(slot + 1), (unsigned long long)cnt);
+                return;
+            }
+            h = (h + 1) & a.s_mask;
+        }
+        atomicOr((unsigned long long *)&a.ctr->overflow, (unsigned long long)OVF_S);
+        return;
+    }
+    const u64 k1 = k1m & ~KMARK;
+    u64 h = fmix64(k0 ^ fmix64(k1)) & a.m_mask;
+    u32 probe = 0, spins = 0;
+    while (probe < MSA_MAX_PROBE) {
+        u64 *slot = a.m_tab + 4 * h;
+        const u64 c0 = atomicCAS((unsigned long long *)slot, 0ull, (unsigned long long)k0);
+        if (c0 == 0) {
+            __hip_atomic_store(slot + 1, k1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            atomicAdd((unsigned long long *)(slot + 2), (unsigned long long)cnt);
+            return;
+        }
+        if (c0 == k0) {
+            const u64 c1 = __hip_atomic_load(slot + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (c1 == 0) {  // claimed, k1 not yet visible: retry this slot
+                if (++spins > (1u << 24)) break;
+                __builtin_amdgcn_s_sleep(1);
+                continue;
+            }
+            if (c1 == k1) {
+                atomicAdd((unsigned long long *)(slot + 2), (unsigned long long)cnt);
+                return;
+            }
+        }
+        h = (h + 1) & a.m_mask;
+        ++probe;
+    }
+    atomicOr((unsigned long long *)&a.ctr->overflow, (unsigned long long)OVF_M);
+}
+// workgroup (p, b): bucket b of partition p = bucketed entries [off[(p B + b) T], off[(p B + b + 1) T])
+#define MBA_T 512
+__global__ __launch_bounds__(MBA_T) void k_mb_agg(ScanArgs a, u32 T, const u64 *__restrict__ off,
+                                                  const u64 *__restrict__ total, const ulonglong2 *__restrict__ in) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    ulonglong2 *keys = reinterpret_cast<ulonglong2 *>(smem);
+    u32 *cnts = reinterpret_cast<u32 *>(smem + MA_SLOTS * 16);
+    const u64 q = (u64)blockIdx.y * MB_B + blockIdx.x;
+    const u64 lo = off[q * T], hi = q + 1 < (u64)MSA_MLOG_PARTS * MB_B ? off[(q + 1) * T] : *total;
+    if (lo >= hi) return;
+    for (u32 i = threadIdx.x; i < MA_SLOTS; i += MBA_T) {
+        keys[i] = make_ulonglong2(0, 0);
+        cnts[i] = 0;
+    }
+    __syncthreads();
+    for (u64 i0 = lo + threadIdx.x; i0 < hi; i0 += (u64)MA_FLY * MBA_T) {
+        ulonglong2 xs[MA_FLY];
+#pragma unroll
+        for (int f = 0; f < MA_FLY; ++f) {
+            const u64 i = i0 + (u64)f * MBA_T;
+            xs[f] = i < hi ? in[i] : make_ulonglong2(0, 0);
+        }
+#pragma unroll
+        for (int f = 0; f < MA_FLY; ++f) {
+            if (i0 + (u64)f * MBA_T >= hi) break;
+            const ulonglong2 x = xs[f];
+            const u32 c = gather8(x.x) | ((gather8(x.y) & 0x7Fu) << 8);
+            const u64 k0 = x.x & MLOG_KEYBITS, k1 = x.y & (MLOG_KEYBITS | KMARK);
+            const u32 slot = ma_find(keys, k0, k1);
+            if (slot != ~0u) atomicAdd(&cnts[slot], c ? c : 1u);
+            else hbm_insert16<true>(a, k0, k1, c ? c : 1u);  // table full: this key's every entry
+        }
+    }
+    __syncthreads();
+    for (u32 i = threadIdx.x; i < MA_SLOTS; i += MBA_T) {
+        const u32 c = cnts[i];
+        if (c) {
+            const ulonglong2 kk = keys[i];
+            mb_insert_once(a, kk.x, kk.y, c);
+        }
+    }
+}
+
 static int g_q_cus = 0;
 // Counting workgroups: one per CU (k_scan_csv: a wave per 16 KiB chunk;
 // k_scan_tokens: a wave per 4 KiB block).  k_miss_agg reads their logs.
@@ -1057,6 +1203,33 @@ hipError_t msa_launch_scan_tokens(const ScanArgs &a, hipStream_t s) {
 }
 // after k_scan_csv on the same stream: fold the logged misses, 16 partitions x
 // groups, one workgroup per CU
+// the bucketed aggregation: scratch sizes (entries = every log's capacity)
+u64 msa_mb_hist_words(const ScanArgs &a, u32 nsrc) {
+    const u32 chunks = (a.mlog_cap + MB_TILE - 1) / MB_TILE;
+    return (u64)MSA_MLOG_PARTS * MB_B * nsrc * chunks;
+}
+hipError_t msa_exclusive_scan(const u64 *in, u64 n, u64 *out, u64 *bsum_scratch, u64 *total, hipStream_t s);
+// hist / off: msa_mb_hist_words u64 each; bsum: (that + 1023) / 1024 + 1 words;
+// total: one word; out: nsrc * PARTS * mlog_cap entries
+hipError_t msa_launch_miss_buckets(const ScanArgs &a, u64 *hist, u64 *off, u64 *bsum, u64 *total, ulonglong2 *out,
+                                   hipStream_t s) {
+    if (!a.nchunks) return hipSuccess;
+    const u32 nsrc = scan_blocks(a);
+    const u32 chunks = (a.mlog_cap + MB_TILE - 1) / MB_TILE, T = nsrc * chunks;
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void *)k_mb_agg, hipFuncAttributeMaxDynamicSharedMemorySize, MA_SLOTS * 20);
+        attr = true;
+    }
+    hipLaunchKernelGGL(k_mb_hist, dim3(T, MSA_MLOG_PARTS), dim3(MB_TT), 0, s, a, chunks, T, hist);
+    hipError_t e = msa_exclusive_scan(hist, msa_mb_hist_words(a, nsrc), off, bsum, total, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_mb_scatter, dim3(T, MSA_MLOG_PARTS), dim3(MB_TT), 0, s, a, chunks, T, (const u64 *)off, out);
+    hipLaunchKernelGGL(k_mb_agg, dim3(MB_B, MSA_MLOG_PARTS), dim3(MBA_T), MA_SLOTS * 20, s, a, T, (const u64 *)off,
+                       (const u64 *)total, (const ulonglong2 *)out);
+    return hipGetLastError();
+}
+u32 msa_scan_blocks(const ScanArgs &a) { return scan_blocks(a); }
 hipError_t msa_launch_miss_agg(const ScanArgs &a, hipStream_t s) {
     if (!a.nchunks) return hipSuccess;
     const u32 blocks = scan_blocks(a);

@@ -65,15 +65,18 @@ __global__ void k_scan_zero_totals(ScanJobs js) {
         __hip_atomic_store(js.j[threadIdx.x].total, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__global__ __launch_bounds__(SCAN_T) void k_scan_top(ScanJobs js) {
+// one workgroup of SCAN_TOP_T threads per array (a 256-thread one walked
+// ~200 block sums per thread for configs[4]'s 50 M blob lengths: 104 us)
+#define SCAN_TOP_T 1024
+__global__ __launch_bounds__(SCAN_TOP_T) void k_scan_top(ScanJobs js) {
     const ScanJob &J = js.j[blockIdx.y];
     if (!J.n) {
         if (threadIdx.x == 0 && J.total) __hip_atomic_store(J.total, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
     }
-    __shared__ u64 wtot[SCAN_T / 64];
+    __shared__ u64 wtot[SCAN_TOP_T / 64];
     const u64 nb = (J.n + SCAN_TILE - 1) / SCAN_TILE;
-    const u64 per = (nb + SCAN_T - 1) / SCAN_T;
+    const u64 per = (nb + SCAN_TOP_T - 1) / SCAN_TOP_T;
     const u64 a = min(nb, (u64)threadIdx.x * per), b = min(nb, a + per);
     u64 s = 0;
     for (u64 i = a; i < b; ++i) s += J.bsum[i];
@@ -91,7 +94,7 @@ __global__ __launch_bounds__(SCAN_T) void k_scan_top(ScanJobs js) {
     // other streams update meanwhile (e.g. the column spans beside the token
     // pass): a write-through store, so no dirty copy of that line stays in
     // this XCD's L2 to be written back over their updates later
-    if (threadIdx.x == SCAN_T - 1 && J.total) __hip_atomic_store(J.total, acc + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == SCAN_TOP_T - 1 && J.total) __hip_atomic_store(J.total, acc + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (u64 i = a; i < b; ++i) { const u64 v = J.bsum[i]; J.bsum[i] = acc; acc += v; }
 }
 
@@ -141,7 +144,7 @@ hipError_t msa_exclusive_scan2(const u64 *in, u64 n, u64 *out, u64 *bsum, u64 *t
     }
     const u64 nb = (nmax + SCAN_TILE - 1) / SCAN_TILE;
     hipLaunchKernelGGL(k_scan_reduce, dim3((u32)nb, ny), dim3(SCAN_T), 0, s, js);
-    hipLaunchKernelGGL(k_scan_top, dim3(1, ny), dim3(SCAN_T), 0, s, js);
+    hipLaunchKernelGGL(k_scan_top, dim3(1, ny), dim3(SCAN_TOP_T), 0, s, js);
     hipLaunchKernelGGL(k_scan_down, dim3((u32)nb, ny), dim3(SCAN_T), 0, s, js);
     return hipGetLastError();
 }
@@ -1817,7 +1820,7 @@ __global__ __launch_bounds__(256) void k_word_entries(EntryArgs a) {
         a.K0[i] = lo;
         a.val[i] = (u32)i;
         a.ref[i] = ref;
-        a.cnt[i] = c;
+        if (a.cnt) a.cnt[i] = c;
         vo[0] |= lo; vo[1] |= hi; vo[2] |= ~c;
         va[0] &= lo; va[1] &= hi; va[2] &= ~c;
     }
@@ -2028,9 +2031,11 @@ struct TieFlags {
 // K0 null: the sort covered K2 and K1 only (K0's bytes are the first refinement round's)
 __device__ __forceinline__ TieFlags tie_flags(const u64 *__restrict__ K2, const u64 *__restrict__ K1,
                                               const u64 *__restrict__ K0, u64 n, u64 i) {
-    const u64 a2 = K2[i], a1 = K1[i], a0 = K0 ? K0[i] : 0;
-    const bool eq_prev = i > 0 && K2[i - 1] == a2 && K1[i - 1] == a1 && (!K0 || K0[i - 1] == a0);
-    const bool eq_next = i + 1 < n && K2[i + 1] == a2 && K1[i + 1] == a1 && (!K0 || K0[i + 1] == a0);
+    // K1 == K2: one plane (the composite key's sort)
+    const bool k1s = K1 != K2;
+    const u64 a2 = K2[i], a1 = k1s ? K1[i] : 0, a0 = K0 ? K0[i] : 0;
+    const bool eq_prev = i > 0 && K2[i - 1] == a2 && (!k1s || K1[i - 1] == a1) && (!K0 || K0[i - 1] == a0);
+    const bool eq_next = i + 1 < n && K2[i + 1] == a2 && (!k1s || K1[i + 1] == a1) && (!K0 || K0[i + 1] == a0);
     return TieFlags{!eq_prev, eq_prev || eq_next};
 }
 // entry (row k, thread t) of block b is entry b * TB_N + k * TB_T + t

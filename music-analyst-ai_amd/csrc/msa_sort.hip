@@ -75,6 +75,9 @@ __global__ __launch_bounds__(256) void k_rx_vary(const u64 *__restrict__ K2, con
 #define GH_FLY 4
 #endif
 #define OS_POS 24               // byte positions: K0 bytes 0..7, K1, K2
+#ifndef OS_LB
+#define OS_LB 1  // statuses per look-back round trip (8: configs[4] 28.5 -> 29.4 ms/step, the passes slower)
+#endif
 #define OS_SPIN_LIMIT (1u << 24)  // polls before a look-back gives up (error, never a hang)
 
 // part[block][pos][digit] = entries of the block's stride with that digit at pos
@@ -211,23 +214,37 @@ __global__ __launch_bounds__(OS_T) void k_os_pass(const u64 *__restrict__ W, con
             __hip_atomic_store(st, os_pack(epoch, 1, h), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
             __hip_atomic_store(st, os_pack(epoch, 0, h), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            u64 q = tile - 1;
+            // look back OS_LB tiles per round trip (their statuses loaded
+            // together; measured: more than one per trip slowed the passes)
+            long long q = (long long)tile - 1;
             u32 spins = 0;
-            for (;;) {
-                const u64 sv =
-                    __hip_atomic_load(status + q * 256 + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const u32 hi = (u32)(sv >> 32);
-                if ((hi >> 1) != epoch) {  // not published yet in this pass
+            bool done = false;
+            while (!done) {
+                u64 sv[OS_LB];
+#pragma unroll
+                for (u32 k = 0; k < OS_LB; ++k)
+                    sv[k] = q - (long long)k >= 0 ? __hip_atomic_load(status + (u64)(q - (long long)k) * 256 + t, __ATOMIC_RELAXED,
+                                                                __HIP_MEMORY_SCOPE_AGENT)
+                                            : 0ull;
+                u32 k = 0;
+                for (; k < OS_LB; ++k) {
+                    const u32 hi = (u32)(sv[k] >> 32);
+                    if ((hi >> 1) != epoch) break;  // not published yet in this pass: reload from here
+                    excl += (u32)sv[k];
+                    if ((hi & 1u) || q - (long long)k == 0) {
+                        done = true;
+                        break;
+                    }
+                }
+                if (done) break;
+                q -= (long long)k;
+                if (k == 0) {
                     if (++spins > OS_SPIN_LIMIT) {
                         atomicOr(err, 1u);
                         break;
                     }
                     __builtin_amdgcn_s_sleep(1);
-                    continue;
                 }
-                excl += (u32)sv;
-                if ((hi & 1u) || q == 0) break;
-                --q;
             }
             __hip_atomic_store(st, os_pack(epoch, 1, (u32)(excl + h)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
@@ -285,18 +302,34 @@ __global__ void k_rx_gather(const u64 *__restrict__ src, const u32 *__restrict__
 
 // the sorted entries; word `wsel` (0 = K0 .. 2 = K2; 3 = none) is already in
 // order in Ws (the last sorted word), the others are gathered through V
-// k0z: keys hold no zero byte (words), so a key whose byte 7 is zero ended
+// kmode bit 0: keys hold no zero byte (words), so a key whose byte 7 is zero ended
 // before byte 8 and its K0 is zero -- not gathered (most words are short)
+// kmode bit 1: Ws holds composite keys (msa_radix_sort_comp) with the gid in
+// the top kmode >> 4 bytes: a key whose last covered byte is zero ended
+// there, so its K1 is the composite key shifted up and its K0 zero -- not
+// gathered at all (short words: a third of configs[4]'s entries)
 __global__ void k_rx_final(const u64 *__restrict__ K2, const u64 *__restrict__ K1, const u64 *__restrict__ K0,
-                           const u32 *__restrict__ V, u64 n, const u64 *__restrict__ Ws, u32 wsel, u32 k0z,
+                           const u32 *__restrict__ V, u64 n, const u64 *__restrict__ Ws, u32 wsel, u32 kmode,
                            u64 *__restrict__ O2, u64 *__restrict__ O1, u64 *__restrict__ O0, u32 *__restrict__ OV) {
     const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const u32 v = V[i];
-    if (O2) O2[i] = wsel == 2 ? Ws[i] : K2[v];  // null: the caller keeps Ws as the sorted K2 plane
-    const u64 k1 = wsel == 1 ? Ws[i] : K1[v];
-    O1[i] = k1;
-    O0[i] = wsel == 0 ? Ws[i] : ((k0z && !(k1 & 0xFFu)) ? 0ull : K0[v]);
+    const u64 w2 = wsel == 2 ? Ws[i] : K2[v];
+    if (O2) O2[i] = w2;  // null: the caller keeps Ws as the sorted K2 plane
+    if ((kmode & 2u) && wsel == 2) {
+        if (!(w2 & 0xFFu)) {
+            O1[i] = w2 << (8 * (kmode >> 4));
+            O0[i] = 0;
+        } else {  // both words' loads in flight together (no dependent K0 load)
+            const u64 k1 = K1[v], k0 = K0[v];
+            O1[i] = k1;
+            O0[i] = k0;
+        }
+    } else {
+        const u64 k1 = wsel == 1 ? Ws[i] : K1[v];
+        O1[i] = k1;
+        O0[i] = wsel == 0 ? Ws[i] : (((kmode & 1u) && !(k1 & 0xFFu)) ? 0ull : K0[v]);
+    }
     if (OV) OV[i] = v;  // null: the caller keeps V as the sorted values
 }
 
@@ -316,7 +349,7 @@ u64 msa_radix_scratch_bytes(u64 n) {
 // msa_launch_sort.  `scratch` holds msa_radix_scratch_bytes(n) bytes.
 hipError_t msa_radix_sort(u64 *const K2[3], u64 *const K1[3], u64 *const K0[3], u32 *const V[3], u64 n, int *which,
                           u8 *scratch, hipStream_t s, const u64 *vary_pre, bool sort_k0, const u64 *hv_host,
-                          bool k0z, u64 **ws_keep, u32 **v_keep) {
+                          u32 kmode, u64 **ws_keep, u32 **v_keep) {
     if (ws_keep) *ws_keep = nullptr;
     if (v_keep) *v_keep = nullptr;
     *which = 1;
@@ -394,7 +427,7 @@ hipError_t msa_radix_sort(u64 *const K2[3], u64 *const K1[3], u64 *const K0[3], 
     const bool vk = v_keep && vloc != 0;
     if (vk) *v_keep = V[vloc];
     hipLaunchKernelGGL(k_rx_final, g1(n), dim3(256), 0, s, K2[0], K1[0], K0[0], (const u32 *)V[vloc], n, Wp, wsel,
-                       (u32)k0z, keep ? nullptr : K2[o], K1[o], K0[o], vk ? nullptr : V[o]);
+                       kmode, keep ? nullptr : K2[o], K1[o], K0[o], vk ? nullptr : V[o]);
     *which = o;
     if ((e = hipGetLastError()) != hipSuccess) return e;
     u32 herr = 0;  // a look-back that gave up (never expected: tiles take tickets in order)
@@ -628,7 +661,7 @@ hipError_t msa_radix_sort_comp(u64 *const K2[3], u64 *const K1[3], u64 *const K0
     if ((e = hipGetLastError()) != hipSuccess) return e;
     u64 *const Kc[3] = {C, K2[1], K2[2]};
     const u64 hvc[3] = {0, 0, vc};
-    if ((e = msa_radix_sort(Kc, K1, K0, V, n, which, scratch, s, nullptr, false, hvc, true, ws_keep, v_keep)) != hipSuccess)
+    if ((e = msa_radix_sort(Kc, K1, K0, V, n, which, scratch, s, nullptr, false, hvc, 1u | 2u | (gB << 4), ws_keep, v_keep)) != hipSuccess)
         return e;
     *gB_out = gB;
     return hipSuccess;
