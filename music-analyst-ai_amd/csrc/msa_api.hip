@@ -306,6 +306,7 @@ struct msa_ctx {
     // (measured and rejected: it slowed the artist pass beside it, 0.13 -> 0.51
     // ms, 2.97-3.00 vs 2.92-2.95 ms/step; profiles/r04_t28_ab_text_at_spans.txt)
     int text_at_spans = 0;
+    int text_at_agg = 0;  // env MSA_TEXT_AT_AGG=1: forked behind the miss aggregation (A/B)
     // the K2 final-state read-back (launch_scan_fn / wait_scan_fn)
     hipEvent_t ev_fin = nullptr;
     State fin_init{};
@@ -1205,6 +1206,8 @@ static int split_once(msa_ctx *c, int flags) {
             if ((rc = launch_text(c, c->side))) return rc;
             HIPC(c, hipEventRecord(c->ev_join, c->side));
             c->side_pending = true;
+        } else if (c->text_at_agg) {  // A/B: forked behind the aggregation (and the spans), before the artist pass
+            if ((rc = start_text_side(c))) return rc;
         }
     }
     // one read-back after the scan: the counters (table overflow, long-word
@@ -1908,6 +1911,7 @@ int msa_create(int device, msa_ctx **out) {
     if (const char *k0 = getenv("MSA_SORT_K0")) c->sort_k0 = atoi(k0) != 0;
     if (const char *ts = getenv("MSA_TEXT_AT_SPLIT")) c->text_at_split = atoi(ts) != 0;
     if (const char *tp = getenv("MSA_TEXT_AT_SPANS")) c->text_at_spans = atoi(tp) != 0;
+    if (const char *ta = getenv("MSA_TEXT_AT_AGG")) c->text_at_agg = atoi(ta) != 0;
     if (const char *cs = getenv("MSA_COMP_SORT")) c->comp_sort = atoi(cs) != 0;
     if (const char *gm = getenv("MSA_GROW_MUL")) c->grow_mul = std::max(2, std::min(16, atoi(gm)));
     if (const char *gs = getenv("MSA_GROW_STEP")) c->grow_step = (u32)std::max(1, std::min(4, atoi(gs)));

@@ -1533,12 +1533,16 @@ __global__ __launch_bounds__(AC_T) void k_artist_count(const u64 *__restrict__ l
 // representative kept), then adds each distinct hash to the HBM table once.
 #define AM_T 1024
 #define AM_SLOTS 4096
+#define AM_STAGE 4096
 __global__ __launch_bounds__(AM_T) void k_artist_merge(const ulonglong2 *__restrict__ alog,
                                                        const u32 *__restrict__ alog_n, u32 alog_cap, u32 nsrc,
                                                        u32 groups, u64 *atab, u64 amask, u32 *alist, u64 alist_cap,
                                                        Counters *ctr) {
     __shared__ u64 mh[AM_SLOTS], mc[AM_SLOTS], ms[AM_SLOTS], mr[AM_SLOTS];
+    __shared__ u32 staged[AM_STAGE], nst;  // the workgroup's new HBM slots (stage_new)
+    __shared__ u64 gbase;
     for (u32 i = threadIdx.x; i < AM_SLOTS; i += AM_T) { mh[i] = 0; mc[i] = 0; ms[i] = 0; mr[i] = ~0ull; }
+    if (threadIdx.x == 0) nst = 0;
     __syncthreads();
     const u32 part = blockIdx.x % AC_PARTS, g = blockIdx.x / AC_PARTS;
     for (u32 src = g; src < nsrc; src += groups) {
@@ -1561,12 +1565,25 @@ __global__ __launch_bounds__(AM_T) void k_artist_merge(const ulonglong2 *__restr
                     done = true;
                 }
             }
-            if (!done) h_insert2(atab, amask, x.x, x.y, y.y, y.x, alist, alist_cap, &ctr->a_claimed, ctr, OVF_A);
+            bool isnew = false;
+            u64 sl = 0;
+            if (!done)
+                sl = h_insert2<false>(atab, amask, x.x, x.y, y.y, y.x, alist, alist_cap, &ctr->a_claimed, ctr, OVF_A,
+                                      &isnew);
+            stage_new(isnew, sl, staged, &nst, AM_STAGE, alist, alist_cap, &ctr->a_claimed, ctr, OVF_A);
         }
     }
     __syncthreads();
-    for (u32 i = threadIdx.x; i < AM_SLOTS; i += AM_T)
-        if (mc[i]) h_insert2(atab, amask, mh[i], mc[i], mr[i], ms[i], alist, alist_cap, &ctr->a_claimed, ctr, OVF_A);
+    for (u32 i = threadIdx.x; i < AM_SLOTS; i += AM_T) {
+        bool isnew = false;
+        u64 sl = 0;
+        if (mc[i])
+            sl = h_insert2<false>(atab, amask, mh[i], mc[i], mr[i], ms[i], alist, alist_cap, &ctr->a_claimed, ctr, OVF_A,
+                                  &isnew);
+        stage_new(isnew, sl, staged, &nst, AM_STAGE, alist, alist_cap, &ctr->a_claimed, ctr, OVF_A);
+    }
+    __syncthreads();
+    stage_flush(staged, &nst, AM_STAGE, &gbase, alist, alist_cap, &ctr->a_claimed, ctr, OVF_A);
 }
 
 // Every HBM artist entry: sum of h2 == count x h2(representative).
@@ -1627,14 +1644,12 @@ __global__ void k_artist_verify(const u8 *__restrict__ arena, const u64 *__restr
 }
 
 // ---------------------------------------------------------------------------
-// words > 16 bytes
-__global__ void k_long_insert(const u8 *__restrict__ buf, u64 seg_end, const u8 *__restrict__ extra, u64 extra_len,
-                              const u64 *__restrict__ l_pos, u64 n,
-                              u32 *__restrict__ l_len, u64 *__restrict__ l_slot, u64 *ltab, u64 lmask, u32 *llist,
-                              u64 llist_cap, Counters *ctr) {
-    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const u64 p = l_pos[i];
+// words > 16 bytes (one occurrence per thread: 1024-thread workgroups of 4
+// occurrences per thread with the new slots listed once per workgroup were
+// slower, 1.48 -> 1.75 ms for configs[4] and 0.04 -> 0.44 ms for configs[2]:
+// the list claims were not what bound it, the inserts in flight are)
+__device__ __forceinline__ u64 long_hash(const u8 *__restrict__ buf, u64 seg_end, const u8 *__restrict__ extra,
+                                         u64 extra_len, u64 p, u32 &len) {
     const u8 *src = tok_at(buf, extra, p);
     const u64 lim = (p & MSA_POS_EXTRA) ? extra_len - (p & ~MSA_POS_EXTRA) : seg_end - p;
     // the token's first 48 bytes from 13 dword loads (the buffers are padded
@@ -1647,7 +1662,7 @@ __global__ void k_long_insert(const u8 *__restrict__ buf, u64 seg_end, const u8 
     for (int k = 0; k < 13; ++k) w[k] = wp[k];
 #pragma unroll
     for (int k = 0; k < 12; ++k) a[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
-    u32 len = 48;
+    len = 48;
 #pragma unroll
     for (int k = 47; k >= 0; --k)
         if (!c_tok((a[k >> 2] >> (8 * (k & 3))) & 0xFFu)) len = (u32)k;
@@ -1673,6 +1688,15 @@ __global__ void k_long_insert(const u8 *__restrict__ buf, u64 seg_end, const u8 
         len = (u32)L;
         h = bytes_hash(src, L, 1);
     }
+    return h;
+}
+__global__ void k_long_insert(const u8 *__restrict__ buf, u64 seg_end, const u8 *__restrict__ extra, u64 extra_len,
+                              const u64 *__restrict__ l_pos, u64 n, u32 *__restrict__ l_len, u64 *__restrict__ l_slot,
+                              u64 *ltab, u64 lmask, u32 *llist, u64 llist_cap, Counters *ctr) {
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    u32 len;
+    const u64 h = long_hash(buf, seg_end, extra, extra_len, l_pos[i], len);
     l_len[i] = len;
     l_slot[i] = h_insert(ltab, lmask, h, 1, i, llist, llist_cap, &ctr->l_claimed, ctr, OVF_LT);
 }

@@ -56,6 +56,40 @@ __device__ __forceinline__ void list_append_wave(bool isnew, u64 slot, u32 *list
     }
 }
 
+// Workgroup-staged list appends: new slots collect in LDS (one LDS add per
+// wave), then stage_flush claims the list range with ONE device add per
+// workgroup.  A full staging area falls back to a device claim per lane.
+__device__ __forceinline__ void stage_new(bool isnew, u64 slot, u32 *staged, u32 *nst, u32 cap, u32 *list,
+                                          u64 list_cap, u64 *claimed, Counters *ctr, u64 ovf_bit) {
+    const u64 B = __ballot(isnew);
+    if (!B) return;
+    const int leader = __ffsll((long long)B) - 1;
+    u32 base = 0;
+    if ((int)lane_id() == leader) base = atomicAdd(nst, (u32)__popcll(B));
+    base = __shfl(base, leader);
+    if (!isnew) return;
+    const u32 at = base + mbcnt(B);
+    if (at < cap) {
+        staged[at] = (u32)slot;
+        return;
+    }
+    const u64 i = atomicAdd((unsigned long long *)claimed, 1ull);
+    if (i < list_cap) list[i] = (u32)slot;
+    else atomicOr((unsigned long long *)&ctr->overflow, (unsigned long long)ovf_bit);
+}
+// after a workgroup barrier that follows every stage_new of the workgroup
+__device__ __forceinline__ void stage_flush(const u32 *staged, const u32 *nst, u32 cap, u64 *gbase, u32 *list,
+                                            u64 list_cap, u64 *claimed, Counters *ctr, u64 ovf_bit) {
+    const u32 m = min(*nst, cap);
+    if (threadIdx.x == 0) *gbase = m ? atomicAdd((unsigned long long *)claimed, (unsigned long long)m) : 0ull;
+    __syncthreads();
+    for (u32 k = threadIdx.x; k < m; k += blockDim.x) {
+        const u64 at = *gbase + k;
+        if (at < list_cap) list[at] = staged[k];
+        else atomicOr((unsigned long long *)&ctr->overflow, (unsigned long long)ovf_bit);
+    }
+}
+
 // S-table insert; claimed slots are appended to `list` (dense, for ranking)
 // unless LIST is false (the main scan: its lists are built afterwards by
 // k_list_build, so new keys do not serialise on one claim counter).
@@ -124,8 +158,13 @@ __device__ __forceinline__ void m_insert(u64 *tab, u64 mask, u64 k0, u64 k1, u64
 
 // H-table insert by 64-bit hash; returns the slot index (or ~0 on overflow).
 // The CAS winner records `rep`; readers only look at rep in a later kernel.
+// LIST false: no list append; *isnew_out tells the caller (k_long_insert
+// stages its new slots per workgroup: a claim per wave on the one counter
+// had serialised at the memory side)
+template <bool LIST = true>
 __device__ __forceinline__ u64 h_insert(u64 *tab, u64 mask, u64 hash, u64 cnt, u64 rep, u32 *list,
-                                        u64 list_cap, u64 *claimed, Counters *ctr, u64 ovf_bit) {
+                                        u64 list_cap, u64 *claimed, Counters *ctr, u64 ovf_bit,
+                                        bool *isnew_out = nullptr) {
     if (hash == 0) hash = 0x8000000000000000ULL;
     u64 h = hash & mask, res = ~0ull;
     bool isnew = false;
@@ -147,7 +186,8 @@ __device__ __forceinline__ u64 h_insert(u64 *tab, u64 mask, u64 hash, u64 cnt, u
         h = (h + 1) & mask;
     }
     if (res == ~0ull) atomicOr((unsigned long long *)&ctr->overflow, (unsigned long long)ovf_bit);
-    list_append_wave(isnew, res, list, list_cap, claimed, ctr, ovf_bit);
+    if (LIST) list_append_wave(isnew, res, list, list_cap, claimed, ctr, ovf_bit);
+    else *isnew_out = isnew;
     return res;
 }
 
@@ -180,8 +220,9 @@ __device__ __forceinline__ u64 akey_hash_bytes(const u8 *p, u64 n, int second) {
 // H-table insert for artist keys with the second hash: sum2 (the sum of h2
 // over the occurrences added) accumulates in the slot's 4th word, so the
 // table can check sum2 == count * h2(rep) afterwards (k_artist_h2_check).
+template <bool LIST = true>
 __device__ __forceinline__ u64 h_insert2(u64 *tab, u64 mask, u64 hash, u64 cnt, u64 rep, u64 sum2, u32 *list,
-                                         u64 list_cap, u64 *claimed, Counters *ctr, u64 ovf_bit) {
+                                         u64 list_cap, u64 *claimed, Counters *ctr, u64 ovf_bit, bool *isnew_out = nullptr) {
     if (hash == 0) hash = 0x8000000000000000ULL;
     u64 h = hash & mask, res = ~0ull;
     bool isnew = false;
@@ -205,7 +246,8 @@ __device__ __forceinline__ u64 h_insert2(u64 *tab, u64 mask, u64 hash, u64 cnt, 
         h = (h + 1) & mask;
     }
     if (res == ~0ull) atomicOr((unsigned long long *)&ctr->overflow, (unsigned long long)ovf_bit);
-    list_append_wave(isnew, res, list, list_cap, claimed, ctr, ovf_bit);
+    if (LIST) list_append_wave(isnew, res, list, list_cap, claimed, ctr, ovf_bit);
+    else *isnew_out = isnew;
     return res;
 }
 
