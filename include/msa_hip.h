@@ -299,7 +299,12 @@ int msa_wcs_set_dialect(msa_wcs *w, int delimiter, int quotechar, int skipinitia
 /* The scripts' --encoding (word_count_per_song.py:63-66,111;
  * split_csv_columns.py:97-101,130): utf8_sig = 1, "utf-8-sig" (default),
  * drops a leading BOM; 0, "utf-8", keeps it as the first field's first
- * character (U+FEFF in the first header name).                             */
+ * character (U+FEFF in the first header name); 2, a single-byte
+ * ASCII-compatible codec (latin-1, cp1252, ...: every byte one character,
+ * decode + encode the identity, so the column splitter's bytes are the
+ * script's; the host decodes the header names and refuses bytes the codec
+ * leaves undefined): no UTF-8 check, no BOM handling; column splitter only
+ * (msa_wcs_run fails with MSA_ERR_ARG).                                    */
 int msa_wcs_set_encoding(msa_wcs *w, int utf8_sig);
 /* log2 of the word-table slots of the next run (0 = sized from the input;
  * the table grows by itself when it fills). */

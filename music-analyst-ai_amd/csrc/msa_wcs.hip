@@ -137,10 +137,17 @@ __device__ __forceinline__ u32 lead_len(u32 b) {
     return b < 0x80 ? 1 : (b < 0xC2 ? 0 : (b < 0xE0 ? 2 : (b < 0xF0 ? 3 : (b < 0xF5 ? 4 : 0))));
 }
 
-__global__ __launch_bounds__(256) void k_wcs_validate(const u8 *__restrict__ buf, u64 n, WCtr *ctr) {
+// utf8 0: a single-byte --encoding (every byte one character): NULs only
+__global__ __launch_bounds__(256) void k_wcs_validate(const u8 *__restrict__ buf, u64 n, WCtr *ctr, u32 utf8) {
     const u64 base = ((u64)blockIdx.x * blockDim.x + threadIdx.x) * 16;
     if (base >= n) return;
     const uint4 v = *(const uint4 *)(buf + base);
+    if (!utf8) {
+        bool nul = false;
+        for (u32 j = 0; j < 16 && base + j < n; ++j) nul |= byte_of(v, j) == 0;
+        if (nul) atomicMin((unsigned long long *)&ctr->err, (unsigned long long)E_NUL);
+        return;
+    }
     // fast path: 16 bytes without NUL of ASCII and whole 2-byte sequences (lead
     // C2..DF, then a continuation byte) -- almost all of a lyrics file
     if (base + 16 <= n && !mask16(v, 0)) {
@@ -1412,6 +1419,7 @@ struct msa_wcs {
     u32 quote = '"';  // quotechar and skipinitialspace (msa_wcs_set_quoting): the column splitter's dialect
     u32 skipsp = 0;
     bool keep_bom = false;  // msa_wcs_set_encoding: "utf-8" keeps a leading BOM as data ("utf-8-sig" drops it)
+    bool one_byte = false;  // msa_wcs_set_encoding 2: a single-byte codec (column splitter only)
     Dia dia() const { return Dia{delim, quote, skipsp}; }
     bool have = false;
     // column splitter results
@@ -1569,9 +1577,11 @@ extern "C" int msa_wcs_set_dialect(msa_wcs *w, int delim, int quotechar, int ski
 // leading BOM; 0 ("utf-8") keeps it as the first field's first character.
 // Invalidates results.
 extern "C" int msa_wcs_set_encoding(msa_wcs *w, int utf8_sig) {
-    if (!w) return MSA_ERR_ARG;
-    if ((utf8_sig == 0) != w->keep_bom) wcs_release_results(w);
-    w->keep_bom = utf8_sig == 0;
+    if (!w || utf8_sig < 0 || utf8_sig > 2) return MSA_ERR_ARG;
+    const bool keep = utf8_sig != 1, one = utf8_sig == 2;
+    if (keep != w->keep_bom || one != w->one_byte) wcs_release_results(w);
+    w->keep_bom = keep;
+    w->one_byte = one;
     return MSA_OK;
 }
 
@@ -1668,7 +1678,7 @@ static int wcs_split_rows(msa_wcs *w, WCtr **ctr_out, u64 *ds_out, u64 *nrows_ou
     WCtr h0{};
     h0.err = ~0ull;
     WCHECK(hipMemcpyAsync(ctr, &h0, sizeof h0, hipMemcpyHostToDevice, st));
-    if (n) hipLaunchKernelGGL(k_wcs_validate, grid1((n + 15) / 16), dim3(256), 0, st, buf, n, ctr);
+    if (n) hipLaunchKernelGGL(k_wcs_validate, grid1((n + 15) / 16), dim3(256), 0, st, buf, n, ctr, w->one_byte ? 0u : 1u);
     // BOM ("utf-8-sig")
     u8 bom[3] = {0, 0, 0};
     if (n >= 3) WCHECK(hipMemcpyAsync(bom, buf, 3, hipMemcpyDeviceToHost, st));
@@ -1729,6 +1739,8 @@ extern "C" int msa_wcs_run(msa_wcs *w) {
     if (!w || !w->d_buf) return MSA_ERR_ARG;
     if (w->quote != '"' || w->skipsp)  // csv.DictReader(fh, delimiter=...): the default dialect otherwise
         return wfail(w, MSA_ERR_ARG, "the per-song counter reads quotechar '\"' without skipinitialspace");
+    if (w->one_byte)  // its tokens are Unicode words of UTF-8 text
+        return wfail(w, MSA_ERR_ARG, "the per-song counter reads UTF-8 only (single-byte encodings: column splitter)");
     WCHECK(hipSetDevice(w->device));
     wcs_release_results(w);
     hipStream_t st = w->stream;

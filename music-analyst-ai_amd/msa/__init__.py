@@ -54,6 +54,48 @@ PIECE_ARTISTS = 1
 SHARD_FN_BYTES = 120  # sizeof(msa_shard_fn)
 
 
+def single_byte_codec(encoding: str):
+    """For an ASCII-compatible single-byte codec (every byte decodes to at most
+    one character, bytes < 0x80 to themselves, and decode + encode is the
+    identity on the bytes it defines): the bytes it leaves undefined (a
+    frozenset, empty for latin-1).  None for any other codec (UTF-8, UTF-16,
+    multi-byte Asian codecs, unknown names)."""
+    import codecs
+
+    try:
+        info = codecs.lookup(encoding)
+    except LookupError:
+        return None
+    if info.name in ("utf-8", "utf-8-sig"):
+        return None
+    bad = set()
+    for b in range(256):
+        try:
+            ch = bytes([b]).decode(info.name)
+        except UnicodeDecodeError:
+            bad.add(b)
+            continue
+        except Exception:
+            return None
+        if len(ch) != 1 or (b < 0x80 and ch != chr(b)):
+            return None
+        try:
+            if ch.encode(info.name) != bytes([b]):
+                return None
+        except Exception:
+            return None
+    if any(b < 0x80 for b in bad):
+        return None
+    for b in bad:  # a byte that only fails alone is a multi-byte lead (Shift-JIS, GBK, ...)
+        for x in range(0x40, 0x100):
+            try:
+                bytes([b, x]).decode(info.name)
+                return None
+            except UnicodeDecodeError:
+                pass
+    return frozenset(bad)
+
+
 class MsaError(RuntimeError):
     def __init__(self, code: int, msg: str):
         super().__init__(f"{MSA_ERR.get(code, code)}: {msg}")
@@ -450,11 +492,17 @@ class WordCountPerSong:
         self._check(self.lib.msa_wcs_set_dialect(self.h, ord(delimiter), ord(quotechar), 1 if skipinitialspace else 0))
 
     def set_encoding(self, encoding: str = "utf-8-sig"):
-        """--encoding: "utf-8-sig" drops a leading BOM, "utf-8" keeps it as data."""
+        """--encoding: "utf-8-sig" drops a leading BOM, "utf-8" keeps it as data;
+        a single-byte ASCII-compatible codec (latin-1, cp1252, ...: see
+        single_byte_codec) reads every byte as one character (the column
+        splitter only)."""
         e = encoding.lower().replace("_", "-")
-        if e not in ("utf-8-sig", "utf-8", "utf8"):
-            raise MsaError(-1, f"only UTF-8 input is implemented on the GPU path, not {encoding!r}")
-        self._check(self.lib.msa_wcs_set_encoding(self.h, 1 if e == "utf-8-sig" else 0))
+        if e in ("utf-8-sig", "utf-8", "utf8"):
+            self._check(self.lib.msa_wcs_set_encoding(self.h, 1 if e == "utf-8-sig" else 0))
+        elif single_byte_codec(encoding) is not None:
+            self._check(self.lib.msa_wcs_set_encoding(self.h, 2))
+        else:
+            raise MsaError(-1, f"only UTF-8 and single-byte ASCII-compatible encodings are implemented, not {encoding!r}")
 
     def count(self):
         self._check(self.lib.msa_wcs_run(self.h))

@@ -13,9 +13,14 @@ csv.Sniffer on the first 65536 characters (msa/sniff.py), ',' when it fails,
 with its skipinitialspace; --quotechar is the reader's and the writer's quote
 character either way.  --encoding utf-8-sig (default) drops a leading BOM and
 writes one at the start of every output file; utf-8 keeps it as the first
-header name's first character and writes none.  The GPU reader takes one-byte
-ASCII delimiters and quotechars other than CR, LF, NUL (and each other);
-other encodings and characters are refused.
+header name's first character and writes none.  A single-byte ASCII-compatible
+codec (latin-1, cp1252, ...; msa.single_byte_codec) reads every byte as one
+character and writes it back unchanged, so the GPU's byte-level split is the
+script's; the header names are decoded and written in that codec, and input
+holding a byte the codec leaves undefined raises the script's
+UnicodeDecodeError.  The GPU reader takes one-byte ASCII delimiters and
+quotechars other than CR, LF, NUL (and each other); multi-byte codecs other
+than UTF-8 (UTF-16, Shift-JIS, ...) and other characters are refused.
 """
 from __future__ import annotations
 
@@ -24,7 +29,7 @@ import re
 from pathlib import Path
 from typing import List, Optional
 
-from . import WordCountPerSong
+from . import WordCountPerSong, single_byte_codec
 from .sniff import detect_csv_params, gpu_supported, read_sample
 
 
@@ -51,8 +56,12 @@ def split_csv_columns(csv_path: str, output_dir: Optional[str] = None, delimiter
     if not in_path.exists():
         raise SystemExit(f"Erro: arquivo não encontrado: {in_path}")
     enc = encoding.lower().replace("_", "-")
-    if enc not in ("utf-8-sig", "utf-8", "utf8"):
-        raise SystemExit("only UTF-8 input is implemented on the GPU path")
+    utf8 = enc in ("utf-8-sig", "utf-8", "utf8")
+    undefined = None if utf8 else single_byte_codec(encoding)
+    if not utf8 and undefined is None:
+        raise SystemExit(f"only UTF-8 and single-byte ASCII-compatible encodings are implemented on the GPU path, "
+                         f"not {encoding!r}")
+    text_enc = "utf-8" if utf8 else encoding  # header names: decoded and written in the file's encoding
     skipinitialspace = False
     if not delimiter:  # detect_csv_params: csv.Sniffer on the script's sample
         delimiter, skipinitialspace = detect_csv_params(read_sample(str(in_path), encoding))
@@ -63,6 +72,11 @@ def split_csv_columns(csv_path: str, output_dir: Optional[str] = None, delimiter
     base_out = Path(output_dir) if output_dir else in_path.with_suffix("").parent / f"{in_path.stem}_columns"
     base_out.mkdir(parents=True, exist_ok=True)
     data = in_path.read_bytes()
+    if undefined:  # bytes the codec leaves undefined: the script's reader raises UnicodeDecodeError
+        import numpy as np
+
+        if np.isin(np.frombuffer(data, np.uint8), np.array(sorted(undefined), np.uint8)).any():
+            data.decode(encoding)
     with WordCountPerSong(device) as w:
         w.set_dialect(delimiter, quotechar, skipinitialspace)
         w.set_encoding(encoding)
@@ -76,7 +90,7 @@ def split_csv_columns(csv_path: str, output_dir: Optional[str] = None, delimiter
         if no_header:
             headers = [f"col{i + 1}" for i in range(ncols)]
         else:
-            raw = [w.column_header(i).decode("utf-8") for i in range(ncols)]
+            raw = [w.column_header(i).decode(text_enc) for i in range(ncols)]
             headers = [h if h.strip() else f"col{i + 1}" for i, h in enumerate(raw)]
         seen, names = set(), []
         for i, h in enumerate(headers, start=1):
@@ -92,7 +106,7 @@ def split_csv_columns(csv_path: str, output_dir: Optional[str] = None, delimiter
             with open(base_out / names[i], "wb") as fh:
                 fh.write(bom)
                 if not no_header:
-                    fh.write(_header_line(headers[i], delimiter, quotechar).encode("utf-8"))
+                    fh.write(_header_line(headers[i], delimiter, quotechar).encode(text_enc))
                 fh.write(w.column_body(i))
     print(f"Concluído. {ncols} arquivo(s) gerado(s) em: {base_out}")
     for name in names:

@@ -9,7 +9,8 @@ main (124-199) for the dialect of detect_csv_params (48-66): the script's
 --delimiter or its csv.Sniffer guess (default ','), the --quotechar (default
 '"'), the sniffed skipinitialspace (False with --delimiter), and the
 --encoding's BOM handling ("utf-8-sig" drops a leading BOM, "utf-8" keeps it
-as the first field's first character):
+as the first field's first character; a single-byte codec such as latin-1
+reads every byte as one character and writes it back unchanged):
 * rows: CPython 3.10 csv.reader (wcs_oracle.csv_rows -- the same _csv state
   machine; blank lines are rows with no fields, csv.reader yields them);
 * columns: len(first row); each later row contributes row[i] or "" (175-178);
@@ -38,9 +39,14 @@ def write_value(v: bytes, delim: bytes = b",", quote: bytes = b'"') -> bytes:
 
 
 def split_columns(data: bytes, has_header: bool = True, delimiter: str = ",", quotechar: str = '"',
-                  skipinitialspace: bool = False, strip_bom: bool = True):
-    """-> (first-row fields, [body bytes of column i]) ; raises WcsError / ValueError("CSV vazio.")."""
-    _utf8_check(data)
+                  skipinitialspace: bool = False, strip_bom: bool = True, utf8: bool = True):
+    """-> (first-row fields, [body bytes of column i]) ; raises WcsError / ValueError("CSV vazio.").
+    utf8 False: a single-byte codec (every byte one character; decode + encode
+    the identity), so the same byte-level split with no UTF-8 check."""
+    if utf8:
+        _utf8_check(data)
+    elif 0 in data:
+        raise WcsError("line contains NUL")
     d, q = delimiter.encode(), quotechar.encode()
     rows = csv_rows(data, ord(delimiter), ord(quotechar), skipinitialspace, strip_bom)
     first = next(rows, None)

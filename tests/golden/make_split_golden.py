@@ -68,6 +68,17 @@ def cases():
     c["utf8_bom"] = (bom + "artist,song\nA,\"x,y\"\n", ["--delimiter", ",", "--encoding", "utf-8"])
     c["utf8_no_bom"] = ("artist,song\nA,\"x,y\"\n", ["--delimiter", ",", "--encoding", "utf-8"])
     c["utf8_bom_sniffed"] = (bom + "a;b;c\n1;2;3\n4;\"5;6\";7\n", ["--encoding", "utf-8"])
+    # single-byte codecs: every byte one character (the input written in that
+    # codec; cases carry bytes)
+    c["latin1_enc"] = ("artista,música,letra\nJosé,\"Ação, é\",\"olá\nmundo ü\"\nÁ,b,\"x\"\"y\"\n".encode("latin-1"),
+                       ["--delimiter", ",", "--encoding", "latin-1"])
+    c["latin1_sniffed"] = ("nome;cidade;nota\nJoão;São Paulo;ótimo\nÉlio;\"Brasília; DF\";bom\n".encode("latin-1"),
+                           ["--encoding", "latin-1"])
+    c["latin1_header_names"] = ("ção,ção,Ç ç,ÿ\n1,2,3,4\n5,6\n".encode("latin-1"),
+                                ["--delimiter", ",", "--encoding", "iso-8859-1"])
+    c["cp1252_enc"] = ("título,preço\n\"Café – 2€\",“aspas”\nx,ƒ\n".encode("cp1252"),
+                       ["--delimiter", ",", "--encoding", "cp1252"])
+    c["err_cp1252_undefined"] = (b"a,b\nx\x81y,z\n", ["--delimiter", ",", "--encoding", "cp1252"])
     return c
 
 
@@ -78,7 +89,7 @@ def main():
     for name, (text, args) in sorted(cases().items()):
         d = os.path.join(OUT, name)
         os.makedirs(d)
-        data = text.encode("utf-8")
+        data = text if isinstance(text, bytes) else text.encode("utf-8")
         with open(os.path.join(d, "input.csv"), "wb") as f:
             f.write(data)
         with open(os.path.join(d, "args.txt"), "w") as f:

@@ -29,8 +29,8 @@ def test_split_golden(msa_mod, name, tmp_path):
     delim = args[args.index("--delimiter") + 1] if "--delimiter" in args else None
     _, quote, _, enc = case_dialect(name, args)
     kw = dict(quotechar=quote, encoding=enc, no_header="--no-header" in args)
-    if exp is None:
-        with pytest.raises((SystemExit, msa_mod.MsaError)):
+    if exp is None:  # UnicodeDecodeError: a byte the single-byte codec leaves undefined, as the script raises
+        with pytest.raises((SystemExit, msa_mod.MsaError, UnicodeDecodeError)):
             split_csv_columns(str(inp), str(od), delim, **kw)
         return
     split_csv_columns(str(inp), str(od), delim, **kw)
@@ -158,3 +158,22 @@ def test_per_song_counter_refuses_other_quoting(msa_mod):
         w.set_quoting("'", False)
         with pytest.raises(msa_mod.MsaError):
             w.run(b"artist,song,text\nA,S,hello world\n")
+
+
+def test_encodings_outside_the_byte_path(msa_mod, tmp_path):
+    """Multi-byte codecs other than UTF-8 are refused by the splitter; a
+    single-byte codec is the splitter's only (the per-song counter's tokens are
+    Unicode words of UTF-8 text)."""
+    from msa import WordCountPerSong
+    from msa.split_columns import split_csv_columns
+
+    inp = tmp_path / "in.csv"
+    inp.write_bytes(b"a,b\n1,2\n")
+    for enc in ("shift_jis", "utf-16", "gbk"):
+        with pytest.raises(SystemExit):
+            split_csv_columns(str(inp), str(tmp_path / enc), ",", encoding=enc)
+    with WordCountPerSong(0) as w:
+        w.set_encoding("latin-1")
+        w.load_csv(b"artist,song,text\na,b,c\n")
+        with pytest.raises(msa_mod.MsaError):
+            w.count()
