@@ -289,6 +289,11 @@ struct msa_ctx {
     hipEvent_t ev_r2_fork = nullptr, ev_r2_join = nullptr;
     // split scan: k_scan_struct done (the spans may start) / the spans done
     hipEvent_t ev_scan_a = nullptr, ev_spans = nullptr;
+    hipEvent_t ev_lb_fork = nullptr, ev_lb_join = nullptr;  // the word lists beside the artist pass
+    // env MSA_LISTS_BESIDE=1: the word lists on rank2 beside the artist pass
+    // (measured neutral: configs[4] 27.31-27.35 vs 27.33-28.09 ms/step, configs[2]
+    // within noise; profiles/r04_t41_*)
+    int lists_beside = 0;
     // text.csv early (beside the token pass): the side stream starts at ev_put
     // (rank2, after the record arrays are final), ev_tscan = its offsets' scan done
     hipEvent_t ev_put = nullptr, ev_tscan = nullptr;
@@ -820,12 +825,13 @@ __global__ void k_put_u64(u64 *p0, u64 v0, u64 *p1, u64 v1) {
 
 // The main scan inserts into the HBM word tables without appending to their
 // slot lists; the lists and claimed counts are built here, once per table.
-static int build_word_lists(msa_ctx *c) {
+static int build_word_lists(msa_ctx *c, hipStream_t st = nullptr) {
     Counters *dc = c->ctr.as<Counters>();
+    if (!st) st = c->stream;
     HIPC(c, msa_launch_list_build(c->s_tab.as<u64>(), c->s_slots, 2, c->s_list.as<u32>(), c->s_slots / 2,
-                                  &dc->s_claimed, dc, (u64)OVF_S, c->stream));
+                                  &dc->s_claimed, dc, (u64)OVF_S, st));
     HIPC(c, msa_launch_list_build(c->m_tab.as<u64>(), c->m_slots, 4, c->m_list.as<u32>(), c->m_slots / 2,
-                                  &dc->m_claimed, dc, (u64)OVF_M, c->stream));
+                                  &dc->m_claimed, dc, (u64)OVF_M, st));
     return MSA_OK;
 }
 
@@ -1213,7 +1219,18 @@ static int split_once(msa_ctx *c, int flags) {
     // one read-back after the scan: the counters (table overflow, long-word
     // occurrences) and -- for the first shard -- the header record's end plus
     // the input's first bytes (the header, almost always)
-    if ((rc = build_word_lists(c))) return rc;
+    // the word tables' slot lists (table scans: streaming) on rank2 beside the
+    // artist pass (LDS tables and atomics) -- both only add to Counters with
+    // atomics; the read-back below waits for both
+    const bool lists_beside = c->lists_beside && !c->artist_exact && c->nrec && !(c->ablate & 32768);
+    if (lists_beside) {
+        HIPC(c, hipEventRecord(c->ev_lb_fork, c->stream));
+        HIPC(c, hipStreamWaitEvent(c->rank2, c->ev_lb_fork, 0));
+        if ((rc = build_word_lists(c, c->rank2))) return rc;
+        HIPC(c, hipEventRecord(c->ev_lb_join, c->rank2));
+    } else if ((rc = build_word_lists(c))) {
+        return rc;
+    }
     // the artist pass of msa_count (lines shortcut) right here, before the
     // read-back: it needs only the split's keys, and its counters come back
     // with the split's -- the text column's gather (launched by msa_count)
@@ -1223,6 +1240,7 @@ static int split_once(msa_ctx *c, int flags) {
         if ((rc = launch_artist_count(c))) return rc;
         c->artist_spec = true;
     }
+    if (lists_beside) HIPC(c, hipStreamWaitEvent(c->stream, c->ev_lb_join, 0));
     HIPC(c, hipMemcpyAsync(c->pin, c->ctr.p, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
     u64 hend = c->n;
     static const u64 kHead = kPinHead;
@@ -1913,6 +1931,7 @@ int msa_create(int device, msa_ctx **out) {
     if (const char *tp = getenv("MSA_TEXT_AT_SPANS")) c->text_at_spans = atoi(tp) != 0;
     if (const char *ta = getenv("MSA_TEXT_AT_AGG")) c->text_at_agg = atoi(ta) != 0;
     if (const char *cs = getenv("MSA_COMP_SORT")) c->comp_sort = atoi(cs) != 0;
+    if (const char *lb = getenv("MSA_LISTS_BESIDE")) c->lists_beside = atoi(lb) != 0;
     if (const char *gm = getenv("MSA_GROW_MUL")) c->grow_mul = std::max(2, std::min(16, atoi(gm)));
     if (const char *gs = getenv("MSA_GROW_STEP")) c->grow_step = (u32)std::max(1, std::min(4, atoi(gs)));
     if (const char *mb = getenv("MSA_MISS_BUCKETS")) c->mb_mode = atoi(mb);
@@ -1937,6 +1956,8 @@ int msa_create(int device, msa_ctx **out) {
         hipEventCreateWithFlags(&c->ev_r2_join, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_scan_a, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_spans, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_lb_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_lb_join, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_put, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_tscan, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fin, hipEventDisableTiming) != hipSuccess ||
@@ -1990,6 +2011,8 @@ void msa_destroy(msa_ctx *c) {
     (void)hipEventDestroy(c->ev_r2_join);
     (void)hipEventDestroy(c->ev_scan_a);
     (void)hipEventDestroy(c->ev_spans);
+    (void)hipEventDestroy(c->ev_lb_fork);
+    (void)hipEventDestroy(c->ev_lb_join);
     (void)hipEventDestroy(c->ev_put);
     (void)hipEventDestroy(c->ev_tscan);
     (void)hipStreamDestroy(c->side);
