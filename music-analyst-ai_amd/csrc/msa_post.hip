@@ -1441,7 +1441,9 @@ __global__ __launch_bounds__(AK_T) void k_artist_key(const u8 *__restrict__ col,
 // count x h2(first record) holds two different keys: reported, never merged
 // silently (k_artist_h2_check does the same for the HBM table).
 #define AC_T 1024
+#ifndef AC_SLOTS
 #define AC_SLOTS 6144
+#endif
 #define AC_PARTS 16       // hash partitions of the flush logs (k_artist_merge)
 #define AC_NB (AC_SLOTS / 4)
 static_assert(AC_SLOTS * 24 + 16 <= 160 * 1024, "artist count LDS exceeds the CU");
