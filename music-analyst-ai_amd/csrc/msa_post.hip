@@ -65,9 +65,13 @@ __global__ void k_scan_zero_totals(ScanJobs js) {
         __hip_atomic_store(js.j[threadIdx.x].total, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// one workgroup of SCAN_TOP_T threads per array (a 256-thread one walked
-// ~200 block sums per thread for configs[4]'s 50 M blob lengths: 104 us)
+// one workgroup per array: SCAN_TOP_T threads for long block-sum arrays
+// (configs[4]'s 50 M blob lengths: 49 K sums), 256 otherwise (a 1024-thread
+// workgroup waited ~70 us for a CU beside the text gather); each thread's
+// run is read 8 loads at a time (one dependent load per element had made the
+// top scan 105 us)
 #define SCAN_TOP_T 1024
+#define SCAN_TOP_BIG 16384
 __global__ __launch_bounds__(SCAN_TOP_T) void k_scan_top(ScanJobs js) {
     const ScanJob &J = js.j[blockIdx.y];
     if (!J.n) {
@@ -75,11 +79,18 @@ __global__ __launch_bounds__(SCAN_TOP_T) void k_scan_top(ScanJobs js) {
         return;
     }
     __shared__ u64 wtot[SCAN_TOP_T / 64];
+    const u32 T = blockDim.x;
     const u64 nb = (J.n + SCAN_TILE - 1) / SCAN_TILE;
-    const u64 per = (nb + SCAN_TOP_T - 1) / SCAN_TOP_T;
+    const u64 per = (nb + T - 1) / T;
     const u64 a = min(nb, (u64)threadIdx.x * per), b = min(nb, a + per);
     u64 s = 0;
-    for (u64 i = a; i < b; ++i) s += J.bsum[i];
+    for (u64 i = a; i < b; i += 8) {
+        u64 x[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) x[k] = i + k < b ? J.bsum[i + k] : 0ull;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s += x[k];
+    }
     const u32 lane = lane_id(), w = threadIdx.x >> 6;
     u64 x = s;  // inclusive wave scan
     for (int o = 1; o < 64; o <<= 1) {
@@ -94,8 +105,18 @@ __global__ __launch_bounds__(SCAN_TOP_T) void k_scan_top(ScanJobs js) {
     // other streams update meanwhile (e.g. the column spans beside the token
     // pass): a write-through store, so no dirty copy of that line stays in
     // this XCD's L2 to be written back over their updates later
-    if (threadIdx.x == SCAN_TOP_T - 1 && J.total) __hip_atomic_store(J.total, acc + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (u64 i = a; i < b; ++i) { const u64 v = J.bsum[i]; J.bsum[i] = acc; acc += v; }
+    if (threadIdx.x == T - 1 && J.total) __hip_atomic_store(J.total, acc + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (u64 i = a; i < b; i += 8) {
+        u64 v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = i + k < b ? J.bsum[i + k] : 0ull;
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            if (i + k < b) {
+                J.bsum[i + k] = acc;
+                acc += v[k];
+            }
+    }
 }
 
 __global__ __launch_bounds__(SCAN_T) void k_scan_down(ScanJobs js) {
@@ -144,7 +165,7 @@ hipError_t msa_exclusive_scan2(const u64 *in, u64 n, u64 *out, u64 *bsum, u64 *t
     }
     const u64 nb = (nmax + SCAN_TILE - 1) / SCAN_TILE;
     hipLaunchKernelGGL(k_scan_reduce, dim3((u32)nb, ny), dim3(SCAN_T), 0, s, js);
-    hipLaunchKernelGGL(k_scan_top, dim3(1, ny), dim3(SCAN_TOP_T), 0, s, js);
+    hipLaunchKernelGGL(k_scan_top, dim3(1, ny), dim3(nb > SCAN_TOP_BIG ? SCAN_TOP_T : SCAN_T), 0, s, js);
     hipLaunchKernelGGL(k_scan_down, dim3((u32)nb, ny), dim3(SCAN_T), 0, s, js);
     return hipGetLastError();
 }
