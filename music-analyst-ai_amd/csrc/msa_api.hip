@@ -1241,6 +1241,14 @@ static int split_once(msa_ctx *c, int flags) {
         c->artist_spec = true;
     }
     if (lists_beside) HIPC(c, hipStreamWaitEvent(c->stream, c->ev_lb_join, 0));
+    // text.csv's gather forked here, ahead of the read-back's copies (it needs
+    // nothing the host reads back): it runs during the copies, the host's
+    // header work and msa_count's launches instead of after them
+    // (MSA_TEXT_AT_SPLIT; otherwise forked by msa_count)
+    if (c->text_deferred && c->text_at_split) {
+        int trc;
+        if ((trc = start_text_side(c))) return trc;
+    }
     HIPC(c, hipMemcpyAsync(c->pin, c->ctr.p, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
     u64 hend = c->n;
     static const u64 kHead = kPinHead;
@@ -1250,14 +1258,6 @@ static int split_once(msa_ctx *c, int flags) {
             HIPC(c, hipMemcpyAsync(c->pin + kPinSmall, c->rec_start.as<u64>() + 1, 8, hipMemcpyDeviceToHost, c->stream));
         if (c->n)
             HIPC(c, hipMemcpyAsync(c->pin + 1024, c->in, std::min<u64>(c->n, kHead), hipMemcpyDeviceToHost, c->stream));
-    }
-    // text.csv's gather forked here, behind the read-back's copies (it needs
-    // nothing the host reads back): it runs during the host's header work and
-    // msa_count's launches instead of after them (MSA_TEXT_AT_SPLIT; otherwise
-    // forked by msa_count)
-    if (c->text_deferred && c->text_at_split) {
-        int trc;
-        if ((trc = start_text_side(c))) return trc;
     }
     HIPC(c, hipStreamSynchronize(c->stream));
     memcpy(&c->h_ctr, c->pin, sizeof(Counters));

@@ -1,5 +1,5 @@
-# round-4 measurement set 5 (after the ranking work): whole GPU suite (timed), smoke, PMC passes (stamped), bench with the CPU leg, kernel trace + timeline
-export TMPDIR=/tmp; D=gpurun_out/r04_final5; mkdir -p $D
+# round-4 measurement set 7 (after the ranking work): whole GPU suite (timed), smoke, PMC passes (stamped), bench with the CPU leg, kernel trace + timeline
+export TMPDIR=/tmp; D=gpurun_out/r04_final7; mkdir -p $D
 s=$(date +%s)
 timeout -k 10 1000 python -u -m pytest tests -m gpu -q --timeout 900 --timeout-method thread > $D/gpu_tests.log 2>&1
 echo "rc=$? seconds=$(( $(date +%s) - s ))" >> $D/gpu_tests.log
