@@ -5,4 +5,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $D/pro
 timeout -k 10 600 python -u bench.py --driver chost --gpus 1 --songs 100000000 --steps 3 --warmup 1 > $D/bench_chost_100m.json 2> $D/bench_chost_100m.err || exit 1
 
 timeout -k 10 300 python -u bench.py --pmc-file profiles/pmc_scan_main.json > $D/bench2.json 2> $D/bench2.err || exit 1
+bash tools/ab_env.sh r04_final8/ab "a:X=1" "b:X=1" "c:X=1" || exit 1
 echo __done__
