@@ -1946,7 +1946,18 @@ int msa_create(int device, msa_ctx **out) {
     }
     // (round 3 measured and removed: the side stream masked off every 8th /
     // 16th CU with hipExtStreamCreateWithCUMask -- no gain)
-    const hipError_t side_e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
+    // text.csv's side stream at the highest priority: its gather is the step's
+    // tail and the ranking beside it has slack (2.88-2.91 vs 2.92-2.96 ms/step,
+    // profiles/r04_t48_ab_side_priority.txt; MSA_SIDE_PRIO=0: default priority)
+    hipError_t side_e;
+    const char *sp = getenv("MSA_SIDE_PRIO");
+    if (!sp || atoi(sp) != 0) {
+        int least = 0, greatest = 0;
+        (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
+        side_e = hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, greatest);
+    } else {
+        side_e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
+    }
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess || side_e != hipSuccess ||
         hipStreamCreateWithFlags(&c->rank2, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
