@@ -244,8 +244,8 @@ int msa_export_copy(msa_ctx *ctx, void *dst);
 int msa_import_partitions(msa_ctx *ctx, int table, const void *src, const uint64_t *blk_off, int nblk);
 /* Root GPU of the final gather: the blocks are every GPU's msa_export_ranked
  * block (ranked, disjoint key partitions); the table's ranking becomes their
- * k-way merge (no re-insertion, no sort; large tables fall back to
- * msa_import_partitions + a ranking of this table).  Replaces, with
+ * k-way merge at any size (each key's global rank = its rank in its own block
+ * + its co-ranks in the others; no re-insertion, no sort).  Replaces, with
  * msa_import_partitions + msa_rank, rank 0's merge + qsort (main 1011-1039).
  * A table merged this way is ranked-only until the next split or partition
  * import: msa_rank keeps its ranking, msa_export_partitions refuses it.     */

@@ -2655,8 +2655,6 @@ extern "C" int msa_debug_stat(msa_ctx *c, const char *name, uint64_t *v) {
     return MSA_OK;
 }
 
-// Not part of include/msa_hip.h: the per-record arrays of the last split
-// (tools/k3_debug.py compares kernel variants with it).
 // Root GPU of the final gather: the received blocks are the GPUs' ranked,
 // disjoint key partitions (msa_export_ranked), merged into this context's
 // ranking of the table by co-rank (csrc/msa_post.hip: k_mr_keys /
@@ -2725,6 +2723,8 @@ int msa_import_ranked(msa_ctx *c, int table, const void *src, const uint64_t *bl
     return MSA_OK;
 }
 
+// Not part of include/msa_hip.h: the per-record arrays of the last split
+// (diagnostics: kernel variants compared record by record).
 extern "C" int msa_debug_records(msa_ctx *c, uint64_t *rec_start, uint32_t *nulrel, uint64_t cap, uint64_t *n) {
     if (!c || !n) return MSA_ERR_ARG;
     HIPC(c, join_side(c));  // text.csv (side stream) may still read the buffers this touches

@@ -28,8 +28,11 @@
 typedef struct msa_shared msa_shared;
 msa_shared *msa_shared_create(int world);
 void msa_shared_destroy(msa_shared *s, int world);
-/* all ranks of the job (process-shared barrier); 0 on success */
+/* all ranks of the job (process-shared barrier); 0 on success, -1 once any
+ * rank has flagged a failure */
 int msa_shared_barrier(msa_shared *s);
+/* flag this job as failed: every rank's current and later barriers return -1 */
+void msa_shared_fail(msa_shared *s);
 /* 128 bytes the ranks share (the rccl transport's ncclUniqueId) */
 unsigned char *msa_shared_blob(msa_shared *s);
 
@@ -77,5 +80,25 @@ void msa_tail_plan(int rank, const uint64_t *heads, const uint64_t *sizes, int w
  * terminated (they may be blocked in a collective).  Returns the first
  * failing rank's exit code, else 0. */
 int msa_spawn_ranks(int world, int (*fn)(int rank, int world, msa_shared *sh, void *arg), void *arg);
+
+/* External launchers: `mpirun -np N prog ...` (MPICH Hydra: PMI_RANK /
+ * PMI_SIZE / PMI_FD; Open MPI: OMPI_COMM_WORLD_RANK / _SIZE) start N unrelated
+ * processes that join as the N ranks of this layer (msa_ranks.c). */
+typedef struct {
+    int rank, world;
+    int local_world;   /* ranks on this node as the launcher states it, -1 if it does not */
+    const char *kind;  /* "hydra" | "openmpi" */
+    int pmi_fd;        /* Hydra's PMI-1 descriptor, -1 without one */
+    char key[160];     /* job key: names the shared block */
+} msa_launch;
+/* 1: started by a launcher (any world size, L filled); 0: not; -1: the
+ * launcher's variables are malformed */
+int msa_launcher_detect(msa_launch *L);
+/* Join the launcher's job (rendezvous in a /dev/shm block keyed by the job;
+ * the PMI handshake under Hydra) and run fn(rank, world, sh, arg) as this
+ * process's rank; a failing rank flags the job so that the others' barriers
+ * return instead of waiting.  Returns fn's exit code (2 if joining failed).
+ * Call before anything touches the GPU. */
+int msa_launcher_run(msa_launch *L, int (*fn)(int rank, int world, msa_shared *sh, void *arg), void *arg);
 
 #endif

@@ -7,6 +7,9 @@
  *   msa_ranks_test exchange N     (N ranks: all-gather, all-to-all-v, barrier)
  *   msa_ranks_test fail N         (rank N-1 fails: the launcher must return its
  *                                  code without hanging the others)
+ *   mpirun -np N msa_ranks_test launched [fail]
+ *                                 (the same checks with N processes an external
+ *                                  launcher started: they join as one job)
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -92,11 +95,20 @@ static int fail_rank(int rank, int world, msa_shared *sh, void *arg) {
     msa_tr *t = msa_tr_shm(sh, rank, world);
     if (rank == world - 1) return 3;  /* dies before the collective */
     unsigned char z = 0, all[MSA_MAX_RANKS];
-    t->allgather(t, &z, 1, all);      /* blocks forever: the launcher must end it */
+    /* must not block forever: the job is flagged as failed (or the forking
+     * launcher ends this rank) */
+    if (t->allgather(t, &z, 1, all)) return 4;
     return 0;
 }
 
 int main(int argc, char **argv) {
+    msa_launch L;
+    const int launched = msa_launcher_detect(&L);
+    if (argc >= 2 && !strcmp(argv[1], "launched")) {  /* under mpirun (or a launcher's environment) */
+        if (launched != 1) { fprintf(stderr, "not started by a launcher (%d)\n", launched); return 1; }
+        if (argc >= 3 && !strcmp(argv[2], "fail")) return msa_launcher_run(&L, fail_rank, NULL);
+        return msa_launcher_run(&L, exchange_rank, NULL);
+    }
     if (argc >= 2 && !strcmp(argv[1], "routing")) return routing();
     if (argc >= 3 && !strcmp(argv[1], "exchange")) return msa_spawn_ranks(atoi(argv[2]), exchange_rank, NULL);
     if (argc >= 3 && !strcmp(argv[1], "fail")) {

@@ -13,8 +13,9 @@
  * own results change with -np: its byte split loses or double-counts records
  * at the cut points; here every record is counted once).
  *
- * --processes N (N > 1): one process per GPU (GPUs D .. D+N-1), the rank layer
- * of msa_ranks.h in place of MPI.  Rank r reads bytes [r*n/N, (r+1)*n/N) of
+ * --processes N (N > 1), or N processes started by `mpirun -np N` (Hydra or
+ * Open MPI, as the reference is launched): one process per GPU (GPUs
+ * D .. D+N-1), the rank layer of msa_ranks.h in place of MPI.  Rank r reads bytes [r*n/N, (r+1)*n/N) of
  * the file, the ranks agree on exact record boundaries (shard transfer
  * functions, all-gathered), move the bytes of cut records to the rank where
  * they begin, split and count locally, merge the count tables by key-hash
@@ -538,7 +539,17 @@ static int rank_main(int rank, int world, msa_shared *sh, void *arg) {
 }
 
 int main(int argc, char **argv) {
+    /* under `mpirun -np N` (the reference's launch, run_performance.sh:23)
+     * this process is one of N ranks of one job */
+    msa_launch L;
+    const int launched = msa_launcher_detect(&L);
+    if (launched < 0) {
+        fprintf(stderr, "malformed MPI launcher environment (PMI_RANK/PMI_SIZE or OMPI_COMM_WORLD_RANK/SIZE)\n");
+        return EXIT_FAILURE;
+    }
+    const int quiet = launched && L.rank != 0; /* messages once per job, as the reference's rank 0 */
     if (argc < 2) {
+        if (quiet) return EXIT_FAILURE;
         fprintf(stderr,
                 "Usage: %s <dataset.csv> [--word-limit N] [--artist-limit N] [--output-dir DIR] [--device D] "
                 "[--processes N]\n",
@@ -562,7 +573,11 @@ int main(int argc, char **argv) {
         else if (!strcmp(argv[i], "--synthetic-songs") && i + 1 < argc) o.synth_songs = strtoull(argv[++i], NULL, 10);
         else if (!strcmp(argv[i], "--bench-steps") && i + 1 < argc) o.bench_steps = atoi(argv[++i]);
         else if (!strcmp(argv[i], "--bench-warmup") && i + 1 < argc) o.bench_warmup = atoi(argv[++i]);
-        else fprintf(stderr, "Ignoring unknown argument: %s\n", argv[i]);
+        else if (!quiet) fprintf(stderr, "Ignoring unknown argument: %s\n", argv[i]);
+    }
+    if (launched && L.world > 1 && o.processes != 1) {
+        if (!quiet) fprintf(stderr, "--processes cannot be combined with the launcher's %d processes\n", L.world);
+        return EXIT_FAILURE;
     }
     if (o.processes < 1 || o.processes > MSA_MAX_RANKS) {
         fprintf(stderr, "--processes must be in 1..%d\n", MSA_MAX_RANKS);
@@ -585,6 +600,7 @@ int main(int argc, char **argv) {
         fprintf(stderr, "--bench-steps needs --synthetic-songs\n");
         return EXIT_FAILURE;
     }
+    if (launched && L.world > 1) return msa_launcher_run(&L, rank_main, &o);
     if (o.processes == 1 && !(rp && rp[0] == '1') && o.bench_steps <= 0) return run_single(&o);
     /* fork the ranks before anything initialises the GPU in this process */
     return msa_spawn_ranks(o.processes, rank_main, &o);

@@ -134,3 +134,48 @@ def test_cli_bench_mode(msa_mod, procs, transport, tmp_path):
     assert res["driver"] == "chost" and res["ranks"] == procs and res["steps"] == 2
     assert res["bytes_total"] == len(msa_mod.gen_corpus(songs, mode="zipf", seed=1))
     assert res["stages"]["csv_scan"][1] == 2 and res["seconds"] > 0
+
+
+# ------------------------------------------------------------- under mpirun
+# The reference is launched as `mpirun -np N ./bin/parallel_spotify <csv>`
+# (scripts/run_performance.sh:23).  The drop-in run the same way joins the N
+# processes as one job (host/msa_ranks.c msa_launcher_run): the np=1 results,
+# written once, with "processes": N.
+MPIRUN = "/opt/conda/bin/mpirun"
+
+
+def _no_launcher_env():
+    return {k: v for k, v in os.environ.items()
+            if not k.startswith(("PMI_", "OMPI_", "PMIX_", "MPI_LOCAL", "HYDRA"))}
+
+
+@pytest.mark.skipif(not os.path.exists(MPIRUN), reason="no mpirun in this image")
+@pytest.mark.parametrize("case,np_", [("zipf_small", 2), ("zipf_small", 4), ("torture_17", 4), ("torture_3", 2),
+                                      ("multiline_artist_header", 2), ("highcard_small", 4), ("nul_bytes", 2),
+                                      ("header_only", 2)])
+def test_cli_under_mpirun_matches_single(case, np_, tmp_path):
+    if case not in CASES:
+        pytest.skip(f"no golden case {case}")
+    res, files = golden(case, 1)
+    out = tmp_path / "out"
+    p = subprocess.run([MPIRUN, "-np", str(np_), CLI, os.path.join(GOLDEN, case, "input.csv"),
+                        "--output-dir", str(out)], capture_output=True, timeout=180, env=_no_launcher_env())
+    assert p.returncode == 0, p.stderr
+    got = read_outputs(str(out))
+    assert got["metrics"] == {"processes": np_, "total_songs": res["total_songs"], "total_words": res["total_words"]}
+    assert got["word_counts.csv"] == files["word_counts.csv"]
+    assert got["top_artists.csv"] == files["top_artists.csv"]
+    assert got["split"] == files["split"]
+    assert p.stdout.decode("latin-1") == res["stdout"]
+
+
+@pytest.mark.skipif(not os.path.exists(MPIRUN), reason="no mpirun in this image")
+@pytest.mark.parametrize("case,msg", [("empty_file", b"Dataset does not contain a header row"),
+                                      ("bad_header", b"Unable to parse dataset header")])
+def test_cli_under_mpirun_errors(case, msg, tmp_path):
+    """A rank that fails ends the job (mpirun itself leaves the others running)."""
+    p = subprocess.run([MPIRUN, "-np", "2", CLI, os.path.join(GOLDEN, case, "input.csv"),
+                        "--output-dir", str(tmp_path / "o")], capture_output=True, timeout=120,
+                       env=_no_launcher_env())
+    assert p.returncode != 0
+    assert msg in p.stderr

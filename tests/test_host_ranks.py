@@ -38,3 +38,93 @@ def test_failed_rank_ends_the_job(ranks_bin, world):
     the launcher) waiting forever: the launcher returns its exit code."""
     p = subprocess.run([ranks_bin, "fail", str(world)], capture_output=True, timeout=60)
     assert p.returncode == 0, p.stderr
+
+
+MPIRUN = "/opt/conda/bin/mpirun"
+needs_mpirun = pytest.mark.skipif(not os.path.exists(MPIRUN), reason="no MPICH Hydra mpirun in this image")
+
+
+def _no_launcher_env():
+    return {k: v for k, v in os.environ.items()
+            if not k.startswith(("PMI_", "OMPI_", "PMIX_", "MPI_LOCAL", "HYDRA"))}
+
+
+def _shm_leftovers():
+    return sorted(f for f in os.listdir("/dev/shm") if f.startswith("msa_"))
+
+
+@needs_mpirun
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_mpirun_ranks_join_one_job(ranks_bin, world, tmp_path):
+    """`mpirun -np N` (Hydra, the reference's launcher: run_performance.sh:23)
+    starts N unrelated processes; they join as one job over PMI-1 and a
+    /dev/shm block and run the same all-gather / all-to-all-v checks as the
+    forked ranks."""
+    before = _shm_leftovers()
+    p = subprocess.run([MPIRUN, "-np", str(world), ranks_bin, "launched"], capture_output=True, timeout=120,
+                       cwd=tmp_path, env=_no_launcher_env())
+    assert p.returncode == 0, p.stderr
+    assert _shm_leftovers() == before
+
+
+@needs_mpirun
+def test_mpirun_failed_rank_ends_the_job(ranks_bin, tmp_path):
+    """mpirun does not end the other processes when one exits with an error:
+    the failing rank flags the job and the others leave their barriers."""
+    before = _shm_leftovers()
+    p = subprocess.run([MPIRUN, "-np", "3", ranks_bin, "launched", "fail"], capture_output=True, timeout=120,
+                       cwd=tmp_path, env=_no_launcher_env())
+    assert p.returncode != 0
+    assert _shm_leftovers() == before
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_openmpi_environment_ranks_join(ranks_bin, world, tmp_path):
+    """Open MPI's variables (OMPI_COMM_WORLD_RANK/SIZE, PMIX_NAMESPACE) and no
+    PMI descriptor: the ranks poll for the block rank 0 publishes.  Rank 0 is
+    started last, so the others really wait for it."""
+    env = _no_launcher_env()
+    ns = f"msa-test-{os.getpid()}-{world}"
+    procs = []
+    for r in list(range(1, world)) + [0]:
+        e = dict(env, OMPI_COMM_WORLD_RANK=str(r), OMPI_COMM_WORLD_SIZE=str(world),
+                 OMPI_COMM_WORLD_LOCAL_SIZE=str(world), PMIX_NAMESPACE=ns)
+        procs.append(subprocess.Popen([ranks_bin, "launched"], env=e, cwd=tmp_path,
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE))
+    for p in procs:
+        out, err = p.communicate(timeout=120)
+        assert p.returncode == 0, err
+    assert not any(ns.replace("-", "_") in f or ns in f for f in _shm_leftovers())
+
+
+def test_launcher_spanning_nodes_is_refused(ranks_bin, tmp_path):
+    """The shared block is node-local: a job whose ranks are not all on this
+    node is refused, not silently split into per-node jobs."""
+    e = dict(_no_launcher_env(), OMPI_COMM_WORLD_RANK="0", OMPI_COMM_WORLD_SIZE="4",
+             OMPI_COMM_WORLD_LOCAL_SIZE="2", PMIX_NAMESPACE=f"msa-span-{os.getpid()}")
+    p = subprocess.run([ranks_bin, "launched"], env=e, capture_output=True, timeout=60, cwd=tmp_path)
+    assert p.returncode != 0 and b"more than one node" in p.stderr
+
+
+@needs_mpirun
+def test_mpirun_cli_without_gpu_fails_cleanly(tmp_path):
+    """bin/parallel_spotify under mpirun on a host without a GPU: every rank
+    fails (no device) and the job ends with an error instead of hanging or
+    writing partial outputs; --processes next to the launcher's ranks is
+    refused."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible: the CLI runs (tests/test_gpu_cli.py)")
+    cli = os.path.join(PKG, "bin", "parallel_spotify")
+    if not os.path.exists(cli):
+        pytest.skip("CLI not built")
+    csv = tmp_path / "in.csv"
+    csv.write_bytes(b"artist,song,link,text\nA,s,l,\"hello world\"\n")
+    env = _no_launcher_env()
+    p = subprocess.run([MPIRUN, "-np", "2", cli, str(csv), "--output-dir", str(tmp_path / "o")],
+                       capture_output=True, timeout=120, env=env)
+    assert p.returncode != 0
+    assert not (tmp_path / "o" / "word_counts.csv").exists()
+    p = subprocess.run([MPIRUN, "-np", "2", cli, str(csv), "--processes", "2", "--output-dir", str(tmp_path / "o")],
+                       capture_output=True, timeout=120, env=env)
+    assert p.returncode != 0 and b"--processes cannot be combined" in p.stderr
