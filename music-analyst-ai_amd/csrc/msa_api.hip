@@ -32,10 +32,6 @@ hipError_t msa_launch_miss_buckets(const ScanArgs &, u64 *, u64 *, u64 *, u64 *,
 hipError_t msa_exclusive_scan(const u64 *, u64, u64 *, u64 *, u64 *, hipStream_t);
 hipError_t msa_exclusive_scan2(const u64 *, u64, u64 *, u64 *, u64 *, const u64 *, u64, u64 *, u64 *, u64 *,
                                hipStream_t);
-hipError_t msa_launch_rec_text(const u8 *, const u64 *, const u32 *, const u64 *, const u64 *, u64, u64, u64 *, u64 *,
-                               u32 *, Counters *, hipStream_t);
-hipError_t msa_launch_text_gather_w(const u8 *, const u64 *, const u64 *, const u64 *, const u32 *, u64, u64,
-                                    const u64 *, u8 *, hipStream_t);
 hipError_t msa_launch_rec_spans(const u8 *, const u64 *, const u32 *, u64, u64, int, u64 *, u64 *, u32 *, u64 *, u64 *,
                                 u32 *, Counters *, const AKeys &, const u64 *, const u64 *, const u64 *, u64 *, int,
                                 hipStream_t);
@@ -212,7 +208,11 @@ struct msa_ctx {
     // columns
     DevBuf acol, alen, aoff, asrc, apairs, tcol, tlen, toff, tsrc, tpairs, scan_bsum, scan_total, tscan_bsum;
     int cus = 256;
-    int ablate = 0;  // MSA_ABLATE: diagnostic kernel ablations (results invalid)
+#ifdef MSA_DIAG
+    int ablate = 0;  // env MSA_ABLATE (diagnostic builds only, make variant): kernel ablations, results invalid
+#else
+    static constexpr int ablate = 0;  // the product library has no ablation switch
+#endif
     int sort_mode = 0;  // MSA_SORT: 0 by size, 1 merge sort, 2 radix sort
     // radix sort + tie refinement scratch, one set per concurrently ranked
     // table (rb[1]: the artists on their own host thread and stream)
@@ -252,7 +252,6 @@ struct msa_ctx {
     u64 mb_min = 24000000;
     u64 mb_prev = 0;     // the last split's logged misses
     DevBuf lmask;         // the split scan's lyric token-byte mask (k_scan_struct -> k_scan_tokens)
-    int k3split = 1;      // MSA_K3SPLIT=0: the fused k_scan_csv instead (A/B runs)
     u64 s_slots = 0, m_slots = 0, l_occ_cap = 0, lt_slots = 0, a_slots = 0;
     u64 s_used_prev = 0, m_used_prev = 0, lt_used_prev = 0, a_used_prev = 0;
     // Table capacities (log2 slots / occurrence capacity).  They start small --
@@ -281,37 +280,14 @@ struct msa_ctx {
     // the artist table is ranked on a stream of its own beside the word table
     // (both small-table sorts are launch/latency-bound chains)
     hipStream_t rank2 = nullptr;
-    // artist.csv beside the ranking (env MSA_AUX_COL=0: on the library stream)
+    // artist.csv beside the ranking
     hipStream_t aux = nullptr;
     hipEvent_t ev_aux_fork = nullptr, ev_aux_join = nullptr;
     bool aux_pending = false;
-    int aux_col = 1;
     hipEvent_t ev_r2_fork = nullptr, ev_r2_join = nullptr;
     // split scan: k_scan_struct done (the spans may start) / the spans done
     hipEvent_t ev_scan_a = nullptr, ev_spans = nullptr;
-    hipEvent_t ev_lb_fork = nullptr, ev_lb_join = nullptr;  // the word lists beside the artist pass
-    // env MSA_LISTS_BESIDE=1: the word lists on rank2 beside the artist pass
-    // (measured neutral: configs[4] 27.31-27.35 vs 27.33-28.09 ms/step, configs[2]
-    // within noise; profiles/r04_t41_*)
-    int lists_beside = 0;
-    // text.csv early (beside the token pass): the side stream starts at ev_put
-    // (rank2, after the record arrays are final), ev_tscan = its offsets' scan done
-    hipEvent_t ev_put = nullptr, ev_tscan = nullptr;
-    // env MSA_EARLY_TEXT=1: text.csv gathered beside the token pass (measured
-    // and rejected: the token pass's neighbours and k_miss_agg slowed down more
-    // than the deferred gather costs, 3.55 vs 3.05 ms/step)
-    int early_text = 0;
-    int gather_w = 0;  // env MSA_GATHER_W=1: the deferred text.csv with the LDS-free gather (A/B)
-    int sort_k0 = 0;   // env MSA_SORT_K0=1: the words' radix sort covers key bytes 8..15 too
-    int text_at_split = 1;  // env MSA_TEXT_AT_SPLIT=0: text.csv's gather forked by msa_count
     int comp_sort = 1;      // env MSA_COMP_SORT=0: the words' radix sort by K2 and K1 (no composite key)
-    u64 grow_mul = 4;       // env MSA_GROW_MUL: a grown table has >= this many slots per key the failed run claimed
-    u32 grow_step = 3;      // env MSA_GROW_STEP: ... and at least 2^step times the slots it had
-    // env MSA_TEXT_AT_SPANS=1: text.csv's gather forked from the spans' stream
-    // (measured and rejected: it slowed the artist pass beside it, 0.13 -> 0.51
-    // ms, 2.97-3.00 vs 2.92-2.95 ms/step; profiles/r04_t28_ab_text_at_spans.txt)
-    int text_at_spans = 0;
-    int text_at_agg = 0;  // env MSA_TEXT_AT_AGG=1: forked behind the miss aggregation (A/B)
     // the K2 final-state read-back (launch_scan_fn / wait_scan_fn)
     hipEvent_t ev_fin = nullptr;
     State fin_init{};
@@ -660,9 +636,12 @@ static int ensure_tables(msa_ctx *c) {
 // stage that is retried.
 static void grow_tables(msa_ctx *c, u64 mask = ~0ull) {
     const u64 f = c->h_ctr.overflow & mask;
-    const u64 mul = c->grow_mul;
-    const u32 step = c->grow_step;
-    auto grow = [mul, step](u32 &lg, u64 claimed) {
+    // a grown table has >= 4 slots per key the failed run claimed and at
+    // least 8 times the slots it had (2 slots per key in one step measured: no
+    // change)
+    constexpr u64 mul = 4;
+    constexpr u32 step = 3;
+    auto grow = [](u32 &lg, u64 claimed) {
         const u32 want = log2_ceil(std::max<u64>(claimed * mul, 1));
         lg = std::max<u32>(lg + step, want);
         if (lg > 31) lg = 31;  // slot lists hold u32 indices
@@ -790,13 +769,7 @@ static int launch_text(msa_ctx *c, hipStream_t st) {
     int rc;
     c->text_deferred = false;
     prof_begin(c, ST_TEXT_COLUMN, st);
-    if (c->gather_w) {  // A/B: the LDS-free gather (k_col_gather_w)
-        HIPC(c, msa_launch_text_gather_w(c->in, c->tlen.as<u64>(), c->toff.as<u64>(), c->tsrc.as<u64>(),
-                                         c->tpairs.as<u32>(), c->nrec, kColHdrRoom,
-                                         &c->ctr.as<Counters>()->col_body[1], c->tcol.as<u8>(), st));
-    } else if ((rc = materialise_column(c, true, kColHdrRoom, c->tcol, c->tlen, c->toff, c->tsrc, c->tpairs, st))) {
-        return rc;
-    }
+    if ((rc = materialise_column(c, true, kColHdrRoom, c->tcol, c->tlen, c->toff, c->tsrc, c->tpairs, st))) return rc;
     prof_end(c, ST_TEXT_COLUMN, c->n * 2 + c->nrec * 40, st);  // ~ the text column read + written
     return MSA_OK;
 }
@@ -870,37 +843,6 @@ static int launch_spans(msa_ctx *c, bool want_text, hipStream_t st) {
                                  c->span_fix.as<u64>(), c->ablate, st));
     if ((rc = scan_columns(c, want_text, st))) return rc;
     prof_end(c, ST_REC_SPANS, nrec * 136, st);  // ~36 B read + 100 B written per record
-    return MSA_OK;
-}
-
-// text.csv's body on the side stream as soon as the record arrays are final:
-// its line spans (k_rec_text), their offsets' scan (the body length into
-// Counters::col_body[1]; the library stream waits for it at ev_tscan before
-// the split's counter read-back) and the LDS-free gather, which fits beside
-// the token pass and the miss aggregation (both hold every CU's LDS) -- the
-// deferred gather had been the step's tail, after the artist pass.
-static int launch_text_early(msa_ctx *c) {
-    const u64 nrec = c->nrec;
-    HIPC(c, ensure(c->tcol, kColHdrRoom + c->n + 1 + MSA_INPUT_PAD));
-    HIPC(c, ensure(c->tlen, nrec * 8));
-    HIPC(c, ensure(c->tsrc, nrec * 8));
-    HIPC(c, ensure(c->tpairs, nrec * 4));
-    HIPC(c, ensure(c->toff, nrec * 8));
-    HIPC(c, ensure(c->tscan_bsum, ((nrec + 1023) / 1024 + 1) * 8));
-    HIPC(c, hipStreamWaitEvent(c->side, c->ev_put, 0));
-    prof_begin(c, ST_TEXT_COLUMN, c->side);
-    u64 *body = &c->ctr.as<Counters>()->col_body[1];
-    HIPC(c, msa_launch_rec_text(c->in, c->rec_start.as<u64>(), c->nulrel.as<u32>(), c->tss.as<u64>(),
-                                c->tse.as<u64>(), nrec, c->cont ? 0 : 1, c->tlen.as<u64>(), c->tsrc.as<u64>(),
-                                c->tpairs.as<u32>(), c->ctr.as<Counters>(), c->side));
-    HIPC(c, msa_exclusive_scan(c->tlen.as<u64>(), nrec, c->toff.as<u64>(), c->tscan_bsum.as<u64>(), body, c->side));
-    HIPC(c, hipEventRecord(c->ev_tscan, c->side));
-    HIPC(c, msa_launch_text_gather_w(c->in, c->tlen.as<u64>(), c->toff.as<u64>(), c->tsrc.as<u64>(),
-                                     c->tpairs.as<u32>(), nrec, kColHdrRoom, body, c->tcol.as<u8>(), c->side));
-    prof_end(c, ST_TEXT_COLUMN, c->n * 2 + c->nrec * 40, c->side);
-    HIPC(c, hipEventRecord(c->ev_join, c->side));
-    c->side_pending = true;
-    c->text_deferred = false;
     return MSA_OK;
 }
 
@@ -1074,7 +1016,7 @@ static int split_once(msa_ctx *c, int flags) {
         a.f0 = c->f0.as<u64>();
         a.tss = c->tss.as<u64>();
         a.tse = c->tse.as<u64>();
-        c->spans = !(c->ablate & 64);  // the round-1 kernel records no spans
+        c->spans = true;
         a.s_tab = c->s_tab.as<u64>();
         a.s_mask = c->s_slots - 1;
         a.s_list = c->s_list.as<u32>();
@@ -1090,20 +1032,22 @@ static int split_once(msa_ctx *c, int flags) {
         a.ablate = c->ablate;
         a.first_rec = c->cont ? 0 : 1;
         {  // miss logs: room for about a quarter of the tokens, or for what the last
-           // split logged (a full partition falls back to an HBM insert per entry)
+           // split logged (a full partition drops its further entries and flags
+           // OVF_MLOG: the split runs again with larger logs; past the 2^24-entry
+           // partition limit the token pass inserts them into HBM instead)
             const u64 parts = (u64)c->cus * MSA_MLOG_PARTS;
             u64 entries = std::max<u64>(std::max<u64>(parts * 1024, c->n / 16), c->mlog_want);
             if (c->mlog_test) entries = std::max<u64>(c->mlog_test, c->mlog_want);  // tests: small first logs
             // (a workgroup's 16 partitions are addressed with 32-bit byte offsets)
             a.mlog_cap = (u32)std::min<u64>(entries / parts, (1u << 24) - 1);
+            a.mlog_direct = entries / parts > a.mlog_cap;  // growing them further is impossible
             c->mlog_cap_last = a.mlog_cap;
             HIPC(c, ensure(c->mlog, parts * a.mlog_cap * 16));
             HIPC(c, ensure(c->mlog_n, parts * 4));
             a.mlog = c->mlog.as<ulonglong2>();
             a.mlog_n = c->mlog_n.as<u32>();
         }
-        a.split = c->k3split;
-        if (a.split) {  // a word per 64 bytes of every 4 KiB block, behind one zero word
+        {  // a word per 64 bytes of every 4 KiB block, behind one zero word
             const u64 words = (c->n + 4095) / 4096 * 64 + 2;
             if (c->lmask.cap < words * 8) {
                 HIPC(c, ensure(c->lmask, words * 8));
@@ -1112,15 +1056,12 @@ static int split_once(msa_ctx *c, int flags) {
             a.lmask = c->lmask.as<u64>();
         }
         prof_begin(c, ST_CSV_SCAN);
-        // k_scan_csv / k_scan_struct (msa_k3.hip); MSA_ABLATE bit 64 selects the round-1 kernel (A/B runs)
-        if (c->ablate & 64) HIPC(c, msa_launch_scan(a, 0, c->stream));
-        else HIPC(c, msa_launch_scan_csv(a, c->stream));
+        HIPC(c, msa_launch_scan_csv(a, c->stream));  // k_scan_struct (msa_k3.hip)
         // algorithmic bytes: every CSV byte once + the per-record SoA it writes
         // (rec_start 8, nulrel 4 with the text column, the span events f0 / tss / tse 24)
         // + the split scan's token-byte mask (1 bit per byte)
-        prof_end(c, ST_CSV_SCAN, c->n + c->nrec * ((want_text ? 12ull : 8ull) + (c->spans ? 24ull : 0ull)) +
-                                     (a.split ? c->n / 8 : 0));
-        if (a.split && !(c->ablate & 64)) {
+        prof_end(c, ST_CSV_SCAN, c->n + c->nrec * ((want_text ? 12ull : 8ull) + 24ull) + c->n / 8);
+        {
             HIPC(c, hipEventRecord(c->ev_scan_a, c->stream));  // the record arrays are final
             prof_begin(c, ST_CSV_TOKENS);
             HIPC(c, msa_launch_scan_tokens(a, c->stream));
@@ -1157,13 +1098,13 @@ static int split_once(msa_ctx *c, int flags) {
     // k_scan_tokens (whose one workgroup per CU leaves wave slots free) and
     // k_miss_agg.  (The fused scan: k_miss_agg measured beside k_rec_fast on
     // rank2 -- both kernels took twice as long, no gain.)
-    const bool spans_beside = a.split && !(c->ablate & 64) && !(c->ablate & 8192);
+    const bool spans_beside = !(c->ablate & 8192);
     hipStream_t sst = c->stream;
     if (spans_beside) {
         sst = c->rank2;
         HIPC(c, hipStreamWaitEvent(c->rank2, c->ev_scan_a, 0));
     }
-    if (!(c->ablate & 64)) {
+    {
         prof_begin(c, ST_MISS_AGG);
         // high cardinality (the last split's logs held far more distinct keys
         // than the aggregating workgroups' LDS tables): bucketed first
@@ -1189,32 +1130,14 @@ static int split_once(msa_ctx *c, int flags) {
                            c->tse.as<u64>() + c->nrec - 1, (u64)SPAN_FIX);
         HIPC(c, hipGetLastError());
     }
-    const bool early = want_text && spans_beside && c->early_text;
-    if (early) {
-        HIPC(c, hipEventRecord(c->ev_put, c->rank2));  // the record arrays (and the put above) are final
-        if ((rc = launch_text_early(c))) return rc;
-    }
-    if ((rc = launch_spans(c, want_text && !early, sst))) return rc;
+    if ((rc = launch_spans(c, want_text, sst))) return rc;
     if (spans_beside) {
         HIPC(c, hipEventRecord(c->ev_spans, c->rank2));
         HIPC(c, hipStreamWaitEvent(c->stream, c->ev_spans, 0));
     }
-    if (early) HIPC(c, hipStreamWaitEvent(c->stream, c->ev_tscan, 0));  // col_body[1] before the read-back
-    if (want_text && !early) {  // text.csv's body: deferred (msa_ctx::text_deferred)
+    if (want_text) {  // text.csv's body: deferred (msa_ctx::text_deferred)
         HIPC(c, ensure(c->tcol, kColHdrRoom + c->n + 1 + MSA_INPUT_PAD));
         c->text_deferred = true;
-        // forked from the spans' stream as soon as they are final (rank2 was
-        // ordered after this split's prologue; the gather reads only the input,
-        // the spans and the body length the spans' scan wrote), not behind the
-        // miss aggregation, the artist pass and the read-back's copies
-        if (spans_beside && c->text_at_spans) {
-            HIPC(c, hipStreamWaitEvent(c->side, c->ev_spans, 0));
-            if ((rc = launch_text(c, c->side))) return rc;
-            HIPC(c, hipEventRecord(c->ev_join, c->side));
-            c->side_pending = true;
-        } else if (c->text_at_agg) {  // A/B: forked behind the aggregation (and the spans), before the artist pass
-            if ((rc = start_text_side(c))) return rc;
-        }
     }
     // one read-back after the scan: the counters (table overflow, long-word
     // occurrences) and -- for the first shard -- the header record's end plus
@@ -1222,15 +1145,8 @@ static int split_once(msa_ctx *c, int flags) {
     // the word tables' slot lists (table scans: streaming) on rank2 beside the
     // artist pass (LDS tables and atomics) -- both only add to Counters with
     // atomics; the read-back below waits for both
-    const bool lists_beside = c->lists_beside && !c->artist_exact && c->nrec && !(c->ablate & 32768);
-    if (lists_beside) {
-        HIPC(c, hipEventRecord(c->ev_lb_fork, c->stream));
-        HIPC(c, hipStreamWaitEvent(c->rank2, c->ev_lb_fork, 0));
-        if ((rc = build_word_lists(c, c->rank2))) return rc;
-        HIPC(c, hipEventRecord(c->ev_lb_join, c->rank2));
-    } else if ((rc = build_word_lists(c))) {
-        return rc;
-    }
+    // (measured neutral on rank2 beside the artist pass, profiles/r04_t41_*)
+    if ((rc = build_word_lists(c))) return rc;
     // the artist pass of msa_count (lines shortcut) right here, before the
     // read-back: it needs only the split's keys, and its counters come back
     // with the split's -- the text column's gather (launched by msa_count)
@@ -1240,12 +1156,10 @@ static int split_once(msa_ctx *c, int flags) {
         if ((rc = launch_artist_count(c))) return rc;
         c->artist_spec = true;
     }
-    if (lists_beside) HIPC(c, hipStreamWaitEvent(c->stream, c->ev_lb_join, 0));
     // text.csv's gather forked here, ahead of the read-back's copies (it needs
     // nothing the host reads back): it runs during the copies, the host's
     // header work and msa_count's launches instead of after them
-    // (MSA_TEXT_AT_SPLIT; otherwise forked by msa_count)
-    if (c->text_deferred && c->text_at_split) {
+    if (c->text_deferred) {
         int trc;
         if ((trc = start_text_side(c))) return trc;
     }
@@ -1441,7 +1355,7 @@ static int do_count(msa_ctx *c) {
                 if ((rc = start_text_side(c))) return rc;  // text.csv beside this read-back and the ranking
                 launch_long_words(c, nl);
                 long_ran = true;
-                HIPC(c, launch_artist_col(c, c->aux_col));   // artist.csv beside text.csv and the ranking
+                HIPC(c, launch_artist_col(c, true));   // artist.csv beside text.csv and the ranking
             }
             if ((rc = sync_counters(c))) return rc;
             long_ok = attempt == 0;
@@ -1667,7 +1581,10 @@ static int sort_and_blob(msa_ctx *c, Ranked &R, const u8 *wbuf, const u8 *wextra
         // refinement -- equal (count, first 8 bytes) runs are rare in a word
         // table, so a round over them is cheaper than 8 passes over all entries
         // (artists: prefixes shared by many names; MSA_SORT_K0=1 sorts K0 for words too)
-        const bool sk0 = slot != 0 || c->sort_k0;
+        // words: the radix passes cover the first 8 key bytes (K2 / K1), the
+        // tie refinement the rest; artists (long shared name prefixes) keep
+        // the K0 passes too
+        const bool sk0 = slot != 0;
         // words: the composite key (dense count rank + first key bytes, one
         // word; msa_sort.hip) when the counts take few enough distinct values
         u32 gB = ~0u;
@@ -1922,21 +1839,12 @@ int msa_create(int device, msa_ctx **out) {
     if (hipSetDevice(device) != hipSuccess) return MSA_ERR_HIP;
     msa_ctx *c = new msa_ctx();
     c->device = device;
+#ifdef MSA_DIAG
     if (const char *ab = getenv("MSA_ABLATE")) c->ablate = atoi(ab);
-    if (const char *ks = getenv("MSA_K3SPLIT")) c->k3split = atoi(ks) != 0;
-    if (const char *et = getenv("MSA_EARLY_TEXT")) c->early_text = atoi(et) != 0;
-    if (const char *gw = getenv("MSA_GATHER_W")) c->gather_w = atoi(gw) != 0;
-    if (const char *k0 = getenv("MSA_SORT_K0")) c->sort_k0 = atoi(k0) != 0;
-    if (const char *ts = getenv("MSA_TEXT_AT_SPLIT")) c->text_at_split = atoi(ts) != 0;
-    if (const char *tp = getenv("MSA_TEXT_AT_SPANS")) c->text_at_spans = atoi(tp) != 0;
-    if (const char *ta = getenv("MSA_TEXT_AT_AGG")) c->text_at_agg = atoi(ta) != 0;
+#endif
     if (const char *cs = getenv("MSA_COMP_SORT")) c->comp_sort = atoi(cs) != 0;
-    if (const char *lb = getenv("MSA_LISTS_BESIDE")) c->lists_beside = atoi(lb) != 0;
-    if (const char *gm = getenv("MSA_GROW_MUL")) c->grow_mul = std::max(2, std::min(16, atoi(gm)));
-    if (const char *gs = getenv("MSA_GROW_STEP")) c->grow_step = (u32)std::max(1, std::min(4, atoi(gs)));
     if (const char *mb = getenv("MSA_MISS_BUCKETS")) c->mb_mode = atoi(mb);
     if (const char *mm = getenv("MSA_MISS_BUCKETS_MIN")) c->mb_min = strtoull(mm, nullptr, 10);
-    if (const char *ac = getenv("MSA_AUX_COL")) c->aux_col = atoi(ac) != 0;
     if (const char *me = getenv("MSA_MLOG_ENTRIES")) c->mlog_test = strtoull(me, nullptr, 10);
     if (const char *so = getenv("MSA_SORT")) c->sort_mode = !strcmp(so, "merge") ? 1 : (!strcmp(so, "radix") ? 2 : 0);
     {
@@ -1948,16 +1856,10 @@ int msa_create(int device, msa_ctx **out) {
     // 16th CU with hipExtStreamCreateWithCUMask -- no gain)
     // text.csv's side stream at the highest priority: its gather is the step's
     // tail and the ranking beside it has slack (2.88-2.91 vs 2.92-2.96 ms/step,
-    // profiles/r04_t48_ab_side_priority.txt; MSA_SIDE_PRIO=0: default priority)
-    hipError_t side_e;
-    const char *sp = getenv("MSA_SIDE_PRIO");
-    if (!sp || atoi(sp) != 0) {
-        int least = 0, greatest = 0;
-        (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
-        side_e = hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, greatest);
-    } else {
-        side_e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
-    }
+    // profiles/r04_t48_ab_side_priority.txt)
+    int least = 0, greatest = 0;
+    (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
+    const hipError_t side_e = hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, greatest);
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess || side_e != hipSuccess ||
         hipStreamCreateWithFlags(&c->rank2, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
@@ -1967,10 +1869,6 @@ int msa_create(int device, msa_ctx **out) {
         hipEventCreateWithFlags(&c->ev_r2_join, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_scan_a, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_spans, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_lb_fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_lb_join, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_put, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_tscan, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fin, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
@@ -2022,10 +1920,6 @@ void msa_destroy(msa_ctx *c) {
     (void)hipEventDestroy(c->ev_r2_join);
     (void)hipEventDestroy(c->ev_scan_a);
     (void)hipEventDestroy(c->ev_spans);
-    (void)hipEventDestroy(c->ev_lb_fork);
-    (void)hipEventDestroy(c->ev_lb_join);
-    (void)hipEventDestroy(c->ev_put);
-    (void)hipEventDestroy(c->ev_tscan);
     (void)hipStreamDestroy(c->side);
     (void)hipStreamDestroy(c->rank2);
     (void)hipStreamDestroy(c->aux);

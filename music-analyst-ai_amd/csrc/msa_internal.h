@@ -284,7 +284,8 @@ struct Counters {
     u64 k3_misses;   // K3 log entries folded by k_miss_agg: LDS-table misses + flushed table entries (diagnostic)
     u64 col_body[2]; // artist.csv / text.csv body bytes (the line-offset scans' totals)
     u64 span_fix;    // records k_rec_fast hands to k_rec_fix (the exact per-record path)
-    u64 mlog_full;   // K3 misses that found their log partition full (inserted straight into HBM)
+    u64 mlog_full;   // K3 misses that found their log partition full (dropped: the split runs again with
+                     // larger logs; at the logs' size limit inserted straight into HBM)
 };
 
 enum { OVF_S = 1, OVF_M = 2, OVF_L = 4, OVF_LT = 8, OVF_A = 16, OVF_REC = 32, OVF_MLOG = 64 };
@@ -338,11 +339,11 @@ struct ScanArgs {
     ulonglong2 *mlog;
     u32 *mlog_n;
     u32 mlog_cap;
+    int mlog_direct; // the logs are at their size limit: a full partition's entries go to the HBM tables
     // split scan (k_scan_struct -> k_scan_tokens): bit i of lmask[1 + i / 64]
     // = byte seg_begin + i is a token byte of a counted lyric field
     // (process_lyrics input, parallel_spotify.c:350-394); lmask[0] = 0 pad
     u64 *lmask;
-    int split;       // 1: k_scan_struct + k_scan_tokens, 0: the fused k_scan_csv
 };
 
 #define MSA_MLOG_PARTS 16

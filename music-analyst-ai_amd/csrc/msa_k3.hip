@@ -35,18 +35,9 @@ namespace {
 // to a per-wave list of the block's token starts: the lanes share the tokens
 // evenly (compaction) instead of each walking its own.
 #define Q_LIST 1024              // token entries per wave-iteration (>= 4 bytes per token)
-// TOK_DIRECT: each probe batch's misses go straight to the logs in one buffer
-// store per wave (no LDS miss buffer); 0: buffered per wave and flushed when
-// full (round 3)
-#ifndef TOK_DIRECT
-#define TOK_DIRECT 1
-#endif
-#if TOK_DIRECT
-#define Q_MISS 0
-#else
-#define Q_MISS 32                // deferred HBM inserts per wave (16 B each)
-#endif
-#define Q_WLDS (Q_LIST * 2 + Q_MISS * 16)
+// Each probe batch's misses go straight to the logs in one buffer store per
+// wave (round 4; the per-wave LDS miss buffers of round 3 are gone).
+#define Q_WLDS (Q_LIST * 2)
 #define Q_CUR ((MSA_MLOG_PARTS + 4) * 4)  // log cursors per partition + the dropped-entry count
 // LDS word table: 3..8-byte words (92 % of the tokens of lyric text) as
 // single u64 keys (12 bytes a slot, 4-slot buckets read as two ds_read_b128);
@@ -55,7 +46,7 @@ namespace {
 // M table 1.95 ms, mixed with an M table 1.99, mixed without an M table (the S
 // table takes the whole LDS) 1.82 -- the design kept.
 #ifndef Q_SSLOTS                 // the rest of the CU's LDS
-#define Q_SSLOTS (((163840 - Q_W * (Q_LIST * 2 + Q_MISS * 16) - Q_CUR) / 12) & ~31)
+#define Q_SSLOTS (((163840 - Q_W * Q_WLDS - Q_CUR) / 12) & ~31)
 #endif
 #define Q_SNB (Q_SSLOTS / 4)
 #define Q_TAB (Q_SSLOTS * 12)
@@ -296,19 +287,6 @@ __device__ __forceinline__ u32 gather8(u64 x) {  // bit 8j + 7 -> bit j
 }
 #define MLOG_KEYBITS 0x7F7F7F7F7F7F7F7Full
 
-__device__ __forceinline__ void flush_miss(const ScanArgs &a, const ulonglong2 *miss, u32 n, u32 *lcur) {
-    wsync();
-    const u32 lane = lane_id();
-    if (lane < n) {
-        const ulonglong2 x = miss[lane];
-        const u32 part = mlog_part(x.x, x.y);
-        const u32 at = atomicAdd(&lcur[part], 1u);
-        if (at < a.mlog_cap) a.mlog[((u64)blockIdx.x * MSA_MLOG_PARTS + part) * a.mlog_cap + at] = x;
-        else hbm_insert16<false>(a, x.x, x.y, 1);
-    }
-    wsync();
-}
-
 // Record structure of one 4 KiB block (read_csv_record 549-633 + parse_csv_line
 // 258-304): from the reader state st at the block start (updated to the state
 // after it) and the block's byte classes, the per-record arrays (rec_start,
@@ -454,7 +432,7 @@ __device__ __forceinline__ u64 struct_block(const ScanArgs &a, State &st, const 
 
 // The token phase of one 4 KiB block (process_lyrics, parallel_spotify.c:
 // 350-394): w = the lane's 64 token-byte bits, Tn = the 64 after them, S0 =
-// the counted token starts.  Shared by k_scan_csv and k_scan_tokens.
+// the counted token starts.
 // the workgroup's miss logs as a buffer resource: a store out of its range
 // (lanes without a miss) is dropped by the bounds check
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t mlog_rsrc(const ScanArgs &a) {
@@ -464,7 +442,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t mlog_rsrc(const ScanArgs &a) {
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ void tok_phase(const ScanArgs &a, u64 ib, u64 lpos, u64 w, u64 Tn, u64 S0, u64 *skeys,
-                                          u32 *scnts, u16 *list, ulonglong2 *miss, u32 &nmiss, u32 *lcur,
+                                          u32 *scnts, u16 *list, u32 *lcur,
                                           u64 &words, __amdgpu_buffer_rsrc_t rsrc) {
     const u32 lane = lane_id();
     // runs: rK bit b = bytes b .. b+K-1 are token bytes (w = Tn:T)
@@ -538,7 +516,6 @@ __device__ __forceinline__ void tok_phase(const ScanArgs &a, u64 ib, u64 lpos, u
         const uint4 v = kv;
         const u32 v4 = k4;
         const bool have = bt * 64 + lane < nS;
-#if TOK_DIRECT
         {  // unconditional (a stale list entry: an address inside the block), so
            // that the loop's vector memory sequence is the same every trip
             en = list[min((bt + 1) * 64 + lane, (u32)Q_LIST - 1u)];
@@ -546,14 +523,6 @@ __device__ __forceinline__ void tok_phase(const ScanArgs &a, u64 ib, u64 lpos, u
             kv = *reinterpret_cast<const uint4 *>(gp);
             k4 = gp[4];
         }
-#else
-        if ((bt + 1) * 64 + lane < nS) {
-            en = list[(bt + 1) * 64 + lane];
-            const u32 *gp = reinterpret_cast<const u32 *>(a.buf + ((ib + (en & 4095u)) & ~3ull));
-            kv = *reinterpret_cast<const uint4 *>(gp);
-            k4 = gp[4];
-        }
-#endif
         if (have) {
             const u32 len = (e >> 12) + 3;
             const u32 sh = (u32)(ib + (e & 4095u)) & 3u;
@@ -579,38 +548,24 @@ __device__ __forceinline__ void tok_phase(const ScanArgs &a, u64 ib, u64 lpos, u
                 mis = !(K3_ABLATE && (a.ablate & 4));
             }
         }
-#if TOK_DIRECT
         // the batch's misses straight to their log partitions: a slot from the
         // partition's LDS cursor, then one store for the whole wave -- every
         // trip, lanes without a miss out of the buffer's range -- so waiting for
         // the next batch's key loads never waits for this store.  A full
         // partition drops the entry and counts it: the split runs again with
-        // larger logs (Counters::mlog_full, OVF_MLOG)
+        // larger logs (Counters::mlog_full, OVF_MLOG) -- unless the logs are at
+        // their size limit (2^24 - 1 entries a partition: mlog_direct), where
+        // the entry goes straight into the HBM table
         u32 off = 0xFFFFFFF0u;
         if (mis) {
             const u32 part = mlog_part(k0, k1);
             const u32 at = atomicAdd(&lcur[part], 1u);
             if (at < a.mlog_cap) off = ((u32)__umul24(part, a.mlog_cap) + at) * 16u;  // cap < 2^24
+            else if (a.mlog_direct) hbm_insert16<false>(a, k0, k1, 1);  // logs at their size limit
             else atomicAdd(&lcur[MSA_MLOG_PARTS], 1u);
         }
         const u32x4_t ent = {(u32)k0, (u32)(k0 >> 32), (u32)k1, (u32)(k1 >> 32)};
         __builtin_amdgcn_raw_buffer_store_b128(ent, rsrc, (int)off, 0, 0);
-#else
-        const u64 MB = __ballot(mis);
-        if (MB) {
-            const u32 nm = (u32)__popcll(MB);
-            if (nmiss + nm > Q_MISS) {
-                flush_miss(a, miss, nmiss, lcur);
-                nmiss = 0;
-            }
-            if (mis) {
-                const u32 at = nmiss + mbcnt(MB);
-                if (at < Q_MISS) miss[at] = make_ulonglong2(k0, k1);
-                else hbm_insert16<false>(a, k0, k1, 1);  // more misses than the buffer holds (> 32 in one pass)
-            }
-            nmiss = min(nmiss + nm, (u32)Q_MISS);
-        }
-#endif
     }
     wsync();
 }
@@ -618,10 +573,8 @@ __device__ __forceinline__ void tok_phase(const ScanArgs &a, u64 ib, u64 lpos, u
 // End of a counting workgroup: the wave's pending misses, total_words, the
 // LDS table flushed into the logs (counts encoded; full partitions: HBM
 // inserts) and the log lengths.
-__device__ __forceinline__ void tok_epilogue(const ScanArgs &a, u64 *skeys, u32 *scnts, ulonglong2 *miss, u32 nmiss,
-                                             u32 *lcur, u64 words) {
+__device__ __forceinline__ void tok_epilogue(const ScanArgs &a, u64 *skeys, u32 *scnts, u32 *lcur, u64 words) {
     const u32 lane = lane_id();
-    if (nmiss) flush_miss(a, miss, nmiss, lcur);
     words = wave_sum64(words);
     if (lane == 0 && words) atomicAdd((unsigned long long *)&a.ctr->total_words, (unsigned long long)words);
     __syncthreads();
@@ -647,149 +600,26 @@ __device__ __forceinline__ void tok_epilogue(const ScanArgs &a, u64 *skeys, u32 
         // the next split sizes the logs from this (full partitions cost an HBM insert per entry)
         if (n > a.mlog_cap) atomicAdd((unsigned long long *)&a.ctr->mlog_full, (unsigned long long)(n - a.mlog_cap));
     }
-    if (TOK_DIRECT && threadIdx.x == 0 && lcur[MSA_MLOG_PARTS])  // misses dropped: this split is repeated
+    if (threadIdx.x == 0 && lcur[MSA_MLOG_PARTS])  // misses dropped: this split is repeated
         atomicOr((unsigned long long *)&a.ctr->overflow, (unsigned long long)OVF_MLOG);
 }
 
 }  // namespace
 
-// SPLIT = 0: k_scan_csv, the fused pass (structure + tokens + LDS counting,
-// one 1024-thread workgroup per CU).  SPLIT = 1: k_scan_struct, the structure
-// alone: no LDS, 256-thread workgroups at SA_MINW waves per SIMD; instead of
-// counting it writes the lyric token-byte mask (ScanArgs::lmask) that
-// k_scan_tokens counts.
+// k_scan_struct: the record structure alone, no LDS, 256-thread workgroups at
+// SA_MINW waves per SIMD; instead of counting it writes the lyric token-byte
+// mask (ScanArgs::lmask) that k_scan_tokens counts.  (The fused pass of rounds
+// 1-3 -- structure, tokens and LDS counting in one 1024-thread workgroup per CU
+// -- was 0.25 ms/step slower and is gone.)
 #ifndef SA_T
 #define SA_T 256
 #endif
 #ifndef SA_MINW
 #define SA_MINW 5
 #endif
-template <int SPLIT>
-__device__ __forceinline__ void scan_body(const ScanArgs &a) {
-    constexpr u32 NT = SPLIT ? SA_T : Q_T;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    u64 *skeys = reinterpret_cast<u64 *>(smem);
-    u32 *scnts = reinterpret_cast<u32 *>(smem + Q_SSLOTS * 8);
-    const u32 lane = lane_id();
-    const u32 wib = threadIdx.x >> 6;
-    unsigned char *wl = smem + Q_TAB + wib * Q_WLDS;
-    u16 *list = reinterpret_cast<u16 *>(wl);
-    ulonglong2 *miss = reinterpret_cast<ulonglong2 *>(wl + Q_LIST * 2);
-    u32 nmiss = 0;  // wave-uniform
-
-    u32 *lcur = reinterpret_cast<u32 *>(smem + Q_TAB + Q_W * Q_WLDS);  // log cursors per key partition
-    if (!SPLIT) {
-        for (u32 i = threadIdx.x; i < Q_SSLOTS; i += Q_T) {
-            skeys[i] = 0;
-            scnts[i] = 0;
-        }
-        if (threadIdx.x < MSA_MLOG_PARTS + 1) lcur[threadIdx.x] = 0;
-        __syncthreads();
-    }
-    const __amdgpu_buffer_rsrc_t rsrc = mlog_rsrc(a);
-
-    // wave-uniform chunk walk (scalar registers; the chunk-start values below
-    // come through scalar loads, which do not wait behind the vector prefetch)
-    const u32 gw = __builtin_amdgcn_readfirstlane(blockIdx.x * (NT / 64) + wib);
-    const u32 nw = gridDim.x * (NT / 64);
-    u64 words = 0;
-
-    // Software pipeline: the next block (the wave's next chunk's first block
-    // after a chunk's last one) and the 16 bytes after THAT block are loaded
-    // while the current block is processed.  Every iteration issues the same
-    // five loads (a dummy re-read of the current block where there is no next
-    // one), so the compiler's vmcnt for the block stays the loop-top wait: no
-    // load the current block's structure or token phase waits for was issued
-    // after the prefetch (vmcnt drains in issue order).
-    uint4 cur[4];
-    uint4 tl = make_uint4(0, 0, 0, 0);  // the 16 bytes after the current block
-    if (gw < a.nchunks) {
-        const u64 b0 = a.seg_begin + (u64)gw * MSA_CHUNK;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) cur[q] = ldg16(a.buf + b0 + lane * 64 + 16 * q);
-        // a vector load: a uniform address here (no store before it) would
-        // become a scalar load, which drops the low address bits -- and
-        // a.buf is a view of the input at any alignment
-        u64 ta = b0 + Q_BLK < a.seg_end ? b0 + Q_BLK : b0;
-        pin64(ta);
-        tl = ldg16(a.buf + ta);
-    }
-    for (u32 c = gw; c < a.nchunks; c += nw) {
-        State st = sload_state(a.carry + c);
-        // K1 saw no '\r' / NUL in this chunk: their masks stay empty
-        const bool rare_chunk = !a.sums || ((*sload(&a.sums[c].h[0]) >> 22) & 1u);
-        const u64 cbase = a.seg_begin + (u64)c * MSA_CHUNK;
-        const u64 cend = min(cbase + (u64)MSA_CHUNK, a.seg_end);
-        u32 prevT = 0;  // the byte before the chunk is a token byte
-        u32 prevQ = 0;  // ... is a '"'
-        if (cbase > a.seg_begin) {
-            // the dword holding the byte (a.buf is a view: any alignment)
-            const size_t pa = (size_t)(a.buf + cbase - 1);
-            const u32 b = (*sload(reinterpret_cast<const u32 *>(pa & ~(size_t)3)) >> (8 * (pa & 3))) & 0xFFu;
-            prevT = (u32)(((b | 0x20u) >= 'a' && (b | 0x20u) <= 'z') || (b >= '0' && b <= '9') || b == '\'');
-            prevQ = (u32)(b == '"');
-        }
-
-        for (u64 ib = cbase; ib < cend; ib += Q_BLK) {
-            const u64 lpos = ib + lane * 64;
-            const bool more = ib + Q_BLK < cend;
-            // the 16 bytes after this block (token continuation, "\r\n" swallow),
-            // loaded with the block; only bytes before the segment end count,
-            // whatever the padding holds
-            const u64 tpos = ib + Q_BLK;
-            const uint4 tail = tl;
-            const u32 tvm = tpos < a.seg_end ? (a.seg_end - tpos >= 16 ? 0xFFFFu : (1u << (a.seg_end - tpos)) - 1u) : 0u;
-            u32 ttok = 0;
-            if (!SPLIT) {
-                u32 tw[4] = {tail.x, tail.y, tail.z, tail.w};
-#pragma unroll
-                for (int d = 0; d < 4; ++d) ttok |= pk4(lower_tok(tw[d])) << (4 * d);
-                ttok &= tvm;
-            }
-            const u64 rem = cend > lpos ? cend - lpos : 0;
-            const Masks k = classify64x(cur, (u32)min(rem, (u64)64), rare_chunk);
-            // the block's bytes now live in the masks: load the next block (and
-            // its tail) into the same registers, in flight during the rest
-            {
-                const u64 nbb = more ? ib + Q_BLK
-                                     : (c + nw < a.nchunks ? a.seg_begin + (u64)(c + nw) * MSA_CHUNK : ib);
-#pragma unroll
-                for (int q = 0; q < 4; ++q) cur[q] = ldg16(a.buf + nbb + lane * 64 + 16 * q);
-                // the tail's address is made opaque (a VGPR the compiler cannot
-                // prove uniform): left uniform, its value is moved to scalar
-                // registers right away -- a wait on the load in this iteration
-                // (and a scalar load would drop the low address bits)
-                u64 ta = nbb + Q_BLK < a.seg_end ? nbb + Q_BLK : nbb;
-                pin64(ta);
-                tl = ldg16(a.buf + ta);
-            }
-
-            const u64 live = struct_block(a, st, k, tail, tvm, lpos, prevQ);
-            prevQ = readlane((u32)(k.Q >> 63), 63);
-            if (SPLIT) {
-                // the lyric token bytes for k_scan_tokens (every lane of the
-                // block writes its word, past the segment end too: zero)
-                a.lmask[1 + ((ib - a.seg_begin) >> 6) + lane] = k.T & live;
-                continue;
-            }
-            // ---- tokens of the lyric field (process_lyrics, 350-394) ----
-            const u64 Tp = from_prev(k.T) >> 63;
-            const u64 tp = lane ? Tp : (u64)prevT;
-            const u64 S0 = k.T & live & ~((k.T << 1) | tp);
-            prevT = readlane((u32)(k.T >> 63), 63);
-            const u64 Tnx = from_next(k.T);
-            const u64 Tn = lane == 63 ? (u64)ttok : Tnx;
-            tok_phase(a, ib, lpos, k.T, Tn, S0, skeys, scnts, list, miss, nmiss, lcur, words, rsrc);
-        }
-    }
-    if (!SPLIT) tok_epilogue(a, skeys, scnts, miss, nmiss, lcur, words);
-}
-
-__global__ __launch_bounds__(Q_T, 1) void k_scan_csv(ScanArgs a) { scan_body<0>(a); }
-
 // k_scan_struct: the split scan's structure pass.  Each wave walks its
 // blocks (the 4 KiB blocks of chunks gw, gw + nw, ...) with the input loaded
-// SA_PF blocks ahead (1: as k_scan_csv; 2: two blocks in flight -- one
+// SA_PF blocks ahead (1: the next block; 2: two blocks in flight -- one
 // block's structure work alone did not cover the HBM latency at these wave
 // counts).  Per block: byte classes, record structure (struct_block), and the
 // lyric token-byte mask for k_scan_tokens.
@@ -872,7 +702,7 @@ __global__ __launch_bounds__(SA_T, SA_MINW) void k_scan_struct(ScanArgs a) {
 // k_scan_tokens: the token phase of the split scan over k_scan_struct's
 // lmask -- no reader state, no byte classes: a wave per 4 KiB block (grid
 // stride), token starts and lengths from the mask, keys re-read from the
-// input, counted in the workgroup's LDS table as in k_scan_csv.  The next
+// input, counted in the workgroup's LDS table.  The next
 // block's mask words and one 16-byte load per lane of its bytes (the keys'
 // cache lines) are in flight while a block is counted.  (Measured and
 // removed: the token lists software-pipelined across blocks, the next
@@ -886,8 +716,6 @@ __global__ __launch_bounds__(Q_T, 1) void k_scan_tokens(ScanArgs a) {
     const u32 wib = threadIdx.x >> 6;
     unsigned char *wl = smem + Q_TAB + wib * Q_WLDS;
     u16 *list = reinterpret_cast<u16 *>(wl);
-    ulonglong2 *miss = reinterpret_cast<ulonglong2 *>(wl + Q_LIST * 2);
-    u32 nmiss = 0;  // wave-uniform
     u32 *lcur = reinterpret_cast<u32 *>(smem + Q_TAB + Q_W * Q_WLDS);
     for (u32 i = threadIdx.x; i < Q_SSLOTS; i += Q_T) {
         skeys[i] = 0;
@@ -921,9 +749,9 @@ __global__ __launch_bounds__(Q_T, 1) void k_scan_tokens(ScanArgs a) {
         const u64 ib = a.seg_begin + blk * Q_BLK;
         const u64 lpos = ib + lane * 64;
         const u64 S0 = L & ~((L << 1) | (Lprev >> 63));
-        tok_phase(a, ib, lpos, L, Lnext, S0, skeys, scnts, list, miss, nmiss, lcur, words, rsrc);
+        tok_phase(a, ib, lpos, L, Lnext, S0, skeys, scnts, list, lcur, words, rsrc);
     }
-    tok_epilogue(a, skeys, scnts, miss, nmiss, lcur, words);
+    tok_epilogue(a, skeys, scnts, lcur, words);
 }
 
 // k_miss_agg: workgroup (partition p, group g) counts partition p of the
@@ -1165,8 +993,8 @@ __global__ __launch_bounds__(MBA_T) void k_mb_agg(ScanArgs a, u32 T, const u64 *
 }
 
 static int g_q_cus = 0;
-// Counting workgroups: one per CU (k_scan_csv: a wave per 16 KiB chunk;
-// k_scan_tokens: a wave per 4 KiB block).  k_miss_agg reads their logs.
+// Counting workgroups: one per CU (k_scan_tokens: a wave per 4 KiB block);
+// k_miss_agg reads their logs.
 static u32 scan_blocks(const ScanArgs &a) {
     if (!g_q_cus) {
         int dev = 0;
@@ -1174,34 +1002,29 @@ static u32 scan_blocks(const ScanArgs &a) {
         hipDeviceProp_t p;
         g_q_cus = (hipGetDeviceProperties(&p, dev) == hipSuccess && p.multiProcessorCount > 0) ? p.multiProcessorCount
                                                                                                  : 256;
-        (void)hipFuncSetAttribute((const void *)k_scan_csv, hipFuncAttributeMaxDynamicSharedMemorySize, Q_LDS);
         (void)hipFuncSetAttribute((const void *)k_scan_tokens, hipFuncAttributeMaxDynamicSharedMemorySize, Q_LDS);
         (void)hipFuncSetAttribute((const void *)k_miss_agg, hipFuncAttributeMaxDynamicSharedMemorySize, MA_SLOTS * 20);
     }
-    const u64 units = a.split ? (a.seg_end - a.seg_begin + Q_BLK - 1) / Q_BLK : a.nchunks;
+    const u64 units = (a.seg_end - a.seg_begin + Q_BLK - 1) / Q_BLK;
     const u64 blocks = (units + Q_W - 1) / Q_W;
     return blocks > (u64)g_q_cus ? (u32)g_q_cus : (u32)blocks;
 }
-// The fused k_scan_csv, or the split scan's first kernel k_scan_struct
-// (msa_launch_scan_tokens then runs the second on the same stream).
+// The split scan's first kernel, k_scan_struct (msa_launch_scan_tokens then
+// runs the second on the same stream).
 hipError_t msa_launch_scan_csv(const ScanArgs &a, hipStream_t s) {
     if (!a.nchunks) return hipSuccess;
-    const u32 blocks = scan_blocks(a);
-    if (a.split) {
-        // a wave per chunk, SA_MINW waves per SIMD while chunks last
-        const u32 waves = std::min<u32>(a.nchunks, (u32)g_q_cus * 4 * SA_MINW);
-        hipLaunchKernelGGL(k_scan_struct, dim3((waves + SA_T / 64 - 1) / (SA_T / 64)), dim3(SA_T), 0, s, a);
-    } else {
-        hipLaunchKernelGGL(k_scan_csv, dim3(blocks), dim3(Q_T), Q_LDS, s, a);
-    }
+    (void)scan_blocks(a);  // the device's CU count
+    // a wave per chunk, SA_MINW waves per SIMD while chunks last
+    const u32 waves = std::min<u32>(a.nchunks, (u32)g_q_cus * 4 * SA_MINW);
+    hipLaunchKernelGGL(k_scan_struct, dim3((waves + SA_T / 64 - 1) / (SA_T / 64)), dim3(SA_T), 0, s, a);
     return hipGetLastError();
 }
 hipError_t msa_launch_scan_tokens(const ScanArgs &a, hipStream_t s) {
-    if (!a.nchunks || !a.split) return hipSuccess;
+    if (!a.nchunks) return hipSuccess;
     hipLaunchKernelGGL(k_scan_tokens, dim3(scan_blocks(a)), dim3(Q_T), Q_LDS, s, a);
     return hipGetLastError();
 }
-// after k_scan_csv on the same stream: fold the logged misses, 16 partitions x
+// after k_scan_tokens on the same stream: fold the logged misses, 16 partitions x
 // groups, one workgroup per CU
 // the bucketed aggregation: scratch sizes (entries = every log's capacity)
 u64 msa_mb_hist_words(const ScanArgs &a, u32 nsrc) {

@@ -785,146 +785,6 @@ __global__ __launch_bounds__(256) void k_rec_fix(const u8 *__restrict__ buf, con
         rec_full(buf, rec_start, nulrel, fix[i], first_rec, want_text, o, ctr, ak);
 }
 
-// The text column's line spans alone, on the side stream right after the
-// record structure pass (k_scan_struct), so that text.csv is gathered beside
-// the token pass instead of after the artist pass: thread per record, the
-// quoted common record from its span events (as k_rec_fast), every other one
-// on the exact path (rec_full without the artist part).  k_rec_fast then runs
-// without the text (its fix list holds only the records its artist span needs).
-__global__ __launch_bounds__(256) void k_rec_text(const u8 *__restrict__ buf, const u64 *__restrict__ rec_start,
-                                                  const u32 *__restrict__ nulrel, const u64 *__restrict__ tss,
-                                                  const u64 *__restrict__ tse, u64 nrec, u64 first_rec, SpanOut o,
-                                                  Counters *ctr, AKeys ak) {
-    const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= nrec) return;
-    const u64 E = tse[r];
-    if (r < first_rec || (E & (SPAN_NOLINE | SPAN_NUL | SPAN_FIX)) == SPAN_NOLINE) {
-        o.tlen[r] = 0;
-        return;
-    }
-    const u64 S = tss[r];
-    const u64 ts = S & SPAN_POS, te = E & SPAN_POS;
-    const bool quoted = (S & SPAN_Q) && (E & SPAN_Q) && te >= ts + 2;
-    if ((E & (SPAN_NUL | SPAN_FIX)) || !quoted) {
-        rec_full(buf, rec_start, nulrel, r, first_rec, 1, o, ctr, ak, false);
-        return;
-    }
-    o.tlen[r] = te - ts + 1;
-    o.tsrc[r] = ts;
-    o.tpairs[r] = 0;
-}
-
-// Segmented gather without LDS (so that it fits beside the token pass, whose
-// workgroups hold every CU's LDS): a wave owns 64 consecutive lines -- lane j
-// holds line j's offset and source -- and so the output range [off[r0],
-// off[r0 + 64]).  Its lanes walk the range's aligned 16-byte slots, two per
-// lane per round, each slot's line found by a binary search over the lanes'
-// offsets (cross-lane reads, all lanes active); a slot inside one line is
-// five dword loads + v_alignbyte and one 16-byte store, a slot that meets a
-// line end is composed from the lines it meets (their offsets re-read from
-// memory, L1), the range's ragged first / last slot stored byte by byte.
-#define CW_T 256
-__global__ __launch_bounds__(CW_T) void k_col_gather_w(const u8 *__restrict__ buf, const u64 *__restrict__ line_len,
-                                                       const u64 *__restrict__ line_off,
-                                                       const u64 *__restrict__ span_src, u64 nrec, u64 hdr,
-                                                       const u64 *__restrict__ body_p, u8 *__restrict__ col) {
-    const u32 lane = lane_id();
-    const u64 r0 = ((u64)blockIdx.x * CW_T + threadIdx.x) & ~63ull;  // the wave's first line
-    if (r0 >= nrec) return;  // wave-uniform
-    const u64 body = *body_p;
-    const u32 wn = (u32)min((u64)64, nrec - r0);
-    // lane j: start of line j (absolute column byte); lanes >= wn: the range end
-    const u64 O1 = hdr + ((r0 + wn < nrec) ? line_off[r0 + wn] : body);
-    const u64 myoff = lane < wn ? hdr + line_off[r0 + lane] : O1;
-    const u64 mysrc = lane < wn ? span_src[r0 + lane] : 0;
-    const u64 O0 = readlane64(myoff, 0);
-    if (O1 <= O0) return;
-    const u64 S0 = O0 & ~15ull;
-    const u64 nslots = (O1 - S0 + 15) / 16;
-    auto lstart = [&](u32 j) -> u64 { return j < wn ? hdr + line_off[r0 + j] : O1; };
-    for (u64 base = 0; base < nslots; base += 128) {
-        u64 A[2];
-        u32 jj[2];
-        uint4 va[2];
-        u32 d4[2], sh[2];
-        bool fast[2], ok[2];
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const u64 si = base + (u64)k * 64 + lane;
-            ok[k] = si < nslots;
-            A[k] = S0 + (ok[k] ? si : nslots - 1) * 16;
-            const u64 lo = max(A[k], O0);
-            // last line j with start <= lo (every lane takes part: cross-lane reads)
-            u32 j = 0;
-#pragma unroll
-            for (u32 step = 32; step > 0; step >>= 1) {
-                const u32 c = j + step;
-                const u32 cl = c < 64 ? c : 63;
-                const u64 oc = ((u64)__shfl((int)(u32)(myoff >> 32), (int)cl) << 32) |
-                               (u32)__shfl((int)(u32)myoff, (int)cl);
-                if (c < wn && oc <= lo) j = c;
-            }
-            jj[k] = j;
-            const u64 ls = ((u64)__shfl((int)(u32)(myoff >> 32), (int)j) << 32) | (u32)__shfl((int)(u32)myoff, (int)j);
-            const u32 jn = j + 1 < 64 ? j + 1 : 63;
-            u64 le = ((u64)__shfl((int)(u32)(myoff >> 32), (int)jn) << 32) | (u32)__shfl((int)(u32)myoff, (int)jn);
-            if (j + 1 >= wn) le = O1;
-            const u64 sj = ((u64)__shfl((int)(u32)(mysrc >> 32), (int)j) << 32) | (u32)__shfl((int)(u32)mysrc, (int)j);
-            fast[k] = ok[k] && A[k] >= O0 && A[k] + 16 <= O1 && A[k] >= ls && A[k] + 16 < le;
-            va[k] = make_uint4(0, 0, 0, 0);
-            d4[k] = 0;
-            sh[k] = 0;
-            if (fast[k]) {
-                const u64 src = sj + (A[k] - ls);
-                const u32 *p = reinterpret_cast<const u32 *>(buf + (src & ~3ull));
-                va[k] = make_uint4(p[0], p[1], p[2], p[3]);
-                d4[k] = p[4];
-                sh[k] = (u32)(src & 3);
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            if (!ok[k]) continue;
-            const u64 a0 = A[k];
-            if (fast[k]) {
-                *reinterpret_cast<uint4 *>(col + a0) = align16(va[k], d4[k], sh[k]);
-                continue;
-            }
-            // a line end in the slot (or the range's ragged edge): compose it
-            const u64 lo = max(a0, O0), hi = min(a0 + 16, O1);
-            uint4 out = make_uint4(0, 0, 0, 0);
-            bool good = true;
-            for (u32 j = jj[k]; j < wn; ++j) {
-                const u64 ls = lstart(j), le = lstart(j + 1);
-                if (ls >= hi) break;
-                if (le > ls) {
-                    const u64 src = span_src[r0 + j];
-                    const u64 a = max(a0, ls), b = min(a0 + 16, le - 1);
-                    if (b > a) {
-                        if (src + a0 < ls) { good = false; break; }  // window would start before the buffer
-                        out = bytes_blend(out, load16u(buf, src + a0 - ls), (u32)(a - a0), (u32)(b - a0));
-                    }
-                    if (le - 1 >= a0 && le - 1 < a0 + 16) out = byte_put(out, (u32)(le - 1 - a0), '\n');
-                }
-                if (le >= hi) break;
-            }
-            if (good && lo == a0 && hi == a0 + 16) {
-                *reinterpret_cast<uint4 *>(col + a0) = out;
-            } else if (good) {  // owned bytes only
-                const u32 d[4] = {out.x, out.y, out.z, out.w};
-                for (u64 q = lo; q < hi; ++q) col[q] = (u8)(d[(q - a0) >> 2] >> (8 * ((q - a0) & 3)));
-            } else {
-                u32 j = jj[k];
-                for (u64 q = lo; q < hi; ++q) {
-                    while (q >= lstart(j + 1)) ++j;
-                    const u64 ls = lstart(j), le = lstart(j + 1);
-                    col[q] = (q + 1 == le) ? (u8)'\n' : buf[span_src[r0 + j] + (q - ls)];
-                }
-            }
-        }
-    }
-}
-
 // Segmented gather.  A workgroup owns 256 consecutive lines (their metadata
 // is one coalesced load into LDS) and therefore the contiguous output range
 // [off[r0], off[r0+256]).  Its threads walk the 16-byte slots (aligned in
@@ -2039,10 +1899,11 @@ __global__ void k_tie_fixup(const u64 *__restrict__ K2, const u64 *__restrict__ 
                             const u32 *key_len, u32 *__restrict__ out) {
     const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    // K0 null: the sort covered K2 and K1 only (K0's bytes are the first refinement round's)
-    const u64 a2 = K2[i], a1 = K1[i], a0 = K0 ? K0[i] : 0;
-    const bool eq_prev = i > 0 && K2[i - 1] == a2 && K1[i - 1] == a1 && (!K0 || K0[i - 1] == a0);
-    const bool eq_next = i + 1 < n && K2[i + 1] == a2 && K1[i + 1] == a1 && (!K0 || K0[i + 1] == a0);
+    // K0 is required (msa_launch_fixup refuses null): full_cmp takes tied
+    // entries as equal in their first 16 key bytes (K1, K0)
+    const u64 a2 = K2[i], a1 = K1[i], a0 = K0[i];
+    const bool eq_prev = i > 0 && K2[i - 1] == a2 && K1[i - 1] == a1 && K0[i - 1] == a0;
+    const bool eq_next = i + 1 < n && K2[i + 1] == a2 && K1[i + 1] == a1 && K0[i + 1] == a0;
     if (!eq_prev && !eq_next) { out[i] = V[i]; return; }
     u64 s = i, e = i + 1;
     while (s > 0 && K2[s - 1] == a2 && K1[s - 1] == a1 && K0[s - 1] == a0) --s;
@@ -2727,24 +2588,7 @@ hipError_t msa_launch_col_write(int text, const u8 *buf, const u64 *len, const u
     hipLaunchKernelGGL(k_col_collapse, grid1(nrec), dim3(256), 0, s, buf, len, off, src, pairs, nrec, hdr, col);
     return hipGetLastError();
 }
-hipError_t msa_launch_rec_text(const u8 *buf, const u64 *rs, const u32 *nul, const u64 *tss, const u64 *tse, u64 nrec,
-                               u64 first_rec, u64 *tlen, u64 *tsrc, u32 *tpairs, Counters *ctr, hipStream_t s) {
-    if (!nrec) return hipSuccess;
-    const SpanOut o{nullptr, nullptr, nullptr, tlen, tsrc, tpairs};
-    const AKeys ak{};
-    hipLaunchKernelGGL(k_rec_text, grid1(nrec), dim3(256), 0, s, buf, rs, nul, tss, tse, nrec, first_rec, o, ctr, ak);
-    return hipGetLastError();
-}
 // text.csv's body with the LDS-free gather (beside the token pass)
-hipError_t msa_launch_text_gather_w(const u8 *buf, const u64 *len, const u64 *off, const u64 *src, const u32 *pairs,
-                                    u64 nrec, u64 hdr, const u64 *body_p, u8 *col, hipStream_t s) {
-    hipLaunchKernelGGL(k_zero_tail, dim3(1), dim3(256), 0, s, col, hdr, body_p, (u32)MSA_INPUT_PAD);
-    if (!nrec) return hipGetLastError();
-    hipLaunchKernelGGL(k_col_gather_w, dim3((u32)((nrec + CW_T - 1) / CW_T)), dim3(CW_T), 0, s, buf, len, off, src,
-                       nrec, hdr, body_p, col);
-    hipLaunchKernelGGL(k_col_collapse, grid1(nrec), dim3(256), 0, s, buf, len, off, src, pairs, nrec, hdr, col);
-    return hipGetLastError();
-}
 hipError_t msa_launch_artist_key(const u8 *col, const u64 *ar_start, const u64 *line_off, const u64 *line_len, u64 hdr,
                                  u64 nrec, u8 *arena, u64 *key_off, u32 *key_len, u64 *key_slot, u64 *atab, u64 amask,
                                  u32 *alist, u64 alist_cap, Counters *ctr, u64 short_base, int cus, int abl,
@@ -2889,6 +2733,7 @@ hipError_t msa_launch_rank_small(u64 *const K2[3], u64 *const K1[3], u64 *const 
 hipError_t msa_launch_fixup(const u64 *K2, const u64 *K1, const u64 *K0, const u32 *V, u64 n, const u64 *ref,
                             const u8 *buf, const u8 *extra, const u64 *l_pos, const u32 *l_len, const u8 *arena, const u64 *key_off,
                             const u32 *key_len, u32 *out, hipStream_t s) {
+    if (!K0) return hipErrorInvalidValue;  // k_tie_fixup compares 16-byte prefixes
     if (n)
         hipLaunchKernelGGL(k_tie_fixup, grid1(n), dim3(256), 0, s, K2, K1, K0, V, n, ref, buf, extra, l_pos, l_len, arena,
                            key_off, key_len, out);

@@ -1811,8 +1811,7 @@ extern "C" int msa_wcs_run(msa_wcs *w) {
             WCHECK(hipMemcpyAsync(&hc, ctr, sizeof hc, hipMemcpyDeviceToHost, st));
             WCHECK(hipStreamSynchronize(st));
             WCHECK(hipEventElapsedTime(&w->wrows_ms, w->ev_a, w->ev_b));
-            if (getenv("MSA_WCS_DEBUG")) fprintf(stderr, "k_wcs_wrows: %llu of %llu rows left to k_wcs_rows\n",
-                                                 (unsigned long long)hc.fallback, (unsigned long long)(R - 2));
+            // (the count is the summary's fallback_rows)
             w->fallback_rows = hc.fallback;
             if (hc.fallback) {
                 a.rows = fb;

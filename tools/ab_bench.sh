@@ -1,5 +1,5 @@
 # End-to-end A/B: bench.py ms_per_step per library variant, alternating (run ON the GPU box):
-#   bash tools/ab_bench.sh OUT variant...   ("base" = the in-tree build; "v@N": with MSA_ABLATE=N)
+#   bash tools/ab_bench.sh OUT variant...   ("base" = the in-tree build; "v@N": with MSA_ABLATE=N -- a -DMSA_DIAG=1 variant build)
 set -e
 out=gpurun_out/$1; shift
 mkdir -p gpurun_out

@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
-"""Diagnostic: time K3 (k_scan_csv) under kernel ablations (MSA_ABLATE bits,
-see msa_k3.hip), with its LDS-table miss count.  K3's ablation bits are
-compiled in only with -DK3_ABLATE=1 (`make variant V=abl FLAGS=-DK3_ABLATE=1`,
-then MSA_LIB=.../libmsa_hip_abl.so); bit 0 (no ablation) times any build.  Results of ablated runs are wrong by design; only the
+"""Diagnostic: time the split scan (k_scan_struct + k_scan_tokens) under
+kernel ablations (MSA_ABLATE bits, see msa_k3.hip / msa_api.hip), with its
+LDS-table miss count.  The product library reads no MSA_ABLATE: build a
+diagnostic variant (`make -C music-analyst-ai_amd variant V=abl
+FLAGS="-DMSA_DIAG=1 -DK3_ABLATE=1"`, then MSA_LIB=.../build/libmsa_hip_abl.so).  Results of ablated runs are wrong by design; only the
 stage times are read.  Usage: python tools/ablate.py [songs] [bits ...]"""
 import ctypes as C
 import os
