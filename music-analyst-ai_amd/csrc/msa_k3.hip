@@ -30,6 +30,9 @@ namespace {
 #endif
 #define Q_W (Q_T / 64)
 #define Q_BLK 4096               // bytes per wave-iteration
+#ifndef TOK_PF
+#define TOK_PF 1                 // batches of key loads in flight ahead of the probed one
+#endif
 // Token keys are re-read from the input (just loaded: L1/L2) rather than
 // from an LDS copy of the block, which leaves the LDS to the word table and
 // to a per-wave list of the block's token starts: the lanes share the tokens
@@ -500,15 +503,23 @@ __device__ __forceinline__ void tok_phase(const ScanArgs &a, u64 ib, u64 lpos, u
     // dword; the next 64 tokens' loads are issued before this batch is
     // probed, so their latency hides behind the LDS work.
     const u32 nb = (nS + 63) >> 6;
-    u32 en = 0;
-    uint4 kv = make_uint4(0, 0, 0, 0);
-    u32 k4 = 0;
-    if (lane < nS) {
-        en = list[lane];
-        const u32 *gp = reinterpret_cast<const u32 *>(a.buf + ((ib + (en & 4095u)) & ~3ull));
-        kv = *reinterpret_cast<const uint4 *>(gp);
-        k4 = gp[4];
-    }
+    // key loads of batch j (a stale list entry past the list's end addresses
+    // a byte inside the block: harmless, and the loop's vector memory sequence
+    // stays the same every trip)
+    auto kload = [&](u32 j, u32 &e, uint4 &v, u32 &v4) {
+        e = list[min(j * 64 + lane, (u32)Q_LIST - 1u)];
+        const u32 *gp = reinterpret_cast<const u32 *>(a.buf + ((ib + (e & 4095u)) & ~3ull));
+        v = *reinterpret_cast<const uint4 *>(gp);
+        v4 = gp[4];
+    };
+    u32 en, k4;
+    uint4 kv;
+    kload(0, en, kv, k4);
+#if TOK_PF > 1
+    u32 en2, k42;  // batch bt + 2's, TOK_PF = 2: two batches of key loads in flight
+    uint4 kv2;
+    kload(1, en2, kv2, k42);
+#endif
     for (u32 bt = 0; bt < nb; ++bt) {
         bool mis = false;
         u64 k0 = 0, k1 = KMARK;
@@ -516,13 +527,14 @@ __device__ __forceinline__ void tok_phase(const ScanArgs &a, u64 ib, u64 lpos, u
         const uint4 v = kv;
         const u32 v4 = k4;
         const bool have = bt * 64 + lane < nS;
-        {  // unconditional (a stale list entry: an address inside the block), so
-           // that the loop's vector memory sequence is the same every trip
-            en = list[min((bt + 1) * 64 + lane, (u32)Q_LIST - 1u)];
-            const u32 *gp = reinterpret_cast<const u32 *>(a.buf + ((ib + (en & 4095u)) & ~3ull));
-            kv = *reinterpret_cast<const uint4 *>(gp);
-            k4 = gp[4];
-        }
+#if TOK_PF > 1
+        en = en2;
+        kv = kv2;
+        k4 = k42;
+        kload(bt + 2, en2, kv2, k42);
+#else
+        kload(bt + 1, en, kv, k4);
+#endif
         if (have) {
             const u32 len = (e >> 12) + 3;
             const u32 sh = (u32)(ib + (e & 4095u)) & 3u;

@@ -128,3 +128,46 @@ def test_mpirun_cli_without_gpu_fails_cleanly(tmp_path):
     p = subprocess.run([MPIRUN, "-np", "2", cli, str(csv), "--processes", "2", "--output-dir", str(tmp_path / "o")],
                        capture_output=True, timeout=120, env=env)
     assert p.returncode != 0 and b"--processes cannot be combined" in p.stderr
+
+
+# ---------------------------------------------------------------- RCCL transport
+# host/msa_rccl.c against the in-process HIP / RCCL stand-ins of
+# host/test_stub (host memory, a thread per rank, RCCL's send/recv matching):
+# the transport's bookkeeping -- not RCCL itself, which the GPU tests run.
+RCCL_BIN = os.path.join(PKG, "bin", "msa_rccl_test")
+
+
+@pytest.fixture(scope="module")
+def rccl_bin():
+    if not os.path.exists(RCCL_BIN):
+        subprocess.run(["make", "-C", PKG, "bin/msa_rccl_test"], check=True, capture_output=True, timeout=120)
+    return RCCL_BIN
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_rccl_transport_exchanges(rccl_bin, world):
+    """All-gathers and all-to-all-v rounds where some rank pairs exchange
+    nothing (an empty send or receive must not be posted: RCCL would wait for
+    it), on the transport's own stream and on an external one (no host wait);
+    every pool buffer and stream released at the end."""
+    p = subprocess.run([rccl_bin, "exchange", str(world)], capture_output=True, timeout=60)
+    assert p.returncode == 0, p.stderr
+
+
+def test_rccl_transport_pool(rccl_bin):
+    """The device buffer pool: a free buffer that fits is reused, at most 16
+    are in use (a 17th request fails), and the smallest free one is evicted to
+    make room for a larger request."""
+    p = subprocess.run([rccl_bin, "pool"], capture_output=True, timeout=60)
+    assert p.returncode == 0, p.stderr
+    assert b"more than 16 transport buffers in use" in p.stderr
+
+
+@pytest.mark.parametrize("what,msg", [("initfail", b"ncclCommInitRank"), ("mallocfail", b"hipMalloc")])
+def test_rccl_transport_failures(rccl_bin, what, msg):
+    """msa_tr_rccl failing to set up its communicator returns NULL with
+    nothing left allocated; an exchange buffer the device cannot provide
+    fails that request only."""
+    p = subprocess.run([rccl_bin, what], capture_output=True, timeout=60)
+    assert p.returncode == 0, p.stderr
+    assert msg in p.stderr
