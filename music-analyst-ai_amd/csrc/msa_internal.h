@@ -288,7 +288,7 @@ struct Counters {
                      // larger logs; at the logs' size limit inserted straight into HBM)
 };
 
-enum { OVF_S = 1, OVF_M = 2, OVF_L = 4, OVF_LT = 8, OVF_A = 16, OVF_REC = 32, OVF_MLOG = 64 };
+enum { OVF_S = 1, OVF_M = 2, OVF_L = 4, OVF_LT = 8, OVF_A = 16, OVF_REC = 32, OVF_MLOG = 64, OVF_FOLD = 128 };
 
 // Artist keys built by k_rec_spans for the lines shortcut of the artist pass:
 // per record the key bytes (duplicate_field(duplicate_field(field0, 1), 0))
@@ -340,6 +340,18 @@ struct ScanArgs {
     u32 *mlog_n;
     u32 mlog_cap;
     int mlog_direct; // the logs are at their size limit: a full partition's entries go to the HBM tables
+    // folded split scan (k_scan_fold: K1 + K2 + k_scan_struct in one pass):
+    // tiles of 4 chunks taken in ticket order (ticket - fold_tbase), each
+    // publishing its chunk functions' composition, then its end state, as
+    // self-validating words (epoch fold_ep in bits 48-63) in fold_stat: 5
+    // arrays of fold_n words (3 function entries, 2 state words)
+    u64 *fold_stat;
+    u64 *fold_ticket;
+    u64 fold_tbase;
+    u32 fold_n, fold_ep;
+    State fold_init;
+    State *fold_fin;       // the state after the segment (device)
+    State *fold_fin_host;  // the same, into pinned host memory
     // split scan (k_scan_struct -> k_scan_tokens): bit i of lmask[1 + i / 64]
     // = byte seg_begin + i is a token byte of a counted lyric field
     // (process_lyrics input, parallel_spotify.c:350-394); lmask[0] = 0 pad

@@ -1,0 +1,101 @@
+// msa_k1.h -- the chunk transfer function of the CSV reader (K1), one 4 KiB
+// block at a time, from the block's byte-class masks.  Shared by the
+// stand-alone summary kernel (k_chunk_summary, msa_scan.hip: the artist column
+// and CPU-free callers) and the folded split scan (k_scan_fold, msa_k3.hip).
+//
+// Follows the record reader of the reference (read_csv_record,
+// parallel_spotify.c:549-633): a terminator is an unquoted '\r' or an unquoted
+// '\n' not preceded by an unquoted '\r'; unquoted commas count the fields
+// (parse_csv_line 258-304, saturated at 3); a NUL ends the C string.
+#pragma once
+#include "msa_internal.h"
+
+// bit j = xor of bits < j (the quote parity before each byte)
+__device__ __forceinline__ u64 k1_pxor_excl64(u64 q) {
+    u64 x = q << 1;
+    x ^= x << 1;
+    x ^= x << 2;
+    x ^= x << 4;
+    x ^= x << 8;
+    x ^= x << 16;
+    x ^= x << 32;
+    return x;
+}
+
+// A chunk's function under both incoming quote parities (h = 0 / 1), built
+// block by block.  Per lane: terminators seen (summed over the wave once per
+// chunk); wave-uniform: the rest.
+struct K1Acc {
+    u32 par, first_nl, anyrare;
+    u32 cr[2], ntl[2], cc[2], zz[2], lend[2];
+};
+__device__ __forceinline__ void k1_init(K1Acc &s) {
+    s.par = s.first_nl = s.anyrare = 0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) s.cr[h] = s.ntl[h] = s.cc[h] = s.zz[h] = s.lend[h] = 0;
+}
+
+// One block: the lane's 64-byte masks (bytes past the chunk end cleared), the
+// raw '\n' flag of the byte after the block (the '\r\n' swallow at lane 63),
+// off = the block's offset in the chunk, lastb = the offset of its last valid
+// byte in the block.
+__device__ __forceinline__ void k1_block(K1Acc &s, u64 Q, u64 C, u64 NL, u64 CR, u64 Z, bool rare, u32 nb_nl,
+                                         u32 off, u32 lastb) {
+    const u32 lane = lane_id();
+    s.anyrare |= rare ? 1u : 0u;
+    if (off == 0) s.first_nl = (u32)(readlane64(NL, 0) & 1u);
+    const u64 B = __ballot(__popcll(Q) & 1u);
+    const u32 pin0 = s.par ^ (mbcnt(B) & 1u);
+    const u64 inq0 = k1_pxor_excl64(Q) ^ (pin0 ? ~0ull : 0ull);
+    s.par ^= (u32)__popcll(B) & 1u;
+    const u64 dn = __shfl_down(NL, 1);
+    const u64 nlnext = (NL >> 1) | ((u64)((lane == 63) ? nb_nl : (u32)(dn & 1u)) << 63);
+    const int Lz = (int)(lastb >> 6);
+    const u32 bz = lastb & 63u;
+    const u64 Bz = __ballot(Z != 0);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const u64 inq = h ? ~inq0 : inq0;
+        const u64 CRu = CR & ~inq, NLu = NL & ~inq, Cu = C & ~inq;
+        const u64 up = __shfl_up(CRu, 1);
+        const u64 pc0 = lane ? ((up >> 63) & 1u) : (u64)s.cr[h];
+        const u64 TERM = CRu | (NLu & ~((CRu << 1) | pc0));
+        const u32 nt = (u32)__popcll(TERM);
+        s.ntl[h] += nt;
+        const u32 cq = min((u32)__popcll(Cu), 3u);
+        const u64 C1 = __ballot(cq >= 1u), C2 = __ballot(cq >= 2u), C3 = __ballot(cq >= 3u);
+        const u64 Bh = __ballot(nt != 0);
+        if (Bh) {
+            const int jl = 63 - __clzll(Bh);
+            const u64 A = (jl == 63) ? 0ull : (~0ull << (jl + 1));  // lanes after jl
+            const u64 tj = readlane64(TERM, jl);
+            const u32 lt_j = 63u - (u32)__clzll(tj);
+            const u64 above = lt_j == 63 ? 0ull : (~0ull << (lt_j + 1));
+            const u32 c_new = (u32)__popcll(readlane64(Cu, jl) & above) + (u32)__popcll(C1 & A) +
+                              (u32)__popcll(C2 & A) + (u32)__popcll(C3 & A);
+            s.cc[h] = min(c_new, 3u);
+            s.zz[h] = ((readlane64(Z, jl) & above) != 0) | ((Bz & A) != 0);
+            const u32 sw_j = (u32)(((readlane64(CRu, jl) & readlane64(nlnext, jl)) >> lt_j) & 1u);
+            s.lend[h] = off + (u32)jl * 64u + lt_j + 1u + sw_j;
+        } else {
+            s.cc[h] = min(s.cc[h] + (u32)__popcll(C1) + (u32)__popcll(C2) + (u32)__popcll(C3), 3u);
+            s.zz[h] |= (Bz != 0);
+        }
+        s.cr[h] = (u32)((readlane64(CRu, Lz) >> bz) & 1u);
+    }
+}
+
+// The chunk's summary (wave-uniform; <= 16384 terminators a chunk: 15 bits)
+__device__ __forceinline__ ChunkSum k1_finish(const K1Acc &s) {
+    ChunkSum r;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        u32 tot = 0;
+#pragma unroll
+        for (int b = 0; b < 15; ++b) tot += (u32)__popcll(__ballot((s.ntl[h] >> b) & 1u)) << b;
+        r.h[h] = tot | (s.cc[h] << 16) | (s.zz[h] << 18) | (s.cr[h] << 19) | (s.par << 20) | (s.first_nl << 21) |
+                 (s.anyrare << 22);
+        r.last_end[h] = s.lend[h];
+    }
+    return r;
+}

@@ -19,6 +19,7 @@
 //     (4-slot buckets); keys the LDS table cannot hold are batched per wave
 //     and inserted into the HBM tables asynchronously (pipelined loads).
 #include "msa_internal.h"
+#include "msa_k1.h"
 #include "msa_tables.h"
 
 #include <algorithm>
@@ -711,6 +712,325 @@ __global__ __launch_bounds__(SA_T, SA_MINW) void k_scan_struct(ScanArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// k_scan_fold: K1 + K2 + k_scan_struct in one pass over the input.  A
+// workgroup of FD_CH waves takes a tile of FD_CH consecutive chunks (a wave
+// each) in ticket order and
+//   A. classifies its chunk's four blocks once, keeping the byte-class masks
+//      in registers, and builds the chunk's transfer function from them (K1's
+//      k1_block over the same masks);
+//   B. wave 0 composes the tile's function, publishes it, and looks back over
+//      the earlier tiles' published functions / end states (decoupled
+//      look-back, 64 tiles a round trip, a log-depth composition across the
+//      wave) for the tile's entry state; it publishes the tile's end state
+//      and hands every chunk its entry state through LDS;
+//   C. every wave runs the record structure over its masks (struct_block)
+//      and writes the token-byte mask, as k_scan_struct does.
+// The input is read once (k_chunk_summary + k_scan_struct read it twice).
+// Statuses are self-validating 64-bit words (epoch in bits 48-63, relaxed
+// agent-scope atomics: no fence, no memset between launches): entries of the
+// tile function pack nterm (17 bits), rs - tile start (17), p, cr, c, z; the
+// end state packs rec (40) | p, cr, c, z and rs (48).
+#define FD_CH 4
+#define FD_T (FD_CH * 64)
+#ifndef FD_MINW
+#define FD_MINW 4
+#endif
+#define FD_SPIN_LIMIT (1u << 24)  // polls before a look-back gives up (error, never a hang)
+
+__device__ __forceinline__ u64 fd_ld(const u64 *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ void fd_st(u64 *p, u64 v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ u64 fd_pack_ent(const FnEnt &e, u64 tb, u64 ep) {
+    return e.nterm | ((e.rs - tb) << 17) | ((u64)e.p << 34) | ((u64)e.cr << 35) | ((u64)e.c << 36) |
+           ((u64)e.z << 38) | (ep << 48);
+}
+__device__ __forceinline__ u64 fd_pack_rec(const State &s, u64 ep) {
+    return s.rec | ((u64)s.p << 40) | ((u64)s.cr << 41) | ((u64)s.c << 42) | ((u64)s.z << 44) | (ep << 48);
+}
+__device__ __forceinline__ State fd_unpack_state(u64 wa, u64 wb) {
+    State s;
+    s.rec = wa & ((1ull << 40) - 1ull);
+    s.p = (u32)(wa >> 40) & 1u;
+    s.cr = (u32)(wa >> 41) & 1u;
+    s.c = (u32)(wa >> 42) & 3u;
+    s.z = (u32)(wa >> 44) & 1u;
+    s.rs = wb & ((1ull << 48) - 1ull);
+    return s;
+}
+// The look-back's functions in registers: three named entries (no array --
+// an entry picked by (p, cr) out of an array is a dynamic index, i.e. scratch
+// memory), picked by masks.  fl = p | cr << 1 | c << 3 | z << 5; has = nt != 0.
+struct LEnt {
+    u64 nt, rs;
+    u32 fl;
+};
+struct LFn {
+    LEnt e0, e1, e2;
+};
+__device__ __forceinline__ LEnt le_unpack(u64 w, u64 tb) {
+    LEnt e;
+    e.nt = w & 0x1FFFFull;
+    e.rs = tb + ((w >> 17) & 0x1FFFFull);
+    e.fl = ((u32)(w >> 34) & 3u) | (((u32)(w >> 36) & 7u) << 3);
+    return e;
+}
+__device__ __forceinline__ LEnt le_identity(u32 idx) {
+    LEnt e;
+    e.nt = 0;
+    e.rs = 0;
+    e.fl = idx == 1 ? 1u : (idx == 2 ? 2u : 0u);
+    return e;
+}
+__device__ __forceinline__ LFn lf_identity() { return LFn{le_identity(0), le_identity(1), le_identity(2)}; }
+__device__ __forceinline__ LEnt le_pick(const LFn &g, u32 p, u32 cr) {
+    const u64 m2 = cr ? ~0ull : 0ull, m1 = (!cr && p) ? ~0ull : 0ull, m0 = ~(m1 | m2);
+    LEnt r;
+    r.nt = (g.e0.nt & m0) | (g.e1.nt & m1) | (g.e2.nt & m2);
+    r.rs = (g.e0.rs & m0) | (g.e1.rs & m1) | (g.e2.rs & m2);
+    r.fl = (g.e0.fl & (u32)m0) | (g.e1.fl & (u32)m1) | (g.e2.fl & (u32)m2);
+    return r;
+}
+// fn_then (msa_internal.h) on LEnt
+__device__ __forceinline__ LEnt le_then(const LEnt &a, const LFn &g) {
+    const LEnt b = le_pick(g, a.fl & 1u, (a.fl >> 1) & 1u);
+    LEnt r;
+    r.nt = a.nt + b.nt;
+    if (b.nt) {
+        r.fl = b.fl;
+        r.rs = b.rs;
+    } else {
+        const u32 c = min(((a.fl >> 3) & 3u) + ((b.fl >> 3) & 3u), 3u);
+        r.fl = (b.fl & 3u) | (c << 3) | ((a.fl | b.fl) & 32u);
+        r.rs = a.rs;
+    }
+    return r;
+}
+__device__ __forceinline__ LFn lf_compose(const LFn &f, const LFn &g) {  // f then g
+    return LFn{le_then(f.e0, g), le_then(f.e1, g), le_then(f.e2, g)};
+}
+// fn_apply (msa_internal.h) on LFn
+__device__ __forceinline__ State lf_apply(const State &s, const LFn &f) {
+    const LEnt b = le_pick(f, s.p, s.cr);
+    State r;
+    r.p = b.fl & 1u;
+    r.cr = (b.fl >> 1) & 1u;
+    r.rec = s.rec + b.nt;
+    if (b.nt) {
+        r.c = (b.fl >> 3) & 3u;
+        r.z = (b.fl >> 5) & 1u;
+        r.rs = b.rs;
+    } else {
+        r.c = min(s.c + ((b.fl >> 3) & 3u), 3u);
+        r.z = s.z | ((b.fl >> 5) & 1u);
+        r.rs = s.rs;
+    }
+    return r;
+}
+__device__ __forceinline__ LEnt le_shfl_up(const LEnt &e, u32 d) {
+    return LEnt{__shfl_up(e.nt, d), __shfl_up(e.rs, d), __shfl_up(e.fl, d)};
+}
+__device__ __forceinline__ LEnt le_readlane(const LEnt &e, int l) {
+    return LEnt{readlane64(e.nt, l), readlane64(e.rs, l), readlane(e.fl, l)};
+}
+__device__ __forceinline__ LFn lf_readlane(const LFn &f, int l) {
+    return LFn{le_readlane(f.e0, l), le_readlane(f.e1, l), le_readlane(f.e2, l)};
+}
+__device__ __forceinline__ State fd_uniform(const State &s) {
+    State r;
+    r.rec = readlane64(s.rec, 0);
+    r.rs = readlane64(s.rs, 0);
+    r.p = readlane(s.p, 0);
+    r.cr = readlane(s.cr, 0);
+    r.c = readlane(s.c, 0);
+    r.z = readlane(s.z, 0);
+    return r;
+}
+
+// The entry state of tile `tile` (> 0), by wave 0: 64 earlier tiles' statuses
+// a round trip (lane l: tile j0 - l).  The nearest published end state
+// (lane k) with every tile after it published at least as a function: that
+// state pushed through lanes k-1 .. 0 (H_{k-1} = F_{k-1} then ... then F_0,
+// an inclusive scan across the lanes) and through the compositions of the
+// newer windows (acc).  A window without an end state is composed whole and
+// the look-back moves 64 tiles further.
+__device__ __forceinline__ State fd_lookback(const ScanArgs &a, u32 tile, u64 ep) {
+    const u32 lane = lane_id();
+    const u64 *W0 = a.fold_stat, *W1 = W0 + a.fold_n, *W2 = W1 + a.fold_n, *W3 = W2 + a.fold_n,
+              *W4 = W3 + a.fold_n;
+    const u64 tile_bytes = (u64)FD_CH * MSA_CHUNK;
+    LFn acc = lf_identity();
+    bool have_acc = false;
+    long long j0 = (long long)tile - 1;
+    u32 spins = 0;
+    for (;;) {
+        const long long t = j0 - (long long)lane;
+        u64 w0 = 0, w1 = 0, w2 = 0, w3 = 0, w4 = 0;
+        if (t >= 0) {
+            w3 = fd_ld(W3 + t);
+            w4 = fd_ld(W4 + t);
+            w0 = fd_ld(W0 + t);
+            w1 = fd_ld(W1 + t);
+            w2 = fd_ld(W2 + t);
+        }
+        const bool inc = (w3 >> 48) == ep && (w4 >> 48) == ep;
+        const bool agg = (w0 >> 48) == ep && (w1 >> 48) == ep && (w2 >> 48) == ep;
+        const u64 Bin = __ballot(t >= 0), Binc = __ballot(t >= 0 && inc), Bok = __ballot(t >= 0 && (inc || agg));
+        const u32 k = Binc ? (u32)__ffsll((long long)Binc) - 1u : 64u;
+        const u64 need = Binc ? bits_lo(k) : Bin;
+        if ((Bok & need) != need) {  // a tile in between has not published yet
+            if (++spins > FD_SPIN_LIMIT) {
+                if (lane == 0) atomicOr((unsigned long long *)&a.ctr->overflow, (unsigned long long)OVF_FOLD);
+                return a.fold_init;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        const u32 nl = Binc ? k : (u32)__popcll(Bin);
+        const u64 tb = a.seg_begin + (u64)(t >= 0 ? t : 0) * tile_bytes;
+        LFn F = lf_identity();
+        if (lane < nl) F = LFn{le_unpack(w0, tb), le_unpack(w1, tb), le_unpack(w2, tb)};
+        for (u32 d = 1; d < nl; d <<= 1) {  // X_l = X_l then X_{l-d} (older first)
+            const LFn Y{le_shfl_up(F.e0, d), le_shfl_up(F.e1, d), le_shfl_up(F.e2, d)};
+            if (lane >= d) F = lf_compose(F, Y);
+        }
+        if (Binc) {
+            State S = fd_unpack_state(readlane64(w3, (int)k), readlane64(w4, (int)k));
+            if (k) S = lf_apply(S, lf_readlane(F, (int)k - 1));
+            if (have_acc) S = lf_apply(S, acc);
+            return S;
+        }
+        const LFn Wn = lf_readlane(F, (int)nl - 1);
+        acc = have_acc ? lf_compose(Wn, acc) : Wn;
+        have_acc = true;
+        j0 -= 64;
+    }
+}
+
+__global__ __launch_bounds__(FD_T, FD_MINW) void k_scan_fold(ScanArgs a) {
+    __shared__ Fn s_fn[FD_CH];
+    __shared__ State s_st[FD_CH];
+    __shared__ u32 s_tile;
+    const u32 lane = lane_id();
+    const u32 wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const u32 ntiles = (a.nchunks + FD_CH - 1) / FD_CH;
+    const u64 ep = a.fold_ep;
+    // a chunk's block j and the 16 bytes after it (no block: the chunk's first
+    // block again, which exists)
+    auto load_blk = [&](u64 cbase, u64 cend, u32 j, uint4 (&v)[4], uint4 &t) {
+        u64 ib = cbase + (u64)j * Q_BLK;
+        if (ib >= cend) ib = cbase;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = ldg16(a.buf + ib + lane * 64 + 16 * q);
+        u64 ta = ib + Q_BLK < a.seg_end ? ib + Q_BLK : ib;
+        pin64(ta);
+        t = ldg16(a.buf + ta);
+    };
+    // (measured: taking the next tile's ticket during the look-back, to load its
+    // first block while this tile's structure runs, made the kernel 1.37 ms
+    // instead of 0.85 -- tiles then start a whole phase after their tickets and
+    // their successors' look-backs wait for them)
+    for (;;) {
+        if (threadIdx.x == 0) {
+            const u64 tk = atomicAdd((unsigned long long *)a.fold_ticket, 1ull) - a.fold_tbase;
+            s_tile = (u32)min(tk, (u64)ntiles);
+        }
+        __syncthreads();
+        const u32 tile = __builtin_amdgcn_readfirstlane(s_tile);
+        if (tile >= ntiles) break;
+        const u32 c = tile * FD_CH + wib;
+        const bool has = c < a.nchunks;
+        const u64 cbase = a.seg_begin + (u64)c * MSA_CHUNK;
+        const u64 cend = has ? min(cbase + (u64)MSA_CHUNK, a.seg_end) : cbase;
+        // ---- A: the chunk's byte classes (kept) and its transfer function
+        Masks m[4];
+        u32 tb[4];  // the byte after each block | (it exists) << 8
+        Fn g = fn_identity(cbase);
+        if (has) {
+            K1Acc acc;
+            k1_init(acc);
+            uint4 v[4], t;
+            load_blk(cbase, cend, 0, v, t);
+#pragma unroll
+            for (u32 j = 0; j < 4; ++j) {
+                const u64 ib = cbase + (u64)j * Q_BLK;
+                const bool valid = ib < cend;
+                uint4 cv[4] = {v[0], v[1], v[2], v[3]};
+                const uint4 ct = t;
+                if (j + 1 < 4) load_blk(cbase, cend, j + 1, v, t);
+                const u64 lpos = ib + lane * 64;
+                const u64 rem = valid && cend > lpos ? cend - lpos : 0;
+                m[j] = classify64x(cv, (u32)min(rem, (u64)64), true);
+                const u32 tex = ib + Q_BLK < a.seg_end ? 1u : 0u;
+                tb[j] = (ct.x & 0xFFu) | (tex << 8);
+                if (valid) {
+                    const u32 nb_nl = (tex && (ct.x & 0xFFu) == '\n') ? 1u : 0u;
+                    const u32 lastb = (u32)(min(ib + (u64)Q_BLK, cend) - 1 - ib);
+                    k1_block(acc, m[j].Q, m[j].C, m[j].NL, m[j].CR, m[j].Z, false, nb_nl, j * Q_BLK, lastb);
+                }
+            }
+            const ChunkSum cs = k1_finish(acc);
+#pragma unroll
+            for (u32 i = 0; i < 3; ++i) g.e[i] = chunk_entry(cs, cbase, i);
+        }
+        if (lane == 0) s_fn[wib] = g;
+        __syncthreads();
+        // ---- B: the tile's function published, its entry state looked up
+        if (wib == 0) {
+            // (the functions stay in LDS: a local copy of an Fn is an array the
+            // entry selects index, i.e. scratch memory)
+            const u64 tbase = a.seg_begin + (u64)tile * FD_CH * MSA_CHUNK;
+            State S;
+            if (tile == 0) {
+                S = a.fold_init;
+            } else {
+                u64 pk[3];
+#pragma unroll
+                for (int i = 0; i < 3; ++i) {
+                    const FnEnt e = fn_then(fn_then(fn_then(s_fn[0].e[i], s_fn[1]), s_fn[2]), s_fn[3]);
+                    pk[i] = fd_pack_ent(e, tbase, ep);
+                }
+                if (lane < 3) fd_st(a.fold_stat + (u64)lane * a.fold_n + tile, lane == 0 ? pk[0] : (lane == 1 ? pk[1] : pk[2]));
+                S = fd_uniform(fd_lookback(a, tile, ep));
+            }
+            const State s1 = fn_apply(S, s_fn[0]), s2 = fn_apply(s1, s_fn[1]), s3 = fn_apply(s2, s_fn[2]),
+                        E = fn_apply(s3, s_fn[3]);
+            const u64 wa = fd_pack_rec(E, ep), wb = E.rs | (ep << 48);
+            if (lane < 2) fd_st(a.fold_stat + (u64)(3 + lane) * a.fold_n + tile, lane == 0 ? wa : wb);
+            if (lane == 0) {
+                s_st[0] = S;
+                s_st[1] = s1;
+                s_st[2] = s2;
+                s_st[3] = s3;
+                if (tile + 1 == ntiles) {
+                    *a.fold_fin = E;
+                    if (a.fold_fin_host) *a.fold_fin_host = E;
+                }
+            }
+        }
+        __syncthreads();
+        // ---- C: the record structure of the chunk from its masks
+        if (has) {
+            State st = fd_uniform(s_st[wib]);
+            u32 prevQ = 0;
+            if (cbase > a.seg_begin) {
+                const size_t pa = (size_t)(a.buf + cbase - 1);
+                const u32 b = (*sload(reinterpret_cast<const u32 *>(pa & ~(size_t)3)) >> (8 * (pa & 3))) & 0xFFu;
+                prevQ = (u32)(b == '"');
+            }
+#pragma unroll
+            for (u32 j = 0; j < 4; ++j) {
+                const u64 ib = cbase + (u64)j * Q_BLK;
+                if (ib < cend) {
+                    const u64 lpos = ib + lane * 64;
+                    const u64 live = struct_block(a, st, m[j], make_uint4(tb[j] & 0xFFu, 0, 0, 0), tb[j] >> 8, lpos, prevQ);
+                    prevQ = readlane((u32)(m[j].Q >> 63), 63);
+                    a.lmask[1 + ((ib - a.seg_begin) >> 6) + lane] = m[j].T & live;
+                }
+            }
+        }
+    }
+}
+
 // k_scan_tokens: the token phase of the split scan over k_scan_struct's
 // lmask -- no reader state, no byte classes: a wave per 4 KiB block (grid
 // stride), token starts and lengths from the mask, keys re-read from the
@@ -1029,6 +1349,19 @@ hipError_t msa_launch_scan_csv(const ScanArgs &a, hipStream_t s) {
     // a wave per chunk, SA_MINW waves per SIMD while chunks last
     const u32 waves = std::min<u32>(a.nchunks, (u32)g_q_cus * 4 * SA_MINW);
     hipLaunchKernelGGL(k_scan_struct, dim3((waves + SA_T / 64 - 1) / (SA_T / 64)), dim3(SA_T), 0, s, a);
+    return hipGetLastError();
+}
+// The folded split scan (k_scan_fold); *tickets = the tickets it takes (the
+// next launch's fold_tbase advances by that many)
+u32 msa_fold_tiles(u32 nchunks) { return (nchunks + FD_CH - 1) / FD_CH; }
+hipError_t msa_launch_scan_fold(const ScanArgs &a, u64 *tickets, hipStream_t s) {
+    *tickets = 0;
+    if (!a.nchunks) return hipSuccess;
+    (void)scan_blocks(a);  // the device's CU count
+    const u32 ntiles = msa_fold_tiles(a.nchunks);
+    const u32 grid = std::min<u32>(ntiles, (u32)g_q_cus * FD_MINW);
+    hipLaunchKernelGGL(k_scan_fold, dim3(grid), dim3(FD_T), 0, s, a);
+    *tickets = (u64)ntiles + grid;
     return hipGetLastError();
 }
 hipError_t msa_launch_scan_tokens(const ScanArgs &a, hipStream_t s) {

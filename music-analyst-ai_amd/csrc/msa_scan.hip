@@ -20,6 +20,7 @@
 // Every wave moves 1 KiB per iteration as one coalesced dwordx4 per lane; all
 // cross-lane work is ballot/mbcnt based (64-wide wavefronts).
 #include "msa_internal.h"
+#include "msa_k1.h"
 #include "msa_tables.h"
 
 namespace {
@@ -111,17 +112,6 @@ __device__ __forceinline__ Classes64 classify64(const uint4 (&v)[4], u64 lpos, u
     k.Q &= vm; k.C &= vm; k.NL &= vm; k.CR &= vm; k.Z &= vm;
     return k;
 }
-__device__ __forceinline__ u64 pxor_excl64(u64 q) {  // bit j = xor of bits < j
-    u64 x = q << 1;
-    x ^= x << 1;
-    x ^= x << 2;
-    x ^= x << 4;
-    x ^= x << 8;
-    x ^= x << 16;
-    x ^= x << 32;
-    return x;
-}
-
 #ifndef K1_MINW
 #define K1_MINW 5  // min waves per SIMD: 96 VGPRs, 5 waves (4 at 111 VGPRs: 0.362 -> 0.338 ms; 6 and 8 spill: 0.43, 0.89)
 #endif
@@ -139,9 +129,8 @@ __global__ __launch_bounds__(256, K1_MINW) void k_chunk_summary(const u8 *__rest
     for (u32 c = gw; c < nchunks; c += nw) {
         const u64 cbase = seg_begin + (u64)c * MSA_CHUNK;
         const u64 cend = min(cbase + (u64)MSA_CHUNK, seg_end);
-        u32 par = 0, first_nl = 0, anyrare = 0;
-        // terminators per lane, summed over the wave once per chunk (not per block)
-        u32 cr[2] = {0, 0}, ntl[2] = {0, 0}, cc[2] = {0, 0}, zz[2] = {0, 0}, lend[2] = {0, 0};
+        K1Acc acc;
+        k1_init(acc);
         for (u64 ibase = cbase; ibase < cend; ibase += K1_ITER) {
             const u64 lpos = ibase + lane * 64;
             // one iteration ahead: the chunk's next block, else the wave's next
@@ -156,70 +145,16 @@ __global__ __launch_bounds__(256, K1_MINW) void k_chunk_summary(const u8 *__rest
                 for (int q = 0; q < 4; ++q) nxt[q] = ld16(buf + nb + 16 * q);
             }
             const Classes64 k = classify64(cur, lpos, cend);
-            anyrare |= k.rare ? 1u : 0u;
-            if (ibase == cbase) first_nl = (u32)(readlane64(k.NL, 0) & 1u);
-            const u64 B = __ballot(__popcll(k.Q) & 1u);
-            const u32 pin0 = par ^ (mbcnt(B) & 1u);
-            const u64 inq0 = pxor_excl64(k.Q) ^ (pin0 ? ~0ull : 0ull);
-            par ^= (u32)__popcll(B) & 1u;
             // raw '\n' at the following byte (for the '\r\n' swallow)
             const u64 nb_pos = ibase + K1_ITER;
             const u32 nb_nl = (nb_pos < seg_end && buf[nb_pos] == '\n') ? 1u : 0u;
-            const u64 dn = __shfl_down(k.NL, 1);
-            const u64 nlnext = (k.NL >> 1) | ((u64)((lane == 63) ? nb_nl : (u32)(dn & 1u)) << 63);
             const u32 lastb = (u32)(min(ibase + (u64)K1_ITER, cend) - 1 - ibase);
-            const int Lz = (int)(lastb >> 6);
-            const u32 bz = lastb & 63u;
-            const u64 Bz = __ballot(k.Z != 0);
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const u64 inq = h ? ~inq0 : inq0;
-                const u64 CRu = k.CR & ~inq, NLu = k.NL & ~inq, Cu = k.C & ~inq;
-                const u64 up = __shfl_up(CRu, 1);
-                const u64 pc0 = lane ? ((up >> 63) & 1u) : (u64)cr[h];
-                const u64 TERM = CRu | (NLu & ~((CRu << 1) | pc0));
-                const u32 nt = (u32)__popcll(TERM);
-                ntl[h] += nt;
-                const u32 cq = min((u32)__popcll(Cu), 3u);
-                const u64 C1 = __ballot(cq >= 1u), C2 = __ballot(cq >= 2u), C3 = __ballot(cq >= 3u);
-                const u64 Bh = __ballot(nt != 0);
-                if (Bh) {
-                    const int jl = 63 - __clzll(Bh);
-                    const u64 A = (jl == 63) ? 0ull : (~0ull << (jl + 1));  // lanes after jl
-                    const u64 tj = readlane64(TERM, jl);
-                    const u32 lt_j = 63u - (u32)__clzll(tj);
-                    const u64 above = lt_j == 63 ? 0ull : (~0ull << (lt_j + 1));
-                    const u32 c_new = (u32)__popcll(readlane64(Cu, jl) & above) + (u32)__popcll(C1 & A) +
-                                      (u32)__popcll(C2 & A) + (u32)__popcll(C3 & A);
-                    cc[h] = min(c_new, 3u);
-                    zz[h] = ((readlane64(k.Z, jl) & above) != 0) | ((Bz & A) != 0);
-                    const u32 sw_j = (u32)(((readlane64(CRu, jl) & readlane64(nlnext, jl)) >> lt_j) & 1u);
-                    lend[h] = (u32)(ibase - cbase) + (u32)jl * 64u + lt_j + 1u + sw_j;
-                } else {
-                    cc[h] = min(cc[h] + (u32)__popcll(C1) + (u32)__popcll(C2) + (u32)__popcll(C3), 3u);
-                    zz[h] |= (Bz != 0);
-                }
-                cr[h] = (u32)((readlane64(CRu, Lz) >> bz) & 1u);
-            }
+            k1_block(acc, k.Q, k.C, k.NL, k.CR, k.Z, k.rare, nb_nl, (u32)(ibase - cbase), lastb);
 #pragma unroll
             for (int q = 0; q < 4; ++q) cur[q] = nxt[q];
         }
-        u32 nterm[2];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {  // <= 16384 terminators per chunk: 15 bits
-            u32 tot = 0;
-#pragma unroll
-            for (int b = 0; b < 15; ++b) tot += (u32)__popcll(__ballot((ntl[h] >> b) & 1u)) << b;
-            nterm[h] = tot;
-        }
-        if (lane == 0) {
-            ChunkSum s;
-            for (int h = 0; h < 2; ++h) {
-                s.h[h] = nterm[h] | (cc[h] << 16) | (zz[h] << 18) | (cr[h] << 19) | (par << 20) | (first_nl << 21) | (anyrare << 22);
-                s.last_end[h] = lend[h];
-            }
-            out[c] = s;
-        }
+        const ChunkSum sum = k1_finish(acc);
+        if (lane == 0) out[c] = sum;
     }
 }
 
