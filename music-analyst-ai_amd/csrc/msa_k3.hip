@@ -1240,12 +1240,14 @@ __global__ __launch_bounds__(MB_TT) void k_mb_scatter(ScanArgs a, u32 chunks, u3
 // one claim per distinct key of a bucket (CAS first: most keys are new)
 __device__ __forceinline__ void mb_insert_once(const ScanArgs &a, u64 k0, u64 k1m, u64 cnt) {
     if (k1m == KMARK) {
-        u64 h = fmix64(k0) & a.s_mask;
+        u64 h = fmix64(k0) & a.s_mask, rest;
+        const u64 claim = tab_claim(k0, cnt, &rest);
         for (u32 probe = 0; probe < MSA_MAX_PROBE; ++probe) {
             u64 *slot = a.s_tab + 2 * h;
-            const u64 old = atomicCAS((unsigned long long *)slot, 0ull, (unsigned long long)k0);
-            if (old == 0 || old == k0) {
-                atomicAdd((unsigned long long *)(slot + 1), (unsigned long long)cnt);
+            const u64 old = atomicCAS((unsigned long long *)slot, 0ull, (unsigned long long)claim);
+            if (old == 0 || (old & TAB_KEY7) == k0) {
+                const u64 add = old == 0 ? rest : cnt;
+                if (add) atomicAdd((unsigned long long *)(slot + 1), (unsigned long long)add);
                 return;
             }
             h = (h + 1) & a.s_mask;
@@ -1254,17 +1256,18 @@ __device__ __forceinline__ void mb_insert_once(const ScanArgs &a, u64 k0, u64 k1
         return;
     }
     const u64 k1 = k1m & ~KMARK;
-    u64 h = fmix64(k0 ^ fmix64(k1)) & a.m_mask;
+    u64 h = fmix64(k0 ^ fmix64(k1)) & a.m_mask, rest;
+    const u64 claim = tab_claim(k0, cnt, &rest);
     u32 probe = 0, spins = 0;
     while (probe < MSA_MAX_PROBE) {
         u64 *slot = a.m_tab + 4 * h;
-        const u64 c0 = atomicCAS((unsigned long long *)slot, 0ull, (unsigned long long)k0);
+        const u64 c0 = atomicCAS((unsigned long long *)slot, 0ull, (unsigned long long)claim);
         if (c0 == 0) {
             __hip_atomic_store(slot + 1, k1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            atomicAdd((unsigned long long *)(slot + 2), (unsigned long long)cnt);
+            if (rest) atomicAdd((unsigned long long *)(slot + 2), (unsigned long long)rest);
             return;
         }
-        if (c0 == k0) {
+        if ((c0 & TAB_KEY7) == k0) {
             const u64 c1 = __hip_atomic_load(slot + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (c1 == 0) {  // claimed, k1 not yet visible: retry this slot
                 if (++spins > (1u << 24)) break;

@@ -67,16 +67,18 @@ __device__ void exp_entry(const ExpSrc &x, u64 e, u64 *count, u32 *len, u64 *k0,
     }
     if (e < x.ns) {
         const u64 slot = x.s_list[e];
-        *k0 = x.s_tab[2 * slot];
-        *count = x.s_tab[2 * slot + 1];
+        const u64 w0 = x.s_tab[2 * slot];
+        *k0 = w0 & TAB_KEY7;
+        *count = x.s_tab[2 * slot + 1] + tab_gather8(w0);
         u32 n = 0;
         while (n < 8 && ((*k0 >> (8 * n)) & 0xFF)) ++n;
         *len = n;
     } else if (e < x.ns + x.nm) {
         const u64 slot = x.m_list[e - x.ns];
-        *k0 = x.m_tab[4 * slot];
+        const u64 w0 = x.m_tab[4 * slot];
+        *k0 = w0 & TAB_KEY7;
         *k1 = x.m_tab[4 * slot + 1];
-        *count = x.m_tab[4 * slot + 2];
+        *count = x.m_tab[4 * slot + 2] + tab_gather8(w0);
         u32 n = 8;
         while (n < 16 && ((*k1 >> (8 * (n - 8))) & 0xFF)) ++n;
         *len = n;

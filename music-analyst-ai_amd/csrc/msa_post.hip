@@ -1703,16 +1703,17 @@ __global__ __launch_bounds__(256) void k_word_entries(EntryArgs a) {
         u64 c, hi, lo, ref;
         if (i < a.ns) {
             const u64 slot = a.s_list[i];
-            const u64 key = a.s_tab[2 * slot];
-            c = a.s_tab[2 * slot + 1];
+            const u64 w0 = a.s_tab[2 * slot], key = w0 & TAB_KEY7;
+            c = a.s_tab[2 * slot + 1] + tab_gather8(w0);
             hi = __builtin_bswap64(key);
             lo = 0;
             ref = ((u64)KIND_S << 60) | slot;
         } else if (i < a.ns + a.nm) {
             const u64 slot = a.m_list[i - a.ns];
-            hi = __builtin_bswap64(a.m_tab[4 * slot]);
+            const u64 w0 = a.m_tab[4 * slot];
+            hi = __builtin_bswap64(w0 & TAB_KEY7);
             lo = __builtin_bswap64(a.m_tab[4 * slot + 1]);
-            c = a.m_tab[4 * slot + 2];
+            c = a.m_tab[4 * slot + 2] + tab_gather8(w0);
             ref = ((u64)KIND_M << 60) | slot;
         } else {
             const u64 slot = a.l_list[i - a.ns - a.nm];
@@ -2102,13 +2103,11 @@ __device__ __forceinline__ u64 entry_key_len(u64 ref, u64 k1, u64 k0, const u32 
     const u64 idx = ref & ((1ull << 60) - 1);
     if (kind == KIND_L) return l_len[idx];
     if (kind == KIND_A) return key_len[idx];
-    u64 n = 0;
-    for (int i = 0; i < 16; ++i) {
-        const u8 b = (u8)((i < 8 ? k1 : k0) >> (56 - 8 * (i & 7)));
-        if (!b) break;
-        ++n;
-    }
-    return n;
+    // S/M key bytes are nonzero and big-endian here, zero padded: the length
+    // is the nonzero bytes above the trailing zero bytes
+    const u64 n1 = k1 ? 8 - ((u64)__builtin_ctzll(k1) >> 3) : 0;
+    if (n1 < 8) return n1;
+    return 8 + (k0 ? 8 - ((u64)__builtin_ctzll(k0) >> 3) : 0);
 }
 
 // SortedKeys: the sorted (K2, K1, K0) planes, position i = rank i (entries tied

@@ -17,6 +17,39 @@
 
 #define MSA_MAX_PROBE 4096u
 
+// S / M keys are lower-cased token bytes (< 0x80) and zero padding, so bit 7
+// of every byte of the first key word is free: a claim writes the key with a
+// count of at most 255 spread over those bits (bit j of the count -> bit
+// 8 j + 7), one CAS for a new key instead of a claim and a count add (the
+// high-cardinality inserts are at the memory-side atomic rate).  A slot's
+// count = its count word + the bits of its first key word; the key = that
+// word & TAB_KEY7.
+#define TAB_KEY7 0x7F7F7F7F7F7F7F7Full
+__host__ __device__ __forceinline__ u64 tab_spread8(u64 c) {  // c < 256
+    u64 r = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r |= ((c >> j) & 1ull) << (8 * j + 7);
+    return r;
+}
+__host__ __device__ __forceinline__ u64 tab_gather8(u64 w) {  // bit 8 j + 7 -> bit j
+    u64 r = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r |= ((w >> (8 * j + 7)) & 1ull) << j;
+    return r;
+}
+// the claim value of a key word and the count left for the count word
+#ifndef TAB_EMBED
+#define TAB_EMBED 1  // 0: the key alone, the count always by an add (A/B builds)
+#endif
+__device__ __forceinline__ u64 tab_claim(u64 k0, u64 cnt, u64 *rest) {
+    if (TAB_EMBED && cnt < 256) {
+        *rest = 0;
+        return k0 | tab_spread8(cnt);
+    }
+    *rest = cnt;
+    return k0;
+}
+
 // Probe by CAS straight away (the CAS returns the slot's key: one L2 atomic
 // per probe) instead of an atomic load first and a CAS only on an empty slot
 // (two for every new key: the high-cardinality inserts).  TAB_CAS_FIRST=0
@@ -96,17 +129,18 @@ __device__ __forceinline__ void stage_flush(const u32 *staged, const u32 *nst, u
 template <bool LIST = true, bool CASF = (TAB_CAS_FIRST != 0)>
 __device__ __forceinline__ void s_insert(u64 *tab, u64 mask, u64 key, u64 cnt, u32 *list,
                                          u64 list_cap, Counters *ctr) {
-    u64 h = fmix64(key) & mask;
+    u64 h = fmix64(key) & mask, rest;
+    const u64 claim = tab_claim(key, cnt, &rest);
     bool isnew = false, found = false;
     for (u32 probe = 0; probe < MSA_MAX_PROBE; ++probe) {
         u64 *slot = tab + 2 * h;
-        const u64 cur = probe_word<CASF>(slot, key);
-        if (cur == 0) {
-            atomicAdd((unsigned long long *)(slot + 1), (unsigned long long)cnt);
+        const u64 cur = probe_word<CASF>(slot, claim);
+        if (cur == 0) {  // claimed with the count (or the count word takes it)
+            if (rest) atomicAdd((unsigned long long *)(slot + 1), (unsigned long long)rest);
             isnew = found = true;
             break;
         }
-        if (cur == key) {
+        if ((cur & TAB_KEY7) == key) {
             atomicAdd((unsigned long long *)(slot + 1), (unsigned long long)cnt);
             found = true;
             break;
@@ -124,19 +158,20 @@ __device__ __forceinline__ void s_insert(u64 *tab, u64 mask, u64 key, u64 cnt, u
 template <bool LIST = true, bool CASF = (TAB_CAS_FIRST != 0)>
 __device__ __forceinline__ void m_insert(u64 *tab, u64 mask, u64 k0, u64 k1, u64 cnt, u32 *list,
                                          u64 list_cap, Counters *ctr) {
-    u64 h = fmix64(k0 ^ fmix64(k1)) & mask;
+    u64 h = fmix64(k0 ^ fmix64(k1)) & mask, rest;
+    const u64 claim = tab_claim(k0, cnt, &rest);
     u32 probe = 0, spins = 0;
     bool isnew = false, found = false;
     while (probe < MSA_MAX_PROBE) {
         u64 *slot = tab + 4 * h;
-        const u64 c0 = probe_word<CASF>(slot, k0);
+        const u64 c0 = probe_word<CASF>(slot, claim);
         if (c0 == 0) {
             __hip_atomic_store(slot + 1, k1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            atomicAdd((unsigned long long *)(slot + 2), (unsigned long long)cnt);
+            if (rest) atomicAdd((unsigned long long *)(slot + 2), (unsigned long long)rest);
             isnew = found = true;
             break;
         }
-        if (c0 == k0) {
+        if ((c0 & TAB_KEY7) == k0) {
             u64 c1 = ld_relaxed(slot + 1);
             if (c1 == 0) {  // claimed, k1 not yet visible: retry this slot
                 if (++spins > (1u << 24)) break;
