@@ -18,7 +18,13 @@ codec (latin-1, cp1252, ...; msa.single_byte_codec) reads every byte as one
 character and writes it back unchanged, so the GPU's byte-level split is the
 script's; the header names are decoded and written in that codec, and input
 holding a byte the codec leaves undefined raises the script's
-UnicodeDecodeError.  The GPU reader takes one-byte ASCII delimiters and
+UnicodeDecodeError.  Known divergence, on that error path only: the error
+comes from decoding the whole file at once, so its message gives the byte's
+position in the file, where the script's TextIOWrapper reports it within the
+chunk it was decoding; and when the byte lies past the script's 64 KiB sniff
+sample the script has already written the column files' first rows when it
+fails, while this path fails before writing any column file
+(tests/test_split_oracle.py::test_split_undefined_byte_late).  The GPU reader takes one-byte ASCII delimiters and
 quotechars other than CR, LF, NUL (and each other); multi-byte codecs other
 than UTF-8 (UTF-16, Shift-JIS, ...) and other characters are refused.
 """

@@ -75,3 +75,22 @@ def test_split_oracle_matches_reference(name):
         hdr = b"" if no_header else _header_line(h, delim, quote).encode(tenc)
         assert want == (BOM if strip else b"") + hdr + bodies[i - 1], cand
     assert sorted(names) == sorted(exp)
+
+
+def test_split_undefined_byte_late(tmp_path):
+    """The documented divergence of msa/split_columns.py on input with a byte
+    the codec leaves undefined (0x81 in cp1252) past the 64 KiB sniff sample:
+    UnicodeDecodeError before any GPU work, and no column file written (the
+    script writes the first rows before its reader reaches the byte)."""
+    from msa.split_columns import split_csv_columns
+
+    rows = b"".join(b"A%d,s,l,words here\n" % i for i in range(5000))
+    data = b"artist,song,link,text\n" + rows + b"B,s,l,bad \x81 byte\n"
+    assert data.index(b"\x81") > 65536
+    src = tmp_path / "in.csv"
+    src.write_bytes(data)
+    out = tmp_path / "out"
+    with pytest.raises(UnicodeDecodeError) as e:
+        split_csv_columns(str(src), output_dir=str(out), delimiter=",", encoding="cp1252")
+    assert e.value.start == data.index(b"\x81")  # the position in the whole file
+    assert not out.exists() or not any(out.iterdir())
