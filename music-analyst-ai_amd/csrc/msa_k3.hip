@@ -445,9 +445,18 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t mlog_rsrc(const ScanArgs &a) {
 }
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 
+// Long-word positions: each wave takes ranges of l_pos from Counters::l_occ
+// lch slots at a time (one device atomic per range, not per block: every
+// wave adding to that one word once per 4 KiB block serialised at the
+// memory side -- 3.1 of configs[4]'s 3.9 ms token pass); the slots of a range
+// a wave does not fill are set to LP_NONE (k_long_insert skips them).
+#define LP_NONE (~0ull)
+__device__ __forceinline__ void lpos_fill(const ScanArgs &a, u64 from, u64 to) {
+    for (u64 k = from + lane_id(); k < to && k < a.l_cap; k += 64) a.l_pos[k] = LP_NONE;
+}
 __device__ __forceinline__ void tok_phase(const ScanArgs &a, u64 ib, u64 lpos, u64 w, u64 Tn, u64 S0, u64 *skeys,
                                           u32 *scnts, u16 *list, u32 *lcur,
-                                          u64 &words, __amdgpu_buffer_rsrc_t rsrc) {
+                                          u64 &words, __amdgpu_buffer_rsrc_t rsrc, u64 &lres, u64 &lend, u64 lch) {
     const u32 lane = lane_id();
     // runs: rK bit b = bytes b .. b+K-1 are token bytes (w = Tn:T)
     const u64 r2 = w & shr128(w, Tn, 1), r2h = Tn & (Tn >> 1);
@@ -461,14 +470,21 @@ __device__ __forceinline__ void tok_phase(const ScanArgs &a, u64 ib, u64 lpos, u
     words += (u64)__popcll(S0 & r3);
 
     // long words (> 16 bytes): positions for k_long_insert
-    const u64 BL = __ballot(sL != 0);
+    const u64 BL = (K3_ABLATE && (a.ablate & 256)) ? 0ull : __ballot(sL != 0);  // 256: no long-word positions
     if (BL) {
         const u32 nl = (u32)__popcll(sL);
         u32 tot;
         const u32 pre = wave_prefix<6>(nl, tot);
-        u64 base = 0;
-        if (lane == 0) base = atomicAdd((unsigned long long *)&a.ctr->l_occ, (unsigned long long)tot);
-        base = readlane64(base, 0) + pre;
+        if (lres + tot > lend) {  // a new range (the rest of the old one unused)
+            lpos_fill(a, lres, lend);
+            const u64 want = tot > lch ? (u64)tot : lch;
+            u64 b = 0;
+            if (lane == 0) b = atomicAdd((unsigned long long *)&a.ctr->l_occ, (unsigned long long)want);
+            lres = readlane64(b, 0);
+            lend = lres + want;
+        }
+        u64 base = lres + pre;
+        lres += tot;
         for (u64 m = sL; m; m &= m - 1) {
             const u32 b = (u32)__ffsll((long long)m) - 1;
             if (base < a.l_cap) a.l_pos[base] = (lpos + b) | a.lpos_tag;
@@ -570,6 +586,7 @@ __device__ __forceinline__ void tok_phase(const ScanArgs &a, u64 ib, u64 lpos, u
         // their size limit (2^24 - 1 entries a partition: mlog_direct), where
         // the entry goes straight into the HBM table
         u32 off = 0xFFFFFFF0u;
+        if (K3_ABLATE && (a.ablate & 512)) mis = false;  // 512: misses neither counted nor stored
         if (mis) {
             const u32 part = mlog_part(k0, k1);
             const u32 at = atomicAdd(&lcur[part], 1u);
@@ -1062,6 +1079,9 @@ __global__ __launch_bounds__(Q_T, 1) void k_scan_tokens(ScanArgs a) {
     const u32 gw = __builtin_amdgcn_readfirstlane(blockIdx.x * Q_W + wib);
     const u32 nw = gridDim.x * Q_W;
     u64 words = 0;
+    // this wave's range of l_pos; ranges of ~a quarter of an even share of the capacity, 64..1024
+    u64 lres = 0, lend = 0;
+    const u64 lch = min<u64>(1024, max<u64>(64, a.l_cap / ((u64)nw * 4)));
     // mask words of the block: this lane's, the one after it and the one before
     u64 Lc = 0, Ln = 0, Lp = 0;
     uint4 warm = make_uint4(0, 0, 0, 0);
@@ -1081,8 +1101,9 @@ __global__ __launch_bounds__(Q_T, 1) void k_scan_tokens(ScanArgs a) {
         const u64 ib = a.seg_begin + blk * Q_BLK;
         const u64 lpos = ib + lane * 64;
         const u64 S0 = L & ~((L << 1) | (Lprev >> 63));
-        tok_phase(a, ib, lpos, L, Lnext, S0, skeys, scnts, list, lcur, words, rsrc);
+        tok_phase(a, ib, lpos, L, Lnext, S0, skeys, scnts, list, lcur, words, rsrc, lres, lend, lch);
     }
+    lpos_fill(a, lres, lend);
     tok_epilogue(a, skeys, scnts, lcur, words);
 }
 

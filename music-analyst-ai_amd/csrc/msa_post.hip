@@ -1578,6 +1578,11 @@ __global__ void k_long_insert(const u8 *__restrict__ buf, u64 seg_end, const u8 
                               u64 *ltab, u64 lmask, u32 *llist, u64 llist_cap, Counters *ctr) {
     const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
+    if (l_pos[i] == ~0ull) {  // a slot of a token-pass range left unused (msa_k3.hip LP_NONE)
+        l_len[i] = 0;
+        l_slot[i] = ~0ull;
+        return;
+    }
     u32 len;
     const u64 h = long_hash(buf, seg_end, extra, extra_len, l_pos[i], len);
     l_len[i] = len;
