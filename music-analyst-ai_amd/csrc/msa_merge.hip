@@ -84,7 +84,7 @@ __device__ void exp_entry(const ExpSrc &x, u64 e, u64 *count, u32 *len, u64 *k0,
         *len = n;
     } else {
         const u64 slot = x.l_list[e - x.ns - x.nm];
-        *count = x.l_tab[4 * slot + 1];
+        *count = x.l_tab[4 * slot + 1] + 1;  // h_insert IMPL1
         const u64 rep = x.l_tab[4 * slot + 2];
         *len = x.l_len[rep];
         *lp = tok_at(x.buf, x.extra, x.l_pos[rep]);
@@ -209,7 +209,7 @@ __global__ void k_imp_insert(const u8 *in, const u64 *blk_off, const u64 *rec_ba
         d.l_pos[i] = kpos | MSA_POS_EXTRA;
         d.l_len[i] = len;
         const u64 h = bytes_hash(in + kpos, len, 1);
-        d.l_slot[i] = h_insert(d.l_tab, d.l_mask, h, count, i, d.l_list, d.l_list_cap, &d.ctr->l_claimed, d.ctr,
+        d.l_slot[i] = h_insert<true, true>(d.l_tab, d.l_mask, h, count, i, d.l_list, d.l_list_cap, &d.ctr->l_claimed, d.ctr,
                                OVF_LT);
     }
 }

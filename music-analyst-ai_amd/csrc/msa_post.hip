@@ -1586,7 +1586,7 @@ __global__ void k_long_insert(const u8 *__restrict__ buf, u64 seg_end, const u8 
     u32 len;
     const u64 h = long_hash(buf, seg_end, extra, extra_len, l_pos[i], len);
     l_len[i] = len;
-    l_slot[i] = h_insert(ltab, lmask, h, 1, i, llist, llist_cap, &ctr->l_claimed, ctr, OVF_LT);
+    l_slot[i] = h_insert<true, true>(ltab, lmask, h, 1, i, llist, llist_cap, &ctr->l_claimed, ctr, OVF_LT);
 }
 
 __device__ __forceinline__ u64 lower8x(u64 x) {  // 'A'..'Z' -> 'a'..'z' in each byte (bytes >= 0x80 kept)
@@ -1722,7 +1722,7 @@ __global__ __launch_bounds__(256) void k_word_entries(EntryArgs a) {
             ref = ((u64)KIND_M << 60) | slot;
         } else {
             const u64 slot = a.l_list[i - a.ns - a.nm];
-            c = a.l_tab[4 * slot + 1];
+            c = a.l_tab[4 * slot + 1] + 1;  // h_insert IMPL1: the first occurrence is implicit
             const u64 rep = a.l_tab[4 * slot + 2];
             const u64 lp = a.l_pos[rep];
             be16w((lp & MSA_POS_EXTRA) ? a.extra : a.buf, lp & ~MSA_POS_EXTRA, a.l_len[rep], 1, &hi, &lo);

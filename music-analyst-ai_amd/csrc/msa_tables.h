@@ -196,7 +196,10 @@ __device__ __forceinline__ void m_insert(u64 *tab, u64 mask, u64 k0, u64 k1, u64
 // LIST false: no list append; *isnew_out tells the caller (k_long_insert
 // stages its new slots per workgroup: a claim per wave on the one counter
 // had serialised at the memory side)
-template <bool LIST = true>
+// IMPL1 (the long-word table): a claimed slot counts one occurrence without
+// an add -- its count word holds the occurrences past the first (readers add
+// 1), so a new word's insert is a claim and the rep store, no count add
+template <bool LIST = true, bool IMPL1 = false>
 __device__ __forceinline__ u64 h_insert(u64 *tab, u64 mask, u64 hash, u64 cnt, u64 rep, u32 *list,
                                         u64 list_cap, u64 *claimed, Counters *ctr, u64 ovf_bit,
                                         bool *isnew_out = nullptr) {
@@ -208,7 +211,8 @@ __device__ __forceinline__ u64 h_insert(u64 *tab, u64 mask, u64 hash, u64 cnt, u
         const u64 cur = probe_word(slot, hash);
         if (cur == 0) {
             __hip_atomic_store(slot + 2, rep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            atomicAdd((unsigned long long *)(slot + 1), (unsigned long long)cnt);
+            const u64 add = IMPL1 ? cnt - 1 : cnt;
+            if (add) atomicAdd((unsigned long long *)(slot + 1), (unsigned long long)add);
             isnew = true;
             res = h;
             break;
