@@ -1813,6 +1813,16 @@ static int do_rank(msa_ctx *c, int tables = 3) {
     };
     int arc = MSA_OK;
     HIPC(c, ensure(c->blob_tot, 64));  // shared by both tables' blob scans: allocated before the thread
+    if (conc_thread) {
+        // the artists' entry arrays sized here, not on the ranking thread: a
+        // regrowth frees a buffer, and hipFree waits for the whole device (the
+        // words' passes included).  The sort's own buffers still grow there on
+        // a larger table than any before -- the first runs, not steady state.
+        for (int k = 0; k < 3; ++k) HIPC(c, ensure(A.K[0][k], A.n * 8));
+        HIPC(c, ensure(A.V[0], A.n * 4));
+        HIPC(c, ensure(A.ref, A.n * 8));
+        HIPC(c, ensure(A.cnt, A.n * 8));
+    }
     std::thread ath;
     struct TJoin {
         std::thread &t;
