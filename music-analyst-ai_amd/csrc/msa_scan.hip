@@ -121,10 +121,18 @@ __global__ __launch_bounds__(256, K1_MINW) void k_chunk_summary(const u8 *__rest
     const u32 lane = lane_id();
     const u32 gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const u32 nw = (gridDim.x * blockDim.x) >> 6;
+    // the byte after a block (raw '\n' there: the '\r\n' swallow at lane 63),
+    // loaded with the block, an iteration ahead and BEFORE that block's data:
+    // vector loads complete in order, so a byte load issued after the next
+    // block's prefetch made every iteration wait for that prefetch
+    auto nbyte = [&](u64 pos) -> u32 { return pos < seg_end ? (u32)buf[pos] : 0u; };
     uint4 cur[4];  // a chunk's first block: loaded during the previous chunk's last one
+    u32 nb_cur = 0;
     if (gw < nchunks) {
+        const u64 b0 = seg_begin + (u64)gw * MSA_CHUNK;
+        nb_cur = nbyte(b0 + K1_ITER);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) cur[q] = ld16(buf + seg_begin + (u64)gw * MSA_CHUNK + lane * 64 + 16 * q);
+        for (int q = 0; q < 4; ++q) cur[q] = ld16(buf + b0 + lane * 64 + 16 * q);
     }
     for (u32 c = gw; c < nchunks; c += nw) {
         const u64 cbase = seg_begin + (u64)c * MSA_CHUNK;
@@ -134,24 +142,26 @@ __global__ __launch_bounds__(256, K1_MINW) void k_chunk_summary(const u8 *__rest
         for (u64 ibase = cbase; ibase < cend; ibase += K1_ITER) {
             const u64 lpos = ibase + lane * 64;
             // one iteration ahead: the chunk's next block, else the wave's next
-            // chunk (reads end < cend + 4096, MSA_INPUT_PAD)
+            // chunk (reads end < cend + 4096, MSA_INPUT_PAD); its following byte first
             uint4 nxt[4] = {cur[0], cur[1], cur[2], cur[3]};
+            u32 nb_next = 0;
             if (ibase + K1_ITER < cend) {
+                nb_next = nbyte(ibase + 2 * K1_ITER);
 #pragma unroll
                 for (int q = 0; q < 4; ++q) nxt[q] = ld16(buf + lpos + K1_ITER + 16 * q);
             } else if (c + nw < nchunks) {
-                const u64 nb = seg_begin + (u64)(c + nw) * MSA_CHUNK + lane * 64;
+                const u64 b1 = seg_begin + (u64)(c + nw) * MSA_CHUNK;
+                nb_next = nbyte(b1 + K1_ITER);
 #pragma unroll
-                for (int q = 0; q < 4; ++q) nxt[q] = ld16(buf + nb + 16 * q);
+                for (int q = 0; q < 4; ++q) nxt[q] = ld16(buf + b1 + lane * 64 + 16 * q);
             }
             const Classes64 k = classify64(cur, lpos, cend);
-            // raw '\n' at the following byte (for the '\r\n' swallow)
-            const u64 nb_pos = ibase + K1_ITER;
-            const u32 nb_nl = (nb_pos < seg_end && buf[nb_pos] == '\n') ? 1u : 0u;
+            const u32 nb_nl = nb_cur == '\n' ? 1u : 0u;
             const u32 lastb = (u32)(min(ibase + (u64)K1_ITER, cend) - 1 - ibase);
             k1_block(acc, k.Q, k.C, k.NL, k.CR, k.Z, k.rare, nb_nl, (u32)(ibase - cbase), lastb);
 #pragma unroll
             for (int q = 0; q < 4; ++q) cur[q] = nxt[q];
+            nb_cur = nb_next;
         }
         const ChunkSum sum = k1_finish(acc);
         if (lane == 0) out[c] = sum;
