@@ -22,6 +22,20 @@ __device__ __forceinline__ u64 k1_pxor_excl64(u64 q) {
     return x;
 }
 
+// lane l receives lane l+1's value (lane 63: 0) / lane l-1's (lane 0: 0):
+// DPP wave shifts (VALU, a few cycles) instead of ds_bpermute (LDS latency in
+// the block's dependency chain)
+__device__ __forceinline__ u64 k1_from_next(u64 v) {
+    const u32 lo = __builtin_amdgcn_update_dpp(0u, (u32)v, 0x130, 0xF, 0xF, false);
+    const u32 hi = __builtin_amdgcn_update_dpp(0u, (u32)(v >> 32), 0x130, 0xF, 0xF, false);
+    return ((u64)hi << 32) | lo;
+}
+__device__ __forceinline__ u64 k1_from_prev(u64 v) {
+    const u32 lo = __builtin_amdgcn_update_dpp(0u, (u32)v, 0x138, 0xF, 0xF, false);
+    const u32 hi = __builtin_amdgcn_update_dpp(0u, (u32)(v >> 32), 0x138, 0xF, 0xF, false);
+    return ((u64)hi << 32) | lo;
+}
+
 // A chunk's function under both incoming quote parities (h = 0 / 1), built
 // block by block.  Per lane: terminators seen (summed over the wave once per
 // chunk); wave-uniform: the rest.
@@ -48,7 +62,7 @@ __device__ __forceinline__ void k1_block(K1Acc &s, u64 Q, u64 C, u64 NL, u64 CR,
     const u32 pin0 = s.par ^ (mbcnt(B) & 1u);
     const u64 inq0 = k1_pxor_excl64(Q) ^ (pin0 ? ~0ull : 0ull);
     s.par ^= (u32)__popcll(B) & 1u;
-    const u64 dn = __shfl_down(NL, 1);
+    const u64 dn = k1_from_next(NL);  // every lane active (whole-wave calls)
     const u64 nlnext = (NL >> 1) | ((u64)((lane == 63) ? nb_nl : (u32)(dn & 1u)) << 63);
     const int Lz = (int)(lastb >> 6);
     const u32 bz = lastb & 63u;
@@ -57,7 +71,7 @@ __device__ __forceinline__ void k1_block(K1Acc &s, u64 Q, u64 C, u64 NL, u64 CR,
     for (int h = 0; h < 2; ++h) {
         const u64 inq = h ? ~inq0 : inq0;
         const u64 CRu = CR & ~inq, NLu = NL & ~inq, Cu = C & ~inq;
-        const u64 up = __shfl_up(CRu, 1);
+        const u64 up = k1_from_prev(CRu);
         const u64 pc0 = lane ? ((up >> 63) & 1u) : (u64)s.cr[h];
         const u64 TERM = CRu | (NLu & ~((CRu << 1) | pc0));
         const u32 nt = (u32)__popcll(TERM);
