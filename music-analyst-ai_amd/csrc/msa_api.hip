@@ -57,6 +57,7 @@ hipError_t msa_launch_artist_key(const u8 *, const u64 *, const u64 *, const u64
 hipError_t msa_launch_long(const u8 *, u64, const u8 *, u64, const u64 *, u64, u32 *, u64 *, u64 *, u64, u32 *, u64,
                            Counters *, hipStream_t);
 hipError_t msa_launch_word_entries(const EntryArgs &, hipStream_t);
+u64 msa_dn_vary_words();
 hipError_t msa_launch_list_build(const u64 *, u64, u32, u32 *, u64, u64 *, Counters *, u64, hipStream_t);
 hipError_t msa_launch_artist_entries(const u64 *, const u32 *, u64, const u8 *, const u64 *, const u32 *, u64 *, u64 *,
                                      u64 *, u32 *, u64 *, u64 *, hipStream_t);
@@ -253,6 +254,18 @@ struct msa_ctx {
     int mb_mode = 0;
     u64 mb_min = 24000000;
     u64 mb_prev = 0;     // the last split's logged misses
+    // Dense entries (k_mb_agg<true>): a split whose previous run counted at
+    // least dense_min distinct 3..16-byte words (high cardinality) buckets its
+    // logs and writes the words' ranking entries directly -- no HBM word
+    // table inserts, slot lists, table clears or k_word_entries over them.
+    // Single GPU only (the multi-GPU merge exports the tables).  env
+    // MSA_DENSE=0 turns it off, MSA_DENSE_MIN sets the threshold.
+    bool dense_on = true;
+    u64 dense_min = 4000000;
+    u64 prev_distinct = 0;  // the last split's distinct S + M words
+    bool dense_w = false;   // the current split's words are dense entries (Ranked rw's planes)
+    bool dense_veto = false;  // a dense split overflowed (a bucket past its LDS table): tables from now on
+    bool sharded = false;     // msa_set_shard was called: a multi-GPU shard
     DevBuf lmask;         // the split scan's lyric token-byte mask (k_scan_struct -> k_scan_tokens)
     u64 s_slots = 0, m_slots = 0, l_occ_cap = 0, lt_slots = 0, a_slots = 0;
     u64 s_used_prev = 0, m_used_prev = 0, lt_used_prev = 0, a_used_prev = 0;
@@ -880,9 +893,16 @@ static int split_columns_rest(msa_ctx *c, bool want_text, const std::string &ah,
     return MSA_OK;
 }
 
+// The S/M slots a split claimed (cleared by the next split's prologue); a
+// dense split claims none.
+static void set_used_prev(msa_ctx *c) {
+    c->s_used_prev = c->dense_w ? 0 : std::min<u64>(c->h_ctr.s_claimed, c->s_slots / 2);
+    c->m_used_prev = c->dense_w ? 0 : std::min<u64>(c->h_ctr.m_claimed, c->m_slots / 2);
+}
 // Word-table overflows of the scan (S/M tables, long-word occurrence list):
 // the split is repeated with grown tables (msa_split_columns' retry loop).
-static const u64 kSplitOvf = OVF_S | OVF_M | OVF_L | OVF_MLOG;  // OVF_MLOG: K3 dropped misses (logs grown)
+// OVF_MLOG: K3 dropped misses (logs grown); OVF_DENSE: a dense split's retry
+static const u64 kSplitOvf = OVF_S | OVF_M | OVF_L | OVF_MLOG | OVF_DENSE;
 static int check_split_overflow(msa_ctx *c, bool read_back = true) {
     int rc;
     if (read_back && (rc = sync_counters(c))) return rc;
@@ -893,8 +913,7 @@ static int check_split_overflow(msa_ctx *c, bool read_back = true) {
                     (unsigned long long)c->h_ctr.overflow);
     // the S/M slots this split claimed: the next split clears them even when no
     // msa_count ran in between
-    c->s_used_prev = std::min<u64>(c->h_ctr.s_claimed, c->s_slots / 2);
-    c->m_used_prev = std::min<u64>(c->h_ctr.m_claimed, c->m_slots / 2);
+    set_used_prev(c);
     return MSA_OK;
 }
 
@@ -1163,11 +1182,34 @@ static int split_once(msa_ctx *c, int flags) {
         sst = c->rank2;
         HIPC(c, hipStreamWaitEvent(c->rank2, c->ev_scan_a, 0));
     }
+    c->dense_w = c->dense_on && !c->dense_veto && !c->sharded && !c->cont && !a.mlog_direct &&
+                 c->prev_distinct >= c->dense_min;
+    if (c->dense_w) {
+        // the words' entry planes, written by the bucketed aggregation: room
+        // for every logged entry a distinct key, plus the long words
+        // (k_word_entries appends them in msa_rank)
+        Ranked &W = c->rw;
+        const u64 cap = (u64)msa_scan_blocks(a) * MSA_MLOG_PARTS * a.mlog_cap;
+        const u64 n = cap + c->lt_slots / 2 + 1;
+        for (int k = 0; k < 3; ++k) HIPC(c, ensure(W.K[0][k], n * 8));
+        HIPC(c, ensure(W.V[0], n * 4));
+        HIPC(c, ensure(W.ref, n * 8));
+        HIPC(c, ensure(W.cnt, n * 8));
+        HIPC(c, ensure(W.vary, msa_dn_vary_words() * 8));
+        a.dn_K2 = W.K[0][0].as<u64>();
+        a.dn_K1 = W.K[0][1].as<u64>();
+        a.dn_K0 = W.K[0][2].as<u64>();
+        a.dn_val = W.V[0].as<u32>();
+        a.dn_ref = W.ref.as<u64>();
+        a.dn_cnt = W.cnt.as<u64>();
+        a.dn_vary = W.vary.as<u64>();
+        a.dn_cap = cap;
+    }
     {
         prof_begin(c, ST_MISS_AGG);
         // high cardinality (the last split's logs held far more distinct keys
         // than the aggregating workgroups' LDS tables): bucketed first
-        const bool mb = c->mb_mode == 1 || (c->mb_mode == 2 && c->mb_prev > c->mb_min);
+        const bool mb = c->dense_w || c->mb_mode == 1 || (c->mb_mode == 2 && c->mb_prev > c->mb_min);
         if (mb) {
             const u64 hw = msa_mb_hist_words(a, msa_scan_blocks(a));
             HIPC(c, ensure(c->mb_hist, hw * 8));
@@ -1205,7 +1247,7 @@ static int split_once(msa_ctx *c, int flags) {
     // artist pass (LDS tables and atomics) -- both only add to Counters with
     // atomics; the read-back below waits for both
     // (measured neutral on rank2 beside the artist pass, profiles/r04_t41_*)
-    if ((rc = build_word_lists(c))) return rc;
+    if (!c->dense_w && (rc = build_word_lists(c))) return rc;  // (dense: the aggregation counted the entries)
     // the artist pass of msa_count (lines shortcut) right here, before the
     // read-back: it needs only the split's keys, and its counters come back
     // with the split's -- the text column's gather (launched by msa_count)
@@ -1234,11 +1276,20 @@ static int split_once(msa_ctx *c, int flags) {
     }
     HIPC(c, hipStreamSynchronize(c->stream));
     memcpy(&c->h_ctr, c->pin, sizeof(Counters));
+    c->prev_distinct = c->h_ctr.s_claimed + c->h_ctr.m_claimed;
+    if (c->dense_w) {
+        // a bucket past its LDS table or the planes (OVF_DENSE from the
+        // device: tables from now on), or a log partition that overflowed
+        // (its flush went into the HBM tables; the logs grow below): the split
+        // runs again (do_split)
+        if (c->h_ctr.overflow & OVF_DENSE) c->dense_veto = true;
+        if (c->h_ctr.mlog_full) c->h_ctr.overflow |= OVF_DENSE | OVF_MLOG;  // (OVF_MLOG: the logs double)
+    }
     // the slots this split claimed are cleared by the next one's prologue even
     // when this split fails below (a bad header) or no msa_count follows; an
-    // artist table that overflowed its list is wiped whole next time
-    c->s_used_prev = std::min<u64>(c->h_ctr.s_claimed, c->s_slots / 2);
-    c->m_used_prev = std::min<u64>(c->h_ctr.m_claimed, c->m_slots / 2);
+    // artist table that overflowed its list is wiped whole next time (a dense
+    // split claims none)
+    set_used_prev(c);
     if (c->artist_spec) {
         c->a_used_prev = std::min<u64>(c->h_ctr.a_claimed, c->a_slots / 2);
         if (c->h_ctr.overflow & OVF_A) c->a_dirty = true;
@@ -1300,6 +1351,11 @@ static int split_once(msa_ctx *c, int flags) {
             f.carry = d_zero;
             f.sums = nullptr;
             f.lpos_tag = MSA_POS_EXTRA;
+            if (c->dense_w) {  // the remainder's words would go into the tables: again, through the tables
+                c->dense_veto = true;
+                c->h_ctr.overflow |= OVF_DENSE;
+                return fail(c, MSA_ERR_CAPACITY, "dense word entries and a multi-line text label: split again");
+            }
             HIPC(c, msa_launch_scan(f, 2, c->stream));
             // the remainder's words may be new keys: list the tables again
             if ((rc = reset_ctr(c, &Counters::s_claimed))) return rc;
@@ -1321,15 +1377,14 @@ static int split_once(msa_ctx *c, int flags) {
 // makes the call fail.
 static int do_split(msa_ctx *c, int flags) {
     int rc = MSA_OK;
-    for (int attempt = 0; attempt < 12; ++attempt) {
+    for (int attempt = 0;; ++attempt) {
         ++c->split_attempts;
         rc = split_once(c, flags);
-        if (rc != MSA_ERR_CAPACITY || !(c->h_ctr.overflow & kSplitOvf)) return rc;
+        if (rc != MSA_ERR_CAPACITY || !(c->h_ctr.overflow & kSplitOvf) || attempt == 11) return rc;
         grow_tables(c, kSplitOvf);
-        if ((rc = ensure_tables(c))) return rc;
-        if ((rc = wipe_tables(c))) return rc;
+        int wrc;
+        if ((wrc = ensure_tables(c)) || (wrc = wipe_tables(c))) return wrc;
     }
-    return rc;
 }
 
 
@@ -1495,8 +1550,7 @@ static int do_count(msa_ctx *c) {
         if ((rc = reset_ctr(c, &Counters::overflow))) return rc;
         if (!keep_collision && (rc = reset_ctr(c, &Counters::collision))) return rc;
     }
-    c->s_used_prev = std::min<u64>(c->h_ctr.s_claimed, c->s_slots / 2);
-    c->m_used_prev = std::min<u64>(c->h_ctr.m_claimed, c->m_slots / 2);
+    set_used_prev(c);
     c->lt_used_prev = std::min<u64>(c->h_ctr.l_claimed, c->lt_slots / 2);
     c->a_used_prev = std::min<u64>(c->h_ctr.a_claimed, c->a_slots / 2);
     if (c->h_ctr.overflow) return fail(c, MSA_ERR_CAPACITY, "table capacity overflow (flags 0x%llx)",
@@ -1725,7 +1779,34 @@ static int do_rank(msa_ctx *c, int tables = 3) {
         W.lthr = c->h_ctr.s_claimed + c->h_ctr.m_claimed;
     }
     prof_begin(c, ST_RANK_WORDS);
-    if (dw && W.n) {
+    // dense split: entries [0, lthr) are written already (k_mb_agg<true>), the
+    // long words' are appended; the planes were sized for them by the split
+    const bool dense = dw && c->dense_w && !c->merged_w;
+    if (dense && W.n && (W.K[0][0].cap < W.n * 8 || W.V[0].cap < W.n * 4 || W.ref.cap < W.n * 8 ||
+                         W.cnt.cap < W.n * 8))
+        return fail(c, MSA_ERR_HIP, "dense word entries: %llu entries past the planes' capacity",
+                    (unsigned long long)W.n);
+    if (dense && W.n) {
+        EntryArgs ea{};
+        const u64 nd = W.lthr;
+        ea.l_tab = c->l_tab.as<u64>();
+        ea.l_list = c->l_list.as<u32>();
+        ea.nl = c->h_ctr.l_claimed;
+        ea.buf = c->in;
+        ea.extra = c->extra.as<u8>();
+        ea.l_pos = c->l_pos.as<u64>();
+        ea.l_len = c->l_len.as<u32>();
+        ea.K2 = W.K[0][0].as<u64>() + nd;
+        ea.K1 = W.K[0][1].as<u64>() + nd;
+        ea.K0 = W.K[0][2].as<u64>() + nd;
+        ea.val = W.V[0].as<u32>() + nd;
+        ea.ref = W.ref.as<u64>() + nd;
+        ea.cnt = W.cnt.as<u64>() + nd;  // the dense entries wrote theirs (the small-table ranking reads it)
+        ea.vbase = nd;
+        W.vary_ok = !small_sort(c, W.n);
+        ea.vary = W.vary_ok ? W.vary.as<u64>() : nullptr;  // the dense planes' OR / AND are there already
+        HIPC(c, msa_launch_word_entries(ea, c->stream));
+    } else if (dw && W.n) {
         for (int k = 0; k < 3; ++k) HIPC(c, ensure(W.K[0][k], W.n * 8));
         HIPC(c, ensure(W.V[0], W.n * 4));
         HIPC(c, ensure(W.ref, W.n * 8));
@@ -1915,6 +1996,8 @@ int msa_create(int device, msa_ctx **out) {
     if (const char *fo = getenv("MSA_FOLD")) c->fold = atoi(fo) != 0;
     if (const char *mb = getenv("MSA_MISS_BUCKETS")) c->mb_mode = atoi(mb);
     if (const char *mm = getenv("MSA_MISS_BUCKETS_MIN")) c->mb_min = strtoull(mm, nullptr, 10);
+    if (const char *de = getenv("MSA_DENSE")) c->dense_on = atoi(de) != 0;
+    if (const char *dm = getenv("MSA_DENSE_MIN")) c->dense_min = strtoull(dm, nullptr, 10);
     if (const char *me = getenv("MSA_MLOG_ENTRIES")) c->mlog_test = strtoull(me, nullptr, 10);
     if (const char *so = getenv("MSA_SORT")) c->sort_mode = !strcmp(so, "merge") ? 1 : (!strcmp(so, "radix") ? 2 : 0);
     {
@@ -2201,6 +2284,7 @@ static_assert(sizeof(msa_shard_fn) == sizeof(Fn), "msa_shard_fn mirrors Fn");
 int msa_set_shard(msa_ctx *c, int first) {
     if (!c) return MSA_ERR_ARG;
     c->cont = first == 0;
+    c->sharded = true;  // the merge exports the word tables: no dense entries from now on
     return MSA_OK;
 }
 
@@ -2429,6 +2513,8 @@ int msa_export_partitions(msa_ctx *c, int table, int nparts, uint64_t *part_byte
     if (c->stage < 2) return fail(c, MSA_ERR_ARG, "msa_export_partitions before msa_count");
     if (c->ranked_only & (table == MSA_TABLE_WORDS ? 1 : 2))
         return fail(c, MSA_ERR_ARG, "msa_export_partitions of a table merged by msa_import_ranked");
+    if (table == MSA_TABLE_WORDS && c->dense_w)
+        return fail(c, MSA_ERR_ARG, "msa_export_partitions of words counted as dense entries (call msa_set_shard first)");
     HIPC(c, hipSetDevice(c->device));
     ExpSrc x;
     u64 n;
@@ -2498,6 +2584,8 @@ int msa_import_partitions(msa_ctx *c, int table, const void *src, const uint64_t
     HIPC(c, launch_artist_col(c));  // it reads key_off / key_len, which an artist import rewrites
     if (table != MSA_TABLE_WORDS && table != MSA_TABLE_ARTISTS) return MSA_ERR_ARG;
     if (c->stage < 2) return fail(c, MSA_ERR_ARG, "msa_import_partitions before msa_count");
+    if (table == MSA_TABLE_WORDS && c->dense_w)
+        return fail(c, MSA_ERR_ARG, "msa_import_partitions into words counted as dense entries (call msa_set_shard first)");
     HIPC(c, hipSetDevice(c->device));
     const bool art = table == MSA_TABLE_ARTISTS;
     const u64 total = blk_off[nblk];
@@ -2596,6 +2684,9 @@ extern "C" int msa_debug_stat(msa_ctx *c, const char *name, uint64_t *v) {
     const Counters &k = c->h_ctr;
     const std::string n(name);
     if (n == "k3_misses") *v = k.k3_misses;
+    else if (n == "dense") *v = c->dense_w ? 1 : 0;  // the last split wrote dense word entries
+    else if (n == "dense_n") *v = k.dense_n;
+    else if (n == "dense_veto") *v = c->dense_veto ? 1 : 0;
     else if (n == "total_words") *v = k.total_words;
     else if (n == "collision") *v = k.collision;
     else if (n == "a_long") *v = k.a_long;

@@ -286,9 +286,10 @@ struct Counters {
     u64 span_fix;    // records k_rec_fast hands to k_rec_fix (the exact per-record path)
     u64 mlog_full;   // K3 misses that found their log partition full (dropped: the split runs again with
                      // larger logs; at the logs' size limit inserted straight into HBM)
+    u64 dense_n;     // dense S/M entries written (the bucketed aggregation's cursor)
 };
 
-enum { OVF_S = 1, OVF_M = 2, OVF_L = 4, OVF_LT = 8, OVF_A = 16, OVF_REC = 32, OVF_MLOG = 64, OVF_FOLD = 128 };
+enum { OVF_S = 1, OVF_M = 2, OVF_L = 4, OVF_LT = 8, OVF_A = 16, OVF_REC = 32, OVF_MLOG = 64, OVF_FOLD = 128, OVF_DENSE = 256 };
 
 // Artist keys built by k_rec_spans for the lines shortcut of the artist pass:
 // per record the key bytes (duplicate_field(duplicate_field(field0, 1), 0))
@@ -356,6 +357,12 @@ struct ScanArgs {
     // = byte seg_begin + i is a token byte of a counted lyric field
     // (process_lyrics input, parallel_spotify.c:350-394); lmask[0] = 0 pad
     u64 *lmask;
+    // dense S/M entries (high cardinality, single GPU): the bucketed
+    // aggregation writes each distinct 3..16-byte word's ranking entry
+    // straight into these planes (null: into the HBM tables) -- see k_mb_agg
+    u64 *dn_K2, *dn_K1, *dn_K0, *dn_ref, *dn_cnt, *dn_vary;
+    u32 *dn_val;
+    u64 dn_cap;
 };
 
 #define MSA_MLOG_PARTS 16
@@ -372,6 +379,9 @@ struct ScanArgs {
 __host__ __device__ inline const u8 *tok_at(const u8 *buf, const u8 *extra, u64 pos) {
     return (pos & MSA_POS_EXTRA) ? extra + (pos & ~MSA_POS_EXTRA) : buf + pos;
 }
+// ranking entries' ref = (kind << 60) | index: an S / M table slot (or a
+// dense entry's own index), a long word's occurrence, an artist record
+enum { KIND_S = 0, KIND_M = 1, KIND_L = 2, KIND_A = 3 };
 struct EntryArgs {
     const u64 *s_tab;
     const u32 *s_list;
@@ -390,6 +400,7 @@ struct EntryArgs {
     u32 *val;
     u64 *ref;
     u64 *cnt;
+    u64 vbase;  // val[i] = vbase + i (the planes start at entry vbase: the dense S/M entries before them)
     // optional: OR of each key plane over all entries ([0..2] = K0, K1, K2)
     // and their AND ([3..5]), for the radix sort's varying-byte mask (the
     // caller zeroes the ORs and sets the ANDs to all ones)

@@ -1120,17 +1120,23 @@ __global__ __launch_bounds__(Q_T, 1) void k_scan_tokens(ScanArgs a) {
 #define MA_FLY 4  // log entries in flight per thread
 #endif
 #define MA_NB (MA_SLOTS / 4)
-__device__ __forceinline__ u32 ma_find(ulonglong2 *keys, u64 k0, u64 k1) {
+__device__ __forceinline__ u32 ma_hash(u64 k0, u64 k1) {
     u32 h = (u32)k0 * 0x9E3779B1u + (u32)(k0 >> 32) * 0x85EBCA77u + (u32)k1 * 0xC2B2AE3Du + (u32)(k1 >> 32);
     h ^= h >> 15;
-    h *= 0x2C1B3C6Du;
+    return h * 0x2C1B3C6Du;
+}
+// PROBES buckets of 4 slots are tried (k_miss_agg: 2, then the HBM table;
+// the dense aggregation: 16, its table a third full at configs[4] -- two
+// buckets left ~1 in 300 keys without a slot there)
+template <int PROBES = 2>
+__device__ __forceinline__ u32 ma_find(ulonglong2 *keys, u64 k0, u64 k1) {
+    const u32 h = ma_hash(k0, k1);
     u32 b = __umulhi(h, (u32)MA_NB);
     // the four slot reads start at a key-dependent slot: a ds_read_b128 lane
     // group spreads over 16 positions of the bank row, not 4 (measured: the
     // aggregation 0.22 -> 0.19 ms; in K3's table it did not pay)
     const u32 ro = h & 3u;
-#pragma unroll
-    for (int p = 0; p < 2; ++p) {
+    for (int p = 0; p < PROBES; ++p) {
         const u32 base = b * 4;
         const ulonglong2 s0 = keys[base + (ro & 3u)], s1 = keys[base + ((ro + 1) & 3u)];
         const ulonglong2 s2 = keys[base + ((ro + 2) & 3u)], s3 = keys[base + ((ro + 3) & 3u)];
@@ -1138,22 +1144,34 @@ __device__ __forceinline__ u32 ma_find(ulonglong2 *keys, u64 k0, u64 k1) {
         const bool e2 = (s2.x == k0) & (s2.y == k1), e3 = (s3.x == k0) & (s3.y == k1);
         const u32 hit = e0 ? 0u : (e1 ? 1u : (e2 ? 2u : (e3 ? 3u : 4u)));
         if (hit < 4) return base + ((ro + hit) & 3u);
-        u32 i = s0.x == 0 ? 0u : (s1.x == 0 ? 1u : (s2.x == 0 ? 2u : (s3.x == 0 ? 3u : 4u)));
-        for (; i < 4; ++i) {
+        // a slot is claimed word by word, each by a CAS: the first word by the
+        // key's first 8 bytes, the second by the rest -- lanes of one key that
+        // meet a slot whose second word is not written yet write the same
+        // value, so a key never takes two slots (a plain store of the second
+        // word had let them move on and claim another)
+#pragma unroll
+        for (u32 i = 0; i < 4; ++i) {
+            const ulonglong2 sn = i == 0 ? s0 : (i == 1 ? s1 : (i == 2 ? s2 : s3));
+            if ((sn.x != 0 && sn.x != k0) || (sn.y != 0 && sn.y != k1)) continue;  // another key's
             const u32 sl = base + ((ro + i) & 3u);
             u64 *kp = reinterpret_cast<u64 *>(&keys[sl]);
-            const u64 old = atomicCAS((unsigned long long *)kp, 0ull, (unsigned long long)k0);
-            if (old == 0) {
-                kp[1] = k1;
-                return sl;
+            u64 w0 = sn.x;
+            if (w0 == 0) {
+                const u64 o = atomicCAS((unsigned long long *)kp, 0ull, (unsigned long long)k0);
+                w0 = o == 0 ? k0 : o;
             }
-            if (old == k0 && kp[1] == k1) return sl;
+            if (w0 != k0) continue;
+            u64 w1 = sn.y;
+            if (w1 == 0) {
+                const u64 o = atomicCAS((unsigned long long *)(kp + 1), 0ull, (unsigned long long)k1);
+                w1 = o == 0 ? k1 : o;
+            }
+            if (w1 == k1) return sl;
         }
         b = (b + 1 == MA_NB) ? 0 : b + 1;
     }
     return ~0u;
 }
-
 __global__ __launch_bounds__(MA_T) void k_miss_agg(ScanArgs a, u32 nsrc, u32 groups) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     ulonglong2 *keys = reinterpret_cast<ulonglong2 *>(smem);
@@ -1307,18 +1325,35 @@ __device__ __forceinline__ void mb_insert_once(const ScanArgs &a, u64 k0, u64 k1
 }
 // workgroup (p, b): bucket b of partition p = bucketed entries [off[(p B + b) T], off[(p B + b + 1) T])
 #define MBA_T 512
+#define MBA_KS ((MA_SLOTS + MBA_T - 1) / MBA_T)  // LDS slots per thread in the dense flush
+// DENSE (ScanArgs::dn_*, single GPU, high cardinality): no HBM table at all --
+// the bucket's distinct keys are final once counted (no other workgroup sees
+// them), so each becomes its ranking entry right here (the K2 / K1 / K0 / val
+// / ref / cnt planes k_word_entries would have written from the table: no
+// inserts, no slot lists, no table clears).  A key the LDS table cannot hold,
+// or entries past the planes' capacity, flag OVF_DENSE: the split runs again
+// through the tables.  The planes' OR / AND go to one partial per workgroup
+// (dn_vary[6 + q * 6 ..]), reduced by k_dn_vary into dn_vary[0..5].
+template <bool DENSE>
 __global__ __launch_bounds__(MBA_T) void k_mb_agg(ScanArgs a, u32 T, const u64 *__restrict__ off,
                                                   const u64 *__restrict__ total, const ulonglong2 *__restrict__ in) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     ulonglong2 *keys = reinterpret_cast<ulonglong2 *>(smem);
     u32 *cnts = reinterpret_cast<u32 *>(smem + MA_SLOTS * 16);
+    __shared__ u32 s_wbase[MBA_T / 64], s_tot, s_ns;
+    __shared__ u64 s_gbase, s_vary[6];
     const u64 q = (u64)blockIdx.y * MB_B + blockIdx.x;
     const u64 lo = off[q * T], hi = q + 1 < (u64)MSA_MLOG_PARTS * MB_B ? off[(q + 1) * T] : *total;
-    if (lo >= hi) return;
+    if (lo >= hi) {
+        if (DENSE && threadIdx.x < 6) a.dn_vary[6 + q * 6 + threadIdx.x] = threadIdx.x < 3 ? 0ull : ~0ull;
+        return;
+    }
     for (u32 i = threadIdx.x; i < MA_SLOTS; i += MBA_T) {
         keys[i] = make_ulonglong2(0, 0);
         cnts[i] = 0;
     }
+    if (DENSE && threadIdx.x < 6) s_vary[threadIdx.x] = threadIdx.x < 3 ? 0ull : ~0ull;
+    if (DENSE && threadIdx.x == 0) s_tot = s_ns = 0;
     __syncthreads();
     for (u64 i0 = lo + threadIdx.x; i0 < hi; i0 += (u64)MA_FLY * MBA_T) {
         ulonglong2 xs[MA_FLY];
@@ -1333,18 +1368,113 @@ __global__ __launch_bounds__(MBA_T) void k_mb_agg(ScanArgs a, u32 T, const u64 *
             const ulonglong2 x = xs[f];
             const u32 c = gather8(x.x) | ((gather8(x.y) & 0x7Fu) << 8);
             const u64 k0 = x.x & MLOG_KEYBITS, k1 = x.y & (MLOG_KEYBITS | KMARK);
-            const u32 slot = ma_find(keys, k0, k1);
+            const u32 slot = ma_find<DENSE ? 16 : 2>(keys, k0, k1);
             if (slot != ~0u) atomicAdd(&cnts[slot], c ? c : 1u);
+            else if (DENSE) atomicOr((unsigned long long *)&a.ctr->overflow, (unsigned long long)OVF_DENSE);
             else hbm_insert16<true>(a, k0, k1, c ? c : 1u);  // table full: this key's every entry
         }
     }
     __syncthreads();
-    for (u32 i = threadIdx.x; i < MA_SLOTS; i += MBA_T) {
-        const u32 c = cnts[i];
-        if (c) {
-            const ulonglong2 kk = keys[i];
-            mb_insert_once(a, kk.x, kk.y, c);
+    if (!DENSE) {
+        for (u32 i = threadIdx.x; i < MA_SLOTS; i += MBA_T) {
+            const u32 c = cnts[i];
+            if (c) {
+                const ulonglong2 kk = keys[i];
+                mb_insert_once(a, kk.x, kk.y, c);
+            }
         }
+        return;
+    }
+    // the workgroup's entries (each key holds one slot: ma_find's claims): a
+    // range per wave (slots threadIdx.x + k MBA_T), the workgroup's range from
+    // one device atomic; each wave's k-th batch of entries is contiguous
+    // (coalesced stores)
+    const u32 lane = lane_id(), wv = threadIdx.x >> 6;
+    u32 nw = 0, nsw = 0;
+    for (u32 k = 0; k < MBA_KS; ++k) {
+        const u32 i = threadIdx.x + k * MBA_T;
+        const bool live = i < MA_SLOTS && cnts[i] != 0;
+        const u64 bm = __ballot(live), bs = __ballot(live && keys[i].y == KMARK);
+        nw += (u32)__popcll(bm);
+        nsw += (u32)__popcll(bs);
+    }
+    if (lane == 0) {
+        s_wbase[wv] = atomicAdd(&s_tot, nw);
+        atomicAdd(&s_ns, nsw);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        s_gbase = atomicAdd((unsigned long long *)&a.ctr->dense_n, (unsigned long long)s_tot);
+        atomicAdd((unsigned long long *)&a.ctr->s_claimed, (unsigned long long)s_ns);
+        atomicAdd((unsigned long long *)&a.ctr->m_claimed, (unsigned long long)(s_tot - s_ns));
+        if (s_gbase + s_tot > a.dn_cap) atomicOr((unsigned long long *)&a.ctr->overflow, (unsigned long long)OVF_DENSE);
+    }
+    __syncthreads();
+    u64 idx = s_gbase + s_wbase[wv];
+    u64 vo[3] = {0, 0, 0}, va[3] = {~0ull, ~0ull, ~0ull};
+    for (u32 k = 0; k < MBA_KS; ++k) {
+        const u32 i = threadIdx.x + k * MBA_T;
+        const u32 c = i < MA_SLOTS ? cnts[i] : 0u;
+        const u64 bm = __ballot(c != 0);
+        const u64 e = idx + mbcnt(bm);
+        idx += (u64)__popcll(bm);
+        if (c == 0 || e >= a.dn_cap) continue;
+        const ulonglong2 kk = keys[i];
+        const bool sk = kk.y == KMARK;
+        const u64 k2 = ~(u64)c, k1 = __builtin_bswap64(kk.x), k0 = sk ? 0ull : __builtin_bswap64(kk.y & ~KMARK);
+        a.dn_K2[e] = k2;
+        a.dn_K1[e] = k1;
+        a.dn_K0[e] = k0;
+        a.dn_val[e] = (u32)e;
+        a.dn_ref[e] = ((u64)(sk ? KIND_S : KIND_M) << 60) | e;
+        a.dn_cnt[e] = c;
+        vo[0] |= k0; vo[1] |= k1; vo[2] |= k2;
+        va[0] &= k0; va[1] &= k1; va[2] &= k2;
+    }
+#pragma unroll
+    for (int w = 0; w < 3; ++w) {
+        for (int o = 32; o > 0; o >>= 1) {
+            vo[w] |= (u64)__shfl_xor((long long)vo[w], o);
+            va[w] &= (u64)__shfl_xor((long long)va[w], o);
+        }
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int w = 0; w < 3; ++w) {
+            atomicOr((unsigned long long *)&s_vary[w], (unsigned long long)vo[w]);
+            atomicAnd((unsigned long long *)&s_vary[3 + w], (unsigned long long)va[w]);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 6) a.dn_vary[6 + q * 6 + threadIdx.x] = s_vary[threadIdx.x];
+}
+// The dense planes' OR / AND from the bucket workgroups' partials (one
+// workgroup) into vary[0..5] (k_word_entries adds the long words' to them).
+#define DV_T 1024
+__global__ __launch_bounds__(DV_T) void k_dn_vary(const u64 *__restrict__ part, u32 nq, u64 *__restrict__ vary) {
+    __shared__ u64 r[DV_T / 64][6];
+    u64 v[6] = {0, 0, 0, ~0ull, ~0ull, ~0ull};
+    for (u32 q = threadIdx.x; q < nq; q += DV_T) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            v[k] |= part[(u64)q * 6 + k];
+            v[3 + k] &= part[(u64)q * 6 + 3 + k];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+        for (int o = 32; o > 0; o >>= 1) {
+            const u64 y = (u64)__shfl_xor((long long)v[k], o);
+            v[k] = k < 3 ? (v[k] | y) : (v[k] & y);
+        }
+    if (lane_id() == 0)
+        for (int k = 0; k < 6; ++k) r[threadIdx.x >> 6][k] = v[k];
+    __syncthreads();
+    if (threadIdx.x < 6) {
+        const u32 k = threadIdx.x;
+        u64 x = r[0][k];
+        for (u32 w = 1; w < DV_T / 64; ++w) x = k < 3 ? (x | r[w][k]) : (x & r[w][k]);
+        vary[k] = x;
     }
 }
 
@@ -1410,18 +1540,29 @@ hipError_t msa_launch_miss_buckets(const ScanArgs &a, u64 *hist, u64 *off, u64 *
     const u32 chunks = (a.mlog_cap + MB_TILE - 1) / MB_TILE, T = nsrc * chunks;
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void *)k_mb_agg, hipFuncAttributeMaxDynamicSharedMemorySize, MA_SLOTS * 20);
+        (void)hipFuncSetAttribute((const void *)k_mb_agg<false>, hipFuncAttributeMaxDynamicSharedMemorySize, MA_SLOTS * 20);
+        (void)hipFuncSetAttribute((const void *)k_mb_agg<true>, hipFuncAttributeMaxDynamicSharedMemorySize, MA_SLOTS * 20);
         attr = true;
     }
     hipLaunchKernelGGL(k_mb_hist, dim3(T, MSA_MLOG_PARTS), dim3(MB_TT), 0, s, a, chunks, T, hist);
     hipError_t e = msa_exclusive_scan(hist, msa_mb_hist_words(a, nsrc), off, bsum, total, s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_mb_scatter, dim3(T, MSA_MLOG_PARTS), dim3(MB_TT), 0, s, a, chunks, T, (const u64 *)off, out);
-    hipLaunchKernelGGL(k_mb_agg, dim3(MB_B, MSA_MLOG_PARTS), dim3(MBA_T), MA_SLOTS * 20, s, a, T, (const u64 *)off,
-                       (const u64 *)total, (const ulonglong2 *)out);
+    if (a.dn_K2) {  // dense entries (the caller zeroed Counters::dense_n with the split's counters)
+        hipLaunchKernelGGL(k_mb_agg<true>, dim3(MB_B, MSA_MLOG_PARTS), dim3(MBA_T), MA_SLOTS * 20, s, a, T,
+                           (const u64 *)off, (const u64 *)total, (const ulonglong2 *)out);
+        hipLaunchKernelGGL(k_dn_vary, dim3(1), dim3(DV_T), 0, s, (const u64 *)a.dn_vary + 6, MSA_MLOG_PARTS * MB_B,
+                           a.dn_vary);
+    } else {
+        hipLaunchKernelGGL(k_mb_agg<false>, dim3(MB_B, MSA_MLOG_PARTS), dim3(MBA_T), MA_SLOTS * 20, s, a, T,
+                           (const u64 *)off, (const u64 *)total, (const ulonglong2 *)out);
+    }
     return hipGetLastError();
 }
 u32 msa_scan_blocks(const ScanArgs &a) { return scan_blocks(a); }
+// the dense planes' OR / AND: dn_vary holds msa_dn_vary_words() words, the
+// reduced six first (the radix sort's varying-byte mask), then the partials
+u64 msa_dn_vary_words() { return (u64)MSA_MLOG_PARTS * MB_B * 6 + 6; }
 hipError_t msa_launch_miss_agg(const ScanArgs &a, hipStream_t s) {
     if (!a.nchunks) return hipSuccess;
     const u32 blocks = scan_blocks(a);

@@ -1625,8 +1625,8 @@ __global__ void k_long_verify(const u8 *__restrict__ buf, const u8 *__restrict__
 // Ranking entries.  Sort key = (K2 = ~count, K1 = key bytes 0..7 big-endian,
 // K0 = key bytes 8..15 big-endian); ascending == entry_compare_desc for all
 // keys that differ within their first 16 bytes (zero padding sorts first,
-// exactly like strcmp's terminator).  ref = (kind << 60) | index.
-enum { KIND_S = 0, KIND_M = 1, KIND_L = 2, KIND_A = 3 };
+// exactly like strcmp's terminator).  ref = (kind << 60) | index (KIND_*:
+// msa_internal.h).
 
 __device__ __forceinline__ void be16(const u8 *p, u64 n, int lower, u64 *hi, u64 *lo) {
     u64 h = 0, l = 0;
@@ -1731,7 +1731,7 @@ __global__ __launch_bounds__(256) void k_word_entries(EntryArgs a) {
         a.K2[i] = ~c;
         a.K1[i] = hi;
         a.K0[i] = lo;
-        a.val[i] = (u32)i;
+        a.val[i] = (u32)(a.vbase + i);
         a.ref[i] = ref;
         if (a.cnt) a.cnt[i] = c;
         vo[0] |= lo; vo[1] |= hi; vo[2] |= ~c;

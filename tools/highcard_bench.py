@@ -43,7 +43,8 @@ with msa.Context(0) as c:
     import ctypes
     c.lib.msa_debug_stat.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint64)]
     dbg = {}
-    for nm in ("k3_misses", "mlog_full", "s_claimed", "m_claimed", "l_claimed", "split_attempts"):
+    for nm in ("k3_misses", "mlog_full", "s_claimed", "m_claimed", "l_claimed", "split_attempts", "dense",
+               "dense_veto"):
         v = ctypes.c_uint64(0)
         if c.lib.msa_debug_stat(c.h, nm.encode(), ctypes.byref(v)) == 0:
             dbg[nm] = v.value
