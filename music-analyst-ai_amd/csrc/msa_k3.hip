@@ -1259,22 +1259,68 @@ __global__ __launch_bounds__(MB_TT) void k_mb_hist(ScanArgs a, u32 chunks, u32 T
     __syncthreads();
     for (u32 k = threadIdx.x; k < MB_B; k += MB_TT) hist[((u64)p * MB_B + k) * T + t] = h[k];
 }
+// The tile sorted by bucket in LDS (counting sort), then written bucket run by
+// bucket run with consecutive lanes on consecutive entries (a scattered
+// 16-byte store per entry had taken 2.0 ms at configs[4]).  LDS: the staged
+// tile (MB_TILE x 16 B), its bucket ids (MB_TILE x 2 B), the bucket counts and
+// offsets (later overlaid by each bucket's output base).
+#define MS_PER (MB_TILE / MB_TT)
+#define MS_LDS (MB_TILE * 18u + MB_B * 8u)
 __global__ __launch_bounds__(MB_TT) void k_mb_scatter(ScanArgs a, u32 chunks, u32 T, const u64 *__restrict__ off,
                                                       ulonglong2 *__restrict__ out) {
-    __shared__ u32 cur[MB_B];
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    ulonglong2 *stage = reinterpret_cast<ulonglong2 *>(smem);
+    u16 *bid = reinterpret_cast<u16 *>(smem + MB_TILE * 16u);
+    u32 *cnt = reinterpret_cast<u32 *>(smem + MB_TILE * 18u);
+    u32 *loff = cnt + MB_B;
+    u64 *gdel = reinterpret_cast<u64 *>(cnt);  // (after the staging) bucket b's output index - loff[b]
+    __shared__ u32 wsum[MB_TT / 64];
     const u32 p = blockIdx.y, t = blockIdx.x, src = t / chunks, c = t % chunks;
     const u32 n = a.mlog_n[src * MSA_MLOG_PARTS + p];
     const u32 lo = c * MB_TILE, hi = min(n, lo + MB_TILE);
     if (lo >= hi) return;  // whole workgroup
-    for (u32 k = threadIdx.x; k < MB_B; k += MB_TT) cur[k] = 0;
+    const u32 m = hi - lo, tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+    for (u32 k = tid; k < MB_B; k += MB_TT) cnt[k] = 0;
     __syncthreads();
-    const u64 base = ((u64)src * MSA_MLOG_PARTS + p) * a.mlog_cap;
-    for (u32 i = lo + threadIdx.x; i < hi; i += MB_TT) {
-        const ulonglong2 x = a.mlog[base + i];
-        const u32 b = mb_bucket(x.x, x.y);
-        const u32 r = atomicAdd(&cur[b], 1u);  // order within a bucket does not matter
-        out[off[((u64)p * MB_B + b) * T + t] + r] = x;
+    const u64 base = ((u64)src * MSA_MLOG_PARTS + p) * a.mlog_cap + lo;
+    ulonglong2 x[MS_PER];
+    u32 bk[MS_PER], r[MS_PER];
+#pragma unroll
+    for (u32 q = 0; q < MS_PER; ++q) {
+        const u32 i = tid + q * MB_TT;
+        x[q] = i < m ? a.mlog[base + i] : make_ulonglong2(0, 0);
     }
+#pragma unroll
+    for (u32 q = 0; q < MS_PER; ++q) {
+        bk[q] = mb_bucket(x[q].x, x[q].y);
+        r[q] = tid + q * MB_TT < m ? atomicAdd(&cnt[bk[q]], 1u) : 0u;
+    }
+    __syncthreads();
+    // exclusive scan of the 1024 counts (2 per thread)
+    static_assert(MB_B == 2 * MB_TT, "two buckets per thread");
+    const u32 c0 = cnt[2 * tid], c1 = cnt[2 * tid + 1];
+    u32 wt;
+    const u32 pre = wave_prefix<14>(c0 + c1, wt);  // <= MB_TILE per tile
+    if (lane == 0) wsum[w] = wt;
+    __syncthreads();
+    u32 wb = 0;
+    for (u32 v = 0; v < w; ++v) wb += wsum[v];
+    const u32 l0 = wb + pre, l1 = l0 + c0;
+    loff[2 * tid] = l0;
+    loff[2 * tid + 1] = l1;
+    __syncthreads();
+#pragma unroll
+    for (u32 q = 0; q < MS_PER; ++q) {
+        if (tid + q * MB_TT >= m) continue;
+        const u32 pos = loff[bk[q]] + r[q];
+        stage[pos] = x[q];
+        bid[pos] = (u16)bk[q];
+    }
+    __syncthreads();  // (every loff read is done before gdel overlays it)
+    gdel[2 * tid] = off[((u64)p * MB_B + 2 * tid) * T + t] - l0;
+    gdel[2 * tid + 1] = off[((u64)p * MB_B + 2 * tid + 1) * T + t] - l1;
+    __syncthreads();
+    for (u32 j = tid; j < m; j += MB_TT) out[gdel[bid[j]] + j] = stage[j];
 }
 // one claim per distinct key of a bucket (CAS first: most keys are new)
 __device__ __forceinline__ void mb_insert_once(const ScanArgs &a, u64 k0, u64 k1m, u64 cnt) {
@@ -1325,35 +1371,18 @@ __device__ __forceinline__ void mb_insert_once(const ScanArgs &a, u64 k0, u64 k1
 }
 // workgroup (p, b): bucket b of partition p = bucketed entries [off[(p B + b) T], off[(p B + b + 1) T])
 #define MBA_T 512
-#define MBA_KS ((MA_SLOTS + MBA_T - 1) / MBA_T)  // LDS slots per thread in the dense flush
-// DENSE (ScanArgs::dn_*, single GPU, high cardinality): no HBM table at all --
-// the bucket's distinct keys are final once counted (no other workgroup sees
-// them), so each becomes its ranking entry right here (the K2 / K1 / K0 / val
-// / ref / cnt planes k_word_entries would have written from the table: no
-// inserts, no slot lists, no table clears).  A key the LDS table cannot hold,
-// or entries past the planes' capacity, flag OVF_DENSE: the split runs again
-// through the tables.  The planes' OR / AND go to one partial per workgroup
-// (dn_vary[6 + q * 6 ..]), reduced by k_dn_vary into dn_vary[0..5].
-template <bool DENSE>
 __global__ __launch_bounds__(MBA_T) void k_mb_agg(ScanArgs a, u32 T, const u64 *__restrict__ off,
                                                   const u64 *__restrict__ total, const ulonglong2 *__restrict__ in) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     ulonglong2 *keys = reinterpret_cast<ulonglong2 *>(smem);
     u32 *cnts = reinterpret_cast<u32 *>(smem + MA_SLOTS * 16);
-    __shared__ u32 s_wbase[MBA_T / 64], s_tot, s_ns;
-    __shared__ u64 s_gbase, s_vary[6];
     const u64 q = (u64)blockIdx.y * MB_B + blockIdx.x;
     const u64 lo = off[q * T], hi = q + 1 < (u64)MSA_MLOG_PARTS * MB_B ? off[(q + 1) * T] : *total;
-    if (lo >= hi) {
-        if (DENSE && threadIdx.x < 6) a.dn_vary[6 + q * 6 + threadIdx.x] = threadIdx.x < 3 ? 0ull : ~0ull;
-        return;
-    }
+    if (lo >= hi) return;
     for (u32 i = threadIdx.x; i < MA_SLOTS; i += MBA_T) {
         keys[i] = make_ulonglong2(0, 0);
         cnts[i] = 0;
     }
-    if (DENSE && threadIdx.x < 6) s_vary[threadIdx.x] = threadIdx.x < 3 ? 0ull : ~0ull;
-    if (DENSE && threadIdx.x == 0) s_tot = s_ns = 0;
     __syncthreads();
     for (u64 i0 = lo + threadIdx.x; i0 < hi; i0 += (u64)MA_FLY * MBA_T) {
         ulonglong2 xs[MA_FLY];
@@ -1368,68 +1397,121 @@ __global__ __launch_bounds__(MBA_T) void k_mb_agg(ScanArgs a, u32 T, const u64 *
             const ulonglong2 x = xs[f];
             const u32 c = gather8(x.x) | ((gather8(x.y) & 0x7Fu) << 8);
             const u64 k0 = x.x & MLOG_KEYBITS, k1 = x.y & (MLOG_KEYBITS | KMARK);
-            const u32 slot = ma_find<DENSE ? 16 : 2>(keys, k0, k1);
+            const u32 slot = ma_find(keys, k0, k1);
             if (slot != ~0u) atomicAdd(&cnts[slot], c ? c : 1u);
-            else if (DENSE) atomicOr((unsigned long long *)&a.ctr->overflow, (unsigned long long)OVF_DENSE);
             else hbm_insert16<true>(a, k0, k1, c ? c : 1u);  // table full: this key's every entry
         }
     }
     __syncthreads();
-    if (!DENSE) {
-        for (u32 i = threadIdx.x; i < MA_SLOTS; i += MBA_T) {
-            const u32 c = cnts[i];
-            if (c) {
-                const ulonglong2 kk = keys[i];
-                mb_insert_once(a, kk.x, kk.y, c);
+    for (u32 i = threadIdx.x; i < MA_SLOTS; i += MBA_T) {
+        const u32 c = cnts[i];
+        if (c) {
+            const ulonglong2 kk = keys[i];
+            mb_insert_once(a, kk.x, kk.y, c);
+        }
+    }
+}
+
+// k_mb_dense (ScanArgs::dn_*, single GPU, high cardinality): no HBM table at
+// all -- a bucket's distinct keys are final once counted (no other workgroup
+// sees them), so each becomes its ranking entry right here (the K2 / K1 / K0 /
+// val / ref / cnt planes k_word_entries would have written from the table: no
+// inserts, no slot lists, no table clears).  Persistent: a workgroup per CU
+// takes buckets blockIdx.x, + gridDim.x, ... with one LDS table, cleared as
+// its entries are written out (no clear pass per bucket, no launch of a
+// workgroup per bucket).  A key the LDS table cannot hold, or entries past
+// the planes' capacity, flag OVF_DENSE: the split runs again through the
+// tables.  The planes' OR / AND: one partial per workgroup
+// (dn_vary[6 + blockIdx.x * 6 ..]), reduced by k_dn_vary into dn_vary[0..5].
+#ifndef MBD_T
+#define MBD_T 1024  // 16 waves: 512 threads (8 waves) 1.57 ms at configs[4]
+#endif
+#define MBD_KS ((MA_SLOTS + MBD_T - 1) / MBD_T)
+__global__ __launch_bounds__(MBD_T) void k_mb_dense(ScanArgs a, u32 T, const u64 *__restrict__ off,
+                                                    const u64 *__restrict__ total, const ulonglong2 *__restrict__ in) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    ulonglong2 *keys = reinterpret_cast<ulonglong2 *>(smem);
+    u32 *cnts = reinterpret_cast<u32 *>(smem + MA_SLOTS * 16);
+    __shared__ u32 s_wbase[MBD_T / 64], s_tot, s_ns;
+    __shared__ u64 s_gbase, s_vary[6];
+    const u32 lane = lane_id(), wv = threadIdx.x >> 6;
+    for (u32 i = threadIdx.x; i < MA_SLOTS; i += MBD_T) {
+        keys[i] = make_ulonglong2(0, 0);
+        cnts[i] = 0;
+    }
+    u64 vo[3] = {0, 0, 0}, va[3] = {~0ull, ~0ull, ~0ull};
+    const u64 nq = (u64)MSA_MLOG_PARTS * MB_B;
+    for (u64 q = blockIdx.x; q < nq; q += gridDim.x) {
+        if (threadIdx.x == 0) s_tot = s_ns = 0;
+        __syncthreads();  // (the table clear / the last bucket's flush done)
+        const u64 lo = off[q * T], hi = q + 1 < nq ? off[(q + 1) * T] : *total;
+        for (u64 i0 = lo + threadIdx.x; i0 < hi; i0 += (u64)MA_FLY * MBD_T) {
+            ulonglong2 xs[MA_FLY];
+#pragma unroll
+            for (int f = 0; f < MA_FLY; ++f) {
+                const u64 i = i0 + (u64)f * MBD_T;
+                xs[f] = i < hi ? in[i] : make_ulonglong2(0, 0);
+            }
+#pragma unroll
+            for (int f = 0; f < MA_FLY; ++f) {
+                if (i0 + (u64)f * MBD_T >= hi) break;
+                const ulonglong2 x = xs[f];
+                const u32 c = gather8(x.x) | ((gather8(x.y) & 0x7Fu) << 8);
+                const u64 k0 = x.x & MLOG_KEYBITS, k1 = x.y & (MLOG_KEYBITS | KMARK);
+                const u32 slot = ma_find<16>(keys, k0, k1);
+                if (slot != ~0u) atomicAdd(&cnts[slot], c ? c : 1u);
+                else atomicOr((unsigned long long *)&a.ctr->overflow, (unsigned long long)OVF_DENSE);
             }
         }
-        return;
-    }
-    // the workgroup's entries (each key holds one slot: ma_find's claims): a
-    // range per wave (slots threadIdx.x + k MBA_T), the workgroup's range from
-    // one device atomic; each wave's k-th batch of entries is contiguous
-    // (coalesced stores)
-    const u32 lane = lane_id(), wv = threadIdx.x >> 6;
-    u32 nw = 0, nsw = 0;
-    for (u32 k = 0; k < MBA_KS; ++k) {
-        const u32 i = threadIdx.x + k * MBA_T;
-        const bool live = i < MA_SLOTS && cnts[i] != 0;
-        const u64 bm = __ballot(live), bs = __ballot(live && keys[i].y == KMARK);
-        nw += (u32)__popcll(bm);
-        nsw += (u32)__popcll(bs);
-    }
-    if (lane == 0) {
-        s_wbase[wv] = atomicAdd(&s_tot, nw);
-        atomicAdd(&s_ns, nsw);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        s_gbase = atomicAdd((unsigned long long *)&a.ctr->dense_n, (unsigned long long)s_tot);
-        atomicAdd((unsigned long long *)&a.ctr->s_claimed, (unsigned long long)s_ns);
-        atomicAdd((unsigned long long *)&a.ctr->m_claimed, (unsigned long long)(s_tot - s_ns));
-        if (s_gbase + s_tot > a.dn_cap) atomicOr((unsigned long long *)&a.ctr->overflow, (unsigned long long)OVF_DENSE);
-    }
-    __syncthreads();
-    u64 idx = s_gbase + s_wbase[wv];
-    u64 vo[3] = {0, 0, 0}, va[3] = {~0ull, ~0ull, ~0ull};
-    for (u32 k = 0; k < MBA_KS; ++k) {
-        const u32 i = threadIdx.x + k * MBA_T;
-        const u32 c = i < MA_SLOTS ? cnts[i] : 0u;
-        const u64 bm = __ballot(c != 0);
-        const u64 e = idx + mbcnt(bm);
-        idx += (u64)__popcll(bm);
-        if (c == 0 || e >= a.dn_cap) continue;
-        const ulonglong2 kk = keys[i];
-        const bool sk = kk.y == KMARK;
-        const u64 k2 = ~(u64)c, k1 = __builtin_bswap64(kk.x), k0 = sk ? 0ull : __builtin_bswap64(kk.y & ~KMARK);
-        a.dn_K2[e] = k2;
-        a.dn_K1[e] = k1;
-        a.dn_K0[e] = k0;
-        a.dn_val[e] = (u32)e;
-        a.dn_ref[e] = ((u64)(sk ? KIND_S : KIND_M) << 60) | e;
-        a.dn_cnt[e] = c;
-        vo[0] |= k0; vo[1] |= k1; vo[2] |= k2;
-        va[0] &= k0; va[1] &= k1; va[2] &= k2;
+        __syncthreads();
+        // the bucket's entries (each key holds one slot: ma_find's claims): a
+        // range per wave (slots threadIdx.x + k MBD_T), the bucket's range
+        // from one device atomic; each wave's k-th batch of entries is
+        // contiguous (coalesced stores)
+        u32 nw = 0, nsw = 0;
+        for (u32 k = 0; k < MBD_KS; ++k) {
+            const u32 i = threadIdx.x + k * MBD_T;
+            const bool live = i < MA_SLOTS && cnts[i] != 0;
+            const u64 bm = __ballot(live), bs = __ballot(live && keys[i].y == KMARK);
+            nw += (u32)__popcll(bm);
+            nsw += (u32)__popcll(bs);
+        }
+        if (lane == 0) {
+            s_wbase[wv] = atomicAdd(&s_tot, nw);
+            atomicAdd(&s_ns, nsw);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0 && s_tot) {
+            s_gbase = atomicAdd((unsigned long long *)&a.ctr->dense_n, (unsigned long long)s_tot);
+            atomicAdd((unsigned long long *)&a.ctr->s_claimed, (unsigned long long)s_ns);
+            atomicAdd((unsigned long long *)&a.ctr->m_claimed, (unsigned long long)(s_tot - s_ns));
+            if (s_gbase + s_tot > a.dn_cap)
+                atomicOr((unsigned long long *)&a.ctr->overflow, (unsigned long long)OVF_DENSE);
+        }
+        __syncthreads();
+        u64 idx = s_gbase + s_wbase[wv];
+        for (u32 k = 0; k < MBD_KS; ++k) {
+            const u32 i = threadIdx.x + k * MBD_T;
+            const u32 c = i < MA_SLOTS ? cnts[i] : 0u;
+            const u64 bm = __ballot(c != 0);
+            const u64 e = idx + mbcnt(bm);
+            idx += (u64)__popcll(bm);
+            if (c == 0) continue;
+            const ulonglong2 kk = keys[i];
+            keys[i] = make_ulonglong2(0, 0);  // the table clear for the next bucket
+            cnts[i] = 0;
+            if (e >= a.dn_cap) continue;
+            const bool sk = kk.y == KMARK;
+            const u64 k2 = ~(u64)c, k1 = __builtin_bswap64(kk.x), k0 = sk ? 0ull : __builtin_bswap64(kk.y & ~KMARK);
+            a.dn_K2[e] = k2;
+            a.dn_K1[e] = k1;
+            a.dn_K0[e] = k0;
+            a.dn_val[e] = (u32)e;
+            a.dn_ref[e] = ((u64)(sk ? KIND_S : KIND_M) << 60) | e;
+            a.dn_cnt[e] = c;
+            vo[0] |= k0; vo[1] |= k1; vo[2] |= k2;
+            va[0] &= k0; va[1] &= k1; va[2] &= k2;
+        }
     }
 #pragma unroll
     for (int w = 0; w < 3; ++w) {
@@ -1438,6 +1520,8 @@ __global__ __launch_bounds__(MBA_T) void k_mb_agg(ScanArgs a, u32 T, const u64 *
             va[w] &= (u64)__shfl_xor((long long)va[w], o);
         }
     }
+    if (threadIdx.x < 6) s_vary[threadIdx.x] = threadIdx.x < 3 ? 0ull : ~0ull;
+    __syncthreads();
     if (lane == 0) {
 #pragma unroll
         for (int w = 0; w < 3; ++w) {
@@ -1446,7 +1530,7 @@ __global__ __launch_bounds__(MBA_T) void k_mb_agg(ScanArgs a, u32 T, const u64 *
         }
     }
     __syncthreads();
-    if (threadIdx.x < 6) a.dn_vary[6 + q * 6 + threadIdx.x] = s_vary[threadIdx.x];
+    if (threadIdx.x < 6) a.dn_vary[6 + (u64)blockIdx.x * 6 + threadIdx.x] = s_vary[threadIdx.x];
 }
 // The dense planes' OR / AND from the bucket workgroups' partials (one
 // workgroup) into vary[0..5] (k_word_entries adds the long words' to them).
@@ -1531,6 +1615,17 @@ u64 msa_mb_hist_words(const ScanArgs &a, u32 nsrc) {
     return (u64)MSA_MLOG_PARTS * MB_B * nsrc * chunks;
 }
 hipError_t msa_exclusive_scan(const u64 *in, u64 n, u64 *out, u64 *bsum_scratch, u64 *total, hipStream_t s);
+// k_mb_dense's workgroups: one per CU (its LDS table is the whole LDS)
+static u32 msa_dn_groups() {
+    if (!g_q_cus) {
+        int dev = 0;
+        hipDeviceProp_t pr;
+        (void)hipGetDevice(&dev);
+        g_q_cus = (hipGetDeviceProperties(&pr, dev) == hipSuccess && pr.multiProcessorCount > 0) ? pr.multiProcessorCount
+                                                                                                   : 256;
+    }
+    return (u32)g_q_cus;
+}
 // hist / off: msa_mb_hist_words u64 each; bsum: (that + 1023) / 1024 + 1 words;
 // total: one word; out: nsrc * PARTS * mlog_cap entries
 hipError_t msa_launch_miss_buckets(const ScanArgs &a, u64 *hist, u64 *off, u64 *bsum, u64 *total, ulonglong2 *out,
@@ -1540,21 +1635,23 @@ hipError_t msa_launch_miss_buckets(const ScanArgs &a, u64 *hist, u64 *off, u64 *
     const u32 chunks = (a.mlog_cap + MB_TILE - 1) / MB_TILE, T = nsrc * chunks;
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void *)k_mb_agg<false>, hipFuncAttributeMaxDynamicSharedMemorySize, MA_SLOTS * 20);
-        (void)hipFuncSetAttribute((const void *)k_mb_agg<true>, hipFuncAttributeMaxDynamicSharedMemorySize, MA_SLOTS * 20);
+        (void)hipFuncSetAttribute((const void *)k_mb_agg, hipFuncAttributeMaxDynamicSharedMemorySize, MA_SLOTS * 20);
+        (void)hipFuncSetAttribute((const void *)k_mb_dense, hipFuncAttributeMaxDynamicSharedMemorySize, MA_SLOTS * 20);
+        (void)hipFuncSetAttribute((const void *)k_mb_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, MS_LDS);
         attr = true;
     }
     hipLaunchKernelGGL(k_mb_hist, dim3(T, MSA_MLOG_PARTS), dim3(MB_TT), 0, s, a, chunks, T, hist);
     hipError_t e = msa_exclusive_scan(hist, msa_mb_hist_words(a, nsrc), off, bsum, total, s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_mb_scatter, dim3(T, MSA_MLOG_PARTS), dim3(MB_TT), 0, s, a, chunks, T, (const u64 *)off, out);
+    hipLaunchKernelGGL(k_mb_scatter, dim3(T, MSA_MLOG_PARTS), dim3(MB_TT), MS_LDS, s, a, chunks, T, (const u64 *)off,
+                       out);
     if (a.dn_K2) {  // dense entries (the caller zeroed Counters::dense_n with the split's counters)
-        hipLaunchKernelGGL(k_mb_agg<true>, dim3(MB_B, MSA_MLOG_PARTS), dim3(MBA_T), MA_SLOTS * 20, s, a, T,
-                           (const u64 *)off, (const u64 *)total, (const ulonglong2 *)out);
-        hipLaunchKernelGGL(k_dn_vary, dim3(1), dim3(DV_T), 0, s, (const u64 *)a.dn_vary + 6, MSA_MLOG_PARTS * MB_B,
-                           a.dn_vary);
+        const u32 g = msa_dn_groups();
+        hipLaunchKernelGGL(k_mb_dense, dim3(g), dim3(MBD_T), MA_SLOTS * 20, s, a, T, (const u64 *)off,
+                           (const u64 *)total, (const ulonglong2 *)out);
+        hipLaunchKernelGGL(k_dn_vary, dim3(1), dim3(DV_T), 0, s, (const u64 *)a.dn_vary + 6, g, a.dn_vary);
     } else {
-        hipLaunchKernelGGL(k_mb_agg<false>, dim3(MB_B, MSA_MLOG_PARTS), dim3(MBA_T), MA_SLOTS * 20, s, a, T,
+        hipLaunchKernelGGL(k_mb_agg, dim3(MB_B, MSA_MLOG_PARTS), dim3(MBA_T), MA_SLOTS * 20, s, a, T,
                            (const u64 *)off, (const u64 *)total, (const ulonglong2 *)out);
     }
     return hipGetLastError();
@@ -1562,7 +1659,7 @@ hipError_t msa_launch_miss_buckets(const ScanArgs &a, u64 *hist, u64 *off, u64 *
 u32 msa_scan_blocks(const ScanArgs &a) { return scan_blocks(a); }
 // the dense planes' OR / AND: dn_vary holds msa_dn_vary_words() words, the
 // reduced six first (the radix sort's varying-byte mask), then the partials
-u64 msa_dn_vary_words() { return (u64)MSA_MLOG_PARTS * MB_B * 6 + 6; }
+u64 msa_dn_vary_words() { return (u64)msa_dn_groups() * 6 + 6; }
 hipError_t msa_launch_miss_agg(const ScanArgs &a, hipStream_t s) {
     if (!a.nchunks) return hipSuccess;
     const u32 blocks = scan_blocks(a);
