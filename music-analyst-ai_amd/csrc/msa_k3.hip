@@ -1441,16 +1441,36 @@ __global__ __launch_bounds__(MBD_T) void k_mb_dense(ScanArgs a, u32 T, const u64
     }
     u64 vo[3] = {0, 0, 0}, va[3] = {~0ull, ~0ull, ~0ull};
     const u64 nq = (u64)MSA_MLOG_PARTS * MB_B;
+    // bucket q's bounds and first batch of entries, loaded while the bucket
+    // before it is written out
+    u64 nlo = 0, nhi = 0;
+    ulonglong2 pf[MA_FLY];
+    auto prefetch = [&](u64 q) {
+        if (q >= nq) return;
+        nlo = off[q * T];
+        nhi = q + 1 < nq ? off[(q + 1) * T] : *total;
+#pragma unroll
+        for (int f = 0; f < MA_FLY; ++f) {
+            const u64 i = nlo + threadIdx.x + (u64)f * MBD_T;
+            pf[f] = i < nhi ? in[i] : make_ulonglong2(0, 0);
+        }
+    };
+    prefetch(blockIdx.x);
     for (u64 q = blockIdx.x; q < nq; q += gridDim.x) {
         if (threadIdx.x == 0) s_tot = s_ns = 0;
         __syncthreads();  // (the table clear / the last bucket's flush done)
-        const u64 lo = off[q * T], hi = q + 1 < nq ? off[(q + 1) * T] : *total;
+        const u64 lo = nlo, hi = nhi;
         for (u64 i0 = lo + threadIdx.x; i0 < hi; i0 += (u64)MA_FLY * MBD_T) {
             ulonglong2 xs[MA_FLY];
+            if (i0 == lo + threadIdx.x) {
 #pragma unroll
-            for (int f = 0; f < MA_FLY; ++f) {
-                const u64 i = i0 + (u64)f * MBD_T;
-                xs[f] = i < hi ? in[i] : make_ulonglong2(0, 0);
+                for (int f = 0; f < MA_FLY; ++f) xs[f] = pf[f];
+            } else {
+#pragma unroll
+                for (int f = 0; f < MA_FLY; ++f) {
+                    const u64 i = i0 + (u64)f * MBD_T;
+                    xs[f] = i < hi ? in[i] : make_ulonglong2(0, 0);
+                }
             }
 #pragma unroll
             for (int f = 0; f < MA_FLY; ++f) {
@@ -1488,6 +1508,7 @@ __global__ __launch_bounds__(MBD_T) void k_mb_dense(ScanArgs a, u32 T, const u64
             if (s_gbase + s_tot > a.dn_cap)
                 atomicOr((unsigned long long *)&a.ctr->overflow, (unsigned long long)OVF_DENSE);
         }
+        prefetch(q + gridDim.x);  // (in flight across the barrier and the write-out)
         __syncthreads();
         u64 idx = s_gbase + s_wbase[wv];
         for (u32 k = 0; k < MBD_KS; ++k) {
