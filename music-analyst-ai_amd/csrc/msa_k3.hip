@@ -1243,9 +1243,20 @@ __device__ __forceinline__ u32 mb_bucket(u64 k0, u64 k1m) {
 }
 // tile (part p, source s, chunk c) = entries [c MB_TILE, (c + 1) MB_TILE) of log (s, p);
 // t = s * chunks + c; hist[(p * MB_B + b) * T + t]
+// XCD-aware tile order: workgroup w runs on XCD w % 8, so the tiles t that
+// share a line of hist (and of the scatter's offsets and output runs) are
+// given to workgroups of one XCD -- the hist lines are then merged in that
+// XCD's L2 instead of written partially from eight (T a multiple of 8; else
+// the identity)
+__device__ __forceinline__ u32 mb_tile(u32 x, u32 T) {
+#ifdef MB_NOXCD  // (A/B builds)
+    return x;
+#endif
+    return (T & 7u) ? x : (x & 7u) * (T >> 3) + (x >> 3);
+}
 __global__ __launch_bounds__(MB_TT) void k_mb_hist(ScanArgs a, u32 chunks, u32 T, u64 *__restrict__ hist) {
     __shared__ u32 h[MB_B];
-    const u32 p = blockIdx.y, t = blockIdx.x, src = t / chunks, c = t % chunks;
+    const u32 p = blockIdx.y, t = mb_tile(blockIdx.x, T), src = t / chunks, c = t % chunks;
     for (u32 k = threadIdx.x; k < MB_B; k += MB_TT) h[k] = 0;
     __syncthreads();
     const u32 n = a.mlog_n[src * MSA_MLOG_PARTS + p];
@@ -1275,7 +1286,7 @@ __global__ __launch_bounds__(MB_TT) void k_mb_scatter(ScanArgs a, u32 chunks, u3
     u32 *loff = cnt + MB_B;
     u64 *gdel = reinterpret_cast<u64 *>(cnt);  // (after the staging) bucket b's output index - loff[b]
     __shared__ u32 wsum[MB_TT / 64];
-    const u32 p = blockIdx.y, t = blockIdx.x, src = t / chunks, c = t % chunks;
+    const u32 p = blockIdx.y, t = mb_tile(blockIdx.x, T), src = t / chunks, c = t % chunks;
     const u32 n = a.mlog_n[src * MSA_MLOG_PARTS + p];
     const u32 lo = c * MB_TILE, hi = min(n, lo + MB_TILE);
     if (lo >= hi) return;  // whole workgroup
