@@ -64,7 +64,7 @@ def test_mpirun_ranks_join_one_job(ranks_bin, world, tmp_path):
     p = subprocess.run([MPIRUN, "-np", str(world), ranks_bin, "launched"], capture_output=True, timeout=120,
                        cwd=tmp_path, env=_no_launcher_env())
     assert p.returncode == 0, p.stderr
-    assert _shm_leftovers() == before
+    assert set(_shm_leftovers()) <= set(before)  # (other xdist workers' jobs may end meanwhile)
 
 
 @needs_mpirun
@@ -75,7 +75,7 @@ def test_mpirun_failed_rank_ends_the_job(ranks_bin, tmp_path):
     p = subprocess.run([MPIRUN, "-np", "3", ranks_bin, "launched", "fail"], capture_output=True, timeout=120,
                        cwd=tmp_path, env=_no_launcher_env())
     assert p.returncode != 0
-    assert _shm_leftovers() == before
+    assert set(_shm_leftovers()) <= set(before)
 
 
 @pytest.mark.parametrize("world", [2, 4])
