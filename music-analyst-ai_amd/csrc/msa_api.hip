@@ -70,7 +70,9 @@ hipError_t msa_radix_sort_comp(u64 *const[3], u64 *const[3], u64 *const[3], u32 
                                hipStream_t, const u64 *, u64 *, u8 *, u32 *, u64 **, u32 **);
 hipError_t msa_comp_finish(u64 *, u64, const u8 *, u32, hipStream_t);
 u64 msa_tie_blocks(u64);
-hipError_t msa_launch_tie_count(const u64 *, const u64 *, const u64 *, u64, u64 *, u64 *, hipStream_t);
+hipError_t msa_launch_tie_count(const u64 *, const u64 *, const u64 *, u64, u64 *, u64 *, u64 *, hipStream_t);
+hipError_t msa_launch_tie_seg(const u64 *, const u64 *, const u64 *, const u32 *, u64, u64 *, u64 *, u64 *, u32 *,
+                              hipStream_t);
 hipError_t msa_launch_tie_build(const u64 *, const u64 *, const u64 *, u64, const u64 *, const u64 *, const u32 *,
                                 const u64 *, u32, const u64 *, const u64 *, const u64 *, const u8 *, const u8 *,
                                 const u64 *, const u32 *, const u8 *, const u64 *, const u32 *, u64 *, u64 *, u64 *,
@@ -311,6 +313,7 @@ struct msa_ctx {
     u64 fold_tbase = 0;
     u32 fold_ep = 0;
     int comp_sort = 1;      // env MSA_COMP_SORT=0: the words' radix sort by K2 and K1 (no composite key)
+    int tie_seg = 1;        // env MSA_TIE_SEG=0: every tie round through the radix sort (no k_tie_seg)
     // the K2 final-state read-back (launch_scan_fn / wait_scan_fn)
     hipEvent_t ev_fin = nullptr;
     State fin_init{};
@@ -1595,13 +1598,18 @@ static int refine_ties(msa_ctx *c, Ranked &R, int cur, const u8 *wbuf, const u8 
     u64 mc = n;
     for (u32 r = 1; r < 4096; ++r) {
         const u64 nb = msa_tie_blocks(mc);
-        HIPC(c, msa_launch_tie_count(K2, K1, K0, mc, rb.t_head.as<u64>(), rb.t_tie.as<u64>(), st));
+        // t_total: [0] runs, [1] tied entries, [2] a run longer than TIE_SEG (k_tie_count)
+        HIPC(c, hipMemsetAsync(rb.t_total.as<u64>() + 2, 0, 8, st));
+        HIPC(c, msa_launch_tie_count(K2, K1, K0, mc, rb.t_head.as<u64>(), rb.t_tie.as<u64>(),
+                                     rb.t_total.as<u64>() + 2, st));
         HIPC(c, msa_exclusive_scan2(rb.t_head.as<u64>(), nb, rb.t_runid.as<u64>(), rb.t_bsum.as<u64>(),
                                     rb.t_total.as<u64>(), rb.t_tie.as<u64>(), nb, rb.t_tpos.as<u64>(),
                                     rb.t_bsum.as<u64>() + nbb, rb.t_total.as<u64>() + 1, st));
-        u64 m = 0;
-        HIPC(c, hipMemcpyAsync(&m, rb.t_total.as<u64>() + 1, 8, hipMemcpyDeviceToHost, st));
+        u64 mb[2] = {0, 0};
+        HIPC(c, hipMemcpyAsync(mb, rb.t_total.as<u64>() + 1, 16, hipMemcpyDeviceToHost, st));
         HIPC(c, hipStreamSynchronize(st));
+        const u64 m = mb[0];
+        const bool seg = c->tie_seg && !mb[1];  // every run short: k_tie_seg orders them
         if (c->ablate & 4096) fprintf(stderr, "refine_ties: n %llu round %u ties %llu\n", (unsigned long long)n, r,
                                       (unsigned long long)m);
         if (!m) return MSA_OK;
@@ -1626,7 +1634,8 @@ static int refine_ties(msa_ctx *c, Ranked &R, int cur, const u8 *wbuf, const u8 
                                      key_off, key_len, k2[0], k1[0], k0[0], vv[0], rb.t_Vn.as<u32>(),
                                      rb.t_Pn.as<u64>(), st));
         int o = 1;
-        HIPC(c, msa_radix_sort(k2, k1, k0, vv, m, &o, rb.sort_scratch.as<u8>(), st));
+        if (seg) HIPC(c, msa_launch_tie_seg(k2[0], k1[0], k0[0], vv[0], m, k2[1], k1[1], k0[1], vv[1], st));
+        else HIPC(c, msa_radix_sort(k2, k1, k0, vv, m, &o, rb.sort_scratch.as<u8>(), st));
         HIPC(c, msa_launch_tie_apply(vv[o], rb.t_Vn.as<u32>(), rb.t_Pn.as<u64>(), m, R.order.as<u32>(),
                                      rb.t_Vc.as<u32>(), rb.t_Pc.as<u64>(), R.K[0][1].as<u64>(), R.K[0][2].as<u64>(),
                                      covered < 8 ? R.K[cur][1].as<u64>() : nullptr,
@@ -1993,6 +2002,7 @@ int msa_create(int device, msa_ctx **out) {
     if (const char *ab = getenv("MSA_ABLATE")) c->ablate = atoi(ab);
 #endif
     if (const char *cs = getenv("MSA_COMP_SORT")) c->comp_sort = atoi(cs) != 0;
+    if (const char *ts = getenv("MSA_TIE_SEG")) c->tie_seg = atoi(ts) != 0;
     if (const char *fo = getenv("MSA_FOLD")) c->fold = atoi(fo) != 0;
     if (const char *mb = getenv("MSA_MISS_BUCKETS")) c->mb_mode = atoi(mb);
     if (const char *mm = getenv("MSA_MISS_BUCKETS_MIN")) c->mb_min = strtoull(mm, nullptr, 10);

@@ -1952,10 +1952,18 @@ __device__ __forceinline__ TieFlags tie_flags(const u64 *__restrict__ K2, const 
     const bool eq_next = i + 1 < n && K2[i + 1] == a2 && (!k1s || K1[i + 1] == a1) && (!K0 || K0[i + 1] == a0);
     return TieFlags{!eq_prev, eq_prev || eq_next};
 }
+// Runs of at most TIE_SEG entries are ordered by k_tie_seg instead of the
+// radix sort; k_tie_count flags a longer one (its head equal to the entry
+// TIE_SEG places on) in *big.
+#define TIE_SEG 64
+__device__ __forceinline__ bool tie_same(const u64 *__restrict__ K2, const u64 *__restrict__ K1,
+                                         const u64 *__restrict__ K0, u64 i, u64 j) {
+    return K2[i] == K2[j] && (K1 == K2 || K1[i] == K1[j]) && (!K0 || K0[i] == K0[j]);
+}
 // entry (row k, thread t) of block b is entry b * TB_N + k * TB_T + t
 __global__ __launch_bounds__(TB_T) void k_tie_count(const u64 *__restrict__ K2, const u64 *__restrict__ K1,
                                                     const u64 *__restrict__ K0, u64 n, u64 *__restrict__ bh,
-                                                    u64 *__restrict__ bt) {
+                                                    u64 *__restrict__ bt, u64 *__restrict__ big) {
     __shared__ u32 ws[2][TB_T / 64];
     const u32 t = threadIdx.x;
     u32 h = 0, q = 0;
@@ -1966,6 +1974,7 @@ __global__ __launch_bounds__(TB_T) void k_tie_count(const u64 *__restrict__ K2, 
             const TieFlags f = tie_flags(K2, K1, K0, n, i);
             h += f.head;
             q += f.tie;
+            if (f.head && f.tie && i + TIE_SEG < n && tie_same(K2, K1, K0, i, i + TIE_SEG)) big[0] = 1;
         }
     }
     for (int o = 32; o > 0; o >>= 1) {
@@ -2099,6 +2108,33 @@ __global__ void k_tie_apply(const u32 *__restrict__ perm, const u32 *__restrict_
     if (ks1) ks1[Pn[j]] = K1u[e];  // the composite key's sort: tied entries share only bytes 0 .. skip-1
     Vc[j] = e;
     Pc[j] = Pn[j];
+}
+
+// A tie round whose runs all hold <= TIE_SEG entries (k_tie_count's flag
+// clear): each entry of the subset counts the members of its run -- contiguous,
+// equal run id K2n -- that the radix sort would put before it ((K1n, K0n),
+// then subset position: the sort is stable) and writes itself and its keys
+// at that place of set 1.  Same output as msa_radix_sort, without its ~20
+// launch-bound passes and its host round trip.
+__global__ void k_tie_seg(const u64 *__restrict__ K2n, const u64 *__restrict__ K1n, const u64 *__restrict__ K0n,
+                          const u32 *__restrict__ Vid, u64 m, u64 *__restrict__ O2, u64 *__restrict__ O1,
+                          u64 *__restrict__ O0, u32 *__restrict__ OV) {
+    const u64 j = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= m) return;
+    const u64 r = K2n[j], a1 = K1n[j], a0 = K0n[j];
+    u64 s = j, e = j + 1;
+    while (s > 0 && K2n[s - 1] == r) --s;
+    while (e < m && K2n[e] == r) ++e;
+    u64 rank = 0;
+    for (u64 i = s; i < e; ++i) {
+        const u64 b1 = K1n[i], b0 = K0n[i];
+        rank += b1 < a1 || (b1 == a1 && (b0 < a0 || (b0 == a0 && i < j)));
+    }
+    const u64 o = s + rank;
+    O2[o] = r;
+    O1[o] = a1;
+    O0[o] = a0;
+    OV[o] = Vid[j];
 }
 
 // ---------------------------------------------------------------------------
@@ -2760,8 +2796,14 @@ hipError_t msa_launch_blob(const u32 *order, u64 n, const u64 *ref, const u64 *K
 }
 
 u64 msa_tie_blocks(u64 n) { return (n + TB_N - 1) / TB_N; }
-hipError_t msa_launch_tie_count(const u64 *K2, const u64 *K1, const u64 *K0, u64 n, u64 *bh, u64 *bt, hipStream_t s) {
-    if (n) hipLaunchKernelGGL(k_tie_count, dim3((u32)msa_tie_blocks(n)), dim3(TB_T), 0, s, K2, K1, K0, n, bh, bt);
+hipError_t msa_launch_tie_count(const u64 *K2, const u64 *K1, const u64 *K0, u64 n, u64 *bh, u64 *bt, u64 *big,
+                                hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_tie_count, dim3((u32)msa_tie_blocks(n)), dim3(TB_T), 0, s, K2, K1, K0, n, bh, bt, big);
+    return hipGetLastError();
+}
+hipError_t msa_launch_tie_seg(const u64 *K2n, const u64 *K1n, const u64 *K0n, const u32 *Vid, u64 m, u64 *O2, u64 *O1,
+                              u64 *O0, u32 *OV, hipStream_t s) {
+    if (m) hipLaunchKernelGGL(k_tie_seg, grid1(m), dim3(256), 0, s, K2n, K1n, K0n, Vid, m, O2, O1, O0, OV);
     return hipGetLastError();
 }
 hipError_t msa_launch_tie_build(const u64 *K2, const u64 *K1, const u64 *K0, u64 mc, const u64 *hoff, const u64 *toff,

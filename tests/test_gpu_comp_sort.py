@@ -77,3 +77,34 @@ def test_comp_sort_zipf(msa_mod, tmp_path, monkeypatch):
     data = msa_mod.gen_corpus(20000, mode="zipf", seed=11)
     with msa_mod.Context(0) as c:
         check_against_oracle(msa_mod, c, data, tmp_path, "comp_zipf")
+
+
+def case_runs(case):
+    """Tie runs of bounded length: groups sharing their first 8 key bytes and a
+    count (k_tie_seg orders runs of <= 64 entries; one longer run sends the
+    round through the radix sort)."""
+    ws = []
+    if case == "short_runs":  # runs of 2..64; long keys tie again on bytes 8..23 (a second round)
+        for g in range(160):
+            size, cnt = 2 + g % 63, 1 + g % 3
+            ws += [("q" + letters(g, 7) + letters(i, 2), cnt) for i in range(size)]
+        for g in range(40):
+            ws += [("zz" + letters(g, 6) + "abcdefghijklmnop" + letters(i, 2), 2) for i in range(1 + g % 20)]
+        return ws
+    sizes = [64] * 40 if case == "runs_64" else [64] * 20 + [65] + [3] * 50
+    for g, size in enumerate(sizes):
+        ws += [("r" + letters(g, 7) + letters(i, 3), 1) for i in range(size)]
+    return ws
+
+
+@pytest.mark.parametrize("seg", ["1", "0"])
+@pytest.mark.parametrize("case", ["short_runs", "runs_64", "runs_65"])
+def test_tie_rounds_short_runs(msa_mod, tmp_path, monkeypatch, case, seg):
+    """k_tie_seg (MSA_TIE_SEG=1, the default) against the radix-sorted tie
+    rounds (MSA_TIE_SEG=0) and the oracle: runs of up to 64 entries, exactly
+    64, and one of 65 (the round falls back to the radix sort)."""
+    monkeypatch.setenv("MSA_SORT", "radix")
+    monkeypatch.setenv("MSA_TIE_SEG", seg)
+    data = corpus(case_runs(case), seed=7 + len(case))
+    with msa_mod.Context(0) as c:
+        check_against_oracle(msa_mod, c, data, tmp_path, f"tieseg_{case}_{seg}")
