@@ -36,15 +36,22 @@ struct ScanJob {
 };
 struct ScanJobs {
     ScanJob j[2];
+    u64 tile;  // elements per block: SCAN_TILE, or SCAN_TILE_BIG for long arrays
 };
+// long arrays (configs[4]'s 50 M blob lengths): 16 elements a thread, so the
+// single-workgroup top scan sees 12 K block sums instead of 49 K (96 us)
+#define SCAN_PER_BIG 16
+#define SCAN_TILE_BIG (SCAN_T * SCAN_PER_BIG)
 
+template <int PER>
 __global__ __launch_bounds__(SCAN_T) void k_scan_reduce(ScanJobs js) {
     const ScanJob &J = js.j[blockIdx.y];
     __shared__ u64 red[SCAN_T / 64];
-    const u64 base = (u64)blockIdx.x * SCAN_TILE;
+    const u64 base = (u64)blockIdx.x * (SCAN_T * PER);
     if (base >= J.n) return;
     u64 s = 0;
-    for (int i = 0; i < SCAN_PER; ++i) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
         const u64 idx = base + (u64)i * SCAN_T + threadIdx.x;
         if (idx < J.n) s += J.in[idx];
     }
@@ -80,7 +87,7 @@ __global__ __launch_bounds__(SCAN_TOP_T) void k_scan_top(ScanJobs js) {
     }
     __shared__ u64 wtot[SCAN_TOP_T / 64];
     const u32 T = blockDim.x;
-    const u64 nb = (J.n + SCAN_TILE - 1) / SCAN_TILE;
+    const u64 nb = (J.n + js.tile - 1) / js.tile;
     const u64 per = (nb + T - 1) / T;
     const u64 a = min(nb, (u64)threadIdx.x * per), b = min(nb, a + per);
     u64 s = 0;
@@ -119,16 +126,18 @@ __global__ __launch_bounds__(SCAN_TOP_T) void k_scan_top(ScanJobs js) {
     }
 }
 
+template <int PER>
 __global__ __launch_bounds__(SCAN_T) void k_scan_down(ScanJobs js) {
     const ScanJob &J = js.j[blockIdx.y];
     __shared__ u64 wsum[SCAN_T / 64];
-    const u64 base = (u64)blockIdx.x * SCAN_TILE;
+    const u64 base = (u64)blockIdx.x * (SCAN_T * PER);
     if (base >= J.n) return;
     const u32 lane = lane_id(), w = threadIdx.x >> 6;
-    // thread t owns elements base + t*SCAN_PER .. +SCAN_PER (blocked)
-    u64 v[SCAN_PER], s = 0;
-    for (int i = 0; i < SCAN_PER; ++i) {
-        const u64 idx = base + (u64)threadIdx.x * SCAN_PER + i;
+    // thread t owns elements base + t*PER .. +PER (blocked)
+    u64 v[PER], s = 0;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const u64 idx = base + (u64)threadIdx.x * PER + i;
         v[i] = idx < J.n ? J.in[idx] : 0;
         s += v[i];
     }
@@ -143,8 +152,9 @@ __global__ __launch_bounds__(SCAN_T) void k_scan_down(ScanJobs js) {
     u64 pre = J.bsum[blockIdx.x];
     for (u32 i = 0; i < w; ++i) pre += wsum[i];
     pre += x - s;
-    for (int i = 0; i < SCAN_PER; ++i) {
-        const u64 idx = base + (u64)threadIdx.x * SCAN_PER + i;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const u64 idx = base + (u64)threadIdx.x * PER + i;
         if (idx < J.n) J.out[idx] = pre;
         pre += v[i];
     }
@@ -163,10 +173,14 @@ hipError_t msa_exclusive_scan2(const u64 *in, u64 n, u64 *out, u64 *bsum, u64 *t
         hipLaunchKernelGGL(k_scan_zero_totals, dim3(1), dim3(64), 0, s, js);
         return hipGetLastError();
     }
-    const u64 nb = (nmax + SCAN_TILE - 1) / SCAN_TILE;
-    hipLaunchKernelGGL(k_scan_reduce, dim3((u32)nb, ny), dim3(SCAN_T), 0, s, js);
-    hipLaunchKernelGGL(k_scan_top, dim3(1, ny), dim3(nb > SCAN_TOP_BIG ? SCAN_TOP_T : SCAN_T), 0, s, js);
-    hipLaunchKernelGGL(k_scan_down, dim3((u32)nb, ny), dim3(SCAN_T), 0, s, js);
+    const bool big = (nmax + SCAN_TILE - 1) / SCAN_TILE > SCAN_TOP_BIG;
+    js.tile = big ? SCAN_TILE_BIG : SCAN_TILE;
+    const u64 nb = (nmax + js.tile - 1) / js.tile;
+    if (big) hipLaunchKernelGGL(k_scan_reduce<SCAN_PER_BIG>, dim3((u32)nb, ny), dim3(SCAN_T), 0, s, js);
+    else hipLaunchKernelGGL(k_scan_reduce<SCAN_PER>, dim3((u32)nb, ny), dim3(SCAN_T), 0, s, js);
+    hipLaunchKernelGGL(k_scan_top, dim3(1, ny), dim3(big ? SCAN_TOP_T : SCAN_T), 0, s, js);
+    if (big) hipLaunchKernelGGL(k_scan_down<SCAN_PER_BIG>, dim3((u32)nb, ny), dim3(SCAN_T), 0, s, js);
+    else hipLaunchKernelGGL(k_scan_down<SCAN_PER>, dim3((u32)nb, ny), dim3(SCAN_T), 0, s, js);
     return hipGetLastError();
 }
 hipError_t msa_exclusive_scan(const u64 *in, u64 n, u64 *out, u64 *bsum_scratch, u64 *total, hipStream_t s) {
