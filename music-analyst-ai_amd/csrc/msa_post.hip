@@ -126,37 +126,56 @@ __global__ __launch_bounds__(SCAN_TOP_T) void k_scan_top(ScanJobs js) {
     }
 }
 
-template <int PER>
+// CH chunks of SCAN_TILE elements a block (CH = SCAN_PER_BIG / SCAN_PER for
+// long arrays), each in the blocked SCAN_PER-a-thread layout -- 16 elements
+// a thread in one run had made the lanes' loads and stores 128 bytes apart
+// (320 vs 171 us for 50 M) -- with every chunk's loads issued up front and
+// the prefix carried from chunk to chunk
+template <int CH>
 __global__ __launch_bounds__(SCAN_T) void k_scan_down(ScanJobs js) {
     const ScanJob &J = js.j[blockIdx.y];
-    __shared__ u64 wsum[SCAN_T / 64];
-    const u64 base = (u64)blockIdx.x * (SCAN_T * PER);
-    if (base >= J.n) return;
+    __shared__ u64 wsum[CH][SCAN_T / 64];
+    const u64 base0 = (u64)blockIdx.x * (SCAN_TILE * CH);
+    if (base0 >= J.n) return;
     const u32 lane = lane_id(), w = threadIdx.x >> 6;
-    // thread t owns elements base + t*PER .. +PER (blocked)
-    u64 v[PER], s = 0;
+    // thread t owns elements base + t*SCAN_PER .. +SCAN_PER (blocked) of each chunk
+    u64 v[CH][SCAN_PER], s[CH], x[CH];
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-        const u64 idx = base + (u64)threadIdx.x * PER + i;
-        v[i] = idx < J.n ? J.in[idx] : 0;
-        s += v[i];
+    for (int c = 0; c < CH; ++c) {
+        s[c] = 0;
+#pragma unroll
+        for (int i = 0; i < SCAN_PER; ++i) {
+            const u64 idx = base0 + (u64)c * SCAN_TILE + (u64)threadIdx.x * SCAN_PER + i;
+            v[c][i] = idx < J.n ? J.in[idx] : 0;
+        }
     }
-    // inclusive wave scan of s
-    u64 x = s;
-    for (int o = 1; o < 64; o <<= 1) {
-        u64 y = __shfl_up(x, o);
-        if (lane >= (u32)o) x += y;
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+#pragma unroll
+        for (int i = 0; i < SCAN_PER; ++i) s[c] += v[c][i];
+        // inclusive wave scan of s
+        x[c] = s[c];
+        for (int o = 1; o < 64; o <<= 1) {
+            const u64 y = __shfl_up(x[c], o);
+            if (lane >= (u32)o) x[c] += y;
+        }
+        if (lane == 63) wsum[c][w] = x[c];
     }
-    if (lane == 63) wsum[w] = x;
     __syncthreads();
-    u64 pre = J.bsum[blockIdx.x];
-    for (u32 i = 0; i < w; ++i) pre += wsum[i];
-    pre += x - s;
+    u64 carry = J.bsum[blockIdx.x];
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-        const u64 idx = base + (u64)threadIdx.x * PER + i;
-        if (idx < J.n) J.out[idx] = pre;
-        pre += v[i];
+    for (int c = 0; c < CH; ++c) {
+        u64 pre = carry;
+        for (u32 i = 0; i < w; ++i) pre += wsum[c][i];
+        pre += x[c] - s[c];
+        const u64 base = base0 + (u64)c * SCAN_TILE;
+#pragma unroll
+        for (int i = 0; i < SCAN_PER; ++i) {
+            const u64 idx = base + (u64)threadIdx.x * SCAN_PER + i;
+            if (idx < J.n) J.out[idx] = pre;
+            pre += v[c][i];
+        }
+        for (u32 i = 0; i < SCAN_T / 64; ++i) carry += wsum[c][i];
     }
 }
 
@@ -179,8 +198,8 @@ hipError_t msa_exclusive_scan2(const u64 *in, u64 n, u64 *out, u64 *bsum, u64 *t
     if (big) hipLaunchKernelGGL(k_scan_reduce<SCAN_PER_BIG>, dim3((u32)nb, ny), dim3(SCAN_T), 0, s, js);
     else hipLaunchKernelGGL(k_scan_reduce<SCAN_PER>, dim3((u32)nb, ny), dim3(SCAN_T), 0, s, js);
     hipLaunchKernelGGL(k_scan_top, dim3(1, ny), dim3(big ? SCAN_TOP_T : SCAN_T), 0, s, js);
-    if (big) hipLaunchKernelGGL(k_scan_down<SCAN_PER_BIG>, dim3((u32)nb, ny), dim3(SCAN_T), 0, s, js);
-    else hipLaunchKernelGGL(k_scan_down<SCAN_PER>, dim3((u32)nb, ny), dim3(SCAN_T), 0, s, js);
+    if (big) hipLaunchKernelGGL(k_scan_down<SCAN_PER_BIG / SCAN_PER>, dim3((u32)nb, ny), dim3(SCAN_T), 0, s, js);
+    else hipLaunchKernelGGL(k_scan_down<1>, dim3((u32)nb, ny), dim3(SCAN_T), 0, s, js);
     return hipGetLastError();
 }
 hipError_t msa_exclusive_scan(const u64 *in, u64 n, u64 *out, u64 *bsum_scratch, u64 *total, hipStream_t s) {
