@@ -28,15 +28,18 @@ hipError_t msa_launch_scan_tokens(const ScanArgs &, hipStream_t);
 hipError_t msa_launch_miss_agg(const ScanArgs &, hipStream_t);
 u64 msa_mb_hist_words(const ScanArgs &, u32);
 u32 msa_scan_blocks(const ScanArgs &);
+u32 msa_tok_wgcu();
 hipError_t msa_launch_scan_fold(const ScanArgs &, u64 *, hipStream_t);
 u32 msa_fold_tiles(u32);
 hipError_t msa_launch_miss_buckets(const ScanArgs &, u64 *, u64 *, u64 *, u64 *, ulonglong2 *, hipStream_t);
 hipError_t msa_exclusive_scan(const u64 *, u64, u64 *, u64 *, u64 *, hipStream_t);
+hipError_t msa_launch_csv_lines(int, const u64 *, const u8 *, const u64 *, u64, u64, u64, int, u64 *, u64 *, u64 *,
+                                u64 *, u8 *, hipStream_t);
 hipError_t msa_exclusive_scan2(const u64 *, u64, u64 *, u64 *, u64 *, const u64 *, u64, u64 *, u64 *, u64 *,
                                hipStream_t);
 hipError_t msa_launch_rec_spans(const u8 *, const u64 *, const u32 *, u64, u64, int, u64 *, u64 *, u32 *, u64 *, u64 *,
                                 u32 *, Counters *, const AKeys &, const u64 *, const u64 *, const u64 *, u64 *, int,
-                                hipStream_t);
+                                hipStream_t, hipEvent_t);
 hipError_t msa_launch_artist_count(const u64 *, const u32 *, const u64 *, const u64 *, u64, u64 *, u64, u32 *, u64,
                                    Counters *, int, int, ulonglong2 *, u32 *, u32, hipStream_t);
 hipError_t msa_launch_first_end(const u8 *, u64, u32, u32, u64 *, hipStream_t);
@@ -160,12 +163,13 @@ enum {
     ST_MISS_AGG,         // K3's logged LDS-table misses -> word tables (k_miss_agg)
     ST_REC_SPANS,        // both columns' line spans + artist keys (k_rec_fast / k_rec_fix) + offset scans
     ST_CSV_TOKENS,       // split scan, second kernel: lyric tokens -> word tables (k_scan_tokens)
+    ST_REC_FAST,         // k_rec_fast alone (inside ST_REC_SPANS)
     ST_COUNT_
 };
 const char *const kStageName[ST_COUNT_] = {"csv_summary", "csv_scan",    "artist_column", "text_column",
                                            "artist_summary", "artist_scan", "artist_keys",  "long_words",
                                            "rank_words",  "rank_artists", "csv_miss_agg", "rec_spans",
-                                           "csv_tokens"};
+                                           "csv_tokens",  "rec_fast"};
 
 struct ProfStage {
     hipEvent_t a = nullptr, b = nullptr;
@@ -260,14 +264,17 @@ struct msa_ctx {
     // least dense_min distinct 3..16-byte words (high cardinality) buckets its
     // logs and writes the words' ranking entries directly -- no HBM word
     // table inserts, slot lists, table clears or k_word_entries over them.
-    // Single GPU only (the multi-GPU merge exports the tables).  env
-    // MSA_DENSE=0 turns it off, MSA_DENSE_MIN sets the threshold.
+    // A multi-GPU shard exports its dense entries' key partitions from the
+    // planes (fill_exp_src); the rank that imports a partition counts it in
+    // its tables.  env MSA_DENSE=0 turns it off, MSA_DENSE_MIN sets the
+    // threshold.
     bool dense_on = true;
     u64 dense_min = 4000000;
     u64 prev_distinct = 0;  // the last split's distinct S + M words
+    bool have_hist = false; // prev_distinct is a split's count (not the context's first split)
     bool dense_w = false;   // the current split's words are dense entries (Ranked rw's planes)
-    bool dense_veto = false;  // a dense split overflowed (a bucket past its LDS table): tables from now on
-    bool sharded = false;     // msa_set_shard was called: a multi-GPU shard
+    bool dense_veto = false;  // a dense split overflowed (a bucket past its LDS table): tables until the input changes
+    bool sharded = false;     // msa_set_shard was called: a multi-GPU shard (diagnostic)
     DevBuf lmask;         // the split scan's lyric token-byte mask (k_scan_struct -> k_scan_tokens)
     u64 s_slots = 0, m_slots = 0, l_occ_cap = 0, lt_slots = 0, a_slots = 0;
     u64 s_used_prev = 0, m_used_prev = 0, lt_used_prev = 0, a_used_prev = 0;
@@ -277,6 +284,7 @@ struct msa_ctx {
     // table (msa_run retries); the grown size is kept for later runs.
     u32 s_log2 = 0, m_log2 = 0, lt_log2 = 0, a_log2 = 0;
     u64 l_occ_want = 0;
+    u64 l_occ_last = 0;  // the last split's long-word position reservations (sizes the waves' ranges)
     u64 mlog_want = 0;  // K3 log entries the last split needed (grown when a log partition filled)
     u64 mlog_test = 0;  // env MSA_MLOG_ENTRIES (tests): the logs' first size, so that they overflow
     u64 mlog_cap_last = 0;  // entries per partition of the last split's logs
@@ -343,6 +351,11 @@ struct msa_ctx {
     // back are copied here asynchronously and waited for with one sync
     // (pageable destinations made every copy a round trip of its own)
     unsigned char *pin = nullptr;
+    // word_counts.csv / top_artists.csv bytes (msa_write_table_csv): line
+    // lengths, offsets and the scan's scratch, the lines, and two pinned
+    // staging halves the host writes from while the next half is copied
+    DevBuf csv_len, csv_pos, csv_bsum, csv_out;
+    unsigned char *csv_pin = nullptr;
     // profiling
     bool prof = false;
     ProfStage ps[ST_COUNT_];
@@ -369,6 +382,14 @@ static void prof_begin(msa_ctx *c, int id, hipStream_t st = nullptr) {
         (void)hipEventCreate(&s.b);
     }
     (void)hipEventRecord(s.a, st ? st : c->stream);
+}
+// a stage whose end event the launcher records itself (between two kernels)
+static hipEvent_t prof_end_event(msa_ctx *c, int id, u64 bytes) {
+    if (!c->prof) return nullptr;
+    ProfStage &s = c->ps[id];
+    s.pend_bytes = bytes;
+    s.pending = true;
+    return s.b;
 }
 static void prof_end(msa_ctx *c, int id, u64 bytes, hipStream_t st = nullptr) {
     if (!c->prof) return;
@@ -613,7 +634,11 @@ static int ensure_tables(msa_ctx *c) {
     if (!c->s_log2) c->s_log2 = std::min<u32>(20, cap_s);
     if (!c->m_log2) c->m_log2 = std::min<u32>(18, cap_s);
     if (!c->lt_log2) c->lt_log2 = std::min<u32>(16, cap_s);
-    if (!c->l_occ_want) c->l_occ_want = std::max<u64>(1ull << 16, n / 1024);
+    // long-word positions: a word of > 16 bytes and its separator take >= 18
+    // bytes; room for one in every 128 bytes (20 B of arrays per slot) covers
+    // corpora far richer in long words than lyrics without a retry -- a cold run
+    // had repeated its whole split for them (configs[4])
+    if (!c->l_occ_want) c->l_occ_want = std::max<u64>(1ull << 16, n / 128);
     const u32 a_need = log2_ceil(std::max<u64>(1ull << 12, 2 * (c->nrec + 1)));
     if (!c->a_log2) c->a_log2 = std::min<u32>(16, a_need);
     const u64 s_slots = 1ull << c->s_log2, m_slots = 1ull << c->m_log2, lt_slots = 1ull << c->lt_log2;
@@ -675,7 +700,11 @@ static void grow_tables(msa_ctx *c, u64 mask = ~0ull) {
     if (f & OVF_S) grow(c->s_log2, c->h_ctr.s_claimed);
     if (f & OVF_M) grow(c->m_log2, c->h_ctr.m_claimed);
     if (f & OVF_LT) grow(c->lt_log2, c->h_ctr.l_claimed);
-    if (f & OVF_A) grow(c->a_log2, c->h_ctr.a_claimed);
+    if (f & OVF_A) {  // artists <= records: one step to the size that holds any input of this length
+        grow(c->a_log2, c->h_ctr.a_claimed);
+        const u32 a_need = log2_ceil(std::max<u64>(1ull << 12, 2 * (c->nrec + 1)));
+        if (c->a_log2 < a_need && a_need <= 31) c->a_log2 = a_need;
+    }
     if (f & OVF_L) c->l_occ_want = std::max<u64>(c->l_occ_want * 8, c->h_ctr.l_occ * 2);
 }
 
@@ -695,6 +724,10 @@ static void take_col_lens(msa_ctx *c) {
     c->tcol_len = c->have_tcol ? c->col_hdr[1] + c->h_ctr.col_body[1] : 0;
     c->a_end = c->acol_len;
     c->col_lens_pending = false;
+    // text.csv's stage bytes, now that the body length is known: the body read
+    // and written + per record its span (len, offset, source, "" pairs: 28 B)
+    if (c->ps[ST_TEXT_COLUMN].pending && c->have_tcol)
+        c->ps[ST_TEXT_COLUMN].pend_bytes = 2 * c->h_ctr.col_body[1] + c->nrec * 28;
 }
 static int sync_counters(msa_ctx *c) {
     HIPC(c, hipMemcpyAsync(c->pin, c->ctr.p, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
@@ -862,11 +895,17 @@ static int launch_spans(msa_ctx *c, bool want_text, hipStream_t st) {
     AKeys ak{c->arena.as<u8>(), c->key_off.as<u64>(), c->key_len.as<u32>(), c->kh1.as<u64>(), c->kh2.as<u64>(),
              long_base, c->a_long_cap};
     if (c->spans) HIPC(c, ensure(c->span_fix, (nrec + 1) * 8));
+    // k_rec_fast's own stage: per record 32 B of span events read (rec_start,
+    // f0, tss, tse), the record's first 32 bytes (its artist key), and 100 B
+    // written (both columns' len / src / pairs 40, key off / len / two
+    // hashes 28, the 32-byte key arena slot)
+    prof_begin(c, ST_REC_FAST, st);
+    const hipEvent_t fast_end = prof_end_event(c, ST_REC_FAST, nrec * 164);
     HIPC(c, msa_launch_rec_spans(c->in, c->rec_start.as<u64>(), c->nulrel.as<u32>(), nrec, c->cont ? 0 : 1,
                                  want_text ? 1 : 0, c->alen.as<u64>(), c->asrc.as<u64>(), c->apairs.as<u32>(),
                                  c->tlen.as<u64>(), c->tsrc.as<u64>(), c->tpairs.as<u32>(), c->ctr.as<Counters>(), ak,
                                  c->spans ? c->f0.as<u64>() : nullptr, c->tss.as<u64>(), c->tse.as<u64>(),
-                                 c->span_fix.as<u64>(), c->ablate, st));
+                                 c->span_fix.as<u64>(), c->ablate, st, fast_end));
     if ((rc = scan_columns(c, want_text, st))) return rc;
     prof_end(c, ST_REC_SPANS, nrec * 136, st);  // ~36 B read + 100 B written per record
     return MSA_OK;
@@ -1078,6 +1117,7 @@ static int split_once(msa_ctx *c, int flags) {
         a.m_list_cap = c->m_slots / 2;
         a.l_pos = c->l_pos.as<u64>();
         a.l_cap = c->l_occ_cap;
+        a.l_expect = c->l_occ_last ? c->l_occ_last : c->n / 1024;
         a.ctr = c->ctr.as<Counters>();
         a.want_nul = want_text ? 1 : 0;
         a.ablate = c->ablate;
@@ -1086,7 +1126,7 @@ static int split_once(msa_ctx *c, int flags) {
            // split logged (a full partition drops its further entries and flags
            // OVF_MLOG: the split runs again with larger logs; past the 2^24-entry
            // partition limit the token pass inserts them into HBM instead)
-            const u64 parts = (u64)c->cus * MSA_MLOG_PARTS;
+            const u64 parts = (u64)c->cus * msa_tok_wgcu() * MSA_MLOG_PARTS;
             u64 entries = std::max<u64>(std::max<u64>(parts * 1024, c->n / 16), c->mlog_want);
             if (c->mlog_test) entries = std::max<u64>(c->mlog_test, c->mlog_want);  // tests: small first logs
             // (a workgroup's 16 partitions are addressed with 32-bit byte offsets)
@@ -1185,8 +1225,14 @@ static int split_once(msa_ctx *c, int flags) {
         sst = c->rank2;
         HIPC(c, hipStreamWaitEvent(c->rank2, c->ev_scan_a, 0));
     }
-    c->dense_w = c->dense_on && !c->dense_veto && !c->sharded && !c->cont && !a.mlog_direct &&
-                 c->prev_distinct >= c->dense_min;
+    // the context's first split of a large input has no count to go by: it
+    // takes the dense entries, exact at any cardinality, and later splits
+    // choose by its count -- a table split that overflowed had cost a cold
+    // configs[4] run a 0.12 s aggregation into full tables before its repeat
+    // (a wrong guess costs a low-cardinality input ~1 ms once)
+    const bool cold_big = !c->have_hist && c->n >= (64ull << 20);
+    c->dense_w = c->dense_on && !c->dense_veto && !a.mlog_direct &&
+                 (c->prev_distinct >= c->dense_min || cold_big);
     if (c->dense_w) {
         // the words' entry planes, written by the bucketed aggregation: room
         // for every logged entry a distinct key, plus the long words
@@ -1280,6 +1326,8 @@ static int split_once(msa_ctx *c, int flags) {
     HIPC(c, hipStreamSynchronize(c->stream));
     memcpy(&c->h_ctr, c->pin, sizeof(Counters));
     c->prev_distinct = c->h_ctr.s_claimed + c->h_ctr.m_claimed;
+    c->have_hist = true;
+    c->l_occ_last = c->h_ctr.l_occ;
     if (c->dense_w) {
         // a bucket past its LDS table or the planes (OVF_DENSE from the
         // device: tables from now on), or a log partition that overflowed
@@ -1303,7 +1351,7 @@ static int split_once(msa_ctx *c, int flags) {
                                // again) and that would not be more (a partition fuller than the rest)
         u64 want = (c->h_ctr.k3_misses + c->h_ctr.mlog_full) / 4 * 5;
         if (c->h_ctr.overflow & OVF_MLOG)
-            want = std::max<u64>(want, 2 * std::max<u64>(c->mlog_want, c->mlog_cap_last * (u64)c->cus * MSA_MLOG_PARTS));
+            want = std::max<u64>(want, 2 * std::max<u64>(c->mlog_want, c->mlog_cap_last * (u64)c->cus * msa_tok_wgcu() * MSA_MLOG_PARTS));
         c->mlog_want = std::max<u64>(c->mlog_want, want);
     }
     if (!c->cont) {
@@ -1384,6 +1432,18 @@ static int do_split(msa_ctx *c, int flags) {
         ++c->split_attempts;
         rc = split_once(c, flags);
         if (rc != MSA_ERR_CAPACITY || !(c->h_ctr.overflow & kSplitOvf) || attempt == 11) return rc;
+        // a table split that overflowed the S / M tables found more distinct
+        // words than they hold: high cardinality, so the repeat takes the dense
+        // entries (no HBM word table to grow) instead of growing the tables --
+        // once; a split that is not dense-eligible grows them as before.  (A
+        // cold run had first counted configs[4] through two rounds of growing
+        // tables: the dense switch needs a count, and only a finished split
+        // gave one.)
+        if (!c->dense_w && (c->h_ctr.overflow & (OVF_S | OVF_M)) && c->dense_on && !c->dense_veto &&
+            c->prev_distinct < c->dense_min) {
+            c->prev_distinct = c->dense_min;
+            c->h_ctr.overflow &= ~(u64)(OVF_S | OVF_M);
+        }
         grow_tables(c, kSplitOvf);
         int wrc;
         if ((wrc = ensure_tables(c)) || (wrc = wipe_tables(c))) return wrc;
@@ -1454,6 +1514,15 @@ static int do_count(msa_ctx *c) {
     // a label with a '\n' (its rest is read as artist records): records != lines
     bool exact = c->artist_exact || c->artist_piece_set || c->a_hdr_getline < c->a_hdr_len;
     const u64 nl = std::min<u64>(c->h_ctr.l_occ, c->l_occ_cap);  // final since the split's read-back
+    {  // the long-word table from the occurrences: distinct long words <= nl,
+       // so 3 slots per occurrence never overflow (growing it round by round
+       // had cost a cold configs[4] run four long-word passes)
+        const u32 lt_need = std::min<u32>(26, log2_ceil(nl * 3 + 1));
+        if (lt_need > c->lt_log2) {
+            c->lt_log2 = lt_need;
+            if ((rc = ensure_tables(c))) return rc;
+        }
+    }
     bool long_ok = false;   // the long-word pass ran and its flags are in h_ctr
     bool long_ran = false;  // the long-word table holds a pass's counts
     if (!exact) {
@@ -1770,6 +1839,8 @@ static int sort_and_blob(msa_ctx *c, Ranked &R, const u8 *wbuf, const u8 *wextra
     return MSA_OK;
 }
 
+static hipError_t grow_keep(DevBuf &b, size_t bytes, size_t keep, hipStream_t s);
+
 // tables: bit 0 words, bit 1 artists (a table left out keeps its ranking)
 static int do_rank(msa_ctx *c, int tables = 3) {
     int rc;
@@ -1791,10 +1862,16 @@ static int do_rank(msa_ctx *c, int tables = 3) {
     // dense split: entries [0, lthr) are written already (k_mb_agg<true>), the
     // long words' are appended; the planes were sized for them by the split
     const bool dense = dw && c->dense_w && !c->merged_w;
-    if (dense && W.n && (W.K[0][0].cap < W.n * 8 || W.V[0].cap < W.n * 4 || W.ref.cap < W.n * 8 ||
-                         W.cnt.cap < W.n * 8))
-        return fail(c, MSA_ERR_HIP, "dense word entries: %llu entries past the planes' capacity",
-                    (unsigned long long)W.n);
+    if (dense && W.n) {
+        // the split sized the planes for the long words its long-word table
+        // could hold then; msa_count may have grown that table since (OVF_LT):
+        // the planes grow too, keeping the dense entries [0, lthr)
+        const u64 nd = W.lthr;
+        for (int k = 0; k < 3; ++k) HIPC(c, grow_keep(W.K[0][k], W.n * 8, nd * 8, c->stream));
+        HIPC(c, grow_keep(W.V[0], W.n * 4, nd * 4, c->stream));
+        HIPC(c, grow_keep(W.ref, W.n * 8, nd * 8, c->stream));
+        HIPC(c, grow_keep(W.cnt, W.n * 8, nd * 8, c->stream));
+    }
     if (dense && W.n) {
         EntryArgs ea{};
         const u64 nd = W.lthr;
@@ -2053,7 +2130,8 @@ void msa_destroy(msa_ctx *c) {
                      &c->nulrel, &c->f0, &c->tss, &c->tse, &c->span_fix, &c->alog, &c->alog_n, &c->acol, &c->alen, &c->aoff, &c->asrc, &c->apairs, &c->tcol, &c->tlen, &c->toff, &c->tsrc, &c->tpairs,
                      &c->tscan_bsum, &c->scan_bsum, &c->scan_total, &c->ar_start, &c->arena, &c->key_off,
                      &c->key_len, &c->key_slot, &c->s_tab, &c->s_list, &c->m_tab, &c->m_list, &c->l_pos, &c->l_len,
-                     &c->l_slot, &c->l_tab, &c->l_list, &c->a_tab, &c->a_list, &c->ctr, &c->kh1, &c->kh2, &c->mlog, &c->mlog_n, &c->lmask, &c->blob_tot, &c->fold_buf};
+                     &c->l_slot, &c->l_tab, &c->l_list, &c->a_tab, &c->a_list, &c->ctr, &c->kh1, &c->kh2, &c->mlog, &c->mlog_n, &c->lmask, &c->blob_tot, &c->fold_buf,
+                     &c->mb_hist, &c->mb_off, &c->mb_bsum, &c->mb_tot, &c->mb_out, &c->csv_len, &c->csv_pos, &c->csv_bsum, &c->csv_out};
     for (DevBuf *b : all) release(*b);
     for (Ranked *R : {&c->rw, &c->ra}) {
         for (auto &s : R->K)
@@ -2076,6 +2154,7 @@ void msa_destroy(msa_ctx *c) {
         if (s.b) (void)hipEventDestroy(s.b);
     }
     (void)hipHostFree(c->pin);
+    if (c->csv_pin) (void)hipHostFree(c->csv_pin);
     (void)hipEventDestroy(c->ev_fork);
     (void)hipEventDestroy(c->ev_join);
     (void)hipEventDestroy(c->ev_r2_fork);
@@ -2103,7 +2182,10 @@ int msa_sync(msa_ctx *c) {
 }
 
 int msa_load_csv(msa_ctx *c, const void *host, size_t n) {
-    if (c) c->fin_cache_n = 0;  // a new input
+    if (c) {
+        c->fin_cache_n = 0;    // a new input
+        c->dense_veto = false;  // a veto holds for the input that raised it
+    }
     if (!c || (!host && n)) return MSA_ERR_ARG;
     HIPC(c, hipSetDevice(c->device));
     HIPC(c, join_side(c));
@@ -2123,6 +2205,7 @@ int msa_load_csv(msa_ctx *c, const void *host, size_t n) {
 int msa_bind_csv(msa_ctx *c, const void *dev, size_t n) {
     if (!c || (!dev && n)) return MSA_ERR_ARG;
     c->fin_cache_n = 0;  // a new input
+    c->dense_veto = false;  // a veto holds for the input that raised it
     HIPC(c, join_side(c));
     c->in = reinterpret_cast<const u8 *>(dev);
     c->n = n;
@@ -2197,33 +2280,56 @@ int msa_write_table_csv(msa_ctx *c, int table, const char *path, const char *key
     if (c->stage < 3) return fail(c, MSA_ERR_ARG, "msa_write_table_csv before msa_rank");
     HIPC(c, hipSetDevice(c->device));
     Ranked &R = table == MSA_TABLE_WORDS ? c->rw : c->ra;
-    int rc = fetch_ranked(c, R);
-    if (rc) return rc;
-    FILE *fp = fopen(path, "w");
-    if (!fp) return fail(c, MSA_ERR_IO, "Failed to open output file %s: %s", path, strerror(errno));
-    std::vector<char> out;
-    out.reserve(1 << 20);
-    auto flush = [&]() {
-        if (!out.empty()) fwrite(out.data(), 1, out.size(), fp);
-        out.clear();
-    };
-    fprintf(fp, "%s,count\n", key_header);
     u64 m = R.n;
     if (limit > 0 && (u64)limit < m) m = (u64)limit;
-    char num[32];
-    for (u64 i = 0; i < m; ++i) {
-        out.push_back('"');
-        for (u64 k = R.h_off[i]; k < R.h_off[i + 1]; ++k) {
-            char ch = R.h_blob[k];
-            if (ch == '"') out.push_back('"');
-            out.push_back(ch);
-        }
-        int l = snprintf(num, sizeof num, "\",%lld\n", (long long)R.h_counts[i]);
-        out.insert(out.end(), num, num + l);
-        if (out.size() > (1 << 20)) flush();
+    // the lines are formatted on the device from the ranked arrays (k_csv_len,
+    // scan, k_csv_put) and written out in one pass
+    u64 total = 0;
+    if (m) {
+        HIPC(c, ensure(c->csv_len, m * 8));
+        HIPC(c, ensure(c->csv_pos, m * 8));
+        HIPC(c, ensure(c->csv_bsum, ((m + 1023) / 1024 + 1) * 8));
+        HIPC(c, ensure(c->small, 4096));
+        u64 *d_total = reinterpret_cast<u64 *>(c->small.as<char>() + 3072);
+        HIPC(c, msa_launch_csv_lines(0, R.off.as<u64>(), R.blob.as<u8>(), R.counts.as<u64>(), R.n, m, R.blob_len,
+                                     table == MSA_TABLE_ARTISTS, c->csv_len.as<u64>(), c->csv_pos.as<u64>(),
+                                     c->csv_bsum.as<u64>(), d_total, nullptr, c->stream));
+        HIPC(c, hipMemcpyAsync(c->pin + kPinSmall, d_total, 8, hipMemcpyDeviceToHost, c->stream));
+        HIPC(c, hipStreamSynchronize(c->stream));
+        memcpy(&total, c->pin + kPinSmall, 8);
+        HIPC(c, ensure(c->csv_out, total + 16));
+        HIPC(c, msa_launch_csv_lines(1, R.off.as<u64>(), R.blob.as<u8>(), R.counts.as<u64>(), R.n, m, R.blob_len,
+                                     table == MSA_TABLE_ARTISTS, c->csv_len.as<u64>(), c->csv_pos.as<u64>(),
+                                     c->csv_bsum.as<u64>(), d_total, c->csv_out.as<u8>(), c->stream));
     }
-    flush();
-    if (fclose(fp) != 0) return fail(c, MSA_ERR_IO, "write failed: %s", path);
+    FILE *fp = fopen(path, "w");
+    if (!fp) return fail(c, MSA_ERR_IO, "Failed to open output file %s: %s", path, strerror(errno));
+    fprintf(fp, "%s,count\n", key_header);
+    // a small file in one pageable copy; a large one through two pinned
+    // halves, half k + 1 copied while half k is written (pinning them costs
+    // ~20 ms once: not worth it for a few MB)
+    static const u64 kHalf = 16ull << 20;
+    bool ok = true;
+    if (total && total <= kHalf) {
+        std::vector<char> h(total);
+        HIPC(c, hipMemcpyAsync(h.data(), c->csv_out.p, total, hipMemcpyDeviceToHost, c->stream));
+        HIPC(c, hipStreamSynchronize(c->stream));
+        ok = fwrite(h.data(), 1, total, fp) == total;
+        total = 0;  // written
+    }
+    if (total && !c->csv_pin) HIPC(c, hipHostMalloc((void **)&c->csv_pin, 2 * kHalf, hipHostMallocDefault));
+    auto half = [&](u64 k) { return c->csv_pin + (k & 1) * kHalf; };
+    auto part = [&](u64 k) { return std::min<u64>(kHalf, total - k * kHalf); };
+    const u64 nk = (total + kHalf - 1) / kHalf;
+    if (nk) HIPC(c, hipMemcpyAsync(half(0), c->csv_out.as<u8>(), part(0), hipMemcpyDeviceToHost, c->stream));
+    for (u64 k = 0; k < nk; ++k) {
+        HIPC(c, hipStreamSynchronize(c->stream));  // half k is in
+        if (k + 1 < nk)  // (its half was written out by the previous trip)
+            HIPC(c, hipMemcpyAsync(half(k + 1), c->csv_out.as<u8>() + (k + 1) * kHalf, part(k + 1),
+                                   hipMemcpyDeviceToHost, c->stream));
+        ok = ok && fwrite(half(k), 1, part(k), fp) == part(k);
+    }
+    if (fclose(fp) != 0 || !ok) return fail(c, MSA_ERR_IO, "write failed: %s", path);
     return MSA_OK;
 }
 
@@ -2294,7 +2400,7 @@ static_assert(sizeof(msa_shard_fn) == sizeof(Fn), "msa_shard_fn mirrors Fn");
 int msa_set_shard(msa_ctx *c, int first) {
     if (!c) return MSA_ERR_ARG;
     c->cont = first == 0;
-    c->sharded = true;  // the merge exports the word tables: no dense entries from now on
+    c->sharded = true;
     return MSA_OK;
 }
 
@@ -2514,7 +2620,14 @@ static void fill_exp_src(msa_ctx *c, int table, ExpSrc &x, u64 *n) {
     x.extra = c->merged_w ? c->imp_w.as<u8>() : c->extra.as<u8>();
     x.l_pos = c->l_pos.as<u64>();
     x.l_len = c->l_len.as<u32>();
-    *n = x.ns + x.nm + x.nl;
+    if (c->dense_w && !c->merged_w) {  // the S / M words are the dense entries' planes
+        x.d_K1 = c->rw.K[0][1].as<u64>();
+        x.d_K0 = c->rw.K[0][2].as<u64>();
+        x.d_cnt = c->rw.cnt.as<u64>();
+        x.nd = x.ns + x.nm;  // (k_mb_dense counts its S and M entries into s_claimed / m_claimed)
+        x.ns = x.nm = 0;
+    }
+    *n = x.nd + x.ns + x.nm + x.nl;
 }
 
 int msa_export_partitions(msa_ctx *c, int table, int nparts, uint64_t *part_bytes) {
@@ -2523,8 +2636,10 @@ int msa_export_partitions(msa_ctx *c, int table, int nparts, uint64_t *part_byte
     if (c->stage < 2) return fail(c, MSA_ERR_ARG, "msa_export_partitions before msa_count");
     if (c->ranked_only & (table == MSA_TABLE_WORDS ? 1 : 2))
         return fail(c, MSA_ERR_ARG, "msa_export_partitions of a table merged by msa_import_ranked");
-    if (table == MSA_TABLE_WORDS && c->dense_w)
-        return fail(c, MSA_ERR_ARG, "msa_export_partitions of words counted as dense entries (call msa_set_shard first)");
+    // dense word entries are exported from their planes, which the ranking
+    // reorders: before msa_rank only (the pipeline's merge comes before it)
+    if (table == MSA_TABLE_WORDS && c->dense_w && !c->merged_w && c->stage >= 3)
+        return fail(c, MSA_ERR_ARG, "msa_export_partitions of dense word entries after msa_rank");
     HIPC(c, hipSetDevice(c->device));
     ExpSrc x;
     u64 n;
@@ -2594,8 +2709,6 @@ int msa_import_partitions(msa_ctx *c, int table, const void *src, const uint64_t
     HIPC(c, launch_artist_col(c));  // it reads key_off / key_len, which an artist import rewrites
     if (table != MSA_TABLE_WORDS && table != MSA_TABLE_ARTISTS) return MSA_ERR_ARG;
     if (c->stage < 2) return fail(c, MSA_ERR_ARG, "msa_import_partitions before msa_count");
-    if (table == MSA_TABLE_WORDS && c->dense_w)
-        return fail(c, MSA_ERR_ARG, "msa_import_partitions into words counted as dense entries (call msa_set_shard first)");
     HIPC(c, hipSetDevice(c->device));
     const bool art = table == MSA_TABLE_ARTISTS;
     const u64 total = blk_off[nblk];

@@ -327,6 +327,7 @@ struct ScanArgs {
     u64 m_list_cap;
     u64 *l_pos;
     u64 l_cap;
+    u64 l_expect;    // long-word occurrences expected (the last split's; sizes the waves' l_pos ranges)
     // K1's chunk summaries of this segment (bit 22 of h[0]: the chunk holds a
     // '\r' or NUL), or null: test every block
     const ChunkSum *sums;
@@ -428,6 +429,11 @@ struct ExpSrc {
     const u64 *key_off;
     const u32 *key_len;
     int artists;
+    // words counted as dense entries (k_mb_dense): entries [0, nd) come from
+    // their planes -- K1 / K0 the key's big-endian bytes, cnt the count -- in
+    // place of the S / M tables (ns = nm = 0); the long words from the table
+    const u64 *d_K1, *d_K0, *d_cnt;
+    u64 nd;
 };
 // Import destination: the (cleared) tables that receive a key partition.
 struct ImpDst {

@@ -29,8 +29,14 @@ namespace {
 #ifndef Q_T
 #define Q_T 1024                 // 16 waves: one workgroup per CU
 #endif
+#ifndef Q_WGCU
+#define Q_WGCU 1                 // token-pass workgroups per CU (2: each with half the LDS -- 8 waves per SIMD)
+#endif
 #define Q_W (Q_T / 64)
 #define Q_BLK 4096               // bytes per wave-iteration
+#ifndef Q_PROBE1
+#define Q_PROBE1 0               // 1: a bucket's second half read only by lanes its first half left open
+#endif
 #ifndef TOK_PF
 #define TOK_PF 1                 // batches of key loads in flight ahead of the probed one
 #endif
@@ -49,13 +55,13 @@ namespace {
 // (csv_scan + k_miss_agg, round 2): S and M words listed apart with a 1024-slot
 // M table 1.95 ms, mixed with an M table 1.99, mixed without an M table (the S
 // table takes the whole LDS) 1.82 -- the design kept.
-#ifndef Q_SSLOTS                 // the rest of the CU's LDS
-#define Q_SSLOTS (((163840 - Q_W * Q_WLDS - Q_CUR) / 12) & ~31)
+#ifndef Q_SSLOTS                 // the rest of the workgroup's share of the CU's LDS
+#define Q_SSLOTS (((163840 / Q_WGCU - Q_W * Q_WLDS - Q_CUR) / 12) & ~31)
 #endif
 #define Q_SNB (Q_SSLOTS / 4)
 #define Q_TAB (Q_SSLOTS * 12)
 #define Q_LDS (Q_TAB + Q_W * Q_WLDS + Q_CUR)
-static_assert(Q_LDS <= 163840, "K3 LDS exceeds the CU's 160 KiB");
+static_assert(Q_LDS * Q_WGCU <= 163840, "K3 LDS exceeds the CU's 160 KiB");
 static_assert(Q_SNB < 4096, "lds_find8 scales 20 hash bits by Q_SNB in 32 bits");
 static_assert(Q_SSLOTS % 32 == 0 && Q_TAB % 16 == 0 && Q_WLDS % 16 == 0,
               "LDS carve-outs stay 16-byte aligned");
@@ -234,8 +240,19 @@ __device__ __forceinline__ u32 lds_find8(u64 *skeys, u64 k0) {
     for (int p = 0; p < 2; ++p) {
         const u32 base = b * 4;
         const ulonglong2 s01 = *reinterpret_cast<const ulonglong2 *>(&skeys[base]);
+#if Q_PROBE1
+        // the bucket's second half read only by the lanes its first half did
+        // not settle (keys are claimed in slot order, so the Zipf head -- seen
+        // first -- sits in slots 0 / 1): fewer lanes per ds_read_b128, fewer
+        // bank conflicts
+        if (s01.x == k0) return base;
+        if (s01.y == k0) return base + 1;
+        const ulonglong2 s23 = *reinterpret_cast<const ulonglong2 *>(&skeys[base + 2]);
+        const u32 hit = s23.x == k0 ? 2u : (s23.y == k0 ? 3u : 4u);
+#else
         const ulonglong2 s23 = *reinterpret_cast<const ulonglong2 *>(&skeys[base + 2]);
         const u32 hit = s01.x == k0 ? 0u : (s01.y == k0 ? 1u : (s23.x == k0 ? 2u : (s23.y == k0 ? 3u : 4u)));
+#endif
         if (hit < 4) return base + hit;
         u32 i = s01.x == 0 ? 0u : (s01.y == 0 ? 1u : (s23.x == 0 ? 2u : (s23.y == 0 ? 3u : 4u)));
         for (; i < 4; ++i) {
@@ -258,8 +275,9 @@ __device__ __forceinline__ void hbm_insert16(const ScanArgs &a, u64 k0, u64 k1m,
 // made up a third of the kernel).  They are logged instead: per workgroup and
 // key partition (16 by key hash), plain 16-byte stores behind an LDS cursor;
 // k_miss_agg then counts each partition in LDS and adds each distinct key to
-// the HBM table once per aggregating workgroup.  A full log partition falls
-// back to the direct insert.
+// the HBM table once per aggregating workgroup.  A full log partition drops
+// the entry and flags OVF_MLOG (the split runs again with larger logs); only
+// at the 2^24-entry partition limit do entries go straight into the HBM table.
 __device__ __forceinline__ u32 mlog_part(u64 k0, u64 k1m) {
     // full-rate operations only: two 64-bit multiplies had cost six
     // quarter-rate v_mul_lo/hi_u32 per probe batch of the token pass
@@ -627,7 +645,8 @@ __device__ __forceinline__ void tok_epilogue(const ScanArgs &a, u64 *skeys, u32 
     if (threadIdx.x < MSA_MLOG_PARTS) {
         const u32 n = lcur[threadIdx.x];
         a.mlog_n[blockIdx.x * MSA_MLOG_PARTS + threadIdx.x] = min(n, a.mlog_cap);
-        // the next split sizes the logs from this (full partitions cost an HBM insert per entry)
+        // the next split sizes the logs from this (a full partition drops its
+        // further entries: OVF_MLOG, the split runs again with larger logs)
         if (n > a.mlog_cap) atomicAdd((unsigned long long *)&a.ctr->mlog_full, (unsigned long long)(n - a.mlog_cap));
     }
     if (threadIdx.x == 0 && lcur[MSA_MLOG_PARTS])  // misses dropped: this split is repeated
@@ -1057,7 +1076,7 @@ __global__ __launch_bounds__(FD_T, FD_MINW) void k_scan_fold(ScanArgs a) {
 // removed: the token lists software-pipelined across blocks, the next
 // block's list built before the current block's last batch is probed --
 // 1.02 vs 0.81 ms.)
-__global__ __launch_bounds__(Q_T, 1) void k_scan_tokens(ScanArgs a) {
+__global__ __launch_bounds__(Q_T, Q_WGCU) void k_scan_tokens(ScanArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     u64 *skeys = reinterpret_cast<u64 *>(smem);
     u32 *scnts = reinterpret_cast<u32 *>(smem + Q_SSLOTS * 8);
@@ -1079,9 +1098,14 @@ __global__ __launch_bounds__(Q_T, 1) void k_scan_tokens(ScanArgs a) {
     const u32 gw = __builtin_amdgcn_readfirstlane(blockIdx.x * Q_W + wib);
     const u32 nw = gridDim.x * Q_W;
     u64 words = 0;
-    // this wave's range of l_pos; ranges of ~a quarter of an even share of the capacity, 64..1024
+    // this wave's range of l_pos; ranges of ~a quarter of an even share of the
+    // occurrences expected (the capacity when none are), 8..1024 -- a floor of
+    // 64 had let ~1 K waves with one long word each reserve a 64 K-slot
+    // capacity whole (OVF_L and a repeated split for a few long words); unused
+    // range slots are walked by k_long_insert, so ranges follow the expected
+    // occurrences, not the (generous) capacity
     u64 lres = 0, lend = 0;
-    const u64 lch = min<u64>(1024, max<u64>(64, a.l_cap / ((u64)nw * 4)));
+    const u64 lch = min<u64>(1024, max<u64>(8, min(a.l_expect ? a.l_expect : a.l_cap, a.l_cap) / ((u64)nw * 4)));
     // mask words of the block: this lane's, the one after it and the one before
     u64 Lc = 0, Ln = 0, Lp = 0;
     uint4 warm = make_uint4(0, 0, 0, 0);
@@ -1346,6 +1370,7 @@ __device__ __forceinline__ void mb_insert_once(const ScanArgs &a, u64 k0, u64 k1
                 if (add) atomicAdd((unsigned long long *)(slot + 1), (unsigned long long)add);
                 return;
             }
+            if (table_full(probe, a.ctr, OVF_S)) break;
             h = (h + 1) & a.s_mask;
         }
         atomicOr((unsigned long long *)&a.ctr->overflow, (unsigned long long)OVF_S);
@@ -1375,6 +1400,7 @@ __device__ __forceinline__ void mb_insert_once(const ScanArgs &a, u64 k0, u64 k1
                 return;
             }
         }
+        if (table_full(probe, a.ctr, OVF_M)) break;
         h = (h + 1) & a.m_mask;
         ++probe;
     }
@@ -1609,8 +1635,9 @@ static u32 scan_blocks(const ScanArgs &a) {
     }
     const u64 units = (a.seg_end - a.seg_begin + Q_BLK - 1) / Q_BLK;
     const u64 blocks = (units + Q_W - 1) / Q_W;
-    return blocks > (u64)g_q_cus ? (u32)g_q_cus : (u32)blocks;
+    return blocks > (u64)g_q_cus * Q_WGCU ? (u32)g_q_cus * Q_WGCU : (u32)blocks;
 }
+u32 msa_tok_wgcu() { return Q_WGCU; }
 // The split scan's first kernel, k_scan_struct (msa_launch_scan_tokens then
 // runs the second on the same stream).
 hipError_t msa_launch_scan_csv(const ScanArgs &a, hipStream_t s) {

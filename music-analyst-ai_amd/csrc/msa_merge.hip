@@ -57,6 +57,18 @@ __device__ void exp_entry(const ExpSrc &x, u64 e, u64 *count, u32 *len, u64 *k0,
     *lower = 0;
     *k0 = 0;
     *k1 = 0;
+    if (x.d_K1) {  // dense entries first, then the long words (ns = nm = 0)
+        if (e < x.nd) {
+            *k0 = __builtin_bswap64(x.d_K1[e]);
+            *k1 = __builtin_bswap64(x.d_K0[e]);
+            *count = x.d_cnt[e];
+            u32 n = 0;
+            while (n < 16 && (((n < 8 ? *k0 : *k1) >> (8 * (n & 7))) & 0xFF)) ++n;
+            *len = n;
+            return;
+        }
+        e -= x.nd;
+    }
     if (x.artists) {
         const u64 slot = x.a_list[e];
         *count = x.a_tab[4 * slot + 1];

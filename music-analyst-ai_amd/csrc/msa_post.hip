@@ -2625,15 +2625,17 @@ static inline dim3 grid1(u64 n, u32 t = 256) { return dim3((u32)((n + t - 1) / t
 hipError_t msa_launch_rec_spans(const u8 *buf, const u64 *rs, const u32 *nul, u64 nrec, u64 first_rec, int text,
                                 u64 *alen, u64 *asrc, u32 *apairs, u64 *tlen, u64 *tsrc, u32 *tpairs, Counters *ctr,
                                 const AKeys &ak, const u64 *f0, const u64 *tss, const u64 *tse, u64 *fix,
-                                int ablate, hipStream_t s) {
+                                int ablate, hipStream_t s, hipEvent_t fast_end) {
     const SpanOut o{alen, asrc, apairs, tlen, tsrc, tpairs};
-    if (!nrec) return hipSuccess;
+    if (!nrec) return fast_end ? hipEventRecord(fast_end, s) : hipSuccess;
     if (!f0) {
         hipLaunchKernelGGL(k_rec_spans, grid1(nrec), dim3(256), 0, s, buf, rs, nul, nrec, first_rec, text, o, ctr, ak);
+        if (fast_end) (void)hipEventRecord(fast_end, s);
         return hipGetLastError();
     }
     hipLaunchKernelGGL(k_rec_fast, grid1(nrec), dim3(256), 0, s, buf, rs, f0, tss, tse, nrec, first_rec, text, o, ctr,
                        ak, fix, ablate);
+    if (fast_end) (void)hipEventRecord(fast_end, s);  // its own profiling stage ends here
     // the listed records: a fixed grid, the count read on the device
     const u64 fb = (nrec + 255) / 256 < 1024 ? (nrec + 255) / 256 : 1024;
     hipLaunchKernelGGL(k_rec_fix, dim3((u32)fb), dim3(256), 0, s, buf, rs, nul, first_rec, text, o, ctr, ak, fix);
@@ -2853,5 +2855,101 @@ hipError_t msa_launch_tie_build(const u64 *K2, const u64 *K1, const u64 *K0, u64
 hipError_t msa_launch_tie_apply(const u32 *perm, const u32 *Vn, const u64 *Pn, u64 m, u32 *order, u32 *Vc, u64 *Pc,
                                 const u64 *K1u, const u64 *K0u, u64 *ks1, u64 *ks0, hipStream_t s) {
     if (m) hipLaunchKernelGGL(k_tie_apply, grid1(m), dim3(256), 0, s, perm, Vn, Pn, m, order, Vc, Pc, K1u, K0u, ks1, ks0);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// word_counts.csv / top_artists.csv lines on the device (write_table_csv +
+// write_csv_entry, parallel_spotify.c:307-344): entry i of the ranked table
+// becomes `"<key with '"' doubled>",<count>\n`.  k_csv_len sizes every line,
+// one exclusive scan places them, k_csv_put writes them: a workgroup stages its
+// entries' keys (contiguous in the rank-ordered blob) and its lines (contiguous
+// in the output) in LDS, so both the key loads and the line stores are
+// coalesced; a workgroup whose keys or lines do not fit (very long keys)
+// writes straight to global memory.  The host copies the bytes out and writes
+// the file once (the per-entry formatting loop on the host had taken 2.4 s for
+// configs[4]'s 50 M words).
+#define CSV_T 256
+#define CSV_KEY_LDS 12288
+#define CSV_OUT_LDS 20480
+__device__ __forceinline__ u32 csv_digits(u64 v) {
+    u32 d = 1;
+    while (v >= 10) {
+        v /= 10;
+        ++d;
+    }
+    return d;
+}
+__device__ __forceinline__ u64 csv_key_end(const u64 *off, u64 i, u64 n, u64 blob_len) {
+    return i + 1 < n ? off[i + 1] : blob_len;
+}
+__global__ __launch_bounds__(CSV_T) void k_csv_len(const u64 *__restrict__ off, const u8 *__restrict__ blob,
+                                                   const u64 *__restrict__ cnt, u64 n, u64 m, u64 blob_len,
+                                                   int quotes, u64 *__restrict__ len) {
+    const u64 i = (u64)blockIdx.x * CSV_T + threadIdx.x;
+    if (i >= m) return;
+    const u64 b = off[i], e = csv_key_end(off, i, n, blob_len);
+    u64 dq = 0;
+    if (quotes)  // artists may hold '"' (word keys never do: token bytes are alnum and '\'')
+        for (u64 k = b; k < e; ++k) dq += blob[k] == '"';
+    len[i] = (e - b) + dq + csv_digits(cnt[i]) + 4;  // '"' key '"' ',' digits '\n'
+}
+__device__ __forceinline__ u8 *csv_line(u8 *o, const u8 *key, u64 klen, u64 count) {
+    *o++ = '"';
+    for (u64 k = 0; k < klen; ++k) {
+        const u8 ch = key[k];
+        if (ch == '"') *o++ = '"';
+        *o++ = ch;
+    }
+    *o++ = '"';
+    *o++ = ',';
+    const u32 d = csv_digits(count);
+    for (u32 k = d; k-- > 0;) {
+        o[k] = (u8)('0' + count % 10);
+        count /= 10;
+    }
+    o += d;
+    *o++ = '\n';
+    return o;
+}
+// pos: the scan of len (exclusive), pos_total: its total
+__global__ __launch_bounds__(CSV_T) void k_csv_put(const u64 *__restrict__ off, const u8 *__restrict__ blob,
+                                                   const u64 *__restrict__ cnt, u64 n, u64 m, u64 blob_len,
+                                                   const u64 *__restrict__ pos, const u64 *__restrict__ pos_total,
+                                                   u8 *__restrict__ out) {
+    __shared__ u8 kbuf[CSV_KEY_LDS];
+    __shared__ u8 obuf[CSV_OUT_LDS];
+    const u64 first = (u64)blockIdx.x * CSV_T, last = min(first + CSV_T, m);  // entries [first, last)
+    const u64 i = first + threadIdx.x;
+    const u64 kb = off[first], ke = csv_key_end(off, last - 1, n, blob_len);
+    const u64 ob = pos[first], oe = last < m ? pos[last] : *pos_total;
+    if (ke - kb <= CSV_KEY_LDS && oe - ob <= CSV_OUT_LDS) {
+        for (u64 j = threadIdx.x; j < ke - kb; j += CSV_T) kbuf[j] = blob[kb + j];
+        __syncthreads();
+        if (i < last) {
+            const u64 b = off[i], e = csv_key_end(off, i, n, blob_len);
+            csv_line(obuf + (pos[i] - ob), kbuf + (b - kb), e - b, cnt[i]);
+        }
+        __syncthreads();
+        for (u64 j = threadIdx.x; j < oe - ob; j += CSV_T) out[ob + j] = obuf[j];
+        return;
+    }
+    if (i < last) {
+        const u64 b = off[i], e = csv_key_end(off, i, n, blob_len);
+        csv_line(out + pos[i], blob + b, e - b, cnt[i]);
+    }
+}
+// lines of entries [0, m) of a ranked table (n entries, keys off / blob, counts
+// cnt).  phase 0: their lengths (len) and offsets (pos, total: the exclusive
+// scan, bsum its scratch); phase 1: the bytes into out (total bytes)
+hipError_t msa_launch_csv_lines(int phase, const u64 *off, const u8 *blob, const u64 *cnt, u64 n, u64 m, u64 blob_len,
+                                int quotes, u64 *len, u64 *pos, u64 *bsum, u64 *total, u8 *out, hipStream_t s) {
+    if (!m) return hipSuccess;
+    if (phase == 0) {
+        hipLaunchKernelGGL(k_csv_len, grid1(m, CSV_T), dim3(CSV_T), 0, s, off, blob, cnt, n, m, blob_len, quotes, len);
+        return msa_exclusive_scan(len, m, pos, bsum, total, s);
+    }
+    hipLaunchKernelGGL(k_csv_put, grid1(m, CSV_T), dim3(CSV_T), 0, s, off, blob, cnt, n, m, blob_len,
+                       (const u64 *)pos, (const u64 *)total, out);
     return hipGetLastError();
 }

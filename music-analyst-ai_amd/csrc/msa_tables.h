@@ -15,7 +15,23 @@
 #pragma once
 #include "msa_internal.h"
 
-#define MSA_MAX_PROBE 4096u
+// Linear probing: a table holds at most half as many keys as slots (its slot
+// list's capacity), where the longest probe runs stay far below this; an
+// insert that probes this far finds the table (nearly) full -- overflow, and
+// the stage repeats with a larger table.  (4096 let a full table take
+// thousands of L2 atomics per insert before the first one gave up.)
+#define MSA_MAX_PROBE 512u
+
+// A table that overflowed is full: every later insert into it would probe up
+// to MSA_MAX_PROBE slots with an L2 atomic each (a cold run on a
+// high-cardinality input spent seconds in such inserts before the retry that
+// grows the table).  Every 16 probes an insert checks the table's overflow bit
+// and gives up once it is set -- the stage is repeated with a larger table
+// anyway; an insert that finds its slot within 16 probes never reads it.
+__device__ __forceinline__ bool table_full(u32 probe, const Counters *ctr, u64 ovf_bit) {
+    return (probe & 15u) == 15u &&
+           (__hip_atomic_load(const_cast<u64 *>(&ctr->overflow), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ovf_bit) != 0;
+}
 
 // S / M keys are lower-cased token bytes (< 0x80) and zero padding, so bit 7
 // of every byte of the first key word is free: a claim writes the key with a
@@ -145,6 +161,7 @@ __device__ __forceinline__ void s_insert(u64 *tab, u64 mask, u64 key, u64 cnt, u
             found = true;
             break;
         }
+        if (table_full(probe, ctr, OVF_S)) break;
         h = (h + 1) & mask;
     }
     if (!found) atomicOr((unsigned long long *)&ctr->overflow, (unsigned long long)OVF_S);
@@ -184,6 +201,7 @@ __device__ __forceinline__ void m_insert(u64 *tab, u64 mask, u64 k0, u64 k1, u64
                 break;
             }
         }
+        if (table_full(probe, ctr, OVF_M)) break;
         h = (h + 1) & mask;
         ++probe;
     }
@@ -222,6 +240,7 @@ __device__ __forceinline__ u64 h_insert(u64 *tab, u64 mask, u64 hash, u64 cnt, u
             res = h;
             break;
         }
+        if (table_full(probe, ctr, ovf_bit)) break;
         h = (h + 1) & mask;
     }
     if (res == ~0ull) atomicOr((unsigned long long *)&ctr->overflow, (unsigned long long)ovf_bit);
@@ -282,6 +301,7 @@ __device__ __forceinline__ u64 h_insert2(u64 *tab, u64 mask, u64 hash, u64 cnt, 
             res = h;
             break;
         }
+        if (table_full(probe, ctr, ovf_bit)) break;
         h = (h + 1) & mask;
     }
     if (res == ~0ull) atomicOr((unsigned long long *)&ctr->overflow, (unsigned long long)ovf_bit);

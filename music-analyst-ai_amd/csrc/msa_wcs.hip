@@ -1416,6 +1416,8 @@ struct msa_wcs {
     u32 delim = ',';  // field delimiter (msa_wcs_set_delimiter: the script's --delimiter or csv.Sniffer's guess)
     hipEvent_t ev_a = nullptr, ev_b = nullptr;  // k_wcs_wrows of the last run (msa_wcs_kernel_ms)
     float wrows_ms = 0;
+    float csvcol_ms = 0;  // k_csvcol<1> of the last msa_csvcol_run (msa_csvcol_kernel)
+    u64 csvcol_out = 0;   // its output bytes
     u32 quote = '"';  // quotechar and skipinitialspace (msa_wcs_set_quoting): the column splitter's dialect
     u32 skipsp = 0;
     bool keep_bom = false;  // msa_wcs_set_encoding: "utf-8" keeps a leading BOM as data ("utf-8-sig" drops it)
@@ -1504,6 +1506,14 @@ extern "C" int msa_wcs_create(int device, msa_wcs **out) {
 // Not part of include/msa_hip.h: the last run's k_wcs_wrows time (HIP events
 // on the context's stream), for tools/bench_wcs.py's roofline.
 extern "C" double msa_wcs_kernel_ms(msa_wcs *w) { return w ? (double)w->wrows_ms : 0.0; }
+// The column splitter's copy kernel (k_csvcol<1>) of the last msa_csvcol_run:
+// HIP-event time and output bytes (tools/bench_wcs.py --path split: roofline)
+extern "C" int msa_csvcol_kernel(msa_wcs *w, double *ms, uint64_t *out_bytes) {
+    if (!w || !ms || !out_bytes) return MSA_ERR_ARG;
+    *ms = w->csvcol_ms;
+    *out_bytes = w->csvcol_out;
+    return MSA_OK;
+}
 
 extern "C" void msa_wcs_destroy(msa_wcs *w) {
     if (!w) return;
@@ -2138,9 +2148,13 @@ extern "C" int msa_csvcol_run(msa_wcs *w, int has_header, uint64_t *ncols, uint6
     if (hc.err != ~0ull) return wcs_input_error(w, hc.err);
     WCHECK(wpool(w, 22, outlen + 16, w->d_ccout));
     a.out = w->d_ccout;
+    WCHECK(hipEventRecord(w->ev_a, st));
     if (cells) hipLaunchKernelGGL(k_csvcol<1>, grid1(R), dim3(256), 0, st, a);
     WCHECK(hipGetLastError());
+    WCHECK(hipEventRecord(w->ev_b, st));
     WCHECK(hipStreamSynchronize(st));
+    WCHECK(hipEventElapsedTime(&w->csvcol_ms, w->ev_a, w->ev_b));
+    w->csvcol_out = outlen;
     w->cc_ncols = nc;
     w->cc_rows = R;
     w->cc_have = true;

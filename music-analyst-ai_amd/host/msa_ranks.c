@@ -468,6 +468,10 @@ static msa_shared *job_create(const char *path, int world) {
     return s;
 }
 
+static int creator_alive(const msa_shared *s) {
+    return s->tag > 0 && (kill((pid_t)s->tag, 0) == 0 || errno == EPERM);
+}
+
 /* the block rank 0 published; without PMI, poll for it (up to `wait_s`) */
 static msa_shared *job_open(const char *path, int world, double wait_s) {
     struct timespec t0, t;
@@ -482,7 +486,10 @@ static msa_shared *job_open(const char *path, int world, double wait_s) {
                 if (s == MAP_FAILED) s = NULL;
             }
             close(fd);
-            if (s && atomic_load(&s->ready) == SH_READY && s->world == world) return s;
+            /* a block whose creator is gone was left by a crashed job of the
+             * same key: keep polling for rank 0's fresh one (job_create
+             * unlinks the stale file before creating its own) */
+            if (s && atomic_load(&s->ready) == SH_READY && s->world == world && creator_alive(s)) return s;
             if (s) munmap(s, shared_bytes(world));
         }
         clock_gettime(CLOCK_MONOTONIC, &t);

@@ -179,3 +179,24 @@ def test_cli_under_mpirun_errors(case, msg, tmp_path):
                        env=_no_launcher_env())
     assert p.returncode != 0
     assert msg in p.stderr
+
+
+@pytest.mark.parametrize("case,procs", [("highcard_small", 2), ("highcard_small", 4), ("zipf_small", 3),
+                                        ("torture_17", 2)])
+def test_cli_processes_dense_entries(case, procs, tmp_path):
+    """--processes N with dense word entries forced on every rank
+    (MSA_DENSE_MIN=0): the ranks' merge exports their dense entries' key
+    partitions -- the same files as the reference at np=1."""
+    if case not in CASES:
+        pytest.skip(f"no golden case {case}")
+    res, files = golden(case, 1)
+    out = tmp_path / "out"
+    p = subprocess.run([CLI, os.path.join(GOLDEN, case, "input.csv"), "--output-dir", str(out),
+                        "--processes", str(procs)], capture_output=True, timeout=180,
+                       env=dict(os.environ, MSA_DENSE_MIN="0"))
+    assert p.returncode == 0, p.stderr
+    got = read_outputs(str(out))
+    assert got["metrics"] == {"processes": procs, "total_songs": res["total_songs"], "total_words": res["total_words"]}
+    assert got["word_counts.csv"] == files["word_counts.csv"]
+    assert got["top_artists.csv"] == files["top_artists.csv"]
+    assert p.stdout.decode("latin-1") == res["stdout"]

@@ -62,15 +62,15 @@ def test_dense_edge_cases(msa_mod, dense_ctx, tmp_path, name):
 def test_dense_then_tables_then_dense(msa_mod, dense_ctx, tmp_path):
     """Dense and table splits alternate on one context: a dense split leaves
     the word tables empty, a table split's claimed slots are cleared by the
-    next split's prologue."""
+    next split's prologue; a new input clears the previous input's veto."""
     a = msa_mod.gen_corpus(30_000, mode="highcard", seed=8)
     check_against_oracle(msa_mod, dense_ctx, a, tmp_path, "alt0")
     assert stat(dense_ctx, "dense") == 1
     check_against_oracle(msa_mod, dense_ctx, EDGE["multiline_text_header"], tmp_path, "alt1")  # vetoes dense
     assert stat(dense_ctx, "dense") == 0
-    check_against_oracle(msa_mod, dense_ctx, a, tmp_path, "alt2")
-    assert stat(dense_ctx, "dense") == 0  # the veto is kept by the context
     assert stat(dense_ctx, "s_table_used") == stat(dense_ctx, "s_claimed")
+    check_against_oracle(msa_mod, dense_ctx, a, tmp_path, "alt2")
+    assert stat(dense_ctx, "dense") == 1  # the veto held for the input that raised it (ADVICE round 5)
 
 
 def test_dense_small_logs(msa_mod, tmp_path, monkeypatch):
@@ -116,14 +116,33 @@ def test_dense_off(msa_mod, tmp_path, monkeypatch):
         assert stat(c, "dense") == 0
 
 
-def test_dense_not_for_shards(msa_mod, dense_ctx, tmp_path):
-    """A shard's word tables are exported by the multi-GPU merge: msa_set_shard
-    turns the dense path off; a dense split refuses the table export."""
+def test_dense_shard_exports_partitions(msa_mod, dense_ctx, tmp_path):
+    """A shard's dense word entries are exported as key-hash partitions from
+    their planes (round 5 turned dense off for shards): a world of one --
+    export, import, rank -- gives the oracle's bytes; after msa_rank the planes
+    are reordered, so a dense export is refused there."""
     data = msa_mod.gen_corpus(20_000, mode="highcard", seed=4)
-    check_against_oracle(msa_mod, dense_ctx, data, tmp_path, "dn_exp")
+    dense_ctx.set_shard(True)
+    p = tmp_path / "sh.csv"
+    p.write_bytes(data)
+    from conftest import read_outputs, run_oracle
+    r = run_oracle(str(p), str(tmp_path / "o"), ranks=1)
+    assert r.returncode == 0
+    exp = read_outputs(str(tmp_path / "o"))
+    dense_ctx.load_csv(data)
+    dense_ctx.split_columns(text_column=False)
+    dense_ctx.count()
+    assert stat(dense_ctx, "dense") == 1
+    for table in (msa_mod.MSA_TABLE_WORDS, msa_mod.MSA_TABLE_ARTISTS):
+        sizes = dense_ctx.export_partitions(table, 1)
+        buf = ctypes.create_string_buffer(max(1, sizes[0]))
+        dense_ctx.export_copy(ctypes.addressof(buf))
+        dense_ctx.import_partitions(table, ctypes.addressof(buf), [0, sizes[0]])
+    dense_ctx.rank()
+    assert msa_mod.table_csv_bytes(dense_ctx.ranked(msa_mod.MSA_TABLE_WORDS), "word") == exp["word_counts.csv"]
+    assert msa_mod.table_csv_bytes(dense_ctx.ranked(msa_mod.MSA_TABLE_ARTISTS), "artist") == exp["top_artists.csv"]
+    # a fresh dense split ranked without a merge: its planes are the ranking's now
+    check_against_oracle(msa_mod, dense_ctx, data, tmp_path, "dn_shard2")
     assert stat(dense_ctx, "dense") == 1
     with pytest.raises(Exception):
         dense_ctx.export_partitions(msa_mod.MSA_TABLE_WORDS, 2)
-    dense_ctx.set_shard(True)
-    check_against_oracle(msa_mod, dense_ctx, data, tmp_path, "dn_shard")
-    assert stat(dense_ctx, "dense") == 0

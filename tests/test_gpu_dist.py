@@ -35,6 +35,12 @@ ctx.load_csv(data)
 del data
 comm = mdist.Comm()
 songs, words = mdist.run_sharded(ctx, comm, text_column=False)
+if os.environ.get("MSA_STAT_OUT"):  # which word path the split took (dense entries or tables)
+    import ctypes
+    ctx.lib.msa_debug_stat.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint64)]
+    v = ctypes.c_uint64(0)
+    ctx.lib.msa_debug_stat(ctx.h, b"dense", ctypes.byref(v))
+    open(os.environ["MSA_STAT_OUT"] + f".{rank}", "w").write(str(v.value))
 if mdist.gather_ranked(ctx, comm):
     w = ctx.ranked(msa.MSA_TABLE_WORDS)
     a = ctx.ranked(msa.MSA_TABLE_ARTISTS)
@@ -364,3 +370,22 @@ def test_configs3_full_size_c_host_four_ranks(msa_mod, tmp_path):
             assert h.digest() == hashes[n].digest(), n
     finally:
         shutil.rmtree(d, ignore_errors=True)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_dense_entries(msa_mod, tmp_path, world):
+    """High cardinality on every shard with dense word entries forced
+    (MSA_DENSE_MIN=0): each rank exports its dense entries' key partitions,
+    imports its own partition into its tables and ranks it; rank 0's merged
+    ranking is the oracle's (np=1) byte for byte.  The cuts fall inside quoted
+    lyrics."""
+    data = msa_mod.gen_corpus(60_000, mode="highcard", seed=23)
+    cuts = cuts_for(data, world, "in_quotes")
+    stat = str(tmp_path / "dense")
+    w, a, m = run_world(tmp_path, data, cuts, env_extra={"MSA_DENSE_MIN": "0", "MSA_STAT_OUT": stat})
+    exp = expected(tmp_path, data)
+    assert m["total_songs"] == exp["metrics"]["total_songs"]
+    assert m["total_words"] == exp["metrics"]["total_words"]
+    assert w == exp["word_counts.csv"]
+    assert a == exp["top_artists.csv"]
+    assert [open(f"{stat}.{r}").read() for r in range(world)] == ["1"] * world

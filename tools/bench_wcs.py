@@ -95,8 +95,20 @@ def main():
 
 
 def bench_split(a):
+    """The column splitter (msa_csvcol_run).  roofline: its copy kernel
+    k_csvcol<1> (thread per row: the row's bytes read once, every cell's
+    quoted line written through an 8-byte write combiner), HIP events on the
+    library's stream (msa_csvcol_kernel); algorithmic bytes per launch = every
+    input byte read once + the column bytes written + 9 B per cell (its output
+    offset and quoted flag); `traffic` from the PMC file of tools/pmc_rowf.sh
+    (profiles/pmc_split_main.json) when it is stamped with this build."""
+    import ctypes as C
+
     data = msa.gen_corpus(a.songs, mode="zipf", seed=1)
     n = len(data)
+    lib = msa.load()
+    lib.msa_csvcol_kernel.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]
+    kms, outb = [], 0
     with msa.WordCountPerSong(0) as w:
         w.load_csv(data)
         for _ in range(a.warmup):
@@ -104,11 +116,32 @@ def bench_split(a):
         t0 = time.perf_counter()
         for _ in range(a.steps):
             nc, nr = w.split_columns(True)
+            ms, ob = C.c_double(), C.c_uint64()
+            lib.msa_csvcol_kernel(w.h, C.byref(ms), C.byref(ob))
+            kms.append(ms.value)
+            outb = ob.value
         dt = (time.perf_counter() - t0) / a.steps
+    k_ms = sum(kms) / len(kms)
+    alg = n + outb + 9 * nc * nr
+    achieved = alg / (k_ms * 1e-3) / 1e9
+    roof = {"kernel": "k_csvcol<1>", "bound": "hbm", "achieved": round(achieved, 1), "peak": 8000.0, "unit": "GB/s",
+            "frac": round(achieved / 8000.0, 4), "traffic": None, "avg_launch_ms": round(k_ms, 4),
+            "alg_bytes_per_launch": alg}
+    pmc = os.path.join(REPO, "profiles", "pmc_split_main.json")
+    if os.path.exists(pmc):
+        p = json.load(open(pmc))
+        k = p.get("kernels", {}).get("k_csvcol<1>")
+        if p.get("build_id") == msa.build_id() and p.get("input_bytes") == n and k:
+            roof["traffic"] = k["hbm_bytes_per_launch"]
+            roof["traffic_over_alg"] = round(k["hbm_bytes_per_launch"] / alg, 3)
+        else:
+            roof["counters"] = {"note": "PMC file not taken on this build / corpus"}
     out = {"metric": "CSV->per-column files GB/s (split_csv_columns.py path)", "value": round(n / dt / 1e9, 3),
            "unit": "GB/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(dt * 1e3, 3),
            "higher_is_better": True, "dtype": "u8", "data": "synthetic (csrc/msa_gen.c Zipfian lyric CSV, seed 1)",
-           "config": {"workload": f"{a.songs} songs, {n} bytes, resident in HBM", "columns": nc, "rows": nr}}
+           "config": {"workload": f"{a.songs} songs, {n} bytes, resident in HBM", "bytes_per_gpu": n, "columns": nc,
+                      "rows": nr, "column_bytes": outb},
+           "roofline": roof}
     if not a.no_cpu_baseline:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import split_oracle  # checker restatement, timed as the CPU baseline only

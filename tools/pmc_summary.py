@@ -26,7 +26,9 @@ sys.path.insert(0, os.path.join(REPO, "music-analyst-ai_amd"))
 KERNELS = ["k_scan_csv", "k_scan_struct", "k_scan_tokens", "k_miss_agg", "k_chunk_summary", "k_rec_spans", "k_rec_fast", "k_rec_fix", "k_col_gather", "k_col_lines",
            "k_artist_count", "k_tile_sort", "k_merge_pass",
            # the per-song counter (tools/pmc_wcs.sh, --wcs)
-           "k_wcs_wrows", "k_wcs_rows", "k_wcs_map", "k_wcs_emit", "k_wcs_validate", "k_wcs_pairs"]
+           "k_wcs_wrows", "k_wcs_rows", "k_wcs_map", "k_wcs_emit", "k_wcs_validate", "k_wcs_pairs",
+           # the column splitter (tools/pmc_split.sh, --split): its two passes apart
+           "k_csvcol<0>", "k_csvcol<1>"]
 PASSES = ["fetch", "write", "sq", "atomic", "sq2"]
 
 
@@ -38,6 +40,8 @@ def build_id():
 
 def short(name):
     name = name.replace("(anonymous namespace)::", "")
+    if name.startswith("void "):
+        name = name[5:]
     for k in KERNELS:
         if name.startswith(k + "(") or name.startswith(k + "<") or name == k:
             return k
@@ -72,6 +76,7 @@ def bench_line(log):
 def main():
     args = [x for x in sys.argv[1:] if not x.startswith("--")]
     wcs = "--wcs" in sys.argv  # passes over tools/bench_wcs.py: the roofline kernel is k_wcs_wrows
+    split = "--split" in sys.argv  # passes over tools/bench_wcs.py --path split: k_csvcol<1>
     out = args[0] if args else "gpurun_out/pmc"
     per = collect(out)
     kernels = {}
@@ -84,7 +89,8 @@ def main():
         kernels[k] = e
     b = bench_line(os.path.join(out, "fetch.log"))
     # the bench line names the roofline kernel ("k_scan_tokens (csv_tokens)", ...)
-    rk = "k_wcs_wrows" if wcs else ((b or {}).get("roofline", {}).get("kernel", "k_scan_csv").split(" ")[0])
+    rk = "k_wcs_wrows" if wcs else ("k_csvcol<1>" if split else
+                                    ((b or {}).get("roofline", {}).get("kernel", "k_scan_csv").split(" ")[0]))
     res = {
         "build_id": build_id(),
         "input_bytes": b["config"]["bytes_per_gpu"] if b else None,
@@ -93,6 +99,8 @@ def main():
         "correction": "hbm = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE halves 16B/lane streams)",
         "command": ("tools/pmc_wcs.sh: rocprofv3 --pmc <group> -- python3 tools/bench_wcs.py --steps 1 --warmup 1 "
                     "--no-cpu-baseline" if wcs else
+                    "tools/pmc_split.sh: rocprofv3 --pmc <group> -- python3 tools/bench_wcs.py --path split --steps 1 "
+                    "--warmup 1 --no-cpu-baseline" if split else
                     "tools/pmc.sh: rocprofv3 --pmc <group> -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline"),
         "kernels": kernels,
     }
