@@ -98,6 +98,10 @@ hipError_t msa_launch_blob(const u32 *, u64, const u64 *, const u64 *, const u64
                            const u8 *, const u64 *, const u32 *, const u8 *, const u64 *, const u32 *, u64 *, u64 *, u64 *, u64 *,
                            u8 *, u64 *, u64, hipStream_t, int, const u64 *, const u64 *, const u64 *, u64);
 
+#ifndef MSA_LISTS_BEFORE_SPANS
+#define MSA_LISTS_BEFORE_SPANS 1  // 0: the library stream waits for the spans before the word lists (A/B builds)
+#endif
+
 // ---------------------------------------------------------------------------
 namespace {
 
@@ -1283,7 +1287,9 @@ static int split_once(msa_ctx *c, int flags) {
     if ((rc = launch_spans(c, want_text, sst))) return rc;
     if (spans_beside) {
         HIPC(c, hipEventRecord(c->ev_spans, c->rank2));
+#if !MSA_LISTS_BEFORE_SPANS
         HIPC(c, hipStreamWaitEvent(c->stream, c->ev_spans, 0));
+#endif
     }
     if (want_text) {  // text.csv's body: deferred (msa_ctx::text_deferred)
         HIPC(c, ensure(c->tcol, kColHdrRoom + c->n + 1 + MSA_INPUT_PAD));
@@ -1297,6 +1303,12 @@ static int split_once(msa_ctx *c, int flags) {
     // atomics; the read-back below waits for both
     // (measured neutral on rank2 beside the artist pass, profiles/r04_t41_*)
     if (!c->dense_w && (rc = build_word_lists(c))) return rc;  // (dense: the aggregation counted the entries)
+#if MSA_LISTS_BEFORE_SPANS
+    // the slot lists need the tables only, not the spans: they run behind
+    // k_miss_agg while the spans (rank2, slowed by the token pass beside them)
+    // finish; everything below waits for the spans
+    if (spans_beside) HIPC(c, hipStreamWaitEvent(c->stream, c->ev_spans, 0));
+#endif
     // the artist pass of msa_count (lines shortcut) right here, before the
     // read-back: it needs only the split's keys, and its counters come back
     // with the split's -- the text column's gather (launched by msa_count)
@@ -1716,7 +1728,8 @@ static int refine_ties(msa_ctx *c, Ranked &R, int cur, const u8 *wbuf, const u8 
         Pc = rb.t_Pc.as<u64>();
         mc = m;
     }
-    return fail(c, MSA_ERR_COLLISION, "tie refinement did not converge (equal keys in one table)");
+    return fail(c, MSA_ERR_COLLISION, "tie refinement did not converge (equal keys in the %s table: %llu of %llu entries tied)",
+                &R == &c->rw ? "word" : "artist", (unsigned long long)mc, (unsigned long long)n);
 }
 
 static bool small_sort(const msa_ctx *c, u64 n) { return c->sort_mode == 1 || (c->sort_mode == 0 && n < kRadixMin); }
@@ -2100,8 +2113,13 @@ int msa_create(int device, msa_ctx **out) {
     int least = 0, greatest = 0;
     (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
     const hipError_t side_e = hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, greatest);
+#ifndef MSA_R2_PRIO
+#define MSA_R2_PRIO 0  // 1: rank2 (the spans beside the token pass, the artists' ranking) at the highest priority
+#endif
+    const hipError_t r2_e = MSA_R2_PRIO ? hipStreamCreateWithPriority(&c->rank2, hipStreamNonBlocking, greatest)
+                                        : hipStreamCreateWithFlags(&c->rank2, hipStreamNonBlocking);
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess || side_e != hipSuccess ||
-        hipStreamCreateWithFlags(&c->rank2, hipStreamNonBlocking) != hipSuccess ||
+        r2_e != hipSuccess ||
         hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_aux_fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_aux_join, hipEventDisableTiming) != hipSuccess ||

@@ -78,13 +78,39 @@ static int rc_allgather(msa_tr *t, const void *in, size_t bytes, void *out) {
     return 0;
 }
 
+/* A rank's block for itself is a device copy on the exchange stream, not an
+ * RCCL message to itself (a world of one sent a 1.8 GB self-message through
+ * ncclSend / ncclRecv and received corrupt bytes: the configs[4] merge failed);
+ * messages to other ranks go in pieces of at most RC_PIECE bytes, the sender
+ * and the receiver cutting the same byte count the same way. */
+#define RC_PIECE ((uint64_t)256 << 20)
 static int rc_alltoallv(msa_tr *t, const void *send, const uint64_t *sc, void *recv, const uint64_t *rc) {
     RcclImpl *im = (RcclImpl *)t->impl;
-    uint64_t so = 0, ro = 0;
+    uint64_t so = 0, ro = 0, sself = 0, rself = 0;
+    for (int p = 0; p < t->rank; ++p) {
+        sself += sc[p];
+        rself += rc[p];
+    }
+    if (sc[t->rank] != rc[t->rank]) {
+        fprintf(stderr, "rank %d: all-to-all: %llu bytes sent to itself, %llu expected\n", t->rank,
+                (unsigned long long)sc[t->rank], (unsigned long long)rc[t->rank]);
+        return -1;
+    }
+    if (sc[t->rank])
+        HIP_OK(hipMemcpyAsync((char *)recv + rself, (const char *)send + sself, sc[t->rank], hipMemcpyDeviceToDevice,
+                              im->stream), "self copy");
     NCCL_OK(ncclGroupStart(), "ncclGroupStart");
     for (int p = 0; p < t->world; ++p) {
-        if (sc[p]) NCCL_OK(ncclSend((const char *)send + so, sc[p], ncclUint8, p, im->comm, im->stream), "ncclSend");
-        if (rc[p]) NCCL_OK(ncclRecv((char *)recv + ro, rc[p], ncclUint8, p, im->comm, im->stream), "ncclRecv");
+        if (p != t->rank) {
+            for (uint64_t k = 0; k < sc[p]; k += RC_PIECE) {
+                const uint64_t n = sc[p] - k < RC_PIECE ? sc[p] - k : RC_PIECE;
+                NCCL_OK(ncclSend((const char *)send + so + k, n, ncclUint8, p, im->comm, im->stream), "ncclSend");
+            }
+            for (uint64_t k = 0; k < rc[p]; k += RC_PIECE) {
+                const uint64_t n = rc[p] - k < RC_PIECE ? rc[p] - k : RC_PIECE;
+                NCCL_OK(ncclRecv((char *)recv + ro + k, n, ncclUint8, p, im->comm, im->stream), "ncclRecv");
+            }
+        }
         so += sc[p];
         ro += rc[p];
     }

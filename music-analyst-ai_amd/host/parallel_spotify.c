@@ -54,6 +54,8 @@ typedef struct {
      * the whole pipeline -- boundary exchange, split, count, merge, rank, full
      * ranked gather -- after bench_warmup untimed ones; no files are written */
     uint64_t synth_songs;
+    uint64_t synth_seed;  /* --synthetic-seed (default 1) */
+    int synth_mode;       /* --synthetic-mode zipf|highcard (configs[2]/[3] or configs[4]) */
     int bench_steps, bench_warmup;
 } Opts;
 
@@ -439,7 +441,7 @@ static int rank_main(int rank, int world, msa_shared *sh, void *arg) {
     size_t len = 0;
     char *part = NULL;
     if (o->synth_songs) {  /* bench mode: this rank's songs of the synthetic corpus */
-        const msa_gen_params gp = {1, o->synth_songs, 50000, 5000, 30, MSA_GEN_ZIPF, 0};
+        const msa_gen_params gp = {o->synth_seed, o->synth_songs, 50000, 5000, 30, o->synth_mode, 0};
         const uint64_t s0 = o->synth_songs * (uint64_t)rank / (uint64_t)world;
         const uint64_t s1 = o->synth_songs * (uint64_t)(rank + 1) / (uint64_t)world;
         if (msa_gen_corpus_range(&gp, s0, s1 - s0, &part, &len)) {
@@ -560,6 +562,8 @@ int main(int argc, char **argv) {
     memset(&o, 0, sizeof o);
     o.dataset = argv[1];
     o.processes = 1;
+    o.synth_seed = 1;
+    o.synth_mode = MSA_GEN_ZIPF;
     snprintf(o.outdir, sizeof o.outdir, "output");
     for (int i = 2; i < argc; ++i) {
         if (!strcmp(argv[i], "--word-limit") && i + 1 < argc) o.word_limit = atoi(argv[++i]);
@@ -571,6 +575,9 @@ int main(int argc, char **argv) {
         else if ((!strcmp(argv[i], "--processes") || !strcmp(argv[i], "-np")) && i + 1 < argc)
             o.processes = atoi(argv[++i]);
         else if (!strcmp(argv[i], "--synthetic-songs") && i + 1 < argc) o.synth_songs = strtoull(argv[++i], NULL, 10);
+        else if (!strcmp(argv[i], "--synthetic-seed") && i + 1 < argc) o.synth_seed = strtoull(argv[++i], NULL, 10);
+        else if (!strcmp(argv[i], "--synthetic-mode") && i + 1 < argc)
+            o.synth_mode = !strcmp(argv[++i], "highcard") ? MSA_GEN_HIGHCARD : MSA_GEN_ZIPF;
         else if (!strcmp(argv[i], "--bench-steps") && i + 1 < argc) o.bench_steps = atoi(argv[++i]);
         else if (!strcmp(argv[i], "--bench-warmup") && i + 1 < argc) o.bench_warmup = atoi(argv[++i]);
         else if (!quiet) fprintf(stderr, "Ignoring unknown argument: %s\n", argv[i]);

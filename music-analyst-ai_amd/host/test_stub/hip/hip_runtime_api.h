@@ -12,7 +12,7 @@ typedef int hipError_t;
 #define hipErrorInvalidDevice 101
 typedef struct stub_stream *hipStream_t;
 #define hipStreamNonBlocking 1u
-typedef enum { hipMemcpyHostToDevice = 1, hipMemcpyDeviceToHost = 2 } hipMemcpyKind;
+typedef enum { hipMemcpyHostToDevice = 1, hipMemcpyDeviceToHost = 2, hipMemcpyDeviceToDevice = 3 } hipMemcpyKind;
 
 hipError_t hipSetDevice(int device);
 hipError_t hipStreamCreateWithFlags(hipStream_t *s, unsigned flags);

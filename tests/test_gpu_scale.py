@@ -193,6 +193,28 @@ def test_configs4_cli(configs4, tmp_path):
     assert (m["total_songs"], m["total_words"]) == (e["total_songs"], e["total_words"])
 
 
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("transport,procs", [("rccl", 1), ("shm", 2)])
+def test_configs4_cli_ranks(configs4, tmp_path, transport, procs):
+    """configs[4] through the rank layer: a world of one over the RCCL
+    transport (MSA_RANK_PATH=1) -- its ~1.8 GB key-partition block for itself
+    is a device copy, not an RCCL message (sent through ncclSend / ncclRecv to
+    itself it had arrived corrupt) -- and two ranks sharing the GPU (shm): the
+    merged word and artist rankings equal the oracle's."""
+    _, path, od = configs4
+    out = tmp_path / "out"
+    env = dict(os.environ, MSA_TRANSPORT=transport)
+    cmd = [CLI, path, "--output-dir", str(out)]
+    if procs > 1:
+        cmd += ["--processes", str(procs)]
+    else:
+        env["MSA_RANK_PATH"] = "1"
+    p = run_with_heartbeat(cmd, 600, f"parallel_spotify configs[4] {transport} x{procs}", env=env)
+    assert p.returncode == 0, p.stderr
+    for f in ("word_counts.csv", "top_artists.csv"):
+        assert files_equal(str(out / f), os.path.join(od, f)), f
+
+
 @pytest.mark.parametrize("sort", ["radix", "merge"])
 def test_sort_designs_agree(msa_mod, tmp_path, sort, monkeypatch):
     """Both ranking sorts, forced on every table size (MSA_SORT): the radix
