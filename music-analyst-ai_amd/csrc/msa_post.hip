@@ -758,7 +758,10 @@ __global__ __launch_bounds__(256) void k_rec_spans(const u8 *__restrict__ buf, c
 // field as is); the artist span comes from the record's first window.  Every
 // other record (unquoted or space-padded lyrics, a NUL, the unterminated last
 // record) is listed for k_rec_fix, the exact path.
-__global__ __launch_bounds__(256) void k_rec_fast(const u8 *__restrict__ buf, const u64 *__restrict__ rec_start,
+#ifndef RF_MINW
+#define RF_MINW 1  // waves per SIMD k_rec_fast is compiled for (8: <= 64 VGPRs, 4 beside the token pass's 4)
+#endif
+__global__ __launch_bounds__(256, RF_MINW) void k_rec_fast(const u8 *__restrict__ buf, const u64 *__restrict__ rec_start,
                                                   const u64 *__restrict__ f0p, const u64 *__restrict__ tss,
                                                   const u64 *__restrict__ tse, u64 nrec, u64 first_rec,
                                                   int want_text, SpanOut o, Counters *ctr, AKeys ak,
