@@ -113,3 +113,34 @@ __device__ __forceinline__ ChunkSum k1_finish(const K1Acc &s) {
     }
     return r;
 }
+
+// The 4 KiB block through LDS: loaded coalesced (instruction q: 1 KiB, lane l
+// the 16 bytes at 1024 q + 16 l -- 16 lines of 64 B per instruction instead of
+// 64 when every lane reads its own 64 contiguous bytes; those loads kept the
+// texture data path ~82 % busy, profiles/r06_pmc_tok_explore.txt), written to
+// the wave's LDS image and read back as lane l = bytes [64 l, 64 l + 64).
+// 16-byte chunk c sits at c ^ ((c >> 4) & 3): the reads' 16-lane groups then
+// hit 16 different slots of the 256-byte bank row (4-way conflicts without),
+// and the writes' 8-lane groups stay on 8 different slots.
+__device__ __forceinline__ u32 blk_swz(u32 c) { return c ^ ((c >> 4) & 3u); }
+// (four named registers, not an array: an array the two prefetch sites
+// assign was kept in scratch memory)
+struct Blk4 {
+    uint4 a, b, c, d;
+};
+__device__ __forceinline__ Blk4 blk_load_co(const u8 *p) {
+    const u32 lane = lane_id();
+    const uint4 *q = reinterpret_cast<const uint4 *>(p + 16 * lane);
+    return Blk4{q[0], q[64], q[128], q[192]};
+}
+__device__ __forceinline__ void blk_transpose(uint4 *st, const Blk4 &r, uint4 (&o)[4]) {
+    const u32 lane = lane_id();
+    st[blk_swz(lane)] = r.a;
+    st[blk_swz(64 + lane)] = r.b;
+    st[blk_swz(128 + lane)] = r.c;
+    st[blk_swz(192 + lane)] = r.d;
+    o[0] = st[blk_swz(4 * lane)];
+    o[1] = st[blk_swz(4 * lane + 1)];
+    o[2] = st[blk_swz(4 * lane + 2)];
+    o[3] = st[blk_swz(4 * lane + 3)];
+}

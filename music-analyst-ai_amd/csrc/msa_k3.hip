@@ -34,12 +34,19 @@ namespace {
 #endif
 #define Q_W (Q_T / 64)
 #define Q_BLK 4096               // bytes per wave-iteration
+#ifndef Q_TDL
+#define Q_TDL 0                  // 1: fewer bytes through the texture data path (see k_scan_tokens)
+#endif
+#ifndef Q_KAL
+#define Q_KAL 0                  // 1: keys re-read as two 16-byte-aligned dwordx4 loads (a 32-byte window) + selects
+#endif
 #ifndef Q_PROBE1
 #define Q_PROBE1 0               // 1: a bucket's second half read only by lanes its first half left open
 #endif
 #ifndef TOK_PF
 #define TOK_PF 1                 // batches of key loads in flight ahead of the probed one
 #endif
+static_assert(!(Q_KAL && TOK_PF > 1), "Q_KAL keeps one batch of key loads in flight");
 // Token keys are re-read from the input (just loaded: L1/L2) rather than
 // from an LDS copy of the block, which leaves the LDS to the word table and
 // to a per-wave list of the block's token starts: the lanes share the tokens
@@ -541,15 +548,46 @@ __device__ __forceinline__ void tok_phase(const ScanArgs &a, u64 ib, u64 lpos, u
     // key loads of batch j (a stale list entry past the list's end addresses
     // a byte inside the block: harmless, and the loop's vector memory sequence
     // stays the same every trip)
+#if Q_KAL
+    // the 32 bytes from the 16-byte boundary at or before the token: two
+    // aligned dwordx4 loads (k4 unused; kv2 = the second half)
+    uint4 kv2, kv2n;
+    auto kload = [&](u32 j, u32 &e, uint4 &v, u32 &v4) {
+        e = list[min(j * 64 + lane, (u32)Q_LIST - 1u)];
+        const size_t pa = (size_t)(a.buf + ib + (e & 4095u)) & ~(size_t)15;
+        const uint4 *gp = reinterpret_cast<const uint4 *>(pa);
+        v = gp[0];
+        kv2n = gp[1];
+        v4 = 0;
+    };
+#elif Q_TDL
+    // 12 bytes from the token's dword (a 3..8-byte word and its offset in
+    // the dword fit), the next 8 only for 9..16-byte words: fewer bytes
+    // returned through the texture data path, which the key gathers kept
+    // ~84 % busy (TD_TD_BUSY, profiles/r06_pmc_tok_explore.txt)
+    auto kload = [&](u32 j, u32 &e, uint4 &v, u32 &v4) {
+        e = list[min(j * 64 + lane, (u32)Q_LIST - 1u)];
+        const u32 *gp = reinterpret_cast<const u32 *>(a.buf + ((ib + (e & 4095u)) & ~3ull));
+        const uint3 w3 = *reinterpret_cast<const uint3 *>(gp);
+        uint2 w2 = make_uint2(0, 0);
+        if ((e >> 12) >= 6) w2 = *reinterpret_cast<const uint2 *>(gp + 3);  // length >= 9
+        v = make_uint4(w3.x, w3.y, w3.z, w2.x);
+        v4 = w2.y;
+    };
+#else
     auto kload = [&](u32 j, u32 &e, uint4 &v, u32 &v4) {
         e = list[min(j * 64 + lane, (u32)Q_LIST - 1u)];
         const u32 *gp = reinterpret_cast<const u32 *>(a.buf + ((ib + (e & 4095u)) & ~3ull));
         v = *reinterpret_cast<const uint4 *>(gp);
         v4 = gp[4];
     };
+#endif
     u32 en, k4;
     uint4 kv;
     kload(0, en, kv, k4);
+#if Q_KAL
+    kv2 = kv2n;
+#endif
 #if TOK_PF > 1
     u32 en2, k42;  // batch bt + 2's, TOK_PF = 2: two batches of key loads in flight
     uint4 kv2;
@@ -561,6 +599,9 @@ __device__ __forceinline__ void tok_phase(const ScanArgs &a, u64 ib, u64 lpos, u
         const u32 e = en;
         const uint4 v = kv;
         const u32 v4 = k4;
+#if Q_KAL
+        const uint4 vb = kv2;
+#endif
         const bool have = bt * 64 + lane < nS;
 #if TOK_PF > 1
         en = en2;
@@ -569,12 +610,26 @@ __device__ __forceinline__ void tok_phase(const ScanArgs &a, u64 ib, u64 lpos, u
         kload(bt + 2, en2, kv2, k42);
 #else
         kload(bt + 1, en, kv, k4);
+#if Q_KAL
+        kv2 = kv2n;
+#endif
 #endif
         if (have) {
             const u32 len = (e >> 12) + 3;
+#if Q_KAL
+            const u32 s16 = (u32)(size_t)(a.buf + ib + (e & 4095u)) & 15u, sh = s16 & 3u;
+            const bool h2 = (s16 & 8u) != 0, h1 = (s16 & 4u) != 0;
+            const u32 t0 = h2 ? v.z : v.x, t1 = h2 ? v.w : v.y, t2 = h2 ? vb.x : v.z, t3 = h2 ? vb.y : v.w,
+                      t4 = h2 ? vb.z : vb.x, t5 = h2 ? vb.w : vb.y;
+            const u32 d0 = h1 ? t1 : t0, d1 = h1 ? t2 : t1, d2 = h1 ? t3 : t2, d3 = h1 ? t4 : t3, d4 = h1 ? t5 : t4;
+            (void)v4;
+            u64 x0 = mk64(__builtin_amdgcn_alignbyte(d1, d0, sh), __builtin_amdgcn_alignbyte(d2, d1, sh));
+            u64 x1 = mk64(__builtin_amdgcn_alignbyte(d3, d2, sh), __builtin_amdgcn_alignbyte(d4, d3, sh));
+#else
             const u32 sh = (u32)(ib + (e & 4095u)) & 3u;
             u64 x0 = mk64(__builtin_amdgcn_alignbyte(v.y, v.x, sh), __builtin_amdgcn_alignbyte(v.z, v.y, sh));
             u64 x1 = mk64(__builtin_amdgcn_alignbyte(v.w, v.z, sh), __builtin_amdgcn_alignbyte(v4, v.w, sh));
+#endif
             if (K3_ABLATE && (a.ablate & 128)) {  // diagnostic: keys made up from the list entry (no re-read)
                 x0 = (u64)e * 0x9E3779B97F4A7C15ull & 0x7F7F7F7F7F7F7F7Full;
                 x1 = x0 >> 3;
@@ -675,6 +730,12 @@ __device__ __forceinline__ void tok_epilogue(const ScanArgs &a, u64 *skeys, u32 
 #ifndef SA_PF
 #define SA_PF 1
 #endif
+#ifndef SA_TAIL1
+#define SA_TAIL1 0
+#endif
+#ifndef SA_LDS
+#define SA_LDS 0  // 1: blocks loaded coalesced and transposed through the wave's LDS image (msa_k1.h blk_*)
+#endif
 __global__ __launch_bounds__(SA_T, SA_MINW) void k_scan_struct(ScanArgs a) {
     const u32 lane = lane_id();
     const u32 wib = threadIdx.x >> 6;
@@ -697,10 +758,40 @@ __global__ __launch_bounds__(SA_T, SA_MINW) void k_scan_struct(ScanArgs a) {
         // drops the low address bits -- a.buf is a view at any alignment)
         u64 ta = ib + Q_BLK < a.seg_end ? ib + Q_BLK : ib;
         pin64(ta);
+#if SA_TAIL1
+        // only lane 63 reads the bytes after the block (struct_block): one
+        // active lane, not 64 copies of the same 16 bytes through the texture
+        // data path (a fifth of the block's own bytes)
+        t = make_uint4(0, 0, 0, 0);
+        if (lane == 63) t = ldg16(a.buf + ta);
+#else
         t = ldg16(a.buf + ta);
+#endif
     };
+#if SA_LDS
+    static_assert(SA_PF == 1, "SA_LDS prefetches one block");
+    __shared__ uint4 sast[SA_T / 64][256];
+    uint4 *bst = sast[threadIdx.x >> 6];
+    auto load_raw = [&](u32 s, Blk4 &r, uint4 &t) {
+        u64 ib;
+        if (!blk_at(s, ib)) ib = a.seg_begin + (u64)gw * MSA_CHUNK;
+        r = blk_load_co(a.buf + ib);
+        u64 ta = ib + Q_BLK < a.seg_end ? ib + Q_BLK : ib;
+        pin64(ta);
+#if SA_TAIL1
+        t = make_uint4(0, 0, 0, 0);
+        if (lane == 63) t = ldg16(a.buf + ta);
+#else
+        t = ldg16(a.buf + ta);
+#endif
+    };
+    Blk4 raw;
+    uint4 tl;
+    load_raw(0, raw, tl);
+#else
     uint4 cur[4], tl;
     load_blk(0, cur, tl);
+#endif
 #if SA_PF > 1
     uint4 nx[4], ntl;
     load_blk(1, nx, ntl);
@@ -727,9 +818,17 @@ __global__ __launch_bounds__(SA_T, SA_MINW) void k_scan_struct(ScanArgs a) {
         const u64 cend = min(a.seg_begin + (u64)c * MSA_CHUNK + (u64)MSA_CHUNK, a.seg_end);
         const u64 lpos = ib + lane * 64;
         const u64 rem = valid && cend > lpos ? cend - lpos : 0;
+#if SA_LDS
+        uint4 cur[4];
+        blk_transpose(bst, raw, cur);
+        load_raw(s + 1, raw, tl);
         const Masks k = classify64x(cur, (u32)min(rem, (u64)64), rare_chunk);
+#else
+        const Masks k = classify64x(cur, (u32)min(rem, (u64)64), rare_chunk);
+#endif
         // the block's bytes now live in the masks: rotate the prefetch
-#if SA_PF > 1
+#if SA_LDS
+#elif SA_PF > 1
 #pragma unroll
         for (int q = 0; q < 4; ++q) cur[q] = nx[q];
         tl = ntl;
@@ -1108,6 +1207,21 @@ __global__ __launch_bounds__(Q_T, Q_WGCU) void k_scan_tokens(ScanArgs a) {
     const u64 lch = min<u64>(1024, max<u64>(8, min(a.l_expect ? a.l_expect : a.l_cap, a.l_cap) / ((u64)nw * 4)));
     // mask words of the block: this lane's, the one after it and the one before
     u64 Lc = 0, Ln = 0, Lp = 0;
+#if Q_TDL
+    // the neighbours' mask words by DPP from the lane's own (only the block's
+    // two edge words loaded, by one lane each); the lines warmed by one dword
+    // a lane, not 16 bytes
+    u32 warm = 0;
+    u64 Le = 0;  // lane 0: the word before the block; lane 63: the word after it
+    auto fetch = [&](u64 blk) {
+        u64 wi = blk * 64 + lane;
+        pin64(wi);
+        Lc = a.lmask[1 + wi];
+        if (lane == 0) Le = a.lmask[wi];  // lmask[0] is the zero pad
+        else if (lane == 63) Le = wi + 1 < nwords ? a.lmask[2 + wi] : 0ull;
+        warm = *reinterpret_cast<const u32 *>(a.buf + ((a.seg_begin + blk * Q_BLK + lane * 64) & ~3ull));
+    };
+#else
     uint4 warm = make_uint4(0, 0, 0, 0);
     auto fetch = [&](u64 blk) {
         u64 wi = blk * 64 + lane;
@@ -1117,10 +1231,18 @@ __global__ __launch_bounds__(Q_T, Q_WGCU) void k_scan_tokens(ScanArgs a) {
         Lp = a.lmask[wi];  // lmask[0] is the zero pad
         warm = ldg16(a.buf + a.seg_begin + blk * Q_BLK + lane * 64);
     };
+#endif
     if (gw < nblk) fetch(gw);
     for (u64 blk = gw; blk < nblk; blk += nw) {
+#if Q_TDL
+        const u64 L = Lc, Le_ = Le;
+        const u64 dn = from_next(L), dp = from_prev(L);
+        const u64 Lnext = lane == 63 ? Le_ : dn, Lprev = lane == 0 ? Le_ : dp;
+        asm volatile("" ::"v"(warm));  // the block's lines are in cache
+#else
         const u64 L = Lc, Lnext = Ln, Lprev = Lp;
         asm volatile("" ::"v"(warm.x));  // the block's lines are in cache
+#endif
         if (blk + nw < nblk) fetch(blk + nw);
         const u64 ib = a.seg_begin + blk * Q_BLK;
         const u64 lpos = ib + lane * 64;

@@ -112,6 +112,9 @@ __device__ __forceinline__ Classes64 classify64(const uint4 (&v)[4], u64 lpos, u
     k.Q &= vm; k.C &= vm; k.NL &= vm; k.CR &= vm; k.Z &= vm;
     return k;
 }
+#ifndef K1_LDS
+#define K1_LDS 0  // 1: blocks loaded coalesced (lane l: bytes 1024 q + 16 l) and transposed through LDS
+#endif
 #ifndef K1_MINW
 #define K1_MINW 5  // min waves per SIMD: 96 VGPRs, 5 waves (4 at 111 VGPRs: 0.362 -> 0.338 ms; 6 and 8 spill: 0.43, 0.89)
 #endif
@@ -126,6 +129,44 @@ __global__ __launch_bounds__(256, K1_MINW) void k_chunk_summary(const u8 *__rest
     // vector loads complete in order, so a byte load issued after the next
     // block's prefetch made every iteration wait for that prefetch
     auto nbyte = [&](u64 pos) -> u32 { return pos < seg_end ? (u32)buf[pos] : 0u; };
+#if K1_LDS
+    __shared__ uint4 k1st[256 / 64][256];
+    uint4 *st = k1st[threadIdx.x >> 6];
+    Blk4 raw{};  // the next block as loaded (coalesced), in flight during the current one
+    u32 nb_cur = 0;
+    if (gw < nchunks) {
+        const u64 b0 = seg_begin + (u64)gw * MSA_CHUNK;
+        nb_cur = nbyte(b0 + K1_ITER);
+        raw = blk_load_co(buf + b0);
+    }
+    for (u32 c = gw; c < nchunks; c += nw) {
+        const u64 cbase = seg_begin + (u64)c * MSA_CHUNK;
+        const u64 cend = min(cbase + (u64)MSA_CHUNK, seg_end);
+        K1Acc acc;
+        k1_init(acc);
+        for (u64 ibase = cbase; ibase < cend; ibase += K1_ITER) {
+            const u64 lpos = ibase + lane * 64;
+            uint4 cur[4];
+            blk_transpose(st, raw, cur);
+            u32 nb_next = 0;
+            if (ibase + K1_ITER < cend) {
+                nb_next = nbyte(ibase + 2 * K1_ITER);
+                raw = blk_load_co(buf + ibase + K1_ITER);
+            } else if (c + nw < nchunks) {
+                const u64 b1 = seg_begin + (u64)(c + nw) * MSA_CHUNK;
+                nb_next = nbyte(b1 + K1_ITER);
+                raw = blk_load_co(buf + b1);
+            }
+            const Classes64 k = classify64(cur, lpos, cend);
+            const u32 nb_nl = nb_cur == '\n' ? 1u : 0u;
+            const u32 lastb = (u32)(min(ibase + (u64)K1_ITER, cend) - 1 - ibase);
+            k1_block(acc, k.Q, k.C, k.NL, k.CR, k.Z, k.rare, nb_nl, (u32)(ibase - cbase), lastb);
+            nb_cur = nb_next;
+        }
+        const ChunkSum sum = k1_finish(acc);
+        if (lane == 0) out[c] = sum;
+    }
+#else
     uint4 cur[4];  // a chunk's first block: loaded during the previous chunk's last one
     u32 nb_cur = 0;
     if (gw < nchunks) {
@@ -166,6 +207,7 @@ __global__ __launch_bounds__(256, K1_MINW) void k_chunk_summary(const u8 *__rest
         const ChunkSum sum = k1_finish(acc);
         if (lane == 0) out[c] = sum;
     }
+#endif
 }
 
 // ---------------------------------------------------------------------------
