@@ -173,6 +173,14 @@ def test_configs4_run(msa_mod, configs4, tmp_path):
         c.run(text_column=True)
         s = check_files_against_oracle(msa_mod, c, od, tmp_path)
         assert s.n_words >= 50_000_000 and s.n_artists > 1_000_000
+        # the cold run (a one-shot CLI run): the first split of a large input
+        # takes the dense entries, so no table grows round by round (round 5:
+        # three split attempts, 6.6 s)
+        import ctypes
+        c.lib.msa_debug_stat.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint64)]
+        v = ctypes.c_uint64(0)
+        assert c.lib.msa_debug_stat(c.h, b"split_attempts", ctypes.byref(v)) == 0
+        assert v.value <= 2, f"{v.value} split attempts on a cold configs[4] run"
 
 
 @pytest.mark.timeout(900)
