@@ -232,6 +232,38 @@ __device__ __forceinline__ u64 pxor_ex64(u64 q) {  // bit j = parity of bits < j
 // 128-bit (hi:lo) >> k, low 64 bits, 0 < k < 64
 __device__ __forceinline__ u64 shr128(u64 lo, u64 hi, u32 k) { return (lo >> k) | (hi << (64 - k)); }
 
+// 9..10-byte words in the LDS table (Q_PK10): a lower-cased token byte has
+// one of 37 values, coded in 6 bits, nonzero -- 'a'..'z' 33..58, '0'..'9'
+// 16..25, '\'' 7: (c & 0x1F) | ((c >> 1) & 0x20) -- so ten of them pack into
+// 60 bits (zero codes past the word's end); bit 63 tags the packed key, which
+// an S key (bytes < 0x80) never has.  The 9..10-byte words (~2/3 of the
+// 9..16-byte tokens of lyric text) are then counted in LDS instead of logged.
+// Measured and not kept (profiles/r06_ab_pk10.txt): WRITE_SIZE -15 %,
+// k_miss_agg 0.305 -> 0.28 ms, but the pack's VALU (+18 %) made the token pass
+// 0.80 -> 0.90 ms, 2.885 -> 2.95 ms/step.
+#ifndef Q_PK10
+#define Q_PK10 0
+#endif
+#define PK10_TAG 0x8000000000000000ull
+__device__ __forceinline__ u64 pk6x8(u64 y) {  // 8 token bytes -> 48 bits of codes
+    y = (y & 0x1F1F1F1F1F1F1F1Full) | ((y >> 1) & 0x2020202020202020ull);
+    y = (y & 0x003F003F003F003Full) | ((y >> 2) & 0x0FC00FC00FC00FC0ull);
+    y = (y & 0x00000FFF00000FFFull) | ((y >> 4) & 0x00FFF00000FFF000ull);
+    return (y & 0xFFFFFFull) | ((y >> 8) & 0xFFFFFF000000ull);
+}
+__device__ __forceinline__ u64 pk10(u64 k0, u64 k1m) {  // k1m: bytes 8, 9 (| KMARK)
+    const u32 h = (u32)k1m & 0xFFFFu;
+    const u32 c = (h & 0x1F1Fu) | ((h >> 1) & 0x2020u);
+    return pk6x8(k0) | ((u64)((c & 0x3Fu) | ((c >> 2) & 0xFC0u)) << 48) | PK10_TAG;
+}
+__device__ __forceinline__ u32 unpk6(u32 c) { return c ? c + (c >= 32 ? 0x40u : 0x20u) : 0u; }
+__device__ __forceinline__ void unpk10(u64 p, u64 &k0, u64 &k1m) {  // the inverse of pk10
+    k0 = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) k0 |= (u64)unpk6((u32)(p >> (6 * j)) & 63u) << (8 * j);
+    k1m = KMARK | unpk6((u32)(p >> 48) & 63u) | (unpk6((u32)(p >> 54) & 63u) << 8);
+}
+
 // LDS lookup of an S key (3..8 bytes, nonzero).  Returns the slot or ~0u.
 __device__ __forceinline__ u32 lds_find8(u64 *skeys, u64 k0) {
     // full-rate 24-bit multiplies only (v_mul_u32_u24; the 32-bit ones are
@@ -642,8 +674,9 @@ __device__ __forceinline__ void tok_phase(const ScanArgs &a, u64 ib, u64 lpos, u
             k1 = lower_tok8(x1) | KMARK;
             if (K3_ABLATE && (a.ablate & 32)) {
                 words += (k0 ^ k1) == 1;  // keep the key build alive
-            } else if (len <= 8) {
-                const u32 slot = lds_find8(skeys, k0);
+            } else if (len <= (Q_PK10 ? 10u : 8u)) {
+                const u64 sk = (Q_PK10 && len > 8) ? pk10(k0, k1) : k0;
+                const u32 slot = lds_find8(skeys, sk);
                 if (slot != ~0u) atomicAdd(&scnts[slot], 1u);
                 else mis = !(K3_ABLATE && (a.ablate & 4));
             } else {
@@ -674,18 +707,25 @@ __device__ __forceinline__ void tok_phase(const ScanArgs &a, u64 ib, u64 lpos, u
 }
 
 // End of a counting workgroup: the wave's pending misses, total_words, the
-// LDS table flushed into the logs (counts encoded; full partitions: HBM
-// inserts) and the log lengths.
+// LDS table flushed into the logs (counts encoded) and the log lengths.  Only
+// this flush inserts into the HBM table when a partition is full (its entries
+// carry counts, at most Q_SSLOTS of them); a full partition during the token
+// walk drops the miss and flags OVF_MLOG instead (tok_batches).
 __device__ __forceinline__ void tok_epilogue(const ScanArgs &a, u64 *skeys, u32 *scnts, u32 *lcur, u64 words) {
     const u32 lane = lane_id();
     words = wave_sum64(words);
     if (lane == 0 && words) atomicAdd((unsigned long long *)&a.ctr->total_words, (unsigned long long)words);
     __syncthreads();
-    // the LDS table into the logs, counts encoded (full partitions: HBM inserts)
+    // the LDS table into the logs, counts encoded (a full partition: HBM insert)
     for (u32 i = threadIdx.x; i < Q_SSLOTS && !(K3_ABLATE && (a.ablate & 32768)); i += Q_T) {  // 32768: no flush
         u32 n = scnts[i];
         if (!n) continue;
-        const ulonglong2 kk = make_ulonglong2(skeys[i], KMARK);
+        ulonglong2 kk = make_ulonglong2(skeys[i], KMARK);
+        if (Q_PK10 && (kk.x & PK10_TAG)) {  // a 9..10-byte word
+            u64 u0, u1;
+            unpk10(kk.x, u0, u1);
+            kk = make_ulonglong2(u0, u1);
+        }
         const u32 part = mlog_part(kk.x, kk.y);
         const u64 base = ((u64)blockIdx.x * MSA_MLOG_PARTS + part) * a.mlog_cap;
         while (n) {

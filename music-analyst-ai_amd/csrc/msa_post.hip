@@ -351,6 +351,21 @@ __device__ __forceinline__ uint4 load16u(const u8 *__restrict__ buf, u64 s) {
     const u32 *p = reinterpret_cast<const u32 *>(buf + (s & ~3ull));
     return align16(make_uint4(p[0], p[1], p[2], p[3]), p[4], (u32)(s & 3));
 }
+// funnel16 without the branch: dword selects + v_alignbyte
+__device__ __forceinline__ uint4 funnel16a(const uint4 &X, const uint4 &Y, u32 ph) {
+    const u32 d = ph >> 2, s = ph & 3u;
+    const u32 w[8] = {X.x, X.y, X.z, X.w, Y.x, Y.y, Y.z, Y.w};
+    u32 c[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) c[i] = d == 0 ? w[i] : (d == 1 ? w[i + 1] : (d == 2 ? w[i + 2] : w[i + 3]));
+    return make_uint4(__builtin_amdgcn_alignbyte(c[1], c[0], s), __builtin_amdgcn_alignbyte(c[2], c[1], s),
+                      __builtin_amdgcn_alignbyte(c[3], c[2], s), __builtin_amdgcn_alignbyte(c[4], c[3], s));
+}
+// lane l receives lane l + 1's value (lane 63: 0): DPP wave shift; every lane active
+__device__ __forceinline__ u32 dpp_next32(u32 v) { return __builtin_amdgcn_update_dpp(0u, v, 0x130, 0xF, 0xF, false); }
+#ifndef CG_AL
+#define CG_AL 0  // 1: text.csv's single-line slots by one aligned 16-byte load + the next lane's (k_col_gather)
+#endif
 // out with its bytes [a, b) (0 <= a <= b <= 16) taken from v
 __device__ __forceinline__ uint4 bytes_blend(const uint4 &out, const uint4 &v, u32 a, u32 b) {
     const u64 lo = bits_from(8 * a) & bits_below(8 * b);
@@ -900,10 +915,17 @@ __global__ __launch_bounds__(CG_T) void k_col_gather(const u8 *__restrict__ buf,
 #ifndef CG_B
 #define CG_B 2
 #endif
+#if CG_AL
+    const u32 lane = t & 63u;
+#endif
     for (u64 s0 = t; s0 < nslots; s0 += (u64)CG_B * CG_T) {
         uint4 va[CG_B];
         u32 jj[CG_B], d4[CG_B], sh[CG_B];
         bool fast[CG_B];
+#if CG_AL
+        uint4 vb[CG_B];  // the 16 aligned bytes after va's: own load, or the next lane's va
+        bool ownb[CG_B];
+#endif
 #pragma unroll
         for (int k = 0; k < CG_B; ++k) {
             const u64 si = s0 + (u64)k * CG_T;
@@ -911,6 +933,10 @@ __global__ __launch_bounds__(CG_T) void k_col_gather(const u8 *__restrict__ buf,
             jj[k] = 0;
             sh[k] = 0;
             d4[k] = 0;
+#if CG_AL
+            va[k] = vb[k] = make_uint4(0, 0, 0, 0);
+            ownb[k] = false;
+#endif
             if (si >= nslots) continue;
             const u64 A = S0 + si * CG_SLOT;
             const u64 lo = max(A, O0), hi = min(A + CG_SLOT, O1);
@@ -931,20 +957,44 @@ __global__ __launch_bounds__(CG_T) void k_col_gather(const u8 *__restrict__ buf,
             const u64 lstart = hdr + w_off[j], lend = hdr + w_off[j + 1];  // '\n' at lend-1
             if (lo == A && hi == A + CG_SLOT && A + CG_SLOT < lend) {
                 const u64 src = w_src[j] + (A - lstart);
+#if CG_AL
+                // one aligned 16-byte load; the 16 bytes after it are the next
+                // lane's load when that lane's slot is the next slot of this
+                // line (a fast one too), else this lane loads them as well
+                const size_t pa = (size_t)(buf + src);
+                const uint4 *p = reinterpret_cast<const uint4 *>(pa & ~(size_t)15);
+                va[k] = p[0];
+                sh[k] = (u32)(pa & 15);
+                ownb[k] = sh[k] && (lane == 63 || !(A + 2 * CG_SLOT < lend && A + 2 * CG_SLOT <= O1));
+                if (ownb[k]) vb[k] = p[1];
+#else
                 const u32 *p = reinterpret_cast<const u32 *>(buf + (src & ~3ull));
                 va[k] = make_uint4(p[0], p[1], p[2], p[3]);
                 d4[k] = p[4];
                 sh[k] = (u32)(src & 3);
+#endif
                 fast[k] = true;
             }
         }
+#if CG_AL
+#pragma unroll
+        for (int k = 0; k < CG_B; ++k) {  // every lane active: DPP reads the source lane's register
+            const uint4 nx = make_uint4(dpp_next32(va[k].x), dpp_next32(va[k].y), dpp_next32(va[k].z),
+                                        dpp_next32(va[k].w));
+            if (!ownb[k]) vb[k] = nx;
+        }
+#endif
 #pragma unroll
         for (int k = 0; k < CG_B; ++k) {
             const u64 si = s0 + (u64)k * CG_T;
             if (si >= nslots) continue;
             const u64 A = S0 + si * CG_SLOT;
             if (fast[k]) {
+#if CG_AL
+                *reinterpret_cast<uint4 *>(col + A) = funnel16a(va[k], vb[k], sh[k]);
+#else
                 *reinterpret_cast<uint4 *>(col + A) = align16(va[k], d4[k], sh[k]);
+#endif
                 continue;
             }
             // the slot holds a line end: compose it from the (usually two) lines

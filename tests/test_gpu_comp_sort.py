@@ -108,3 +108,19 @@ def test_tie_rounds_short_runs(msa_mod, tmp_path, monkeypatch, case, seg):
     data = corpus(case_runs(case), seed=7 + len(case))
     with msa_mod.Context(0) as c:
         check_against_oracle(msa_mod, c, data, tmp_path, f"tieseg_{case}_{seg}")
+
+
+def test_blob_regrow(msa_mod, tmp_path, monkeypatch):
+    """The key blob of radix-sorted tables (k_blob_len, the offsets' scan,
+    k_blob_write) against the oracle, three inputs on one context: the second
+    holds 70-byte words, longer than the blob estimate allows for (48 bytes
+    per long word) -- its blob is written past the capacity, grown and written
+    again; the third is a high-cardinality table of > 1 M keys."""
+    monkeypatch.setenv("MSA_SORT", "radix")
+    with msa_mod.Context(0) as c:
+        check_against_oracle(msa_mod, c, corpus(case_words("byte_gid"), seed=3), tmp_path, "blob_small")
+        ws = [(letters(i, 6) + "x" * 63 + letters(i, 1), 1 + i % 2) for i in range(4000)]
+        ws += [(letters(i, 5), 1) for i in range(3000)]
+        check_against_oracle(msa_mod, c, corpus(ws, seed=5), tmp_path, "blob_long")
+        big = msa_mod.gen_corpus(100000, mode="highcard", seed=9)
+        check_against_oracle(msa_mod, c, big, tmp_path, "blob_hc")
