@@ -50,7 +50,18 @@ def _no_launcher_env():
 
 
 def _shm_leftovers():
-    return sorted(f for f in os.listdir("/dev/shm") if f.startswith("msa_"))
+    """msa_* blocks in /dev/shm, except those of a job still running (msa_<pid>_...
+    with that process alive: another xdist worker's job, created after a
+    test's `before` snapshot)."""
+    out = []
+    for f in os.listdir("/dev/shm"):
+        if not f.startswith("msa_"):
+            continue
+        pid = f.split("_")[1]
+        if pid.isdigit() and os.path.exists(f"/proc/{pid}"):
+            continue
+        out.append(f)
+    return sorted(out)
 
 
 @needs_mpirun
