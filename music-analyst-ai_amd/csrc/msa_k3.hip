@@ -43,6 +43,12 @@ namespace {
 #ifndef Q_PROBE1
 #define Q_PROBE1 0               // 1: a bucket's second half read only by lanes its first half left open
 #endif
+#ifndef Q_LIST2
+#define Q_LIST2 1                // 1: the token list built two starts a trip (lowest + highest)
+#endif
+#ifndef Q_X2
+#define Q_X2 0                   // 1: two probe batches a trip in the token pass
+#endif
 #ifndef TOK_PF
 #define TOK_PF 1                 // batches of key loads in flight ahead of the probed one
 #endif
@@ -265,16 +271,43 @@ __device__ __forceinline__ void unpk10(u64 p, u64 &k0, u64 &k1m) {  // the inver
 }
 
 // LDS lookup of an S key (3..8 bytes, nonzero).  Returns the slot or ~0u.
-__device__ __forceinline__ u32 lds_find8(u64 *skeys, u64 k0) {
-    // full-rate 24-bit multiplies only (v_mul_u32_u24; the 32-bit ones are
-    // quarter rate); the bucket is the top 20 bits scaled to Q_SNB (< 2^12)
-    // (HIP's __umul24 returns int: the products are taken as u32 before any shift)
+// The bucket: full-rate 24-bit multiplies only (v_mul_u32_u24; the 32-bit
+// ones are quarter rate), the top 20 bits scaled to Q_SNB (< 2^12) (HIP's
+// __umul24 returns int: the products are taken as u32 before any shift)
+__device__ __forceinline__ u32 lds_bucket8(u64 k0) {
     const u32 lo = (u32)k0, hi = (u32)(k0 >> 32);
     u32 t = lo + ((hi << 13) | (hi >> 19));
     t ^= t >> 17;
     u32 h = (u32)__umul24(t, 0x9E3779u);
     h ^= h >> 13;
-    u32 b = (u32)__umul24(h >> 12, (u32)Q_SNB) >> 20;
+    return (u32)__umul24(h >> 12, (u32)Q_SNB) >> 20;
+}
+__device__ __forceinline__ u32 match4(const ulonglong2 &s01, const ulonglong2 &s23, u64 k) {
+    return s01.x == k ? 0u : (s01.y == k ? 1u : (s23.x == k ? 2u : (s23.y == k ? 3u : 4u)));
+}
+// a key not among bucket b's four (s01, s23): claim its first empty slot
+// (CAS; a racing claim of the same key is a hit), else the next bucket
+__device__ __forceinline__ u32 lds_find8_rest(u64 *skeys, u64 k0, u32 b, ulonglong2 s01, ulonglong2 s23) {
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+        const u32 base = b * 4;
+        if (p) {
+            s01 = *reinterpret_cast<const ulonglong2 *>(&skeys[base]);
+            s23 = *reinterpret_cast<const ulonglong2 *>(&skeys[base + 2]);
+            const u32 hit = match4(s01, s23, k0);
+            if (hit < 4) return base + hit;
+        }
+        u32 i = s01.x == 0 ? 0u : (s01.y == 0 ? 1u : (s23.x == 0 ? 2u : (s23.y == 0 ? 3u : 4u)));
+        for (; i < 4; ++i) {
+            const u64 old = atomicCAS((unsigned long long *)&skeys[base + i], 0ull, (unsigned long long)k0);
+            if (old == 0 || old == k0) return base + i;
+        }
+        b = (b + 1 == Q_SNB) ? 0 : b + 1;
+    }
+    return ~0u;
+}
+__device__ __forceinline__ u32 lds_find8(u64 *skeys, u64 k0) {
+    u32 b = lds_bucket8(k0);
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
         const u32 base = b * 4;
@@ -290,7 +323,7 @@ __device__ __forceinline__ u32 lds_find8(u64 *skeys, u64 k0) {
         const u32 hit = s23.x == k0 ? 2u : (s23.y == k0 ? 3u : 4u);
 #else
         const ulonglong2 s23 = *reinterpret_cast<const ulonglong2 *>(&skeys[base + 2]);
-        const u32 hit = s01.x == k0 ? 0u : (s01.y == k0 ? 1u : (s23.x == k0 ? 2u : (s23.y == k0 ? 3u : 4u)));
+        const u32 hit = match4(s01, s23, k0);
 #endif
         if (hit < 4) return base + hit;
         u32 i = s01.x == 0 ? 0u : (s01.y == 0 ? 1u : (s23.x == 0 ? 2u : (s23.y == 0 ? 3u : 4u)));
@@ -301,6 +334,20 @@ __device__ __forceinline__ u32 lds_find8(u64 *skeys, u64 k0) {
         b = (b + 1 == Q_SNB) ? 0 : b + 1;
     }
     return ~0u;
+}
+// Two keys a lane (Q_X2): both buckets' four reads in flight together, then
+// the hits; the rest one key after the other.  p*: probe this key at all.
+__device__ __forceinline__ void lds_find8x2(u64 *skeys, bool pa, u64 ka, bool pb, u64 kb, u32 &sa, u32 &sb) {
+    const u32 ba = lds_bucket8(ka), bb = lds_bucket8(kb);
+    const ulonglong2 a01 = *reinterpret_cast<const ulonglong2 *>(&skeys[ba * 4]);
+    const ulonglong2 a23 = *reinterpret_cast<const ulonglong2 *>(&skeys[ba * 4 + 2]);
+    const ulonglong2 b01 = *reinterpret_cast<const ulonglong2 *>(&skeys[bb * 4]);
+    const ulonglong2 b23 = *reinterpret_cast<const ulonglong2 *>(&skeys[bb * 4 + 2]);
+    const u32 ha = match4(a01, a23, ka), hb = match4(b01, b23, kb);
+    sa = ha < 4 ? ba * 4 + ha : ~0u;
+    sb = hb < 4 ? bb * 4 + hb : ~0u;
+    if (pa && ha >= 4) sa = lds_find8_rest(skeys, ka, ba, a01, a23);
+    if (pb && hb >= 4) sb = lds_find8_rest(skeys, kb, bb, b01, b23);
 }
 
 template <bool CASF = (TAB_CAS_FIRST != 0)>
@@ -511,6 +558,7 @@ typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void lpos_fill(const ScanArgs &a, u64 from, u64 to) {
     for (u64 k = from + lane_id(); k < to && k < a.l_cap; k += 64) a.l_pos[k] = LP_NONE;
 }
+static_assert(!(Q_X2 && (Q_KAL || Q_TDL || TOK_PF > 1 || K3_ABLATE || Q_PK10)), "Q_X2: the plain key loads only");
 __device__ __forceinline__ void tok_phase(const ScanArgs &a, u64 ib, u64 lpos, u64 w, u64 Tn, u64 S0, u64 *skeys,
                                           u32 *scnts, u16 *list, u32 *lcur,
                                           u64 &words, __amdgpu_buffer_rsrc_t rsrc, u64 &lres, u64 &lend, u64 lch) {
@@ -559,19 +607,42 @@ __device__ __forceinline__ void tok_phase(const ScanArgs &a, u64 ib, u64 lpos, u
     // re-read from memory
     u64 m = (K3_ABLATE && (a.ablate & 3)) ? 0ull : (sS | sM);
     u32 nS;
-    u32 li = wave_prefix<5>((u32)__popcll(m), nS);
+    const u32 ntl = (u32)__popcll(m);
+    u32 li = wave_prefix<5>(ntl, nS);
+    // token length (<= 16 here): first non-token bit at or after b, from the
+    // 32 bits [b, b + 32) of (Tn:T)
+    const u32 d0 = (u32)w, d1 = (u32)(w >> 32), d2 = (u32)Tn;
+    auto entry = [&](u32 b) -> u16 {
+        const u32 run = __builtin_amdgcn_alignbit(b >= 32 ? d2 : d1, b >= 32 ? d1 : d0, b & 31u);
+        const u32 len = (u32)__ffs(~run) - 1;  // 3..16
+        return (u16)((lane * 64 + b) | ((len - 3) << 12));
+    };
+#if Q_LIST2
+    // two tokens a trip, the lowest and the highest start left (half the
+    // trips of the loop-carried chain; the lane's list range filled from
+    // both ends)
+    u32 hi = li + ntl;
+    while (__ballot(m != 0)) {
+        if (m) {
+            const u32 b = (u32)__ffsll((long long)m) - 1;
+            const u32 bh = 63u - (u32)__clzll(m);
+            m &= m - 1;
+            list[li++] = entry(b);
+            if (bh != b) {
+                m &= ~(1ull << bh);
+                list[--hi] = entry(bh);
+            }
+        }
+    }
+#else
     while (__ballot(m != 0)) {
         if (m) {
             const u32 b = (u32)__ffsll((long long)m) - 1;
             m &= m - 1;
-            // token length (<= 16 here): first non-token bit at or after b,
-            // from the 32 bits [b, b + 32) of (Tn:T)
-            const u32 d0 = (u32)w, d1 = (u32)(w >> 32), d2 = (u32)Tn;
-            const u32 run = __builtin_amdgcn_alignbit(b >= 32 ? d2 : d1, b >= 32 ? d1 : d0, b & 31u);
-            const u32 len = (u32)__ffs(~run) - 1;  // 3..16
-            list[li++] = (u16)((lane * 64 + b) | ((len - 3) << 12));
+            list[li++] = entry(b);
         }
     }
+#endif
     wsync();
     // Keys are re-read from the block (L2) as dwords from the token's
     // dword; the next 64 tokens' loads are issued before this batch is
@@ -614,6 +685,55 @@ __device__ __forceinline__ void tok_phase(const ScanArgs &a, u64 ib, u64 lpos, u
         v4 = gp[4];
     };
 #endif
+#if Q_X2
+    // two batches a trip (the lanes' j-th tokens of batches 2i and 2i + 1):
+    // two independent key builds, probes and log stores in flight together
+    // -- the pass waits on each batch's dependent chain at 4 waves per SIMD
+    u32 enA, k4A, enB, k4B;
+    uint4 kvA, kvB;
+    kload(0, enA, kvA, k4A);
+    kload(1, enB, kvB, k4B);
+    auto keyof = [&](u32 e, const uint4 &v, u32 v4, u64 &k0, u64 &k1) {
+        const u32 len = (e >> 12) + 3;
+        const u32 sh = (u32)(ib + (e & 4095u)) & 3u;
+        u64 x0 = mk64(__builtin_amdgcn_alignbyte(v.y, v.x, sh), __builtin_amdgcn_alignbyte(v.z, v.y, sh));
+        u64 x1 = mk64(__builtin_amdgcn_alignbyte(v.w, v.z, sh), __builtin_amdgcn_alignbyte(v4, v.w, sh));
+        const u32 nbits = 8 * len;  // 24..128
+        x0 &= bits_lo(nbits);
+        x1 = nbits <= 64 ? 0ull : (x1 & bits_lo(nbits - 64));
+        k0 = lower_tok8(x0);
+        k1 = lower_tok8(x1) | KMARK;
+        return len;
+    };
+    auto logmiss = [&](bool mis, u64 k0, u64 k1) {
+        u32 off = 0xFFFFFFF0u;
+        if (mis) {
+            const u32 part = mlog_part(k0, k1);
+            const u32 at = atomicAdd(&lcur[part], 1u);
+            if (at < a.mlog_cap) off = ((u32)__umul24(part, a.mlog_cap) + at) * 16u;  // cap < 2^24
+            else if (a.mlog_direct) hbm_insert16<false>(a, k0, k1, 1);  // logs at their size limit
+            else atomicAdd(&lcur[MSA_MLOG_PARTS], 1u);
+        }
+        const u32x4_t ent = {(u32)k0, (u32)(k0 >> 32), (u32)k1, (u32)(k1 >> 32)};
+        __builtin_amdgcn_raw_buffer_store_b128(ent, rsrc, (int)off, 0, 0);
+    };
+    for (u32 bt = 0; bt < nb; bt += 2) {
+        const u32 eA = enA, v4A = k4A, eB = enB, v4B = k4B;
+        const uint4 vA = kvA, vB = kvB;
+        const bool hA = bt * 64 + lane < nS, hB = (bt + 1) * 64 + lane < nS;
+        kload(bt + 2, enA, kvA, k4A);
+        kload(bt + 3, enB, kvB, k4B);
+        u64 a0 = 0, a1 = KMARK, b0 = 0, b1 = KMARK;
+        const u32 lA = keyof(eA, vA, v4A, a0, a1), lB = keyof(eB, vB, v4B, b0, b1);
+        const bool pA = hA && lA <= 8, pB = hB && lB <= 8;
+        u32 sA, sB;
+        lds_find8x2(skeys, pA, a0, pB, b0, sA, sB);
+        if (pA && sA != ~0u) atomicAdd(&scnts[sA], 1u);
+        if (pB && sB != ~0u) atomicAdd(&scnts[sB], 1u);
+        logmiss(hA && !(pA && sA != ~0u), a0, a1);
+        if (bt + 1 < nb) logmiss(hB && !(pB && sB != ~0u), b0, b1);
+    }
+#else
     u32 en, k4;
     uint4 kv;
     kload(0, en, kv, k4);
@@ -703,6 +823,7 @@ __device__ __forceinline__ void tok_phase(const ScanArgs &a, u64 ib, u64 lpos, u
         const u32x4_t ent = {(u32)k0, (u32)(k0 >> 32), (u32)k1, (u32)(k1 >> 32)};
         __builtin_amdgcn_raw_buffer_store_b128(ent, rsrc, (int)off, 0, 0);
     }
+#endif
     wsync();
 }
 
