@@ -101,6 +101,9 @@ hipError_t msa_launch_blob(const u32 *, u64, const u64 *, const u64 *, const u64
 #ifndef MSA_LISTS_BEFORE_SPANS
 #define MSA_LISTS_BEFORE_SPANS 1  // 0: the library stream waits for the spans before the word lists (A/B builds)
 #endif
+#ifndef MSA_ARTIST_EARLY
+#define MSA_ARTIST_EARLY 1  // 0: the split's artist pass waits for the offset scans too (A/B builds)
+#endif
 
 // ---------------------------------------------------------------------------
 namespace {
@@ -316,6 +319,7 @@ struct msa_ctx {
     hipEvent_t ev_r2_fork = nullptr, ev_r2_join = nullptr;
     // split scan: k_scan_struct done (the spans may start) / the spans done
     hipEvent_t ev_scan_a = nullptr, ev_spans = nullptr;
+    hipEvent_t ev_fix = nullptr;  // rank2: the artist keys written (k_rec_fast + k_rec_fix), before the offset scans
     // the folded split scan (k_scan_fold): tile statuses (5 words a tile) behind
     // the ticket counter, the tickets taken so far, the status epoch
     // env MSA_FOLD=1 (opt-in: measured as fast as K1 + K2 + k_scan_struct, 0.85
@@ -910,6 +914,7 @@ static int launch_spans(msa_ctx *c, bool want_text, hipStream_t st) {
                                  c->tlen.as<u64>(), c->tsrc.as<u64>(), c->tpairs.as<u32>(), c->ctr.as<Counters>(), ak,
                                  c->spans ? c->f0.as<u64>() : nullptr, c->tss.as<u64>(), c->tse.as<u64>(),
                                  c->span_fix.as<u64>(), c->ablate, st, fast_end));
+    if (st == c->rank2) HIPC(c, hipEventRecord(c->ev_fix, st));  // the artist pass may start here
     if ((rc = scan_columns(c, want_text, st))) return rc;
     prof_end(c, ST_REC_SPANS, nrec * 136, st);  // ~36 B read + 100 B written per record
     return MSA_OK;
@@ -1307,7 +1312,14 @@ static int split_once(msa_ctx *c, int flags) {
     // the slot lists need the tables only, not the spans: they run behind
     // k_miss_agg while the spans (rank2, slowed by the token pass beside them)
     // finish; everything below waits for the spans
+#if MSA_ARTIST_EARLY
+    // the artist pass needs the keys only: it waits for k_rec_fix, not for the
+    // offset scans behind it on rank2 (it starts as k_miss_agg's workgroups
+    // leave the CUs, ~80 us earlier); the scans are waited for after it
+    if (spans_beside) HIPC(c, hipStreamWaitEvent(c->stream, c->ev_fix, 0));
+#else
     if (spans_beside) HIPC(c, hipStreamWaitEvent(c->stream, c->ev_spans, 0));
+#endif
 #endif
     // the artist pass of msa_count (lines shortcut) right here, before the
     // read-back: it needs only the split's keys, and its counters come back
@@ -1318,6 +1330,9 @@ static int split_once(msa_ctx *c, int flags) {
         if ((rc = launch_artist_count(c))) return rc;
         c->artist_spec = true;
     }
+#if MSA_LISTS_BEFORE_SPANS && MSA_ARTIST_EARLY
+    if (spans_beside) HIPC(c, hipStreamWaitEvent(c->stream, c->ev_spans, 0));
+#endif
     // text.csv's gather forked here, ahead of the read-back's copies (it needs
     // nothing the host reads back): it runs during the copies, the host's
     // header work and msa_count's launches instead of after them
@@ -2127,6 +2142,7 @@ int msa_create(int device, msa_ctx **out) {
         hipEventCreateWithFlags(&c->ev_r2_join, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_scan_a, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_spans, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_fix, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fin, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
@@ -2180,6 +2196,7 @@ void msa_destroy(msa_ctx *c) {
     (void)hipEventDestroy(c->ev_r2_join);
     (void)hipEventDestroy(c->ev_scan_a);
     (void)hipEventDestroy(c->ev_spans);
+    (void)hipEventDestroy(c->ev_fix);
     (void)hipStreamDestroy(c->side);
     (void)hipStreamDestroy(c->rank2);
     (void)hipStreamDestroy(c->aux);
