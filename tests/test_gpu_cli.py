@@ -14,12 +14,17 @@ pytestmark = pytest.mark.gpu
 CLI = os.path.join(PKG, "bin", "parallel_spotify")
 
 
+@pytest.mark.parametrize("writer", ["host", "device"])
 @pytest.mark.parametrize("case", [c for c in CASES if c.startswith(("zipf", "torture", "multiline", "nul", "long"))])
-def test_cli_matches_reference(case, tmp_path):
+def test_cli_matches_reference(case, writer, tmp_path):
+    """writer: word_counts.csv / top_artists.csv formatted by the host loop
+    (tables up to MSA_CSV_HOST_MAX lines, the default for these sizes) or on
+    the device (k_csv_len, scan, k_csv_put: MSA_CSV_HOST_MAX=0)."""
     res, files = golden(case, 1)
     out = tmp_path / "out"
+    env = dict(os.environ, MSA_CSV_HOST_MAX="0" if writer == "device" else str(1 << 20))
     p = subprocess.run([CLI, os.path.join(GOLDEN, case, "input.csv"), "--output-dir", str(out)],
-                       capture_output=True, timeout=120)
+                       capture_output=True, timeout=120, env=env)
     assert p.returncode == 0, p.stderr
     got = read_outputs(str(out))
     assert got["metrics"] == {k: res[k] for k in ("processes", "total_songs", "total_words")}
@@ -31,12 +36,14 @@ def test_cli_matches_reference(case, tmp_path):
     assert set(m) == {"processes", "total_songs", "total_words", "compute_time", "total_time"}
 
 
-def test_cli_limits(tmp_path):
+@pytest.mark.parametrize("writer", ["host", "device"])
+def test_cli_limits(writer, tmp_path):
     case = "zipf_small"
     res, files = golden(case, 1)
     out = tmp_path / "out"
+    env = dict(os.environ, MSA_CSV_HOST_MAX="0" if writer == "device" else str(1 << 20))
     p = subprocess.run([CLI, os.path.join(GOLDEN, case, "input.csv"), "--output-dir", str(out),
-                        "--word-limit", "7", "--artist-limit", "3"], capture_output=True, timeout=120)
+                        "--word-limit", "7", "--artist-limit", "3"], capture_output=True, timeout=120, env=env)
     assert p.returncode == 0, p.stderr
     w = open(out / "word_counts.csv", "rb").read()
     a = open(out / "top_artists.csv", "rb").read()
