@@ -2716,6 +2716,17 @@ hipError_t msa_launch_col_write(int text, const u8 *buf, const u64 *len, const u
     hipLaunchKernelGGL(k_col_collapse, grid1(nrec), dim3(256), 0, s, buf, len, off, src, pairs, nrec, hdr, col);
     return hipGetLastError();
 }
+// Lines of one column laid out at absolute offsets: line j = the source
+// bytes [src[j], src[j] + off[j+1] - off[j] - 1) and a '\n' (the column
+// splitter's raw-copy values; body_p = the offset right after the column)
+hipError_t msa_launch_gather_lines(const u8 *buf, const u64 *len, const u64 *off, const u64 *src, u64 nrec,
+                                   const u64 *body_p, u8 *col, hipStream_t s) {
+    if (!nrec) return hipSuccess;
+    const u64 groups = (nrec + CG_T - 1) / CG_T;
+    hipLaunchKernelGGL(k_col_gather, dim3((u32)groups), dim3(CG_T), 0, s, buf, len, off, src, (const u32 *)nullptr,
+                       nrec, (u64)0, body_p, col);
+    return hipGetLastError();
+}
 // text.csv's body with the LDS-free gather (beside the token pass)
 hipError_t msa_launch_artist_key(const u8 *col, const u64 *ar_start, const u64 *line_off, const u64 *line_len, u64 hdr,
                                  u64 nrec, u8 *arena, u64 *key_off, u32 *key_len, u64 *key_slot, u64 *atab, u64 amask,

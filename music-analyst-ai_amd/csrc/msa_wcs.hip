@@ -38,6 +38,8 @@
 #include "msa_internal.h"
 
 hipError_t msa_exclusive_scan(const u64 *in, u64 n, u64 *out, u64 *bsum_scratch, u64 *total, hipStream_t s);
+hipError_t msa_launch_gather_lines(const u8 *buf, const u64 *len, const u64 *off, const u64 *src, u64 nrec,
+                                   const u64 *body_p, u8 *col, hipStream_t s);
 hipError_t msa_launch_sort(u64 *const K2[3], u64 *const K1[3], u64 *const K0[3], u32 *const V[3], u64 n, int *which,
                            hipStream_t s);
 
@@ -1249,12 +1251,34 @@ struct ColArgs {
     u8 *out;
     WCtr *ctr;
     Dia dia;           // the reader's dialect; the writer quotes with its delimiter and quotechar
+    u64 *src;          // [ncols * R]: a raw-copy value's source bytes (pass 0, CC_RAW)
+    u64 *fix;          // rows with a value that is not a raw copy (pass 0 lists them, pass 1 walks them)
+    u64 *nfix;
 };
 
+// Raw copies (CC_RAW): most values are written exactly as they stand in the
+// input -- an unquoted value that needs no quoting, or a quoted one that
+// needs quoting (the reader's and the writer's quotechar and doubling agree),
+// its quotes included -- so pass 0 records each value's source and whether
+// it is such a copy, a segmented gather (k_col_gather, msa_post.hip) copies
+// every column's lines with coalesced 16-byte stores, and pass 1 walks only
+// the rows holding another value, writing those values over the gather's.
+// (Pass 1 over every row, one thread a row through an 8-byte write combiner,
+// had been latency-bound: 4.4 ms for configs[2]'s 5 M rows.)
+#ifndef CC_RAW
+#define CC_RAW 1
+#endif
 template <int PASS>
 __global__ __launch_bounds__(256) void k_csvcol(ColArgs a) {
-    const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x + a.first;
-    if (r >= a.nrows) return;
+    u64 r;
+    if (PASS == 1 && a.fix) {
+        const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+        if (i >= *a.nfix) return;
+        r = a.fix[i];
+    } else {
+        r = (u64)blockIdx.x * blockDim.x + threadIdx.x + a.first;
+        if (r >= a.nrows) return;
+    }
     const u64 rs = a.rend[r - 1], re = a.rend[r];
     const u64 j = r - a.first;  // output row
     u32 s = SR, chars = 0;
@@ -1265,12 +1289,20 @@ __global__ __launch_bounds__(256) void k_csvcol(ColArgs a) {
     u64 acc = 0;
     u32 nacc = 0;
     bool q = false;
+    bool wr = true;  // pass 1: this value is written here (not a raw copy)
+    // pass 0, raw-copy tracking: the value's first source byte (its opening
+    // quote when quoted), quoted, bytes after a closing quote, any value of
+    // the row left to pass 1
+    u64 fs = ~0ull;
+    bool qin = false, bad = false, anyfix = false;
     auto put = [&](u32 c) {
+        if (PASS == 1 && !wr) return;
         if (nacc == 0 && ((uintptr_t)dst & 7u) != 0) { *dst++ = (u8)c; return; }
         acc |= (u64)c << (8 * nacc);
         if (++nacc == 8) { *(u64 *)dst = acc; dst += 8; acc = 0; nacc = 0; }
     };
     auto flush = [&]() {
+        if (PASS == 1 && !wr) return;
         for (u32 k = 0; k < nacc; ++k) dst[k] = (u8)(acc >> (8 * k));
         dst += nacc;
         acc = 0;
@@ -1279,20 +1311,29 @@ __global__ __launch_bounds__(256) void k_csvcol(ColArgs a) {
     auto open_field = [&]() {
         clen = 0;
         special = false;
+        fs = ~0ull;
+        qin = bad = false;
         if (PASS == 1 && f < a.ncols) {
             const u64 k = f * a.R + j;
             dst = a.out + a.off[k];
-            q = a.quoted[k] != 0;
+            wr = (a.quoted[k] & 2u) == 0;
+            q = (a.quoted[k] & 1u) != 0;
             if (q) put(a.dia.quote);
         }
     };
-    auto save = [&]() {
+    // fend: one past the value's last source byte; sv: the reader's state there
+    auto save = [&](u64 fend, u32 sv) {
         if (f < a.ncols) {
             if (PASS == 0) {
                 const u64 k = f * a.R + j;
                 const bool qq = special || clen == 0;  // clen already counts doubled quotes
                 a.len[k] = qq ? clen + 3 : clen + 1;
-                a.quoted[k] = qq;
+                bool raw = CC_RAW && !bad && fs != ~0ull;
+                if (qq) raw = raw && qin && sv == QQ && fend - fs == clen + 2;
+                else raw = raw && !qin && fend - fs == clen;
+                a.quoted[k] = (qq ? 1u : 0u) | (raw ? 2u : 0u);
+                if (a.src) a.src[k] = raw ? fs : 0;
+                anyfix |= !raw;
             } else {
                 if (q) put(a.dia.quote);
                 put('\n');
@@ -1327,6 +1368,11 @@ __global__ __launch_bounds__(256) void k_csvcol(ColArgs a) {
             int prev = -1;
             auto run = [&](u32 m) {
                 if (!m) return;
+                if (s == SR || s == SF) {  // an unquoted value starts here
+                    if (fs == ~0ull) fs = b0 + (u32)__builtin_ctz(m);
+                } else if (s == QQ) {
+                    bad = true;  // bytes after a closing quote
+                }
                 if (PASS == 0) {
                     chars += (u32)__popc(m & ~CONT);
                     if (chars > FIELD_LIMIT) limit = true;
@@ -1347,7 +1393,17 @@ __global__ __launch_bounds__(256) void k_csvcol(ColArgs a) {
                 const u32 cls = cls_of(b, a.dia);
                 const u32 tnext = cls_next(cls);
                 const u32 act = (cls_act(cls) >> (2 * s)) & 3u;
-                if (act & 2u) save();
+                if (act & 2u) save(i, s);
+                if (s == SR || s == SF) {
+                    if (cls == C_Q) {  // an opening quote
+                        qin = true;
+                        fs = i;
+                    } else if ((act & 1u) && fs == ~0ull) {
+                        fs = i;
+                    }
+                } else if (s == QQ && cls != C_Q && !(act & 2u)) {
+                    bad = true;
+                }
                 if (act & 1u) {
                     if ((b & 0xC0) != 0x80 && ++chars > FIELD_LIMIT) limit = true;
                     if (f < a.ncols) {
@@ -1362,7 +1418,7 @@ __global__ __launch_bounds__(256) void k_csvcol(ColArgs a) {
                 }
                 s = step(tnext, s);
                 if (eol) {
-                    if (s == SF || s == IF || s == QQ) save();
+                    if (s == SF || s == IF || s == QQ) save(i + 1, s);
                     if (s != IQ) s = SR;
                 }
                 prev = (int)p;
@@ -1370,18 +1426,23 @@ __global__ __launch_bounds__(256) void k_csvcol(ColArgs a) {
             run(O & ~(prev < 0 ? 0u : ((2u << prev) - 1u)));
         }
     }
-    if (s == IQ) { save(); any = true; }
+    if (s == IQ) { save(re, s); any = true; }
     if (PASS == 0 && limit) wcs_err(a.ctr, r, E_LIMIT);
     (void)any;
     // missing fields (and every field of a blank row) are ""
     for (; f < a.ncols; ++f) {
         const u64 k = f * a.R + j;
-        if (PASS == 0) { a.len[k] = 3; a.quoted[k] = 1; }
-        else {
+        if (PASS == 0) {
+            a.len[k] = 3;
+            a.quoted[k] = 1;
+            if (a.src) a.src[k] = 0;
+            anyfix = true;
+        } else {
             u8 *d = a.out + a.off[k];
             d[0] = (u8)a.dia.quote; d[1] = (u8)a.dia.quote; d[2] = '\n';
         }
     }
+    if (PASS == 0 && a.fix && anyfix) a.fix[atomicAdd((unsigned long long *)a.nfix, 1ull)] = r;
 }
 
 inline dim3 grid1(u64 n, u32 t = 256) { return dim3((u32)((n + t - 1) / t)); }
@@ -1416,7 +1477,7 @@ struct msa_wcs {
     u32 delim = ',';  // field delimiter (msa_wcs_set_delimiter: the script's --delimiter or csv.Sniffer's guess)
     hipEvent_t ev_a = nullptr, ev_b = nullptr;  // k_wcs_wrows of the last run (msa_wcs_kernel_ms)
     float wrows_ms = 0;
-    float csvcol_ms = 0;  // k_csvcol<1> of the last msa_csvcol_run (msa_csvcol_kernel)
+    float csvcol_ms = 0;  // the copy phase of the last msa_csvcol_run (msa_csvcol_kernel): the gathers + k_csvcol<1>
     u64 csvcol_out = 0;   // its output bytes
     u32 quote = '"';  // quotechar and skipinitialspace (msa_wcs_set_quoting): the column splitter's dialect
     u32 skipsp = 0;
@@ -1431,8 +1492,8 @@ struct msa_wcs {
     u8 *d_ccout = nullptr;
     bool cc_have = false;
     // scratch owned by the run
-    void *scr[26] = {nullptr};  // grow-only pool: buffers persist across runs
-    u64 scr_cap[26] = {0};
+    void *scr[29] = {nullptr};  // grow-only pool: buffers persist across runs
+    u64 scr_cap[29] = {0};
 };
 
 static int wfail(msa_wcs *w, int code, const char *fmt, ...) {
@@ -2133,6 +2194,13 @@ extern "C" int msa_csvcol_run(msa_wcs *w, int has_header, uint64_t *ncols, uint6
     a.buf = w->d_buf; a.n = w->n; a.rend = w->d_rend; a.first = first; a.nrows = nr + 1;
     a.ncols = nc; a.R = R; a.len = len; a.quoted = quoted; a.off = w->d_ccoff; a.out = nullptr; a.ctr = ctr;
     a.dia = w->dia();
+    a.src = nullptr; a.fix = nullptr; a.nfix = nullptr;
+#if CC_RAW
+    WCHECK(wpool(w, 26, (cells + 1) * 8, a.src));
+    WCHECK(wpool(w, 27, (R + 1) * 8, a.fix));
+    WCHECK(wpool(w, 28, 16, a.nfix));
+    WCHECK(hipMemsetAsync(a.nfix, 0, 8, st));
+#endif
     if (cells) {
         hipLaunchKernelGGL(k_csvcol<0>, grid1(R), dim3(256), 0, st, a);
         WCHECK(msa_exclusive_scan(len, cells, w->d_ccoff, bsum, total, st));
@@ -2149,7 +2217,15 @@ extern "C" int msa_csvcol_run(msa_wcs *w, int has_header, uint64_t *ncols, uint6
     WCHECK(wpool(w, 22, outlen + 16, w->d_ccout));
     a.out = w->d_ccout;
     WCHECK(hipEventRecord(w->ev_a, st));
+#if CC_RAW
+    // every column's lines as raw copies, then the rows holding another value
+    for (u64 f = 0; cells && f < nc; ++f)
+        WCHECK(msa_launch_gather_lines(w->d_buf, len + f * R, w->d_ccoff + f * R, a.src + f * R, R,
+                                       w->d_ccoff + (f + 1) * R, a.out, st));
     if (cells) hipLaunchKernelGGL(k_csvcol<1>, grid1(R), dim3(256), 0, st, a);
+#else
+    if (cells) hipLaunchKernelGGL(k_csvcol<1>, grid1(R), dim3(256), 0, st, a);
+#endif
     WCHECK(hipGetLastError());
     WCHECK(hipEventRecord(w->ev_b, st));
     WCHECK(hipStreamSynchronize(st));

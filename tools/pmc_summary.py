@@ -76,7 +76,7 @@ def bench_line(log):
 def main():
     args = [x for x in sys.argv[1:] if not x.startswith("--")]
     wcs = "--wcs" in sys.argv  # passes over tools/bench_wcs.py: the roofline kernel is k_wcs_wrows
-    split = "--split" in sys.argv  # passes over tools/bench_wcs.py --path split: k_csvcol<1>
+    split = "--split" in sys.argv  # passes over tools/bench_wcs.py --path split: its copy phase
     out = args[0] if args else "gpurun_out/pmc"
     per = collect(out)
     kernels = {}
@@ -89,7 +89,15 @@ def main():
         kernels[k] = e
     b = bench_line(os.path.join(out, "fetch.log"))
     # the bench line names the roofline kernel ("k_scan_tokens (csv_tokens)", ...)
-    rk = "k_wcs_wrows" if wcs else ("k_csvcol<1>" if split else
+    if split and b and "k_col_gather" in kernels and "k_csvcol<1>" in kernels:
+        # the splitter's copy phase per run: one k_col_gather per column + k_csvcol<1>
+        nc = b["config"]["columns"]
+        g, c1 = kernels["k_col_gather"], kernels["k_csvcol<1>"]
+        kernels["copy_phase"] = {k: nc * g[k] + c1[k] for k in
+                                 ("hbm_bytes_per_launch", "fetch_raw_bytes_per_launch", "write_bytes_per_launch")
+                                 if k in g and k in c1}
+        kernels["copy_phase"]["counters"] = {"note": f"{nc} x k_col_gather + k_csvcol<1>, per run"}
+    rk = "k_wcs_wrows" if wcs else ("copy_phase" if split else
                                     ((b or {}).get("roofline", {}).get("kernel", "k_scan_csv").split(" ")[0]))
     res = {
         "build_id": build_id(),
@@ -110,7 +118,7 @@ def main():
     with open(os.path.join(out, "pmc.json"), "w") as f:
         json.dump(res, f, indent=1)
     for k, e in sorted(kernels.items()):
-        print(k, json.dumps({x: round(y, 1) for x, y in e["counters"].items()}))
+        print(k, json.dumps({x: (round(y, 1) if isinstance(y, float) else y) for x, y in e["counters"].items()}))
         if "hbm_bytes_per_launch" in e:
             print("   hbm bytes/launch", e["hbm_bytes_per_launch"])
     print("traffic_over_alg", res.get("traffic_over_alg"))
