@@ -72,6 +72,9 @@ constexpr u32 A_SP = PA(0, 0, 1, 1, 1, 0);
 constexpr u32 A_SPD = PA(0, 0, 2, 1, 2, 0);
 #undef PA
 
+#ifndef WCS_PF
+#define WCS_PF 1  // 0: the row-split walks and the splitter's row walk without the next vector's load in flight (A/B)
+#endif
 constexpr u32 SEG = 256;        // bytes per lane in the map / emit passes
 constexpr u32 BLK = 256;        // threads per block in the state scan
 constexpr u32 PER = 4;          // segments per thread in the state scan
@@ -213,10 +216,19 @@ __device__ __forceinline__ bool eol_after(u32 b, u32 next, u64 i, u64 n) {
 // end of a line after byte i.
 template <typename W>
 __device__ __forceinline__ void seg_walk(const u8 *__restrict__ buf, u64 base, u64 ds, u64 n, Dia dia, W &wk) {
+#if WCS_PF
+    uint4 vn = base < n ? *(const uint4 *)(buf + base) : make_uint4(0, 0, 0, 0);
+#endif
     for (u32 q = 0; q < SEG / 16; ++q) {
         const u64 b0 = base + q * 16;
         if (b0 >= n) break;
+#if WCS_PF
+        // the next vector's load in flight while this one is walked
+        const uint4 v = vn;
+        if (q + 1 < SEG / 16 && b0 + 16 < n) vn = *(const uint4 *)(buf + b0 + 16);
+#else
         const uint4 v = *(const uint4 *)(buf + b0);
+#endif
         u32 vm = 0xFFFFu;
         if (b0 < ds) vm &= 0xFFFFu << (u32)(ds - b0);
         if (b0 + 16 > n) vm &= (1u << (u32)(n - b0)) - 1u;
@@ -1351,8 +1363,16 @@ __global__ __launch_bounds__(256) void k_csvcol(ColArgs a) {
         // (all of them are added to the field and never need quoting or
         // doubling): pass 0 counts them (field-limit characters =
         // non-continuation bytes), pass 1 copies them through the combiner
+#if WCS_PF
+        uint4 vn = (rs & ~15ull) < re ? *(const uint4 *)(a.buf + (rs & ~15ull)) : make_uint4(0, 0, 0, 0);
+#endif
         for (u64 b0 = rs & ~15ull; b0 < re; b0 += 16) {
+#if WCS_PF
+            const uint4 v = vn;  // the next vector's load in flight while this one is walked
+            if (b0 + 16 < re) vn = *(const uint4 *)(a.buf + b0 + 16);
+#else
             const uint4 v = *(const uint4 *)(a.buf + b0);
+#endif
             u32 vm = 0xFFFFu;
             if (b0 < rs) vm &= 0xFFFFu << (u32)(rs - b0);
             if (b0 + 16 > re) vm &= (1u << (u32)(re - b0)) - 1u;
