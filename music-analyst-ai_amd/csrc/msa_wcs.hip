@@ -1145,10 +1145,19 @@ __global__ __launch_bounds__(256) void k_wcs_list(const u64 *__restrict__ gtab, 
                                                   u64 *__restrict__ K2, u64 *__restrict__ K1, u64 *__restrict__ K0,
                                                   u32 *__restrict__ V) {
     const u64 slot = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (slot >= nslots) return;
     const u64 *g = gtab + slot * 4;
-    if (g[0] == 0) return;
-    const u64 idx = atomicAdd((unsigned long long *)&ctr->listed, 1ull);
+    const bool used = slot < nslots && g[0] != 0;
+    // one claim per wave (a claim per used slot on the one counter had
+    // serialised: 256 us for 33 K words); the list order does not matter,
+    // the sort keys are unique
+    const u64 um = __ballot(used);
+    if (!um) return;
+    const u32 lead = (u32)__builtin_ctzll(um);
+    u64 base = 0;
+    if (lane_id() == lead) base = atomicAdd((unsigned long long *)&ctr->listed, (unsigned long long)__popcll(um));
+    base = readlane64(base, (int)lead);
+    if (!used) return;
+    const u64 idx = base + mbcnt(um);
     K2[idx] = 0xFFFFFFFFull - g[3];
     K1[idx] = (~g[2]) >> 20;
     K0[idx] = 0;
