@@ -310,33 +310,46 @@ __global__ __launch_bounds__(BLK) void k_wcs_state_block(const u32 *__restrict__
     if (threadIdx.x == BLK - 1) bmap[blockIdx.x] = x;
 }
 
-// Entering state of every block: the block maps are staged in LDS by the
-// whole workgroup, then one thread composes them in order (nb = nseg / 1024).
-constexpr u32 TOP_T = 1024, TOP_CHUNK = 16384;
-__global__ __launch_bounds__(TOP_T) void k_wcs_state_top(u32 *__restrict__ bmap, u64 nb, u32 *__restrict__ final_state) {
-    __shared__ u32 sm[TOP_CHUNK];
-    u32 s = SR;
-    for (u64 c0 = 0; c0 < nb; c0 += TOP_CHUNK) {
-        const u32 m = (u32)(nb - c0 < TOP_CHUNK ? nb - c0 : TOP_CHUNK);
-        for (u32 k = threadIdx.x; k < m; k += TOP_T) sm[k] = bmap[c0 + k];
+constexpr u32 TOP_T = 1024;
+
+// The block maps' entering states with every thread: a chunk of TOP2_PER
+// block maps each, a scan of the chunks' composites in LDS, then each thread
+// steps through its chunk (k_wcs_state_top's one-thread loop over configs[2]'s
+// 4.5 K block maps took 100 us)
+constexpr u32 TOP2_PER = 16;
+__global__ __launch_bounds__(TOP_T) void k_wcs_state_top2(u32 *__restrict__ bmap, u64 nb, u32 *__restrict__ final_state) {
+    __shared__ u32 sh[TOP_T];
+    __shared__ u32 carry;
+    const u32 t = threadIdx.x;
+    if (t == 0) carry = SR;
+    __syncthreads();
+    for (u64 c0 = 0; c0 < nb; c0 += (u64)TOP_T * TOP2_PER) {
+        const u64 k0 = c0 + (u64)t * TOP2_PER;
+        u32 x = MAP_ID;
+        for (u32 k = 0; k < TOP2_PER; ++k)
+            if (k0 + k < nb) x = compose(x, bmap[k0 + k]);
+        sh[t] = x;
         __syncthreads();
-        if (threadIdx.x == 0) {
-            for (u32 k = 0; k < m; ++k) {
-                const u32 t = sm[k];
-                sm[k] = s;
-                s = step(t, s);
-            }
+        for (u32 o = 1; o < TOP_T; o <<= 1) {  // inclusive scan of the chunk composites
+            const u32 y = t >= o ? sh[t - o] : MAP_ID;
+            __syncthreads();
+            x = compose(y, x);
+            sh[t] = x;
+            __syncthreads();
+        }
+        const u32 cin = carry;
+        u32 st = ::step(t ? sh[t - 1] : MAP_ID, cin);
+        for (u32 k = 0; k < TOP2_PER; ++k) {
+            if (k0 + k >= nb) break;
+            const u32 tm = bmap[k0 + k];
+            bmap[k0 + k] = st;
+            st = ::step(tm, st);
         }
         __syncthreads();
-        for (u32 k = threadIdx.x; k < m; k += TOP_T) bmap[c0 + k] = sm[k];
-        __syncthreads();
-        s = __shfl(s, 0);  // every wave needs the carry; wave 0 lane 0 holds it
-        if (threadIdx.x == 0) sm[0] = s;
-        __syncthreads();
-        s = sm[0];
+        if (t == TOP_T - 1) carry = ::step(sh[TOP_T - 1], cin);
         __syncthreads();
     }
-    if (threadIdx.x == 0) *final_state = s;
+    if (t == 0) *final_state = carry;
 }
 
 __global__ __launch_bounds__(BLK) void k_wcs_state_down(const u32 *__restrict__ map, const u64 *__restrict__ cnt6,
@@ -1804,7 +1817,7 @@ static int wcs_split_rows(msa_wcs *w, WCtr **ctr_out, u64 *ds_out, u64 *nrows_ou
         dfin = bmap + nb;
         hipLaunchKernelGGL(k_wcs_map, grid1(nseg), dim3(256), 0, st, buf, ds, n, nseg, w->dia(), map, cnt6);
         hipLaunchKernelGGL(k_wcs_state_block, dim3((u32)nb), dim3(BLK), 0, st, (const u32 *)map, nseg, bmap);
-        hipLaunchKernelGGL(k_wcs_state_top, dim3(1), dim3(TOP_T), 0, st, bmap, nb, dfin);
+        hipLaunchKernelGGL(k_wcs_state_top2, dim3(1), dim3(TOP_T), 0, st, bmap, nb, dfin);
         hipLaunchKernelGGL(k_wcs_state_down, dim3((u32)nb), dim3(BLK), 0, st, (const u32 *)map, (const u64 *)cnt6,
                            nseg, (const u32 *)bmap, sstate, cnt);
         WCHECK(msa_exclusive_scan(cnt, nseg, roff, bsum, total, st));
