@@ -72,6 +72,9 @@ constexpr u32 A_SP = PA(0, 0, 1, 1, 1, 0);
 constexpr u32 A_SPD = PA(0, 0, 2, 1, 2, 0);
 #undef PA
 
+#ifndef CC_IQ
+#define CC_IQ 1  // 0: the splitter's pass 0 and the row-end walk step through line ends inside quotes too (A/B)
+#endif
 #ifndef WCS_PF
 #define WCS_PF 1  // 0: the row-split walks and the splitter's row walk without the next vector's load in flight (A/B)
 #endif
@@ -242,6 +245,20 @@ __device__ __forceinline__ void seg_walk(const u8 *__restrict__ buf, u64 base, u
         if (has_last && ((vm >> pl) & 1u)) E |= 1u << pl;
         int prev = -1;
         while (E) {
+#if CC_IQ
+            if (W::single() && wk.in_iq()) {
+                // inside quotes nothing but a quotechar moves a one-state walker
+                // (line ends there are no row ends): straight to the next one
+                const u32 qn = Q & vm & (prev < 0 ? 0xFFFFu : ~((2u << prev) - 1u));
+                if (!qn) {
+                    prev = 15;
+                    break;
+                }
+                const u32 pq = (u32)__builtin_ctz(qn);
+                prev = (int)pq - 1;
+                E &= ~((1u << pq) - 1u);
+            }
+#endif
             const u32 p = (u32)__builtin_ctz(E);
             E &= E - 1;
             const u32 upto_prev = prev < 0 ? 0u : ((2u << prev) - 1u);
@@ -259,6 +276,8 @@ __device__ __forceinline__ void seg_walk(const u8 *__restrict__ buf, u64 base, u
 }
 
 struct MapWalker {
+    static constexpr bool single() { return false; }  // the states of all 6 entering states
+    __device__ __forceinline__ bool in_iq() const { return false; }
     u32 m;
     u64 c6;
     __device__ __forceinline__ void step(u32 t) { m = map_apply(t, m); }
@@ -374,9 +393,11 @@ __global__ __launch_bounds__(BLK) void k_wcs_state_down(const u32 *__restrict__ 
 }
 
 struct EmitWalker {
+    static constexpr bool single() { return true; }
     u32 s;
     u64 o;
     u64 *rend;
+    __device__ __forceinline__ bool in_iq() const { return s == IQ; }
     __device__ __forceinline__ void step(u32 t) { s = ::step(t, s); }
     __device__ __forceinline__ void eol(u64 i) {
         if (s != SR && s != IQ) rend[o++] = i + 1;
@@ -1398,8 +1419,8 @@ __global__ __launch_bounds__(256) void k_csvcol(ColArgs a) {
             u32 vm = 0xFFFFu;
             if (b0 < rs) vm &= 0xFFFFu << (u32)(rs - b0);
             if (b0 + 16 > re) vm &= (1u << (u32)(re - b0)) - 1u;
-            const u32 S = (mask16(v, a.dia.quote) | mask16(v, a.dia.delim) | mask16(v, '\n') | mask16(v, '\r') |
-                           (a.dia.skip ? mask16(v, ' ') : 0u)) & vm;
+            const u32 Qm = mask16(v, a.dia.quote) & vm, DNm = (mask16(v, a.dia.delim) | mask16(v, '\n')) & vm;
+            const u32 S = (Qm | DNm | mask16(v, '\r') | (a.dia.skip ? mask16(v, ' ') : 0u)) & vm;
             const u32 O = vm & ~S;
             const u32 W[4] = {v.x, v.y, v.z, v.w};
             u32 CONT = 0;
@@ -1425,6 +1446,31 @@ __global__ __launch_bounds__(256) void k_csvcol(ColArgs a) {
                 s = step(T_O, s);
             };
             while (E) {
+#if CC_IQ
+                if (PASS == 0 && s == IQ) {
+                    // inside quotes every byte up to the next quotechar is added
+                    // to the value (delimiters and line ends too): one step to it
+                    // (the lyric fields' line breaks had each been a trip)
+                    const u32 after = prev < 0 ? vm : (vm & ~((2u << prev) - 1u));
+                    const u32 qn = Qm & after;
+                    const u32 rng = qn ? (after & ((1u << __builtin_ctz(qn)) - 1u)) : after;
+                    if (rng) {
+                        chars += (u32)__popc(rng & ~CONT);
+                        if (chars > FIELD_LIMIT) limit = true;
+                        if (f < a.ncols) {
+                            clen += (u32)__popc(rng);
+                            special |= (rng & DNm) != 0;
+                        }
+                    }
+                    if (!qn) {
+                        prev = 15;
+                        break;
+                    }
+                    const u32 pq = (u32)__builtin_ctz(qn);
+                    prev = (int)pq - 1;
+                    E &= ~((1u << pq) - 1u);  // (the quote's own bit stays)
+                }
+#endif
                 const u32 p = (u32)__builtin_ctz(E);
                 E &= E - 1;
                 run(O & ((1u << p) - 1u) & ~(prev < 0 ? 0u : ((2u << prev) - 1u)));
