@@ -1479,6 +1479,37 @@ __device__ __forceinline__ u32 ma_find(ulonglong2 *keys, u64 k0, u64 k1) {
     }
     return ~0u;
 }
+#ifndef MA_FLAT
+#define MA_FLAT 1  // 0: one source log at a time, no load pipelining (A/B)
+#endif
+#ifndef MA_DIAG
+#define MA_DIAG 0  // timing diagnostics only, results wrong (profiles/r06_ab_miss_agg.txt): 1 no flush,
+                   // 2 LDS-full entries dropped, 4 plain adds, 8 no probe (hash slot), 32 a slot per thread
+#endif
+#ifndef MA_PB
+#define MA_PB 0  // 1: the batch's bucket reads issued together before the first count (MA_FLAT)
+#endif
+__device__ __forceinline__ void ma_count(const ScanArgs &a, ulonglong2 *keys, u32 *cnts, ulonglong2 x) {
+    const u32 c = gather8(x.x) | ((gather8(x.y) & 0x7Fu) << 8);
+    const u64 k0 = x.x & MLOG_KEYBITS, k1 = x.y & (MLOG_KEYBITS | KMARK);
+#if MA_DIAG & 32
+    const u32 slot = threadIdx.x;  // timing diagnostic: no probe, no two lanes on one slot
+#elif MA_DIAG & 8
+    const u32 slot = ma_hash(k0, k1) % MA_SLOTS;  // timing diagnostic: no probe
+#else
+    const u32 slot = ma_find(keys, k0, k1);
+#endif
+#if MA_DIAG & 4
+    if (slot != ~0u) cnts[slot] += c ? c : 1u;  // timing diagnostic: plain add (races)
+#else
+    if (slot != ~0u) atomicAdd(&cnts[slot], c ? c : 1u);
+#endif
+#if MA_DIAG & 2
+    else {}  // timing diagnostic: dropped
+#else
+    else hbm_insert16<false>(a, k0, k1, c ? c : 1u);  // table full: one insert per entry
+#endif
+}
 __global__ __launch_bounds__(MA_T) void k_miss_agg(ScanArgs a, u32 nsrc, u32 groups) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     ulonglong2 *keys = reinterpret_cast<ulonglong2 *>(smem);
@@ -1489,6 +1520,87 @@ __global__ __launch_bounds__(MA_T) void k_miss_agg(ScanArgs a, u32 nsrc, u32 gro
     }
     __syncthreads();
     const u32 part = blockIdx.x % MSA_MLOG_PARTS, g = blockIdx.x / MSA_MLOG_PARTS;
+#if MA_FLAT
+    // The workgroup's source logs (K3 workgroups g, g + G, ...) as ONE stream
+    // per thread, 64 sources at a time: a thread's entries are i = t, t + T, ...
+    // of each log in turn, so every batch is full (one log at a time had left
+    // a partial batch per log: ~32 batches per thread instead of ~22), and the
+    // next batch's loads are in flight while this one is counted.
+    __shared__ u32 sn[64];
+    for (u32 c0 = 0; g + c0 * groups < nsrc; c0 += 64) {
+        __syncthreads();  // the previous chunk's readers of sn are done
+        if (threadIdx.x < 64) {
+            const u32 src = g + (c0 + threadIdx.x) * groups;
+            const u32 n = src < nsrc ? a.mlog_n[src * MSA_MLOG_PARTS + part] : 0u;
+            sn[threadIdx.x] = n;
+            u64 tot = n;
+            for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
+            if (threadIdx.x == 0 && tot) atomicAdd((unsigned long long *)&a.ctr->k3_misses, (unsigned long long)tot);
+        }
+        __syncthreads();
+        u32 k = 0, i = threadIdx.x;
+        while (k < 64 && i >= sn[k]) { ++k; i = threadIdx.x; }
+        auto fetch = [&](ulonglong2 (&x)[MA_FLY], u32 &nx) {
+            nx = 0;
+#pragma unroll
+            for (int q = 0; q < MA_FLY; ++q) {
+                if (k < 64) {
+                    const u64 src = g + (c0 + k) * groups;
+                    x[q] = a.mlog[(src * MSA_MLOG_PARTS + part) * a.mlog_cap + i];
+                    ++nx;
+                    i += MA_T;
+                    while (k < 64 && i >= sn[k]) { ++k; i = threadIdx.x; }
+                }
+            }
+        };
+        ulonglong2 cur[MA_FLY], nxt[MA_FLY];
+        u32 ncur, nnxt;
+        fetch(cur, ncur);
+        while (ncur) {
+            fetch(nxt, nnxt);
+#if MA_PB
+            // the batch's first bucket reads together (stale reads are safe:
+            // a hit is an exact key match, a slot that looked free goes through
+            // ma_find's CAS claim)
+            ulonglong2 sl[MA_FLY][4];
+            u32 bs[MA_FLY];
+#pragma unroll
+            for (int q = 0; q < MA_FLY; ++q) {
+                if ((u32)q < ncur) {
+                    const u64 k0 = cur[q].x & MLOG_KEYBITS, k1 = cur[q].y & (MLOG_KEYBITS | KMARK);
+                    const u32 h = ma_hash(k0, k1);
+                    bs[q] = __umulhi(h, (u32)MA_NB) * 4;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) sl[q][j] = keys[bs[q] + j];
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < MA_FLY; ++q) {
+                if ((u32)q >= ncur) break;
+                const ulonglong2 x = cur[q];
+                const u64 k0 = x.x & MLOG_KEYBITS, k1 = x.y & (MLOG_KEYBITS | KMARK);
+                u32 hit = 4;
+#pragma unroll
+                for (int j = 3; j >= 0; --j)
+                    if (sl[q][j].x == k0 && sl[q][j].y == k1) hit = (u32)j;
+                if (hit < 4) {
+                    const u32 c = gather8(x.x) | ((gather8(x.y) & 0x7Fu) << 8);
+                    atomicAdd(&cnts[bs[q] + hit], c ? c : 1u);
+                } else {
+                    ma_count(a, keys, cnts, x);
+                }
+            }
+#else
+#pragma unroll
+            for (int q = 0; q < MA_FLY; ++q)
+                if ((u32)q < ncur) ma_count(a, keys, cnts, cur[q]);
+#endif
+#pragma unroll
+            for (int q = 0; q < MA_FLY; ++q) cur[q] = nxt[q];
+            ncur = nnxt;
+        }
+    }
+#else
     for (u32 src = g; src < nsrc; src += groups) {
         const u64 base = ((u64)src * MSA_MLOG_PARTS + part) * a.mlog_cap;
         const u32 n = a.mlog_n[src * MSA_MLOG_PARTS + part];
@@ -1505,16 +1617,13 @@ __global__ __launch_bounds__(MA_T) void k_miss_agg(ScanArgs a, u32 nsrc, u32 gro
 #pragma unroll
             for (int q = 0; q < MA_FLY; ++q) {
                 if (i0 + q * MA_T >= n) break;
-                const ulonglong2 x = xs[q];
-                const u32 c = gather8(x.x) | ((gather8(x.y) & 0x7Fu) << 8);
-                const u64 k0 = x.x & MLOG_KEYBITS, k1 = x.y & (MLOG_KEYBITS | KMARK);
-                const u32 slot = ma_find(keys, k0, k1);
-                if (slot != ~0u) atomicAdd(&cnts[slot], c ? c : 1u);
-                else hbm_insert16<false>(a, k0, k1, c ? c : 1u);  // table full: one insert per entry
+                ma_count(a, keys, cnts, xs[q]);
             }
         }
     }
+#endif
     __syncthreads();
+#if !(MA_DIAG & 1)
     for (u32 i = threadIdx.x; i < MA_SLOTS; i += MA_T) {
         const u32 c = cnts[i];
         if (c) {
@@ -1522,6 +1631,7 @@ __global__ __launch_bounds__(MA_T) void k_miss_agg(ScanArgs a, u32 nsrc, u32 gro
             hbm_insert16(a, kk.x, kk.y, c);
         }
     }
+#endif
 }
 
 // ---------------------------------------------------------------------------
