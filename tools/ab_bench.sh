@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 for vv in "$@"; do
   v=${vv%@*}; ab=0; [ "$vv" != "$v" ] && ab=${vv#*@}
   if [ "$v" = base ]; then L=$PWD/music-analyst-ai_amd/libmsa_hip.so; else L=$PWD/music-analyst-ai_amd/variants/libmsa_hip_$v.so; fi
-  MSA_ABLATE=$ab MSA_LIB=$L timeout -k 10 200 python -u bench.py --steps 20 --warmup 3 --no-cpu-baseline > $out.$v.json 2>> $out.err
+  MSA_ABLATE=$ab MSA_LIB=$L timeout -k 10 200 python -u bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-pcie > $out.$v.json 2>> $out.err
   python3 -c "import json,sys; d=json.load(open('$out.$v.json')); print('$vv', d['ms_per_step'], d['value'], d['roofline']['avg_launch_ms'], json.dumps(d['stage_ms']))" >> $out.log
 done
 echo done >> $out.log

@@ -6,7 +6,7 @@ mkdir -p gpurun_out
 : > $out.log
 for spec in "$@"; do
   name=${spec%%:*}; vars=${spec#*:}
-  env $vars timeout -k 10 200 python -u bench.py --steps 20 --warmup 3 --no-cpu-baseline > $out.$name.json 2>> $out.err
+  env $vars timeout -k 10 200 python -u bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-pcie > $out.$name.json 2>> $out.err
   python3 -c "import json,sys; d=json.load(open('$out.$name.json')); print('$name', d['ms_per_step'], d['value'], d['roofline']['avg_launch_ms'], json.dumps(d['stage_ms']))" >> $out.log
 done
 echo done >> $out.log

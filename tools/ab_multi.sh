@@ -19,7 +19,7 @@ for V in "$@"; do
 done
 for v in "${ok[@]}"; do
   if [ $v = base ]; then LL=$PWD/music-analyst-ai_amd/libmsa_hip.so; else LL=$PWD/music-analyst-ai_amd/variants/libmsa_hip_$v.so; fi
-  MSA_LIB=$LL timeout -s KILL 150 rocprofv3 --pmc TD_TD_BUSY_sum TD_BUSY_max TA_TA_BUSY_sum TA_BUSY_max --output-format csv -d $D/pmc_$v -o run -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline > $D/pmc_$v.log 2>&1 || exit $?
+  MSA_LIB=$LL timeout -s KILL 150 rocprofv3 --pmc TD_TD_BUSY_sum TD_BUSY_max TA_TA_BUSY_sum TA_BUSY_max --output-format csv -d $D/pmc_$v -o run -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-pcie > $D/pmc_$v.log 2>&1 || exit $?
   echo "== $v" >> $D/summary.txt
   python3 tools/pmc_kernels.py $D/pmc_$v "k_" 2>&1 | grep -A4 -E "^(k_scan_tokens|k_scan_struct|k_chunk_summary)" >> $D/summary.txt
 done

@@ -13,8 +13,8 @@ timeout -k 10 600 python -u -m pytest $F -x -q --timeout 300 --timeout-method th
 echo "parity ok" >> $D/summary.txt
 for v in base $V; do
   if [ $v = base ]; then LL=$PWD/music-analyst-ai_amd/libmsa_hip.so; else LL=$PWD/music-analyst-ai_amd/variants/libmsa_hip_$v.so; fi
-  MSA_LIB=$LL timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $D/pmcw_$v -o run -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline > $D/pmcw_$v.log 2>&1
-  MSA_LIB=$LL timeout -s KILL 150 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU SQ_WAIT_ANY SQ_WAVE_CYCLES --output-format csv -d $D/pmcq_$v -o run -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline > $D/pmcq_$v.log 2>&1
+  MSA_LIB=$LL timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $D/pmcw_$v -o run -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-pcie > $D/pmcw_$v.log 2>&1
+  MSA_LIB=$LL timeout -s KILL 150 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU SQ_WAIT_ANY SQ_WAVE_CYCLES --output-format csv -d $D/pmcq_$v -o run -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-pcie > $D/pmcq_$v.log 2>&1
   echo "== $v" >> $D/summary.txt
   LAST=1 python3 tools/pmc_kernels.py $D/pmcw_$v k_scan_tokens >> $D/summary.txt 2>&1
   LAST=1 python3 tools/pmc_kernels.py $D/pmcw_$v k_miss_agg >> $D/summary.txt 2>&1

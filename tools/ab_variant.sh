@@ -14,7 +14,7 @@ echo "parity rc=$rc" >> $D/summary.txt
 [ $rc -eq 0 ] || exit $rc
 for v in base $V; do
   if [ $v = base ]; then LL=$PWD/music-analyst-ai_amd/libmsa_hip.so; else LL=$L; fi
-  MSA_LIB=$LL timeout -s KILL 150 rocprofv3 --pmc TD_TD_BUSY_sum TD_BUSY_max TA_TA_BUSY_sum TA_BUSY_max --output-format csv -d $D/pmc_$v -o run -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline > $D/pmc_$v.log 2>&1
+  MSA_LIB=$LL timeout -s KILL 150 rocprofv3 --pmc TD_TD_BUSY_sum TD_BUSY_max TA_TA_BUSY_sum TA_BUSY_max --output-format csv -d $D/pmc_$v -o run -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-pcie > $D/pmc_$v.log 2>&1
   echo "== $v" >> $D/summary.txt
   python3 tools/pmc_kernels.py $D/pmc_$v k_scan >> $D/summary.txt 2>&1
 done

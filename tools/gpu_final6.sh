@@ -20,7 +20,7 @@ bash tools/pmc.sh $D/pmc
 cp $D/pmc/pmc.json profiles/pmc_scan_main.json
 cp $D/pmc/pmc.json $D/pmc_scan_main.json
 timeout -k 10 300 python -u bench.py > $D/bench.json 2> $D/bench.err
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $D/prof -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline > $D/prof.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $D/prof -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-pcie > $D/prof.log 2>&1
 python3 tools/timeline.py $D/prof > $D/step_timeline.txt 2>&1 || true
 bash tools/pmc_wcs.sh $D/pmc_wcs
 cp $D/pmc_wcs/pmc.json profiles/pmc_wcs_main.json

@@ -8,5 +8,5 @@ mkdir -p $D
 K=${2:+-k "$2"}
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread $K > $D/gpu_tests.log 2>&1
 timeout -k 10 300 python -u bench.py > $D/bench.json 2> $D/bench.err
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $D/prof -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline > $D/prof.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $D/prof -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-pcie > $D/prof.log 2>&1
 echo done

@@ -18,7 +18,7 @@ export TMPDIR=/tmp
 OUT=${1:-gpurun_out/pmc}
 STEPS=${STEPS:-1}
 mkdir -p "$OUT"
-B=(python3 bench.py --steps "$STEPS" --warmup 1 --no-cpu-baseline)
+B=(python3 bench.py --steps "$STEPS" --warmup 1 --no-cpu-baseline --no-pcie)
 pass() {  # name counters...
   local name=$1; shift
   timeout -s KILL 150 rocprofv3 --pmc "$@" --output-format csv -d "$OUT/$name" -o run -- "${B[@]}" > "$OUT/$name.log" 2>&1

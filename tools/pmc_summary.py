@@ -109,7 +109,7 @@ def main():
                     "--no-cpu-baseline" if wcs else
                     "tools/pmc_split.sh: rocprofv3 --pmc <group> -- python3 tools/bench_wcs.py --path split --steps 1 "
                     "--warmup 1 --no-cpu-baseline" if split else
-                    "tools/pmc.sh: rocprofv3 --pmc <group> -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline"),
+                    "tools/pmc.sh: rocprofv3 --pmc <group> -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-pcie"),
         "kernels": kernels,
     }
     k3 = kernels.get(rk, {})

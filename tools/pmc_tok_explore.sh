@@ -5,7 +5,7 @@ export TMPDIR=/tmp
 OUT=${1:-gpurun_out/pmc_tok}
 mkdir -p "$OUT"
 timeout -s KILL 60 rocprofv3 -L > "$OUT/avail.txt" 2>&1 || true
-B=(python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline)
+B=(python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-pcie)
 pass() {
   local name=$1; shift
   timeout -s KILL 150 rocprofv3 --pmc "$@" --output-format csv -d "$OUT/$name" -o run -- "${B[@]}" > "$OUT/$name.log" 2>&1 || echo "pass $name failed" >> "$OUT/fail.txt"
