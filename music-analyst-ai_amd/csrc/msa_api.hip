@@ -104,6 +104,9 @@ hipError_t msa_launch_blob(const u32 *, u64, const u64 *, const u64 *, const u64
 #ifndef MSA_ARTIST_EARLY
 #define MSA_ARTIST_EARLY 1  // 0: the split's artist pass waits for the offset scans too (A/B builds)
 #endif
+#ifndef MSA_ARTIST_SIDE
+#define MSA_ARTIST_SIDE 1  // 0: the split's artist pass on the library stream, text.csv forked after it (A/B builds)
+#endif
 
 // ---------------------------------------------------------------------------
 namespace {
@@ -320,6 +323,7 @@ struct msa_ctx {
     // split scan: k_scan_struct done (the spans may start) / the spans done
     hipEvent_t ev_scan_a = nullptr, ev_spans = nullptr;
     hipEvent_t ev_fix = nullptr;  // rank2: the artist keys written (k_rec_fast + k_rec_fix), before the offset scans
+    hipEvent_t ev_art = nullptr;  // side stream: the split's artist pass done (MSA_ARTIST_SIDE)
     // the folded split scan (k_scan_fold): tile statuses (5 words a tile) behind
     // the ticket counter, the tickets taken so far, the status epoch
     // env MSA_FOLD=1 (opt-in: measured as fast as K1 + K2 + k_scan_struct, 0.85
@@ -1047,7 +1051,7 @@ static int split_prologue(msa_ctx *c, u64 nul_n, bool rs0) {
     return MSA_OK;
 }
 
-static int launch_artist_count(msa_ctx *c);
+static int launch_artist_count(msa_ctx *c, hipStream_t st = nullptr);
 static int split_once(msa_ctx *c, int flags) {
     int rc;
     c->artist_deferred = c->text_deferred = false;  // superseded by this split
@@ -1308,6 +1312,29 @@ static int split_once(msa_ctx *c, int flags) {
     // artist pass (LDS tables and atomics) -- both only add to Counters with
     // atomics; the read-back below waits for both
     // (measured neutral on rank2 beside the artist pass, profiles/r04_t41_*)
+    const bool art_ok = !c->artist_exact && c->nrec && !(c->ablate & 32768);
+#if MSA_ARTIST_SIDE && MSA_LISTS_BEFORE_SPANS && MSA_ARTIST_EARLY
+    // with text.csv: the artist pass and then text.csv's gather on the side
+    // stream, from rank2's k_rec_fix (the keys) and its offset scans -- not
+    // from the library stream, whose k_miss_agg and slot lists they do not
+    // need (the table clears of the prologue came before rank2's fork).  The
+    // gather follows the artist pass on ONE stream (a fork after it had cost
+    // ~30 us of cross-stream wait on the step's critical path); the library
+    // stream waits for the artist pass (its counters) before the read-back.
+    const bool art_side = c->text_deferred && spans_beside && art_ok;
+    if (art_side) {
+        HIPC(c, hipStreamWaitEvent(c->side, c->ev_fix, 0));
+        if ((rc = launch_artist_count(c, c->side))) return rc;
+        c->artist_spec = true;
+        HIPC(c, hipEventRecord(c->ev_art, c->side));
+        HIPC(c, hipStreamWaitEvent(c->side, c->ev_spans, 0));
+        if ((rc = launch_text(c, c->side))) return rc;
+        HIPC(c, hipEventRecord(c->ev_join, c->side));
+        c->side_pending = true;
+    }
+#else
+    const bool art_side = false;
+#endif
     if (!c->dense_w && (rc = build_word_lists(c))) return rc;  // (dense: the aggregation counted the entries)
 #if MSA_LISTS_BEFORE_SPANS
     // the slot lists need the tables only, not the spans: they run behind
@@ -1317,7 +1344,7 @@ static int split_once(msa_ctx *c, int flags) {
     // the artist pass needs the keys only: it waits for k_rec_fix, not for the
     // offset scans behind it on rank2 (it starts as k_miss_agg's workgroups
     // leave the CUs, ~80 us earlier); the scans are waited for after it
-    if (spans_beside) HIPC(c, hipStreamWaitEvent(c->stream, c->ev_fix, 0));
+    if (spans_beside && !art_side) HIPC(c, hipStreamWaitEvent(c->stream, c->ev_fix, 0));
 #else
     if (spans_beside) HIPC(c, hipStreamWaitEvent(c->stream, c->ev_spans, 0));
 #endif
@@ -1327,7 +1354,9 @@ static int split_once(msa_ctx *c, int flags) {
     // with the split's -- the text column's gather (launched by msa_count)
     // then no longer waits behind a second round trip and the artist kernels
     // (an exact-reader input resets the table in msa_count)
-    if (!c->artist_exact && c->nrec && !(c->ablate & 32768)) {
+    if (art_side) {
+        HIPC(c, hipStreamWaitEvent(c->stream, c->ev_art, 0));
+    } else if (art_ok) {
         if ((rc = launch_artist_count(c))) return rc;
         c->artist_spec = true;
     }
@@ -1517,7 +1546,8 @@ static int wipe_long_table(msa_ctx *c) {
 
 // The artist pass of the lines shortcut (k_artist_count + merge + h2 check)
 // over the split's keys, on the library stream.
-static int launch_artist_count(msa_ctx *c) {
+static int launch_artist_count(msa_ctx *c, hipStream_t st) {
+    if (!st) st = c->stream;
     const u64 nrec = c->nrec;
     // flush logs of the per-CU tables: (workgroup, 16 partitions) x cap
     // entries of 32 B; a workgroup holds <= min(6144, its records) keys
@@ -1526,12 +1556,12 @@ static int launch_artist_count(msa_ctx *c) {
     const u32 alog_cap = (u32)std::min<u64>(1024, std::max<u64>(64, per_wg / 8));
     HIPC(c, ensure(c->alog, (size_t)c->cus * 16 * alog_cap * 32));
     HIPC(c, ensure(c->alog_n, (size_t)c->cus * 16 * 4));
-    prof_begin(c, ST_ARTIST_KEYS);
+    prof_begin(c, ST_ARTIST_KEYS, st);
     HIPC(c, msa_launch_artist_count(c->alen.as<u64>(), c->key_len.as<u32>(), c->kh1.as<u64>(), c->kh2.as<u64>(), nrec,
                                     c->a_tab.as<u64>(), c->a_slots - 1, c->a_list.as<u32>(), c->a_slots / 2,
                                     c->ctr.as<Counters>(), c->cus, c->ablate, c->alog.as<ulonglong2>(),
-                                    c->alog_n.as<u32>(), alog_cap, c->stream));
-    prof_end(c, ST_ARTIST_KEYS, nrec * 28);
+                                    c->alog_n.as<u32>(), alog_cap, st));
+    prof_end(c, ST_ARTIST_KEYS, nrec * 28, st);
     return MSA_OK;
 }
 
@@ -2145,6 +2175,7 @@ int msa_create(int device, msa_ctx **out) {
         hipEventCreateWithFlags(&c->ev_scan_a, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_spans, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fix, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_art, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fin, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
@@ -2199,6 +2230,7 @@ void msa_destroy(msa_ctx *c) {
     (void)hipEventDestroy(c->ev_scan_a);
     (void)hipEventDestroy(c->ev_spans);
     (void)hipEventDestroy(c->ev_fix);
+    (void)hipEventDestroy(c->ev_art);
     (void)hipStreamDestroy(c->side);
     (void)hipStreamDestroy(c->rank2);
     (void)hipStreamDestroy(c->aux);
