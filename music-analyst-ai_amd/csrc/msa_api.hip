@@ -107,6 +107,9 @@ hipError_t msa_launch_blob(const u32 *, u64, const u64 *, const u64 *, const u64
 #ifndef MSA_ARTIST_SIDE
 #define MSA_ARTIST_SIDE 1  // 0: the split's artist pass on the library stream, text.csv forked after it (A/B builds)
 #endif
+#ifndef MSA_ARTIST_SIDE_DENSE
+#define MSA_ARTIST_SIDE_DENSE 0  // 1: MSA_ARTIST_SIDE for dense splits too (A/B builds)
+#endif
 
 // ---------------------------------------------------------------------------
 namespace {
@@ -1321,7 +1324,10 @@ static int split_once(msa_ctx *c, int flags) {
     // gather follows the artist pass on ONE stream (a fork after it had cost
     // ~30 us of cross-stream wait on the step's critical path); the library
     // stream waits for the artist pass (its counters) before the read-back.
-    const bool art_side = c->text_deferred && spans_beside && art_ok;
+    // (not for a dense split: there the bucketed aggregation is the critical
+    // path and the artist pass + gather beside it slowed configs[4] 16.9 ->
+    // 17.2 ms/step)
+    const bool art_side = c->text_deferred && spans_beside && art_ok && (MSA_ARTIST_SIDE_DENSE || !c->dense_w);
     if (art_side) {
         HIPC(c, hipStreamWaitEvent(c->side, c->ev_fix, 0));
         if ((rc = launch_artist_count(c, c->side))) return rc;
