@@ -58,6 +58,28 @@ def test_torture(msa_mod, ctx, tmp_path, seed):
     check_against_oracle(msa_mod, ctx, data, tmp_path, f"torture{seed}")
 
 
+@pytest.mark.parametrize("seed", [2, 5])
+def test_torture_repeat_runs(msa_mod, ctx, tmp_path, seed):
+    """Repeated runs on one loaded input (what bench.py times: later splits size
+    their tables, logs and the dense choice from the earlier ones) give the
+    oracle's bytes every time, on corpora whose records take the exact path."""
+    msa = msa_mod
+    data = msa.gen_corpus(1500, mode="torture", seed=seed)
+    p = tmp_path / "t.csv"
+    p.write_bytes(data)
+    r = run_oracle(str(p), str(tmp_path / "orc"), ranks=1)
+    assert r.returncode == 0, r.stderr
+    exp = read_outputs(str(tmp_path / "orc"))
+    ctx.load_csv(data)
+    for _ in range(3):
+        ctx.run(text_column=True)
+        s = ctx.summary()
+        assert msa.table_csv_bytes(ctx.ranked(msa.MSA_TABLE_WORDS), "word") == exp["word_counts.csv"]
+        assert msa.table_csv_bytes(ctx.ranked(msa.MSA_TABLE_ARTISTS), "artist") == exp["top_artists.csv"]
+        got = {s.artist_file + ".csv": ctx.split_column(0), s.text_file + ".csv": ctx.split_column(1)}
+        assert got == exp["split"]
+
+
 @pytest.mark.parametrize("mode,songs,crlf", [("zipf", 3000, False), ("zipf", 2000, True), ("highcard", 3000, False)])
 def test_small_corpora(msa_mod, ctx, tmp_path, mode, songs, crlf):
     data = msa_mod.gen_corpus(songs, mode=mode, seed=7, vocab=20000, n_artists=500, crlf=crlf)
